@@ -1,0 +1,39 @@
+# Builds the product library (HIP for gfx950 + host C) and the test-only oracle.
+#   make            -> uvhttp_amd/lib/libuvhttp_ws_amd.so  +  oracle/_build/libws_oracle.so
+ROCM ?= /opt/rocm
+HIPCC ?= $(ROCM)/bin/hipcc
+CC ?= gcc
+ARCH ?= gfx950
+BUILD := uvhttp_amd/build
+LIB := uvhttp_amd/lib/libuvhttp_ws_amd.so
+
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Iinclude -Wall -Werror \
+            -mcode-object-version=5
+CFLAGS := -O2 -DNDEBUG -fPIC -std=gnu11 -Iinclude -Wall -Wextra -Werror
+
+all: $(LIB) oracle
+
+$(BUILD)/ws_gpu.o: uvhttp_amd/csrc/ws_gpu.hip include/uvhttp_ws_amd.h
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(BUILD)/ws_host.o: uvhttp_amd/csrc/ws_host.c include/uvhttp_ws_amd.h
+	@mkdir -p $(BUILD)
+	$(CC) $(CFLAGS) -c -o $@ $<
+
+$(LIB): $(BUILD)/ws_gpu.o $(BUILD)/ws_host.o
+	@mkdir -p $(dir $@)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+
+oracle:
+	$(MAKE) -C oracle
+
+asm: uvhttp_amd/csrc/ws_gpu.hip
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o $(BUILD)/ws_gpu.s $<
+
+clean:
+	rm -rf $(BUILD) uvhttp_amd/lib
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle clean asm

@@ -1,0 +1,287 @@
+#!/usr/bin/env python3
+"""bench.py — WebSocket payload unmask GiB/s (device-resident) on MI355X.
+
+Metric (BASELINE.json): "WebSocket payload unmask GiB/s (device-resident), 64 KiB frames,
+1/2/4/8 GPU".  One *step* = one pass of the hot path — frame-header parse + validation +
+fragment state machine + payload unmask (include/uvhttp_ws_amd.h, decode_inplace) — over one
+batch of synthetic masked frames already resident in HBM.  Default workload = BASELINE
+config C3: 65 536 x 64 KiB masked BINARY frames per GPU.  Multi-GPU: one process per GPU
+(torch.distributed.run), each rank decodes its own shard (frames are independent: weak
+scaling, no data-path collective); a gloo barrier brackets the timed region and the max
+elapsed time over ranks is used.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4] [--mode inplace|compact]
+
+Rank 0 prints ONE JSON line.  `roofline` comes from HIP events bracketing the payload kernel
+on its stream during the timed steps; `cpu_baseline` times the CPU port of the reference path
+(oracle/, test infrastructure) on this host, rank 0 at N=1 only.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import platform
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+CONFIGS = {
+    # name: (frames per GPU, payload bytes, fragmented, max_message_size)
+    "c2": (65536, 4096, False, 64 * 1024 * 1024),
+    "c3": (65536, 65536, False, 64 * 1024 * 1024),
+    "c4": (1048576, 256, True, 256 * 1024 * 1024),
+}
+WORKLOAD = {
+    "c2": "C2: 65536 x 4 KiB masked BINARY frames per GPU",
+    "c3": "C3: 65536 x 64 KiB masked BINARY frames per GPU (C5 shard shape)",
+    "c4": "C4: 1048576 x 256 B masked frames, one fragmented message per GPU",
+}
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
+SEED = 0x5EED0001
+GIB = float(1 << 30)
+
+
+def header_size(p):
+    return 2 if p < 126 else 4 if p < 65536 else 10
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(cfg_name, target_s=10.0):
+    """Time the oracle (CPU port of src/uvhttp_websocket.c, gcc -O2) on a bounded sample of
+    the same workload: per-frame header parse + apply_mask (the unmask path), 1 thread.
+    Also times the process_data loop fed 16 KiB reads (the live libuv shape)."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import _oracle  # test infrastructure: CPU baseline leg only
+    L = _oracle.load()
+    n, plen, frag, mm = CONFIGS[cfg_name]
+    sample = max(1, min(n, (128 << 20) // max(plen, 1)))  # ~128 MiB of payload
+    wire, stride = _oracle.gen_frames(sample, plen, SEED, fragmented=frag, total=sample)
+    ptr = _oracle._ptr(wire)
+    payload = 0
+    t0 = time.perf_counter()
+    passes = 0
+    while True:
+        payload += L.oracle_unmask_frames(ptr, sample, stride)
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= target_s * 0.5 or passes >= 1000:
+            break
+    unmask_gibs = payload / el / GIB
+    # stream decode of the (re-masked) sample in 16 KiB reads
+    if passes % 2:
+        L.oracle_unmask_frames(ptr, sample, stride)  # restore masked bytes
+    sp = 0
+    t1 = time.perf_counter()
+    spasses = 0
+    while True:
+        sp += L.oracle_stream_decode(ptr, wire.size, 16384, 16 * 1024 * 1024, mm, None)
+        spasses += 1
+        el2 = time.perf_counter() - t1
+        if el2 >= target_s * 0.5 or spasses >= 1000:
+            break
+    stream_gibs = sp / el2 / GIB
+    cc = subprocess.run(["gcc", "--version"], capture_output=True, text=True).stdout
+    return {
+        "value": round(unmask_gibs, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+        "sample": f"{sample} frames x {plen} B of the {cfg_name.upper()} workload "
+                  f"({sample * plen / GIB:.3f} GiB payload), header parse + apply_mask per "
+                  f"frame, {passes} passes in {el:.1f} s",
+        "stream_decode_16k_reads": round(stream_gibs, 3),
+        "stream_decode_sample": f"process_data fed 16 KiB reads, {spasses} passes in {el2:.1f} s",
+        "compiler": cc.splitlines()[0] if cc else "gcc", "flags": "-O2 -DNDEBUG",
+        "cpu": cpu_model(), "host_threads": os.cpu_count(),
+    }
+
+
+def pmc_traffic(cfg_name, mode):
+    """HBM bytes per payload-kernel launch measured with rocprofv3 PMC counters (collected by
+    tools/profile.sh into profiles/, FETCH_SIZE doubled per the gfx950 calibration)."""
+    p = os.path.join(REPO, "profiles", f"traffic_{cfg_name}_{mode}.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        with open(p) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--mode", default="inplace", choices=["inplace", "compact"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--e2e", action="store_true", help="also time host->device->host")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
+
+    import torch
+    import torch.distributed as dist
+    import uvhttp_amd as U
+
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(local)
+    dev = f"cuda:{local}"
+
+    n, plen, frag, mm = CONFIGS[args.config]
+    stride = U.gen_frame_stride(plen)
+    wire_len = stride * n
+    eng = U.GpuEngine(local)
+    stream = torch.cuda.current_stream(local)
+    wire = torch.empty(wire_len + 64, dtype=torch.uint8, device=dev)
+    eng.gen_frames(wire, n, plen, SEED + rank, opcode0=2, fragmented=frag, stream=stream)
+    desc, summ = eng.alloc_outputs(n)
+    arena = msgs = None
+    if args.mode == "compact":
+        arena = torch.empty(n * plen + 64, dtype=torch.uint8, device=dev)
+        msgs = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+    eng.reserve(n, wire_len, n * plen if arena is not None else 0)
+
+    def step():
+        if arena is None:
+            eng.decode_inplace(wire, n, stride=stride, max_message_size=mm, wire_len=wire_len,
+                               desc=desc, summary=summ, stream=stream)
+        else:
+            eng.decode_compact(wire, n, arena, stride=stride, max_message_size=mm,
+                               wire_len=wire_len, desc=desc, msgs=msgs, summary=summ,
+                               stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    s = eng.read_summary(summ)
+    if s["n_delivered"] != n or s["status"] != 0:
+        raise SystemExit(f"decode failed: {s}")
+    eng.kernel_time()  # discard warmup events
+
+    eng.set_timing(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    eng.set_timing(False)
+    k_ms, k_n = eng.kernel_time()
+    s = eng.read_summary(summ)
+    assert s["n_delivered"] == n and s["status"] == 0, s
+
+    el_t = torch.tensor([elapsed], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+    el_max = float(el_t.item())
+
+    payload_per_rank = n * plen
+    total_payload = payload_per_rank * world * args.steps
+    value = total_payload / el_max / GIB
+
+    # algorithmic bytes of the payload kernel per launch: in place, every
+    # frame's header+key+payload is read and its payload written; compact reads the same
+    # and writes the payload into the arena.
+    alg_bytes = n * ((header_size(plen) + 4 + plen) + plen)
+    avg_kernel_s = (k_ms / 1e3 / k_n) if k_n else float("nan")
+    achieved = alg_bytes / avg_kernel_s / 1e9 if k_n else None
+    traffic = pmc_traffic(args.config, args.mode)
+
+    e2e = None
+    if args.e2e and rank == 0:
+        e2e = e2e_rate(torch, eng, n, plen, stride, wire_len, mm, dev, stream)
+
+    if rank == 0:
+        out = {
+            "metric": "WebSocket payload unmask GiB/s (device-resident), 64 KiB frames, 1/2/4/8 GPU",
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(el_max / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (splitmix64 payload + per-frame keys, generated on device)",
+            "config": {
+                "workload": WORKLOAD[args.config],
+                "mode": args.mode,
+                "frames_per_gpu": n,
+                "payload_bytes_per_frame": plen,
+                "wire_bytes_per_frame": stride,
+                "parallelism": f"shard{world} (independent frames, no collective)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "k_unmask_inplace" if args.mode == "inplace" else "k_gather_compact",
+                "achieved": round(achieved, 1) if achieved else None,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                "traffic": traffic,
+                "alg_bytes_per_launch": alg_bytes,
+                "avg_kernel_us": round(avg_kernel_s * 1e6, 2) if k_n else None,
+                "launches_timed": k_n,
+            },
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_seconds)
+        if e2e:
+            out["e2e_pcie"] = e2e
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    eng.close()
+
+
+def e2e_rate(torch, eng, n, plen, stride, wire_len, mm, dev, stream):
+    """Host-memory pipeline: pinned host wire -> H2D -> decode -> D2H of the payload region.
+    Recorded in DESIGN.md (PCIe-bound; never the metric)."""
+    host = torch.empty(wire_len, dtype=torch.uint8, pin_memory=True)
+    dwire = torch.empty(wire_len + 64, dtype=torch.uint8, device=dev)
+    eng.gen_frames(dwire, n, plen, SEED, opcode0=2, stream=stream)
+    host.copy_(dwire[:wire_len])
+    back = torch.empty(wire_len, dtype=torch.uint8, pin_memory=True)
+    desc, summ = eng.alloc_outputs(n)
+    reps = 3
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        dwire[:wire_len].copy_(host, non_blocking=True)
+        eng.decode_inplace(dwire, n, stride=stride, max_message_size=mm, wire_len=wire_len,
+                           desc=desc, summary=summ, stream=stream)
+        back.copy_(dwire[:wire_len], non_blocking=True)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return {"value": round(n * plen * reps / el / GIB, 2), "unit": "GiB/s",
+            "note": "pinned host buffer -> H2D -> decode_inplace -> D2H, serial, 1 stream"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,361 @@
+/*
+ * uvhttp_ws_amd.h — C ABI of the MI355X-native WebSocket frame-decode / unmask path.
+ *
+ * Two surfaces live here:
+ *
+ *  1. The DROP-IN decode surface of the reference header include/uvhttp_websocket.h
+ *     (adam-ikari/uvhttp v2.7.0).  Same symbol names, same argument meaning, same
+ *     struct layouts (x86-64: uvhttp_ws_frame_header_t 16 B, uvhttp_ws_frame_t 48 B,
+ *     uvhttp_ws_connection_t 248 B), same error convention (UVHTTP_OK = 0, every decode
+ *     failure UVHTTP_ERROR_INVALID_PARAM = -1).  When the reference header has already
+ *     been included (UVHTTP_WEBSOCKET_H defined) its own type definitions are used and
+ *     only the function prototypes below are re-stated.
+ *
+ *  2. The BATCHED DEVICE surface (new): many masked frames resident in MI355X HBM are
+ *     header-parsed, validated, fragment-checked and unmasked by hand-written gfx950
+ *     kernels.  Plain pointers and sizes only; the stream is an opaque hipStream_t.
+ *     These entry points never compute on the CPU: with no usable GPU they return
+ *     UVHTTP_WS_GPU_ENODEV.
+ *
+ * Batch semantics (the parity contract, checked against the oracle in tests/):
+ *   a batch of n frames laid out back to back is decoded exactly as the reference's
+ *   uvhttp_ws_process_data (src/uvhttp_websocket.c:825-1097) decodes the same bytes when
+ *   it is called once per frame with exactly that frame's wire bytes on a fresh server
+ *   connection with the given limits: frames before the first failing frame are
+ *   delivered (unmasked), the first failing frame and everything after it are left
+ *   untouched, and the failure reason is reported per frame.
+ */
+#ifndef UVHTTP_WS_AMD_H
+#define UVHTTP_WS_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------------------------ */
+/* 1. Drop-in types (ABI-identical to the reference; only when its header is absent)    */
+/* ------------------------------------------------------------------------------------ */
+#ifndef UVHTTP_WEBSOCKET_H
+
+#ifndef UVHTTP_ERROR_H
+/* include/uvhttp_error.h:16-20 — only the two codes the decode path returns. */
+typedef int uvhttp_error_t;
+#define UVHTTP_OK 0
+#define UVHTTP_ERROR_INVALID_PARAM (-1)
+#endif
+
+#ifndef UVHTTP_CONFIG_H
+/* include/uvhttp_config.h — full layout kept so uvhttp_ws_connection_create can read
+ * websocket_* at the reference offsets (64..79). */
+typedef struct {
+    int max_connections;
+    int read_buffer_size;
+    int backlog;
+    int keepalive_timeout;
+    int request_timeout;
+    int connection_timeout;
+    size_t max_body_size;
+    size_t max_header_size;
+    size_t max_url_size;
+    size_t max_file_size;
+    int max_requests_per_connection;
+    int rate_limit_window;
+    int websocket_max_frame_size;
+    int websocket_max_message_size;
+    int websocket_ping_interval;
+    int websocket_ping_timeout;
+    int tcp_keepalive_timeout;
+    int sendfile_timeout_ms;
+    int sendfile_max_retry;
+    int cache_default_max_entries;
+    int cache_default_ttl;
+    int lru_cache_batch_eviction_size;
+    int rate_limit_max_requests;
+    int rate_limit_max_window_seconds;
+    int rate_limit_min_timeout_seconds;
+} uvhttp_config_t;
+#endif
+
+/* mbedtls is never touched on the decode path; the pointer is carried opaquely. */
+typedef struct mbedtls_ssl_context mbedtls_ssl_context;
+
+/* include/uvhttp_websocket.h:24-31 */
+typedef enum {
+    UVHTTP_WS_OPCODE_CONTINUATION = 0x0,
+    UVHTTP_WS_OPCODE_TEXT = 0x1,
+    UVHTTP_WS_OPCODE_BINARY = 0x2,
+    UVHTTP_WS_OPCODE_CLOSE = 0x8,
+    UVHTTP_WS_OPCODE_PING = 0x9,
+    UVHTTP_WS_OPCODE_PONG = 0xA
+} uvhttp_ws_opcode_t;
+
+/* include/uvhttp_websocket.h:34-39 */
+typedef enum {
+    UVHTTP_WS_STATE_CONNECTING = 0,
+    UVHTTP_WS_STATE_OPEN = 1,
+    UVHTTP_WS_STATE_CLOSING = 2,
+    UVHTTP_WS_STATE_CLOSED = 3
+} uvhttp_ws_state_t;
+
+/* include/uvhttp_websocket.h:42-51 — 16 bytes, payload_length at offset 8. */
+typedef struct {
+    uint8_t fin : 1;
+    uint8_t rsv1 : 1;
+    uint8_t rsv2 : 1;
+    uint8_t rsv3 : 1;
+    uint8_t opcode : 4;
+    uint8_t mask : 1;
+    uint8_t payload_len : 7;  /* raw 7-bit length code (0..127) */
+    uint64_t payload_length;  /* decoded length */
+} uvhttp_ws_frame_header_t;
+
+/* include/uvhttp_websocket.h:54-60 — 48 bytes. */
+typedef struct {
+    uvhttp_ws_frame_header_t header;
+    uint64_t payload_length;
+    uint8_t masking_key[4];
+    uint8_t* payload;
+    size_t payload_size;
+} uvhttp_ws_frame_t;
+
+/* include/uvhttp_websocket.h:63-69 */
+typedef struct {
+    int max_frame_size;
+    int max_message_size;
+    int ping_interval;
+    int ping_timeout;
+    int enable_compression;
+} uvhttp_ws_config_t;
+
+struct uvhttp_ws_connection;
+
+/* include/uvhttp_websocket.h:75-82 */
+typedef int (*uvhttp_ws_on_message_callback)(struct uvhttp_ws_connection* conn,
+                                             const char* data, size_t len, int opcode);
+typedef int (*uvhttp_ws_on_close_callback)(struct uvhttp_ws_connection* conn, int code,
+                                           const char* reason);
+typedef int (*uvhttp_ws_on_error_callback)(struct uvhttp_ws_connection* conn,
+                                           int error_code, const char* error_msg);
+
+/* include/uvhttp_websocket.h:85-121 — 248 bytes. */
+typedef struct uvhttp_ws_connection {
+    int fd;
+    uvhttp_ws_state_t state;
+    uvhttp_ws_config_t config;
+    mbedtls_ssl_context* ssl;
+    int is_server;
+    char client_key[64];
+    uint8_t* recv_buffer;
+    size_t recv_buffer_size;
+    size_t recv_buffer_pos;
+    uint8_t* send_buffer;
+    size_t send_buffer_size;
+    uint8_t* fragmented_message;
+    size_t fragmented_size;
+    size_t fragmented_capacity;
+    uvhttp_ws_opcode_t fragmented_opcode;
+    uvhttp_ws_on_message_callback on_message;
+    uvhttp_ws_on_close_callback on_close;
+    uvhttp_ws_on_error_callback on_error;
+    void* user_data;
+    uint64_t bytes_sent;
+    uint64_t bytes_received;
+    uint64_t frames_sent;
+    uint64_t frames_received;
+} uvhttp_ws_connection_t;
+
+#endif /* !UVHTTP_WEBSOCKET_H */
+
+/* Reference defaults (include/uvhttp_defaults.h:171-207). */
+#define UVHTTP_WS_AMD_DEFAULT_MAX_FRAME_SIZE (16 * 1024 * 1024)
+#define UVHTTP_WS_AMD_DEFAULT_MAX_MESSAGE_SIZE (64 * 1024 * 1024)
+#define UVHTTP_WS_AMD_DEFAULT_RECV_BUFFER_SIZE (64 * 1024)
+#define UVHTTP_WS_AMD_DEFAULT_PING_INTERVAL 30
+#define UVHTTP_WS_AMD_DEFAULT_PING_TIMEOUT 10
+
+/* ------------------------------------------------------------------------------------ */
+/* 1b. Drop-in decode functions (replace the reference symbols of the same name)        */
+/* ------------------------------------------------------------------------------------ */
+
+/* replaces src/uvhttp_websocket.c:71-109 (decl include/uvhttp_websocket.h:128-130) */
+struct uvhttp_ws_connection* uvhttp_ws_connection_create(int fd, mbedtls_ssl_context* ssl,
+                                                         int is_server,
+                                                         const uvhttp_config_t* config);
+/* replaces src/uvhttp_websocket.c:112-130 (decl include/uvhttp_websocket.h:135) */
+void uvhttp_ws_connection_free(struct uvhttp_ws_connection* conn);
+/* replaces src/uvhttp_websocket.c:1100-1111 (decl include/uvhttp_websocket.h:217-220) */
+void uvhttp_ws_set_callbacks(struct uvhttp_ws_connection* conn,
+                             uvhttp_ws_on_message_callback on_message,
+                             uvhttp_ws_on_close_callback on_close,
+                             uvhttp_ws_on_error_callback on_error);
+/* replaces src/uvhttp_websocket.c:133-185 (decl include/uvhttp_websocket.h:228-230) */
+uvhttp_error_t uvhttp_ws_parse_frame_header(const uint8_t* data, size_t len,
+                                            uvhttp_ws_frame_header_t* header,
+                                            size_t* header_size);
+/* replaces src/uvhttp_websocket.c:188-197 (decl include/uvhttp_websocket.h:250-251) */
+void uvhttp_ws_apply_mask(uint8_t* data, size_t len, const uint8_t* masking_key);
+/* replaces src/uvhttp_websocket.c:825-1097 (decl include/uvhttp_websocket.h:212-213) */
+uvhttp_error_t uvhttp_ws_process_data(struct uvhttp_ws_connection* conn, const uint8_t* data,
+                                      size_t len);
+
+/* Control-frame hook (new).  The reference answers PING with uvhttp_ws_send_pong and
+ * echoes CLOSE with uvhttp_ws_send_frame through the server wrapper stored in
+ * conn->user_data (src/uvhttp_websocket.c:1028-1084); the send side is outside this
+ * library, so the integration layer registers this sink and forwards to those calls
+ * (INTEGRATION.md).  opcode is UVHTTP_WS_OPCODE_PONG (reply to a PING, payload = the
+ * ping payload) or UVHTTP_WS_OPCODE_CLOSE (echo, payload = code + reason, <= 127 B).
+ * It is called only when conn->user_data != NULL, exactly where the reference sends. */
+typedef void (*uvhttp_ws_amd_control_sink)(struct uvhttp_ws_connection* conn, int opcode,
+                                           const uint8_t* payload, size_t len);
+void uvhttp_ws_amd_set_control_sink(uvhttp_ws_amd_control_sink sink);
+
+/* ------------------------------------------------------------------------------------ */
+/* 2. Batched device surface (MI355X / gfx950)                                          */
+/* ------------------------------------------------------------------------------------ */
+
+/* Return codes of the device surface (0 = OK; negative = failure, nothing launched). */
+#define UVHTTP_WS_GPU_OK 0
+#define UVHTTP_WS_GPU_EINVAL (-1)  /* bad argument (NULL, misaligned, sizes) */
+#define UVHTTP_WS_GPU_ENODEV (-2)  /* no usable MI355X / HIP runtime error at setup */
+#define UVHTTP_WS_GPU_ENOMEM (-3)  /* device workspace allocation failed */
+#define UVHTTP_WS_GPU_ELAUNCH (-4) /* kernel launch / HIP call failed */
+
+/* Per-frame status (uvhttp_ws_frame_desc_t.status).  Negative values are the reasons
+ * uvhttp_ws_process_data returns UVHTTP_ERROR_INVALID_PARAM, with the reference check
+ * that raises each one. */
+#define UVHTTP_WS_FRAME_OK 0
+#define UVHTTP_WS_FRAME_INCOMPLETE 1        /* last frame not fully present (need more data, :925-932) */
+#define UVHTTP_WS_FRAME_SKIPPED 2           /* after the first failing frame: not processed */
+#define UVHTTP_WS_FRAME_ERR_PARSE (-1)      /* 64-bit length with MSB set (:178-180) */
+#define UVHTTP_WS_FRAME_ERR_RSV (-2)        /* RSV1-3 set (:895-897) */
+#define UVHTTP_WS_FRAME_ERR_CONTROL (-3)    /* control frame > 125 B or FIN=0 (:902-906) */
+#define UVHTTP_WS_FRAME_ERR_UNMASKED (-4)   /* server got an unmasked frame (:910-912) */
+#define UVHTTP_WS_FRAME_ERR_TOO_BIG (-5)    /* payload > max_frame_size (:919-921) */
+#define UVHTTP_WS_FRAME_ERR_BUFFER (-6)     /* wire bytes exceed recv-buffer cap (:851-857) */
+#define UVHTTP_WS_FRAME_ERR_FRAGMENT (-7)   /* CONT with no start / data inside fragment (:964-996) */
+#define UVHTTP_WS_FRAME_ERR_MESSAGE (-8)    /* fragments exceed max_message_size (:786-791) */
+#define UVHTTP_WS_FRAME_ERR_LAYOUT (-9)     /* offset table disagrees with the frame lengths */
+
+/* Frame flags (uvhttp_ws_frame_desc_t.flags). */
+#define UVHTTP_WS_FLAG_FIN 0x01u
+#define UVHTTP_WS_FLAG_MASK 0x02u
+#define UVHTTP_WS_FLAG_RSV1 0x04u
+#define UVHTTP_WS_FLAG_RSV2 0x08u
+#define UVHTTP_WS_FLAG_RSV3 0x10u
+#define UVHTTP_WS_FLAG_MSG_END 0x20u  /* this frame completes a data message (on_message fires) */
+
+/* One decoded frame (device-written, 32 bytes). */
+typedef struct {
+    uint64_t payload_off;  /* byte offset of the unmasked payload: in the wire buffer
+                              (in-place decode, and control frames of a compact decode)
+                              or in the message arena (data frames of a compact decode) */
+    uint64_t payload_len;  /* header.payload_length */
+    uint32_t masking_key;  /* key bytes k0..k3 as a little-endian word (k0 = low byte) */
+    uint32_t message;      /* index of the message this data frame belongs to (compact) */
+    uint8_t opcode;        /* header.opcode */
+    uint8_t flags;         /* UVHTTP_WS_FLAG_* */
+    uint8_t header_size;   /* 2 / 4 / 10 (mask key excluded, as parse_frame_header) */
+    int8_t status;         /* UVHTTP_WS_FRAME_* */
+    uint32_t wire_len;     /* header + key + payload bytes (saturated at 2^32-1) */
+} uvhttp_ws_frame_desc_t;
+
+/* One complete data message (compact decode only, 32 bytes).  The payload handed to
+ * on_message is arena[arena_off, arena_off + len); the opcode is the first frame's. */
+typedef struct {
+    uint64_t arena_off;
+    uint64_t len;
+    uint32_t first_frame;
+    uint32_t last_frame;
+    int32_t opcode;
+    uint32_t reserved;
+} uvhttp_ws_message_desc_t;
+
+/* Batch summary (device-written; copy back after the stream completes). */
+typedef struct {
+    uint32_t n_frames;        /* frames in the batch */
+    uint32_t n_delivered;     /* frames processed before the first failing frame */
+    int32_t status;           /* UVHTTP_OK, or UVHTTP_ERROR_INVALID_PARAM on a failing frame */
+    int32_t first_status;     /* status of frame n_delivered (0 if all delivered) */
+    uint64_t consumed_bytes;  /* wire bytes of the delivered frames (recv-buffer drain) */
+    uint64_t payload_bytes;   /* sum of delivered payload bytes */
+    uint32_t n_messages;      /* complete data messages among the delivered frames */
+    uint32_t state_closed;    /* 1 if a delivered CLOSE frame set state = CLOSED */
+    uint64_t arena_bytes;     /* compact: arena bytes written */
+    uint64_t pending_bytes;   /* bytes of a fragmented message still open at the end */
+} uvhttp_ws_batch_summary_t;
+
+/* A batch of frames resident in device memory. */
+typedef struct {
+    uint8_t* wire;             /* device pointer, 16-byte aligned; frames back to back */
+    uint64_t wire_len;         /* bytes readable at wire */
+    const uint64_t* frame_off; /* device pointer: n_frames start offsets, or NULL */
+    uint64_t frame_stride;     /* when frame_off == NULL: frame i starts at i*stride */
+    uint32_t n_frames;
+    int32_t max_frame_size;    /* uvhttp_ws_config_t.max_frame_size */
+    int32_t max_message_size;  /* uvhttp_ws_config_t.max_message_size */
+    int32_t is_server;         /* 1: unmasked frames are rejected (reference server) */
+} uvhttp_ws_batch_t;
+
+typedef struct uvhttp_ws_gpu_engine uvhttp_ws_gpu_engine_t;
+
+/* Create an engine bound to HIP device `device` (owns the scratch workspace). */
+int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out);
+void uvhttp_ws_gpu_engine_free(uvhttp_ws_gpu_engine_t* eng);
+/* Pre-size the workspace so later decode calls never allocate (hipGraph capture). */
+int uvhttp_ws_gpu_engine_reserve(uvhttp_ws_gpu_engine_t* eng, uint32_t max_frames,
+                                 uint64_t max_wire_bytes, uint64_t max_arena_bytes);
+/* Kernel timing: when enabled, HIP events bracket the dominant (payload) kernel of every
+ * decode call on its stream; kernel_time returns the summed milliseconds and the number
+ * of bracketed launches completed so far (synchronises on the last event). */
+int uvhttp_ws_gpu_engine_set_timing(uvhttp_ws_gpu_engine_t* eng, int enable);
+int uvhttp_ws_gpu_engine_kernel_time(uvhttp_ws_gpu_engine_t* eng, double* ms,
+                                     uint64_t* launches);
+const char* uvhttp_ws_gpu_engine_last_error(const uvhttp_ws_gpu_engine_t* eng);
+
+/* In-place decode: parse + validate every frame, run the fragment state machine, then
+ * unmask the payload of every delivered frame in place in batch->wire (the reference
+ * unmasks inside recv_buffer, src/uvhttp_websocket.c:937-947).  d_desc (n_frames
+ * entries) and d_summary are device pointers.  Asynchronous on `stream`. */
+int uvhttp_ws_gpu_decode_inplace(uvhttp_ws_gpu_engine_t* eng, const uvhttp_ws_batch_t* batch,
+                                 uvhttp_ws_frame_desc_t* d_desc,
+                                 uvhttp_ws_batch_summary_t* d_summary, void* stream);
+
+/* Compact decode: as above, but data-frame payloads are unmasked out of place into
+ * d_arena at the exclusive prefix sum of data payload lengths, so every message —
+ * including a fragmented one (uvhttp_ws_fragment_append, :781-822) — is one contiguous
+ * arena range described by d_msgs.  Control-frame payloads are unmasked in place in the
+ * wire.  d_msgs needs room for n_frames entries; arena_cap must cover the data payload. */
+int uvhttp_ws_gpu_decode_compact(uvhttp_ws_gpu_engine_t* eng, const uvhttp_ws_batch_t* batch,
+                                 uint8_t* d_arena, uint64_t arena_cap,
+                                 uvhttp_ws_frame_desc_t* d_desc,
+                                 uvhttp_ws_message_desc_t* d_msgs,
+                                 uvhttp_ws_batch_summary_t* d_summary, void* stream);
+
+/* Unmask only (no framing): data[i] ^= key[i % 4] for a device buffer — the batched form
+ * of uvhttp_ws_apply_mask for callers that parsed headers themselves. */
+int uvhttp_ws_gpu_apply_mask(uvhttp_ws_gpu_engine_t* eng, uint8_t* d_data, uint64_t len,
+                             const uint8_t masking_key[4], void* stream);
+
+/* Synthetic masked-frame generator (bench / parity inputs; not on the decode path).
+ * Writes n_frames frames of payload_len bytes back to back at d_wire (stride =
+ * header + 4 + payload_len).  Frame i: opcode = (i == 0 || !fragmented) ? opcode0 :
+ * CONTINUATION; FIN = !fragmented || i == n_frames - 1; key = splitmix64(seed ^ i)
+ * low 32 bits (frames 0 and 1 forced to 0x00000000 / 0xFFFFFFFF when force_keys);
+ * plaintext byte b = byte (b & 7) of splitmix64(seed + ((uint64)i << 32) + (b >> 3)).
+ * Same definition as oracle/ws_oracle.c:oracle_gen_frames. */
+uint64_t uvhttp_ws_gen_frame_stride(uint64_t payload_len);
+int uvhttp_ws_gpu_gen_frames(uvhttp_ws_gpu_engine_t* eng, uint8_t* d_wire, uint32_t n_frames,
+                             uint64_t payload_len, uint64_t seed, int opcode0, int fragmented,
+                             int force_keys, void* stream);
+
+/* Library identity, for the loader checks in tests/. */
+const char* uvhttp_ws_amd_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* UVHTTP_WS_AMD_H */

@@ -1,0 +1,205 @@
+"""ctypes binding of the CPU oracle (oracle/ws_oracle.c) — test infrastructure only.
+
+Used by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg; never by the
+product package.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(REPO, "oracle", "_build", "libws_oracle.so")
+
+
+class OrcHeader(C.Structure):
+    _fields_ = [("fin", C.c_uint8), ("rsv1", C.c_uint8), ("rsv2", C.c_uint8),
+                ("rsv3", C.c_uint8), ("opcode", C.c_uint8), ("mask", C.c_uint8),
+                ("len_code", C.c_uint8), ("payload_length", C.c_uint64)]
+
+
+class OrcSummary(C.Structure):
+    _fields_ = [("n_frames", C.c_uint32), ("n_delivered", C.c_uint32), ("status", C.c_int32),
+                ("first_status", C.c_int32), ("consumed_bytes", C.c_uint64),
+                ("payload_bytes", C.c_uint64), ("n_messages", C.c_uint32),
+                ("state_closed", C.c_uint32), ("arena_bytes", C.c_uint64),
+                ("pending_bytes", C.c_uint64)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_L = None
+
+
+def load():
+    global _L
+    if _L is not None:
+        return _L
+    if not os.path.exists(ORACLE_SO):
+        subprocess.run(["make", "-C", os.path.join(REPO, "oracle")], check=True,
+                       stdout=subprocess.DEVNULL)
+    L = C.CDLL(ORACLE_SO)
+    vp, u32, u64, i32, sz = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int32, C.c_size_t
+    sig = {
+        "oracle_parse_frame_header": (C.c_int, [vp, sz, C.POINTER(OrcHeader), C.POINTER(sz)]),
+        "oracle_apply_mask": (None, [vp, sz, vp]),
+        "oracle_conn_new": (vp, [C.c_int, C.c_int, C.c_int, C.c_int]),
+        "oracle_conn_free": (None, [vp]),
+        "oracle_conn_set_wrapper": (None, [vp, C.c_int]),
+        "oracle_conn_set_digest": (None, [vp, C.c_int]),
+        "oracle_conn_set_recv_state": (C.c_int, [vp, sz, vp, sz]),
+        "oracle_conn_state": (C.c_int, [vp]),
+        "oracle_conn_last_reason": (C.c_int, [vp]),
+        "oracle_conn_n_events": (u64, [vp]),
+        "oracle_conn_n_messages": (u64, [vp]),
+        "oracle_conn_digest": (u64, [vp]),
+        "oracle_conn_recv_pos": (sz, [vp]),
+        "oracle_conn_recv_size": (sz, [vp]),
+        "oracle_conn_frag_size": (sz, [vp]),
+        "oracle_conn_events": (sz, [vp, vp, sz]),
+        "oracle_process_data": (C.c_int, [vp, vp, sz]),
+        "oracle_decode_batch": (C.c_int, [vp, u64, vp, u64, u32, C.c_int, C.c_int, C.c_int, vp,
+                                          u64, vp, vp, vp, vp, C.POINTER(OrcSummary)]),
+        "oracle_gen_stride": (u64, [u64]),
+        "oracle_gen_key": (u32, [u64, u32, C.c_int]),
+        "oracle_gen_frames": (None, [vp, u32, u32, u32, u64, u64, C.c_int, C.c_int, C.c_int]),
+        "oracle_gen_plain": (None, [vp, u32, u64, u64]),
+        "oracle_unmask_frames": (u64, [vp, u32, u64]),
+        "oracle_stream_decode": (u64, [vp, u64, sz, C.c_int, C.c_int, C.POINTER(u64)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _ = i32
+    _L = L
+    return L
+
+
+def _ptr(a: np.ndarray):
+    return C.c_void_p(a.ctypes.data) if a is not None and a.size else None
+
+
+def parse_frame_header(data: bytes, length=None, null=None):
+    L = load()
+    buf = (C.c_uint8 * max(1, len(data))).from_buffer_copy(bytes(data) or b"\0")
+    n = len(data) if length is None else length
+    h, hs = OrcHeader(), C.c_size_t(0)
+    rc = L.oracle_parse_frame_header(None if null == "data" else buf, n,
+                                     None if null == "header" else C.byref(h),
+                                     None if null == "header_size" else C.byref(hs))
+    return rc, h, hs.value
+
+
+def apply_mask(data: bytearray, key, length=None, null=None):
+    L = load()
+    n = len(data) if length is None else length
+    buf = (C.c_uint8 * max(1, len(data))).from_buffer(data) if len(data) else None
+    kb = (C.c_uint8 * 4).from_buffer_copy(bytes(key)) if key else None
+    L.oracle_apply_mask(None if null == "data" else buf, n, None if null == "key" else kb)
+    return data
+
+
+EV_MESSAGE, EV_CLOSE, EV_PONG, EV_CLOSE_ECHO = 1, 2, 3, 4
+
+
+class OracleConn:
+    def __init__(self, is_server=1, max_frame_size=16 * 1024 * 1024,
+                 max_message_size=64 * 1024 * 1024, record=1, wrapper=False):
+        self.L = load()
+        self.c = self.L.oracle_conn_new(is_server, max_frame_size, max_message_size, record)
+        if wrapper:
+            self.L.oracle_conn_set_wrapper(self.c, 1)
+
+    def set_recv_state(self, size, fill: bytes, pos):
+        buf = (C.c_uint8 * max(1, pos)).from_buffer_copy(fill[:pos] + b"\0" * (pos - len(fill[:pos])) if pos else b"\0")
+        return self.L.oracle_conn_set_recv_state(self.c, size, buf, pos)
+
+    def process_data(self, data: bytes, length=None, null=False):
+        buf = (C.c_uint8 * max(1, len(data))).from_buffer_copy(bytes(data) or b"\0")
+        n = len(data) if length is None else length
+        return self.L.oracle_process_data(self.c, None if null else buf, n)
+
+    @property
+    def state(self):
+        return self.L.oracle_conn_state(self.c)
+
+    @property
+    def recv_size(self):
+        return self.L.oracle_conn_recv_size(self.c)
+
+    @property
+    def last_reason(self):
+        return self.L.oracle_conn_last_reason(self.c)
+
+    def events(self):
+        n = self.L.oracle_conn_events(self.c, None, 0)
+        raw = (C.c_uint8 * max(1, n))()
+        self.L.oracle_conn_events(self.c, raw, n)
+        b = bytes(raw)[:n]
+        out, i = [], 0
+        while i < n:
+            typ = b[i]
+            a = int.from_bytes(b[i + 1:i + 5], "little", signed=True)
+            ln = int.from_bytes(b[i + 5:i + 13], "little")
+            payload = b[i + 13:i + 13 + ln]
+            i += 13 + ln
+            name = {EV_MESSAGE: "message", EV_CLOSE: "close", EV_PONG: "pong",
+                    EV_CLOSE_ECHO: "close_echo"}[typ]
+            out.append((name, a, payload))
+        return out
+
+    def __del__(self):
+        try:
+            self.L.oracle_conn_free(self.c)
+        except Exception:
+            pass
+
+
+def decode_batch(wire: np.ndarray, n_frames, stride=None, offsets=None, wire_len=None,
+                 max_frame_size=16 * 1024 * 1024, max_message_size=64 * 1024 * 1024,
+                 is_server=1, compact=False, arena_cap=None):
+    """Oracle batch decode; returns dict(wire=…, arena=…, status=…, summary=…, msgs=…).
+    `wire` is copied (the caller's array is not modified)."""
+    L = load()
+    w = np.array(wire, dtype=np.uint8, copy=True)
+    wl = w.size if wire_len is None else wire_len
+    status = np.zeros(max(1, n_frames), dtype=np.int8)
+    msg_off = np.zeros(max(1, n_frames), dtype=np.uint64)
+    msg_len = np.zeros(max(1, n_frames), dtype=np.uint64)
+    msg_op = np.zeros(max(1, n_frames), dtype=np.int32)
+    arena = None
+    if compact:
+        cap = w.size if arena_cap is None else arena_cap
+        arena = np.zeros(max(1, cap), dtype=np.uint8)
+    offs = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
+    s = OrcSummary()
+    L.oracle_decode_batch(_ptr(w), wl, _ptr(offs), stride or 0, n_frames, max_frame_size,
+                          max_message_size, is_server, _ptr(arena),
+                          0 if arena is None else arena.size, _ptr(status), _ptr(msg_off),
+                          _ptr(msg_len), _ptr(msg_op), C.byref(s))
+    sd = s.as_dict()
+    nm = sd["n_messages"]
+    return dict(wire=w, arena=arena, status=status[:n_frames], summary=sd,
+                msg_off=msg_off[:nm], msg_len=msg_len[:nm], msg_opcode=msg_op[:nm])
+
+
+def gen_frames(n_frames, payload_len, seed, opcode0=2, fragmented=False, force_keys=False,
+               first=0, count=None, total=None):
+    L = load()
+    stride = int(L.oracle_gen_stride(payload_len))
+    count = n_frames if count is None else count
+    total = n_frames if total is None else total
+    out = np.empty(stride * count, dtype=np.uint8)
+    L.oracle_gen_frames(_ptr(out), first, count, total, payload_len, seed, opcode0,
+                        1 if fragmented else 0, 1 if force_keys else 0)
+    return out, stride
+
+
+def gen_plain(i, payload_len, seed):
+    L = load()
+    out = np.empty(max(1, payload_len), dtype=np.uint8)
+    L.oracle_gen_plain(_ptr(out), i, payload_len, seed)
+    return out[:payload_len]

@@ -1,0 +1,62 @@
+"""The C-ABI library loads and exports every function include/*.h declares; the device
+surface refuses cleanly (ENODEV) where there is no MI355X.  No compute on a GPU here."""
+import ctypes as C
+import glob
+import os
+import re
+
+import pytest
+
+import uvhttp_amd as U
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_functions():
+    names = set()
+    for h in glob.glob(os.path.join(REPO, "include", "*.h")):
+        src = open(h).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        for m in re.finditer(r"^[A-Za-z_][\w\s\*]*?\b(uvhttp_\w+)\s*\(", src, flags=re.M):
+            if "typedef" in src[src.rfind("\n", 0, m.start()) + 1:m.end()]:
+                continue
+            names.add(m.group(1))
+    return sorted(names)
+
+
+def test_every_declared_symbol_is_exported():
+    names = _declared_functions()
+    assert len(names) >= 19, names
+    L = C.CDLL(U.LIB_PATH)
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+
+
+def test_version_string():
+    assert b"gfx950" in U.lib().uvhttp_ws_amd_version()
+
+
+def test_gfx950_code_object_present():
+    """The library carries a gfx950 code object (offload bundle)."""
+    blob = open(U.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_no_gpu_means_enodev():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    h = C.c_void_p()
+    assert U.lib().uvhttp_ws_gpu_engine_create(0, C.byref(h)) == -2
+    with pytest.raises(U.GpuError):
+        U.GpuEngine(0)
+
+
+def test_product_does_not_reference_oracle():
+    """The product library and package never load the oracle (no CPU fallback path)."""
+    for p in glob.glob(os.path.join(REPO, "uvhttp_amd", "**", "*"), recursive=True):
+        if os.path.isfile(p) and p.endswith((".py", ".c", ".hip", ".h")):
+            txt = open(p).read()
+            assert "libws_oracle" not in txt and "import _oracle" not in txt, p
+    blob = open(U.LIB_PATH, "rb").read()
+    assert b"libws_oracle" not in blob and b"oracle_" not in blob

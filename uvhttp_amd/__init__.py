@@ -1,0 +1,405 @@
+"""uvhttp_amd — MI355X-native WebSocket frame decode / payload unmask for uvhttp.
+
+The product is the C-ABI library ``uvhttp_amd/lib/libuvhttp_ws_amd.so`` (gfx950 HIP kernels
++ host C), declared in ``include/uvhttp_ws_amd.h``.  This package is a thin ctypes mirror of
+that ABI so tests and ``bench.py`` can drive it from Python:
+
+* the reference's decode surface (``src/uvhttp_websocket.c`` of adam-ikari/uvhttp v2.7.0):
+  :func:`parse_frame_header`, :func:`apply_mask`, :class:`WsConnection` (``process_data``);
+* the batched device surface: :class:`GpuEngine` (``decode_inplace`` / ``decode_compact``).
+
+Nothing here computes a result in Python, and there is no CPU fallback: if the library is
+missing, :func:`lib` raises; if no MI355X is present, :class:`GpuEngine` raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+__all__ = [
+    "lib", "LIB_PATH", "FrameHeader", "FrameDesc", "MessageDesc", "BatchSummary", "Batch",
+    "WsConnectionStruct", "parse_frame_header", "apply_mask", "WsConnection", "GpuEngine",
+    "GpuError", "OPCODES", "FRAME_STATUS", "gen_frame_stride",
+]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libuvhttp_ws_amd.so")
+
+OPCODES = dict(CONTINUATION=0x0, TEXT=0x1, BINARY=0x2, CLOSE=0x8, PING=0x9, PONG=0xA)
+FRAME_STATUS = {
+    0: "OK", 1: "INCOMPLETE", 2: "SKIPPED", -1: "ERR_PARSE", -2: "ERR_RSV", -3: "ERR_CONTROL",
+    -4: "ERR_UNMASKED", -5: "ERR_TOO_BIG", -6: "ERR_BUFFER", -7: "ERR_FRAGMENT",
+    -8: "ERR_MESSAGE", -9: "ERR_LAYOUT",
+}
+FLAG_FIN, FLAG_MASK, FLAG_MSG_END = 0x01, 0x02, 0x20
+
+
+class GpuError(RuntimeError):
+    pass
+
+
+# ---- struct mirrors (include/uvhttp_ws_amd.h) ------------------------------------------
+
+class FrameHeader(C.Structure):
+    """uvhttp_ws_frame_header_t (16 B; bitfields in bytes 0-1, payload_length @8)."""
+    _fields_ = [("fin", C.c_uint8, 1), ("rsv1", C.c_uint8, 1), ("rsv2", C.c_uint8, 1),
+                ("rsv3", C.c_uint8, 1), ("opcode", C.c_uint8, 4), ("mask", C.c_uint8, 1),
+                ("payload_len", C.c_uint8, 7), ("payload_length", C.c_uint64)]
+
+
+class FrameDesc(C.Structure):
+    _fields_ = [("payload_off", C.c_uint64), ("payload_len", C.c_uint64),
+                ("masking_key", C.c_uint32), ("message", C.c_uint32), ("opcode", C.c_uint8),
+                ("flags", C.c_uint8), ("header_size", C.c_uint8), ("status", C.c_int8),
+                ("wire_len", C.c_uint32)]
+
+
+class MessageDesc(C.Structure):
+    _fields_ = [("arena_off", C.c_uint64), ("len", C.c_uint64), ("first_frame", C.c_uint32),
+                ("last_frame", C.c_uint32), ("opcode", C.c_int32), ("reserved", C.c_uint32)]
+
+
+class BatchSummary(C.Structure):
+    _fields_ = [("n_frames", C.c_uint32), ("n_delivered", C.c_uint32), ("status", C.c_int32),
+                ("first_status", C.c_int32), ("consumed_bytes", C.c_uint64),
+                ("payload_bytes", C.c_uint64), ("n_messages", C.c_uint32),
+                ("state_closed", C.c_uint32), ("arena_bytes", C.c_uint64),
+                ("pending_bytes", C.c_uint64)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class Batch(C.Structure):
+    _fields_ = [("wire", C.c_void_p), ("wire_len", C.c_uint64), ("frame_off", C.c_void_p),
+                ("frame_stride", C.c_uint64), ("n_frames", C.c_uint32),
+                ("max_frame_size", C.c_int32), ("max_message_size", C.c_int32),
+                ("is_server", C.c_int32)]
+
+
+ON_MESSAGE = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_char), C.c_size_t, C.c_int)
+ON_CLOSE = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_char_p)
+ON_ERROR = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_char_p)
+CONTROL_SINK = C.CFUNCTYPE(None, C.c_void_p, C.c_int, C.POINTER(C.c_uint8), C.c_size_t)
+
+
+class WsConfig(C.Structure):
+    _fields_ = [("max_frame_size", C.c_int), ("max_message_size", C.c_int),
+                ("ping_interval", C.c_int), ("ping_timeout", C.c_int),
+                ("enable_compression", C.c_int)]
+
+
+class WsConnectionStruct(C.Structure):
+    """uvhttp_ws_connection_t (248 B on x86-64)."""
+    _fields_ = [("fd", C.c_int), ("state", C.c_int), ("config", WsConfig),
+                ("ssl", C.c_void_p), ("is_server", C.c_int), ("client_key", C.c_char * 64),
+                ("recv_buffer", C.c_void_p), ("recv_buffer_size", C.c_size_t),
+                ("recv_buffer_pos", C.c_size_t), ("send_buffer", C.c_void_p),
+                ("send_buffer_size", C.c_size_t), ("fragmented_message", C.c_void_p),
+                ("fragmented_size", C.c_size_t), ("fragmented_capacity", C.c_size_t),
+                ("fragmented_opcode", C.c_int), ("on_message", C.c_void_p),
+                ("on_close", C.c_void_p), ("on_error", C.c_void_p), ("user_data", C.c_void_p),
+                ("bytes_sent", C.c_uint64), ("bytes_received", C.c_uint64),
+                ("frames_sent", C.c_uint64), ("frames_received", C.c_uint64)]
+
+
+class UvhttpConfig(C.Structure):
+    """uvhttp_config_t (include/uvhttp_config.h); websocket_* at offsets 64..79."""
+    _fields_ = [("max_connections", C.c_int), ("read_buffer_size", C.c_int),
+                ("backlog", C.c_int), ("keepalive_timeout", C.c_int),
+                ("request_timeout", C.c_int), ("connection_timeout", C.c_int),
+                ("max_body_size", C.c_size_t), ("max_header_size", C.c_size_t),
+                ("max_url_size", C.c_size_t), ("max_file_size", C.c_size_t),
+                ("max_requests_per_connection", C.c_int), ("rate_limit_window", C.c_int),
+                ("websocket_max_frame_size", C.c_int), ("websocket_max_message_size", C.c_int),
+                ("websocket_ping_interval", C.c_int), ("websocket_ping_timeout", C.c_int),
+                ("tcp_keepalive_timeout", C.c_int), ("sendfile_timeout_ms", C.c_int),
+                ("sendfile_max_retry", C.c_int), ("cache_default_max_entries", C.c_int),
+                ("cache_default_ttl", C.c_int), ("lru_cache_batch_eviction_size", C.c_int),
+                ("rate_limit_max_requests", C.c_int), ("rate_limit_max_window_seconds", C.c_int),
+                ("rate_limit_min_timeout_seconds", C.c_int)]
+
+
+# ---- library ----------------------------------------------------------------------------
+
+_LIB = None
+
+
+def lib() -> C.CDLL:
+    """Load the product library.  Raises if it has not been built (no fallback)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} missing: run `make` (or __graft_entry__.build())")
+    try:  # share torch's HIP runtime (same SONAME) so torch device pointers are valid
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    L = C.CDLL(LIB_PATH)
+    vp, u32, u64, i32 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int32
+    sig = {
+        "uvhttp_ws_amd_version": (C.c_char_p, []),
+        "uvhttp_ws_parse_frame_header": (C.c_int, [vp, C.c_size_t, C.POINTER(FrameHeader),
+                                                   C.POINTER(C.c_size_t)]),
+        "uvhttp_ws_apply_mask": (None, [vp, C.c_size_t, vp]),
+        "uvhttp_ws_connection_create": (C.POINTER(WsConnectionStruct),
+                                        [C.c_int, vp, C.c_int, C.POINTER(UvhttpConfig)]),
+        "uvhttp_ws_connection_free": (None, [C.POINTER(WsConnectionStruct)]),
+        "uvhttp_ws_set_callbacks": (None, [C.POINTER(WsConnectionStruct), ON_MESSAGE, ON_CLOSE,
+                                           ON_ERROR]),
+        "uvhttp_ws_process_data": (C.c_int, [C.POINTER(WsConnectionStruct), vp, C.c_size_t]),
+        "uvhttp_ws_amd_set_control_sink": (None, [CONTROL_SINK]),
+        "uvhttp_ws_gpu_engine_create": (C.c_int, [C.c_int, C.POINTER(vp)]),
+        "uvhttp_ws_gpu_engine_free": (None, [vp]),
+        "uvhttp_ws_gpu_engine_reserve": (C.c_int, [vp, u32, u64, u64]),
+        "uvhttp_ws_gpu_engine_set_timing": (C.c_int, [vp, C.c_int]),
+        "uvhttp_ws_gpu_engine_kernel_time": (C.c_int, [vp, C.POINTER(C.c_double),
+                                                       C.POINTER(u64)]),
+        "uvhttp_ws_gpu_engine_last_error": (C.c_char_p, [vp]),
+        "uvhttp_ws_gpu_decode_inplace": (C.c_int, [vp, C.POINTER(Batch), vp, vp, vp]),
+        "uvhttp_ws_gpu_decode_compact": (C.c_int, [vp, C.POINTER(Batch), vp, u64, vp, vp, vp,
+                                                   vp]),
+        "uvhttp_ws_gpu_apply_mask": (C.c_int, [vp, vp, u64, vp, vp]),
+        "uvhttp_ws_gen_frame_stride": (u64, [u64]),
+        "uvhttp_ws_gpu_gen_frames": (C.c_int, [vp, vp, u32, u64, u64, C.c_int, C.c_int, C.c_int,
+                                               vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _ = i32
+    _LIB = L
+    return L
+
+
+def gen_frame_stride(payload_len: int) -> int:
+    return int(lib().uvhttp_ws_gen_frame_stride(payload_len))
+
+
+# ---- host drop-in surface ---------------------------------------------------------------
+
+def parse_frame_header(data, length=None, null=None):
+    """uvhttp_ws_parse_frame_header -> (rc, FrameHeader, header_size)."""
+    L = lib()
+    buf = (C.c_uint8 * max(1, len(data))).from_buffer_copy(bytes(data) or b"\0")
+    n = len(data) if length is None else length
+    hdr, hs = FrameHeader(), C.c_size_t(0)
+    rc = L.uvhttp_ws_parse_frame_header(None if null == "data" else buf, n,
+                                        None if null == "header" else C.byref(hdr),
+                                        None if null == "header_size" else C.byref(hs))
+    return rc, hdr, hs.value
+
+
+def apply_mask(data: bytearray, key, length=None, null=None):
+    """uvhttp_ws_apply_mask in place on a bytearray."""
+    L = lib()
+    n = len(data) if length is None else length
+    buf = (C.c_uint8 * max(1, len(data))).from_buffer(data) if len(data) else None
+    kb = (C.c_uint8 * 4).from_buffer_copy(bytes(key)) if key else None
+    L.uvhttp_ws_apply_mask(None if null == "data" else buf, n, None if null == "key" else kb)
+    return data
+
+
+class WsConnection:
+    """One server-side connection of the drop-in stream decoder (records callbacks)."""
+
+    def __init__(self, is_server=1, max_frame_size=None, max_message_size=None,
+                 callbacks=True, user_data=False):
+        L = lib()
+        self._L = L
+        cfg = None
+        if max_frame_size is not None or max_message_size is not None:
+            cfg = UvhttpConfig()
+            cfg.websocket_max_frame_size = 16 * 1024 * 1024 if max_frame_size is None \
+                else max_frame_size
+            cfg.websocket_max_message_size = 64 * 1024 * 1024 if max_message_size is None \
+                else max_message_size
+            cfg.websocket_ping_interval = 30
+            cfg.websocket_ping_timeout = 10
+        self.ptr = L.uvhttp_ws_connection_create(0, None, is_server,
+                                                 C.byref(cfg) if cfg is not None else None)
+        if not self.ptr:
+            raise MemoryError("uvhttp_ws_connection_create failed")
+        self.events = []
+        if callbacks:
+            self._cbs = (ON_MESSAGE(self._on_message), ON_CLOSE(self._on_close),
+                         ON_ERROR(self._on_error))
+            L.uvhttp_ws_set_callbacks(self.ptr, *self._cbs)
+        if user_data:
+            self.ptr.contents.user_data = 1
+
+    def _on_message(self, conn, data, n, opcode):
+        self.events.append(("message", opcode, C.string_at(data, n) if n else b""))
+        return 0
+
+    def _on_close(self, conn, code, reason):
+        self.events.append(("close", code, None))
+        return 0
+
+    def _on_error(self, conn, code, msg):
+        self.events.append(("error", code, None))
+        return 0
+
+    @property
+    def struct(self) -> WsConnectionStruct:
+        return self.ptr.contents
+
+    def process_data(self, data: bytes, length=None, null=False) -> int:
+        buf = (C.c_uint8 * max(1, len(data))).from_buffer_copy(bytes(data) or b"\0")
+        n = len(data) if length is None else length
+        return self._L.uvhttp_ws_process_data(self.ptr, None if null else buf, n)
+
+    def close(self):
+        if getattr(self, "ptr", None):
+            self._L.uvhttp_ws_connection_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# ---- batched device surface -------------------------------------------------------------
+
+class GpuEngine:
+    """Owns a uvhttp_ws_gpu_engine_t on one MI355X.  Device buffers are torch tensors
+    (plumbing only); every decode runs the gfx950 kernels through the C-ABI."""
+
+    DESC_BYTES = 32
+    MSG_BYTES = 32
+
+    def __init__(self, device: int = 0):
+        import torch
+        self.torch = torch
+        L = lib()
+        self._L = L
+        self.device = device
+        h = C.c_void_p()
+        rc = L.uvhttp_ws_gpu_engine_create(device, C.byref(h))
+        if rc != 0:
+            raise GpuError(f"uvhttp_ws_gpu_engine_create({device}) failed rc={rc} "
+                           "(needs an MI355X / gfx950 and the HIP runtime)")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._L.uvhttp_ws_gpu_engine_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != 0:
+            err = self._L.uvhttp_ws_gpu_engine_last_error(self.h)
+            raise GpuError(f"{what} rc={rc}: {err.decode() if err else ''}")
+
+    def _stream(self, stream):
+        if stream is None:
+            stream = self.torch.cuda.current_stream(self.device)
+        return C.c_void_p(stream.cuda_stream)
+
+    def reserve(self, max_frames, max_wire, max_arena=0):
+        self._check(self._L.uvhttp_ws_gpu_engine_reserve(self.h, max_frames, max_wire,
+                                                         max_arena), "reserve")
+
+    def set_timing(self, on: bool):
+        self._check(self._L.uvhttp_ws_gpu_engine_set_timing(self.h, 1 if on else 0), "timing")
+
+    def kernel_time(self):
+        ms, n = C.c_double(0), C.c_uint64(0)
+        self._check(self._L.uvhttp_ws_gpu_engine_kernel_time(self.h, C.byref(ms), C.byref(n)),
+                    "kernel_time")
+        return ms.value, n.value
+
+    def alloc_outputs(self, n_frames):
+        t = self.torch
+        dev = f"cuda:{self.device}"
+        desc = t.empty(max(1, n_frames) * self.DESC_BYTES, dtype=t.uint8, device=dev)
+        summ = t.zeros(C.sizeof(BatchSummary), dtype=t.uint8, device=dev)
+        return desc, summ
+
+    def _batch(self, wire, n_frames, stride, offsets, max_frame_size, max_message_size,
+               is_server, wire_len):
+        b = Batch()
+        b.wire = wire.data_ptr()
+        b.wire_len = wire.numel() if wire_len is None else wire_len
+        b.frame_off = offsets.data_ptr() if offsets is not None else None
+        b.frame_stride = stride or 0
+        b.n_frames = n_frames
+        b.max_frame_size = max_frame_size
+        b.max_message_size = max_message_size
+        b.is_server = is_server
+        return b
+
+    def decode_inplace(self, wire, n_frames, stride=None, offsets=None,
+                       max_frame_size=16 * 1024 * 1024, max_message_size=64 * 1024 * 1024,
+                       is_server=1, wire_len=None, desc=None, summary=None, stream=None):
+        if desc is None or summary is None:
+            desc, summary = self.alloc_outputs(n_frames)
+        b = self._batch(wire, n_frames, stride, offsets, max_frame_size, max_message_size,
+                        is_server, wire_len)
+        self._check(self._L.uvhttp_ws_gpu_decode_inplace(
+            self.h, C.byref(b), C.c_void_p(desc.data_ptr()), C.c_void_p(summary.data_ptr()),
+            self._stream(stream)), "decode_inplace")
+        return desc, summary
+
+    def decode_compact(self, wire, n_frames, arena, stride=None, offsets=None,
+                       max_frame_size=16 * 1024 * 1024, max_message_size=64 * 1024 * 1024,
+                       is_server=1, wire_len=None, desc=None, msgs=None, summary=None,
+                       stream=None):
+        t = self.torch
+        if desc is None or summary is None:
+            desc, summary = self.alloc_outputs(n_frames)
+        if msgs is None:
+            msgs = t.empty(max(1, n_frames) * self.MSG_BYTES, dtype=t.uint8,
+                           device=f"cuda:{self.device}")
+        b = self._batch(wire, n_frames, stride, offsets, max_frame_size, max_message_size,
+                        is_server, wire_len)
+        self._check(self._L.uvhttp_ws_gpu_decode_compact(
+            self.h, C.byref(b), C.c_void_p(arena.data_ptr()), arena.numel(),
+            C.c_void_p(desc.data_ptr()), C.c_void_p(msgs.data_ptr()),
+            C.c_void_p(summary.data_ptr()), self._stream(stream)), "decode_compact")
+        return desc, msgs, summary
+
+    def apply_mask(self, data, key, length=None, offset=0, stream=None):
+        kb = (C.c_uint8 * 4).from_buffer_copy(bytes(key))
+        n = data.numel() - offset if length is None else length
+        self._check(self._L.uvhttp_ws_gpu_apply_mask(
+            self.h, C.c_void_p(data.data_ptr() + offset), n, kb, self._stream(stream)),
+            "apply_mask")
+
+    def gen_frames(self, wire, n_frames, payload_len, seed, opcode0=2, fragmented=False,
+                   force_keys=False, stream=None):
+        self._check(self._L.uvhttp_ws_gpu_gen_frames(
+            self.h, C.c_void_p(wire.data_ptr()), n_frames, payload_len, seed, opcode0,
+            1 if fragmented else 0, 1 if force_keys else 0, self._stream(stream)), "gen_frames")
+
+    # -- read-back helpers (host copies of device outputs) --
+    @staticmethod
+    def read_summary(summary) -> dict:
+        raw = bytes(summary.cpu().numpy().tobytes())
+        return BatchSummary.from_buffer_copy(raw).as_dict()
+
+    @staticmethod
+    def read_desc(desc, n_frames):
+        import numpy as np
+        dt = np.dtype([("payload_off", "<u8"), ("payload_len", "<u8"), ("masking_key", "<u4"),
+                       ("message", "<u4"), ("opcode", "u1"), ("flags", "u1"),
+                       ("header_size", "u1"), ("status", "i1"), ("wire_len", "<u4")])
+        assert dt.itemsize == 32
+        return desc[: n_frames * 32].cpu().numpy().view(dt)
+
+    @staticmethod
+    def read_msgs(msgs, n_msgs):
+        import numpy as np
+        dt = np.dtype([("arena_off", "<u8"), ("len", "<u8"), ("first_frame", "<u4"),
+                       ("last_frame", "<u4"), ("opcode", "<i4"), ("reserved", "<u4")])
+        return msgs[: n_msgs * 32].cpu().numpy().view(dt)

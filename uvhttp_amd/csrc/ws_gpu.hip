@@ -1,0 +1,1086 @@
+// ws_gpu.hip — MI355X (gfx950) batched WebSocket frame decode + payload unmask.
+//
+// Replaces, for frames already resident in HBM, the per-frame work of
+// src/uvhttp_websocket.c (adam-ikari/uvhttp v2.7.0):
+//   uvhttp_ws_parse_frame_header  :133-185   -> k_parse (one lane per frame)
+//   validation in process_data    :851-932   -> k_parse (local) + k_resolve (state machine)
+//   fragment state machine        :950-1015  -> k_resolve (segmented scan, no serial walk)
+//   uvhttp_ws_fragment_append     :781-822   -> prefix offsets + k_gather_compact
+//   uvhttp_ws_apply_mask          :188-197   -> k_unmask_inplace / k_gather_compact
+//
+// Pipeline per decode call (one stream, no host sync):
+//   k_parse    frames -> desc[] (header, key, local status), per-block scan aggregates,
+//              tile -> first-frame map for the in-place tiles
+//   k_scan     one workgroup: exclusive scan of the block aggregates
+//   k_resolve  frames -> state machine status, message ids, arena offsets, first_bad
+//   k_unmask_inplace / k_gather_compact   the HBM-bound payload pass (the roofline kernel)
+//   k_finalize statuses after the first failure -> SKIPPED, batch summary
+//
+// The payload pass is pure streaming integer work: 16-byte loads/stores per lane, the
+// 4-byte key rotated once per (vector, frame) into a 32-bit word, no LDS on the fast path,
+// no MFMA (nothing here is matrix-shaped).
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "uvhttp_ws_amd.h"
+
+namespace {
+
+constexpr int kBlock = 256;                 // threads per workgroup (4 waves of 64)
+constexpr int kVecPerThread = 4;            // 16-byte vectors per lane per tile
+constexpr uint64_t kTile = (uint64_t)kBlock * kVecPerThread * 16;  // 16 KiB tile
+constexpr int kStage = 256;                 // frames staged in LDS per round
+constexpr uint32_t kMaxFrames = 1u << 26;   // k_scan handles <= 2^18 block aggregates
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------------------------
+// scan element: everything the fragment state machine needs about frames [0, i)
+// ------------------------------------------------------------------------------------
+struct ScanElem {
+    int32_t last_data;   // max: index of the latest data frame (-1 none)
+    int32_t last_start;  // max: index of the latest non-CONT data frame (-1 none)
+    uint64_t data_pay;   // sum: payload bytes of data frames (arena offset)
+    uint64_t all_pay;    // sum: payload bytes of all frames
+    uint64_t seg_pay;    // segmented sum: data payload since the latest start
+    uint32_t seg_flag;   // segment contains a start
+    uint32_t n_fin;      // sum: data frames with FIN (completed messages)
+    uint32_t n_close;    // sum: CLOSE frames
+    uint32_t pad;
+};
+
+__device__ __host__ inline ScanElem scan_identity() {
+    ScanElem e;
+    e.last_data = -1;
+    e.last_start = -1;
+    e.data_pay = 0;
+    e.all_pay = 0;
+    e.seg_pay = 0;
+    e.seg_flag = 0;
+    e.n_fin = 0;
+    e.n_close = 0;
+    e.pad = 0;
+    return e;
+}
+
+__device__ __host__ inline ScanElem scan_combine(const ScanElem& a, const ScanElem& b) {
+    ScanElem r;
+    r.last_data = a.last_data > b.last_data ? a.last_data : b.last_data;
+    r.last_start = a.last_start > b.last_start ? a.last_start : b.last_start;
+    r.data_pay = a.data_pay + b.data_pay;
+    r.all_pay = a.all_pay + b.all_pay;
+    r.seg_pay = b.seg_flag ? b.seg_pay : a.seg_pay + b.seg_pay;
+    r.seg_flag = a.seg_flag | b.seg_flag;
+    r.n_fin = a.n_fin + b.n_fin;
+    r.n_close = a.n_close + b.n_close;
+    r.pad = 0;
+    return r;
+}
+
+__device__ inline bool is_data_op(uint32_t op) { return op <= 2u; }
+
+// element of frame i, rebuilt from its descriptor (local status must be OK for the
+// state machine to consider it; invalid frames never precede a delivered frame)
+__device__ inline ScanElem scan_elem_of(const uvhttp_ws_frame_desc_t& d, int32_t i) {
+    ScanElem e = scan_identity();
+    const uint32_t op = d.opcode;
+    e.all_pay = d.payload_len;
+    if (is_data_op(op)) {
+        e.last_data = i;
+        e.data_pay = d.payload_len;
+        e.seg_pay = d.payload_len;
+        if (op != 0) {
+            e.last_start = i;
+            e.seg_flag = 1;
+        }
+        e.n_fin = (d.flags & UVHTTP_WS_FLAG_FIN) ? 1u : 0u;
+    } else if (op == 8) {
+        e.n_close = 1;
+    }
+    return e;
+}
+
+__device__ inline ScanElem shfl_up_elem(const ScanElem& e, int delta) {
+    ScanElem r;
+    r.last_data = __shfl_up(e.last_data, delta, 64);
+    r.last_start = __shfl_up(e.last_start, delta, 64);
+    r.data_pay = __shfl_up(e.data_pay, delta, 64);
+    r.all_pay = __shfl_up(e.all_pay, delta, 64);
+    r.seg_pay = __shfl_up(e.seg_pay, delta, 64);
+    r.seg_flag = __shfl_up(e.seg_flag, delta, 64);
+    r.n_fin = __shfl_up(e.n_fin, delta, 64);
+    r.n_close = __shfl_up(e.n_close, delta, 64);
+    r.pad = 0;
+    return r;
+}
+
+// Block-wide exclusive scan (256 threads = 4 waves): wave-level Hillis-Steele over the 64
+// lanes with __shfl_up, then the 4 wave totals through LDS.  Returns the exclusive prefix
+// for this thread; *total receives the block aggregate.
+__device__ ScanElem block_exclusive_scan(ScanElem v, ScanElem* total) {
+    __shared__ ScanElem wave_tot[kBlock / 64];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    ScanElem inc = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        ScanElem o = shfl_up_elem(inc, d);
+        if (lane >= d) inc = scan_combine(o, inc);
+    }
+    if (lane == 63) wave_tot[wave] = inc;
+    __syncthreads();
+    ScanElem wave_pre = scan_identity();
+    ScanElem all = scan_identity();
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) {
+        if (w < wave) wave_pre = scan_combine(wave_pre, wave_tot[w]);
+        all = scan_combine(all, wave_tot[w]);
+    }
+    ScanElem exc = shfl_up_elem(inc, 1);
+    if (lane == 0) exc = scan_identity();
+    __syncthreads();
+    *total = all;
+    return scan_combine(wave_pre, exc);
+}
+
+// ------------------------------------------------------------------------------------
+// workspace layout (device), carved from one allocation
+// ------------------------------------------------------------------------------------
+struct Workspace {
+    ScanElem* block_agg;   // [n_blocks + 1]: aggregates, then exclusive prefixes + total
+    uint32_t* tile_first;  // [n_tiles]: first frame whose slot contains the tile start
+    uint32_t* first_bad;   // [1]
+    uint32_t* arena_first; // [n_arena_tiles]
+};
+
+struct BatchArgs {
+    uint8_t* wire;
+    uint64_t wire_len;
+    const uint64_t* frame_off;
+    uint64_t frame_stride;
+    uint32_t n;
+    int32_t max_frame_size;
+    int32_t max_message_size;
+    int32_t is_server;
+    uint64_t n_tiles;        // in-place tiles over the wire
+    uint8_t* arena;          // compact mode (nullptr: in-place)
+    uint64_t arena_cap;
+    uint64_t n_arena_tiles;
+};
+
+__device__ inline uint64_t frame_start(const BatchArgs& a, uint32_t i) {
+    return a.frame_off ? a.frame_off[i] : (uint64_t)i * a.frame_stride;
+}
+
+__device__ inline uint32_t rotr32(uint32_t x, uint32_t s) {
+    return s ? (x >> s) | (x << (32u - s)) : x;
+}
+
+// ------------------------------------------------------------------------------------
+// k_parse: one lane per frame.  Header parse + every check process_data makes before the
+// state machine (src/uvhttp_websocket.c:832-932), in the reference's order, on the bytes
+// the batch contract feeds (include/uvhttp_ws_amd.h "Batch semantics").
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_parse(BatchArgs a, uvhttp_ws_frame_desc_t* desc,
+                                                  Workspace ws) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *ws.first_bad = a.n;
+    ScanElem elem = scan_identity();
+    if (i < a.n) {
+        const uint64_t o = frame_start(a, i);
+        uint64_t end = (i + 1 < a.n) ? frame_start(a, i + 1) : a.wire_len;
+        if (end > a.wire_len) end = a.wire_len;
+        const uint64_t slot = end > o ? end - o : 0;
+        const bool last = (i + 1 == a.n);
+        const uint8_t* p = a.wire + o;
+
+        uvhttp_ws_frame_desc_t d;
+        d.payload_off = 0;
+        d.payload_len = 0;
+        d.masking_key = 0;
+        d.message = 0;
+        d.opcode = 0;
+        d.flags = 0;
+        d.header_size = 0;
+        d.status = UVHTTP_WS_FRAME_OK;
+        d.wire_len = 0;
+
+        bool parsable = false, msb = false;
+        uint64_t plen = 0, wlen = 0;
+        uint32_t hsz = 2, b0 = 0, b1 = 0;
+        if (slot >= 2) {
+            b0 = p[0];
+            b1 = p[1];
+            const uint32_t code = b1 & 0x7F;
+            const uint32_t need = code == 126 ? 4 : code == 127 ? 10 : 2;
+            if (slot >= need) {
+                parsable = true;
+                plen = code;
+                if (need > 2) {
+                    plen = 0;
+                    for (uint32_t k = 2; k < need; ++k) plen = (plen << 8) | p[k];
+                }
+                msb = (need == 10) && (plen >> 63);
+                hsz = need;
+                if (!msb) {
+                    const uint32_t m = (b1 >> 7) ? 4u : 0u;
+                    wlen = hsz + m + plen;
+                    if (m && slot >= hsz + 4) {
+                        d.masking_key = (uint32_t)p[hsz] | ((uint32_t)p[hsz + 1] << 8) |
+                                        ((uint32_t)p[hsz + 2] << 16) |
+                                        ((uint32_t)p[hsz + 3] << 24);
+                    }
+                    d.payload_off = o + hsz + m;
+                }
+            }
+        }
+        d.opcode = (uint8_t)(b0 & 0x0F);
+        d.flags = (uint8_t)(((b0 >> 7) & 1) | (((b1 >> 7) & 1) << 1) | (((b0 >> 6) & 1) << 2) |
+                            (((b0 >> 5) & 1) << 3) | (((b0 >> 4) & 1) << 4));
+        d.header_size = (uint8_t)hsz;
+        d.payload_len = plen;
+        d.wire_len = wlen > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)wlen;
+
+        int st = UVHTTP_WS_FRAME_OK;
+        uint64_t fed;
+        if (!last && (!parsable || (!msb && wlen != slot))) {
+            st = UVHTTP_WS_FRAME_ERR_LAYOUT;
+            fed = slot;
+        } else {
+            fed = (last && parsable && !msb && wlen < slot) ? wlen : slot;
+        }
+        if (st == UVHTTP_WS_FRAME_OK) {
+            // recv buffer cap (:851-857): an empty buffer grows to max(max_frame, 64 KiB)
+            const uint64_t mf = (uint64_t)(int64_t)a.max_frame_size;
+            const uint64_t cap = mf > 65536u ? mf : 65536u;
+            if (fed > cap) st = UVHTTP_WS_FRAME_ERR_BUFFER;
+            else if (!parsable) st = UVHTTP_WS_FRAME_INCOMPLETE;
+            else if (msb) st = UVHTTP_WS_FRAME_ERR_PARSE;
+            else if (d.flags & (UVHTTP_WS_FLAG_RSV1 | UVHTTP_WS_FLAG_RSV2 | UVHTTP_WS_FLAG_RSV3))
+                st = UVHTTP_WS_FRAME_ERR_RSV;
+            else if (d.opcode >= 8 && (plen > 125 || !(d.flags & UVHTTP_WS_FLAG_FIN)))
+                st = UVHTTP_WS_FRAME_ERR_CONTROL;
+            else if (a.is_server && !(d.flags & UVHTTP_WS_FLAG_MASK))
+                st = UVHTTP_WS_FRAME_ERR_UNMASKED;
+            else if (plen > mf) st = UVHTTP_WS_FRAME_ERR_TOO_BIG;
+            else if (fed < wlen) st = UVHTTP_WS_FRAME_INCOMPLETE;
+        }
+        d.status = (int8_t)st;
+        desc[i] = d;
+        if (st == UVHTTP_WS_FRAME_OK) elem = scan_elem_of(d, (int32_t)i);
+
+        // tiles whose start byte lies in this frame's slot (frame 0 also owns the bytes
+        // before its start): the in-place payload pass starts its frame walk there
+        const uint64_t lo = (i == 0) ? 0 : o;
+        const uint64_t hi = last ? a.wire_len : end;
+        if (hi > lo) {
+            for (uint64_t t = (lo + kTile - 1) / kTile; t * kTile < hi && t < a.n_tiles; ++t)
+                ws.tile_first[t] = i;
+        }
+    }
+    ScanElem total;
+    (void)block_exclusive_scan(elem, &total);
+    if (threadIdx.x == 0) ws.block_agg[blockIdx.x] = total;
+}
+
+// k_scan: one workgroup turns the block aggregates into exclusive block prefixes and
+// stores the grand total at block_agg[n_blocks].
+__global__ __launch_bounds__(kBlock) void k_scan(Workspace ws, uint32_t n_blocks) {
+    const uint32_t per = (n_blocks + kBlock - 1) / kBlock;
+    const uint32_t beg = threadIdx.x * per;
+    const uint32_t fin = beg + per < n_blocks ? beg + per : n_blocks;
+    ScanElem run = scan_identity();
+    for (uint32_t b = beg; b < fin; ++b) run = scan_combine(run, ws.block_agg[b]);
+    ScanElem total;
+    ScanElem pre = block_exclusive_scan(run, &total);
+    for (uint32_t b = beg; b < fin; ++b) {
+        ScanElem v = ws.block_agg[b];
+        ws.block_agg[b] = pre;
+        pre = scan_combine(pre, v);
+    }
+    if (threadIdx.x == 0) ws.block_agg[n_blocks] = total;
+}
+
+// k_resolve: one lane per frame.  With E = scan over frames [0, i), the state before data
+// frame i follows from the latest data frame p alone (all frames before a delivered frame
+// are valid): PENDING iff p exists, p has FIN=0, and p is not a zero-length start (a
+// zero-length first fragment allocates nothing, so fragmented_message stays NULL,
+// src/uvhttp_websocket.c:794-816 + :964).
+__global__ __launch_bounds__(kBlock) void k_resolve(BatchArgs a, uvhttp_ws_frame_desc_t* desc,
+                                                    uvhttp_ws_message_desc_t* msgs,
+                                                    Workspace ws) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    ScanElem elem = scan_identity();
+    uvhttp_ws_frame_desc_t d;
+    if (i < a.n) {
+        d = desc[i];
+        if (d.status == UVHTTP_WS_FRAME_OK) elem = scan_elem_of(d, (int32_t)i);
+    }
+    ScanElem total;
+    ScanElem ex = block_exclusive_scan(elem, &total);
+    if (i >= a.n) return;
+    ex = scan_combine(ws.block_agg[blockIdx.x], ex);
+
+    int st = d.status;
+    if (st == UVHTTP_WS_FRAME_OK && is_data_op(d.opcode)) {
+        bool pending = false;
+        if (ex.last_data >= 0) {
+            const uvhttp_ws_frame_desc_t pd = desc[ex.last_data];
+            const bool p_start = pd.opcode != 0;
+            pending = !(pd.flags & UVHTTP_WS_FLAG_FIN) && !(p_start && pd.payload_len == 0);
+        }
+        const uint64_t lim = (uint64_t)(int64_t)a.max_message_size;
+        const bool is_cont = d.opcode == 0;
+        const bool fin = d.flags & UVHTTP_WS_FLAG_FIN;
+        if (!pending) {
+            if (is_cont) st = UVHTTP_WS_FRAME_ERR_FRAGMENT;
+            else if (!fin && lim != 0 && d.payload_len > lim) st = UVHTTP_WS_FRAME_ERR_MESSAGE;
+        } else {
+            const uint64_t acc = ex.seg_pay;  // bytes of the open message so far
+            if (!is_cont) st = UVHTTP_WS_FRAME_ERR_FRAGMENT;
+            else if (lim != 0 && (acc > lim || d.payload_len > lim - acc))
+                st = UVHTTP_WS_FRAME_ERR_MESSAGE;
+        }
+        if (st == UVHTTP_WS_FRAME_OK) {
+            d.message = ex.n_fin;
+            if (a.arena) d.payload_off = ex.data_pay;
+            if (fin) {
+                d.flags |= UVHTTP_WS_FLAG_MSG_END;
+                if (msgs) {
+                    uvhttp_ws_message_desc_t m;
+                    const uint64_t before = pending ? ex.seg_pay : 0;
+                    m.arena_off = a.arena ? ex.data_pay - before : 0;
+                    m.len = before + d.payload_len;
+                    m.first_frame = pending ? (uint32_t)ex.last_start : i;
+                    m.last_frame = i;
+                    m.opcode = pending ? desc[ex.last_start].opcode : d.opcode;
+                    m.reserved = 0;
+                    msgs[ex.n_fin] = m;
+                }
+            }
+            // arena tiles whose first byte lies in this data frame's payload
+            if (a.arena && d.payload_len) {
+                const uint64_t lo = ex.data_pay, hi = ex.data_pay + d.payload_len;
+                for (uint64_t t = (lo + kTile - 1) / kTile; t * kTile < hi && t < a.n_arena_tiles;
+                     ++t)
+                    ws.arena_first[t] = i;
+            }
+        }
+        desc[i].status = (int8_t)st;
+        desc[i].message = d.message;
+        desc[i].payload_off = d.payload_off;
+        desc[i].flags = d.flags;
+    }
+    if (st != UVHTTP_WS_FRAME_OK) atomicMin(ws.first_bad, i);
+}
+
+// ------------------------------------------------------------------------------------
+// payload helpers
+// ------------------------------------------------------------------------------------
+
+// bytes [lo, hi) of dword m (0..3) of a 16-byte vector as a 32-bit byte-lane mask
+__device__ inline uint32_t lane_bytes(int lo, int hi, int m) {
+    int l = lo - 4 * m, h = hi - 4 * m;
+    l = l < 0 ? 0 : (l > 4 ? 4 : l);
+    h = h < 0 ? 0 : (h > 4 ? 4 : h);
+    if (h <= l) return 0u;
+    const uint32_t up = h == 4 ? 0xFFFFFFFFu : ((1u << (8 * h)) - 1u);
+    return up & ~((1u << (8 * l)) - 1u);
+}
+
+// mask vector contribution of one payload range [ps, pe) with key `key` (payload byte j
+// uses key byte j & 3) to the 16-byte vector at address `va`.
+__device__ inline void add_mask(u32x4& m, uint64_t va, uint64_t ps, uint64_t pe, uint32_t key) {
+    if (pe <= va || ps >= va + 16) return;
+    const uint32_t rk = rotr32(key, 8u * (uint32_t)((va - ps) & 3u));
+    if (ps <= va && va + 16 <= pe) {
+        m = u32x4{rk, rk, rk, rk};
+        return;
+    }
+    const int lo = ps > va ? (int)(ps - va) : 0;
+    const int hi = pe < va + 16 ? (int)(pe - va) : 16;
+    m.x |= rk & lane_bytes(lo, hi, 0);
+    m.y |= rk & lane_bytes(lo, hi, 1);
+    m.z |= rk & lane_bytes(lo, hi, 2);
+    m.w |= rk & lane_bytes(lo, hi, 3);
+}
+
+__device__ inline bool any_bits(const u32x4& m) { return (m.x | m.y | m.z | m.w) != 0u; }
+
+// ------------------------------------------------------------------------------------
+// k_unmask_inplace: the roofline kernel of the in-place decode.
+// One workgroup per 16 KiB tile of the wire buffer; lane t handles the 16-byte vectors
+// tile + (v*256 + t)*16, v < 4 (coalesced: a wave covers 1 KiB per instruction).  The
+// payload loads are issued first — they depend only on the tile index — and the frame
+// lookup (tile_first -> descriptors -> LDS) runs while they are in flight.  Every byte of
+// the wire belongs to exactly one tile, so whole-vector stores never race: bytes outside
+// any delivered payload are XORed with 0 and vectors with no payload byte are not stored.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_unmask_inplace(
+    BatchArgs a, const uvhttp_ws_frame_desc_t* __restrict__ desc, Workspace ws) {
+    __shared__ uint64_t s_ps[kStage];
+    __shared__ uint64_t s_pe[kStage];
+    __shared__ uint32_t s_key[kStage];
+
+    const uint64_t tile = blockIdx.x;
+    const uint64_t t0 = tile * kTile;
+    const uint64_t vend = a.wire_len;
+    // last 16-byte vector that lies wholly inside the wire (loads are clamped to it so they
+    // can be issued unconditionally; the one straddling vector is finished bytewise)
+    const uint64_t full_end = vend & ~(uint64_t)15;
+    const uint64_t clamp_va = full_end ? full_end - 16 : 0;
+
+    u32x4 data[kVecPerThread];
+    uint64_t va[kVecPerThread];
+#pragma unroll
+    for (int v = 0; v < kVecPerThread; ++v) {
+        va[v] = t0 + ((uint64_t)v * kBlock + threadIdx.x) * 16u;
+        const uint64_t la = va[v] < full_end ? va[v] : clamp_va;
+        data[v] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.wire + la));
+    }
+
+    const uint32_t nb = *ws.first_bad;  // frames >= nb are not delivered
+    if (nb == 0 || a.n == 0) return;
+    const uint32_t last = (nb < a.n ? nb : a.n) - 1;
+    uint32_t f0 = ws.tile_first[tile];
+    uint32_t f1 = (tile + 1 < a.n_tiles) ? ws.tile_first[tile + 1] : last;
+    if (f0 > last) return;  // the tile starts past the delivered frames
+    if (f1 > last) f1 = last;
+
+    u32x4 m[kVecPerThread];
+#pragma unroll
+    for (int v = 0; v < kVecPerThread; ++v) m[v] = u32x4{0, 0, 0, 0};
+
+    if (f1 - f0 < 2) {
+        // fast path (frames of ~8 KiB and up): at most two frames touch the tile; their
+        // descriptors are uniform scalar loads
+        for (uint32_t f = f0; f <= f1; ++f) {
+            const uint64_t ps = desc[f].payload_off;
+            const uint64_t pe = ps + desc[f].payload_len;
+            const uint32_t key = desc[f].masking_key;
+#pragma unroll
+            for (int v = 0; v < kVecPerThread; ++v) add_mask(m[v], va[v], ps, pe, key);
+        }
+    } else {
+        // general path: stage <= 256 frame ranges in LDS, binary-search per vector
+        for (uint32_t base = f0; base <= f1; base += kStage) {
+            const uint32_t cnt = (f1 - base + 1) < (uint32_t)kStage ? (f1 - base + 1) : kStage;
+            __syncthreads();
+            if (threadIdx.x < cnt) {
+                const uvhttp_ws_frame_desc_t d = desc[base + threadIdx.x];
+                s_ps[threadIdx.x] = d.payload_off;
+                s_pe[threadIdx.x] = d.payload_off + d.payload_len;
+                s_key[threadIdx.x] = d.masking_key;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int v = 0; v < kVecPerThread; ++v) {
+                // last staged frame whose payload starts before the vector's end
+                int lo = 0, hi = (int)cnt - 1, j = -1;
+                while (lo <= hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (s_ps[mid] < va[v] + 16) {
+                        j = mid;
+                        lo = mid + 1;
+                    } else {
+                        hi = mid - 1;
+                    }
+                }
+                for (; j >= 0; --j) {
+                    if (s_pe[j] <= va[v]) {
+                        if (s_pe[j] != s_ps[j]) break;  // empty payloads don't end the walk
+                        continue;
+                    }
+                    add_mask(m[v], va[v], s_ps[j], s_pe[j], s_key[j]);
+                }
+            }
+        }
+    }
+
+#pragma unroll
+    for (int v = 0; v < kVecPerThread; ++v) {
+        if (any_bits(m[v]) && va[v] + 16 <= vend)
+            __builtin_nontemporal_store(data[v] ^ m[v], reinterpret_cast<u32x4*>(a.wire + va[v]));
+    }
+    // the single vector that straddles the end of the wire: byte stores
+    if (full_end != vend && full_end >= t0 && full_end < t0 + kTile) {
+#pragma unroll
+        for (int v = 0; v < kVecPerThread; ++v) {
+            if (va[v] == full_end && any_bits(m[v])) {
+                const uint32_t mw[4] = {m[v].x, m[v].y, m[v].z, m[v].w};
+                for (uint64_t bq = 0; full_end + bq < vend; ++bq) {
+                    const uint8_t mb = (uint8_t)(mw[bq >> 2] >> (8 * (bq & 3)));
+                    if (mb) a.wire[full_end + bq] ^= mb;
+                }
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// k_gather_compact: the roofline kernel of the compact decode.  One workgroup per 16 KiB
+// tile of the message arena; lane t produces the aligned arena vectors of its tile.  Each
+// vector's bytes come from the delivered data frame(s) covering it: out[o] =
+// wire[ps_f + (o - aoff_f)] ^ key_f[(o - aoff_f) & 3].  The source window is unaligned
+// (payload starts at header+key offsets), read as one 16-byte load.
+// ------------------------------------------------------------------------------------
+__device__ inline u32x4 load16_any(const uint8_t* base, int64_t addr, uint64_t limit) {
+    if (addr >= 0 && (uint64_t)addr + 16 <= limit) {
+        u32x4 r;
+        __builtin_memcpy(&r, base + addr, 16);
+        return r;
+    }
+    uint32_t w[4] = {0, 0, 0, 0};
+    for (int b = 0; b < 16; ++b) {
+        const int64_t x = addr + b;
+        if (x >= 0 && (uint64_t)x < limit) w[b >> 2] |= (uint32_t)base[x] << (8 * (b & 3));
+    }
+    return u32x4{w[0], w[1], w[2], w[3]};
+}
+
+// block-wide inclusive max-scan of one u64 per thread (256 threads)
+__device__ uint64_t block_inclusive_max(uint64_t v) {
+    __shared__ uint64_t wave_max[kBlock / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t o = __shfl_up(v, d, 64);
+        if (lane >= d && o > v) v = o;
+    }
+    if (lane == 63) wave_max[wave] = v;
+    __syncthreads();
+    for (int w = 0; w < wave; ++w)
+        if (wave_max[w] > v) v = wave_max[w];
+    __syncthreads();
+    return v;
+}
+
+__global__ __launch_bounds__(kBlock) void k_gather_compact(BatchArgs a,
+                                                           const uvhttp_ws_frame_desc_t* desc,
+                                                           Workspace ws, uint64_t arena_bytes_cap) {
+    __shared__ uint64_t s_as[kStage];  // arena start of the data payload
+    __shared__ uint64_t s_ae[kStage];  // arena end (== start for control frames)
+    __shared__ uint64_t s_ps[kStage];  // wire offset of the payload
+    __shared__ uint32_t s_key[kStage];
+
+    const uint64_t tile = blockIdx.x;
+    const uint64_t t0 = tile * kTile;
+    const uint32_t nb = *ws.first_bad;
+    if (nb == 0 || a.n == 0) return;
+    const uint32_t last = (nb < a.n ? nb : a.n) - 1;
+    const uint32_t f0 = ws.arena_first[tile];
+    if (f0 > last) return;
+    uint32_t f1 = (tile + 1 < a.n_arena_tiles) ? ws.arena_first[tile + 1] : last;
+    if (f1 > last || f1 < f0) f1 = last;
+
+    uint64_t oa[kVecPerThread];
+    u32x4 out[kVecPerThread];
+    bool touched[kVecPerThread];
+#pragma unroll
+    for (int v = 0; v < kVecPerThread; ++v) {
+        oa[v] = t0 + ((uint64_t)v * kBlock + threadIdx.x) * 16u;
+        out[v] = u32x4{0, 0, 0, 0};
+        touched[v] = false;
+    }
+    uint64_t arena_end = 0;  // end of the delivered data payload staged so far
+
+    for (uint32_t base = f0; base <= f1; base += kStage) {
+        const uint32_t cnt = (f1 - base + 1) < (uint32_t)kStage ? (f1 - base + 1) : kStage;
+        uint64_t as = 0, ae = 0, ps = 0;
+        uint32_t key = 0;
+        bool data = false;
+        if (threadIdx.x < cnt) {
+            const uint32_t f = base + threadIdx.x;
+            const uvhttp_ws_frame_desc_t d = desc[f];
+            data = d.opcode <= 2;
+            if (data) {
+                as = d.payload_off;
+                ae = as + d.payload_len;
+                ps = frame_start(a, f) + d.header_size + ((d.flags & UVHTTP_WS_FLAG_MASK) ? 4u : 0u);
+            }
+            key = d.masking_key;
+        }
+        // control frames take the running arena end so s_as stays sorted
+        const uint64_t run = block_inclusive_max(data ? ae : 0);
+        if (threadIdx.x < cnt) {
+            s_as[threadIdx.x] = data ? as : run;
+            s_ae[threadIdx.x] = data ? ae : run;
+            s_ps[threadIdx.x] = ps;
+            s_key[threadIdx.x] = key;
+        }
+        __syncthreads();
+        if (cnt && s_ae[cnt - 1] > arena_end) arena_end = s_ae[cnt - 1];
+#pragma unroll
+        for (int v = 0; v < kVecPerThread; ++v) {
+            // last staged frame starting before the vector's end
+            int lo = 0, hi = (int)cnt - 1, j = -1;
+            while (lo <= hi) {
+                const int mid = (lo + hi) >> 1;
+                if (s_as[mid] < oa[v] + 16) {
+                    j = mid;
+                    lo = mid + 1;
+                } else {
+                    hi = mid - 1;
+                }
+            }
+            for (; j >= 0; --j) {
+                const uint64_t fa = s_as[j], fe = s_ae[j];
+                if (fe == fa) continue;  // control frame or empty payload
+                if (fe <= oa[v]) break;
+                const int lo_b = fa > oa[v] ? (int)(fa - oa[v]) : 0;
+                const int hi_b = fe < oa[v] + 16 ? (int)(fe - oa[v]) : 16;
+                // window byte b <- wire[ps + (oa + b - fa)]
+                const int64_t wstart = (int64_t)s_ps[j] + (int64_t)(oa[v] - fa);
+                const u32x4 w = load16_any(a.wire, wstart, a.wire_len);
+                const uint32_t rk = rotr32(s_key[j], 8u * (uint32_t)((oa[v] - fa) & 3u));
+                const u32x4 sel{lane_bytes(lo_b, hi_b, 0), lane_bytes(lo_b, hi_b, 1),
+                                lane_bytes(lo_b, hi_b, 2), lane_bytes(lo_b, hi_b, 3)};
+                out[v] |= (w ^ u32x4{rk, rk, rk, rk}) & sel;
+                touched[v] = true;
+            }
+        }
+        __syncthreads();
+    }
+
+    const uint64_t lim = arena_end < arena_bytes_cap ? arena_end : arena_bytes_cap;
+#pragma unroll
+    for (int v = 0; v < kVecPerThread; ++v) {
+        if (!touched[v] || oa[v] >= lim) continue;
+        if (oa[v] + 16 <= lim) {
+            __builtin_nontemporal_store(out[v], reinterpret_cast<u32x4*>(a.arena + oa[v]));
+        } else {
+            const uint32_t ow[4] = {out[v].x, out[v].y, out[v].z, out[v].w};
+            for (uint64_t b = 0; b < 16 && oa[v] + b < lim; ++b)
+                a.arena[oa[v] + b] = (uint8_t)(ow[b >> 2] >> (8 * (b & 3)));
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// k_finalize: statuses after the first failing frame become SKIPPED; control payloads of
+// a compact decode are unmasked in place (<= 125 B each); block 0 writes the summary.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_finalize(BatchArgs a, uvhttp_ws_frame_desc_t* desc,
+                                                     Workspace ws,
+                                                     uvhttp_ws_batch_summary_t* summary,
+                                                     uint32_t n_blocks) {
+    const uint32_t nb = *ws.first_bad;
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i < a.n && i > nb) desc[i].status = UVHTTP_WS_FRAME_SKIPPED;
+    if (a.arena && i < a.n && i < nb) {
+        const uvhttp_ws_frame_desc_t d = desc[i];
+        if (d.opcode > 2 && d.payload_len) {
+            const uint32_t key = d.masking_key;
+            for (uint64_t b = 0; b < d.payload_len; ++b)
+                a.wire[d.payload_off + b] ^= (uint8_t)(key >> (8 * (b & 3)));
+        }
+    }
+    if (blockIdx.x != 0) return;
+
+    // E(nb): exclusive scan value at the first bad frame (or the total)
+    ScanElem e;
+    if (nb >= a.n) {
+        e = ws.block_agg[n_blocks];
+    } else {
+        const uint32_t b = nb / kBlock;
+        const uint32_t f = b * kBlock + threadIdx.x;
+        ScanElem el = scan_identity();
+        if (f < nb) el = scan_elem_of(desc[f], (int32_t)f);
+        ScanElem part;
+        (void)block_exclusive_scan(el, &part);
+        e = scan_combine(ws.block_agg[b], part);
+    }
+    if (threadIdx.x != 0) return;
+    uvhttp_ws_batch_summary_t s;
+    s.n_frames = a.n;
+    s.n_delivered = nb < a.n ? nb : a.n;
+    s.first_status = nb < a.n ? desc[nb].status : 0;
+    s.status = s.first_status < 0 ? -1 : 0;
+    const uint64_t start0 = a.n ? frame_start(a, 0) : 0;
+    if (a.n == 0) {
+        s.consumed_bytes = 0;
+    } else if (nb < a.n) {
+        s.consumed_bytes = frame_start(a, nb) - start0;
+    } else {
+        s.consumed_bytes = frame_start(a, a.n - 1) + desc[a.n - 1].wire_len - start0;
+    }
+    s.payload_bytes = e.all_pay;
+    s.n_messages = e.n_fin;
+    s.state_closed = e.n_close ? 1u : 0u;
+    s.arena_bytes = a.arena ? e.data_pay : 0;
+    uint64_t pend = 0;
+    if (e.last_data >= 0) {
+        const uvhttp_ws_frame_desc_t pd = desc[e.last_data];
+        const bool p_start = pd.opcode != 0;
+        if (!(pd.flags & UVHTTP_WS_FLAG_FIN) && !(p_start && pd.payload_len == 0)) pend = e.seg_pay;
+    }
+    s.pending_bytes = pend;
+    *summary = s;
+}
+
+// plain unmask of one buffer with one key (uvhttp_ws_apply_mask over device memory)
+__global__ __launch_bounds__(kBlock) void k_apply_mask(uint8_t* data, uint64_t len, uint32_t key,
+                                                       uint64_t head) {
+    // bytes [0, head) are the unaligned head; vectors start at data + head
+    const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    if (tid < head && tid < len) data[tid] ^= (uint8_t)(key >> (8 * (tid & 3)));
+    const uint64_t body = len > head ? len - head : 0;
+    const uint64_t nvec = body / 16;
+    const uint32_t rk = rotr32(key, 8u * (uint32_t)(head & 3u));
+    const u32x4 km{rk, rk, rk, rk};
+    u32x4* vp = reinterpret_cast<u32x4*>(data + head);
+    for (uint64_t v = tid; v < nvec; v += stride) vp[v] ^= km;
+    const uint64_t tail0 = head + nvec * 16;
+    if (tid < len - tail0 && tail0 < len) {
+        const uint64_t b = tail0 + tid;
+        data[b] ^= (uint8_t)(key >> (8 * (b & 3)));
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// synthetic frames (definition shared with oracle_gen_frames)
+// ------------------------------------------------------------------------------------
+__device__ __host__ inline uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+__device__ __host__ inline uint64_t gen_header_size(uint64_t p) {
+    return p < 126 ? 2 : p < 65536 ? 4 : 10;
+}
+
+__global__ __launch_bounds__(kBlock) void k_gen_frames(uint8_t* wire, uint32_t n, uint64_t plen,
+                                                       uint64_t seed, int opcode0, int fragmented,
+                                                       int force_keys, uint64_t words_per_frame) {
+    const uint64_t gid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t total = (uint64_t)n * words_per_frame;
+    const uint64_t hs = gen_header_size(plen);
+    const uint64_t stride = hs + 4 + plen;
+    for (uint64_t g = gid; g < total; g += (uint64_t)gridDim.x * kBlock) {
+        const uint32_t i = (uint32_t)(g / words_per_frame);
+        const uint64_t wi = g - (uint64_t)i * words_per_frame;
+        uint8_t* w = wire + (uint64_t)i * stride;
+        uint32_t key = (uint32_t)splitmix64(seed ^ (uint64_t)i);
+        if (force_keys && i == 0) key = 0u;
+        if (force_keys && i == 1) key = 0xFFFFFFFFu;
+        if (wi == 0) {
+            const int fin = !fragmented || i + 1 == n;
+            const int op = (i == 0 || !fragmented) ? opcode0 : 0;
+            w[0] = (uint8_t)((fin ? 0x80 : 0) | (op & 0x0F));
+            if (hs == 2) {
+                w[1] = (uint8_t)(0x80 | plen);
+            } else if (hs == 4) {
+                w[1] = 0x80 | 126;
+                w[2] = (uint8_t)(plen >> 8);
+                w[3] = (uint8_t)plen;
+            } else {
+                w[1] = 0x80 | 127;
+                for (int k = 0; k < 8; ++k) w[2 + k] = (uint8_t)(plen >> (56 - 8 * k));
+            }
+            for (int k = 0; k < 4; ++k) w[hs + k] = (uint8_t)(key >> (8 * k));
+        }
+        const uint64_t b = wi * 8;
+        if (b < plen) {
+            const uint64_t r = splitmix64(seed + ((uint64_t)i << 32) + wi);
+            uint8_t* pl = w + hs + 4;
+            for (int k = 0; k < 8 && b + k < plen; ++k)
+                pl[b + k] = (uint8_t)(r >> (8 * k)) ^ (uint8_t)(key >> (8 * ((b + k) & 3)));
+        }
+    }
+}
+
+}  // namespace
+
+// ======================================================================================
+// engine + C ABI
+// ======================================================================================
+struct uvhttp_ws_gpu_engine {
+    int device;
+    void* ws_mem;
+    size_t ws_bytes;
+    uint32_t cap_frames;
+    uint64_t cap_tiles, cap_arena_tiles;
+    Workspace ws;
+    int timing;
+    hipEvent_t ev[2 * 1024];
+    int ev_created;
+    int ev_used;       // event pairs recorded and not yet harvested
+    double time_ms;
+    uint64_t launches;
+    char err[256];
+};
+
+static int set_err(uvhttp_ws_gpu_engine_t* e, int code, const char* what, hipError_t h) {
+    if (e) snprintf(e->err, sizeof(e->err), "%s: %s", what, h == hipSuccess ? "" : hipGetErrorString(h));
+    return code;
+}
+
+extern "C" {
+
+const char* uvhttp_ws_amd_version(void) { return "uvhttp_ws_amd 0.1.0 gfx950"; }
+
+uint64_t uvhttp_ws_gen_frame_stride(uint64_t payload_len) {
+    return gen_header_size(payload_len) + 4 + payload_len;
+}
+
+int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out) {
+    if (!out) return UVHTTP_WS_GPU_EINVAL;
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0 || device < 0 || device >= count)
+        return UVHTTP_WS_GPU_ENODEV;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return UVHTTP_WS_GPU_ENODEV;
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return UVHTTP_WS_GPU_ENODEV;
+    uvhttp_ws_gpu_engine_t* e = (uvhttp_ws_gpu_engine_t*)calloc(1, sizeof(*e));
+    if (!e) return UVHTTP_WS_GPU_ENOMEM;
+    e->device = device;
+    *out = e;
+    return UVHTTP_WS_GPU_OK;
+}
+
+void uvhttp_ws_gpu_engine_free(uvhttp_ws_gpu_engine_t* e) {
+    if (!e) return;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(e->device);
+    if (e->ws_mem) (void)hipFree(e->ws_mem);
+    for (int k = 0; k < e->ev_created; ++k) (void)hipEventDestroy(e->ev[k]);
+    (void)hipSetDevice(prev);
+    free(e);
+}
+
+const char* uvhttp_ws_gpu_engine_last_error(const uvhttp_ws_gpu_engine_t* e) {
+    return e ? e->err : "no engine";
+}
+
+static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+int uvhttp_ws_gpu_engine_reserve(uvhttp_ws_gpu_engine_t* e, uint32_t max_frames,
+                                 uint64_t max_wire_bytes, uint64_t max_arena_bytes) {
+    if (!e) return UVHTTP_WS_GPU_EINVAL;
+    if (max_frames > kMaxFrames) return set_err(e, UVHTTP_WS_GPU_EINVAL, "too many frames", hipSuccess);
+    const uint64_t tiles = (max_wire_bytes + kTile - 1) / kTile + 1;
+    const uint64_t atiles = (max_arena_bytes + kTile - 1) / kTile + 1;
+    if (e->ws_mem && max_frames <= e->cap_frames && tiles <= e->cap_tiles &&
+        atiles <= e->cap_arena_tiles)
+        return UVHTTP_WS_GPU_OK;
+    const uint32_t fr = max_frames > e->cap_frames ? max_frames : e->cap_frames;
+    const uint64_t tl = tiles > e->cap_tiles ? tiles : e->cap_tiles;
+    const uint64_t at = atiles > e->cap_arena_tiles ? atiles : e->cap_arena_tiles;
+    const uint64_t nblk = (fr + kBlock - 1) / kBlock + 2;
+    size_t off_agg = 0;
+    size_t off_tiles = align_up(off_agg + nblk * sizeof(ScanElem), 256);
+    size_t off_bad = align_up(off_tiles + tl * sizeof(uint32_t), 256);
+    size_t off_arena = align_up(off_bad + 16, 256);
+    size_t bytes = align_up(off_arena + at * sizeof(uint32_t), 256);
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(e->device);
+    if (e->ws_mem) (void)hipFree(e->ws_mem);
+    e->ws_mem = nullptr;
+    hipError_t h = hipMalloc(&e->ws_mem, bytes);
+    (void)hipSetDevice(prev);
+    if (h != hipSuccess) {
+        e->cap_frames = 0;
+        e->cap_tiles = e->cap_arena_tiles = 0;
+        return set_err(e, UVHTTP_WS_GPU_ENOMEM, "hipMalloc workspace", h);
+    }
+    char* b = (char*)e->ws_mem;
+    e->ws.block_agg = (ScanElem*)(b + off_agg);
+    e->ws.tile_first = (uint32_t*)(b + off_tiles);
+    e->ws.first_bad = (uint32_t*)(b + off_bad);
+    e->ws.arena_first = (uint32_t*)(b + off_arena);
+    e->ws_bytes = bytes;
+    e->cap_frames = fr;
+    e->cap_tiles = tl;
+    e->cap_arena_tiles = at;
+    return UVHTTP_WS_GPU_OK;
+}
+
+int uvhttp_ws_gpu_engine_set_timing(uvhttp_ws_gpu_engine_t* e, int enable) {
+    if (!e) return UVHTTP_WS_GPU_EINVAL;
+    e->timing = enable ? 1 : 0;
+    return UVHTTP_WS_GPU_OK;
+}
+
+static void harvest(uvhttp_ws_gpu_engine_t* e) {
+    if (!e->ev_used) return;
+    (void)hipEventSynchronize(e->ev[2 * e->ev_used - 1]);
+    for (int k = 0; k < e->ev_used; ++k) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, e->ev[2 * k], e->ev[2 * k + 1]) == hipSuccess) {
+            e->time_ms += ms;
+            e->launches++;
+        }
+    }
+    e->ev_used = 0;
+}
+
+int uvhttp_ws_gpu_engine_kernel_time(uvhttp_ws_gpu_engine_t* e, double* ms, uint64_t* launches) {
+    if (!e) return UVHTTP_WS_GPU_EINVAL;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(e->device);
+    harvest(e);
+    (void)hipSetDevice(prev);
+    if (ms) *ms = e->time_ms;
+    if (launches) *launches = e->launches;
+    e->time_ms = 0;
+    e->launches = 0;
+    return UVHTTP_WS_GPU_OK;
+}
+
+static int timing_begin(uvhttp_ws_gpu_engine_t* e, hipStream_t s) {
+    if (!e->timing) return -1;
+    if (e->ev_used * 2 + 2 > (int)(sizeof(e->ev) / sizeof(e->ev[0]))) harvest(e);
+    const int k = e->ev_used;
+    while (e->ev_created < 2 * k + 2) {
+        if (hipEventCreate(&e->ev[e->ev_created]) != hipSuccess) return -1;
+        e->ev_created++;
+    }
+    (void)hipEventRecord(e->ev[2 * k], s);
+    return k;
+}
+
+static void timing_end(uvhttp_ws_gpu_engine_t* e, int k, hipStream_t s) {
+    if (k < 0) return;
+    (void)hipEventRecord(e->ev[2 * k + 1], s);
+    e->ev_used = k + 1;
+}
+
+static int check_batch(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b,
+                       const void* d_desc, const void* d_summary) {
+    if (!e || !b || !d_desc || !d_summary) return UVHTTP_WS_GPU_EINVAL;
+    if (b->n_frames && !b->wire) return set_err(e, UVHTTP_WS_GPU_EINVAL, "wire is NULL", hipSuccess);
+    if (((uintptr_t)b->wire) & 15u)
+        return set_err(e, UVHTTP_WS_GPU_EINVAL, "wire must be 16-byte aligned", hipSuccess);
+    if (b->n_frames > kMaxFrames) return set_err(e, UVHTTP_WS_GPU_EINVAL, "too many frames", hipSuccess);
+    if (!b->frame_off && b->n_frames > 1 && b->frame_stride == 0)
+        return set_err(e, UVHTTP_WS_GPU_EINVAL, "stride 0", hipSuccess);
+    return UVHTTP_WS_GPU_OK;
+}
+
+static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uint8_t* arena,
+                      uint64_t arena_cap, uvhttp_ws_frame_desc_t* d_desc,
+                      uvhttp_ws_message_desc_t* d_msgs, uvhttp_ws_batch_summary_t* d_summary,
+                      void* stream) {
+    int rc = check_batch(e, b, d_desc, d_summary);
+    if (rc) return rc;
+    const uint64_t n_tiles = (b->wire_len + kTile - 1) / kTile;
+    // arena tiles: bounded by both the capacity and the data payload that can exist
+    uint64_t arena_need = arena ? (arena_cap < b->wire_len ? arena_cap : b->wire_len) : 0;
+    const uint64_t n_atiles = arena ? (arena_need + kTile - 1) / kTile : 0;
+    rc = uvhttp_ws_gpu_engine_reserve(e, b->n_frames, b->wire_len, arena_need);
+    if (rc) return rc;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    if (prev != e->device) (void)hipSetDevice(e->device);
+    hipStream_t s = (hipStream_t)stream;
+
+    BatchArgs a;
+    a.wire = b->wire;
+    a.wire_len = b->wire_len;
+    a.frame_off = b->frame_off;
+    a.frame_stride = b->frame_stride;
+    a.n = b->n_frames;
+    a.max_frame_size = b->max_frame_size;
+    a.max_message_size = b->max_message_size;
+    a.is_server = b->is_server;
+    a.n_tiles = n_tiles;
+    a.arena = arena;
+    a.arena_cap = arena_cap;
+    a.n_arena_tiles = n_atiles;
+
+    const uint32_t n_blocks = (a.n + kBlock - 1) / kBlock;
+    const uint32_t grid_f = n_blocks ? n_blocks : 1;
+    hipLaunchKernelGGL(k_parse, dim3(grid_f), dim3(kBlock), 0, s, a, d_desc, e->ws);
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(kBlock), 0, s, e->ws, grid_f);
+    hipLaunchKernelGGL(k_resolve, dim3(grid_f), dim3(kBlock), 0, s, a, d_desc, d_msgs, e->ws);
+    const int tk = timing_begin(e, s);
+    if (!arena) {
+        if (n_tiles)
+            hipLaunchKernelGGL(k_unmask_inplace, dim3((uint32_t)n_tiles), dim3(kBlock), 0, s, a,
+                               d_desc, e->ws);
+    } else if (n_atiles && a.n) {
+        hipLaunchKernelGGL(k_gather_compact, dim3((uint32_t)n_atiles), dim3(kBlock), 0, s, a,
+                           d_desc, e->ws, arena_cap);
+    }
+    timing_end(e, tk, s);
+    hipLaunchKernelGGL(k_finalize, dim3(grid_f), dim3(kBlock), 0, s, a, d_desc, e->ws, d_summary,
+                       grid_f);
+    hipError_t h = hipGetLastError();
+    if (prev != e->device) (void)hipSetDevice(prev);
+    if (h != hipSuccess) return set_err(e, UVHTTP_WS_GPU_ELAUNCH, "launch", h);
+    return UVHTTP_WS_GPU_OK;
+}
+
+int uvhttp_ws_gpu_decode_inplace(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b,
+                                 uvhttp_ws_frame_desc_t* d_desc,
+                                 uvhttp_ws_batch_summary_t* d_summary, void* stream) {
+    return run_decode(e, b, nullptr, 0, d_desc, nullptr, d_summary, stream);
+}
+
+int uvhttp_ws_gpu_decode_compact(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b,
+                                 uint8_t* d_arena, uint64_t arena_cap,
+                                 uvhttp_ws_frame_desc_t* d_desc, uvhttp_ws_message_desc_t* d_msgs,
+                                 uvhttp_ws_batch_summary_t* d_summary, void* stream) {
+    if (!d_arena || !d_msgs) return set_err(e, UVHTTP_WS_GPU_EINVAL, "arena/msgs NULL", hipSuccess);
+    if (((uintptr_t)d_arena) & 15u)
+        return set_err(e, UVHTTP_WS_GPU_EINVAL, "arena must be 16-byte aligned", hipSuccess);
+    return run_decode(e, b, d_arena, arena_cap, d_desc, d_msgs, d_summary, stream);
+}
+
+int uvhttp_ws_gpu_apply_mask(uvhttp_ws_gpu_engine_t* e, uint8_t* d_data, uint64_t len,
+                             const uint8_t key[4], void* stream) {
+    if (!e || (!d_data && len) || !key) return UVHTTP_WS_GPU_EINVAL;
+    if (!len) return UVHTTP_WS_GPU_OK;
+    const uint32_t k = (uint32_t)key[0] | ((uint32_t)key[1] << 8) | ((uint32_t)key[2] << 16) |
+                       ((uint32_t)key[3] << 24);
+    uint64_t head = (16u - ((uintptr_t)d_data & 15u)) & 15u;
+    if (head > len) head = len;
+    const uint64_t nvec = (len - head) / 16;
+    uint64_t grid = (nvec + kBlock - 1) / kBlock;
+    if (grid < 1) grid = 1;
+    if (grid > 8192) grid = 8192;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    if (prev != e->device) (void)hipSetDevice(e->device);
+    hipStream_t s = (hipStream_t)stream;
+    const int tk = timing_begin(e, s);
+    hipLaunchKernelGGL(k_apply_mask, dim3((uint32_t)grid), dim3(kBlock), 0, s, d_data, len, k, head);
+    timing_end(e, tk, s);
+    hipError_t h = hipGetLastError();
+    if (prev != e->device) (void)hipSetDevice(prev);
+    if (h != hipSuccess) return set_err(e, UVHTTP_WS_GPU_ELAUNCH, "launch", h);
+    return UVHTTP_WS_GPU_OK;
+}
+
+int uvhttp_ws_gpu_gen_frames(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint32_t n_frames,
+                             uint64_t payload_len, uint64_t seed, int opcode0, int fragmented,
+                             int force_keys, void* stream) {
+    if (!e || (!d_wire && n_frames)) return UVHTTP_WS_GPU_EINVAL;
+    if (!n_frames) return UVHTTP_WS_GPU_OK;
+    const uint64_t wpf = payload_len ? (payload_len + 7) / 8 : 1;
+    uint64_t total = (uint64_t)n_frames * wpf;
+    uint64_t grid = (total + kBlock - 1) / kBlock;
+    if (grid > 65536) grid = 65536;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    if (prev != e->device) (void)hipSetDevice(e->device);
+    hipLaunchKernelGGL(k_gen_frames, dim3((uint32_t)grid), dim3(kBlock), 0, (hipStream_t)stream,
+                       d_wire, n_frames, payload_len, seed, opcode0, fragmented, force_keys, wpf);
+    hipError_t h = hipGetLastError();
+    if (prev != e->device) (void)hipSetDevice(prev);
+    if (h != hipSuccess) return set_err(e, UVHTTP_WS_GPU_ELAUNCH, "launch", h);
+    return UVHTTP_WS_GPU_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,312 @@
+/*
+ * ws_host.c — drop-in host side of the decode surface (include/uvhttp_ws_amd.h §1b).
+ *
+ * These are the functions src/uvhttp_connection.c links against
+ * (on_websocket_read -> uvhttp_ws_process_data, src/uvhttp_connection.c:1154-1164).  A live
+ * libuv read is <= 16 KiB (include/uvhttp_constants.h:207-208), far below what pays for a
+ * device round trip, so the per-connection stream path runs here on the host; batches of
+ * frames resident in HBM go through the gfx950 kernels in ws_gpu.hip instead.
+ *
+ * Structure: process_data = append (grow_recv) -> repeat { scan_frame -> unmask ->
+ * dispatch_frame -> drain } until the buffered bytes hold no complete frame.  The observable
+ * behaviour — return codes, callback order and arguments, recv/fragment buffer sizes, state —
+ * matches src/uvhttp_websocket.c:825-1097; tests/test_host_dropin.py replays the reference's
+ * own known-answer tests and a randomized stream against the oracle to check it.
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "uvhttp_ws_amd.h"
+
+static uvhttp_ws_amd_control_sink g_control_sink = NULL;
+
+void uvhttp_ws_amd_set_control_sink(uvhttp_ws_amd_control_sink sink) { g_control_sink = sink; }
+
+/* ---- connection lifetime (src/uvhttp_websocket.c:71-130, 1100-1111) ------------------- */
+
+struct uvhttp_ws_connection* uvhttp_ws_connection_create(int fd, mbedtls_ssl_context* ssl,
+                                                         int is_server,
+                                                         const uvhttp_config_t* config) {
+    uvhttp_ws_connection_t* c = (uvhttp_ws_connection_t*)calloc(1, sizeof(*c));
+    if (c == NULL) return NULL;
+    c->fd = fd;
+    c->ssl = ssl;
+    c->is_server = is_server;
+    c->state = UVHTTP_WS_STATE_CONNECTING;
+    c->config.max_frame_size =
+        config ? config->websocket_max_frame_size : UVHTTP_WS_AMD_DEFAULT_MAX_FRAME_SIZE;
+    c->config.max_message_size =
+        config ? config->websocket_max_message_size : UVHTTP_WS_AMD_DEFAULT_MAX_MESSAGE_SIZE;
+    c->config.ping_interval =
+        config ? config->websocket_ping_interval : UVHTTP_WS_AMD_DEFAULT_PING_INTERVAL;
+    c->config.ping_timeout =
+        config ? config->websocket_ping_timeout : UVHTTP_WS_AMD_DEFAULT_PING_TIMEOUT;
+    c->recv_buffer_size = UVHTTP_WS_AMD_DEFAULT_RECV_BUFFER_SIZE;
+    c->recv_buffer = (uint8_t*)malloc(c->recv_buffer_size);
+    if (c->recv_buffer == NULL) {
+        free(c);
+        return NULL;
+    }
+    return c;
+}
+
+void uvhttp_ws_connection_free(struct uvhttp_ws_connection* c) {
+    if (c == NULL) return;
+    free(c->recv_buffer);
+    free(c->send_buffer);
+    free(c->fragmented_message);
+    free(c);
+}
+
+void uvhttp_ws_set_callbacks(struct uvhttp_ws_connection* c,
+                             uvhttp_ws_on_message_callback on_message,
+                             uvhttp_ws_on_close_callback on_close,
+                             uvhttp_ws_on_error_callback on_error) {
+    if (c == NULL) return;
+    c->on_message = on_message;
+    c->on_close = on_close;
+    c->on_error = on_error;
+}
+
+/* ---- header + mask --------------------------------------------------------------------- */
+
+/* Length code -> bytes of header before the mask key (RFC 6455 §5.2). */
+static size_t header_span(uint8_t second_byte) {
+    uint8_t code = second_byte & 0x7F;
+    return code == 126 ? 4 : code == 127 ? 10 : 2;
+}
+
+uvhttp_error_t uvhttp_ws_parse_frame_header(const uint8_t* data, size_t len,
+                                            uvhttp_ws_frame_header_t* header,
+                                            size_t* header_size) {
+    if (data == NULL || header == NULL || header_size == NULL || len < 2)
+        return UVHTTP_ERROR_INVALID_PARAM;
+    memset(header, 0, sizeof(*header));
+    const uint8_t b0 = data[0], b1 = data[1];
+    header->fin = b0 >> 7;
+    header->rsv1 = (b0 >> 6) & 1;
+    header->rsv2 = (b0 >> 5) & 1;
+    header->rsv3 = (b0 >> 4) & 1;
+    header->opcode = b0 & 0x0F;
+    header->mask = b1 >> 7;
+    header->payload_len = b1 & 0x7F;
+    const size_t span = header_span(b1);
+    uint64_t length = b1 & 0x7F;
+    header->payload_length = length;
+    *header_size = 2;
+    if (span > 2) {
+        if (len < span) return UVHTTP_ERROR_INVALID_PARAM;
+        length = 0;
+        for (size_t k = 2; k < span; ++k) length = (length << 8) | data[k];
+        header->payload_length = length;
+        if (span == 10 && (length >> 63)) return UVHTTP_ERROR_INVALID_PARAM;
+        *header_size = span;
+    }
+    header->payload_length = length;
+    return UVHTTP_OK;
+}
+
+/* Word-at-a-time XOR: the key rotated to the first aligned byte is replicated into a
+ * 64-bit word; head and tail bytes use the plain byte rule. */
+void uvhttp_ws_apply_mask(uint8_t* data, size_t len, const uint8_t* key) {
+    if (data == NULL || key == NULL) return;
+    size_t i = 0;
+    while (i < len && ((uintptr_t)(data + i) & 7u)) {
+        data[i] ^= key[i & 3];
+        ++i;
+    }
+    if (len - i >= 8) {
+        uint8_t rot[8];
+        for (int b = 0; b < 8; ++b) rot[b] = key[(i + (size_t)b) & 3];
+        uint64_t k64;
+        memcpy(&k64, rot, 8);
+        uint64_t* w = (uint64_t*)(void*)(data + i);
+        size_t nw = (len - i) / 8;
+        for (size_t j = 0; j < nw; ++j) w[j] ^= k64;
+        i += nw * 8;
+    }
+    for (; i < len; ++i) data[i] ^= key[i & 3];
+}
+
+/* ---- stream decode ----------------------------------------------------------------------- */
+
+enum scan_outcome { SCAN_FRAME, SCAN_NEED_MORE, SCAN_REJECT };
+
+typedef struct {
+    uvhttp_ws_frame_header_t hdr;
+    size_t head;  /* header bytes before the key */
+    size_t total; /* header + key + payload */
+} frame_view_t;
+
+/* Recv-buffer growth (src/uvhttp_websocket.c:832-866): double until the new bytes fit,
+ * never beyond config.max_frame_size. */
+static int grow_recv(uvhttp_ws_connection_t* c, size_t extra) {
+    const size_t want = c->recv_buffer_pos + extra;
+    if (want <= c->recv_buffer_size) return 0;
+    size_t cap = c->recv_buffer_size;
+    do {
+        if (cap > SIZE_MAX / 2) return -1;
+        cap *= 2;
+    } while (want > cap);
+    const size_t ceiling = (size_t)c->config.max_frame_size;
+    if (cap > ceiling) {
+        cap = ceiling;
+        if (want > cap) return -1;
+    }
+    uint8_t* nb = (uint8_t*)realloc(c->recv_buffer, cap);
+    if (nb == NULL) return -1;
+    c->recv_buffer = nb;
+    c->recv_buffer_size = cap;
+    return 0;
+}
+
+/* Decide what the head of the receive buffer holds (src/uvhttp_websocket.c:876-932). */
+static enum scan_outcome scan_frame(const uvhttp_ws_connection_t* c, frame_view_t* v) {
+    const uint8_t* buf = c->recv_buffer;
+    const size_t have = c->recv_buffer_pos;
+    if (uvhttp_ws_parse_frame_header(buf, have, &v->hdr, &v->head) != UVHTTP_OK)
+        return have < header_span(buf[1]) ? SCAN_NEED_MORE : SCAN_REJECT;
+    const uvhttp_ws_frame_header_t* h = &v->hdr;
+    if (h->rsv1 | h->rsv2 | h->rsv3) return SCAN_REJECT;
+    if (h->opcode >= UVHTTP_WS_OPCODE_CLOSE && (h->payload_length > 125 || !h->fin))
+        return SCAN_REJECT;
+    if (c->is_server && !h->mask) return SCAN_REJECT;
+    if (h->payload_length > (uint64_t)c->config.max_frame_size) return SCAN_REJECT;
+    v->total = v->head + (h->mask ? 4u : 0u) + (size_t)h->payload_length;
+    return have < v->total ? SCAN_NEED_MORE : SCAN_FRAME;
+}
+
+/* uvhttp_ws_fragment_append semantics (src/uvhttp_websocket.c:781-822). */
+static int append_fragment(uvhttp_ws_connection_t* c, const uint8_t* p, size_t n) {
+    const size_t limit = (size_t)c->config.max_message_size;
+    if (limit != 0 && (c->fragmented_size > limit || n > limit - c->fragmented_size)) return -1;
+    if (n > c->fragmented_capacity - c->fragmented_size) {
+        const size_t need = c->fragmented_size + n;
+        size_t cap = c->fragmented_capacity;
+        if (cap == 0) {
+            cap = need;
+        } else {
+            while (cap < need) {
+                if (cap > SIZE_MAX / 2) return -1;
+                cap *= 2;
+            }
+        }
+        uint8_t* nb = (uint8_t*)realloc(c->fragmented_message, cap);
+        if (nb == NULL) return -1;
+        c->fragmented_message = nb;
+        c->fragmented_capacity = cap;
+    }
+    if (n) memcpy(c->fragmented_message + c->fragmented_size, p, n);
+    c->fragmented_size += n;
+    return 0;
+}
+
+static void drop_fragment(uvhttp_ws_connection_t* c) {
+    free(c->fragmented_message);
+    c->fragmented_message = NULL;
+    c->fragmented_size = 0;
+    c->fragmented_capacity = 0;
+}
+
+/* Data frames: RFC 6455 §5.4 reassembly (src/uvhttp_websocket.c:950-1015). */
+static int on_data_frame(uvhttp_ws_connection_t* c, const uvhttp_ws_frame_header_t* h,
+                         const uint8_t* payload) {
+    const size_t n = (size_t)h->payload_length;
+    const int is_cont = h->opcode == UVHTTP_WS_OPCODE_CONTINUATION;
+    if (c->fragmented_message != NULL) { /* a message is open */
+        if (!is_cont) return -1;
+        if (append_fragment(c, payload, n) != 0) return -1;
+        if (h->fin) {
+            if (c->on_message)
+                c->on_message(c, (const char*)c->fragmented_message, c->fragmented_size,
+                              c->fragmented_opcode);
+            drop_fragment(c);
+        }
+        return 0;
+    }
+    if (is_cont) return -1;
+    if (h->fin) {
+        if (c->on_message) c->on_message(c, (const char*)payload, n, h->opcode);
+        return 0;
+    }
+    c->fragmented_opcode = (uvhttp_ws_opcode_t)h->opcode;
+    c->fragmented_size = 0;
+    c->fragmented_capacity = 0;
+    c->fragmented_message = NULL;
+    return append_fragment(c, payload, n);
+}
+
+/* CLOSE (src/uvhttp_websocket.c:1016-1069). */
+static void on_close_frame(uvhttp_ws_connection_t* c, const uint8_t* payload, size_t n) {
+    int code = 1000;
+    const char* reason = "";
+    if (n >= 2) {
+        code = (payload[0] << 8) | payload[1];
+        if (n > 2) reason = (const char*)(payload + 2);
+    }
+    const int wired = c->user_data != NULL; /* read before on_close may clear it */
+    if (c->on_close) c->on_close(c, code, reason);
+    if (wired && g_control_sink) {
+        uint8_t echo[2 + 125];
+        size_t elen = 0;
+        if (n >= 2) {
+            size_t r = n - 2 > 125 ? 125 : n - 2;
+            memcpy(echo, payload, 2 + r);
+            elen = 2 + r;
+        }
+        g_control_sink(c, UVHTTP_WS_OPCODE_CLOSE, echo, elen);
+    }
+    c->state = UVHTTP_WS_STATE_CLOSED;
+}
+
+static int dispatch_frame(uvhttp_ws_connection_t* c, const uvhttp_ws_frame_header_t* h,
+                          const uint8_t* payload) {
+    switch (h->opcode) {
+        case UVHTTP_WS_OPCODE_CONTINUATION:
+        case UVHTTP_WS_OPCODE_TEXT:
+        case UVHTTP_WS_OPCODE_BINARY:
+            return on_data_frame(c, h, payload);
+        case UVHTTP_WS_OPCODE_CLOSE:
+            on_close_frame(c, payload, (size_t)h->payload_length);
+            return 0;
+        case UVHTTP_WS_OPCODE_PING: /* src/uvhttp_websocket.c:1070-1084 */
+            if (c->user_data != NULL && g_control_sink)
+                g_control_sink(c, UVHTTP_WS_OPCODE_PONG, payload, (size_t)h->payload_length);
+            return 0;
+        default: /* PONG and reserved opcodes are ignored (:1085) */
+            return 0;
+    }
+}
+
+uvhttp_error_t uvhttp_ws_process_data(struct uvhttp_ws_connection* c, const uint8_t* data,
+                                      size_t len) {
+    if (c == NULL || data == NULL) return UVHTTP_ERROR_INVALID_PARAM;
+    if (grow_recv(c, len) != 0) return UVHTTP_ERROR_INVALID_PARAM;
+    if (len) memcpy(c->recv_buffer + c->recv_buffer_pos, data, len);
+    c->recv_buffer_pos += len;
+
+    while (c->recv_buffer_pos >= 2) {
+        frame_view_t v;
+        const enum scan_outcome s = scan_frame(c, &v);
+        if (s == SCAN_NEED_MORE) break;
+        if (s == SCAN_REJECT) return UVHTTP_ERROR_INVALID_PARAM;
+
+        uint8_t* payload = NULL;
+        if (v.hdr.payload_length > 0) {
+            payload = c->recv_buffer + v.head;
+            if (v.hdr.mask) {
+                uint8_t key[4];
+                memcpy(key, payload, 4);
+                payload += 4;
+                uvhttp_ws_apply_mask(payload, (size_t)v.hdr.payload_length, key);
+            }
+        }
+        if (dispatch_frame(c, &v.hdr, payload) != 0) return UVHTTP_ERROR_INVALID_PARAM;
+
+        const size_t rest = c->recv_buffer_pos - v.total;
+        if (rest) memmove(c->recv_buffer, c->recv_buffer + v.total, rest);
+        c->recv_buffer_pos = rest;
+    }
+    return UVHTTP_OK;
+}
