@@ -307,6 +307,10 @@ void uvhttp_ws_gpu_engine_free(uvhttp_ws_gpu_engine_t* eng);
 /* Pre-size the workspace so later decode calls never allocate (hipGraph capture). */
 int uvhttp_ws_gpu_engine_reserve(uvhttp_ws_gpu_engine_t* eng, uint32_t max_frames,
                                  uint64_t max_wire_bytes, uint64_t max_arena_bytes);
+/* Payload-kernel workgroup shape: `block` threads x `vectors_per_lane` 16-byte vectors per
+ * workgroup tile; (0, 0) = automatic (by average frame size).  Supported: 64x1, 64x2, 64x4,
+ * 128x1, 128x2, 256x1, 256x2, 256x4.  A tuning knob only: results are identical. */
+int uvhttp_ws_gpu_engine_set_tile(uvhttp_ws_gpu_engine_t* eng, int block, int vectors_per_lane);
 /* Kernel timing: when enabled, HIP events bracket the dominant (payload) kernel of every
  * decode call on its stream; kernel_time returns the summed milliseconds and the number
  * of bracketed launches completed so far (synchronises on the last event). */

@@ -354,3 +354,19 @@ def test_config_c4_default_limit_rejects(torch, eng):
     s = eng.read_summary(summ)
     assert s["n_delivered"] == 262144 and s["first_status"] == -8 and s["status"] == -1
     assert s["pending_bytes"] == 262144 * 256
+
+
+@pytest.mark.parametrize("shape", [(64, 1), (64, 2), (64, 4), (128, 1), (128, 2), (256, 1),
+                                   (256, 2), (256, 4)])
+def test_tile_shapes_identical(torch, eng, shape):
+    """Every payload-kernel workgroup shape gives the oracle's bytes (tuning knob only)."""
+    rng = random.Random(77)
+    eng.set_tile(*shape)
+    try:
+        for sizes in ([0, 3, 17, 126, 300], [5000, 65536, 70000]):
+            wire, offs = _rand_batch(rng, 200, sizes, p_ctrl=0.1, p_frag=0.4)
+            for compact in (False, True):
+                ref, got = _run_both(torch, eng, wire, 200, offs=offs, mm=0, compact=compact)
+                _compare(ref, got, compact)
+    finally:
+        eng.set_tile(0, 0)

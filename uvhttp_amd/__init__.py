@@ -154,6 +154,7 @@ def lib() -> C.CDLL:
         "uvhttp_ws_gpu_engine_free": (None, [vp]),
         "uvhttp_ws_gpu_engine_reserve": (C.c_int, [vp, u32, u64, u64]),
         "uvhttp_ws_gpu_engine_set_timing": (C.c_int, [vp, C.c_int]),
+        "uvhttp_ws_gpu_engine_set_tile": (C.c_int, [vp, C.c_int, C.c_int]),
         "uvhttp_ws_gpu_engine_kernel_time": (C.c_int, [vp, C.POINTER(C.c_double),
                                                        C.POINTER(u64)]),
         "uvhttp_ws_gpu_engine_last_error": (C.c_char_p, [vp]),
@@ -309,6 +310,10 @@ class GpuEngine:
     def reserve(self, max_frames, max_wire, max_arena=0):
         self._check(self._L.uvhttp_ws_gpu_engine_reserve(self.h, max_frames, max_wire,
                                                          max_arena), "reserve")
+
+    def set_tile(self, block: int, vectors_per_lane: int):
+        self._check(self._L.uvhttp_ws_gpu_engine_set_tile(self.h, block, vectors_per_lane),
+                    "set_tile")
 
     def set_timing(self, on: bool):
         self._check(self._L.uvhttp_ws_gpu_engine_set_timing(self.h, 1 if on else 0), "timing")

@@ -31,10 +31,9 @@
 namespace {
 
 constexpr int kBlock = 256;                 // threads per workgroup (4 waves of 64)
-constexpr int kVecPerThread = 4;            // 16-byte vectors per lane per tile
-constexpr uint64_t kTile = (uint64_t)kBlock * kVecPerThread * 16;  // 16 KiB tile
-constexpr int kStage = 256;                 // frames staged in LDS per round
+constexpr uint64_t kMapTile = 16384;        // granularity of the tile -> first-frame maps
 constexpr uint32_t kMaxFrames = 1u << 26;   // k_scan handles <= 2^18 block aggregates
+constexpr uint32_t kNoFrame = 0xFFFFFFFFu;  // tile map entry no frame claimed this call
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -273,15 +272,12 @@ __global__ __launch_bounds__(kBlock) void k_parse(BatchArgs a, uvhttp_ws_frame_d
         desc[i] = d;
         if (st == UVHTTP_WS_FRAME_OK) elem = scan_elem_of(d, (int32_t)i);
 
-        // tiles whose start byte lies in this frame's slot (frame 0 also owns the bytes
-        // before its start): the in-place payload pass starts its frame walk there
-        const uint64_t lo = (i == 0) ? 0 : o;
-        const uint64_t hi = last ? a.wire_len : end;
-        if (hi > lo) {
-            for (uint64_t t = (lo + kTile - 1) / kTile; t * kTile < hi && t < a.n_tiles; ++t)
-                ws.tile_first[t] = i;
-        }
     }
+    // reset the tile -> first-frame maps (k_resolve fills them with atomicMin)
+    const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t gstride = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t t = gtid; t < a.n_tiles; t += gstride) ws.tile_first[t] = kNoFrame;
+    for (uint64_t t = gtid; t < a.n_arena_tiles; t += gstride) ws.arena_first[t] = kNoFrame;
     ScanElem total;
     (void)block_exclusive_scan(elem, &total);
     if (threadIdx.x == 0) ws.block_agg[blockIdx.x] = total;
@@ -325,6 +321,18 @@ __global__ __launch_bounds__(kBlock) void k_resolve(BatchArgs a, uvhttp_ws_frame
     if (i >= a.n) return;
     ex = scan_combine(ws.block_agg[blockIdx.x], ex);
 
+    // in-place tiles whose start byte lies in this frame's slot (frame 0 also owns the
+    // bytes before its start); atomicMin keeps the map deterministic even when a bad
+    // offset table makes slots overlap
+    {
+        const uint64_t o = frame_start(a, i);
+        uint64_t end = (i + 1 < a.n) ? frame_start(a, i + 1) : a.wire_len;
+        if (end > a.wire_len) end = a.wire_len;
+        const uint64_t lo = (i == 0) ? 0 : o;
+        for (uint64_t t = (lo + kMapTile - 1) / kMapTile; t * kMapTile < end && t < a.n_tiles; ++t)
+            atomicMin(&ws.tile_first[t], i);
+    }
+
     int st = d.status;
     if (st == UVHTTP_WS_FRAME_OK && is_data_op(d.opcode)) {
         bool pending = false;
@@ -365,9 +373,9 @@ __global__ __launch_bounds__(kBlock) void k_resolve(BatchArgs a, uvhttp_ws_frame
             // arena tiles whose first byte lies in this data frame's payload
             if (a.arena && d.payload_len) {
                 const uint64_t lo = ex.data_pay, hi = ex.data_pay + d.payload_len;
-                for (uint64_t t = (lo + kTile - 1) / kTile; t * kTile < hi && t < a.n_arena_tiles;
+                for (uint64_t t = (lo + kMapTile - 1) / kMapTile; t * kMapTile < hi && t < a.n_arena_tiles;
                      ++t)
-                    ws.arena_first[t] = i;
+                    atomicMin(&ws.arena_first[t], i);
             }
         }
         desc[i].status = (int8_t)st;
@@ -413,32 +421,35 @@ __device__ inline bool any_bits(const u32x4& m) { return (m.x | m.y | m.z | m.w)
 
 // ------------------------------------------------------------------------------------
 // k_unmask_inplace: the roofline kernel of the in-place decode.
-// One workgroup per 16 KiB tile of the wire buffer; lane t handles the 16-byte vectors
-// tile + (v*256 + t)*16, v < 4 (coalesced: a wave covers 1 KiB per instruction).  The
-// payload loads are issued first — they depend only on the tile index — and the frame
-// lookup (tile_first -> descriptors -> LDS) runs while they are in flight.  Every byte of
-// the wire belongs to exactly one tile, so whole-vector stores never race: bytes outside
-// any delivered payload are XORed with 0 and vectors with no payload byte are not stored.
+// One workgroup per BLOCK*VPT*16-byte tile of the wire buffer (default 64 threads x 1
+// vector = 1 KiB: on MI355X many small workgroups with one 16-byte load per lane stream
+// read+write at 6.7 TB/s against 5.9 TB/s for 16 KiB workgroups — tools/stream_probe.hip,
+// profiles/r01_stream_probe.txt).  Lane t handles the vectors tile + (v*BLOCK + t)*16.
+// The payload loads are issued first — they depend only on the tile index — and the frame
+// lookup (coarse map -> descriptors) runs while they are in flight.  Every byte of the
+// wire belongs to exactly one tile, so whole-vector stores never race: bytes outside any
+// delivered payload are XORed with 0 and vectors with no payload byte are not stored.
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_unmask_inplace(
+template <int BLOCK, int VPT>
+__global__ __launch_bounds__(BLOCK) void k_unmask_inplace(
     BatchArgs a, const uvhttp_ws_frame_desc_t* __restrict__ desc, Workspace ws) {
-    __shared__ uint64_t s_ps[kStage];
-    __shared__ uint64_t s_pe[kStage];
-    __shared__ uint32_t s_key[kStage];
+    constexpr uint64_t kT = (uint64_t)BLOCK * VPT * 16;
+    __shared__ uint64_t s_ps[BLOCK];
+    __shared__ uint64_t s_pe[BLOCK];
+    __shared__ uint32_t s_key[BLOCK];
 
-    const uint64_t tile = blockIdx.x;
-    const uint64_t t0 = tile * kTile;
+    const uint64_t t0 = (uint64_t)blockIdx.x * kT;
     const uint64_t vend = a.wire_len;
-    // last 16-byte vector that lies wholly inside the wire (loads are clamped to it so they
-    // can be issued unconditionally; the one straddling vector is finished bytewise)
+    // loads are clamped to the last whole vector so they can be issued unconditionally;
+    // the one vector straddling the end of the wire is finished bytewise
     const uint64_t full_end = vend & ~(uint64_t)15;
     const uint64_t clamp_va = full_end ? full_end - 16 : 0;
 
-    u32x4 data[kVecPerThread];
-    uint64_t va[kVecPerThread];
+    u32x4 data[VPT];
+    uint64_t va[VPT];
 #pragma unroll
-    for (int v = 0; v < kVecPerThread; ++v) {
-        va[v] = t0 + ((uint64_t)v * kBlock + threadIdx.x) * 16u;
+    for (int v = 0; v < VPT; ++v) {
+        va[v] = t0 + ((uint64_t)v * BLOCK + threadIdx.x) * 16u;
         const uint64_t la = va[v] < full_end ? va[v] : clamp_va;
         data[v] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.wire + la));
     }
@@ -446,14 +457,17 @@ __global__ __launch_bounds__(kBlock) void k_unmask_inplace(
     const uint32_t nb = *ws.first_bad;  // frames >= nb are not delivered
     if (nb == 0 || a.n == 0) return;
     const uint32_t last = (nb < a.n ? nb : a.n) - 1;
-    uint32_t f0 = ws.tile_first[tile];
-    uint32_t f1 = (tile + 1 < a.n_tiles) ? ws.tile_first[tile + 1] : last;
-    if (f0 > last) return;  // the tile starts past the delivered frames
-    if (f1 > last) f1 = last;
+    // frames overlapping [t0, t0 + kT): from the first frame of the coarse map tile holding
+    // t0 to the first frame of the coarse tile after the one holding the tile's last byte
+    const uint64_t c0 = t0 / kMapTile, c1 = (t0 + kT - 1) / kMapTile + 1;
+    const uint32_t f0 = ws.tile_first[c0];
+    uint32_t f1 = (c1 < a.n_tiles) ? ws.tile_first[c1] : last;
+    if (f0 > last) return;  // the tile starts past the delivered frames (or is unclaimed)
+    if (f1 > last || f1 < f0) f1 = last;
 
-    u32x4 m[kVecPerThread];
+    u32x4 m[VPT];
 #pragma unroll
-    for (int v = 0; v < kVecPerThread; ++v) m[v] = u32x4{0, 0, 0, 0};
+    for (int v = 0; v < VPT; ++v) m[v] = u32x4{0, 0, 0, 0};
 
     if (f1 - f0 < 2) {
         // fast path (frames of ~8 KiB and up): at most two frames touch the tile; their
@@ -463,12 +477,13 @@ __global__ __launch_bounds__(kBlock) void k_unmask_inplace(
             const uint64_t pe = ps + desc[f].payload_len;
             const uint32_t key = desc[f].masking_key;
 #pragma unroll
-            for (int v = 0; v < kVecPerThread; ++v) add_mask(m[v], va[v], ps, pe, key);
+            for (int v = 0; v < VPT; ++v) add_mask(m[v], va[v], ps, pe, key);
         }
     } else {
-        // general path: stage <= 256 frame ranges in LDS, binary-search per vector
-        for (uint32_t base = f0; base <= f1; base += kStage) {
-            const uint32_t cnt = (f1 - base + 1) < (uint32_t)kStage ? (f1 - base + 1) : kStage;
+        // general path: stage BLOCK frame ranges per round in LDS, binary-search per vector
+        for (uint32_t base = f0; base <= f1; base += BLOCK) {
+            const uint32_t cnt = (f1 - base + 1) < (uint32_t)BLOCK ? (f1 - base + 1) : BLOCK;
+            // skip rounds that end before the tile or start after it
             __syncthreads();
             if (threadIdx.x < cnt) {
                 const uvhttp_ws_frame_desc_t d = desc[base + threadIdx.x];
@@ -477,8 +492,9 @@ __global__ __launch_bounds__(kBlock) void k_unmask_inplace(
                 s_key[threadIdx.x] = d.masking_key;
             }
             __syncthreads();
+            if (s_ps[0] >= t0 + kT) break;  // this and later rounds start past the tile
 #pragma unroll
-            for (int v = 0; v < kVecPerThread; ++v) {
+            for (int v = 0; v < VPT; ++v) {
                 // last staged frame whose payload starts before the vector's end
                 int lo = 0, hi = (int)cnt - 1, j = -1;
                 while (lo <= hi) {
@@ -502,14 +518,14 @@ __global__ __launch_bounds__(kBlock) void k_unmask_inplace(
     }
 
 #pragma unroll
-    for (int v = 0; v < kVecPerThread; ++v) {
+    for (int v = 0; v < VPT; ++v) {
         if (any_bits(m[v]) && va[v] + 16 <= vend)
             __builtin_nontemporal_store(data[v] ^ m[v], reinterpret_cast<u32x4*>(a.wire + va[v]));
     }
     // the single vector that straddles the end of the wire: byte stores
-    if (full_end != vend && full_end >= t0 && full_end < t0 + kTile) {
+    if (full_end != vend && full_end >= t0 && full_end < t0 + kT) {
 #pragma unroll
-        for (int v = 0; v < kVecPerThread; ++v) {
+        for (int v = 0; v < VPT; ++v) {
             if (va[v] == full_end && any_bits(m[v])) {
                 const uint32_t mw[4] = {m[v].x, m[v].y, m[v].z, m[v].w};
                 for (uint64_t bq = 0; full_end + bq < vend; ++bq) {
@@ -522,11 +538,11 @@ __global__ __launch_bounds__(kBlock) void k_unmask_inplace(
 }
 
 // ------------------------------------------------------------------------------------
-// k_gather_compact: the roofline kernel of the compact decode.  One workgroup per 16 KiB
-// tile of the message arena; lane t produces the aligned arena vectors of its tile.  Each
-// vector's bytes come from the delivered data frame(s) covering it: out[o] =
-// wire[ps_f + (o - aoff_f)] ^ key_f[(o - aoff_f) & 3].  The source window is unaligned
-// (payload starts at header+key offsets), read as one 16-byte load.
+// k_gather_compact: the roofline kernel of the compact decode.  One workgroup per
+// BLOCK*VPT*16-byte tile of the message arena; lane t produces the aligned arena vectors of
+// its tile.  Each vector's bytes come from the delivered data frame(s) covering it:
+// out[o] = wire[ps_f + (o - aoff_f)] ^ key_f[(o - aoff_f) & 3].  The source window is
+// unaligned (payload starts at header+key offsets) and read as one 16-byte load.
 // ------------------------------------------------------------------------------------
 __device__ inline u32x4 load16_any(const uint8_t* base, int64_t addr, uint64_t limit) {
     if (addr >= 0 && (uint64_t)addr + 16 <= limit) {
@@ -542,54 +558,59 @@ __device__ inline u32x4 load16_any(const uint8_t* base, int64_t addr, uint64_t l
     return u32x4{w[0], w[1], w[2], w[3]};
 }
 
-// block-wide inclusive max-scan of one u64 per thread (256 threads)
+// block-wide inclusive max-scan of one u64 per thread
+template <int BLOCK>
 __device__ uint64_t block_inclusive_max(uint64_t v) {
-    __shared__ uint64_t wave_max[kBlock / 64];
+    __shared__ uint64_t wave_max[BLOCK / 64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
         const uint64_t o = __shfl_up(v, d, 64);
         if (lane >= d && o > v) v = o;
     }
-    if (lane == 63) wave_max[wave] = v;
-    __syncthreads();
-    for (int w = 0; w < wave; ++w)
-        if (wave_max[w] > v) v = wave_max[w];
-    __syncthreads();
+    if (BLOCK > 64) {
+        if (lane == 63) wave_max[wave] = v;
+        __syncthreads();
+        for (int w = 0; w < wave; ++w)
+            if (wave_max[w] > v) v = wave_max[w];
+        __syncthreads();
+    }
     return v;
 }
 
-__global__ __launch_bounds__(kBlock) void k_gather_compact(BatchArgs a,
-                                                           const uvhttp_ws_frame_desc_t* desc,
-                                                           Workspace ws, uint64_t arena_bytes_cap) {
-    __shared__ uint64_t s_as[kStage];  // arena start of the data payload
-    __shared__ uint64_t s_ae[kStage];  // arena end (== start for control frames)
-    __shared__ uint64_t s_ps[kStage];  // wire offset of the payload
-    __shared__ uint32_t s_key[kStage];
+template <int BLOCK, int VPT>
+__global__ __launch_bounds__(BLOCK) void k_gather_compact(
+    BatchArgs a, const uvhttp_ws_frame_desc_t* __restrict__ desc, Workspace ws,
+    uint64_t arena_bytes_cap) {
+    constexpr uint64_t kT = (uint64_t)BLOCK * VPT * 16;
+    __shared__ uint64_t s_as[BLOCK];  // arena start of the data payload
+    __shared__ uint64_t s_ae[BLOCK];  // arena end (== start for control frames)
+    __shared__ uint64_t s_ps[BLOCK];  // wire offset of the payload
+    __shared__ uint32_t s_key[BLOCK];
 
-    const uint64_t tile = blockIdx.x;
-    const uint64_t t0 = tile * kTile;
+    const uint64_t t0 = (uint64_t)blockIdx.x * kT;
     const uint32_t nb = *ws.first_bad;
     if (nb == 0 || a.n == 0) return;
     const uint32_t last = (nb < a.n ? nb : a.n) - 1;
-    const uint32_t f0 = ws.arena_first[tile];
+    const uint64_t c0 = t0 / kMapTile, c1 = (t0 + kT - 1) / kMapTile + 1;
+    const uint32_t f0 = ws.arena_first[c0];
     if (f0 > last) return;
-    uint32_t f1 = (tile + 1 < a.n_arena_tiles) ? ws.arena_first[tile + 1] : last;
+    uint32_t f1 = (c1 < a.n_arena_tiles) ? ws.arena_first[c1] : last;
     if (f1 > last || f1 < f0) f1 = last;
 
-    uint64_t oa[kVecPerThread];
-    u32x4 out[kVecPerThread];
-    bool touched[kVecPerThread];
+    uint64_t oa[VPT];
+    u32x4 out[VPT];
+    bool touched[VPT];
 #pragma unroll
-    for (int v = 0; v < kVecPerThread; ++v) {
-        oa[v] = t0 + ((uint64_t)v * kBlock + threadIdx.x) * 16u;
+    for (int v = 0; v < VPT; ++v) {
+        oa[v] = t0 + ((uint64_t)v * BLOCK + threadIdx.x) * 16u;
         out[v] = u32x4{0, 0, 0, 0};
         touched[v] = false;
     }
     uint64_t arena_end = 0;  // end of the delivered data payload staged so far
 
-    for (uint32_t base = f0; base <= f1; base += kStage) {
-        const uint32_t cnt = (f1 - base + 1) < (uint32_t)kStage ? (f1 - base + 1) : kStage;
+    for (uint32_t base = f0; base <= f1; base += BLOCK) {
+        const uint32_t cnt = (f1 - base + 1) < (uint32_t)BLOCK ? (f1 - base + 1) : BLOCK;
         uint64_t as = 0, ae = 0, ps = 0;
         uint32_t key = 0;
         bool data = false;
@@ -605,7 +626,9 @@ __global__ __launch_bounds__(kBlock) void k_gather_compact(BatchArgs a,
             key = d.masking_key;
         }
         // control frames take the running arena end so s_as stays sorted
-        const uint64_t run = block_inclusive_max(data ? ae : 0);
+        uint64_t run = block_inclusive_max<BLOCK>(data ? ae : 0);
+        if (run < arena_end) run = arena_end;
+        __syncthreads();
         if (threadIdx.x < cnt) {
             s_as[threadIdx.x] = data ? as : run;
             s_ae[threadIdx.x] = data ? ae : run;
@@ -614,8 +637,9 @@ __global__ __launch_bounds__(kBlock) void k_gather_compact(BatchArgs a,
         }
         __syncthreads();
         if (cnt && s_ae[cnt - 1] > arena_end) arena_end = s_ae[cnt - 1];
+        if (s_as[0] >= t0 + kT) break;
 #pragma unroll
-        for (int v = 0; v < kVecPerThread; ++v) {
+        for (int v = 0; v < VPT; ++v) {
             // last staged frame starting before the vector's end
             int lo = 0, hi = (int)cnt - 1, j = -1;
             while (lo <= hi) {
@@ -643,12 +667,11 @@ __global__ __launch_bounds__(kBlock) void k_gather_compact(BatchArgs a,
                 touched[v] = true;
             }
         }
-        __syncthreads();
     }
 
     const uint64_t lim = arena_end < arena_bytes_cap ? arena_end : arena_bytes_cap;
 #pragma unroll
-    for (int v = 0; v < kVecPerThread; ++v) {
+    for (int v = 0; v < VPT; ++v) {
         if (!touched[v] || oa[v] >= lim) continue;
         if (oa[v] + 16 <= lim) {
             __builtin_nontemporal_store(out[v], reinterpret_cast<u32x4*>(a.arena + oa[v]));
@@ -809,6 +832,7 @@ struct uvhttp_ws_gpu_engine {
     uint64_t cap_tiles, cap_arena_tiles;
     Workspace ws;
     int timing;
+    int tile_block, tile_vpt;  // payload kernel shape, 0 = automatic
     hipEvent_t ev[2 * 1024];
     int ev_created;
     int ev_used;       // event pairs recorded and not yet harvested
@@ -867,8 +891,8 @@ int uvhttp_ws_gpu_engine_reserve(uvhttp_ws_gpu_engine_t* e, uint32_t max_frames,
                                  uint64_t max_wire_bytes, uint64_t max_arena_bytes) {
     if (!e) return UVHTTP_WS_GPU_EINVAL;
     if (max_frames > kMaxFrames) return set_err(e, UVHTTP_WS_GPU_EINVAL, "too many frames", hipSuccess);
-    const uint64_t tiles = (max_wire_bytes + kTile - 1) / kTile + 1;
-    const uint64_t atiles = (max_arena_bytes + kTile - 1) / kTile + 1;
+    const uint64_t tiles = (max_wire_bytes + kMapTile - 1) / kMapTile + 1;
+    const uint64_t atiles = (max_arena_bytes + kMapTile - 1) / kMapTile + 1;
     if (e->ws_mem && max_frames <= e->cap_frames && tiles <= e->cap_tiles &&
         atiles <= e->cap_arena_tiles)
         return UVHTTP_WS_GPU_OK;
@@ -903,6 +927,20 @@ int uvhttp_ws_gpu_engine_reserve(uvhttp_ws_gpu_engine_t* e, uint32_t max_frames,
     e->cap_tiles = tl;
     e->cap_arena_tiles = at;
     return UVHTTP_WS_GPU_OK;
+}
+
+int uvhttp_ws_gpu_engine_set_tile(uvhttp_ws_gpu_engine_t* e, int block, int vectors_per_lane) {
+    if (!e) return UVHTTP_WS_GPU_EINVAL;
+    static const int ok[][2] = {{0, 0}, {64, 1}, {64, 2}, {64, 4}, {128, 1},
+                                {128, 2}, {256, 1}, {256, 2}, {256, 4}};
+    for (const auto& c : ok) {
+        if (c[0] == block && c[1] == vectors_per_lane) {
+            e->tile_block = block;
+            e->tile_vpt = vectors_per_lane;
+            return UVHTTP_WS_GPU_OK;
+        }
+    }
+    return set_err(e, UVHTTP_WS_GPU_EINVAL, "unsupported tile shape", hipSuccess);
 }
 
 int uvhttp_ws_gpu_engine_set_timing(uvhttp_ws_gpu_engine_t* e, int enable) {
@@ -974,10 +1012,10 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
                       void* stream) {
     int rc = check_batch(e, b, d_desc, d_summary);
     if (rc) return rc;
-    const uint64_t n_tiles = (b->wire_len + kTile - 1) / kTile;
+    const uint64_t n_tiles = (b->wire_len + kMapTile - 1) / kMapTile;
     // arena tiles: bounded by both the capacity and the data payload that can exist
     uint64_t arena_need = arena ? (arena_cap < b->wire_len ? arena_cap : b->wire_len) : 0;
-    const uint64_t n_atiles = arena ? (arena_need + kTile - 1) / kTile : 0;
+    const uint64_t n_atiles = arena ? (arena_need + kMapTile - 1) / kMapTile : 0;
     rc = uvhttp_ws_gpu_engine_reserve(e, b->n_frames, b->wire_len, arena_need);
     if (rc) return rc;
     int prev = 0;
@@ -1004,14 +1042,36 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
     hipLaunchKernelGGL(k_parse, dim3(grid_f), dim3(kBlock), 0, s, a, d_desc, e->ws);
     hipLaunchKernelGGL(k_scan, dim3(1), dim3(kBlock), 0, s, e->ws, grid_f);
     hipLaunchKernelGGL(k_resolve, dim3(grid_f), dim3(kBlock), 0, s, a, d_desc, d_msgs, e->ws);
+    // payload kernel tile shape: explicit (set_tile) or by average wire bytes per frame
+    // (auto shapes from tools/tile_sweep.py on MI355X, profiles/r01_tile_sweep.txt)
+    int blk = e->tile_block, vpt = e->tile_vpt;
+    if (!blk) {
+        const uint64_t avg = a.n ? b->wire_len / a.n : 0;
+        if (!arena) {
+            blk = avg >= 32768 ? 64 : 256;
+            vpt = avg >= 32768 ? 1 : avg >= 2048 ? 2 : 4;
+        } else {
+            blk = avg >= 2048 ? 64 : 256;
+            vpt = 2;
+        }
+    }
+    const uint64_t span = arena ? (n_atiles ? arena_need : 0) : b->wire_len;
+    const uint64_t tile_bytes = (uint64_t)blk * vpt * 16;
+    const uint32_t grid_p = (uint32_t)((span + tile_bytes - 1) / tile_bytes);
     const int tk = timing_begin(e, s);
-    if (!arena) {
-        if (n_tiles)
-            hipLaunchKernelGGL(k_unmask_inplace, dim3((uint32_t)n_tiles), dim3(kBlock), 0, s, a,
-                               d_desc, e->ws);
-    } else if (n_atiles && a.n) {
-        hipLaunchKernelGGL(k_gather_compact, dim3((uint32_t)n_atiles), dim3(kBlock), 0, s, a,
-                           d_desc, e->ws, arena_cap);
+    if (grid_p && a.n) {
+#define UVWS_LAUNCH(B, V)                                                                        \
+    if (blk == B && vpt == V) {                                                                  \
+        if (!arena)                                                                              \
+            hipLaunchKernelGGL((k_unmask_inplace<B, V>), dim3(grid_p), dim3(B), 0, s, a, d_desc, \
+                               e->ws);                                                           \
+        else                                                                                     \
+            hipLaunchKernelGGL((k_gather_compact<B, V>), dim3(grid_p), dim3(B), 0, s, a, d_desc, \
+                               e->ws, arena_cap);                                                \
+    } else
+        UVWS_LAUNCH(64, 1) UVWS_LAUNCH(64, 2) UVWS_LAUNCH(64, 4) UVWS_LAUNCH(128, 1)
+        UVWS_LAUNCH(128, 2) UVWS_LAUNCH(256, 1) UVWS_LAUNCH(256, 2) UVWS_LAUNCH(256, 4) {}
+#undef UVWS_LAUNCH
     }
     timing_end(e, tk, s);
     hipLaunchKernelGGL(k_finalize, dim3(grid_f), dim3(kBlock), 0, s, a, d_desc, e->ws, d_summary,
