@@ -12,6 +12,9 @@ elapsed time over ranks is used.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4] [--mode inplace|compact]
 
+--config c5 runs BASELINE config C5 instead: 8 388 608 x 64 KiB frames in total, split into
+contiguous per-rank shards (strong scaling), each decoded in resident 1 048 576-frame passes.
+
 Rank 0 prints ONE JSON line.  `roofline` comes from HIP events bracketing the payload kernel
 on its stream during the timed steps; `cpu_baseline` times the CPU port of the reference path
 (oracle/, test infrastructure) on this host, rank 0 at N=1 only.
@@ -29,16 +32,46 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 CONFIGS = {
-    # name: (frames per GPU, payload bytes, fragmented, max_message_size)
+    # name: (frames, payload bytes, fragmented, max_message_size)
+    # c2/c3/c4: frames per GPU (weak scaling); c5: frames in total, sharded (strong scaling)
     "c2": (65536, 4096, False, 64 * 1024 * 1024),
     "c3": (65536, 65536, False, 64 * 1024 * 1024),
     "c4": (1048576, 256, True, 256 * 1024 * 1024),
+    "c5": (8388608, 65536, False, 64 * 1024 * 1024),
 }
+C5_CHUNK = 1048576  # frames resident per decode pass (68.7 GB of wire at 64 KiB frames)
 WORKLOAD = {
     "c2": "C2: 65536 x 4 KiB masked BINARY frames per GPU",
     "c3": "C3: 65536 x 64 KiB masked BINARY frames per GPU (C5 shard shape)",
     "c4": "C4: 1048576 x 256 B masked frames, one fragmented message per GPU",
+    "c5": "C5: 8388608 x 64 KiB masked BINARY frames sharded evenly over the GPUs",
 }
+
+
+def shard_plan(cfg_name, rank, world):
+    """Frames this rank decodes: (first_frame, frames_per_pass, passes).  c2-c4 give every
+    rank its own full batch (weak scaling); c5 splits 8 388 608 frames into contiguous
+    per-rank ranges [r*N/W, (r+1)*N/W), each decoded in resident chunks of <= 1 048 576
+    frames; no frame is shared, so no data-path collective exists."""
+    n, _, _, _ = CONFIGS[cfg_name]
+    if cfg_name != "c5":
+        return rank * n, n, 1
+    lo, hi = rank * n // world, (rank + 1) * n // world
+    per = min(hi - lo, C5_CHUNK)
+    passes = (hi - lo + per - 1) // per
+    return lo, per, passes
+
+
+def max_over_ranks(value, world):
+    """The timed region is the slowest rank's (gloo all_reduce MAX of a host scalar)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([value], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
 SEED = 0x5EED0001
 GIB = float(1 << 30)
@@ -147,13 +180,14 @@ def main():
     torch.cuda.set_device(local)
     dev = f"cuda:{local}"
 
-    n, plen, frag, mm = CONFIGS[args.config]
+    _, plen, frag, mm = CONFIGS[args.config]
+    first, n, passes = shard_plan(args.config, rank, world)
     stride = U.gen_frame_stride(plen)
     wire_len = stride * n
     eng = U.GpuEngine(local)
     stream = torch.cuda.current_stream(local)
     wire = torch.empty(wire_len + 64, dtype=torch.uint8, device=dev)
-    eng.gen_frames(wire, n, plen, SEED + rank, opcode0=2, fragmented=frag, stream=stream)
+    eng.gen_frames(wire, n, plen, SEED + first, opcode0=2, fragmented=frag, stream=stream)
     desc, summ = eng.alloc_outputs(n)
     arena = msgs = None
     if args.mode == "compact":
@@ -162,6 +196,10 @@ def main():
     eng.reserve(n, wire_len, n * plen if arena is not None else 0)
 
     def step():
+        for _ in range(passes):
+            one_pass()
+
+    def one_pass():
         if arena is None:
             eng.decode_inplace(wire, n, stride=stride, max_message_size=mm, wire_len=wire_len,
                                desc=desc, summary=summ, stream=stream)
@@ -194,12 +232,8 @@ def main():
     s = eng.read_summary(summ)
     assert s["n_delivered"] == n and s["status"] == 0, s
 
-    el_t = torch.tensor([elapsed], dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
-    el_max = float(el_t.item())
-
-    payload_per_rank = n * plen
+    el_max = max_over_ranks(elapsed, world)
+    payload_per_rank = n * plen * passes
     total_payload = payload_per_rank * world * args.steps
     value = total_payload / el_max / GIB
 
@@ -213,7 +247,7 @@ def main():
 
     e2e = None
     if args.e2e and rank == 0:
-        e2e = e2e_rate(torch, eng, n, plen, stride, wire_len, mm, dev, stream)
+        e2e = e2e_rate(n, plen, stride, mm, local)
 
     if rank == 0:
         out = {
@@ -225,14 +259,15 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(el_max / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.config == "c5" else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (splitmix64 payload + per-frame keys, generated on device)",
             "config": {
                 "workload": WORKLOAD[args.config],
                 "mode": args.mode,
-                "frames_per_gpu": n,
+                "frames_per_gpu": n * passes,
+                "decode_passes_per_step": passes,
                 "payload_bytes_per_frame": plen,
                 "wire_bytes_per_frame": stride,
                 "parallelism": f"shard{world} (independent frames, no collective)",
@@ -260,27 +295,40 @@ def main():
     eng.close()
 
 
-def e2e_rate(torch, eng, n, plen, stride, wire_len, mm, dev, stream):
-    """Host-memory pipeline: pinned host wire -> H2D -> decode -> D2H of the payload region.
-    Recorded in DESIGN.md (PCIe-bound; never the metric)."""
-    host = torch.empty(wire_len, dtype=torch.uint8, pin_memory=True)
-    dwire = torch.empty(wire_len + 64, dtype=torch.uint8, device=dev)
-    eng.gen_frames(dwire, n, plen, SEED, opcode0=2, stream=stream)
-    host.copy_(dwire[:wire_len])
-    back = torch.empty(wire_len, dtype=torch.uint8, pin_memory=True)
-    desc, summ = eng.alloc_outputs(n)
-    reps = 3
-    torch.cuda.synchronize()
+def e2e_rate(n, plen, stride, mm, local, depth=3, slot_frames=1024):
+    """Host-memory pipeline (uvhttp_ws_gpu_pipeline_*): masked frames in pinned host slots
+    -> H2D -> decode_inplace -> D2H, `depth` slots on their own streams so copies and kernels
+    overlap.  PCIe-bound; recorded in DESIGN.md, never the metric."""
+    import uvhttp_amd as U
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import _oracle  # bench input generation only (host frames)
+    slot_frames = min(slot_frames, n)
+    wl = stride * slot_frames
+    pipe = U.GpuPipeline(local, depth=depth, slot_bytes=wl, slot_frames=slot_frames)
+    host, _ = _oracle.gen_frames(slot_frames, plen, SEED)
+    for k in range(depth):
+        pipe.buffer(k)[:wl] = host
+    total = max(depth, n // slot_frames)
+    for k in range(depth):  # warm
+        pipe.submit(k, wl, slot_frames, stride=stride, max_message_size=mm)
+    for k in range(depth):
+        pipe.wait(k)
     t0 = time.perf_counter()
-    for _ in range(reps):
-        dwire[:wire_len].copy_(host, non_blocking=True)
-        eng.decode_inplace(dwire, n, stride=stride, max_message_size=mm, wire_len=wire_len,
-                           desc=desc, summary=summ, stream=stream)
-        back.copy_(dwire[:wire_len], non_blocking=True)
-    torch.cuda.synchronize()
+    busy = set()
+    for k in range(total):
+        slot = k % depth
+        if slot in busy:
+            _, _, s = pipe.wait(slot)
+            assert s["n_delivered"] == slot_frames
+        pipe.submit(slot, wl, slot_frames, stride=stride, max_message_size=mm)
+        busy.add(slot)
+    for slot in busy:
+        pipe.wait(slot)
     el = time.perf_counter() - t0
-    return {"value": round(n * plen * reps / el / GIB, 2), "unit": "GiB/s",
-            "note": "pinned host buffer -> H2D -> decode_inplace -> D2H, serial, 1 stream"}
+    pipe.close()
+    return {"value": round(total * slot_frames * plen / el / GIB, 2), "unit": "GiB/s",
+            "slots": depth, "slot_frames": slot_frames, "batches": total,
+            "note": "pinned host slots -> H2D -> decode_inplace -> D2H, overlapped across slots"}
 
 
 if __name__ == "__main__":

@@ -355,6 +355,42 @@ int uvhttp_ws_gpu_gen_frames(uvhttp_ws_gpu_engine_t* eng, uint8_t* d_wire, uint3
                              uint64_t payload_len, uint64_t seed, int opcode0, int fragmented,
                              int force_keys, void* stream);
 
+/* ---- host-memory pipeline (libuv read buffers in, decoded payloads out) ---------------- */
+/* A pipeline owns `depth` slots.  Each slot = a pinned host staging buffer (the caller
+ * writes masked frames there, e.g. hands it out from the libuv alloc callback), a device
+ * wire buffer, its own engine (workspace) and its own HIP stream, so slot k's H2D copy,
+ * slot k-1's kernels and slot k-2's D2H copy overlap.  submit() enqueues
+ *   H2D(wire[0, wire_len)) -> decode_inplace -> D2H(wire, desc, summary)
+ * and returns at once; wait() blocks until the slot's decoded bytes, descriptors and
+ * summary are back in pinned host memory (the in-place contract: delivered payloads are
+ * unmasked inside the slot buffer). */
+typedef struct uvhttp_ws_gpu_pipeline uvhttp_ws_gpu_pipeline_t;
+int uvhttp_ws_gpu_pipeline_create(int device, int depth, uint64_t slot_bytes,
+                                  uint32_t slot_frames, uvhttp_ws_gpu_pipeline_t** out);
+void uvhttp_ws_gpu_pipeline_free(uvhttp_ws_gpu_pipeline_t* p);
+uint8_t* uvhttp_ws_gpu_pipeline_slot_buffer(uvhttp_ws_gpu_pipeline_t* p, int slot);
+uint64_t* uvhttp_ws_gpu_pipeline_slot_offsets(uvhttp_ws_gpu_pipeline_t* p, int slot);
+/* offsets: when use_offsets != 0 the first n entries of slot_offsets() are used, else
+ * frame i starts at i * stride.  Limits as uvhttp_ws_batch_t. */
+int uvhttp_ws_gpu_pipeline_submit(uvhttp_ws_gpu_pipeline_t* p, int slot, uint64_t wire_len,
+                                  int use_offsets, uint64_t stride, uint32_t n_frames,
+                                  int32_t max_frame_size, int32_t max_message_size,
+                                  int32_t is_server);
+int uvhttp_ws_gpu_pipeline_wait(uvhttp_ws_gpu_pipeline_t* p, int slot,
+                                const uvhttp_ws_frame_desc_t** desc,
+                                const uvhttp_ws_batch_summary_t** summary);
+
+/* Deliver a decoded in-place batch to a connection exactly as uvhttp_ws_process_data would
+ * have (src/uvhttp_websocket.c:950-1084): on_message per complete message (fragments
+ * reassembled in conn->fragmented_message with the reference growth rules), on_close +
+ * state = CLOSED for CLOSE, control-sink echo / pong when conn->user_data != NULL.  `wire`
+ * is the host copy of the decoded wire (slot buffer).  Frames [0, summary->n_delivered) are
+ * delivered; returns UVHTTP_OK, or UVHTTP_ERROR_INVALID_PARAM if the batch failed (after
+ * delivering the frames before the failure, like process_data). */
+uvhttp_error_t uvhttp_ws_deliver_batch(struct uvhttp_ws_connection* conn, const uint8_t* wire,
+                                       const uvhttp_ws_frame_desc_t* desc,
+                                       const uvhttp_ws_batch_summary_t* summary);
+
 /* Library identity, for the loader checks in tests/. */
 const char* uvhttp_ws_amd_version(void);
 

@@ -370,3 +370,82 @@ def test_tile_shapes_identical(torch, eng, shape):
                 _compare(ref, got, compact)
     finally:
         eng.set_tile(0, 0)
+
+
+def test_pipeline_and_delivery(torch, eng):
+    """Host-memory pipeline: batches written into pinned slots, decoded on the device with
+    overlapped copies, delivered to a connection; bytes, statuses, summaries and the callback
+    transcript equal the oracle's per-frame process_data."""
+    import uvhttp_amd as U
+    pipe = U.GpuPipeline(0, depth=3, slot_bytes=4 << 20, slot_frames=4096)
+    rng = random.Random(4242)
+    batches = []
+    for b in range(7):
+        sizes = [[0, 5, 125, 126, 1000], [4096, 20000], [65536, 70000]][b % 3]
+        n = rng.choice([1, 40, 300]) if b % 3 == 0 else rng.choice([1, 20, 50])
+        wire, offs = _rand_batch(rng, n, sizes, p_ctrl=0.1, p_frag=0.3,
+                                 p_bad=0.01 if b == 5 else 0.0)
+        assert wire.size <= (4 << 20)
+        batches.append((wire, offs))
+    inflight = {}
+    for k, (wire, offs) in enumerate(batches):
+        slot = k % 3
+        if slot in inflight:
+            _check_slot(pipe, *inflight.pop(slot))
+        buf = pipe.buffer(slot)
+        buf[: wire.size] = wire
+        pipe.offsets(slot)[: offs.size] = offs
+        pipe.submit(slot, wire.size, offs.size, use_offsets=True, max_message_size=0)
+        inflight[slot] = (slot, wire, offs)
+    for v in inflight.values():
+        _check_slot(pipe, *v)
+    pipe.close()
+
+
+def _check_slot(pipe, slot, wire, offs):
+    import uvhttp_amd as U
+    dp, sp, summ = pipe.wait(slot)
+    n = offs.size
+    ref = _oracle.decode_batch(wire, n, offsets=offs, max_message_size=0)
+    assert summ == ref["summary"]
+    if n:
+        assert np.array_equal(pipe.desc_array(dp, n)["status"], ref["status"])
+    assert np.array_equal(pipe.buffer(slot)[: wire.size], ref["wire"])
+    # delivery transcript vs the oracle fed the same frames one by one
+    conn = U.WsConnection(1, max_message_size=0)
+    rc = pipe.deliver(conn, slot, dp, sp)
+    oc = _oracle.OracleConn(1, max_message_size=0, record=1)
+    orc_rc = 0
+    for i in range(summ["n_delivered"]):
+        end = offs[i + 1] if i + 1 < n else wire.size
+        assert oc.process_data(wire[offs[i]:end].tobytes()) == 0
+    if summ["status"]:
+        orc_rc = -1
+    assert rc == orc_rc
+    got = [(k, a, p) for k, a, p in conn.events if k in ("message", "close")]
+    exp = [(k, a, p if k == "message" else None) for k, a, p in oc.events() if k in ("message", "close")]
+    assert got == exp
+
+
+def test_config_c5_chunk(torch, eng):
+    """One C5 pass: 1 048 576 x 64 KiB frames (68.7 GB of wire, > 2^32 work-items of payload
+    tiles).  Summary and statuses exact; sampled frames checked byte for byte."""
+    import uvhttp_amd as U
+    n, plen = 1048576, 65536
+    stride = U.gen_frame_stride(plen)
+    wl = stride * n
+    d = torch.empty(wl + 64, dtype=torch.uint8, device="cuda")
+    eng.gen_frames(d, n, plen, SEED, opcode0=2, force_keys=True)
+    desc, summ = eng.decode_inplace(d, n, stride=stride, wire_len=wl)
+    torch.cuda.synchronize()
+    s = eng.read_summary(summ)
+    assert s["n_delivered"] == n and s["status"] == 0 and s["payload_bytes"] == n * plen
+    assert s["consumed_bytes"] == wl and s["n_messages"] == n
+    assert not eng.read_desc(desc, n)["status"].any()
+    for i in list(range(0, n, 4099)) + [n - 1]:
+        got = d[i * stride:(i + 1) * stride].cpu().numpy()
+        ow, _ = _oracle.gen_frames(n, plen, SEED, force_keys=True, first=i, count=1, total=n)
+        _oracle.load().oracle_unmask_frames(_oracle._ptr(ow), 1, stride)
+        assert np.array_equal(got, ow), i
+    del d
+    torch.cuda.empty_cache()

@@ -19,7 +19,7 @@ import os
 __all__ = [
     "lib", "LIB_PATH", "FrameHeader", "FrameDesc", "MessageDesc", "BatchSummary", "Batch",
     "WsConnectionStruct", "parse_frame_header", "apply_mask", "WsConnection", "GpuEngine",
-    "GpuError", "OPCODES", "FRAME_STATUS", "gen_frame_stride",
+    "GpuError", "OPCODES", "FRAME_STATUS", "gen_frame_stride", "GpuPipeline",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -163,6 +163,14 @@ def lib() -> C.CDLL:
                                                    vp]),
         "uvhttp_ws_gpu_apply_mask": (C.c_int, [vp, vp, u64, vp, vp]),
         "uvhttp_ws_gen_frame_stride": (u64, [u64]),
+        "uvhttp_ws_gpu_pipeline_create": (C.c_int, [C.c_int, C.c_int, u64, u32, C.POINTER(vp)]),
+        "uvhttp_ws_gpu_pipeline_free": (None, [vp]),
+        "uvhttp_ws_gpu_pipeline_slot_buffer": (vp, [vp, C.c_int]),
+        "uvhttp_ws_gpu_pipeline_slot_offsets": (vp, [vp, C.c_int]),
+        "uvhttp_ws_gpu_pipeline_submit": (C.c_int, [vp, C.c_int, u64, C.c_int, u64, u32, i32, i32,
+                                                    i32]),
+        "uvhttp_ws_gpu_pipeline_wait": (C.c_int, [vp, C.c_int, C.POINTER(vp), C.POINTER(vp)]),
+        "uvhttp_ws_deliver_batch": (C.c_int, [C.POINTER(WsConnectionStruct), vp, vp, vp]),
         "uvhttp_ws_gpu_gen_frames": (C.c_int, [vp, vp, u32, u64, u64, C.c_int, C.c_int, C.c_int,
                                                vp]),
     }
@@ -170,7 +178,6 @@ def lib() -> C.CDLL:
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    _ = i32
     _LIB = L
     return L
 
@@ -408,3 +415,69 @@ class GpuEngine:
         dt = np.dtype([("arena_off", "<u8"), ("len", "<u8"), ("first_frame", "<u4"),
                        ("last_frame", "<u4"), ("opcode", "<i4"), ("reserved", "<u4")])
         return msgs[: n_msgs * 32].cpu().numpy().view(dt)
+
+
+class GpuPipeline:
+    """Host-memory pipeline (include/uvhttp_ws_amd.h): pinned staging slots, each decoded by
+    H2D -> decode_inplace -> D2H on its own stream, so consecutive slots overlap."""
+
+    def __init__(self, device=0, depth=3, slot_bytes=1 << 26, slot_frames=1 << 16):
+        import numpy as np
+        self.np = np
+        L = lib()
+        self._L = L
+        h = C.c_void_p()
+        rc = L.uvhttp_ws_gpu_pipeline_create(device, depth, slot_bytes, slot_frames, C.byref(h))
+        if rc != 0:
+            raise GpuError(f"uvhttp_ws_gpu_pipeline_create rc={rc}")
+        self.h = h
+        self.depth, self.slot_bytes, self.slot_frames = depth, slot_bytes, slot_frames
+
+    def buffer(self, slot):
+        ptr = self._L.uvhttp_ws_gpu_pipeline_slot_buffer(self.h, slot)
+        return self.np.ctypeslib.as_array((C.c_uint8 * self.slot_bytes).from_address(ptr))
+
+    def offsets(self, slot):
+        ptr = self._L.uvhttp_ws_gpu_pipeline_slot_offsets(self.h, slot)
+        return self.np.ctypeslib.as_array((C.c_uint64 * self.slot_frames).from_address(ptr))
+
+    def submit(self, slot, wire_len, n_frames, stride=0, use_offsets=False,
+               max_frame_size=16 * 1024 * 1024, max_message_size=64 * 1024 * 1024, is_server=1):
+        rc = self._L.uvhttp_ws_gpu_pipeline_submit(self.h, slot, wire_len, 1 if use_offsets else 0,
+                                                   stride, n_frames, max_frame_size,
+                                                   max_message_size, is_server)
+        if rc != 0:
+            raise GpuError(f"pipeline submit rc={rc}")
+
+    def wait(self, slot):
+        """-> (desc pointer, summary pointer, summary dict)"""
+        dp, sp = C.c_void_p(), C.c_void_p()
+        rc = self._L.uvhttp_ws_gpu_pipeline_wait(self.h, slot, C.byref(dp), C.byref(sp))
+        if rc != 0:
+            raise GpuError(f"pipeline wait rc={rc}")
+        summ = BatchSummary.from_address(sp.value)
+        return dp, sp, summ.as_dict()
+
+    def desc_array(self, dp, n):
+        raw = (C.c_uint8 * (32 * max(1, n))).from_address(dp.value)
+        dt = self.np.dtype([("payload_off", "<u8"), ("payload_len", "<u8"),
+                            ("masking_key", "<u4"), ("message", "<u4"), ("opcode", "u1"),
+                            ("flags", "u1"), ("header_size", "u1"), ("status", "i1"),
+                            ("wire_len", "<u4")])
+        return self.np.frombuffer(raw, dtype=dt, count=n)
+
+    def deliver(self, conn, slot, dp, sp):
+        """uvhttp_ws_deliver_batch on a WsConnection from this slot's decoded bytes."""
+        ptr = self._L.uvhttp_ws_gpu_pipeline_slot_buffer(self.h, slot)
+        return self._L.uvhttp_ws_deliver_batch(conn.ptr, C.c_void_p(ptr), dp, sp)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._L.uvhttp_ws_gpu_pipeline_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

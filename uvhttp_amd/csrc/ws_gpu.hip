@@ -432,13 +432,14 @@ __device__ inline bool any_bits(const u32x4& m) { return (m.x | m.y | m.z | m.w)
 // ------------------------------------------------------------------------------------
 template <int BLOCK, int VPT>
 __global__ __launch_bounds__(BLOCK) void k_unmask_inplace(
-    BatchArgs a, const uvhttp_ws_frame_desc_t* __restrict__ desc, Workspace ws) {
+    BatchArgs a, const uvhttp_ws_frame_desc_t* __restrict__ desc, Workspace ws,
+    uint64_t tile_base) {
     constexpr uint64_t kT = (uint64_t)BLOCK * VPT * 16;
     __shared__ uint64_t s_ps[BLOCK];
     __shared__ uint64_t s_pe[BLOCK];
     __shared__ uint32_t s_key[BLOCK];
 
-    const uint64_t t0 = (uint64_t)blockIdx.x * kT;
+    const uint64_t t0 = (tile_base + blockIdx.x) * kT;
     const uint64_t vend = a.wire_len;
     // loads are clamped to the last whole vector so they can be issued unconditionally;
     // the one vector straddling the end of the wire is finished bytewise
@@ -581,14 +582,14 @@ __device__ uint64_t block_inclusive_max(uint64_t v) {
 template <int BLOCK, int VPT>
 __global__ __launch_bounds__(BLOCK) void k_gather_compact(
     BatchArgs a, const uvhttp_ws_frame_desc_t* __restrict__ desc, Workspace ws,
-    uint64_t arena_bytes_cap) {
+    uint64_t arena_bytes_cap, uint64_t tile_base) {
     constexpr uint64_t kT = (uint64_t)BLOCK * VPT * 16;
     __shared__ uint64_t s_as[BLOCK];  // arena start of the data payload
     __shared__ uint64_t s_ae[BLOCK];  // arena end (== start for control frames)
     __shared__ uint64_t s_ps[BLOCK];  // wire offset of the payload
     __shared__ uint32_t s_key[BLOCK];
 
-    const uint64_t t0 = (uint64_t)blockIdx.x * kT;
+    const uint64_t t0 = (tile_base + blockIdx.x) * kT;
     const uint32_t nb = *ws.first_bad;
     if (nb == 0 || a.n == 0) return;
     const uint32_t last = (nb < a.n ? nb : a.n) - 1;
@@ -1057,17 +1058,20 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
     }
     const uint64_t span = arena ? (n_atiles ? arena_need : 0) : b->wire_len;
     const uint64_t tile_bytes = (uint64_t)blk * vpt * 16;
-    const uint32_t grid_p = (uint32_t)((span + tile_bytes - 1) / tile_bytes);
+    const uint64_t n_ptiles = (span + tile_bytes - 1) / tile_bytes;
+    // the dispatch packet counts work-items in 32 bits: split very large passes
+    const uint64_t max_tiles = (1ull << 24);
     const int tk = timing_begin(e, s);
-    if (grid_p && a.n) {
+    for (uint64_t tb = 0; a.n && tb < n_ptiles; tb += max_tiles) {
+        const uint32_t grid_p = (uint32_t)((n_ptiles - tb) < max_tiles ? (n_ptiles - tb) : max_tiles);
 #define UVWS_LAUNCH(B, V)                                                                        \
     if (blk == B && vpt == V) {                                                                  \
         if (!arena)                                                                              \
             hipLaunchKernelGGL((k_unmask_inplace<B, V>), dim3(grid_p), dim3(B), 0, s, a, d_desc, \
-                               e->ws);                                                           \
+                               e->ws, tb);                                                       \
         else                                                                                     \
             hipLaunchKernelGGL((k_gather_compact<B, V>), dim3(grid_p), dim3(B), 0, s, a, d_desc, \
-                               e->ws, arena_cap);                                                \
+                               e->ws, arena_cap, tb);                                            \
     } else
         UVWS_LAUNCH(64, 1) UVWS_LAUNCH(64, 2) UVWS_LAUNCH(64, 4) UVWS_LAUNCH(128, 1)
         UVWS_LAUNCH(128, 2) UVWS_LAUNCH(256, 1) UVWS_LAUNCH(256, 2) UVWS_LAUNCH(256, 4) {}
@@ -1141,6 +1145,164 @@ int uvhttp_ws_gpu_gen_frames(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint32_
     if (prev != e->device) (void)hipSetDevice(prev);
     if (h != hipSuccess) return set_err(e, UVHTTP_WS_GPU_ELAUNCH, "launch", h);
     return UVHTTP_WS_GPU_OK;
+}
+
+// ---- host-memory pipeline ----------------------------------------------------------------
+
+struct PipeSlot {
+    uvhttp_ws_gpu_engine_t* eng;
+    hipStream_t stream;
+    uint8_t* h_wire;   // pinned
+    uint64_t* h_off;   // pinned
+    uvhttp_ws_frame_desc_t* h_desc;  // pinned
+    uvhttp_ws_batch_summary_t* h_sum;  // pinned
+    uint8_t* d_wire;
+    uint64_t* d_off;
+    uvhttp_ws_frame_desc_t* d_desc;
+    uvhttp_ws_batch_summary_t* d_sum;
+    int busy;
+};
+
+struct uvhttp_ws_gpu_pipeline {
+    int device, depth;
+    uint64_t slot_bytes;
+    uint32_t slot_frames;
+    PipeSlot* slots;
+};
+
+void uvhttp_ws_gpu_pipeline_free(uvhttp_ws_gpu_pipeline_t* p) {
+    if (!p) return;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(p->device);
+    for (int k = 0; k < p->depth && p->slots; ++k) {
+        PipeSlot& s = p->slots[k];
+        if (s.stream) (void)hipStreamSynchronize(s.stream);
+        if (s.h_wire) (void)hipHostFree(s.h_wire);
+        if (s.h_off) (void)hipHostFree(s.h_off);
+        if (s.h_desc) (void)hipHostFree(s.h_desc);
+        if (s.h_sum) (void)hipHostFree(s.h_sum);
+        if (s.d_wire) (void)hipFree(s.d_wire);
+        if (s.d_off) (void)hipFree(s.d_off);
+        if (s.d_desc) (void)hipFree(s.d_desc);
+        if (s.d_sum) (void)hipFree(s.d_sum);
+        if (s.stream) (void)hipStreamDestroy(s.stream);
+        uvhttp_ws_gpu_engine_free(s.eng);
+    }
+    free(p->slots);
+    (void)hipSetDevice(prev);
+    free(p);
+}
+
+int uvhttp_ws_gpu_pipeline_create(int device, int depth, uint64_t slot_bytes,
+                                  uint32_t slot_frames, uvhttp_ws_gpu_pipeline_t** out) {
+    if (!out || depth < 1 || depth > 16 || !slot_bytes || !slot_frames) return UVHTTP_WS_GPU_EINVAL;
+    *out = nullptr;
+    uvhttp_ws_gpu_pipeline_t* p = (uvhttp_ws_gpu_pipeline_t*)calloc(1, sizeof(*p));
+    if (!p) return UVHTTP_WS_GPU_ENOMEM;
+    p->device = device;
+    p->depth = depth;
+    p->slot_bytes = slot_bytes;
+    p->slot_frames = slot_frames;
+    p->slots = (PipeSlot*)calloc((size_t)depth, sizeof(PipeSlot));
+    if (!p->slots) {
+        free(p);
+        return UVHTTP_WS_GPU_ENOMEM;
+    }
+    int rc = UVHTTP_WS_GPU_OK;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    for (int k = 0; k < depth && rc == UVHTTP_WS_GPU_OK; ++k) {
+        PipeSlot& s = p->slots[k];
+        rc = uvhttp_ws_gpu_engine_create(device, &s.eng);
+        if (rc) break;
+        rc = uvhttp_ws_gpu_engine_reserve(s.eng, slot_frames, slot_bytes, 0);
+        if (rc) break;
+        (void)hipSetDevice(device);
+        const size_t pad = 64;
+        if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess ||
+            hipHostMalloc((void**)&s.h_wire, slot_bytes + pad, hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc((void**)&s.h_off, (size_t)slot_frames * 8, hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc((void**)&s.h_desc, (size_t)slot_frames * sizeof(uvhttp_ws_frame_desc_t),
+                          hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc((void**)&s.h_sum, sizeof(uvhttp_ws_batch_summary_t), hipHostMallocDefault) !=
+                hipSuccess ||
+            hipMalloc((void**)&s.d_wire, slot_bytes + pad) != hipSuccess ||
+            hipMalloc((void**)&s.d_off, (size_t)slot_frames * 8) != hipSuccess ||
+            hipMalloc((void**)&s.d_desc, (size_t)slot_frames * sizeof(uvhttp_ws_frame_desc_t)) !=
+                hipSuccess ||
+            hipMalloc((void**)&s.d_sum, sizeof(uvhttp_ws_batch_summary_t)) != hipSuccess)
+            rc = UVHTTP_WS_GPU_ENOMEM;
+    }
+    (void)hipSetDevice(prev);
+    if (rc) {
+        uvhttp_ws_gpu_pipeline_free(p);
+        return rc;
+    }
+    *out = p;
+    return UVHTTP_WS_GPU_OK;
+}
+
+uint8_t* uvhttp_ws_gpu_pipeline_slot_buffer(uvhttp_ws_gpu_pipeline_t* p, int slot) {
+    return (p && slot >= 0 && slot < p->depth) ? p->slots[slot].h_wire : nullptr;
+}
+
+uint64_t* uvhttp_ws_gpu_pipeline_slot_offsets(uvhttp_ws_gpu_pipeline_t* p, int slot) {
+    return (p && slot >= 0 && slot < p->depth) ? p->slots[slot].h_off : nullptr;
+}
+
+int uvhttp_ws_gpu_pipeline_submit(uvhttp_ws_gpu_pipeline_t* p, int slot, uint64_t wire_len,
+                                  int use_offsets, uint64_t stride, uint32_t n_frames,
+                                  int32_t max_frame_size, int32_t max_message_size,
+                                  int32_t is_server) {
+    if (!p || slot < 0 || slot >= p->depth) return UVHTTP_WS_GPU_EINVAL;
+    PipeSlot& s = p->slots[slot];
+    if (s.busy || wire_len > p->slot_bytes || n_frames > p->slot_frames) return UVHTTP_WS_GPU_EINVAL;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(p->device);
+    hipError_t h = hipSuccess;
+    if (wire_len) h = hipMemcpyAsync(s.d_wire, s.h_wire, wire_len, hipMemcpyHostToDevice, s.stream);
+    if (h == hipSuccess && use_offsets && n_frames)
+        h = hipMemcpyAsync(s.d_off, s.h_off, (size_t)n_frames * 8, hipMemcpyHostToDevice, s.stream);
+    int rc = h == hipSuccess ? UVHTTP_WS_GPU_OK : UVHTTP_WS_GPU_ELAUNCH;
+    if (!rc) {
+        uvhttp_ws_batch_t b;
+        b.wire = s.d_wire;
+        b.wire_len = wire_len;
+        b.frame_off = use_offsets ? s.d_off : nullptr;
+        b.frame_stride = stride;
+        b.n_frames = n_frames;
+        b.max_frame_size = max_frame_size;
+        b.max_message_size = max_message_size;
+        b.is_server = is_server;
+        rc = uvhttp_ws_gpu_decode_inplace(s.eng, &b, s.d_desc, s.d_sum, s.stream);
+    }
+    if (!rc && wire_len)
+        h = hipMemcpyAsync(s.h_wire, s.d_wire, wire_len, hipMemcpyDeviceToHost, s.stream);
+    if (!rc && h == hipSuccess && n_frames)
+        h = hipMemcpyAsync(s.h_desc, s.d_desc, (size_t)n_frames * sizeof(uvhttp_ws_frame_desc_t),
+                           hipMemcpyDeviceToHost, s.stream);
+    if (!rc && h == hipSuccess)
+        h = hipMemcpyAsync(s.h_sum, s.d_sum, sizeof(uvhttp_ws_batch_summary_t),
+                           hipMemcpyDeviceToHost, s.stream);
+    if (!rc && h != hipSuccess) rc = UVHTTP_WS_GPU_ELAUNCH;
+    if (!rc) s.busy = 1;
+    (void)hipSetDevice(prev);
+    return rc;
+}
+
+int uvhttp_ws_gpu_pipeline_wait(uvhttp_ws_gpu_pipeline_t* p, int slot,
+                                const uvhttp_ws_frame_desc_t** desc,
+                                const uvhttp_ws_batch_summary_t** summary) {
+    if (!p || slot < 0 || slot >= p->depth) return UVHTTP_WS_GPU_EINVAL;
+    PipeSlot& s = p->slots[slot];
+    if (!s.busy) return UVHTTP_WS_GPU_EINVAL;
+    const hipError_t h = hipStreamSynchronize(s.stream);
+    s.busy = 0;
+    if (desc) *desc = s.h_desc;
+    if (summary) *summary = s.h_sum;
+    return h == hipSuccess ? UVHTTP_WS_GPU_OK : UVHTTP_WS_GPU_ELAUNCH;
 }
 
 }  // extern "C"

@@ -310,3 +310,24 @@ uvhttp_error_t uvhttp_ws_process_data(struct uvhttp_ws_connection* c, const uint
     }
     return UVHTTP_OK;
 }
+
+/* ---- delivery of a device-decoded batch (include/uvhttp_ws_amd.h) ----------------------- */
+
+uvhttp_error_t uvhttp_ws_deliver_batch(struct uvhttp_ws_connection* c, const uint8_t* wire,
+                                       const uvhttp_ws_frame_desc_t* desc,
+                                       const uvhttp_ws_batch_summary_t* summary) {
+    if (c == NULL || summary == NULL || (summary->n_delivered && (wire == NULL || desc == NULL)))
+        return UVHTTP_ERROR_INVALID_PARAM;
+    for (uint32_t i = 0; i < summary->n_delivered; ++i) {
+        const uvhttp_ws_frame_desc_t* d = &desc[i];
+        uvhttp_ws_frame_header_t h;
+        memset(&h, 0, sizeof(h));
+        h.fin = (d->flags & UVHTTP_WS_FLAG_FIN) ? 1 : 0;
+        h.mask = (d->flags & UVHTTP_WS_FLAG_MASK) ? 1 : 0;
+        h.opcode = d->opcode & 0x0F;
+        h.payload_length = d->payload_len;
+        const uint8_t* payload = d->payload_len ? wire + d->payload_off : NULL;
+        if (dispatch_frame(c, &h, payload) != 0) return UVHTTP_ERROR_INVALID_PARAM;
+    }
+    return summary->status == 0 ? UVHTTP_OK : UVHTTP_ERROR_INVALID_PARAM;
+}
