@@ -201,16 +201,21 @@ void uvhttp_ws_apply_mask(uint8_t* data, size_t len, const uint8_t* masking_key)
 uvhttp_error_t uvhttp_ws_process_data(struct uvhttp_ws_connection* conn, const uint8_t* data,
                                       size_t len);
 
-/* Control-frame hook (new).  The reference answers PING with uvhttp_ws_send_pong and
- * echoes CLOSE with uvhttp_ws_send_frame through the server wrapper stored in
- * conn->user_data (src/uvhttp_websocket.c:1028-1084); the send side is outside this
- * library, so the integration layer registers this sink and forwards to those calls
- * (INTEGRATION.md).  opcode is UVHTTP_WS_OPCODE_PONG (reply to a PING, payload = the
- * ping payload) or UVHTTP_WS_OPCODE_CLOSE (echo, payload = code + reason, <= 127 B).
- * It is called only when conn->user_data != NULL, exactly where the reference sends. */
-typedef void (*uvhttp_ws_amd_control_sink)(struct uvhttp_ws_connection* conn, int opcode,
-                                           const uint8_t* payload, size_t len);
-void uvhttp_ws_amd_set_control_sink(uvhttp_ws_amd_control_sink sink);
+/* Control-frame hooks (new).  The reference answers PING with uvhttp_ws_send_pong and
+ * echoes CLOSE with uvhttp_ws_send_frame through the server context reached from the
+ * wrapper in conn->user_data (src/uvhttp_websocket.c:1028-1084); for CLOSE it captures that
+ * context BEFORE calling on_close (which frees the wrapper) and sends AFTER.  The send side
+ * lives outside this library, so the integration layer registers:
+ *   resolver(conn) -> the server context (wrapper->conn->server->context) or NULL; called
+ *                     only when conn->user_data != NULL, at the point the reference reads it;
+ *   sink(ctx, conn, opcode, payload, len) -> send; called only with a non-NULL ctx.
+ * opcode is UVHTTP_WS_OPCODE_PONG (payload = the ping payload) or UVHTTP_WS_OPCODE_CLOSE
+ * (payload = code + reason truncated to 125 B, empty when the close had < 2 bytes). */
+typedef void* (*uvhttp_ws_amd_context_resolver)(struct uvhttp_ws_connection* conn);
+typedef void (*uvhttp_ws_amd_control_sink)(void* ctx, struct uvhttp_ws_connection* conn,
+                                           int opcode, const uint8_t* payload, size_t len);
+void uvhttp_ws_amd_set_control_hooks(uvhttp_ws_amd_context_resolver resolver,
+                                     uvhttp_ws_amd_control_sink sink);
 
 /* ------------------------------------------------------------------------------------ */
 /* 2. Batched device surface (MI355X / gfx950)                                          */

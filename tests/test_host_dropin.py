@@ -117,11 +117,16 @@ def test_random_streams_match_oracle(seed):
     orc = _oracle.OracleConn(1, mfs, mms, record=1, wrapper=True)
     sink_events = []
 
+    @U.CONTEXT_RESOLVER
+    def resolver(conn):
+        return 0x5E  # stands for wrapper->conn->server->context
+
     @U.CONTROL_SINK
-    def sink(conn, op, p, n):
+    def sink(ctx, conn, op, p, n):
+        assert ctx == 0x5E
         sink_events.append(("pong" if op == 0xA else "close_echo", op, C.string_at(p, n) if n else b""))
 
-    U.lib().uvhttp_ws_amd_set_control_sink(sink)
+    U.lib().uvhttp_ws_amd_set_control_hooks(resolver, sink)
     try:
         pos = 0
         while pos < len(stream):
@@ -147,4 +152,4 @@ def test_random_streams_match_oracle(seed):
             assert [e[2] for e in sink_events if e[0] == kind] == \
                 [p for k, a, p in oev if k == kind]
     finally:
-        U.lib().uvhttp_ws_amd_set_control_sink(U.CONTROL_SINK())
+        U.lib().uvhttp_ws_amd_set_control_hooks(U.CONTEXT_RESOLVER(), U.CONTROL_SINK())

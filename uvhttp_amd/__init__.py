@@ -80,7 +80,9 @@ class Batch(C.Structure):
 ON_MESSAGE = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_char), C.c_size_t, C.c_int)
 ON_CLOSE = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_char_p)
 ON_ERROR = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_char_p)
-CONTROL_SINK = C.CFUNCTYPE(None, C.c_void_p, C.c_int, C.POINTER(C.c_uint8), C.c_size_t)
+CONTEXT_RESOLVER = C.CFUNCTYPE(C.c_void_p, C.c_void_p)
+CONTROL_SINK = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_uint8),
+                           C.c_size_t)
 
 
 class WsConfig(C.Structure):
@@ -149,7 +151,7 @@ def lib() -> C.CDLL:
         "uvhttp_ws_set_callbacks": (None, [C.POINTER(WsConnectionStruct), ON_MESSAGE, ON_CLOSE,
                                            ON_ERROR]),
         "uvhttp_ws_process_data": (C.c_int, [C.POINTER(WsConnectionStruct), vp, C.c_size_t]),
-        "uvhttp_ws_amd_set_control_sink": (None, [CONTROL_SINK]),
+        "uvhttp_ws_amd_set_control_hooks": (None, [CONTEXT_RESOLVER, CONTROL_SINK]),
         "uvhttp_ws_gpu_engine_create": (C.c_int, [C.c_int, C.POINTER(vp)]),
         "uvhttp_ws_gpu_engine_free": (None, [vp]),
         "uvhttp_ws_gpu_engine_reserve": (C.c_int, [vp, u32, u64, u64]),

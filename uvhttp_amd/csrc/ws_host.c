@@ -19,9 +19,19 @@
 
 #include "uvhttp_ws_amd.h"
 
+static uvhttp_ws_amd_context_resolver g_resolver = NULL;
 static uvhttp_ws_amd_control_sink g_control_sink = NULL;
 
-void uvhttp_ws_amd_set_control_sink(uvhttp_ws_amd_control_sink sink) { g_control_sink = sink; }
+void uvhttp_ws_amd_set_control_hooks(uvhttp_ws_amd_context_resolver resolver,
+                                     uvhttp_ws_amd_control_sink sink) {
+    g_resolver = resolver;
+    g_control_sink = sink;
+}
+
+/* the server context the reference reaches through conn->user_data, or NULL */
+static void* server_context(uvhttp_ws_connection_t* c) {
+    return (c->user_data != NULL && g_resolver != NULL) ? g_resolver(c) : NULL;
+}
 
 /* ---- connection lifetime (src/uvhttp_websocket.c:71-130, 1100-1111) ------------------- */
 
@@ -245,9 +255,9 @@ static void on_close_frame(uvhttp_ws_connection_t* c, const uint8_t* payload, si
         code = (payload[0] << 8) | payload[1];
         if (n > 2) reason = (const char*)(payload + 2);
     }
-    const int wired = c->user_data != NULL; /* read before on_close may clear it */
+    void* ctx = server_context(c); /* captured before on_close frees the wrapper */
     if (c->on_close) c->on_close(c, code, reason);
-    if (wired && g_control_sink) {
+    if (ctx != NULL && g_control_sink != NULL) {
         uint8_t echo[2 + 125];
         size_t elen = 0;
         if (n >= 2) {
@@ -255,7 +265,7 @@ static void on_close_frame(uvhttp_ws_connection_t* c, const uint8_t* payload, si
             memcpy(echo, payload, 2 + r);
             elen = 2 + r;
         }
-        g_control_sink(c, UVHTTP_WS_OPCODE_CLOSE, echo, elen);
+        g_control_sink(ctx, c, UVHTTP_WS_OPCODE_CLOSE, echo, elen);
     }
     c->state = UVHTTP_WS_STATE_CLOSED;
 }
@@ -270,10 +280,12 @@ static int dispatch_frame(uvhttp_ws_connection_t* c, const uvhttp_ws_frame_heade
         case UVHTTP_WS_OPCODE_CLOSE:
             on_close_frame(c, payload, (size_t)h->payload_length);
             return 0;
-        case UVHTTP_WS_OPCODE_PING: /* src/uvhttp_websocket.c:1070-1084 */
-            if (c->user_data != NULL && g_control_sink)
-                g_control_sink(c, UVHTTP_WS_OPCODE_PONG, payload, (size_t)h->payload_length);
+        case UVHTTP_WS_OPCODE_PING: { /* src/uvhttp_websocket.c:1070-1084 */
+            void* ctx = server_context(c);
+            if (ctx != NULL && g_control_sink != NULL)
+                g_control_sink(ctx, c, UVHTTP_WS_OPCODE_PONG, payload, (size_t)h->payload_length);
             return 0;
+        }
         default: /* PONG and reserved opcodes are ignored (:1085) */
             return 0;
     }
