@@ -243,6 +243,7 @@ void uvhttp_ws_amd_set_control_hooks(uvhttp_ws_amd_context_resolver resolver,
 #define UVHTTP_WS_FRAME_ERR_FRAGMENT (-7)   /* CONT with no start / data inside fragment (:964-996) */
 #define UVHTTP_WS_FRAME_ERR_MESSAGE (-8)    /* fragments exceed max_message_size (:786-791) */
 #define UVHTTP_WS_FRAME_ERR_LAYOUT (-9)     /* offset table disagrees with the frame lengths */
+#define UVHTTP_WS_FRAME_ERR_CAPACITY (-10)  /* stream decode: more frames than the desc array holds */
 
 /* Frame flags (uvhttp_ws_frame_desc_t.flags). */
 #define UVHTTP_WS_FLAG_FIN 0x01u
@@ -359,6 +360,58 @@ uint64_t uvhttp_ws_gen_frame_stride(uint64_t payload_len);
 int uvhttp_ws_gpu_gen_frames(uvhttp_ws_gpu_engine_t* eng, uint8_t* d_wire, uint32_t n_frames,
                              uint64_t payload_len, uint64_t seed, int opcode0, int fragmented,
                              int force_keys, void* stream);
+
+/* ---- batched stateful stream decode (many connections per launch) --------------------- */
+/* One entry per connection: the bytes uvhttp_ws_process_data would hold after appending the
+ * new read (recv_buffer[0, recv_buffer_pos) followed by the read), placed at wire[begin,
+ * begin + len), plus the connection state the decoder reads.  Streams must be ordered by
+ * `begin` and must not overlap.  Frame boundaries are found on the device (one lane walks
+ * each connection's headers), so no offset table is needed. */
+typedef struct {
+    uint64_t begin;             /* offset of the connection's bytes in the batch wire */
+    uint64_t len;               /* recv_buffer_pos + new bytes */
+    uint64_t recv_buffer_size;  /* conn->recv_buffer_size before the call */
+    uint64_t pending_bytes;     /* conn->fragmented_size if conn->fragmented_message, else 0 */
+    int32_t pending_opcode;     /* conn->fragmented_opcode */
+    int32_t max_frame_size;     /* conn->config.max_frame_size */
+    int32_t max_message_size;   /* conn->config.max_message_size */
+    int32_t is_server;          /* conn->is_server */
+} uvhttp_ws_stream_t;
+
+/* Per-connection outcome: exactly what uvhttp_ws_process_data(conn, bytes, len) returns and
+ * leaves behind (src/uvhttp_websocket.c:825-1097). */
+typedef struct {
+    uint32_t first_frame;        /* this connection's frames start at desc[first_frame] */
+    uint32_t n_frames;           /* frames found: delivered + (if it failed) the failing one */
+    uint32_t n_delivered;
+    int32_t status;              /* process_data's return: UVHTTP_OK or ..._INVALID_PARAM */
+    int32_t first_status;        /* UVHTTP_WS_FRAME_* of the failing frame (0 if none) */
+    uint32_t reserved;
+    uint64_t consumed_bytes;     /* complete frames drained from the front of the buffer */
+    uint64_t recv_buffer_size;   /* after the call (the buffer may have grown) */
+    uint64_t pending_bytes;      /* open fragmented message after the call (0 = none) */
+} uvhttp_ws_stream_result_t;
+
+/* Decode every connection's frames in one set of launches, in place (delivered payloads
+ * unmasked inside wire).  d_desc has room for max_frames; if the streams hold more frames
+ * every result reports UVHTTP_WS_FRAME_ERR_CAPACITY and nothing is unmasked. */
+int uvhttp_ws_gpu_decode_streams(uvhttp_ws_gpu_engine_t* eng, uint8_t* d_wire, uint64_t wire_len,
+                                 const uvhttp_ws_stream_t* d_streams, uint32_t n_streams,
+                                 uint32_t max_frames, uvhttp_ws_frame_desc_t* d_desc,
+                                 uvhttp_ws_stream_result_t* d_results, void* stream);
+
+/* Host side of the stream decode.  stream_init fills a descriptor from a live connection
+ * (the caller copies recv_buffer[0, recv_buffer_pos) and the new read to wire[begin, ...));
+ * deliver_stream then applies a decoded result to the connection exactly as process_data
+ * would have: recv buffer growth, on_message / on_close / control hooks for the delivered
+ * frames (fragments reassembled in conn->fragmented_message), and the undelivered tail kept
+ * in recv_buffer.  `wire` and `desc` are host copies of the decoded batch. */
+void uvhttp_ws_stream_init(const struct uvhttp_ws_connection* conn, uint64_t begin,
+                           uint64_t len, uvhttp_ws_stream_t* out);
+uvhttp_error_t uvhttp_ws_deliver_stream(struct uvhttp_ws_connection* conn, const uint8_t* wire,
+                                        const uvhttp_ws_frame_desc_t* desc,
+                                        const uvhttp_ws_stream_t* s,
+                                        const uvhttp_ws_stream_result_t* r);
 
 /* ---- host-memory pipeline (libuv read buffers in, decoded payloads out) ---------------- */
 /* A pipeline owns `depth` slots.  Each slot = a pinned host staging buffer (the caller

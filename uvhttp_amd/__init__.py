@@ -19,7 +19,8 @@ import os
 __all__ = [
     "lib", "LIB_PATH", "FrameHeader", "FrameDesc", "MessageDesc", "BatchSummary", "Batch",
     "WsConnectionStruct", "parse_frame_header", "apply_mask", "WsConnection", "GpuEngine",
-    "GpuError", "OPCODES", "FRAME_STATUS", "gen_frame_stride", "GpuPipeline",
+    "GpuError", "OPCODES", "FRAME_STATUS", "gen_frame_stride", "GpuPipeline", "Stream",
+    "StreamResult",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -29,7 +30,7 @@ OPCODES = dict(CONTINUATION=0x0, TEXT=0x1, BINARY=0x2, CLOSE=0x8, PING=0x9, PONG
 FRAME_STATUS = {
     0: "OK", 1: "INCOMPLETE", 2: "SKIPPED", -1: "ERR_PARSE", -2: "ERR_RSV", -3: "ERR_CONTROL",
     -4: "ERR_UNMASKED", -5: "ERR_TOO_BIG", -6: "ERR_BUFFER", -7: "ERR_FRAGMENT",
-    -8: "ERR_MESSAGE", -9: "ERR_LAYOUT",
+    -8: "ERR_MESSAGE", -9: "ERR_LAYOUT", -10: "ERR_CAPACITY",
 }
 FLAG_FIN, FLAG_MASK, FLAG_MSG_END = 0x01, 0x02, 0x20
 
@@ -65,6 +66,25 @@ class BatchSummary(C.Structure):
                 ("payload_bytes", C.c_uint64), ("n_messages", C.c_uint32),
                 ("state_closed", C.c_uint32), ("arena_bytes", C.c_uint64),
                 ("pending_bytes", C.c_uint64)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class Stream(C.Structure):
+    """uvhttp_ws_stream_t (48 B)."""
+    _fields_ = [("begin", C.c_uint64), ("len", C.c_uint64), ("recv_buffer_size", C.c_uint64),
+                ("pending_bytes", C.c_uint64), ("pending_opcode", C.c_int32),
+                ("max_frame_size", C.c_int32), ("max_message_size", C.c_int32),
+                ("is_server", C.c_int32)]
+
+
+class StreamResult(C.Structure):
+    """uvhttp_ws_stream_result_t (48 B)."""
+    _fields_ = [("first_frame", C.c_uint32), ("n_frames", C.c_uint32),
+                ("n_delivered", C.c_uint32), ("status", C.c_int32), ("first_status", C.c_int32),
+                ("reserved", C.c_uint32), ("consumed_bytes", C.c_uint64),
+                ("recv_buffer_size", C.c_uint64), ("pending_bytes", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -173,6 +193,11 @@ def lib() -> C.CDLL:
                                                     i32]),
         "uvhttp_ws_gpu_pipeline_wait": (C.c_int, [vp, C.c_int, C.POINTER(vp), C.POINTER(vp)]),
         "uvhttp_ws_deliver_batch": (C.c_int, [C.POINTER(WsConnectionStruct), vp, vp, vp]),
+        "uvhttp_ws_gpu_decode_streams": (C.c_int, [vp, vp, u64, vp, u32, u32, vp, vp, vp]),
+        "uvhttp_ws_stream_init": (None, [C.POINTER(WsConnectionStruct), u64, u64,
+                                         C.POINTER(Stream)]),
+        "uvhttp_ws_deliver_stream": (C.c_int, [C.POINTER(WsConnectionStruct), vp, vp,
+                                               C.POINTER(Stream), C.POINTER(StreamResult)]),
         "uvhttp_ws_gpu_gen_frames": (C.c_int, [vp, vp, u32, u64, u64, C.c_int, C.c_int, C.c_int,
                                                vp]),
     }
@@ -382,6 +407,30 @@ class GpuEngine:
             C.c_void_p(desc.data_ptr()), C.c_void_p(msgs.data_ptr()),
             C.c_void_p(summary.data_ptr()), self._stream(stream)), "decode_compact")
         return desc, msgs, summary
+
+    def decode_streams(self, wire, streams_dev, n_streams, max_frames, desc=None, results=None,
+                       wire_len=None, stream=None):
+        """uvhttp_ws_gpu_decode_streams; streams_dev = device uint8 tensor of n_streams
+        uvhttp_ws_stream_t records.  Returns (desc, results) device tensors."""
+        t = self.torch
+        dev = f"cuda:{self.device}"
+        if desc is None:
+            desc = t.empty(max(1, max_frames) * 32, dtype=t.uint8, device=dev)
+        if results is None:
+            results = t.zeros(max(1, n_streams) * C.sizeof(StreamResult), dtype=t.uint8,
+                              device=dev)
+        self._check(self._L.uvhttp_ws_gpu_decode_streams(
+            self.h, C.c_void_p(wire.data_ptr()), wire.numel() if wire_len is None else wire_len,
+            C.c_void_p(streams_dev.data_ptr()), n_streams, max_frames,
+            C.c_void_p(desc.data_ptr()), C.c_void_p(results.data_ptr()), self._stream(stream)),
+            "decode_streams")
+        return desc, results
+
+    @staticmethod
+    def read_stream_results(results, n):
+        raw = bytes(results[: n * C.sizeof(StreamResult)].cpu().numpy().tobytes())
+        sz = C.sizeof(StreamResult)
+        return [StreamResult.from_buffer_copy(raw, k * sz) for k in range(n)]
 
     def apply_mask(self, data, key, length=None, offset=0, stream=None):
         kb = (C.c_uint8 * 4).from_buffer_copy(bytes(key))

@@ -49,7 +49,7 @@ struct ScanElem {
     uint32_t seg_flag;   // segment contains a start
     uint32_t n_fin;      // sum: data frames with FIN (completed messages)
     uint32_t n_close;    // sum: CLOSE frames
-    uint32_t pad;
+    uint32_t head;       // segment (connection) start: the scan restarts here
 };
 
 __device__ __host__ inline ScanElem scan_identity() {
@@ -62,11 +62,13 @@ __device__ __host__ inline ScanElem scan_identity() {
     e.seg_flag = 0;
     e.n_fin = 0;
     e.n_close = 0;
-    e.pad = 0;
+    e.head = 0;
     return e;
 }
 
+// segmented: a connection start in b discards everything before it
 __device__ __host__ inline ScanElem scan_combine(const ScanElem& a, const ScanElem& b) {
+    if (b.head) return b;
     ScanElem r;
     r.last_data = a.last_data > b.last_data ? a.last_data : b.last_data;
     r.last_start = a.last_start > b.last_start ? a.last_start : b.last_start;
@@ -76,7 +78,7 @@ __device__ __host__ inline ScanElem scan_combine(const ScanElem& a, const ScanEl
     r.seg_flag = a.seg_flag | b.seg_flag;
     r.n_fin = a.n_fin + b.n_fin;
     r.n_close = a.n_close + b.n_close;
-    r.pad = 0;
+    r.head = a.head;
     return r;
 }
 
@@ -84,8 +86,9 @@ __device__ inline bool is_data_op(uint32_t op) { return op <= 2u; }
 
 // element of frame i, rebuilt from its descriptor (local status must be OK for the
 // state machine to consider it; invalid frames never precede a delivered frame)
-__device__ inline ScanElem scan_elem_of(const uvhttp_ws_frame_desc_t& d, int32_t i) {
+__device__ inline ScanElem scan_elem_of(const uvhttp_ws_frame_desc_t& d, int32_t i, bool head) {
     ScanElem e = scan_identity();
+    e.head = head ? 1u : 0u;
     const uint32_t op = d.opcode;
     e.all_pay = d.payload_len;
     if (is_data_op(op)) {
@@ -113,7 +116,7 @@ __device__ inline ScanElem shfl_up_elem(const ScanElem& e, int delta) {
     r.seg_flag = __shfl_up(e.seg_flag, delta, 64);
     r.n_fin = __shfl_up(e.n_fin, delta, 64);
     r.n_close = __shfl_up(e.n_close, delta, 64);
-    r.pad = 0;
+    r.head = __shfl_up(e.head, delta, 64);
     return r;
 }
 
@@ -156,6 +159,16 @@ struct Workspace {
     uint32_t* arena_first; // [n_arena_tiles]
 };
 
+// extra scratch of the stream decode (one allocation per engine, grown on demand)
+struct StreamScratch {
+    uint64_t* frame_off;   // [max_frames] frame starts found by the walk
+    uint32_t* frame_seg;   // [max_frames] connection of each frame
+    uint64_t* open_after;  // [max_frames] open fragmented bytes after the frame
+    uint32_t* seg_bad;     // [n_streams] first undelivered frame of each connection
+    uint32_t* walk_agg;    // [stream blocks + 1] frame counts per block, then prefixes
+    uint32_t* n_total;     // [1] frames found (device-side frame count)
+};
+
 struct BatchArgs {
     uint8_t* wire;
     uint64_t wire_len;
@@ -169,10 +182,57 @@ struct BatchArgs {
     uint8_t* arena;          // compact mode (nullptr: in-place)
     uint64_t arena_cap;
     uint64_t n_arena_tiles;
+    // stream mode (streams != nullptr): frames come from the walk, n is the capacity and the
+    // real count is *n_dev; limits and initial fragment state are per connection
+    const uvhttp_ws_stream_t* streams;
+    const uint32_t* frame_seg;
+    const uint32_t* n_dev;
+    uint64_t* open_after;
+    uint32_t* seg_bad;
 };
 
 __device__ inline uint64_t frame_start(const BatchArgs& a, uint32_t i) {
     return a.frame_off ? a.frame_off[i] : (uint64_t)i * a.frame_stride;
+}
+
+__device__ inline uint32_t nframes(const BatchArgs& a) { return a.n_dev ? *a.n_dev : a.n; }
+
+// what frame i needs to know about its connection (batch mode: one implicit connection)
+struct SegInfo {
+    uint32_t seg;
+    bool head, last;         // first / last frame of its connection
+    uint64_t end;            // end of the bytes this frame may use
+    int32_t max_frame_size, max_message_size, is_server;
+    uint64_t init_pending;   // open fragmented message when the call starts
+    int32_t init_opcode;
+};
+
+__device__ inline SegInfo seg_info(const BatchArgs& a, uint32_t i, uint32_t n) {
+    SegInfo g;
+    if (a.streams) {
+        g.seg = a.frame_seg[i];
+        g.head = (i == 0) || a.frame_seg[i - 1] != g.seg;
+        g.last = (i + 1 == n) || a.frame_seg[i + 1] != g.seg;
+        const uvhttp_ws_stream_t st = a.streams[g.seg];
+        g.end = g.last ? st.begin + st.len : frame_start(a, i + 1);
+        g.max_frame_size = st.max_frame_size;
+        g.max_message_size = st.max_message_size;
+        g.is_server = st.is_server;
+        g.init_pending = st.pending_bytes;
+        g.init_opcode = st.pending_opcode;
+    } else {
+        g.seg = 0;
+        g.head = (i == 0);
+        g.last = (i + 1 == n);
+        g.end = g.last ? a.wire_len : frame_start(a, i + 1);
+        g.max_frame_size = a.max_frame_size;
+        g.max_message_size = a.max_message_size;
+        g.is_server = a.is_server;
+        g.init_pending = 0;
+        g.init_opcode = 0;
+    }
+    if (g.end > a.wire_len) g.end = a.wire_len;
+    return g;
 }
 
 __device__ inline uint32_t rotr32(uint32_t x, uint32_t s) {
@@ -187,18 +247,18 @@ __device__ inline uint32_t rotr32(uint32_t x, uint32_t s) {
 __global__ __launch_bounds__(kBlock) void k_parse(BatchArgs a, uvhttp_ws_frame_desc_t* desc,
                                                   Workspace ws) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *ws.first_bad = a.n;
+    const uint32_t n = nframes(a);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *ws.first_bad = n;
     ScanElem elem = scan_identity();
-    if (i < a.n) {
+    if (i < n) {
+        const SegInfo g = seg_info(a, i, n);
         const uint64_t o = frame_start(a, i);
-        uint64_t end = (i + 1 < a.n) ? frame_start(a, i + 1) : a.wire_len;
-        if (end > a.wire_len) end = a.wire_len;
-        const uint64_t slot = end > o ? end - o : 0;
-        const bool last = (i + 1 == a.n);
+        const uint64_t slot = g.end > o ? g.end - o : 0;
+        const bool last = g.last;
         const uint8_t* p = a.wire + o;
 
         uvhttp_ws_frame_desc_t d;
-        d.payload_off = 0;
+        d.payload_off = o;  // frames that do not parse keep a monotonic (empty) payload
         d.payload_len = 0;
         d.masking_key = 0;
         d.message = 0;
@@ -246,32 +306,33 @@ __global__ __launch_bounds__(kBlock) void k_parse(BatchArgs a, uvhttp_ws_frame_d
 
         int st = UVHTTP_WS_FRAME_OK;
         uint64_t fed;
-        if (!last && (!parsable || (!msb && wlen != slot))) {
-            st = UVHTTP_WS_FRAME_ERR_LAYOUT;
+        if (!a.streams && !last && (!parsable || (!msb && wlen != slot))) {
+            st = UVHTTP_WS_FRAME_ERR_LAYOUT;  // batch mode only: streams are walked
             fed = slot;
         } else {
             fed = (last && parsable && !msb && wlen < slot) ? wlen : slot;
         }
         if (st == UVHTTP_WS_FRAME_OK) {
-            // recv buffer cap (:851-857): an empty buffer grows to max(max_frame, 64 KiB)
-            const uint64_t mf = (uint64_t)(int64_t)a.max_frame_size;
+            // recv buffer cap (:851-857): an empty buffer grows to max(max_frame, 64 KiB);
+            // a stream decode checks it once per connection in k_walk instead
+            const uint64_t mf = (uint64_t)(int64_t)g.max_frame_size;
             const uint64_t cap = mf > 65536u ? mf : 65536u;
-            if (fed > cap) st = UVHTTP_WS_FRAME_ERR_BUFFER;
+            if (!a.streams && fed > cap) st = UVHTTP_WS_FRAME_ERR_BUFFER;
             else if (!parsable) st = UVHTTP_WS_FRAME_INCOMPLETE;
             else if (msb) st = UVHTTP_WS_FRAME_ERR_PARSE;
             else if (d.flags & (UVHTTP_WS_FLAG_RSV1 | UVHTTP_WS_FLAG_RSV2 | UVHTTP_WS_FLAG_RSV3))
                 st = UVHTTP_WS_FRAME_ERR_RSV;
             else if (d.opcode >= 8 && (plen > 125 || !(d.flags & UVHTTP_WS_FLAG_FIN)))
                 st = UVHTTP_WS_FRAME_ERR_CONTROL;
-            else if (a.is_server && !(d.flags & UVHTTP_WS_FLAG_MASK))
+            else if (g.is_server && !(d.flags & UVHTTP_WS_FLAG_MASK))
                 st = UVHTTP_WS_FRAME_ERR_UNMASKED;
             else if (plen > mf) st = UVHTTP_WS_FRAME_ERR_TOO_BIG;
             else if (fed < wlen) st = UVHTTP_WS_FRAME_INCOMPLETE;
         }
         d.status = (int8_t)st;
         desc[i] = d;
-        if (st == UVHTTP_WS_FRAME_OK) elem = scan_elem_of(d, (int32_t)i);
-
+        if (st == UVHTTP_WS_FRAME_OK) elem = scan_elem_of(d, (int32_t)i, g.head);
+        elem.head = g.head ? 1u : 0u;
     }
     // reset the tile -> first-frame maps (k_resolve fills them with atomicMin)
     const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -301,59 +362,72 @@ __global__ __launch_bounds__(kBlock) void k_scan(Workspace ws, uint32_t n_blocks
     if (threadIdx.x == 0) ws.block_agg[n_blocks] = total;
 }
 
-// k_resolve: one lane per frame.  With E = scan over frames [0, i), the state before data
-// frame i follows from the latest data frame p alone (all frames before a delivered frame
-// are valid): PENDING iff p exists, p has FIN=0, and p is not a zero-length start (a
-// zero-length first fragment allocates nothing, so fragmented_message stays NULL,
-// src/uvhttp_websocket.c:794-816 + :964).
+// k_resolve: one lane per frame.  With E = scan over the frames of the same connection
+// before i, the state before frame i follows from the latest data frame p alone (all
+// frames before a delivered frame are valid): PENDING iff p exists, p has FIN=0, and p is
+// not a zero-length start (a zero-length first fragment allocates nothing, so
+// fragmented_message stays NULL, src/uvhttp_websocket.c:794-816 + :964).  With no data
+// frame before i in its connection, the state is the connection's initial one.
 __global__ __launch_bounds__(kBlock) void k_resolve(BatchArgs a, uvhttp_ws_frame_desc_t* desc,
                                                     uvhttp_ws_message_desc_t* msgs,
                                                     Workspace ws) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t n = nframes(a);
     ScanElem elem = scan_identity();
     uvhttp_ws_frame_desc_t d;
-    if (i < a.n) {
+    SegInfo g;
+    if (i < n) {
         d = desc[i];
-        if (d.status == UVHTTP_WS_FRAME_OK) elem = scan_elem_of(d, (int32_t)i);
+        g = seg_info(a, i, n);
+        if (d.status == UVHTTP_WS_FRAME_OK) elem = scan_elem_of(d, (int32_t)i, g.head);
+        elem.head = g.head ? 1u : 0u;
     }
     ScanElem total;
     ScanElem ex = block_exclusive_scan(elem, &total);
-    if (i >= a.n) return;
+    if (i >= n) return;
     ex = scan_combine(ws.block_agg[blockIdx.x], ex);
+    if (g.head) ex = scan_identity();  // nothing of this connection precedes its first frame
 
-    // in-place tiles whose start byte lies in this frame's slot (frame 0 also owns the
-    // bytes before its start); atomicMin keeps the map deterministic even when a bad
-    // offset table makes slots overlap
+    // in-place tiles whose start byte lies in this frame's span up to the next frame (frame
+    // 0 also owns the bytes before its start); atomicMin keeps the map deterministic even
+    // when a bad offset table makes slots overlap
     {
         const uint64_t o = frame_start(a, i);
-        uint64_t end = (i + 1 < a.n) ? frame_start(a, i + 1) : a.wire_len;
+        uint64_t end = (i + 1 < n) ? frame_start(a, i + 1) : a.wire_len;
         if (end > a.wire_len) end = a.wire_len;
         const uint64_t lo = (i == 0) ? 0 : o;
         for (uint64_t t = (lo + kMapTile - 1) / kMapTile; t * kMapTile < end && t < a.n_tiles; ++t)
             atomicMin(&ws.tile_first[t], i);
     }
 
+    // fragment state before this frame
+    bool pending;
+    if (ex.last_data >= 0) {
+        const uvhttp_ws_frame_desc_t pd = desc[ex.last_data];
+        const bool p_start = pd.opcode != 0;
+        pending = !(pd.flags & UVHTTP_WS_FLAG_FIN) && !(p_start && pd.payload_len == 0);
+    } else {
+        pending = g.init_pending > 0;
+    }
+    // bytes of the open message so far (the connection's carried part when no start yet)
+    const uint64_t acc = ex.seg_flag ? ex.seg_pay : g.init_pending + ex.seg_pay;
+    uint64_t open_after = pending ? acc : 0;
+
     int st = d.status;
     if (st == UVHTTP_WS_FRAME_OK && is_data_op(d.opcode)) {
-        bool pending = false;
-        if (ex.last_data >= 0) {
-            const uvhttp_ws_frame_desc_t pd = desc[ex.last_data];
-            const bool p_start = pd.opcode != 0;
-            pending = !(pd.flags & UVHTTP_WS_FLAG_FIN) && !(p_start && pd.payload_len == 0);
-        }
-        const uint64_t lim = (uint64_t)(int64_t)a.max_message_size;
+        const uint64_t lim = (uint64_t)(int64_t)g.max_message_size;
         const bool is_cont = d.opcode == 0;
         const bool fin = d.flags & UVHTTP_WS_FLAG_FIN;
         if (!pending) {
             if (is_cont) st = UVHTTP_WS_FRAME_ERR_FRAGMENT;
             else if (!fin && lim != 0 && d.payload_len > lim) st = UVHTTP_WS_FRAME_ERR_MESSAGE;
         } else {
-            const uint64_t acc = ex.seg_pay;  // bytes of the open message so far
             if (!is_cont) st = UVHTTP_WS_FRAME_ERR_FRAGMENT;
             else if (lim != 0 && (acc > lim || d.payload_len > lim - acc))
                 st = UVHTTP_WS_FRAME_ERR_MESSAGE;
         }
         if (st == UVHTTP_WS_FRAME_OK) {
+            open_after = fin ? 0 : (pending ? acc + d.payload_len : d.payload_len);
             d.message = ex.n_fin;
             if (a.arena) d.payload_off = ex.data_pay;
             if (fin) {
@@ -383,7 +457,11 @@ __global__ __launch_bounds__(kBlock) void k_resolve(BatchArgs a, uvhttp_ws_frame
         desc[i].payload_off = d.payload_off;
         desc[i].flags = d.flags;
     }
-    if (st != UVHTTP_WS_FRAME_OK) atomicMin(ws.first_bad, i);
+    if (a.open_after) a.open_after[i] = open_after;
+    if (st != UVHTTP_WS_FRAME_OK) {
+        if (a.seg_bad) atomicMin(&a.seg_bad[g.seg], i);
+        else atomicMin(ws.first_bad, i);
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -455,9 +533,10 @@ __global__ __launch_bounds__(BLOCK) void k_unmask_inplace(
         data[v] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.wire + la));
     }
 
-    const uint32_t nb = *ws.first_bad;  // frames >= nb are not delivered
-    if (nb == 0 || a.n == 0) return;
-    const uint32_t last = (nb < a.n ? nb : a.n) - 1;
+    const uint32_t n = nframes(a);
+    const uint32_t nb = *ws.first_bad;  // batch mode: frames >= nb are not delivered
+    if (nb == 0 || n == 0) return;
+    const uint32_t last = (nb < n ? nb : n) - 1;
     // frames overlapping [t0, t0 + kT): from the first frame of the coarse map tile holding
     // t0 to the first frame of the coarse tile after the one holding the tile's last byte
     const uint64_t c0 = t0 / kMapTile, c1 = (t0 + kT - 1) / kMapTile + 1;
@@ -474,6 +553,7 @@ __global__ __launch_bounds__(BLOCK) void k_unmask_inplace(
         // fast path (frames of ~8 KiB and up): at most two frames touch the tile; their
         // descriptors are uniform scalar loads
         for (uint32_t f = f0; f <= f1; ++f) {
+            if (desc[f].status != UVHTTP_WS_FRAME_OK) continue;  // undelivered (stream mode)
             const uint64_t ps = desc[f].payload_off;
             const uint64_t pe = ps + desc[f].payload_len;
             const uint32_t key = desc[f].masking_key;
@@ -488,8 +568,9 @@ __global__ __launch_bounds__(BLOCK) void k_unmask_inplace(
             __syncthreads();
             if (threadIdx.x < cnt) {
                 const uvhttp_ws_frame_desc_t d = desc[base + threadIdx.x];
+                const bool ok = d.status == UVHTTP_WS_FRAME_OK;  // undelivered: empty range
                 s_ps[threadIdx.x] = d.payload_off;
-                s_pe[threadIdx.x] = d.payload_off + d.payload_len;
+                s_pe[threadIdx.x] = d.payload_off + (ok ? d.payload_len : 0);
                 s_key[threadIdx.x] = d.masking_key;
             }
             __syncthreads();
@@ -590,9 +671,10 @@ __global__ __launch_bounds__(BLOCK) void k_gather_compact(
     __shared__ uint32_t s_key[BLOCK];
 
     const uint64_t t0 = (tile_base + blockIdx.x) * kT;
+    const uint32_t n = nframes(a);
     const uint32_t nb = *ws.first_bad;
-    if (nb == 0 || a.n == 0) return;
-    const uint32_t last = (nb < a.n ? nb : a.n) - 1;
+    if (nb == 0 || n == 0) return;
+    const uint32_t last = (nb < n ? nb : n) - 1;
     const uint64_t c0 = t0 / kMapTile, c1 = (t0 + kT - 1) / kMapTile + 1;
     const uint32_t f0 = ws.arena_first[c0];
     if (f0 > last) return;
@@ -713,7 +795,7 @@ __global__ __launch_bounds__(kBlock) void k_finalize(BatchArgs a, uvhttp_ws_fram
         const uint32_t b = nb / kBlock;
         const uint32_t f = b * kBlock + threadIdx.x;
         ScanElem el = scan_identity();
-        if (f < nb) el = scan_elem_of(desc[f], (int32_t)f);
+        if (f < nb) el = scan_elem_of(desc[f], (int32_t)f, f == 0);
         ScanElem part;
         (void)block_exclusive_scan(el, &part);
         e = scan_combine(ws.block_agg[b], part);
@@ -744,6 +826,184 @@ __global__ __launch_bounds__(kBlock) void k_finalize(BatchArgs a, uvhttp_ws_fram
     }
     s.pending_bytes = pend;
     *summary = s;
+}
+
+// ------------------------------------------------------------------------------------
+// stream decode: frame discovery.  One lane per connection walks its buffered bytes header
+// by header exactly as process_data's loop does (:872-932) and stops where process_data
+// stops: fewer bytes than a header needs, a frame process_data rejects before unmasking
+// (counted: it is the failing frame), or an incomplete frame (not counted: it stays in the
+// buffer).  Pass 1 counts frames; pass 2 (after a scan of the counts) writes the offsets.
+// The recv-buffer growth check (:832-866) runs once per connection on all its bytes.
+// ------------------------------------------------------------------------------------
+struct WalkArgs {
+    const uint8_t* wire;
+    uint64_t wire_len;
+    const uvhttp_ws_stream_t* streams;
+    uint32_t n_streams;
+    uint32_t max_frames;
+    uvhttp_ws_stream_result_t* results;
+    StreamScratch sc;
+};
+
+// process_data's buffer growth: returns false on failure, else the size after the call
+__device__ inline bool grow_recv(uint64_t have, uint64_t size, int32_t max_frame, uint64_t* out) {
+    *out = size;
+    if (have <= size) return true;
+    uint64_t ns = size;
+    if (ns > (~0ull) / 2) return false;
+    ns *= 2;
+    while (have > ns) {
+        if (ns > (~0ull) / 2) return false;
+        ns *= 2;
+    }
+    const uint64_t ceiling = (uint64_t)(int64_t)max_frame;
+    if (ns > ceiling) {
+        ns = ceiling;
+        if (have > ns) return false;
+    }
+    *out = ns;
+    return true;
+}
+
+template <bool WRITE>
+__device__ inline uint32_t walk_stream(const WalkArgs& w, uint32_t s, uint32_t first) {
+    const uvhttp_ws_stream_t st = w.streams[s];
+    const uint8_t* p = w.wire + st.begin;
+    const uint64_t L = st.begin + st.len <= w.wire_len ? st.len : 0;
+    uint64_t grown;
+    if (!grow_recv(L, st.recv_buffer_size, st.max_frame_size, &grown)) return 0;
+    const uint64_t mf = (uint64_t)(int64_t)st.max_frame_size;
+    uint32_t count = 0;
+    uint64_t pos = 0;
+    while (L - pos >= 2) {
+        const uint32_t b0 = p[pos], b1 = p[pos + 1];
+        const uint32_t code = b1 & 0x7F;
+        const uint32_t need = code == 126 ? 4 : code == 127 ? 10 : 2;
+        if (L - pos < need) break;
+        uint64_t plen = code;
+        if (need > 2) {
+            plen = 0;
+            for (uint32_t k = 2; k < need; ++k) plen = (plen << 8) | p[pos + k];
+        }
+        const bool bad = (need == 10 && (plen >> 63)) || (b0 & 0x70) ||
+                         ((b0 & 0x0F) >= 8 && (plen > 125 || !(b0 & 0x80))) ||
+                         (st.is_server && !(b1 & 0x80)) || plen > mf;
+        const uint64_t wl = need + ((b1 & 0x80) ? 4u : 0u) + plen;
+        if (!bad && L - pos < wl) break;  // incomplete: waits for more bytes
+        if (WRITE && first + count < w.max_frames) {
+            w.sc.frame_off[first + count] = st.begin + pos;
+            w.sc.frame_seg[first + count] = s;
+        }
+        ++count;
+        if (bad) break;  // process_data returns at this frame
+        pos += wl;
+    }
+    return count;
+}
+
+__device__ inline uint32_t block_exclusive_sum_u32(uint32_t v, uint32_t* total) {
+    __shared__ uint32_t wsum[kBlock / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t inc = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += o;
+    }
+    if (lane == 63) wsum[wave] = inc;
+    __syncthreads();
+    uint32_t pre = 0, all = 0;
+    for (int k = 0; k < kBlock / 64; ++k) {
+        if (k < wave) pre += wsum[k];
+        all += wsum[k];
+    }
+    __syncthreads();
+    *total = all;
+    return pre + inc - v;
+}
+
+__global__ __launch_bounds__(kBlock) void k_walk_count(WalkArgs w) {
+    const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t c = s < w.n_streams ? walk_stream<false>(w, s, 0) : 0;
+    if (s < w.n_streams) w.results[s].n_frames = c;
+    uint32_t total;
+    (void)block_exclusive_sum_u32(c, &total);
+    if (threadIdx.x == 0) w.sc.walk_agg[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kBlock) void k_walk_scan(WalkArgs w, uint32_t n_blocks) {
+    const uint32_t per = (n_blocks + kBlock - 1) / kBlock;
+    const uint32_t beg = threadIdx.x * per;
+    const uint32_t fin = beg + per < n_blocks ? beg + per : n_blocks;
+    uint32_t run = 0;
+    for (uint32_t b = beg; b < fin; ++b) run += w.sc.walk_agg[b];
+    uint32_t total;
+    uint32_t pre = block_exclusive_sum_u32(run, &total);
+    for (uint32_t b = beg; b < fin; ++b) {
+        const uint32_t v = w.sc.walk_agg[b];
+        w.sc.walk_agg[b] = pre;
+        pre += v;
+    }
+    if (threadIdx.x == 0) *w.sc.n_total = total <= w.max_frames ? total : 0;
+}
+
+__global__ __launch_bounds__(kBlock) void k_walk_write(WalkArgs w) {
+    const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t c = s < w.n_streams ? w.results[s].n_frames : 0;
+    uint32_t total;
+    const uint32_t first = w.sc.walk_agg[blockIdx.x] + block_exclusive_sum_u32(c, &total);
+    if (s >= w.n_streams) return;
+    const bool fits = *w.sc.n_total != 0 || c == 0;  // n_total 0 with frames = overflow
+    uvhttp_ws_stream_result_t r;
+    const uvhttp_ws_stream_t st = w.streams[s];
+    uint64_t grown;
+    const uint64_t L = st.begin + st.len <= w.wire_len ? st.len : 0;
+    const bool grow_ok = grow_recv(L, st.recv_buffer_size, st.max_frame_size, &grown);
+    r.first_frame = first;
+    r.n_frames = c;
+    r.n_delivered = 0;
+    r.status = grow_ok ? 0 : -1;
+    r.first_status = grow_ok ? 0 : UVHTTP_WS_FRAME_ERR_BUFFER;
+    r.reserved = 0;
+    r.consumed_bytes = 0;
+    r.recv_buffer_size = grow_ok ? grown : st.recv_buffer_size;
+    r.pending_bytes = st.pending_bytes;
+    if (!fits) {
+        r.status = -1;
+        r.first_status = UVHTTP_WS_FRAME_ERR_CAPACITY;
+        r.n_frames = 0;
+    } else if (c) {
+        (void)walk_stream<true>(w, s, first);
+    }
+    w.sc.seg_bad[s] = first + (fits ? c : 0);
+    w.results[s] = r;
+}
+
+// k_stream_mark: after the state machine.  Frames past their connection's first failure
+// become SKIPPED (so the payload pass leaves them masked); per-connection results.
+__global__ __launch_bounds__(kBlock) void k_stream_mark(BatchArgs a, uvhttp_ws_frame_desc_t* desc,
+                                                        uvhttp_ws_stream_result_t* results,
+                                                        uint32_t n_streams) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t n = nframes(a);
+    if (i < n && i > a.seg_bad[a.frame_seg[i]]) desc[i].status = UVHTTP_WS_FRAME_SKIPPED;
+    if (i >= n_streams) return;
+    uvhttp_ws_stream_result_t r = results[i];
+    if (r.first_status != 0) return;  // buffer growth or capacity failure: nothing decoded
+    const uint32_t bad = a.seg_bad[i];
+    const uint32_t delivered = bad - r.first_frame;
+    r.n_delivered = delivered;
+    if (delivered < r.n_frames) {
+        r.first_status = desc[bad].status;
+        r.status = r.first_status < 0 ? -1 : 0;
+    }
+    if (delivered) {
+        const uint32_t lastf = r.first_frame + delivered - 1;
+        r.consumed_bytes = frame_start(a, lastf) + desc[lastf].wire_len - a.streams[i].begin;
+        r.pending_bytes = a.open_after[lastf];
+    }
+    results[i] = r;
 }
 
 // plain unmask of one buffer with one key (uvhttp_ws_apply_mask over device memory)
@@ -834,6 +1094,9 @@ struct uvhttp_ws_gpu_engine {
     Workspace ws;
     int timing;
     int tile_block, tile_vpt;  // payload kernel shape, 0 = automatic
+    void* ss_mem;              // stream-decode scratch
+    uint32_t ss_frames, ss_streams;
+    StreamScratch ss;
     hipEvent_t ev[2 * 1024];
     int ev_created;
     int ev_used;       // event pairs recorded and not yet harvested
@@ -877,6 +1140,7 @@ void uvhttp_ws_gpu_engine_free(uvhttp_ws_gpu_engine_t* e) {
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(e->device);
     if (e->ws_mem) (void)hipFree(e->ws_mem);
+    if (e->ss_mem) (void)hipFree(e->ss_mem);
     for (int k = 0; k < e->ev_created; ++k) (void)hipEventDestroy(e->ev[k]);
     (void)hipSetDevice(prev);
     free(e);
@@ -1025,6 +1289,7 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
     hipStream_t s = (hipStream_t)stream;
 
     BatchArgs a;
+    memset(&a, 0, sizeof(a));  // stream-mode fields stay null in batch mode
     a.wire = b->wire;
     a.wire_len = b->wire_len;
     a.frame_off = b->frame_off;
@@ -1100,6 +1365,118 @@ int uvhttp_ws_gpu_decode_compact(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batc
     if (((uintptr_t)d_arena) & 15u)
         return set_err(e, UVHTTP_WS_GPU_EINVAL, "arena must be 16-byte aligned", hipSuccess);
     return run_decode(e, b, d_arena, arena_cap, d_desc, d_msgs, d_summary, stream);
+}
+
+static int reserve_streams(uvhttp_ws_gpu_engine_t* e, uint32_t frames, uint32_t streams) {
+    if (e->ss_mem && frames <= e->ss_frames && streams <= e->ss_streams) return UVHTTP_WS_GPU_OK;
+    const uint32_t fr = frames > e->ss_frames ? frames : e->ss_frames;
+    const uint32_t sn = streams > e->ss_streams ? streams : e->ss_streams;
+    const uint64_t sblk = (sn + kBlock - 1) / kBlock + 2;
+    size_t o_off = 0;
+    size_t o_seg = align_up(o_off + (size_t)fr * 8, 256);
+    size_t o_open = align_up(o_seg + (size_t)fr * 4, 256);
+    size_t o_bad = align_up(o_open + (size_t)fr * 8, 256);
+    size_t o_agg = align_up(o_bad + (size_t)sn * 4, 256);
+    size_t o_tot = align_up(o_agg + sblk * 4, 256);
+    size_t bytes = align_up(o_tot + 16, 256);
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(e->device);
+    if (e->ss_mem) (void)hipFree(e->ss_mem);
+    e->ss_mem = nullptr;
+    const hipError_t h = hipMalloc(&e->ss_mem, bytes);
+    (void)hipSetDevice(prev);
+    if (h != hipSuccess) {
+        e->ss_frames = e->ss_streams = 0;
+        return set_err(e, UVHTTP_WS_GPU_ENOMEM, "hipMalloc stream scratch", h);
+    }
+    char* b = (char*)e->ss_mem;
+    e->ss.frame_off = (uint64_t*)(b + o_off);
+    e->ss.frame_seg = (uint32_t*)(b + o_seg);
+    e->ss.open_after = (uint64_t*)(b + o_open);
+    e->ss.seg_bad = (uint32_t*)(b + o_bad);
+    e->ss.walk_agg = (uint32_t*)(b + o_agg);
+    e->ss.n_total = (uint32_t*)(b + o_tot);
+    e->ss_frames = fr;
+    e->ss_streams = sn;
+    return UVHTTP_WS_GPU_OK;
+}
+
+int uvhttp_ws_gpu_decode_streams(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint64_t wire_len,
+                                 const uvhttp_ws_stream_t* d_streams, uint32_t n_streams,
+                                 uint32_t max_frames, uvhttp_ws_frame_desc_t* d_desc,
+                                 uvhttp_ws_stream_result_t* d_results, void* stream) {
+    if (!e || (!d_wire && wire_len) || (!d_streams && n_streams) || !d_results ||
+        (!d_desc && max_frames))
+        return UVHTTP_WS_GPU_EINVAL;
+    if (((uintptr_t)d_wire) & 15u)
+        return set_err(e, UVHTTP_WS_GPU_EINVAL, "wire must be 16-byte aligned", hipSuccess);
+    if (max_frames > kMaxFrames || n_streams > kMaxFrames)
+        return set_err(e, UVHTTP_WS_GPU_EINVAL, "too many frames/streams", hipSuccess);
+    if (!n_streams) return UVHTTP_WS_GPU_OK;
+    const uint32_t cap = max_frames ? max_frames : 1;
+    int rc = uvhttp_ws_gpu_engine_reserve(e, cap, wire_len, 0);
+    if (!rc) rc = reserve_streams(e, cap, n_streams);
+    if (rc) return rc;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    if (prev != e->device) (void)hipSetDevice(e->device);
+    hipStream_t s = (hipStream_t)stream;
+
+    WalkArgs w;
+    w.wire = d_wire;
+    w.wire_len = wire_len;
+    w.streams = d_streams;
+    w.n_streams = n_streams;
+    w.max_frames = max_frames;
+    w.results = d_results;
+    w.sc = e->ss;
+    const uint32_t nsb = (n_streams + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(k_walk_count, dim3(nsb), dim3(kBlock), 0, s, w);
+    hipLaunchKernelGGL(k_walk_scan, dim3(1), dim3(kBlock), 0, s, w, nsb);
+    hipLaunchKernelGGL(k_walk_write, dim3(nsb), dim3(kBlock), 0, s, w);
+
+    BatchArgs a;
+    memset(&a, 0, sizeof(a));
+    a.wire = d_wire;
+    a.wire_len = wire_len;
+    a.frame_off = e->ss.frame_off;
+    a.n = cap;
+    a.n_tiles = (wire_len + kMapTile - 1) / kMapTile;
+    a.streams = d_streams;
+    a.frame_seg = e->ss.frame_seg;
+    a.n_dev = e->ss.n_total;
+    a.open_after = e->ss.open_after;
+    a.seg_bad = e->ss.seg_bad;
+    const uint32_t grid_f = (cap + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(k_parse, dim3(grid_f), dim3(kBlock), 0, s, a, d_desc, e->ws);
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(kBlock), 0, s, e->ws, grid_f);
+    hipLaunchKernelGGL(k_resolve, dim3(grid_f), dim3(kBlock), 0, s, a, d_desc,
+                       (uvhttp_ws_message_desc_t*)nullptr, e->ws);
+    const uint32_t grid_m = grid_f > nsb ? grid_f : nsb;
+    hipLaunchKernelGGL(k_stream_mark, dim3(grid_m), dim3(kBlock), 0, s, a, d_desc, d_results,
+                       n_streams);
+    int blk = e->tile_block ? e->tile_block : 256, vpt = e->tile_block ? e->tile_vpt : 2;
+    const uint64_t tile_bytes = (uint64_t)blk * vpt * 16;
+    const uint64_t n_ptiles = (wire_len + tile_bytes - 1) / tile_bytes;
+    const uint64_t max_tiles = (1ull << 24);
+    const int tk = timing_begin(e, s);
+    for (uint64_t tb = 0; tb < n_ptiles; tb += max_tiles) {
+        const uint32_t grid_p = (uint32_t)((n_ptiles - tb) < max_tiles ? (n_ptiles - tb) : max_tiles);
+#define UVWS_LAUNCH(B, V)                                                                        \
+    if (blk == B && vpt == V)                                                                    \
+        hipLaunchKernelGGL((k_unmask_inplace<B, V>), dim3(grid_p), dim3(B), 0, s, a, d_desc,     \
+                           e->ws, tb);                                                           \
+    else
+        UVWS_LAUNCH(64, 1) UVWS_LAUNCH(64, 2) UVWS_LAUNCH(64, 4) UVWS_LAUNCH(128, 1)
+        UVWS_LAUNCH(128, 2) UVWS_LAUNCH(256, 1) UVWS_LAUNCH(256, 2) UVWS_LAUNCH(256, 4) {}
+#undef UVWS_LAUNCH
+    }
+    timing_end(e, tk, s);
+    const hipError_t h = hipGetLastError();
+    if (prev != e->device) (void)hipSetDevice(prev);
+    if (h != hipSuccess) return set_err(e, UVHTTP_WS_GPU_ELAUNCH, "launch", h);
+    return UVHTTP_WS_GPU_OK;
 }
 
 int uvhttp_ws_gpu_apply_mask(uvhttp_ws_gpu_engine_t* e, uint8_t* d_data, uint64_t len,

@@ -343,3 +343,54 @@ uvhttp_error_t uvhttp_ws_deliver_batch(struct uvhttp_ws_connection* c, const uin
     }
     return summary->status == 0 ? UVHTTP_OK : UVHTTP_ERROR_INVALID_PARAM;
 }
+
+/* ---- stream decode, host side (include/uvhttp_ws_amd.h) ---------------------------------- */
+
+void uvhttp_ws_stream_init(const struct uvhttp_ws_connection* c, uint64_t begin, uint64_t len,
+                           uvhttp_ws_stream_t* out) {
+    if (c == NULL || out == NULL) return;
+    memset(out, 0, sizeof(*out));
+    out->begin = begin;
+    out->len = len;
+    out->recv_buffer_size = c->recv_buffer_size;
+    out->pending_bytes = c->fragmented_message != NULL ? c->fragmented_size : 0;
+    out->pending_opcode = (int32_t)c->fragmented_opcode;
+    out->max_frame_size = c->config.max_frame_size;
+    out->max_message_size = c->config.max_message_size;
+    out->is_server = c->is_server;
+}
+
+uvhttp_error_t uvhttp_ws_deliver_stream(struct uvhttp_ws_connection* c, const uint8_t* wire,
+                                        const uvhttp_ws_frame_desc_t* desc,
+                                        const uvhttp_ws_stream_t* s,
+                                        const uvhttp_ws_stream_result_t* r) {
+    if (c == NULL || s == NULL || r == NULL || (s->len && wire == NULL))
+        return UVHTTP_ERROR_INVALID_PARAM;
+    /* growth failed: process_data returns before touching the buffer (:836-857) */
+    if (r->first_status == UVHTTP_WS_FRAME_ERR_BUFFER ||
+        r->first_status == UVHTTP_WS_FRAME_ERR_CAPACITY)
+        return UVHTTP_ERROR_INVALID_PARAM;
+    if (r->recv_buffer_size != c->recv_buffer_size) {
+        uint8_t* nb = (uint8_t*)realloc(c->recv_buffer, (size_t)r->recv_buffer_size);
+        if (nb == NULL) return UVHTTP_ERROR_INVALID_PARAM;
+        c->recv_buffer = nb;
+        c->recv_buffer_size = (size_t)r->recv_buffer_size;
+    }
+    const uint8_t* base = wire + s->begin;
+    for (uint32_t k = 0; k < r->n_delivered; ++k) {
+        const uvhttp_ws_frame_desc_t* d = &desc[r->first_frame + k];
+        uvhttp_ws_frame_header_t h;
+        memset(&h, 0, sizeof(h));
+        h.fin = (d->flags & UVHTTP_WS_FLAG_FIN) ? 1 : 0;
+        h.mask = (d->flags & UVHTTP_WS_FLAG_MASK) ? 1 : 0;
+        h.opcode = d->opcode & 0x0F;
+        h.payload_length = d->payload_len;
+        const uint8_t* payload = d->payload_len ? wire + d->payload_off : NULL;
+        if (dispatch_frame(c, &h, payload) != 0) break; /* cannot happen after a clean decode */
+    }
+    /* what process_data leaves buffered: everything after the delivered frames */
+    const size_t rest = (size_t)(s->len - r->consumed_bytes);
+    if (rest) memmove(c->recv_buffer, base + r->consumed_bytes, rest);
+    c->recv_buffer_pos = rest;
+    return r->status == 0 ? UVHTTP_OK : UVHTTP_ERROR_INVALID_PARAM;
+}
