@@ -155,10 +155,13 @@ def pmc_traffic(cfg_name, mode):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
-    ap.add_argument("--mode", default="inplace", choices=["inplace", "compact"])
+    ap.add_argument("--mode", default="inplace", choices=["inplace", "compact", "streams"])
+    ap.add_argument("--conns", type=int, default=0,
+                    help="streams mode: connections the frames are split over "
+                         "(default: one frame per connection, 4096 for c4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--e2e", action="store_true", help="also time host->device->host")
@@ -194,13 +197,34 @@ def main():
         arena = torch.empty(n * plen + 64, dtype=torch.uint8, device=dev)
         msgs = torch.empty(n * 32, dtype=torch.uint8, device=dev)
     eng.reserve(n, wire_len, n * plen if arena is not None else 0)
+    streams_dev = None
+    if args.mode == "streams":
+        import numpy as np
+        conns = args.conns or (4096 if frag else n)
+        per = n // conns
+        st = np.zeros(conns, dtype=[("begin", "<u8"), ("len", "<u8"), ("rbs", "<u8"),
+                                    ("pend", "<u8"), ("pop", "<i4"), ("mf", "<i4"),
+                                    ("mm", "<i4"), ("srv", "<i4")])
+        st["begin"] = np.arange(conns, dtype=np.uint64) * per * stride
+        st["len"] = per * stride
+        st["rbs"] = max(65536, per * stride)
+        st["mf"], st["mm"], st["srv"] = 16 * 1024 * 1024, mm, 1
+        if frag:  # connection k continues the message: all its frames are continuations
+            st["pend"][1:] = 1
+            st["pop"] = 2
+        streams_dev = torch.from_numpy(st.view(np.uint8).copy()).to(dev)
+        s_desc = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+        s_res = torch.empty(conns * 48, dtype=torch.uint8, device=dev)
 
     def step():
         for _ in range(passes):
             one_pass()
 
     def one_pass():
-        if arena is None:
+        if streams_dev is not None:
+            eng.decode_streams(wire, streams_dev, streams_dev.numel() // 48, n, desc=s_desc,
+                               results=s_res, wire_len=wire_len, stream=stream)
+        elif arena is None:
             eng.decode_inplace(wire, n, stride=stride, max_message_size=mm, wire_len=wire_len,
                                desc=desc, summary=summ, stream=stream)
         else:
@@ -211,9 +235,14 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    s = eng.read_summary(summ)
-    if s["n_delivered"] != n or s["status"] != 0:
-        raise SystemExit(f"decode failed: {s}")
+    if streams_dev is not None:
+        rs = eng.read_stream_results(s_res, streams_dev.numel() // 48)
+        if sum(r.n_delivered for r in rs) != n or any(r.status for r in rs):
+            raise SystemExit(f"stream decode failed: {rs[0].as_dict()}")
+    else:
+        s = eng.read_summary(summ)
+        if s["n_delivered"] != n or s["status"] != 0:
+            raise SystemExit(f"decode failed: {s}")
     eng.kernel_time()  # discard warmup events
 
     eng.set_timing(True)
@@ -229,8 +258,9 @@ def main():
     elapsed = time.perf_counter() - t0
     eng.set_timing(False)
     k_ms, k_n = eng.kernel_time()
-    s = eng.read_summary(summ)
-    assert s["n_delivered"] == n and s["status"] == 0, s
+    if streams_dev is None:
+        s = eng.read_summary(summ)
+        assert s["n_delivered"] == n and s["status"] == 0, s
 
     el_max = max_over_ranks(elapsed, world)
     payload_per_rank = n * plen * passes
@@ -274,7 +304,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_unmask_inplace" if args.mode == "inplace" else "k_gather_compact",
+                "kernel": "k_gather_compact" if args.mode == "compact" else "k_unmask_inplace",
                 "achieved": round(achieved, 1) if achieved else None,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

@@ -604,3 +604,37 @@ uint64_t oracle_stream_decode(const uint8_t* wire, uint64_t len, size_t chunk,
     oracle_conn_free(c);
     return bytes;
 }
+
+/* ---- send side: uvhttp_ws_build_frame (:204-285) --------------------------------------- */
+/* The reference draws the client masking key from the context DRBG (:257-266, :55-68);
+ * here the key is an argument (the DRBG is host-side mbedtls, outside this path). */
+long oracle_build_frame(uint8_t* buf, size_t cap, const uint8_t* payload, size_t plen,
+                        int opcode, int mask, int fin, const uint8_t* key) {
+    if (!buf) return -1;
+    size_t hs = plen < 126 ? 2 : plen < 65536 ? 4 : 10;
+    if (plen > SIZE_MAX - hs - (mask ? 4 : 0)) return -1;
+    size_t total = hs + plen + (mask ? 4 : 0);
+    if (cap < total) return -1;
+    buf[0] = (uint8_t)((fin ? 0x80 : 0x00) | (opcode & 0x0F));
+    if (plen < 126) {
+        buf[1] = (uint8_t)((mask ? 0x80 : 0x00) | plen);
+    } else if (plen < 65536) {
+        buf[1] = (uint8_t)((mask ? 0x80 : 0x00) | 126);
+        buf[2] = (uint8_t)((plen >> 8) & 0xFF);
+        buf[3] = (uint8_t)(plen & 0xFF);
+    } else {
+        uint64_t l = (uint64_t)plen;
+        buf[1] = (uint8_t)((mask ? 0x80 : 0x00) | 127);
+        for (int k = 0; k < 8; ++k) buf[2 + k] = (uint8_t)((l >> (56 - 8 * k)) & 0xFF);
+    }
+    if (mask) {
+        for (int k = 0; k < 4; ++k) buf[hs + k] = key[k];
+        if (payload && plen > 0) {
+            memcpy(buf + hs + 4, payload, plen);
+            oracle_apply_mask(buf + hs + 4, plen, key);
+        }
+    } else if (payload && plen > 0) {
+        memcpy(buf + hs, payload, plen);
+    }
+    return (long)total;
+}

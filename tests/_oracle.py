@@ -63,6 +63,7 @@ def load():
         "oracle_decode_batch": (C.c_int, [vp, u64, vp, u64, u32, C.c_int, C.c_int, C.c_int, vp,
                                           u64, vp, vp, vp, vp, C.POINTER(OrcSummary)]),
         "oracle_gen_stride": (u64, [u64]),
+        "oracle_build_frame": (C.c_long, [vp, sz, vp, sz, C.c_int, C.c_int, C.c_int, vp]),
         "oracle_gen_key": (u32, [u64, u32, C.c_int]),
         "oracle_gen_frames": (None, [vp, u32, u32, u32, u64, u64, C.c_int, C.c_int, C.c_int]),
         "oracle_gen_plain": (None, [vp, u32, u64, u64]),
@@ -203,3 +204,15 @@ def gen_plain(i, payload_len, seed):
     out = np.empty(max(1, payload_len), dtype=np.uint8)
     L.oracle_gen_plain(_ptr(out), i, payload_len, seed)
     return out[:payload_len]
+
+
+def build_frame(payload: bytes, opcode, mask, fin, key=b"\x00\x00\x00\x00", cap=None):
+    """oracle_build_frame -> (rc, bytes)"""
+    L = load()
+    cap = len(payload) + 14 if cap is None else cap
+    out = (C.c_uint8 * max(1, cap))()
+    src = (C.c_uint8 * max(1, len(payload))).from_buffer_copy(payload or b"\0")
+    kb = (C.c_uint8 * 4).from_buffer_copy(bytes(key))
+    rc = L.oracle_build_frame(out, cap, src if payload else None, len(payload), opcode, mask,
+                              fin, kb)
+    return rc, bytes(out)[: max(rc, 0)]

@@ -232,6 +232,32 @@ process_cases = [
 ]
 
 
+def bcase(id, src, fill, n, opcode, mask, fin, cap, expect):
+    return dict(id=id, src=src, fill=fill, length=n, opcode=opcode, mask=mask, fin=fin, cap=cap,
+                expect=expect)
+
+
+build_cases = [
+    bcase("small_hello", FIX + ":105-115", "hello", 5, TEXT, 0, 1, 64,
+          dict(rc=7, head="8105", payload_plain=True)),
+    bcase("ext16_200", FIX + ":117-131", "x", 200, TEXT, 0, 1, 256,
+          dict(rc=204, head="817e00c8", payload_plain=True)),
+    bcase("ext16_boundary", FIX + ":133-145", "y", 65535, BINARY, 0, 1, 65536 + 16,
+          dict(rc=4 + 65535, head="827effff")),
+    bcase("ext64_70000", FIX + ":147-166", "z", 70000, BINARY, 0, 1, 70016,
+          dict(rc=10 + 70000, head="827f0000000000011170", payload_plain=True)),
+    bcase("insufficient_buffer", FIX + ":168-175", "\0", 200, TEXT, 0, 1, 8, dict(rc=-1)),
+    bcase("masked_ext64", BOOST2 + ":719-747", "D", 70000, TEXT, 1, 1, 70014,
+          dict(rc=70014, head="81ff0000000000011170")),
+    bcase("masked_ext16", BOOST2 + ":752-777", "E", 300, BINARY, 1, 1, 308,
+          dict(rc=308, head="82fe012c")),
+    bcase("server_short", BOOST + ":217-230", "Hello", 5, TEXT, 0, 1, 64,
+          dict(rc=7, head="8105", payload_plain=True)),
+    bcase("server_medium", BOOST + ":232-254", "B", 300, TEXT, 0, 1, 304,
+          dict(rc=304, head="817e012c", payload_plain=True)),
+]
+
+
 def main():
     out = dict(
         reference="adam-ikari/uvhttp v2.7.0",
@@ -239,13 +265,14 @@ def main():
         parse_frame_header=parse_cases,
         apply_mask=mask_cases,
         process_data=process_cases,
+        build_frame=build_cases,
     )
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)),
                         "reference_known_answers.json")
     with open(path, "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
         f.write("\n")
-    print(path, len(parse_cases), len(mask_cases), len(process_cases))
+    print(path, len(parse_cases), len(mask_cases), len(process_cases), len(build_cases))
 
 
 if __name__ == "__main__":

@@ -63,3 +63,25 @@ def test_oracle_generator_roundtrip():
         for i in range(4):
             got = out["wire"][i * stride + hs + 4: i * stride + hs + 4 + plen]
             assert np.array_equal(got, _oracle.gen_plain(i, plen, 0x5EED0001)), (plen, i)
+
+
+def test_oracle_build_frame_known_answers(known_answers):
+    for case in known_answers["build_frame"]:
+        fill = case["fill"].encode().decode("unicode_escape").encode("latin-1")
+        payload = (fill * (case["length"] // len(fill) + 1))[: case["length"]]
+        key = b"\x11\x22\x33\x44"
+        rc, out = _oracle.build_frame(payload, case["opcode"], case["mask"], case["fin"], key,
+                                      cap=case["cap"])
+        exp = case["expect"]
+        assert rc == exp["rc"] if exp["rc"] >= 0 else rc < 0, case["id"]
+        if rc < 0:
+            continue
+        head = bytes.fromhex(exp["head"])
+        assert out[: len(head)] == head, case["id"]
+        hs = len(head)
+        if case["mask"]:
+            assert out[hs:hs + 4] == key
+            body = bytes(b ^ key[i & 3] for i, b in enumerate(out[hs + 4:]))
+            assert body == payload, case["id"]
+        elif exp.get("payload_plain"):
+            assert out[hs:] == payload, case["id"]

@@ -153,7 +153,8 @@ __device__ ScanElem block_exclusive_scan(ScanElem v, ScanElem* total) {
 // workspace layout (device), carved from one allocation
 // ------------------------------------------------------------------------------------
 struct Workspace {
-    ScanElem* block_agg;   // [n_blocks + 1]: aggregates, then exclusive prefixes + total
+    ScanElem* block_agg;   // [n_blocks]: aggregates, then exclusive prefixes within a group
+    ScanElem* group_agg;   // [n_groups + 1]: group totals -> exclusive prefixes + grand total
     uint32_t* tile_first;  // [n_tiles]: first frame whose slot contains the tile start
     uint32_t* first_bad;   // [1]
     uint32_t* arena_first; // [n_arena_tiles]
@@ -268,20 +269,43 @@ __global__ __launch_bounds__(kBlock) void k_parse(BatchArgs a, uvhttp_ws_frame_d
         d.status = UVHTTP_WS_FRAME_OK;
         d.wire_len = 0;
 
+        // the at most 14 header bytes (2 + 8 length + 4 key) in one 16-byte load; bytes past
+        // the slot are loaded but never used (only the last 16 bytes of the wire go bytewise)
+        uint32_t hw0 = 0, hw1 = 0, hw2 = 0, hw3 = 0;
+        if (o + 16 <= a.wire_len) {
+            u32x4 v;
+            __builtin_memcpy(&v, p, 16);
+            hw0 = v.x, hw1 = v.y, hw2 = v.z, hw3 = v.w;
+        } else {
+            const uint64_t avail = a.wire_len > o ? a.wire_len - o : 0;
+            uint32_t t[4] = {0, 0, 0, 0};
+            for (uint32_t k = 0; k < 16 && k < avail; ++k) t[k >> 2] |= (uint32_t)p[k] << (8 * (k & 3));
+            hw0 = t[0], hw1 = t[1], hw2 = t[2], hw3 = t[3];
+        }
+        const uint64_t hlo = (uint64_t)hw0 | ((uint64_t)hw1 << 32);
+        const uint64_t hhi = (uint64_t)hw2 | ((uint64_t)hw3 << 32);
+        auto hb = [&](int k) -> uint32_t {  // header byte k (k is a constant after inlining)
+            return (uint32_t)((k < 8 ? hlo >> (8 * k) : hhi >> (8 * (k - 8))) & 0xFF);
+        };
+
         bool parsable = false, msb = false;
         uint64_t plen = 0, wlen = 0;
         uint32_t hsz = 2, b0 = 0, b1 = 0;
         if (slot >= 2) {
-            b0 = p[0];
-            b1 = p[1];
+            b0 = hb(0);
+            b1 = hb(1);
             const uint32_t code = b1 & 0x7F;
             const uint32_t need = code == 126 ? 4 : code == 127 ? 10 : 2;
             if (slot >= need) {
                 parsable = true;
-                plen = code;
-                if (need > 2) {
-                    plen = 0;
-                    for (uint32_t k = 2; k < need; ++k) plen = (plen << 8) | p[k];
+                if (need == 2) {
+                    plen = code;
+                } else if (need == 4) {
+                    plen = ((uint64_t)hb(2) << 8) | hb(3);
+                } else {
+                    plen = ((uint64_t)hb(2) << 56) | ((uint64_t)hb(3) << 48) | ((uint64_t)hb(4) << 40) |
+                           ((uint64_t)hb(5) << 32) | ((uint64_t)hb(6) << 24) | ((uint64_t)hb(7) << 16) |
+                           ((uint64_t)hb(8) << 8) | (uint64_t)hb(9);
                 }
                 msb = (need == 10) && (plen >> 63);
                 hsz = need;
@@ -289,9 +313,9 @@ __global__ __launch_bounds__(kBlock) void k_parse(BatchArgs a, uvhttp_ws_frame_d
                     const uint32_t m = (b1 >> 7) ? 4u : 0u;
                     wlen = hsz + m + plen;
                     if (m && slot >= hsz + 4) {
-                        d.masking_key = (uint32_t)p[hsz] | ((uint32_t)p[hsz + 1] << 8) |
-                                        ((uint32_t)p[hsz + 2] << 16) |
-                                        ((uint32_t)p[hsz + 3] << 24);
+                        d.masking_key = need == 2 ? (uint32_t)(hlo >> 16)
+                                      : need == 4 ? (uint32_t)(hlo >> 32)
+                                                  : (uint32_t)(hhi >> 16);
                     }
                     d.payload_off = o + hsz + m;
                 }
@@ -344,22 +368,46 @@ __global__ __launch_bounds__(kBlock) void k_parse(BatchArgs a, uvhttp_ws_frame_d
     if (threadIdx.x == 0) ws.block_agg[blockIdx.x] = total;
 }
 
-// k_scan: one workgroup turns the block aggregates into exclusive block prefixes and
-// stores the grand total at block_agg[n_blocks].
-__global__ __launch_bounds__(kBlock) void k_scan(Workspace ws, uint32_t n_blocks) {
-    const uint32_t per = (n_blocks + kBlock - 1) / kBlock;
-    const uint32_t beg = threadIdx.x * per;
-    const uint32_t fin = beg + per < n_blocks ? beg + per : n_blocks;
+// k_scan_groups + k_scan_top: two-level exclusive scan of the per-block aggregates.  A
+// single workgroup is bound by one CU's memory bandwidth (~24 GB/s), so groups of 256
+// aggregates are scanned by separate workgroups, then one workgroup scans the group totals.
+// Block b's exclusive prefix = group_agg[b / 256] (+) block_agg[b].  256-thread workgroups
+// keep the 48-byte scan element in registers (a 1024-thread version spilled).
+constexpr int kScanThreads = kBlock;
+
+__global__ __launch_bounds__(kBlock) void k_scan_groups(Workspace ws, uint32_t n_blocks) {
+    const uint32_t b = blockIdx.x * kBlock + threadIdx.x;
+    const ScanElem v = b < n_blocks ? ws.block_agg[b] : scan_identity();
+    ScanElem total;
+    const ScanElem pre = block_exclusive_scan(v, &total);
+    if (b < n_blocks) ws.block_agg[b] = pre;
+    if (threadIdx.x == 0) ws.group_agg[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kBlock) void k_scan_top(Workspace ws, uint32_t n_groups) {
+    // up to 4 groups per thread (2^26 frames -> 2^18 blocks -> 1024 groups)
+    constexpr int kPer = 4;
+    ScanElem v[kPer];
     ScanElem run = scan_identity();
-    for (uint32_t b = beg; b < fin; ++b) run = scan_combine(run, ws.block_agg[b]);
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const uint32_t g = threadIdx.x * kPer + k;
+        v[k] = g < n_groups ? ws.group_agg[g] : scan_identity();
+        run = scan_combine(run, v[k]);
+    }
     ScanElem total;
     ScanElem pre = block_exclusive_scan(run, &total);
-    for (uint32_t b = beg; b < fin; ++b) {
-        ScanElem v = ws.block_agg[b];
-        ws.block_agg[b] = pre;
-        pre = scan_combine(pre, v);
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const uint32_t g = threadIdx.x * kPer + k;
+        if (g < n_groups) ws.group_agg[g] = pre;
+        pre = scan_combine(pre, v[k]);
     }
-    if (threadIdx.x == 0) ws.block_agg[n_blocks] = total;
+    if (threadIdx.x == 0) ws.group_agg[n_groups] = total;
+}
+
+__device__ inline ScanElem block_prefix(const Workspace& ws, uint32_t b) {
+    return scan_combine(ws.group_agg[b / kScanThreads], ws.block_agg[b]);
 }
 
 // k_resolve: one lane per frame.  With E = scan over the frames of the same connection
@@ -385,7 +433,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(BatchArgs a, uvhttp_ws_frame
     ScanElem total;
     ScanElem ex = block_exclusive_scan(elem, &total);
     if (i >= n) return;
-    ex = scan_combine(ws.block_agg[blockIdx.x], ex);
+    ex = scan_combine(block_prefix(ws, blockIdx.x), ex);
     if (g.head) ex = scan_identity();  // nothing of this connection precedes its first frame
 
     // in-place tiles whose start byte lies in this frame's span up to the next frame (frame
@@ -553,7 +601,7 @@ __global__ __launch_bounds__(BLOCK) void k_unmask_inplace(
         // fast path (frames of ~8 KiB and up): at most two frames touch the tile; their
         // descriptors are uniform scalar loads
         for (uint32_t f = f0; f <= f1; ++f) {
-            if (desc[f].status != UVHTTP_WS_FRAME_OK) continue;  // undelivered (stream mode)
+            if (a.streams && desc[f].status != UVHTTP_WS_FRAME_OK) continue;  // undelivered
             const uint64_t ps = desc[f].payload_off;
             const uint64_t pe = ps + desc[f].payload_len;
             const uint32_t key = desc[f].masking_key;
@@ -568,7 +616,7 @@ __global__ __launch_bounds__(BLOCK) void k_unmask_inplace(
             __syncthreads();
             if (threadIdx.x < cnt) {
                 const uvhttp_ws_frame_desc_t d = desc[base + threadIdx.x];
-                const bool ok = d.status == UVHTTP_WS_FRAME_OK;  // undelivered: empty range
+                const bool ok = !a.streams || d.status == UVHTTP_WS_FRAME_OK;  // undelivered: empty
                 s_ps[threadIdx.x] = d.payload_off;
                 s_pe[threadIdx.x] = d.payload_off + (ok ? d.payload_len : 0);
                 s_key[threadIdx.x] = d.masking_key;
@@ -790,7 +838,7 @@ __global__ __launch_bounds__(kBlock) void k_finalize(BatchArgs a, uvhttp_ws_fram
     // E(nb): exclusive scan value at the first bad frame (or the total)
     ScanElem e;
     if (nb >= a.n) {
-        e = ws.block_agg[n_blocks];
+        e = ws.group_agg[(n_blocks + kScanThreads - 1) / kScanThreads];
     } else {
         const uint32_t b = nb / kBlock;
         const uint32_t f = b * kBlock + threadIdx.x;
@@ -798,7 +846,7 @@ __global__ __launch_bounds__(kBlock) void k_finalize(BatchArgs a, uvhttp_ws_fram
         if (f < nb) el = scan_elem_of(desc[f], (int32_t)f, f == 0);
         ScanElem part;
         (void)block_exclusive_scan(el, &part);
-        e = scan_combine(ws.block_agg[b], part);
+        e = scan_combine(block_prefix(ws, b), part);
     }
     if (threadIdx.x != 0) return;
     uvhttp_ws_batch_summary_t s;
@@ -1165,8 +1213,10 @@ int uvhttp_ws_gpu_engine_reserve(uvhttp_ws_gpu_engine_t* e, uint32_t max_frames,
     const uint64_t tl = tiles > e->cap_tiles ? tiles : e->cap_tiles;
     const uint64_t at = atiles > e->cap_arena_tiles ? atiles : e->cap_arena_tiles;
     const uint64_t nblk = (fr + kBlock - 1) / kBlock + 2;
+    const uint64_t ngrp = nblk / kScanThreads + 2;
     size_t off_agg = 0;
-    size_t off_tiles = align_up(off_agg + nblk * sizeof(ScanElem), 256);
+    size_t off_grp = align_up(off_agg + nblk * sizeof(ScanElem), 256);
+    size_t off_tiles = align_up(off_grp + ngrp * sizeof(ScanElem), 256);
     size_t off_bad = align_up(off_tiles + tl * sizeof(uint32_t), 256);
     size_t off_arena = align_up(off_bad + 16, 256);
     size_t bytes = align_up(off_arena + at * sizeof(uint32_t), 256);
@@ -1184,6 +1234,7 @@ int uvhttp_ws_gpu_engine_reserve(uvhttp_ws_gpu_engine_t* e, uint32_t max_frames,
     }
     char* b = (char*)e->ws_mem;
     e->ws.block_agg = (ScanElem*)(b + off_agg);
+    e->ws.group_agg = (ScanElem*)(b + off_grp);
     e->ws.tile_first = (uint32_t*)(b + off_tiles);
     e->ws.first_bad = (uint32_t*)(b + off_bad);
     e->ws.arena_first = (uint32_t*)(b + off_arena);
@@ -1306,7 +1357,11 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
     const uint32_t n_blocks = (a.n + kBlock - 1) / kBlock;
     const uint32_t grid_f = n_blocks ? n_blocks : 1;
     hipLaunchKernelGGL(k_parse, dim3(grid_f), dim3(kBlock), 0, s, a, d_desc, e->ws);
-    hipLaunchKernelGGL(k_scan, dim3(1), dim3(kBlock), 0, s, e->ws, grid_f);
+    {
+        const uint32_t n_groups = (grid_f + kScanThreads - 1) / kScanThreads;
+        hipLaunchKernelGGL(k_scan_groups, dim3(n_groups), dim3(kBlock), 0, s, e->ws, grid_f);
+        hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, s, e->ws, n_groups);
+    }
     hipLaunchKernelGGL(k_resolve, dim3(grid_f), dim3(kBlock), 0, s, a, d_desc, d_msgs, e->ws);
     // payload kernel tile shape: explicit (set_tile) or by average wire bytes per frame
     // (auto shapes from tools/tile_sweep.py on MI355X, profiles/r01_tile_sweep.txt)
@@ -1450,7 +1505,11 @@ int uvhttp_ws_gpu_decode_streams(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uin
     a.seg_bad = e->ss.seg_bad;
     const uint32_t grid_f = (cap + kBlock - 1) / kBlock;
     hipLaunchKernelGGL(k_parse, dim3(grid_f), dim3(kBlock), 0, s, a, d_desc, e->ws);
-    hipLaunchKernelGGL(k_scan, dim3(1), dim3(kBlock), 0, s, e->ws, grid_f);
+    {
+        const uint32_t n_groups = (grid_f + kScanThreads - 1) / kScanThreads;
+        hipLaunchKernelGGL(k_scan_groups, dim3(n_groups), dim3(kBlock), 0, s, e->ws, grid_f);
+        hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, s, e->ws, n_groups);
+    }
     hipLaunchKernelGGL(k_resolve, dim3(grid_f), dim3(kBlock), 0, s, a, d_desc,
                        (uvhttp_ws_message_desc_t*)nullptr, e->ws);
     const uint32_t grid_m = grid_f > nsb ? grid_f : nsb;
