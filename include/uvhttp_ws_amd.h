@@ -413,6 +413,30 @@ uvhttp_error_t uvhttp_ws_deliver_stream(struct uvhttp_ws_connection* conn, const
                                         const uvhttp_ws_stream_t* s,
                                         const uvhttp_ws_stream_result_t* r);
 
+/* ---- batched send-side framing ---------------------------------------------------------- */
+/* One frame to build: uvhttp_ws_build_frame(ctx, buf, size, payload, len, opcode, mask, fin)
+ * (src/uvhttp_websocket.c:204-285).  The reference draws a client's masking key from the
+ * context DRBG (:257-266, host-side mbedtls); here the caller supplies it. */
+typedef struct {
+    uint64_t payload_off;  /* payload = src[payload_off, payload_off + payload_len) */
+    uint64_t payload_len;
+    uint32_t masking_key;  /* used when mask != 0; key bytes k0..k3, k0 = low byte */
+    uint8_t opcode;        /* written as opcode & 0x0F */
+    uint8_t fin;
+    uint8_t mask;          /* 0: server frame (no key, payload copied); 1: client frame */
+    uint8_t reserved0;
+    uint64_t reserved1;
+} uvhttp_ws_build_desc_t;  /* 32 bytes */
+
+/* Build n frames back to back into d_out: frame i at d_out_off[i] (exclusive prefix sum of
+ * the frame sizes, header 2/4/10 by payload length, +4 key bytes when masked); d_out_off[n]
+ * = total bytes.  If the total exceeds out_cap nothing is written to d_out (d_out_off still
+ * is, so the caller can size the buffer), like build_frame's buffer_size check. */
+int uvhttp_ws_gpu_build_frames(uvhttp_ws_gpu_engine_t* eng, const uint8_t* d_src,
+                               uint64_t src_len, const uvhttp_ws_build_desc_t* d_frames,
+                               uint32_t n_frames, uint8_t* d_out, uint64_t out_cap,
+                               uint64_t* d_out_off, void* stream);
+
 /* ---- host-memory pipeline (libuv read buffers in, decoded payloads out) ---------------- */
 /* A pipeline owns `depth` slots.  Each slot = a pinned host staging buffer (the caller
  * writes masked frames there, e.g. hands it out from the libuv alloc callback), a device

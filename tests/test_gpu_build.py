@@ -1,0 +1,128 @@
+"""Batched send-side framing: uvhttp_ws_gpu_build_frames against the
+oracle's restatement of uvhttp_ws_build_frame (src/uvhttp_websocket.c:204-285), the reference
+tests' known answers, and build -> decode round trips."""
+import random
+
+import numpy as np
+import pytest
+
+import _oracle
+
+pytestmark = pytest.mark.gpu
+
+BUILD_DT = np.dtype([("payload_off", "<u8"), ("payload_len", "<u8"), ("key", "<u4"),
+                     ("opcode", "u1"), ("fin", "u1"), ("mask", "u1"), ("r0", "u1"),
+                     ("r1", "<u8")])
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    if not t.cuda.is_available():
+        pytest.skip("no GPU")
+    return t
+
+
+@pytest.fixture(scope="module")
+def eng(torch):
+    import uvhttp_amd as U
+    e = U.GpuEngine(0)
+    yield e
+    e.close()
+
+
+def _build(torch, eng, src, frames, cap_extra=64, cap=None):
+    total = 0
+    exp = []
+    for f in frames:
+        payload = src[f["payload_off"]:f["payload_off"] + f["payload_len"]].tobytes()
+        key = int(f["key"]).to_bytes(4, "little")
+        rc, b = _oracle.build_frame(payload, int(f["opcode"]), int(f["mask"]), int(f["fin"]), key)
+        assert rc == len(b)
+        exp.append(b)
+        total += rc
+    cap = total + cap_extra if cap is None else cap
+    dsrc = torch.from_numpy(src.copy()).to("cuda") if src.size else \
+        torch.zeros(16, dtype=torch.uint8, device="cuda")
+    dfr = torch.from_numpy(frames.view(np.uint8).copy()).to("cuda") if len(frames) else \
+        torch.zeros(32, dtype=torch.uint8, device="cuda")
+    out = torch.zeros(max(16, cap), dtype=torch.uint8, device="cuda")
+    off = eng.build_frames(dsrc, dfr, len(frames), out[:cap] if cap else out[:0])
+    torch.cuda.synchronize()
+    return exp, total, out.cpu().numpy(), off.cpu().numpy()
+
+
+def _rand_frames(rng, src_len, n, sizes):
+    fr = np.zeros(n, BUILD_DT)
+    for i in range(n):
+        p = min(rng.choice(sizes), src_len)
+        fr[i]["payload_len"] = p
+        fr[i]["payload_off"] = rng.randint(0, src_len - p) if src_len > p else 0
+        fr[i]["key"] = rng.getrandbits(32)
+        fr[i]["opcode"] = rng.choice([0, 1, 2, 8, 9, 10, 0x13])
+        fr[i]["fin"] = rng.choice([0, 1])
+        fr[i]["mask"] = rng.choice([0, 1])
+    return fr
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_build_matches_oracle(torch, eng, seed):
+    rng = random.Random(seed)
+    src = np.frombuffer(rng.randbytes(300000), np.uint8).copy()
+    sizes = [[0, 1, 5, 125, 126, 127, 200], [1000, 4095, 65535, 65536, 70000],
+             [0, 3, 300, 65536]][seed % 3]
+    frames = _rand_frames(rng, src.size, rng.choice([1, 17, 300, 2000]), sizes)
+    exp, total, out, off = _build(torch, eng, src, frames)
+    assert int(off[len(frames)]) == total
+    assert np.array_equal(off[:len(frames)], np.cumsum([0] + [len(b) for b in exp[:-1]]))
+    assert out[:total].tobytes() == b"".join(exp)
+    assert not out[total:].any()  # nothing past the frames
+
+
+def test_build_capacity(torch, eng):
+    rng = random.Random(5)
+    src = np.frombuffer(rng.randbytes(5000), np.uint8).copy()
+    frames = _rand_frames(rng, src.size, 40, [10, 100, 1000])
+    exp, total, out, off = _build(torch, eng, src, frames, cap=100)
+    assert int(off[len(frames)]) == total > 100
+    assert not out.any()  # all-or-nothing, like build_frame's size check
+
+
+def test_build_known_answers(torch, eng, known_answers):
+    for case in known_answers["build_frame"]:
+        if case["expect"]["rc"] < 0:
+            continue
+        fill = case["fill"].encode().decode("unicode_escape").encode("latin-1")
+        payload = (fill * (case["length"] // len(fill) + 1))[: case["length"]]
+        src = np.frombuffer(payload, np.uint8).copy()
+        fr = np.zeros(1, BUILD_DT)
+        fr[0]["payload_len"] = len(payload)
+        fr[0]["key"] = 0x44332211
+        fr[0]["opcode"], fr[0]["fin"], fr[0]["mask"] = case["opcode"], case["fin"], case["mask"]
+        exp, total, out, off = _build(torch, eng, src, fr)
+        assert total == case["expect"]["rc"], case["id"]
+        head = bytes.fromhex(case["expect"]["head"])
+        assert out[: len(head)].tobytes() == head, case["id"]
+        assert out[:total].tobytes() == exp[0], case["id"]
+
+
+def test_build_then_decode_roundtrip(torch, eng):
+    """Client (masked) frames built on the device decode back to their payloads."""
+    rng = random.Random(11)
+    src = np.frombuffer(rng.randbytes(1 << 20), np.uint8).copy()
+    frames = _rand_frames(rng, src.size, 500, [0, 7, 126, 4096, 65536])
+    frames["mask"] = 1
+    frames["opcode"] = 2
+    frames["fin"] = 1
+    exp, total, out, off = _build(torch, eng, src, frames)
+    wire = torch.from_numpy(out.copy()).to("cuda")
+    offs = torch.from_numpy(off[:len(frames)].astype(np.int64)).to("cuda")
+    desc, summ = eng.decode_inplace(wire, len(frames), offsets=offs, wire_len=total)
+    torch.cuda.synchronize()
+    s = eng.read_summary(summ)
+    assert s["n_delivered"] == len(frames) and s["status"] == 0
+    d = eng.read_desc(desc, len(frames))
+    w = wire.cpu().numpy()
+    for i, f in enumerate(frames):
+        got = w[d[i]["payload_off"]:d[i]["payload_off"] + d[i]["payload_len"]]
+        assert np.array_equal(got, src[f["payload_off"]:f["payload_off"] + f["payload_len"]])

@@ -194,6 +194,7 @@ def lib() -> C.CDLL:
         "uvhttp_ws_gpu_pipeline_wait": (C.c_int, [vp, C.c_int, C.POINTER(vp), C.POINTER(vp)]),
         "uvhttp_ws_deliver_batch": (C.c_int, [C.POINTER(WsConnectionStruct), vp, vp, vp]),
         "uvhttp_ws_gpu_decode_streams": (C.c_int, [vp, vp, u64, vp, u32, u32, vp, vp, vp]),
+        "uvhttp_ws_gpu_build_frames": (C.c_int, [vp, vp, u64, vp, u32, vp, u64, vp, vp]),
         "uvhttp_ws_stream_init": (None, [C.POINTER(WsConnectionStruct), u64, u64,
                                          C.POINTER(Stream)]),
         "uvhttp_ws_deliver_stream": (C.c_int, [C.POINTER(WsConnectionStruct), vp, vp,
@@ -425,6 +426,18 @@ class GpuEngine:
             C.c_void_p(desc.data_ptr()), C.c_void_p(results.data_ptr()), self._stream(stream)),
             "decode_streams")
         return desc, results
+
+    def build_frames(self, src, frames_dev, n_frames, out, out_off=None, stream=None):
+        """uvhttp_ws_gpu_build_frames; frames_dev = device uint8 tensor of n_frames
+        uvhttp_ws_build_desc_t (32 B each).  Returns out_off (device int64[n+1])."""
+        t = self.torch
+        if out_off is None:
+            out_off = t.zeros(n_frames + 1, dtype=t.int64, device=f"cuda:{self.device}")
+        self._check(self._L.uvhttp_ws_gpu_build_frames(
+            self.h, C.c_void_p(src.data_ptr()), src.numel(), C.c_void_p(frames_dev.data_ptr()),
+            n_frames, C.c_void_p(out.data_ptr()), out.numel(), C.c_void_p(out_off.data_ptr()),
+            self._stream(stream)), "build_frames")
+        return out_off
 
     @staticmethod
     def read_stream_results(results, n):

@@ -1054,6 +1054,229 @@ __global__ __launch_bounds__(kBlock) void k_stream_mark(BatchArgs a, uvhttp_ws_f
     results[i] = r;
 }
 
+// ------------------------------------------------------------------------------------
+// send side: batched uvhttp_ws_build_frame (:204-285).  kb_size -> two-level u64 scan ->
+// kb_offsets -> kb_emit.  kb_emit is an HBM-bound scatter: one workgroup per output tile,
+// each 16-byte output vector assembled from the covering frame's header image (staged in
+// LDS) and its payload (one unaligned 16-byte source window, XORed with the rotated key
+// for client frames).  Bytes per frame: P read + (H + 4m + P) written.
+// ------------------------------------------------------------------------------------
+struct BuildArgs {
+    const uint8_t* src;
+    uint64_t src_len;
+    const uvhttp_ws_build_desc_t* frames;
+    uint32_t n;
+    uint8_t* out;
+    uint64_t out_cap;
+    uint64_t* out_off;   // [n + 1]
+    uint64_t* blk;       // per-block sums -> prefixes (u64 scratch)
+    uint64_t* grp;       // per-group sums -> prefixes, [n_groups] = total
+    uint32_t* map;       // output tile (16 KiB) -> first frame
+    uint64_t n_map;
+};
+
+__device__ inline uint64_t build_size(const uvhttp_ws_build_desc_t& f) {
+    const uint64_t p = f.payload_len;
+    return (p < 126 ? 2 : p < 65536 ? 4 : 10) + (f.mask ? 4 : 0) + p;
+}
+
+__device__ inline uint64_t block_exclusive_sum_u64(uint64_t v, uint64_t* total) {
+    __shared__ uint64_t wsum[kBlock / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint64_t inc = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t o = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += o;
+    }
+    if (lane == 63) wsum[wave] = inc;
+    __syncthreads();
+    uint64_t pre = 0, all = 0;
+    for (int k = 0; k < kBlock / 64; ++k) {
+        if (k < wave) pre += wsum[k];
+        all += wsum[k];
+    }
+    __syncthreads();
+    *total = all;
+    return pre + inc - v;
+}
+
+__global__ __launch_bounds__(kBlock) void kb_size(BuildArgs b) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t sz = i < b.n ? build_size(b.frames[i]) : 0;
+    uint64_t total;
+    (void)block_exclusive_sum_u64(sz, &total);
+    if (threadIdx.x == 0) b.blk[blockIdx.x] = total;
+    const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    for (uint64_t t = gtid; t < b.n_map; t += (uint64_t)gridDim.x * kBlock) b.map[t] = kNoFrame;
+}
+
+__global__ __launch_bounds__(kBlock) void kb_scan_groups(BuildArgs b, uint32_t n_blocks) {
+    const uint32_t k = blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t v = k < n_blocks ? b.blk[k] : 0;
+    uint64_t total;
+    const uint64_t pre = block_exclusive_sum_u64(v, &total);
+    if (k < n_blocks) b.blk[k] = pre;
+    if (threadIdx.x == 0) b.grp[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kBlock) void kb_scan_top(BuildArgs b, uint32_t n_groups) {
+    constexpr int kPer = 4;
+    uint64_t v[kPer], run = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const uint32_t g = threadIdx.x * kPer + k;
+        v[k] = g < n_groups ? b.grp[g] : 0;
+        run += v[k];
+    }
+    uint64_t total;
+    uint64_t pre = block_exclusive_sum_u64(run, &total);
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const uint32_t g = threadIdx.x * kPer + k;
+        if (g < n_groups) b.grp[g] = pre;
+        pre += v[k];
+    }
+    if (threadIdx.x == 0) b.grp[n_groups] = total;
+}
+
+__global__ __launch_bounds__(kBlock) void kb_offsets(BuildArgs b, uint32_t n_groups) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t sz = i < b.n ? build_size(b.frames[i]) : 0;
+    uint64_t total;
+    const uint64_t local = block_exclusive_sum_u64(sz, &total);
+    if (i >= b.n) return;
+    const uint64_t off = b.grp[blockIdx.x / kBlock] + b.blk[blockIdx.x] + local;
+    b.out_off[i] = off;
+    if (i + 1 == b.n) b.out_off[b.n] = b.grp[n_groups];
+    if (b.grp[n_groups] > b.out_cap) return;  // nothing will be written
+    for (uint64_t t = (off + kMapTile - 1) / kMapTile; t * kMapTile < off + sz && t < b.n_map; ++t)
+        atomicMin(&b.map[t], i);
+}
+
+template <int BLOCK, int VPT>
+__global__ __launch_bounds__(BLOCK) void kb_emit(BuildArgs b, uint64_t tile_base) {
+    constexpr uint64_t kT = (uint64_t)BLOCK * VPT * 16;
+    __shared__ uint64_t s_start[BLOCK];  // frame start in out
+    __shared__ uint64_t s_pstart[BLOCK]; // payload start in out
+    __shared__ uint64_t s_end[BLOCK];
+    __shared__ uint64_t s_src[BLOCK];
+    __shared__ uint32_t s_key[BLOCK];    // 0 for server frames (XOR no-op)
+    __shared__ u32x4 s_hdr[BLOCK];       // header image (<= 14 bytes)
+
+    const uint64_t total = b.out_off[b.n];
+    if (total > b.out_cap || b.n == 0) return;
+    const uint64_t t0 = (tile_base + blockIdx.x) * kT;
+    if (t0 >= total) return;
+    const uint64_t c0 = t0 / kMapTile, c1 = (t0 + kT - 1) / kMapTile + 1;
+    const uint32_t last = b.n - 1;
+    uint32_t f0 = b.map[c0];
+    if (f0 > last) f0 = 0;  // cannot happen for t0 < total; stay in bounds regardless
+    uint32_t f1 = (c1 < b.n_map) ? b.map[c1] : last;
+    if (f1 > last || f1 < f0) f1 = last;
+
+    uint64_t oa[VPT];
+    u32x4 out[VPT];
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {
+        oa[v] = t0 + ((uint64_t)v * BLOCK + threadIdx.x) * 16u;
+        out[v] = u32x4{0, 0, 0, 0};
+    }
+    for (uint32_t base = f0; base <= f1; base += BLOCK) {
+        const uint32_t cnt = (f1 - base + 1) < (uint32_t)BLOCK ? (f1 - base + 1) : BLOCK;
+        __syncthreads();
+        if (threadIdx.x < cnt) {
+            const uint32_t f = base + threadIdx.x;
+            const uvhttp_ws_build_desc_t d = b.frames[f];
+            const uint64_t p = d.payload_len;
+            const uint32_t hs = p < 126 ? 2 : p < 65536 ? 4 : 10;
+            const uint32_t m = d.mask ? 4 : 0;
+            uint8_t h[16] = {0};
+            h[0] = (uint8_t)((d.fin ? 0x80 : 0) | (d.opcode & 0x0F));
+            const uint8_t mb = d.mask ? 0x80 : 0;
+            if (hs == 2) {
+                h[1] = (uint8_t)(mb | p);
+            } else if (hs == 4) {
+                h[1] = (uint8_t)(mb | 126);
+                h[2] = (uint8_t)(p >> 8);
+                h[3] = (uint8_t)p;
+            } else {
+                h[1] = (uint8_t)(mb | 127);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) h[2 + k] = (uint8_t)(p >> (56 - 8 * k));
+            }
+            if (m) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) h[hs + k] = (uint8_t)(d.masking_key >> (8 * k));
+            }
+            u32x4 img;
+            __builtin_memcpy(&img, h, 16);
+            const uint64_t st = b.out_off[f];
+            s_start[threadIdx.x] = st;
+            s_pstart[threadIdx.x] = st + hs + m;
+            s_end[threadIdx.x] = st + hs + m + p;
+            s_src[threadIdx.x] = d.payload_off;
+            s_key[threadIdx.x] = d.mask ? d.masking_key : 0u;
+            s_hdr[threadIdx.x] = img;
+        }
+        __syncthreads();
+        if (s_start[0] >= t0 + kT) break;
+#pragma unroll
+        for (int v = 0; v < VPT; ++v) {
+            int lo = 0, hi = (int)cnt - 1, j = -1;
+            while (lo <= hi) {
+                const int mid = (lo + hi) >> 1;
+                if (s_start[mid] < oa[v] + 16) {
+                    j = mid;
+                    lo = mid + 1;
+                } else {
+                    hi = mid - 1;
+                }
+            }
+            for (; j >= 0; --j) {
+                const uint64_t fs = s_start[j], ps = s_pstart[j], fe = s_end[j];
+                if (fe <= oa[v]) break;
+                // header bytes [fs, ps) of the vector
+                if (ps > oa[v] && fs < oa[v] + 16) {
+                    const u32x4 img = s_hdr[j];
+                    const uint32_t iw[4] = {img.x, img.y, img.z, img.w};
+                    uint32_t ow[4] = {0, 0, 0, 0};
+                    for (int bq = 0; bq < 16; ++bq) {
+                        const uint64_t x = oa[v] + bq;
+                        if (x >= fs && x < ps) {
+                            const uint32_t k = (uint32_t)(x - fs);
+                            ow[bq >> 2] |= ((iw[k >> 2] >> (8 * (k & 3))) & 0xFF) << (8 * (bq & 3));
+                        }
+                    }
+                    out[v] |= u32x4{ow[0], ow[1], ow[2], ow[3]};
+                }
+                // payload bytes [ps, fe)
+                if (fe > ps && ps < oa[v] + 16) {
+                    const int lo_b = ps > oa[v] ? (int)(ps - oa[v]) : 0;
+                    const int hi_b = fe < oa[v] + 16 ? (int)(fe - oa[v]) : 16;
+                    const int64_t wstart = (int64_t)s_src[j] + ((int64_t)oa[v] - (int64_t)ps);
+                    const u32x4 w = load16_any(b.src, wstart, b.src_len);
+                    const uint32_t rk = rotr32(s_key[j], 8u * (uint32_t)((oa[v] - ps) & 3u));
+                    const u32x4 sel{lane_bytes(lo_b, hi_b, 0), lane_bytes(lo_b, hi_b, 1),
+                                    lane_bytes(lo_b, hi_b, 2), lane_bytes(lo_b, hi_b, 3)};
+                    out[v] |= (w ^ u32x4{rk, rk, rk, rk}) & sel;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {
+        if (oa[v] >= total) continue;
+        if (oa[v] + 16 <= total) {
+            __builtin_nontemporal_store(out[v], reinterpret_cast<u32x4*>(b.out + oa[v]));
+        } else {
+            const uint32_t ow[4] = {out[v].x, out[v].y, out[v].z, out[v].w};
+            for (uint64_t bq = 0; oa[v] + bq < total; ++bq)
+                b.out[oa[v] + bq] = (uint8_t)(ow[bq >> 2] >> (8 * (bq & 3)));
+        }
+    }
+}
+
 // plain unmask of one buffer with one key (uvhttp_ws_apply_mask over device memory)
 __global__ __launch_bounds__(kBlock) void k_apply_mask(uint8_t* data, uint64_t len, uint32_t key,
                                                        uint64_t head) {
@@ -1530,6 +1753,61 @@ int uvhttp_ws_gpu_decode_streams(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uin
         UVWS_LAUNCH(64, 1) UVWS_LAUNCH(64, 2) UVWS_LAUNCH(64, 4) UVWS_LAUNCH(128, 1)
         UVWS_LAUNCH(128, 2) UVWS_LAUNCH(256, 1) UVWS_LAUNCH(256, 2) UVWS_LAUNCH(256, 4) {}
 #undef UVWS_LAUNCH
+    }
+    timing_end(e, tk, s);
+    const hipError_t h = hipGetLastError();
+    if (prev != e->device) (void)hipSetDevice(prev);
+    if (h != hipSuccess) return set_err(e, UVHTTP_WS_GPU_ELAUNCH, "launch", h);
+    return UVHTTP_WS_GPU_OK;
+}
+
+int uvhttp_ws_gpu_build_frames(uvhttp_ws_gpu_engine_t* e, const uint8_t* d_src, uint64_t src_len,
+                               const uvhttp_ws_build_desc_t* d_frames, uint32_t n_frames,
+                               uint8_t* d_out, uint64_t out_cap, uint64_t* d_out_off,
+                               void* stream) {
+    if (!e || (!d_frames && n_frames) || !d_out_off || (!d_out && out_cap) ||
+        (!d_src && src_len))
+        return UVHTTP_WS_GPU_EINVAL;
+    if (((uintptr_t)d_out) & 15u)
+        return set_err(e, UVHTTP_WS_GPU_EINVAL, "out must be 16-byte aligned", hipSuccess);
+    if (n_frames > kMaxFrames) return set_err(e, UVHTTP_WS_GPU_EINVAL, "too many frames", hipSuccess);
+    // scratch: reuse the engine workspace (block/group aggregates as u64, arena map)
+    int rc = uvhttp_ws_gpu_engine_reserve(e, n_frames ? n_frames : 1, 0, out_cap);
+    if (rc) return rc;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    if (prev != e->device) (void)hipSetDevice(e->device);
+    hipStream_t s = (hipStream_t)stream;
+    BuildArgs b;
+    b.src = d_src;
+    b.src_len = src_len;
+    b.frames = d_frames;
+    b.n = n_frames;
+    b.out = d_out;
+    b.out_cap = out_cap;
+    b.out_off = d_out_off;
+    b.blk = reinterpret_cast<uint64_t*>(e->ws.block_agg);
+    b.grp = reinterpret_cast<uint64_t*>(e->ws.group_agg);
+    b.map = e->ws.arena_first;
+    b.n_map = (out_cap + kMapTile - 1) / kMapTile;
+    const uint32_t grid_f = n_frames ? (n_frames + kBlock - 1) / kBlock : 1;
+    const uint32_t n_groups = (grid_f + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(kb_size, dim3(grid_f), dim3(kBlock), 0, s, b);
+    hipLaunchKernelGGL(kb_scan_groups, dim3(n_groups), dim3(kBlock), 0, s, b, grid_f);
+    hipLaunchKernelGGL(kb_scan_top, dim3(1), dim3(kBlock), 0, s, b, n_groups);
+    hipLaunchKernelGGL(kb_offsets, dim3(grid_f), dim3(kBlock), 0, s, b, n_groups);
+    if (!n_frames) {
+        // d_out_off[0] = 0 (total) for an empty batch
+        (void)hipMemsetAsync(d_out_off, 0, 8, s);
+    }
+    constexpr int kB = 64, kV = 2;
+    const uint64_t tile_bytes = (uint64_t)kB * kV * 16;
+    const uint64_t n_ptiles = (out_cap + tile_bytes - 1) / tile_bytes;
+    const uint64_t max_tiles = (1ull << 24);
+    const int tk = timing_begin(e, s);
+    for (uint64_t tb = 0; n_frames && tb < n_ptiles; tb += max_tiles) {
+        const uint32_t grid_p = (uint32_t)((n_ptiles - tb) < max_tiles ? (n_ptiles - tb) : max_tiles);
+        hipLaunchKernelGGL((kb_emit<kB, kV>), dim3(grid_p), dim3(kB), 0, s, b, tb);
     }
     timing_end(e, tk, s);
     const hipError_t h = hipGetLastError();
