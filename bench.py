@@ -158,7 +158,8 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
-    ap.add_argument("--mode", default="inplace", choices=["inplace", "compact", "streams"])
+    ap.add_argument("--mode", default="inplace",
+                    choices=["inplace", "compact", "streams", "build", "build_masked"])
     ap.add_argument("--conns", type=int, default=0,
                     help="streams mode: connections the frames are split over "
                          "(default: one frame per connection, 4096 for c4)")
@@ -197,7 +198,22 @@ def main():
         arena = torch.empty(n * plen + 64, dtype=torch.uint8, device=dev)
         msgs = torch.empty(n * 32, dtype=torch.uint8, device=dev)
     eng.reserve(n, wire_len, n * plen if arena is not None else 0)
-    streams_dev = None
+    streams_dev = build_dev = None
+    if args.mode.startswith("build"):
+        # send side: frame n payloads of the config (server echo: unmasked; client: masked)
+        import numpy as np
+        fr = np.zeros(n, dtype=[("po", "<u8"), ("pl", "<u8"), ("key", "<u4"), ("op", "u1"),
+                                ("fin", "u1"), ("mask", "u1"), ("r0", "u1"), ("r1", "<u8")])
+        fr["po"] = np.arange(n, dtype=np.uint64) * plen
+        fr["pl"] = plen
+        fr["key"] = np.arange(n, dtype=np.uint32) * 2654435761
+        fr["op"], fr["fin"] = 2, 1
+        fr["mask"] = 1 if args.mode == "build_masked" else 0
+        build_dev = torch.from_numpy(fr.view(np.uint8).copy()).to(dev)
+        build_src = torch.empty(n * plen + 64, dtype=torch.uint8, device=dev)
+        build_src.random_(0, 256)
+        build_out = torch.empty(n * (plen + 14) + 64, dtype=torch.uint8, device=dev)
+        build_off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
     if args.mode == "streams":
         import numpy as np
         conns = args.conns or (4096 if frag else n)
@@ -221,7 +237,9 @@ def main():
             one_pass()
 
     def one_pass():
-        if streams_dev is not None:
+        if build_dev is not None:
+            eng.build_frames(build_src, build_dev, n, build_out, out_off=build_off, stream=stream)
+        elif streams_dev is not None:
             eng.decode_streams(wire, streams_dev, streams_dev.numel() // 48, n, desc=s_desc,
                                results=s_res, wire_len=wire_len, stream=stream)
         elif arena is None:
@@ -235,7 +253,10 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if streams_dev is not None:
+    if build_dev is not None:
+        if int(build_off[n].item()) != n * (stride - (0 if args.mode == "build_masked" else 4)):
+            raise SystemExit("build failed")
+    elif streams_dev is not None:
         rs = eng.read_stream_results(s_res, streams_dev.numel() // 48)
         if sum(r.n_delivered for r in rs) != n or any(r.status for r in rs):
             raise SystemExit(f"stream decode failed: {rs[0].as_dict()}")
@@ -258,7 +279,7 @@ def main():
     elapsed = time.perf_counter() - t0
     eng.set_timing(False)
     k_ms, k_n = eng.kernel_time()
-    if streams_dev is None:
+    if streams_dev is None and build_dev is None:
         s = eng.read_summary(summ)
         assert s["n_delivered"] == n and s["status"] == 0, s
 
@@ -271,6 +292,8 @@ def main():
     # frame's header+key+payload is read and its payload written; compact reads the same
     # and writes the payload into the arena.
     alg_bytes = n * ((header_size(plen) + 4 + plen) + plen)
+    if build_dev is not None:  # payload read + frame written
+        alg_bytes = n * (plen + header_size(plen) + (4 if args.mode == "build_masked" else 0) + plen)
     avg_kernel_s = (k_ms / 1e3 / k_n) if k_n else float("nan")
     achieved = alg_bytes / avg_kernel_s / 1e9 if k_n else None
     traffic = pmc_traffic(args.config, args.mode)
@@ -304,7 +327,8 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_gather_compact" if args.mode == "compact" else "k_unmask_inplace",
+                "kernel": {"compact": "k_gather_compact", "build": "kb_emit",
+                           "build_masked": "kb_emit"}.get(args.mode, "k_unmask_inplace"),
                 "achieved": round(achieved, 1) if achieved else None,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

@@ -5,8 +5,8 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/bench_matrix_${TAG:-r01}.jsonl
 : > "$OUT"
 for cfg in c3 c2 c4; do
-  for mode in inplace compact streams; do
-    timeout -k 10 300 python bench.py --config $cfg --mode $mode --steps 20 --warmup 5 \
+  for mode in ${MODES:-inplace compact streams build build_masked}; do
+    timeout -k 10 300 python bench.py --config $cfg --mode $mode --steps ${STEPS:-100} --warmup 10 \
       --no-cpu-baseline >> "$OUT" 2>> gpurun_out/bench_matrix.err || { echo "fail $cfg $mode"; exit 1; }
   done
 done
