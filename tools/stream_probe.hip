@@ -200,19 +200,17 @@ int main(int argc, char** argv) {
 #define ADD_PERSIST(B, VPT, NT, WPC)                                                                 \
     V.push_back({"pers b" #B " v" #VPT " nt" #NT " wg/cu" #WPC,                                      \
                  [=](hipStream_t st) { hipLaunchKernelGGL((k_xor_persist<B, VPT, NT>), dim3(ncu * WPC), dim3(B), 0, st, a, nvec, 0x9u); }, {}})
-    ADD_COPY(256, 4, true, true);
-    ADD_COPY(256, 1, true, true);
-    ADD_XOR(256, 4, true, true);
-    ADD_XOR(256, 1, true, true);
-    ADD_XOR(256, 1, false, false);
-    ADD_XOR(256, 1, true, false);
-    ADD_XOR(128, 1, true, true);
+    ADD_COPY(64, 1, true, true);
     ADD_XOR(64, 1, true, true);
-    ADD_XOR(64, 2, true, true);
-    ADD_XOR(128, 2, true, true);
-    ADD_XOR(512, 1, true, true);
-    ADD_XOR(1024, 1, true, true);
-    ADD_XOR(64, 4, true, true);
+    ADD_XOR(64, 1, false, false);
+    ADD_XOR(64, 1, true, false);
+    ADD_XOR(64, 1, false, true);
+    ADD_XOR(128, 1, true, true);
+    ADD_XOR(256, 1, true, true);
+    V.push_back({"buf b64 aux nt/nt", [=](hipStream_t st) { hipLaunchKernelGGL((k_xor_buf<64, 1, 2, 2>), GRID(64, 1), dim3(64), 0, st, a, nvec, 5u); }, {}});
+    V.push_back({"buf b64 aux sc1|nt/nt", [=](hipStream_t st) { hipLaunchKernelGGL((k_xor_buf<64, 1, 18, 2>), GRID(64, 1), dim3(64), 0, st, a, nvec, 5u); }, {}});
+    V.push_back({"buf b64 aux nt/sc1|nt", [=](hipStream_t st) { hipLaunchKernelGGL((k_xor_buf<64, 1, 2, 18>), GRID(64, 1), dim3(64), 0, st, a, nvec, 5u); }, {}});
+    V.push_back({"buf b64 aux sc0|nt/sc0|nt", [=](hipStream_t st) { hipLaunchKernelGGL((k_xor_buf<64, 1, 3, 3>), GRID(64, 1), dim3(64), 0, st, a, nvec, 5u); }, {}});
     {
         const uint64_t ntile = (nvec + 255) / 256;
         uint32_t *fb, *tm;

@@ -556,7 +556,10 @@ __device__ inline bool any_bits(const u32x4& m) { return (m.x | m.y | m.z | m.w)
 // wire belongs to exactly one tile, so whole-vector stores never race: bytes outside any
 // delivered payload are XORed with 0 and vectors with no payload byte are not stored.
 // ------------------------------------------------------------------------------------
-template <int BLOCK, int VPT>
+// store-path cache policy of the payload pass: 0 = global_store nt; 18 = buffer_store with
+// sc1|nt (write-through, not kept in L2), measured 1.7 % faster for the 64x1 shape
+// (tools/stream_probe.hip, profiles/r01_stream_probe_policy.txt)
+template <int BLOCK, int VPT, int STORE_AUX = 0>
 __global__ __launch_bounds__(BLOCK) void k_unmask_inplace(
     BatchArgs a, const uvhttp_ws_frame_desc_t* __restrict__ desc, Workspace ws,
     uint64_t tile_base) {
@@ -647,10 +650,27 @@ __global__ __launch_bounds__(BLOCK) void k_unmask_inplace(
         }
     }
 
+    if (STORE_AUX == 0) {
 #pragma unroll
-    for (int v = 0; v < VPT; ++v) {
-        if (any_bits(m[v]) && va[v] + 16 <= vend)
-            __builtin_nontemporal_store(data[v] ^ m[v], reinterpret_cast<u32x4*>(a.wire + va[v]));
+        for (int v = 0; v < VPT; ++v) {
+            if (any_bits(m[v]) && va[v] + 16 <= vend)
+                __builtin_nontemporal_store(data[v] ^ m[v], reinterpret_cast<u32x4*>(a.wire + va[v]));
+        }
+    } else {
+        // buffer resource over this tile (wave-uniform: built from kernel args + blockIdx)
+        const uint64_t room = vend > t0 ? vend - t0 : 0;
+        const uint32_t nrec = (uint32_t)(room < kT ? room : kT);
+        __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(a.wire + t0, 0, (int)nrec, 0x00020000);
+#pragma unroll
+        for (int v = 0; v < VPT; ++v) {
+            if (any_bits(m[v]) && va[v] + 16 <= vend) {
+                const u32x4 x = data[v] ^ m[v];
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, x), rs,
+                    (uint32_t)(va[v] - t0), 0, STORE_AUX);
+            }
+        }
     }
     // the single vector that straddles the end of the wire: byte stores
     if (full_end != vend && full_end >= t0 && full_end < t0 + kT) {
@@ -1365,6 +1385,7 @@ struct uvhttp_ws_gpu_engine {
     Workspace ws;
     int timing;
     int tile_block, tile_vpt;  // payload kernel shape, 0 = automatic
+    int store_aux;             // payload store cache policy (0 = nt global store, 18 = sc1|nt)
     void* ss_mem;              // stream-decode scratch
     uint32_t ss_frames, ss_streams;
     StreamScratch ss;
@@ -1401,6 +1422,8 @@ int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out) {
     uvhttp_ws_gpu_engine_t* e = (uvhttp_ws_gpu_engine_t*)calloc(1, sizeof(*e));
     if (!e) return UVHTTP_WS_GPU_ENOMEM;
     e->device = device;
+    e->store_aux = 18;
+    if (const char* sp = getenv("UVHTTP_WS_STORE_POLICY")) e->store_aux = atoi(sp) == 18 ? 18 : 0;
     *out = e;
     return UVHTTP_WS_GPU_OK;
 }
@@ -1609,7 +1632,10 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
         const uint32_t grid_p = (uint32_t)((n_ptiles - tb) < max_tiles ? (n_ptiles - tb) : max_tiles);
 #define UVWS_LAUNCH(B, V)                                                                        \
     if (blk == B && vpt == V) {                                                                  \
-        if (!arena)                                                                              \
+        if (!arena && e->store_aux == 18)                                                        \
+            hipLaunchKernelGGL((k_unmask_inplace<B, V, 18>), dim3(grid_p), dim3(B), 0, s, a,     \
+                               d_desc, e->ws, tb);                                               \
+        else if (!arena)                                                                         \
             hipLaunchKernelGGL((k_unmask_inplace<B, V>), dim3(grid_p), dim3(B), 0, s, a, d_desc, \
                                e->ws, tb);                                                       \
         else                                                                                     \
