@@ -126,6 +126,7 @@ def cpu_baseline(cfg_name, target_s=10.0):
         if el2 >= target_s * 0.5 or spasses >= 1000:
             break
     stream_gibs = sp / el2 / GIB
+    mt = cpu_baseline_threads(L, _oracle, cfg_name, target_s * 0.5)
     cc = subprocess.run(["gcc", "--version"], capture_output=True, text=True).stdout
     return {
         "value": round(unmask_gibs, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
@@ -136,7 +137,47 @@ def cpu_baseline(cfg_name, target_s=10.0):
         "stream_decode_sample": f"process_data fed 16 KiB reads, {spasses} passes in {el2:.1f} s",
         "compiler": cc.splitlines()[0] if cc else "gcc", "flags": "-O2 -DNDEBUG",
         "cpu": cpu_model(), "host_threads": os.cpu_count(),
+        "multi_thread": mt,
     }
+
+
+def cpu_baseline_threads(L, orc, cfg_name, seconds):
+    """SURVEY §8(d)'s all-cores variant: T threads, one independent connection stream each
+    (its own ~32 MiB sample of the workload), header parse + apply_mask, timed together.
+    T = this process's CPU share (16 on the GPU box; UVHTTP_WS_CPU_THREADS overrides)."""
+    import threading
+    n, plen, frag, _ = CONFIGS[cfg_name]
+    try:
+        share = len(os.sched_getaffinity(0))
+    except AttributeError:
+        share = os.cpu_count() or 1
+    T = int(os.environ.get("UVHTTP_WS_CPU_THREADS", min(16, share)))
+    sample = max(1, min(n, (32 << 20) // max(plen, 1)))
+    bufs = [orc.gen_frames(sample, plen, SEED + 1 + t, fragmented=frag, total=sample)
+            for t in range(T)]
+    done = [0] * T
+    start = threading.Barrier(T + 1)
+    stop = threading.Event()
+
+    def work(t):
+        w, stride = bufs[t]
+        ptr = orc._ptr(w)
+        start.wait()
+        while not stop.is_set():  # ctypes drops the GIL inside the call
+            done[t] += L.oracle_unmask_frames(ptr, sample, stride)
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(T)]
+    for x in th:
+        x.start()
+    start.wait()
+    t0 = time.perf_counter()
+    time.sleep(seconds)
+    stop.set()
+    for x in th:
+        x.join()
+    el = time.perf_counter() - t0
+    return {"value": round(sum(done) / el / GIB, 3), "unit": "GiB/s", "cores": T,
+            "sample": f"{T} threads x {sample} frames x {plen} B, {el:.1f} s"}
 
 
 def pmc_traffic(cfg_name, mode):
