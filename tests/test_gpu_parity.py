@@ -449,3 +449,23 @@ def test_config_c5_chunk(torch, eng):
         assert np.array_equal(got, ow), i
     del d
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("fpt", [1, 2, 4, 8, 16])
+def test_plan_frames_per_lane_identical(torch, fpt, monkeypatch):
+    """k_plan's frames-per-lane variants (and multi-window look-back: 40 000 frames are 157
+    blocks at one frame per lane) give the oracle's statuses, bytes, summaries and messages,
+    for valid batches and batches with a failure deep inside."""
+    import uvhttp_amd as U
+    monkeypatch.setenv("UVHTTP_WS_PLAN_FPT", str(fpt))
+    e = U.GpuEngine(0)
+    try:
+        rng = random.Random(1000 + fpt)
+        for p_bad in (0.0, 0.00005):
+            wire, offs = _rand_batch(rng, 40000, [0, 1, 7, 125, 126, 300], p_ctrl=0.05,
+                                     p_frag=0.3, p_bad=p_bad)
+            for compact in (False, True):
+                ref, got = _run_both(torch, e, wire, 40000, offs=offs, mm=0, compact=compact)
+                _compare(ref, got, compact)
+    finally:
+        e.close()

@@ -27,10 +27,20 @@ def torch():
     return t
 
 
-@pytest.fixture(scope="module")
-def eng(torch):
+@pytest.fixture(scope="module", params=["lane", "wave"])
+def eng(torch, request):
+    """Both frame-discovery walks (a lane or a wave per connection) must decode alike."""
+    import os
     import uvhttp_amd as U
-    e = U.GpuEngine(0)
+    old = os.environ.get("UVHTTP_WS_WALK")
+    os.environ["UVHTTP_WS_WALK"] = request.param
+    try:
+        e = U.GpuEngine(0)
+    finally:
+        if old is None:
+            os.environ.pop("UVHTTP_WS_WALK", None)
+        else:
+            os.environ["UVHTTP_WS_WALK"] = old
     yield e
     e.close()
 

@@ -1,0 +1,87 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of two builds of libuvhttp_ws_amd.so in ONE process on one device.
+
+  python tools/ab_lib.py LIB_A LIB_B cfg:mode [cfg:mode ...]     (mode: inplace | compact)
+
+LIB_B may be "tree" for the in-tree build.  Each round runs K decode steps with engine A,
+then K with engine B, on the same device buffers; reports the median whole-step time
+(torch events around the K steps) and the median payload-kernel time (engine timing)."""
+import os
+import statistics
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import torch  # noqa: E402
+
+import uvhttp_amd as U  # noqa: E402
+
+CFG = {"c2": (65536, 4096, False), "c3": (65536, 65536, False), "c4": (1048576, 256, True)}
+
+
+def main():
+    libs = [U.load_library(p if p != "tree" else U.LIB_PATH) for p in sys.argv[1:3]]
+    names = [os.path.basename(p) for p in sys.argv[1:3]]
+    rounds, K = 7, 20
+    st = torch.cuda.current_stream()
+    for pair in sys.argv[3:]:
+        cfg, mode = pair.split(":")
+        n, plen, frag = CFG[cfg]
+        engs = [U.GpuEngine(0, library=L) for L in libs]
+        stride = U.gen_frame_stride(plen)
+        wl = stride * n
+        wire = torch.empty(wl + 64, dtype=torch.uint8, device="cuda")
+        engs[0].gen_frames(wire, n, plen, 7, opcode0=2, fragmented=frag)
+        mm = 256 << 20
+        outs = []
+        for e in engs:
+            desc, summ = e.alloc_outputs(n)
+            arena = torch.empty(n * plen + 64, dtype=torch.uint8, device="cuda") if mode == "compact" else None
+            msgs = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+            outs.append((desc, summ, arena, msgs))
+
+        def run(k):
+            e = engs[k]
+            desc, summ, arena, msgs = outs[k]
+            if mode == "inplace":
+                e.decode_inplace(wire, n, stride=stride, max_message_size=mm, wire_len=wl,
+                                 desc=desc, summary=summ, stream=st)
+            else:
+                e.decode_compact(wire, n, arena, stride=stride, max_message_size=mm,
+                                 wire_len=wl, desc=desc, msgs=msgs, summary=summ, stream=st)
+
+        step = [[], []]
+        kern = [[], []]
+        for r in range(rounds):
+            for k in (0, 1):
+                for _ in range(3):
+                    run(k)
+                engs[k].set_timing(True)
+                engs[k].kernel_time()
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(st)
+                for _ in range(K):
+                    run(k)
+                b.record(st)
+                b.synchronize()
+                engs[k].set_timing(False)
+                ms, cnt = engs[k].kernel_time()
+                if r:
+                    step[k].append(a.elapsed_time(b) / K)
+                    kern[k].append(ms / max(cnt, 1))
+        for k in (0, 1):
+            s = engs[k].read_summary(outs[k][1])
+            assert s["n_delivered"] == n and s["status"] == 0, (names[k], s)
+        ms = [statistics.median(x) for x in step]
+        ks = [statistics.median(x) for x in kern]
+        print(f"{cfg} {mode:8s} step A {ms[0]*1e3:9.1f} us  B {ms[1]*1e3:9.1f} us  "
+              f"({(ms[0]/ms[1]-1)*100:+.1f}% B faster) | payload A {ks[0]*1e3:8.1f} B {ks[1]*1e3:8.1f} us "
+              f"| other A {(ms[0]-ks[0])*1e3:6.1f} B {(ms[1]-ks[1])*1e3:6.1f} us", flush=True)
+        for e in engs:
+            e.close()
+        del wire, outs
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

@@ -17,7 +17,7 @@ for pair in "$@"; do
 import csv, glob, sys
 f = glob.glob(sys.argv[1] + "/**/*kernel_stats.csv", recursive=True)[0]
 for r in csv.DictReader(open(f)):
-    n = r["Name"].split("(")[0].replace("(anonymous namespace)::", "")
+    n = r["Name"].replace("(anonymous namespace)::", "").split("(")[0]
     print(f'{n[:60]:60s} calls {r["Calls"]:>4s} avg {float(r["AverageNs"])/1e3:9.2f} us')
 PY
 done

@@ -150,15 +150,21 @@ _LIB = None
 def lib() -> C.CDLL:
     """Load the product library.  Raises if it has not been built (no fallback)."""
     global _LIB
-    if _LIB is not None:
-        return _LIB
-    if not os.path.exists(LIB_PATH):
-        raise ImportError(f"{LIB_PATH} missing: run `make` (or __graft_entry__.build())")
+    if _LIB is None:
+        _LIB = load_library(LIB_PATH)
+    return _LIB
+
+
+def load_library(path: str) -> C.CDLL:
+    """Load a build of libuvhttp_ws_amd.so from `path` and declare its entry points (lib()
+    uses the in-tree build; tools/ab_lib.py loads a second build beside it for A/B runs)."""
+    if not os.path.exists(path):
+        raise ImportError(f"{path} missing: run `make` (or __graft_entry__.build())")
     try:  # share torch's HIP runtime (same SONAME) so torch device pointers are valid
         import torch  # noqa: F401
     except ImportError:
         pass
-    L = C.CDLL(LIB_PATH)
+    L = C.CDLL(path)
     vp, u32, u64, i32 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int32
     sig = {
         "uvhttp_ws_amd_version": (C.c_char_p, []),
@@ -206,7 +212,6 @@ def lib() -> C.CDLL:
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    _LIB = L
     return L
 
 
@@ -308,10 +313,10 @@ class GpuEngine:
     DESC_BYTES = 32
     MSG_BYTES = 32
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, library: C.CDLL = None):
         import torch
         self.torch = torch
-        L = lib()
+        L = library or lib()
         self._L = L
         self.device = device
         h = C.c_void_p()

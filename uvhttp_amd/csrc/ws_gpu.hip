@@ -2,19 +2,18 @@
 //
 // Replaces, for frames already resident in HBM, the per-frame work of
 // src/uvhttp_websocket.c (adam-ikari/uvhttp v2.7.0):
-//   uvhttp_ws_parse_frame_header  :133-185   -> k_parse (one lane per frame)
-//   validation in process_data    :851-932   -> k_parse (local) + k_resolve (state machine)
-//   fragment state machine        :950-1015  -> k_resolve (segmented scan, no serial walk)
+//   uvhttp_ws_parse_frame_header  :133-185   -> parse_one (one lane per frame)
+//   validation in process_data    :851-932   -> parse_one (local) + resolve_one (state machine)
+//   fragment state machine        :950-1015  -> resolve_one (segmented scan, no serial walk)
 //   uvhttp_ws_fragment_append     :781-822   -> prefix offsets + k_gather_compact
 //   uvhttp_ws_apply_mask          :188-197   -> k_unmask_inplace / k_gather_compact
 //
-// Pipeline per decode call (one stream, no host sync):
-//   k_parse    frames -> desc[] (header, key, local status), per-block scan aggregates,
-//              tile -> first-frame map for the in-place tiles
-//   k_scan     one workgroup: exclusive scan of the block aggregates
-//   k_resolve  frames -> state machine status, message ids, arena offsets, first_bad
-//   k_unmask_inplace / k_gather_compact   the HBM-bound payload pass (the roofline kernel)
-//   k_finalize statuses after the first failure -> SKIPPED, batch summary
+// Pipeline per decode call (one stream, no host sync, two launches):
+//   k_plan     frames -> desc[] (header, key, status), single-pass decoupled look-back scan,
+//              state machine, message ids, arena offsets, first failure, tile -> first-frame
+//              maps; its last block writes the batch summary
+//   k_unmask_inplace / k_gather_compact   the HBM-bound payload pass (the roofline kernel);
+//              its first lanes also mark frames after the first failure SKIPPED
 //
 // The payload pass is pure streaming integer work: 16-byte loads/stores per lane, the
 // 4-byte key rotated once per (vector, frame) into a 32-bit word, no LDS on the fast path,
@@ -46,11 +45,15 @@ struct ScanElem {
     uint64_t data_pay;   // sum: payload bytes of data frames (arena offset)
     uint64_t all_pay;    // sum: payload bytes of all frames
     uint64_t seg_pay;    // segmented sum: data payload since the latest start
-    uint32_t seg_flag;   // segment contains a start
     uint32_t n_fin;      // sum: data frames with FIN (completed messages)
     uint32_t n_close;    // sum: CLOSE frames
-    uint32_t head;       // segment (connection) start: the scan restarts here
+    uint32_t bits;       // kSegFlag | kHead | kLastOpen | start opcode << 4
 };
+// bits: the segment contains a start; a connection starts here (the scan restarts); the
+// latest data frame leaves a message open (FIN=0 and not a zero-length start, whose empty
+// first fragment allocates nothing: src/uvhttp_websocket.c:794-816 + :964); the opcode of
+// the latest start (the message's opcode)
+constexpr uint32_t kSegFlag = 1u, kHead = 2u, kLastOpen = 4u, kOpShift = 4u, kOpMask = 0xF0u;
 
 __device__ __host__ inline ScanElem scan_identity() {
     ScanElem e;
@@ -59,26 +62,26 @@ __device__ __host__ inline ScanElem scan_identity() {
     e.data_pay = 0;
     e.all_pay = 0;
     e.seg_pay = 0;
-    e.seg_flag = 0;
     e.n_fin = 0;
     e.n_close = 0;
-    e.head = 0;
+    e.bits = 0;
     return e;
 }
 
 // segmented: a connection start in b discards everything before it
 __device__ __host__ inline ScanElem scan_combine(const ScanElem& a, const ScanElem& b) {
-    if (b.head) return b;
+    if (b.bits & kHead) return b;
     ScanElem r;
     r.last_data = a.last_data > b.last_data ? a.last_data : b.last_data;
     r.last_start = a.last_start > b.last_start ? a.last_start : b.last_start;
     r.data_pay = a.data_pay + b.data_pay;
     r.all_pay = a.all_pay + b.all_pay;
-    r.seg_pay = b.seg_flag ? b.seg_pay : a.seg_pay + b.seg_pay;
-    r.seg_flag = a.seg_flag | b.seg_flag;
+    r.seg_pay = (b.bits & kSegFlag) ? b.seg_pay : a.seg_pay + b.seg_pay;
     r.n_fin = a.n_fin + b.n_fin;
     r.n_close = a.n_close + b.n_close;
-    r.head = a.head;
+    const uint32_t open = (b.last_data >= 0 ? b.bits : a.bits) & kLastOpen;
+    const uint32_t op = (b.last_start >= 0 ? b.bits : a.bits) & kOpMask;
+    r.bits = ((a.bits | b.bits) & kSegFlag) | (a.bits & kHead) | open | op;
     return r;
 }
 
@@ -88,8 +91,8 @@ __device__ inline bool is_data_op(uint32_t op) { return op <= 2u; }
 // state machine to consider it; invalid frames never precede a delivered frame)
 __device__ inline ScanElem scan_elem_of(const uvhttp_ws_frame_desc_t& d, int32_t i, bool head) {
     ScanElem e = scan_identity();
-    e.head = head ? 1u : 0u;
     const uint32_t op = d.opcode;
+    const bool fin = d.flags & UVHTTP_WS_FLAG_FIN;
     e.all_pay = d.payload_len;
     if (is_data_op(op)) {
         e.last_data = i;
@@ -97,12 +100,14 @@ __device__ inline ScanElem scan_elem_of(const uvhttp_ws_frame_desc_t& d, int32_t
         e.seg_pay = d.payload_len;
         if (op != 0) {
             e.last_start = i;
-            e.seg_flag = 1;
+            e.bits |= kSegFlag | (op << kOpShift);
         }
-        e.n_fin = (d.flags & UVHTTP_WS_FLAG_FIN) ? 1u : 0u;
+        if (!fin && !(op != 0 && d.payload_len == 0)) e.bits |= kLastOpen;
+        e.n_fin = fin ? 1u : 0u;
     } else if (op == 8) {
         e.n_close = 1;
     }
+    if (head) e.bits |= kHead;
     return e;
 }
 
@@ -113,11 +118,34 @@ __device__ inline ScanElem shfl_up_elem(const ScanElem& e, int delta) {
     r.data_pay = __shfl_up(e.data_pay, delta, 64);
     r.all_pay = __shfl_up(e.all_pay, delta, 64);
     r.seg_pay = __shfl_up(e.seg_pay, delta, 64);
-    r.seg_flag = __shfl_up(e.seg_flag, delta, 64);
     r.n_fin = __shfl_up(e.n_fin, delta, 64);
     r.n_close = __shfl_up(e.n_close, delta, 64);
-    r.head = __shfl_up(e.head, delta, 64);
+    r.bits = __shfl_up(e.bits, delta, 64);
     return r;
+}
+
+__device__ inline ScanElem shfl_down_elem(const ScanElem& e, int delta) {
+    ScanElem r;
+    r.last_data = __shfl_down(e.last_data, delta, 64);
+    r.last_start = __shfl_down(e.last_start, delta, 64);
+    r.data_pay = __shfl_down(e.data_pay, delta, 64);
+    r.all_pay = __shfl_down(e.all_pay, delta, 64);
+    r.seg_pay = __shfl_down(e.seg_pay, delta, 64);
+    r.n_fin = __shfl_down(e.n_fin, delta, 64);
+    r.n_close = __shfl_down(e.n_close, delta, 64);
+    r.bits = __shfl_down(e.bits, delta, 64);
+    return r;
+}
+
+// ordered wave reduction: lane 0 ends with v[63] (+) ... (+) v[0] — lane 63 is the OLDEST
+__device__ inline ScanElem wave_reduce_newest_first(ScanElem v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const ScanElem o = shfl_down_elem(v, d);
+        if (lane + d < 64) v = scan_combine(o, v);
+    }
+    return v;
 }
 
 // Block-wide exclusive scan (256 threads = 4 waves): wave-level Hillis-Steele over the 64
@@ -152,13 +180,35 @@ __device__ ScanElem block_exclusive_scan(ScanElem v, ScanElem* total) {
 // ------------------------------------------------------------------------------------
 // workspace layout (device), carved from one allocation
 // ------------------------------------------------------------------------------------
-struct Workspace {
-    ScanElem* block_agg;   // [n_blocks]: aggregates, then exclusive prefixes within a group
-    ScanElem* group_agg;   // [n_groups + 1]: group totals -> exclusive prefixes + grand total
-    uint32_t* tile_first;  // [n_tiles]: first frame whose slot contains the tile start
-    uint32_t* first_bad;   // [1]
-    uint32_t* arena_first; // [n_arena_tiles]
+struct alignas(16) LbRec {
+    uint32_t w[16];
 };
+
+struct Workspace {
+    ScanElem* block_agg;   // [n_blocks]: k_plan block aggregates (build: u64 block sums)
+    ScanElem* group_agg;   // build only: u64 group sums
+    ScanElem* block_incl;  // [n_blocks]: k_plan inclusive prefixes (look-back "P" values)
+    ScanElem* block_excl;  // [n_blocks]: k_plan exclusive prefixes (summary)
+    LbRec* rec_a;          // [n_blocks]: look-back aggregate records
+    LbRec* rec_p;          // [n_blocks]: look-back inclusive-prefix records
+    uint32_t* counters;    // [0] block ticket, [1] blocks done; reset by the last block
+    uint64_t* tile_first;  // [n_tiles]: tagged first frame whose slot contains the tile start
+    uint64_t* first_bad;   // [1]: tagged first failing frame of the batch
+    uint64_t* arena_first; // [n_arena_tiles]: tagged first data frame of the arena tile
+};
+
+// Epoch tags.  Every decode call gets a fresh 32-bit epoch; map entries and first_bad are
+// stored as (epoch << 32) | ~frame and claimed with atomicMax, so within a call the smallest
+// frame wins and entries left by earlier calls read as "unclaimed" — no reset pass.
+__device__ inline uint64_t tag_of(uint32_t epoch, uint32_t frame) {
+    return ((uint64_t)epoch << 32) | (uint32_t)~frame;
+}
+__device__ inline void tag_claim(uint64_t* p, uint32_t epoch, uint32_t frame) {
+    atomicMax(reinterpret_cast<unsigned long long*>(p), (unsigned long long)tag_of(epoch, frame));
+}
+__device__ inline uint32_t tag_get(uint64_t v, uint32_t epoch, uint32_t none) {
+    return (uint32_t)(v >> 32) == epoch ? ~(uint32_t)v : none;
+}
 
 // extra scratch of the stream decode (one allocation per engine, grown on demand)
 struct StreamScratch {
@@ -190,7 +240,14 @@ struct BatchArgs {
     const uint32_t* n_dev;
     uint64_t* open_after;
     uint32_t* seg_bad;
+    uint32_t epoch;          // tag of this call's map / first_bad entries
+    uvhttp_ws_batch_summary_t* summary;  // batch mode: written by k_finalize
+    uint32_t plan_frames;    // frames per k_plan block (kBlock * FPT)
 };
+
+__device__ inline uint32_t first_bad_of(const BatchArgs& a, const Workspace& ws, uint32_t n) {
+    return tag_get(*ws.first_bad, a.epoch, n);
+}
 
 __device__ inline uint64_t frame_start(const BatchArgs& a, uint32_t i) {
     return a.frame_off ? a.frame_off[i] : (uint64_t)i * a.frame_stride;
@@ -241,203 +298,142 @@ __device__ inline uint32_t rotr32(uint32_t x, uint32_t s) {
 }
 
 // ------------------------------------------------------------------------------------
-// k_parse: one lane per frame.  Header parse + every check process_data makes before the
-// state machine (src/uvhttp_websocket.c:832-932), in the reference's order, on the bytes
-// the batch contract feeds (include/uvhttp_ws_amd.h "Batch semantics").
+// parse_one: frame i's header parse + every check process_data makes before the state
+// machine (src/uvhttp_websocket.c:832-932), in the reference's order, on the bytes the
+// batch contract feeds (include/uvhttp_ws_amd.h "Batch semantics").  Writes desc[i] and
+// returns the frame's scan element.
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_parse(BatchArgs a, uvhttp_ws_frame_desc_t* desc,
-                                                  Workspace ws) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t n = nframes(a);
-    if (blockIdx.x == 0 && threadIdx.x == 0) *ws.first_bad = n;
-    ScanElem elem = scan_identity();
-    if (i < n) {
-        const SegInfo g = seg_info(a, i, n);
-        const uint64_t o = frame_start(a, i);
-        const uint64_t slot = g.end > o ? g.end - o : 0;
-        const bool last = g.last;
-        const uint8_t* p = a.wire + o;
+// the at most 14 header bytes (2 + 8 length + 4 key) of the frame at o in one 16-byte load;
+// bytes past the frame's slot are loaded but never used (only the last 16 bytes of the wire
+// go bytewise)
+__device__ inline u32x4 load_header(const BatchArgs& a, uint64_t o) {
+    if (o + 16 <= a.wire_len) {
+        u32x4 v;
+        __builtin_memcpy(&v, a.wire + o, 16);
+        return v;
+    }
+    const uint64_t avail = a.wire_len > o ? a.wire_len - o : 0;
+    uint32_t t[4] = {0, 0, 0, 0};
+    for (uint32_t k = 0; k < 16 && k < avail; ++k) t[k >> 2] |= (uint32_t)a.wire[o + k] << (8 * (k & 3));
+    return u32x4{t[0], t[1], t[2], t[3]};
+}
 
-        uvhttp_ws_frame_desc_t d;
-        d.payload_off = o;  // frames that do not parse keep a monotonic (empty) payload
-        d.payload_len = 0;
-        d.masking_key = 0;
-        d.message = 0;
-        d.opcode = 0;
-        d.flags = 0;
-        d.header_size = 0;
-        d.status = UVHTTP_WS_FRAME_OK;
-        d.wire_len = 0;
+__device__ inline ScanElem parse_hdr(const BatchArgs& a, uvhttp_ws_frame_desc_t* desc, uint32_t i,
+                                     const SegInfo& g, uint64_t o, u32x4 hv) {
+    const uint64_t slot = g.end > o ? g.end - o : 0;
+    const bool last = g.last;
 
-        // the at most 14 header bytes (2 + 8 length + 4 key) in one 16-byte load; bytes past
-        // the slot are loaded but never used (only the last 16 bytes of the wire go bytewise)
-        uint32_t hw0 = 0, hw1 = 0, hw2 = 0, hw3 = 0;
-        if (o + 16 <= a.wire_len) {
-            u32x4 v;
-            __builtin_memcpy(&v, p, 16);
-            hw0 = v.x, hw1 = v.y, hw2 = v.z, hw3 = v.w;
-        } else {
-            const uint64_t avail = a.wire_len > o ? a.wire_len - o : 0;
-            uint32_t t[4] = {0, 0, 0, 0};
-            for (uint32_t k = 0; k < 16 && k < avail; ++k) t[k >> 2] |= (uint32_t)p[k] << (8 * (k & 3));
-            hw0 = t[0], hw1 = t[1], hw2 = t[2], hw3 = t[3];
-        }
-        const uint64_t hlo = (uint64_t)hw0 | ((uint64_t)hw1 << 32);
-        const uint64_t hhi = (uint64_t)hw2 | ((uint64_t)hw3 << 32);
-        auto hb = [&](int k) -> uint32_t {  // header byte k (k is a constant after inlining)
-            return (uint32_t)((k < 8 ? hlo >> (8 * k) : hhi >> (8 * (k - 8))) & 0xFF);
-        };
+    uvhttp_ws_frame_desc_t d;
+    d.payload_off = o;  // frames that do not parse keep a monotonic (empty) payload
+    d.payload_len = 0;
+    d.masking_key = 0;
+    d.message = 0;
+    d.opcode = 0;
+    d.flags = 0;
+    d.header_size = 0;
+    d.status = UVHTTP_WS_FRAME_OK;
+    d.wire_len = 0;
 
-        bool parsable = false, msb = false;
-        uint64_t plen = 0, wlen = 0;
-        uint32_t hsz = 2, b0 = 0, b1 = 0;
-        if (slot >= 2) {
-            b0 = hb(0);
-            b1 = hb(1);
-            const uint32_t code = b1 & 0x7F;
-            const uint32_t need = code == 126 ? 4 : code == 127 ? 10 : 2;
-            if (slot >= need) {
-                parsable = true;
-                if (need == 2) {
-                    plen = code;
-                } else if (need == 4) {
-                    plen = ((uint64_t)hb(2) << 8) | hb(3);
-                } else {
-                    plen = ((uint64_t)hb(2) << 56) | ((uint64_t)hb(3) << 48) | ((uint64_t)hb(4) << 40) |
-                           ((uint64_t)hb(5) << 32) | ((uint64_t)hb(6) << 24) | ((uint64_t)hb(7) << 16) |
-                           ((uint64_t)hb(8) << 8) | (uint64_t)hb(9);
+    const uint32_t hw0 = hv.x, hw1 = hv.y, hw2 = hv.z, hw3 = hv.w;
+    const uint64_t hlo = (uint64_t)hw0 | ((uint64_t)hw1 << 32);
+    const uint64_t hhi = (uint64_t)hw2 | ((uint64_t)hw3 << 32);
+    auto hb = [&](int k) -> uint32_t {  // header byte k (k is a constant after inlining)
+        return (uint32_t)((k < 8 ? hlo >> (8 * k) : hhi >> (8 * (k - 8))) & 0xFF);
+    };
+
+    bool parsable = false, msb = false;
+    uint64_t plen = 0, wlen = 0;
+    uint32_t hsz = 2, b0 = 0, b1 = 0;
+    if (slot >= 2) {
+        b0 = hb(0);
+        b1 = hb(1);
+        const uint32_t code = b1 & 0x7F;
+        const uint32_t need = code == 126 ? 4 : code == 127 ? 10 : 2;
+        if (slot >= need) {
+            parsable = true;
+            if (need == 2) {
+                plen = code;
+            } else if (need == 4) {
+                plen = ((uint64_t)hb(2) << 8) | hb(3);
+            } else {
+                plen = ((uint64_t)hb(2) << 56) | ((uint64_t)hb(3) << 48) | ((uint64_t)hb(4) << 40) |
+                       ((uint64_t)hb(5) << 32) | ((uint64_t)hb(6) << 24) | ((uint64_t)hb(7) << 16) |
+                       ((uint64_t)hb(8) << 8) | (uint64_t)hb(9);
+            }
+            msb = (need == 10) && (plen >> 63);
+            hsz = need;
+            if (!msb) {
+                const uint32_t m = (b1 >> 7) ? 4u : 0u;
+                wlen = hsz + m + plen;
+                if (m && slot >= hsz + 4) {
+                    d.masking_key = need == 2 ? (uint32_t)(hlo >> 16)
+                                  : need == 4 ? (uint32_t)(hlo >> 32)
+                                              : (uint32_t)(hhi >> 16);
                 }
-                msb = (need == 10) && (plen >> 63);
-                hsz = need;
-                if (!msb) {
-                    const uint32_t m = (b1 >> 7) ? 4u : 0u;
-                    wlen = hsz + m + plen;
-                    if (m && slot >= hsz + 4) {
-                        d.masking_key = need == 2 ? (uint32_t)(hlo >> 16)
-                                      : need == 4 ? (uint32_t)(hlo >> 32)
-                                                  : (uint32_t)(hhi >> 16);
-                    }
-                    d.payload_off = o + hsz + m;
-                }
+                d.payload_off = o + hsz + m;
             }
         }
-        d.opcode = (uint8_t)(b0 & 0x0F);
-        d.flags = (uint8_t)(((b0 >> 7) & 1) | (((b1 >> 7) & 1) << 1) | (((b0 >> 6) & 1) << 2) |
-                            (((b0 >> 5) & 1) << 3) | (((b0 >> 4) & 1) << 4));
-        d.header_size = (uint8_t)hsz;
-        d.payload_len = plen;
-        d.wire_len = wlen > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)wlen;
-
-        int st = UVHTTP_WS_FRAME_OK;
-        uint64_t fed;
-        if (!a.streams && !last && (!parsable || (!msb && wlen != slot))) {
-            st = UVHTTP_WS_FRAME_ERR_LAYOUT;  // batch mode only: streams are walked
-            fed = slot;
-        } else {
-            fed = (last && parsable && !msb && wlen < slot) ? wlen : slot;
-        }
-        if (st == UVHTTP_WS_FRAME_OK) {
-            // recv buffer cap (:851-857): an empty buffer grows to max(max_frame, 64 KiB);
-            // a stream decode checks it once per connection in k_walk instead
-            const uint64_t mf = (uint64_t)(int64_t)g.max_frame_size;
-            const uint64_t cap = mf > 65536u ? mf : 65536u;
-            if (!a.streams && fed > cap) st = UVHTTP_WS_FRAME_ERR_BUFFER;
-            else if (!parsable) st = UVHTTP_WS_FRAME_INCOMPLETE;
-            else if (msb) st = UVHTTP_WS_FRAME_ERR_PARSE;
-            else if (d.flags & (UVHTTP_WS_FLAG_RSV1 | UVHTTP_WS_FLAG_RSV2 | UVHTTP_WS_FLAG_RSV3))
-                st = UVHTTP_WS_FRAME_ERR_RSV;
-            else if (d.opcode >= 8 && (plen > 125 || !(d.flags & UVHTTP_WS_FLAG_FIN)))
-                st = UVHTTP_WS_FRAME_ERR_CONTROL;
-            else if (g.is_server && !(d.flags & UVHTTP_WS_FLAG_MASK))
-                st = UVHTTP_WS_FRAME_ERR_UNMASKED;
-            else if (plen > mf) st = UVHTTP_WS_FRAME_ERR_TOO_BIG;
-            else if (fed < wlen) st = UVHTTP_WS_FRAME_INCOMPLETE;
-        }
-        d.status = (int8_t)st;
-        desc[i] = d;
-        if (st == UVHTTP_WS_FRAME_OK) elem = scan_elem_of(d, (int32_t)i, g.head);
-        elem.head = g.head ? 1u : 0u;
     }
-    // reset the tile -> first-frame maps (k_resolve fills them with atomicMin)
-    const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    const uint64_t gstride = (uint64_t)gridDim.x * kBlock;
-    for (uint64_t t = gtid; t < a.n_tiles; t += gstride) ws.tile_first[t] = kNoFrame;
-    for (uint64_t t = gtid; t < a.n_arena_tiles; t += gstride) ws.arena_first[t] = kNoFrame;
-    ScanElem total;
-    (void)block_exclusive_scan(elem, &total);
-    if (threadIdx.x == 0) ws.block_agg[blockIdx.x] = total;
-}
+    d.opcode = (uint8_t)(b0 & 0x0F);
+    d.flags = (uint8_t)(((b0 >> 7) & 1) | (((b1 >> 7) & 1) << 1) | (((b0 >> 6) & 1) << 2) |
+                        (((b0 >> 5) & 1) << 3) | (((b0 >> 4) & 1) << 4));
+    d.header_size = (uint8_t)hsz;
+    d.payload_len = plen;
+    d.wire_len = wlen > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)wlen;
 
-// k_scan_groups + k_scan_top: two-level exclusive scan of the per-block aggregates.  A
-// single workgroup is bound by one CU's memory bandwidth (~24 GB/s), so groups of 256
-// aggregates are scanned by separate workgroups, then one workgroup scans the group totals.
-// Block b's exclusive prefix = group_agg[b / 256] (+) block_agg[b].  256-thread workgroups
-// keep the 48-byte scan element in registers (a 1024-thread version spilled).
-constexpr int kScanThreads = kBlock;
-
-__global__ __launch_bounds__(kBlock) void k_scan_groups(Workspace ws, uint32_t n_blocks) {
-    const uint32_t b = blockIdx.x * kBlock + threadIdx.x;
-    const ScanElem v = b < n_blocks ? ws.block_agg[b] : scan_identity();
-    ScanElem total;
-    const ScanElem pre = block_exclusive_scan(v, &total);
-    if (b < n_blocks) ws.block_agg[b] = pre;
-    if (threadIdx.x == 0) ws.group_agg[blockIdx.x] = total;
-}
-
-__global__ __launch_bounds__(kBlock) void k_scan_top(Workspace ws, uint32_t n_groups) {
-    // up to 4 groups per thread (2^26 frames -> 2^18 blocks -> 1024 groups)
-    constexpr int kPer = 4;
-    ScanElem v[kPer];
-    ScanElem run = scan_identity();
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-        const uint32_t g = threadIdx.x * kPer + k;
-        v[k] = g < n_groups ? ws.group_agg[g] : scan_identity();
-        run = scan_combine(run, v[k]);
+    int st = UVHTTP_WS_FRAME_OK;
+    uint64_t fed;
+    if (!a.streams && !last && (!parsable || (!msb && wlen != slot))) {
+        st = UVHTTP_WS_FRAME_ERR_LAYOUT;  // batch mode only: streams are walked
+        fed = slot;
+    } else {
+        fed = (last && parsable && !msb && wlen < slot) ? wlen : slot;
     }
-    ScanElem total;
-    ScanElem pre = block_exclusive_scan(run, &total);
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-        const uint32_t g = threadIdx.x * kPer + k;
-        if (g < n_groups) ws.group_agg[g] = pre;
-        pre = scan_combine(pre, v[k]);
+    if (st == UVHTTP_WS_FRAME_OK) {
+        // recv buffer cap (:851-857): an empty buffer grows to max(max_frame, 64 KiB);
+        // a stream decode checks it once per connection in k_walk instead
+        const uint64_t mf = (uint64_t)(int64_t)g.max_frame_size;
+        const uint64_t cap = mf > 65536u ? mf : 65536u;
+        if (!a.streams && fed > cap) st = UVHTTP_WS_FRAME_ERR_BUFFER;
+        else if (!parsable) st = UVHTTP_WS_FRAME_INCOMPLETE;
+        else if (msb) st = UVHTTP_WS_FRAME_ERR_PARSE;
+        else if (d.flags & (UVHTTP_WS_FLAG_RSV1 | UVHTTP_WS_FLAG_RSV2 | UVHTTP_WS_FLAG_RSV3))
+            st = UVHTTP_WS_FRAME_ERR_RSV;
+        else if (d.opcode >= 8 && (plen > 125 || !(d.flags & UVHTTP_WS_FLAG_FIN)))
+            st = UVHTTP_WS_FRAME_ERR_CONTROL;
+        else if (g.is_server && !(d.flags & UVHTTP_WS_FLAG_MASK))
+            st = UVHTTP_WS_FRAME_ERR_UNMASKED;
+        else if (plen > mf) st = UVHTTP_WS_FRAME_ERR_TOO_BIG;
+        else if (fed < wlen) st = UVHTTP_WS_FRAME_INCOMPLETE;
     }
-    if (threadIdx.x == 0) ws.group_agg[n_groups] = total;
+    d.status = (int8_t)st;
+    desc[i] = d;
+    ScanElem elem = scan_identity();
+    if (st == UVHTTP_WS_FRAME_OK) elem = scan_elem_of(d, (int32_t)i, g.head);
+    else if (g.head) elem.bits = kHead;
+    return elem;
 }
 
-__device__ inline ScanElem block_prefix(const Workspace& ws, uint32_t b) {
-    return scan_combine(ws.group_agg[b / kScanThreads], ws.block_agg[b]);
+__device__ inline ScanElem parse_one(const BatchArgs& a, uvhttp_ws_frame_desc_t* desc, uint32_t i,
+                                     const SegInfo& g) {
+    const uint64_t o = frame_start(a, i);
+    return parse_hdr(a, desc, i, g, o, load_header(a, o));
 }
 
-// k_resolve: one lane per frame.  With E = scan over the frames of the same connection
-// before i, the state before frame i follows from the latest data frame p alone (all
-// frames before a delivered frame are valid): PENDING iff p exists, p has FIN=0, and p is
-// not a zero-length start (a zero-length first fragment allocates nothing, so
+// resolve_one: frame i's state-machine step.  With E = scan over the frames of the same
+// connection before i, the state before frame i follows from the latest data frame p alone
+// (all frames before a delivered frame are valid): PENDING iff p exists, p has FIN=0, and p
+// is not a zero-length start (a zero-length first fragment allocates nothing, so
 // fragmented_message stays NULL, src/uvhttp_websocket.c:794-816 + :964).  With no data
 // frame before i in its connection, the state is the connection's initial one.
-__global__ __launch_bounds__(kBlock) void k_resolve(BatchArgs a, uvhttp_ws_frame_desc_t* desc,
-                                                    uvhttp_ws_message_desc_t* msgs,
-                                                    Workspace ws) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t n = nframes(a);
-    ScanElem elem = scan_identity();
-    uvhttp_ws_frame_desc_t d;
-    SegInfo g;
-    if (i < n) {
-        d = desc[i];
-        g = seg_info(a, i, n);
-        if (d.status == UVHTTP_WS_FRAME_OK) elem = scan_elem_of(d, (int32_t)i, g.head);
-        elem.head = g.head ? 1u : 0u;
-    }
-    ScanElem total;
-    ScanElem ex = block_exclusive_scan(elem, &total);
-    if (i >= n) return;
-    ex = scan_combine(block_prefix(ws, blockIdx.x), ex);
+__device__ inline void resolve_one(const BatchArgs& a, uvhttp_ws_frame_desc_t* desc,
+                                   uvhttp_ws_message_desc_t* msgs, const Workspace& ws,
+                                   uint32_t i, uint32_t n, const SegInfo& g, ScanElem ex,
+                                   uvhttp_ws_frame_desc_t d) {
     if (g.head) ex = scan_identity();  // nothing of this connection precedes its first frame
 
     // in-place tiles whose start byte lies in this frame's span up to the next frame (frame
-    // 0 also owns the bytes before its start); atomicMin keeps the map deterministic even
+    // 0 also owns the bytes before its start); the max-of-tag claim keeps the smallest frame
     // when a bad offset table makes slots overlap
     {
         const uint64_t o = frame_start(a, i);
@@ -445,20 +441,14 @@ __global__ __launch_bounds__(kBlock) void k_resolve(BatchArgs a, uvhttp_ws_frame
         if (end > a.wire_len) end = a.wire_len;
         const uint64_t lo = (i == 0) ? 0 : o;
         for (uint64_t t = (lo + kMapTile - 1) / kMapTile; t * kMapTile < end && t < a.n_tiles; ++t)
-            atomicMin(&ws.tile_first[t], i);
+            tag_claim(&ws.tile_first[t], a.epoch, i);
     }
 
-    // fragment state before this frame
-    bool pending;
-    if (ex.last_data >= 0) {
-        const uvhttp_ws_frame_desc_t pd = desc[ex.last_data];
-        const bool p_start = pd.opcode != 0;
-        pending = !(pd.flags & UVHTTP_WS_FLAG_FIN) && !(p_start && pd.payload_len == 0);
-    } else {
-        pending = g.init_pending > 0;
-    }
+    // fragment state before this frame: the latest data frame of the connection, carried
+    // in the scan (no other block's descriptors are read)
+    const bool pending = ex.last_data >= 0 ? (ex.bits & kLastOpen) != 0 : g.init_pending > 0;
     // bytes of the open message so far (the connection's carried part when no start yet)
-    const uint64_t acc = ex.seg_flag ? ex.seg_pay : g.init_pending + ex.seg_pay;
+    const uint64_t acc = (ex.bits & kSegFlag) ? ex.seg_pay : g.init_pending + ex.seg_pay;
     uint64_t open_after = pending ? acc : 0;
 
     int st = d.status;
@@ -487,7 +477,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(BatchArgs a, uvhttp_ws_frame
                     m.len = before + d.payload_len;
                     m.first_frame = pending ? (uint32_t)ex.last_start : i;
                     m.last_frame = i;
-                    m.opcode = pending ? desc[ex.last_start].opcode : d.opcode;
+                    m.opcode = pending ? (uint8_t)((ex.bits & kOpMask) >> kOpShift) : d.opcode;
                     m.reserved = 0;
                     msgs[ex.n_fin] = m;
                 }
@@ -497,7 +487,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(BatchArgs a, uvhttp_ws_frame
                 const uint64_t lo = ex.data_pay, hi = ex.data_pay + d.payload_len;
                 for (uint64_t t = (lo + kMapTile - 1) / kMapTile; t * kMapTile < hi && t < a.n_arena_tiles;
                      ++t)
-                    atomicMin(&ws.arena_first[t], i);
+                    tag_claim(&ws.arena_first[t], a.epoch, i);
             }
         }
         desc[i].status = (int8_t)st;
@@ -508,8 +498,282 @@ __global__ __launch_bounds__(kBlock) void k_resolve(BatchArgs a, uvhttp_ws_frame
     if (a.open_after) a.open_after[i] = open_after;
     if (st != UVHTTP_WS_FRAME_OK) {
         if (a.seg_bad) atomicMin(&a.seg_bad[g.seg], i);
-        else atomicMin(ws.first_bad, i);
+        else tag_claim(ws.first_bad, a.epoch, i);
     }
+}
+
+// ------------------------------------------------------------------------------------
+// Single-pass decoupled look-back (one launch for parse + scan + state machine).
+// Blocks take tickets in launch order, so a block only ever waits on blocks that already
+// run.  A block publishes its aggregate ("A" record), then all 256 lanes look back at 256
+// predecessors at a time, combining aggregates until they meet a published inclusive
+// prefix ("P" record).  A record is 64 bytes: four 16-byte chunks, each 12 bytes of the
+// scan value + a 4-byte tag (epoch << 2 | kind), written and read as single device-coherent
+// (sc1) 16-byte accesses.  A reader accepts a record only when all four tags carry this
+// call's epoch and kind, so one round trip both polls and fetches — no flags, no L2
+// writeback or invalidate.  Polls are bounded so a defect cannot hang the device: on
+// exhaustion the block proceeds and its result is wrong (the parity tests catch that).
+// ------------------------------------------------------------------------------------
+constexpr uint32_t kRecAgg = 1, kRecPrefix = 2;
+constexpr uint32_t kMaxPolls = 1u << 20;
+constexpr int kAuxSc1 = 16;  // buffer-op cache policy: device scope (sc1)
+static_assert(sizeof(ScanElem) == 48, "scan value packs into 11 of the record's 12 data words");
+
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+
+__device__ inline __amdgpu_buffer_rsrc_t rec_rsrc(const LbRec* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<LbRec*>(base), 0, 0x7FFFFFFF, 0x00020000);
+}
+
+// the scan value as 11 words, in record order
+#define UVWS_ELEM_WORDS(e)                                                                   \
+    (uint32_t)(e).last_data, (uint32_t)(e).last_start, (uint32_t)(e).data_pay,               \
+        (uint32_t)((e).data_pay >> 32), (uint32_t)(e).all_pay, (uint32_t)((e).all_pay >> 32), \
+        (uint32_t)(e).seg_pay, (uint32_t)((e).seg_pay >> 32), (e).n_fin, (e).n_close, (e).bits
+
+__device__ inline void rec_store(LbRec* recs, uint32_t j, const ScanElem& v, uint32_t tag) {
+    const uint32_t w[12] = {UVWS_ELEM_WORDS(v), 0u};
+    const __amdgpu_buffer_rsrc_t rs = rec_rsrc(recs);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const u32x4v x = {w[3 * c], w[3 * c + 1], w[3 * c + 2], tag};
+        __builtin_amdgcn_raw_buffer_store_b128(x, rs, j * 64u + 16u * c, 0, kAuxSc1);
+    }
+}
+
+__device__ inline void rec_fetch(const LbRec* recs, uint32_t j, u32x4v x[4]) {
+    const __amdgpu_buffer_rsrc_t rs = rec_rsrc(recs);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) x[c] = __builtin_amdgcn_raw_buffer_load_b128(rs, j * 64u + 16u * c, 0, kAuxSc1);
+}
+
+__device__ inline bool rec_valid(const u32x4v x[4], uint32_t tag) {
+    return x[0].w == tag && x[1].w == tag && x[2].w == tag && x[3].w == tag;
+}
+
+__device__ inline ScanElem rec_value(const u32x4v x[4]) {
+    ScanElem e;
+    e.last_data = (int32_t)x[0].x;
+    e.last_start = (int32_t)x[0].y;
+    e.data_pay = (uint64_t)x[0].z | ((uint64_t)x[1].x << 32);
+    e.all_pay = (uint64_t)x[1].y | ((uint64_t)x[1].z << 32);
+    e.seg_pay = (uint64_t)x[2].x | ((uint64_t)x[2].y << 32);
+    e.n_fin = x[2].z;
+    e.n_close = x[3].x;
+    e.bits = x[3].y;
+    return e;
+}
+
+// exclusive prefix of block b (all threads call; the value is broadcast through LDS)
+__device__ ScanElem lookback_prefix(const Workspace& ws, uint32_t b, const ScanElem& agg,
+                                    uint32_t epoch) {
+    __shared__ ScanElem s_wave[kBlock / 64];
+    __shared__ ScanElem s_pre;
+    __shared__ int s_kstar;
+    __shared__ int s_go;
+    const uint32_t tag_a = (epoch << 2) | kRecAgg, tag_p = (epoch << 2) | kRecPrefix;
+    if (threadIdx.x == 0) {
+        if (b == 0) {
+            rec_store(ws.rec_p, 0, agg, tag_p);
+            s_pre = scan_identity();
+            ws.block_excl[0] = scan_identity();
+            ws.block_incl[0] = agg;
+        } else {
+            rec_store(ws.rec_a, b, agg, tag_a);
+        }
+    }
+    if (b == 0) {
+        __syncthreads();
+        return s_pre;
+    }
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    ScanElem run = scan_identity();  // thread 0: combination of the predecessors seen so far
+    int64_t end = b;                 // window: blocks [end - 256, end)
+    uint32_t polls = 0;
+    for (;;) {
+        const int64_t j = end - 1 - t;  // larger t = older block
+        ScanElem v = scan_identity();
+        bool is_p = j < 0, ready = j < 0;  // lanes before block 0: identity "P"
+        for (;;) {
+            if (!ready) {  // both records in one round trip
+                u32x4v xp[4], xa[4];
+                rec_fetch(ws.rec_p, (uint32_t)j, xp);
+                rec_fetch(ws.rec_a, (uint32_t)j, xa);
+                if (rec_valid(xp, tag_p)) {
+                    v = rec_value(xp), is_p = true, ready = true;
+                } else if (rec_valid(xa, tag_a)) {
+                    v = rec_value(xa), ready = true;
+                }
+            }
+            if (__syncthreads_and(ready) || ++polls > kMaxPolls) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        // nearest published prefix (smallest t with P)
+        if (t == 0) s_kstar = kBlock;
+        __syncthreads();
+        const uint64_t pm = __ballot(is_p);
+        if (lane == 0 && pm) atomicMin(&s_kstar, wave * 64 + __builtin_ctzll(pm));
+        __syncthreads();
+        const int kstar = s_kstar;
+        if (t > kstar || j < 0) v = scan_identity();
+        v = wave_reduce_newest_first(v);
+        if (lane == 0) s_wave[wave] = v;
+        __syncthreads();
+        if (t == 0) {
+            ScanElem w = scan_identity();
+#pragma unroll
+            for (int k = kBlock / 64 - 1; k >= 0; --k) w = scan_combine(w, s_wave[k]);
+            run = scan_combine(w, run);
+            s_go = (kstar < kBlock || polls > kMaxPolls) ? 0 : 1;
+        }
+        __syncthreads();
+        if (!s_go) break;
+        end -= kBlock;
+    }
+    if (t == 0) {
+        s_pre = run;
+        const ScanElem incl = scan_combine(run, agg);
+        ws.block_excl[b] = run;
+        ws.block_incl[b] = incl;
+        rec_store(ws.rec_p, b, incl, tag_p);
+    }
+    __syncthreads();
+    return s_pre;
+}
+
+// k_plan: one launch per decode: parse -> block scan -> look-back -> state machine.  Each
+// lane owns FPT consecutive frames (FPT > 1 keeps the block count, and with it the look-back
+// chain, short for large batches): pass 1 parses them and reduces their scan elements,
+// pass 2 (after the block's prefix is known) re-reads their descriptors and runs the state
+// machine in frame order.  The block holding the last ticket resets the counter for the
+// next call.
+template <int FPT>
+__global__ __launch_bounds__(kBlock) void k_plan(BatchArgs a, uvhttp_ws_frame_desc_t* desc,
+                                                 uvhttp_ws_message_desc_t* msgs, Workspace ws) {
+    __shared__ uint32_t s_ticket;
+    if (threadIdx.x == 0) {
+        const uint32_t t =
+            __hip_atomic_fetch_add(&ws.counters[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t + 1 == gridDim.x)
+            __hip_atomic_store(&ws.counters[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_ticket = t;
+    }
+    __syncthreads();
+    const uint32_t b = s_ticket;
+    const uint32_t n = nframes(a);
+    const uint32_t i0 = (b * kBlock + threadIdx.x) * FPT;
+    if (FPT == 1) {
+        SegInfo g;
+        ScanElem elem = scan_identity();
+        if (i0 < n) {
+            g = seg_info(a, i0, n);
+            elem = parse_one(a, desc, i0, g);
+        }
+        ScanElem agg;
+        const ScanElem local = block_exclusive_scan(elem, &agg);
+        const ScanElem pre = lookback_prefix(ws, b, agg, a.epoch);
+        if (i0 < n) resolve_one(a, desc, msgs, ws, i0, n, g, scan_combine(pre, local), desc[i0]);
+        return;
+    }
+    // pass 1: all header loads of the lane's frames in flight together, then parse
+    ScanElem tagg = scan_identity();
+    {
+        uint64_t o[FPT];
+        u32x4 hv[FPT];
+#pragma unroll
+        for (int k = 0; k < FPT; ++k) o[k] = i0 + k < n ? frame_start(a, i0 + k) : 0;
+#pragma unroll
+        for (int k = 0; k < FPT; ++k) hv[k] = i0 + k < n ? load_header(a, o[k]) : u32x4{0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < FPT; ++k) {
+            const uint32_t i = i0 + k;
+            if (i < n) tagg = scan_combine(tagg, parse_hdr(a, desc, i, seg_info(a, i, n), o[k], hv[k]));
+        }
+    }
+    ScanElem agg;
+    const ScanElem local = block_exclusive_scan(tagg, &agg);
+    ScanElem run = scan_combine(lookback_prefix(ws, b, agg, a.epoch), local);
+    // pass 2: the lane's descriptors (its own pass-1 stores) loaded together, then the state
+    // machine in frame order
+    uvhttp_ws_frame_desc_t dv[FPT];
+#pragma unroll
+    for (int k = 0; k < FPT; ++k)
+        if (i0 + k < n) dv[k] = desc[i0 + k];
+#pragma unroll
+    for (int k = 0; k < FPT; ++k) {
+        const uint32_t i = i0 + k;
+        if (i < n) {
+            const SegInfo g = seg_info(a, i, n);
+            ScanElem e = scan_identity();
+            if (dv[k].status == UVHTTP_WS_FRAME_OK) e = scan_elem_of(dv[k], (int32_t)i, g.head);
+            else if (g.head) e.bits = kHead;
+            resolve_one(a, desc, msgs, ws, i, n, g, run, dv[k]);
+            run = scan_combine(run, e);
+        }
+    }
+}
+
+// summary of a batch decode, after k_plan (one wave of k_finalize): E(nb) is
+// the exclusive scan value at the first failing frame (or the total)
+__device__ void write_summary(const BatchArgs& a, const uvhttp_ws_frame_desc_t* desc,
+                              const Workspace& ws, uint32_t nb) {
+    const uint32_t n = a.n;
+    const int lane = threadIdx.x & 63;
+    ScanElem e;
+    if (nb >= n) {
+        e = ws.block_incl[n ? (n - 1) / a.plan_frames : 0];
+    } else {
+        const uint32_t b = nb / a.plan_frames;
+        e = ws.block_excl[b];
+        for (uint32_t f0 = b * a.plan_frames; f0 < nb; f0 += 64) {
+            const uint32_t f = f0 + (63 - lane);  // lane 63 holds the oldest frame
+            ScanElem el = scan_identity();
+            if (f < nb) el = scan_elem_of(desc[f], (int32_t)f, f == 0);
+            el = wave_reduce_newest_first(el);
+            e = scan_combine(e, el);
+        }
+    }
+    if (lane != 0) return;
+    uvhttp_ws_batch_summary_t s;
+    s.n_frames = n;
+    s.n_delivered = nb < n ? nb : n;
+    s.first_status = nb < n ? desc[nb].status : 0;
+    s.status = s.first_status < 0 ? -1 : 0;
+    const uint64_t start0 = n ? frame_start(a, 0) : 0;
+    if (n == 0) {
+        s.consumed_bytes = 0;
+    } else if (nb < n) {
+        s.consumed_bytes = frame_start(a, nb) - start0;
+    } else {
+        s.consumed_bytes = frame_start(a, n - 1) + desc[n - 1].wire_len - start0;
+    }
+    s.payload_bytes = e.all_pay;
+    s.n_messages = e.n_fin;
+    s.state_closed = e.n_close ? 1u : 0u;
+    s.arena_bytes = a.arena ? e.data_pay : 0;
+    s.pending_bytes = (e.last_data >= 0 && (e.bits & kLastOpen)) ? e.seg_pay : 0;
+    *a.summary = s;
+}
+
+// k_finalize (batch mode, after the payload pass, one lane per frame): statuses after the
+// first failure become SKIPPED; a compact decode unmasks control payloads (<= 125 B) in
+// place; wave 0 of block 0 writes the batch summary
+__global__ __launch_bounds__(kBlock) void k_finalize(BatchArgs a, uvhttp_ws_frame_desc_t* desc,
+                                                     Workspace ws) {
+    const uint32_t nb = first_bad_of(a, ws, a.n);
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i < a.n) {
+        if (i > nb) desc[i].status = UVHTTP_WS_FRAME_SKIPPED;
+        if (a.arena && i < nb) {
+            const uvhttp_ws_frame_desc_t d = desc[i];
+            if (d.opcode > 2 && d.payload_len) {
+                const uint32_t key = d.masking_key;
+                for (uint64_t q = 0; q < d.payload_len; ++q)
+                    a.wire[d.payload_off + q] ^= (uint8_t)(key >> (8 * (q & 3)));
+            }
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x < 64) write_summary(a, desc, ws, nb);
 }
 
 // ------------------------------------------------------------------------------------
@@ -559,10 +823,11 @@ __device__ inline bool any_bits(const u32x4& m) { return (m.x | m.y | m.z | m.w)
 // store-path cache policy of the payload pass: 0 = global_store nt; 18 = buffer_store with
 // sc1|nt (write-through, not kept in L2), measured 1.7 % faster for the 64x1 shape
 // (tools/stream_probe.hip, profiles/r01_stream_probe_policy.txt)
-template <int BLOCK, int VPT, int STORE_AUX = 0>
-__global__ __launch_bounds__(BLOCK) void k_unmask_inplace(
-    BatchArgs a, const uvhttp_ws_frame_desc_t* __restrict__ desc, Workspace ws,
-    uint64_t tile_base) {
+template <int BLOCK, int VPT, int STORE_AUX>
+__device__ __forceinline__ void unmask_tile(const BatchArgs& a,
+                                            const uvhttp_ws_frame_desc_t* __restrict__ desc,
+                                            const Workspace& ws, uint64_t tile_base,
+                                            uint32_t& n_out, uint32_t& nb_out) {
     constexpr uint64_t kT = (uint64_t)BLOCK * VPT * 16;
     __shared__ uint64_t s_ps[BLOCK];
     __shared__ uint64_t s_pe[BLOCK];
@@ -584,15 +849,18 @@ __global__ __launch_bounds__(BLOCK) void k_unmask_inplace(
         data[v] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.wire + la));
     }
 
+    // batch mode: frames >= nb are not delivered (read after the loads are issued)
     const uint32_t n = nframes(a);
-    const uint32_t nb = *ws.first_bad;  // batch mode: frames >= nb are not delivered
-    if (nb == 0 || n == 0) return;
+    const uint32_t nb = first_bad_of(a, ws, n);
+    n_out = n;
+    nb_out = nb;
+    if (nb == 0 || n == 0 || t0 >= vend) return;
     const uint32_t last = (nb < n ? nb : n) - 1;
     // frames overlapping [t0, t0 + kT): from the first frame of the coarse map tile holding
     // t0 to the first frame of the coarse tile after the one holding the tile's last byte
     const uint64_t c0 = t0 / kMapTile, c1 = (t0 + kT - 1) / kMapTile + 1;
-    const uint32_t f0 = ws.tile_first[c0];
-    uint32_t f1 = (c1 < a.n_tiles) ? ws.tile_first[c1] : last;
+    const uint32_t f0 = tag_get(ws.tile_first[c0], a.epoch, kNoFrame);
+    uint32_t f1 = (c1 < a.n_tiles) ? tag_get(ws.tile_first[c1], a.epoch, kNoFrame) : last;
     if (f0 > last) return;  // the tile starts past the delivered frames (or is unclaimed)
     if (f1 > last || f1 < f0) f1 = last;
 
@@ -687,6 +955,14 @@ __global__ __launch_bounds__(BLOCK) void k_unmask_inplace(
     }
 }
 
+template <int BLOCK, int VPT, int STORE_AUX = 0>
+__global__ __launch_bounds__(BLOCK) void k_unmask_inplace(
+    BatchArgs a, const uvhttp_ws_frame_desc_t* __restrict__ desc, Workspace ws,
+    uint64_t tile_base) {
+    uint32_t n, nb;
+    unmask_tile<BLOCK, VPT, STORE_AUX>(a, desc, ws, tile_base, n, nb);
+}
+
 // ------------------------------------------------------------------------------------
 // k_gather_compact: the roofline kernel of the compact decode.  One workgroup per
 // BLOCK*VPT*16-byte tile of the message arena; lane t produces the aligned arena vectors of
@@ -729,9 +1005,10 @@ __device__ uint64_t block_inclusive_max(uint64_t v) {
 }
 
 template <int BLOCK, int VPT>
-__global__ __launch_bounds__(BLOCK) void k_gather_compact(
-    BatchArgs a, const uvhttp_ws_frame_desc_t* __restrict__ desc, Workspace ws,
-    uint64_t arena_bytes_cap, uint64_t tile_base) {
+__device__ __forceinline__ void gather_tile(const BatchArgs& a,
+                                            const uvhttp_ws_frame_desc_t* __restrict__ desc,
+                                            const Workspace& ws, uint64_t arena_bytes_cap,
+                                            uint64_t tile_base, uint32_t n, uint32_t nb) {
     constexpr uint64_t kT = (uint64_t)BLOCK * VPT * 16;
     __shared__ uint64_t s_as[BLOCK];  // arena start of the data payload
     __shared__ uint64_t s_ae[BLOCK];  // arena end (== start for control frames)
@@ -739,14 +1016,12 @@ __global__ __launch_bounds__(BLOCK) void k_gather_compact(
     __shared__ uint32_t s_key[BLOCK];
 
     const uint64_t t0 = (tile_base + blockIdx.x) * kT;
-    const uint32_t n = nframes(a);
-    const uint32_t nb = *ws.first_bad;
-    if (nb == 0 || n == 0) return;
+    if (nb == 0 || n == 0 || t0 >= a.n_arena_tiles * kMapTile) return;
     const uint32_t last = (nb < n ? nb : n) - 1;
     const uint64_t c0 = t0 / kMapTile, c1 = (t0 + kT - 1) / kMapTile + 1;
-    const uint32_t f0 = ws.arena_first[c0];
+    const uint32_t f0 = tag_get(ws.arena_first[c0], a.epoch, kNoFrame);
     if (f0 > last) return;
-    uint32_t f1 = (c1 < a.n_arena_tiles) ? ws.arena_first[c1] : last;
+    uint32_t f1 = (c1 < a.n_arena_tiles) ? tag_get(ws.arena_first[c1], a.epoch, kNoFrame) : last;
     if (f1 > last || f1 < f0) f1 = last;
 
     uint64_t oa[VPT];
@@ -834,66 +1109,12 @@ __global__ __launch_bounds__(BLOCK) void k_gather_compact(
     }
 }
 
-// ------------------------------------------------------------------------------------
-// k_finalize: statuses after the first failing frame become SKIPPED; control payloads of
-// a compact decode are unmasked in place (<= 125 B each); block 0 writes the summary.
-// ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_finalize(BatchArgs a, uvhttp_ws_frame_desc_t* desc,
-                                                     Workspace ws,
-                                                     uvhttp_ws_batch_summary_t* summary,
-                                                     uint32_t n_blocks) {
-    const uint32_t nb = *ws.first_bad;
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i < a.n && i > nb) desc[i].status = UVHTTP_WS_FRAME_SKIPPED;
-    if (a.arena && i < a.n && i < nb) {
-        const uvhttp_ws_frame_desc_t d = desc[i];
-        if (d.opcode > 2 && d.payload_len) {
-            const uint32_t key = d.masking_key;
-            for (uint64_t b = 0; b < d.payload_len; ++b)
-                a.wire[d.payload_off + b] ^= (uint8_t)(key >> (8 * (b & 3)));
-        }
-    }
-    if (blockIdx.x != 0) return;
-
-    // E(nb): exclusive scan value at the first bad frame (or the total)
-    ScanElem e;
-    if (nb >= a.n) {
-        e = ws.group_agg[(n_blocks + kScanThreads - 1) / kScanThreads];
-    } else {
-        const uint32_t b = nb / kBlock;
-        const uint32_t f = b * kBlock + threadIdx.x;
-        ScanElem el = scan_identity();
-        if (f < nb) el = scan_elem_of(desc[f], (int32_t)f, f == 0);
-        ScanElem part;
-        (void)block_exclusive_scan(el, &part);
-        e = scan_combine(block_prefix(ws, b), part);
-    }
-    if (threadIdx.x != 0) return;
-    uvhttp_ws_batch_summary_t s;
-    s.n_frames = a.n;
-    s.n_delivered = nb < a.n ? nb : a.n;
-    s.first_status = nb < a.n ? desc[nb].status : 0;
-    s.status = s.first_status < 0 ? -1 : 0;
-    const uint64_t start0 = a.n ? frame_start(a, 0) : 0;
-    if (a.n == 0) {
-        s.consumed_bytes = 0;
-    } else if (nb < a.n) {
-        s.consumed_bytes = frame_start(a, nb) - start0;
-    } else {
-        s.consumed_bytes = frame_start(a, a.n - 1) + desc[a.n - 1].wire_len - start0;
-    }
-    s.payload_bytes = e.all_pay;
-    s.n_messages = e.n_fin;
-    s.state_closed = e.n_close ? 1u : 0u;
-    s.arena_bytes = a.arena ? e.data_pay : 0;
-    uint64_t pend = 0;
-    if (e.last_data >= 0) {
-        const uvhttp_ws_frame_desc_t pd = desc[e.last_data];
-        const bool p_start = pd.opcode != 0;
-        if (!(pd.flags & UVHTTP_WS_FLAG_FIN) && !(p_start && pd.payload_len == 0)) pend = e.seg_pay;
-    }
-    s.pending_bytes = pend;
-    *summary = s;
+template <int BLOCK, int VPT>
+__global__ __launch_bounds__(BLOCK) void k_gather_compact(
+    BatchArgs a, const uvhttp_ws_frame_desc_t* __restrict__ desc, Workspace ws,
+    uint64_t arena_bytes_cap, uint64_t tile_base) {
+    const uint32_t n = nframes(a);
+    gather_tile<BLOCK, VPT>(a, desc, ws, arena_bytes_cap, tile_base, n, first_bad_of(a, ws, n));
 }
 
 // ------------------------------------------------------------------------------------
@@ -991,6 +1212,107 @@ __device__ inline uint32_t block_exclusive_sum_u32(uint32_t v, uint32_t* total) 
     return pre + inc - v;
 }
 
+// Wave-per-connection walk (connections with many small frames): the 64 lanes stage a
+// 2 KiB window of the connection's bytes in LDS with one coalesced 16-byte load each (x2),
+// then every lane parses the same headers from LDS (broadcast reads) — a hop costs an LDS
+// round trip instead of dependent global byte loads, and a window reload is one memory
+// round trip for ~8 frames of 256 B.  Same decisions as walk_stream, byte for byte.
+constexpr int kWinVec = 2;
+constexpr uint32_t kWin = 64u * 16u * kWinVec;
+
+template <bool WRITE>
+__device__ inline uint32_t walk_stream_wave(const WalkArgs& w, uint32_t s, uint32_t first,
+                                            uint8_t* win) {
+    const int lane = threadIdx.x & 63;
+    const uvhttp_ws_stream_t st = w.streams[s];
+    const uint64_t L = st.begin + st.len <= w.wire_len ? st.len : 0;
+    uint64_t grown;
+    if (!grow_recv(L, st.recv_buffer_size, st.max_frame_size, &grown)) return 0;
+    const uint64_t mf = (uint64_t)(int64_t)st.max_frame_size;
+    uint32_t count = 0;
+    uint64_t pos = 0;
+    uint64_t wb = 0;
+    bool have = false;
+    while (L - pos >= 2) {
+        const uint64_t at = st.begin + pos;
+        if (!have || at < wb || at + 10 > wb + kWin) {
+            wb = at & ~(uint64_t)15;
+            have = true;
+#pragma unroll
+            for (int v = 0; v < kWinVec; ++v) {
+                const uint32_t o = (uint32_t)(v * 64 + lane) * 16u;
+                const uint64_t src = wb + o;
+                u32x4 x;
+                if (src + 16 <= w.wire_len) {
+                    x = *reinterpret_cast<const u32x4*>(w.wire + src);
+                } else {
+                    uint32_t t[4] = {0, 0, 0, 0};
+                    for (uint32_t k = 0; k < 16 && src + k < w.wire_len; ++k)
+                        t[k >> 2] |= (uint32_t)w.wire[src + k] << (8 * (k & 3));
+                    x = u32x4{t[0], t[1], t[2], t[3]};
+                }
+                *reinterpret_cast<u32x4*>(win + o) = x;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        const uint8_t* h = win + (at - wb);
+        const uint32_t b0 = h[0], b1 = h[1];
+        const uint32_t code = b1 & 0x7F;
+        const uint32_t need = code == 126 ? 4 : code == 127 ? 10 : 2;
+        if (L - pos < need) break;
+        uint64_t plen = code;
+        if (need > 2) {
+            plen = 0;
+            for (uint32_t k = 2; k < need; ++k) plen = (plen << 8) | h[k];
+        }
+        const bool bad = (need == 10 && (plen >> 63)) || (b0 & 0x70) ||
+                         ((b0 & 0x0F) >= 8 && (plen > 125 || !(b0 & 0x80))) ||
+                         (st.is_server && !(b1 & 0x80)) || plen > mf;
+        const uint64_t wl = need + ((b1 & 0x80) ? 4u : 0u) + plen;
+        if (!bad && L - pos < wl) break;  // incomplete: waits for more bytes
+        if (WRITE && lane == 0 && first + count < w.max_frames) {
+            w.sc.frame_off[first + count] = at;
+            w.sc.frame_seg[first + count] = s;
+        }
+        ++count;
+        if (bad) break;  // process_data returns at this frame
+        pos += wl;
+    }
+    return count;
+}
+
+// wave mode pass 1: frames per connection (one wave each)
+__global__ __launch_bounds__(kBlock) void k_walk_count_wave(WalkArgs w) {
+    __shared__ __attribute__((aligned(16))) uint8_t win[kBlock / 64][kWin];
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t s = blockIdx.x * (kBlock / 64) + wave;
+    if (s >= w.n_streams) return;
+    const uint32_t c = walk_stream_wave<false>(w, s, 0, win[wave]);
+    if ((threadIdx.x & 63) == 0) w.results[s].n_frames = c;
+}
+
+// wave mode: per-256-connection sums of the counts (the lane-mode count pass's aggregate)
+__global__ __launch_bounds__(kBlock) void k_walk_agg(WalkArgs w) {
+    const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t c = s < w.n_streams ? w.results[s].n_frames : 0;
+    uint32_t total;
+    (void)block_exclusive_sum_u32(c, &total);
+    if (threadIdx.x == 0) w.sc.walk_agg[blockIdx.x] = total;
+}
+
+// wave mode pass 2: offsets, after k_walk_write<false> placed each connection's first frame
+__global__ __launch_bounds__(kBlock) void k_walk_write_wave(WalkArgs w) {
+    __shared__ __attribute__((aligned(16))) uint8_t win[kBlock / 64][kWin];
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t s = blockIdx.x * (kBlock / 64) + wave;
+    if (s >= w.n_streams) return;
+    const uvhttp_ws_stream_result_t r = w.results[s];
+    if (r.n_frames) (void)walk_stream_wave<true>(w, s, r.first_frame, win[wave]);
+}
+
+
 __global__ __launch_bounds__(kBlock) void k_walk_count(WalkArgs w) {
     const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t c = s < w.n_streams ? walk_stream<false>(w, s, 0) : 0;
@@ -1016,6 +1338,7 @@ __global__ __launch_bounds__(kBlock) void k_walk_scan(WalkArgs w, uint32_t n_blo
     if (threadIdx.x == 0) *w.sc.n_total = total <= w.max_frames ? total : 0;
 }
 
+template <bool WALK>
 __global__ __launch_bounds__(kBlock) void k_walk_write(WalkArgs w) {
     const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t c = s < w.n_streams ? w.results[s].n_frames : 0;
@@ -1041,7 +1364,7 @@ __global__ __launch_bounds__(kBlock) void k_walk_write(WalkArgs w) {
         r.status = -1;
         r.first_status = UVHTTP_WS_FRAME_ERR_CAPACITY;
         r.n_frames = 0;
-    } else if (c) {
+    } else if (c && WALK) {
         (void)walk_stream<true>(w, s, first);
     }
     w.sc.seg_bad[s] = first + (fits ? c : 0);
@@ -1386,6 +1709,9 @@ struct uvhttp_ws_gpu_engine {
     int timing;
     int tile_block, tile_vpt;  // payload kernel shape, 0 = automatic
     int store_aux;             // payload store cache policy (0 = nt global store, 18 = sc1|nt)
+    uint32_t epoch;            // tag of the latest decode call, 1 .. kMaxEpoch
+    int plan_fpt;              // k_plan frames per lane, 0 = automatic
+    int walk_mode;             // stream frame discovery: 0 automatic, 1 lane, 2 wave
     void* ss_mem;              // stream-decode scratch
     uint32_t ss_frames, ss_streams;
     StreamScratch ss;
@@ -1424,6 +1750,9 @@ int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out) {
     e->device = device;
     e->store_aux = 18;
     if (const char* sp = getenv("UVHTTP_WS_STORE_POLICY")) e->store_aux = atoi(sp) == 18 ? 18 : 0;
+    if (const char* fp = getenv("UVHTTP_WS_PLAN_FPT")) e->plan_fpt = atoi(fp);
+    if (const char* wm = getenv("UVHTTP_WS_WALK"))
+        e->walk_mode = strcmp(wm, "lane") == 0 ? 1 : strcmp(wm, "wave") == 0 ? 2 : 0;
     *out = e;
     return UVHTTP_WS_GPU_OK;
 }
@@ -1459,21 +1788,31 @@ int uvhttp_ws_gpu_engine_reserve(uvhttp_ws_gpu_engine_t* e, uint32_t max_frames,
     const uint64_t tl = tiles > e->cap_tiles ? tiles : e->cap_tiles;
     const uint64_t at = atiles > e->cap_arena_tiles ? atiles : e->cap_arena_tiles;
     const uint64_t nblk = (fr + kBlock - 1) / kBlock + 2;
-    const uint64_t ngrp = nblk / kScanThreads + 2;
+    const uint64_t ngrp = nblk / kBlock + 2;
     size_t off_agg = 0;
     size_t off_grp = align_up(off_agg + nblk * sizeof(ScanElem), 256);
-    size_t off_tiles = align_up(off_grp + ngrp * sizeof(ScanElem), 256);
-    size_t off_bad = align_up(off_tiles + tl * sizeof(uint32_t), 256);
+    size_t off_incl = align_up(off_grp + ngrp * sizeof(ScanElem), 256);
+    size_t off_excl = align_up(off_incl + nblk * sizeof(ScanElem), 256);
+    size_t off_reca = align_up(off_excl + nblk * sizeof(ScanElem), 256);
+    size_t off_recp = align_up(off_reca + nblk * sizeof(LbRec), 256);
+    size_t off_cnt = align_up(off_recp + nblk * sizeof(LbRec), 256);
+    size_t off_tiles = align_up(off_cnt + 16, 256);
+    size_t off_bad = align_up(off_tiles + tl * sizeof(uint64_t), 256);
     size_t off_arena = align_up(off_bad + 16, 256);
-    size_t bytes = align_up(off_arena + at * sizeof(uint32_t), 256);
+    size_t bytes = align_up(off_arena + at * sizeof(uint64_t), 256);
     int prev = 0;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(e->device);
     if (e->ws_mem) (void)hipFree(e->ws_mem);
     e->ws_mem = nullptr;
     hipError_t h = hipMalloc(&e->ws_mem, bytes);
+    // zero: ticket counters start at 0 and no flag / tag matches a live epoch (epochs >= 1)
+    if (h == hipSuccess) h = hipMemset(e->ws_mem, 0, bytes);
+    if (h == hipSuccess) h = hipDeviceSynchronize();
     (void)hipSetDevice(prev);
     if (h != hipSuccess) {
+        if (e->ws_mem) (void)hipFree(e->ws_mem);
+        e->ws_mem = nullptr;
         e->cap_frames = 0;
         e->cap_tiles = e->cap_arena_tiles = 0;
         return set_err(e, UVHTTP_WS_GPU_ENOMEM, "hipMalloc workspace", h);
@@ -1481,9 +1820,14 @@ int uvhttp_ws_gpu_engine_reserve(uvhttp_ws_gpu_engine_t* e, uint32_t max_frames,
     char* b = (char*)e->ws_mem;
     e->ws.block_agg = (ScanElem*)(b + off_agg);
     e->ws.group_agg = (ScanElem*)(b + off_grp);
-    e->ws.tile_first = (uint32_t*)(b + off_tiles);
-    e->ws.first_bad = (uint32_t*)(b + off_bad);
-    e->ws.arena_first = (uint32_t*)(b + off_arena);
+    e->ws.block_incl = (ScanElem*)(b + off_incl);
+    e->ws.block_excl = (ScanElem*)(b + off_excl);
+    e->ws.rec_a = (LbRec*)(b + off_reca);
+    e->ws.rec_p = (LbRec*)(b + off_recp);
+    e->ws.counters = (uint32_t*)(b + off_cnt);
+    e->ws.tile_first = (uint64_t*)(b + off_tiles);
+    e->ws.first_bad = (uint64_t*)(b + off_bad);
+    e->ws.arena_first = (uint64_t*)(b + off_arena);
     e->ws_bytes = bytes;
     e->cap_frames = fr;
     e->cap_tiles = tl;
@@ -1556,6 +1900,41 @@ static void timing_end(uvhttp_ws_gpu_engine_t* e, int k, hipStream_t s) {
     e->ev_used = k + 1;
 }
 
+// Flags hold the epoch in 30 bits.  When the epoch space is used up the workspace is cleared
+// on the call's stream (once per 2^30 - 1 calls), so no entry left by an earlier call can
+// carry a live tag.
+constexpr uint32_t kMaxEpoch = (1u << 30) - 1;
+
+static uint32_t next_epoch(uvhttp_ws_gpu_engine_t* e, hipStream_t s) {
+    if (e->epoch >= kMaxEpoch) {
+        (void)hipMemsetAsync(e->ws_mem, 0, e->ws_bytes, s);
+        e->epoch = 0;
+    }
+    return ++e->epoch;
+}
+
+// k_plan launch: frames per lane chosen so the grid stays within ~256 blocks (the look-back
+// sees every predecessor in one window); UVHTTP_WS_PLAN_FPT pins it for tuning
+static void launch_plan(uvhttp_ws_gpu_engine_t* e, BatchArgs& a, uint32_t n_cap,
+                        uvhttp_ws_frame_desc_t* d_desc, uvhttp_ws_message_desc_t* d_msgs,
+                        hipStream_t s) {
+    int fpt = e->plan_fpt;
+    if (fpt != 1 && fpt != 2 && fpt != 4 && fpt != 8 && fpt != 16) {
+        fpt = 1;
+        while (fpt < 16 && ((uint64_t)n_cap + kBlock * fpt - 1) / (kBlock * fpt) > 256) fpt *= 2;
+    }
+    const uint32_t per = kBlock * fpt;
+    a.plan_frames = per;
+    const uint32_t grid = n_cap ? (n_cap + per - 1) / per : 1;
+    switch (fpt) {
+        case 1: hipLaunchKernelGGL(k_plan<1>, dim3(grid), dim3(kBlock), 0, s, a, d_desc, d_msgs, e->ws); break;
+        case 2: hipLaunchKernelGGL(k_plan<2>, dim3(grid), dim3(kBlock), 0, s, a, d_desc, d_msgs, e->ws); break;
+        case 4: hipLaunchKernelGGL(k_plan<4>, dim3(grid), dim3(kBlock), 0, s, a, d_desc, d_msgs, e->ws); break;
+        case 8: hipLaunchKernelGGL(k_plan<8>, dim3(grid), dim3(kBlock), 0, s, a, d_desc, d_msgs, e->ws); break;
+        default: hipLaunchKernelGGL(k_plan<16>, dim3(grid), dim3(kBlock), 0, s, a, d_desc, d_msgs, e->ws); break;
+    }
+}
+
 static int check_batch(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b,
                        const void* d_desc, const void* d_summary) {
     if (!e || !b || !d_desc || !d_summary) return UVHTTP_WS_GPU_EINVAL;
@@ -1599,16 +1978,11 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
     a.arena = arena;
     a.arena_cap = arena_cap;
     a.n_arena_tiles = n_atiles;
+    a.summary = d_summary;
 
-    const uint32_t n_blocks = (a.n + kBlock - 1) / kBlock;
-    const uint32_t grid_f = n_blocks ? n_blocks : 1;
-    hipLaunchKernelGGL(k_parse, dim3(grid_f), dim3(kBlock), 0, s, a, d_desc, e->ws);
-    {
-        const uint32_t n_groups = (grid_f + kScanThreads - 1) / kScanThreads;
-        hipLaunchKernelGGL(k_scan_groups, dim3(n_groups), dim3(kBlock), 0, s, e->ws, grid_f);
-        hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, s, e->ws, n_groups);
-    }
-    hipLaunchKernelGGL(k_resolve, dim3(grid_f), dim3(kBlock), 0, s, a, d_desc, d_msgs, e->ws);
+    a.epoch = next_epoch(e, s);
+
+    launch_plan(e, a, a.n, d_desc, d_msgs, s);
     // payload kernel tile shape: explicit (set_tile) or by average wire bytes per frame
     // (auto shapes from tools/tile_sweep.py on MI355X, profiles/r01_tile_sweep.txt)
     int blk = e->tile_block, vpt = e->tile_vpt;
@@ -1622,7 +1996,7 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
             vpt = 2;
         }
     }
-    const uint64_t span = arena ? (n_atiles ? arena_need : 0) : b->wire_len;
+    const uint64_t span = arena ? n_atiles * kMapTile : b->wire_len;
     const uint64_t tile_bytes = (uint64_t)blk * vpt * 16;
     const uint64_t n_ptiles = (span + tile_bytes - 1) / tile_bytes;
     // the dispatch packet counts work-items in 32 bits: split very large passes
@@ -1647,8 +2021,10 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
 #undef UVWS_LAUNCH
     }
     timing_end(e, tk, s);
-    hipLaunchKernelGGL(k_finalize, dim3(grid_f), dim3(kBlock), 0, s, a, d_desc, e->ws, d_summary,
-                       grid_f);
+    {
+        const uint32_t grid_fin = a.n ? (a.n + kBlock - 1) / kBlock : 1;
+        hipLaunchKernelGGL(k_finalize, dim3(grid_fin), dim3(kBlock), 0, s, a, d_desc, e->ws);
+    }
     hipError_t h = hipGetLastError();
     if (prev != e->device) (void)hipSetDevice(prev);
     if (h != hipSuccess) return set_err(e, UVHTTP_WS_GPU_ELAUNCH, "launch", h);
@@ -1736,9 +2112,21 @@ int uvhttp_ws_gpu_decode_streams(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uin
     w.results = d_results;
     w.sc = e->ss;
     const uint32_t nsb = (n_streams + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL(k_walk_count, dim3(nsb), dim3(kBlock), 0, s, w);
-    hipLaunchKernelGGL(k_walk_scan, dim3(1), dim3(kBlock), 0, s, w, nsb);
-    hipLaunchKernelGGL(k_walk_write, dim3(nsb), dim3(kBlock), 0, s, w);
+    // frame discovery: a lane per connection, or a wave per connection when the waves fit
+    // the chip in about one round (UVHTTP_WS_WALK=lane|wave pins it)
+    const bool wave_walk = e->walk_mode ? e->walk_mode == 2 : n_streams <= 16384;
+    if (wave_walk) {
+        const uint32_t nwb = (n_streams + kBlock / 64 - 1) / (kBlock / 64);
+        hipLaunchKernelGGL(k_walk_count_wave, dim3(nwb), dim3(kBlock), 0, s, w);
+        hipLaunchKernelGGL(k_walk_agg, dim3(nsb), dim3(kBlock), 0, s, w);
+        hipLaunchKernelGGL(k_walk_scan, dim3(1), dim3(kBlock), 0, s, w, nsb);
+        hipLaunchKernelGGL(k_walk_write<false>, dim3(nsb), dim3(kBlock), 0, s, w);
+        hipLaunchKernelGGL(k_walk_write_wave, dim3(nwb), dim3(kBlock), 0, s, w);
+    } else {
+        hipLaunchKernelGGL(k_walk_count, dim3(nsb), dim3(kBlock), 0, s, w);
+        hipLaunchKernelGGL(k_walk_scan, dim3(1), dim3(kBlock), 0, s, w, nsb);
+        hipLaunchKernelGGL(k_walk_write<true>, dim3(nsb), dim3(kBlock), 0, s, w);
+    }
 
     BatchArgs a;
     memset(&a, 0, sizeof(a));
@@ -1752,15 +2140,9 @@ int uvhttp_ws_gpu_decode_streams(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uin
     a.n_dev = e->ss.n_total;
     a.open_after = e->ss.open_after;
     a.seg_bad = e->ss.seg_bad;
+    a.epoch = next_epoch(e, s);
+    launch_plan(e, a, cap, d_desc, nullptr, s);
     const uint32_t grid_f = (cap + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL(k_parse, dim3(grid_f), dim3(kBlock), 0, s, a, d_desc, e->ws);
-    {
-        const uint32_t n_groups = (grid_f + kScanThreads - 1) / kScanThreads;
-        hipLaunchKernelGGL(k_scan_groups, dim3(n_groups), dim3(kBlock), 0, s, e->ws, grid_f);
-        hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, s, e->ws, n_groups);
-    }
-    hipLaunchKernelGGL(k_resolve, dim3(grid_f), dim3(kBlock), 0, s, a, d_desc,
-                       (uvhttp_ws_message_desc_t*)nullptr, e->ws);
     const uint32_t grid_m = grid_f > nsb ? grid_f : nsb;
     hipLaunchKernelGGL(k_stream_mark, dim3(grid_m), dim3(kBlock), 0, s, a, d_desc, d_results,
                        n_streams);
@@ -1814,7 +2196,7 @@ int uvhttp_ws_gpu_build_frames(uvhttp_ws_gpu_engine_t* e, const uint8_t* d_src, 
     b.out_off = d_out_off;
     b.blk = reinterpret_cast<uint64_t*>(e->ws.block_agg);
     b.grp = reinterpret_cast<uint64_t*>(e->ws.group_agg);
-    b.map = e->ws.arena_first;
+    b.map = reinterpret_cast<uint32_t*>(e->ws.arena_first);
     b.n_map = (out_cap + kMapTile - 1) / kMapTile;
     const uint32_t grid_f = n_frames ? (n_frames + kBlock - 1) / kBlock : 1;
     const uint32_t n_groups = (grid_f + kBlock - 1) / kBlock;
