@@ -469,3 +469,24 @@ def test_plan_frames_per_lane_identical(torch, fpt, monkeypatch):
                 _compare(ref, got, compact)
     finally:
         e.close()
+
+
+def test_epoch_wraparound(torch, monkeypatch):
+    """Decode calls on both sides of the epoch wrap (the workspace is cleared when the 30-bit
+    call tag runs out) decode like the oracle: big and small batches alternate so stale map
+    entries of an earlier call would show."""
+    import uvhttp_amd as U
+    monkeypatch.setenv("UVHTTP_WS_EPOCH_START", str((1 << 30) - 4))
+    e = U.GpuEngine(0)
+    try:
+        rng = random.Random(31337)
+        for k in range(8):
+            n = 3000 if k % 2 == 0 else 40
+            sizes = [70000, 5000, 125] if k % 2 == 0 else [0, 3, 300]
+            wire, offs = _rand_batch(rng, n, sizes, p_ctrl=0.1, p_frag=0.3,
+                                     p_bad=0.002 if k % 3 == 2 else 0.0)
+            for compact in (False, True):
+                ref, got = _run_both(torch, e, wire, n, offs=offs, mm=0, compact=compact)
+                _compare(ref, got, compact)
+    finally:
+        e.close()

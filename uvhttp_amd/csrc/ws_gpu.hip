@@ -33,6 +33,7 @@ constexpr int kBlock = 256;                 // threads per workgroup (4 waves of
 constexpr uint64_t kMapTile = 16384;        // granularity of the tile -> first-frame maps
 constexpr uint32_t kMaxFrames = 1u << 26;   // k_scan handles <= 2^18 block aggregates
 constexpr uint32_t kNoFrame = 0xFFFFFFFFu;  // tile map entry no frame claimed this call
+constexpr uint32_t kMaxEpoch = (1u << 30) - 1;  // decode-call tags run 1 .. kMaxEpoch
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -606,7 +607,8 @@ __device__ ScanElem lookback_prefix(const Workspace& ws, uint32_t b, const ScanE
                 }
             }
             if (__syncthreads_and(ready) || ++polls > kMaxPolls) break;
-            __builtin_amdgcn_s_sleep(1);
+            // back off so waiting blocks do not flood memory while predecessors still parse
+            __builtin_amdgcn_s_sleep(8);
         }
         // nearest published prefix (smallest t with P)
         if (t == 0) s_kstar = kBlock;
@@ -1035,7 +1037,37 @@ __device__ __forceinline__ void gather_tile(const BatchArgs& a,
     }
     uint64_t arena_end = 0;  // end of the delivered data payload staged so far
 
-    for (uint32_t base = f0; base <= f1; base += BLOCK) {
+    // fast path (data frames of ~4 KiB and up): at most two data frames cover the tile; their
+    // descriptors are uniform scalar loads, no LDS staging
+    bool fast = false;
+    if (f1 - f0 < 2) {
+        const uvhttp_ws_frame_desc_t d0 = desc[f0];
+        const uvhttp_ws_frame_desc_t d1 = desc[f1];
+        if (d0.opcode <= 2 && d1.opcode <= 2) {
+            fast = true;
+            for (uint32_t f = f0; f <= f1; ++f) {
+                const uvhttp_ws_frame_desc_t& d = f == f0 ? d0 : d1;
+                const uint64_t fa = d.payload_off, fe = fa + d.payload_len;
+                const uint64_t ps = frame_start(a, f) + d.header_size + ((d.flags & UVHTTP_WS_FLAG_MASK) ? 4u : 0u);
+#pragma unroll
+                for (int v = 0; v < VPT; ++v) {
+                    if (fe <= oa[v] || fa >= oa[v] + 16) continue;
+                    const int lo_b = fa > oa[v] ? (int)(fa - oa[v]) : 0;
+                    const int hi_b = fe < oa[v] + 16 ? (int)(fe - oa[v]) : 16;
+                    const int64_t wstart = (int64_t)ps + (int64_t)(oa[v] - fa);
+                    const u32x4 w = load16_any(a.wire, wstart, a.wire_len);
+                    const uint32_t rk = rotr32(d.masking_key, 8u * (uint32_t)((oa[v] - fa) & 3u));
+                    const u32x4 sel{lane_bytes(lo_b, hi_b, 0), lane_bytes(lo_b, hi_b, 1),
+                                    lane_bytes(lo_b, hi_b, 2), lane_bytes(lo_b, hi_b, 3)};
+                    out[v] |= (w ^ u32x4{rk, rk, rk, rk}) & sel;
+                    touched[v] = true;
+                }
+                if (fe > arena_end) arena_end = fe;
+            }
+        }
+    }
+
+    for (uint32_t base = f0; !fast && base <= f1; base += BLOCK) {
         const uint32_t cnt = (f1 - base + 1) < (uint32_t)BLOCK ? (f1 - base + 1) : BLOCK;
         uint64_t as = 0, ae = 0, ps = 0;
         uint32_t key = 0;
@@ -1497,6 +1529,62 @@ __global__ __launch_bounds__(kBlock) void kb_offsets(BuildArgs b, uint32_t n_gro
         atomicMin(&b.map[t], i);
 }
 
+// header image of a built frame (<= 14 bytes: byte 0, byte 1, extended length, key)
+__device__ inline u32x4 build_header(const uvhttp_ws_build_desc_t& d, uint32_t* hsz) {
+    const uint64_t p = d.payload_len;
+    const uint32_t hs = p < 126 ? 2 : p < 65536 ? 4 : 10;
+    uint32_t w[4] = {0, 0, 0, 0};
+    auto put = [&](uint32_t k, uint32_t byte) { w[k >> 2] |= (byte & 0xFF) << (8 * (k & 3)); };
+    put(0, (d.fin ? 0x80 : 0) | (d.opcode & 0x0F));
+    const uint32_t mb = d.mask ? 0x80 : 0;
+    if (hs == 2) {
+        put(1, mb | (uint32_t)p);
+    } else if (hs == 4) {
+        put(1, mb | 126);
+        put(2, (uint32_t)(p >> 8));
+        put(3, (uint32_t)p);
+    } else {
+        put(1, mb | 127);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) put(2 + k, (uint32_t)(p >> (56 - 8 * k)));
+    }
+    if (d.mask) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) put(hs + k, d.masking_key >> (8 * k));
+    }
+    *hsz = hs + (d.mask ? 4u : 0u);
+    return u32x4{w[0], w[1], w[2], w[3]};
+}
+
+// bytes of output vector [oa, oa + 16) that belong to frame (header image img over
+// [fs, ps), payload src[sp ...] over [ps, fe), key for client frames)
+__device__ inline void build_vector(const BuildArgs& b, uint64_t oa, uint64_t fs, uint64_t ps,
+                                    uint64_t fe, uint64_t sp, uint32_t key, const u32x4& img,
+                                    u32x4& out) {
+    if (ps > oa && fs < oa + 16) {
+        const uint32_t iw[4] = {img.x, img.y, img.z, img.w};
+        uint32_t ow[4] = {0, 0, 0, 0};
+        for (int bq = 0; bq < 16; ++bq) {
+            const uint64_t x = oa + bq;
+            if (x >= fs && x < ps) {
+                const uint32_t k = (uint32_t)(x - fs);
+                ow[bq >> 2] |= ((iw[k >> 2] >> (8 * (k & 3))) & 0xFF) << (8 * (bq & 3));
+            }
+        }
+        out |= u32x4{ow[0], ow[1], ow[2], ow[3]};
+    }
+    if (fe > ps && ps < oa + 16 && fe > oa) {
+        const int lo_b = ps > oa ? (int)(ps - oa) : 0;
+        const int hi_b = fe < oa + 16 ? (int)(fe - oa) : 16;
+        const int64_t wstart = (int64_t)sp + ((int64_t)oa - (int64_t)ps);
+        const u32x4 w = load16_any(b.src, wstart, b.src_len);
+        const uint32_t rk = rotr32(key, 8u * (uint32_t)((oa - ps) & 3u));
+        const u32x4 sel{lane_bytes(lo_b, hi_b, 0), lane_bytes(lo_b, hi_b, 1),
+                        lane_bytes(lo_b, hi_b, 2), lane_bytes(lo_b, hi_b, 3)};
+        out |= (w ^ u32x4{rk, rk, rk, rk}) & sel;
+    }
+}
+
 template <int BLOCK, int VPT>
 __global__ __launch_bounds__(BLOCK) void kb_emit(BuildArgs b, uint64_t tile_base) {
     constexpr uint64_t kT = (uint64_t)BLOCK * VPT * 16;
@@ -1525,39 +1613,33 @@ __global__ __launch_bounds__(BLOCK) void kb_emit(BuildArgs b, uint64_t tile_base
         oa[v] = t0 + ((uint64_t)v * BLOCK + threadIdx.x) * 16u;
         out[v] = u32x4{0, 0, 0, 0};
     }
-    for (uint32_t base = f0; base <= f1; base += BLOCK) {
+    if (f1 - f0 < 2) {
+        // fast path (frames of ~4 KiB and up): at most two frames touch the tile; their
+        // descriptors are uniform scalar loads, no LDS staging
+        for (uint32_t f = f0; f <= f1; ++f) {
+            const uvhttp_ws_build_desc_t d = b.frames[f];
+            uint32_t hm;
+            const u32x4 img = build_header(d, &hm);
+            const uint64_t st = b.out_off[f];
+            const uint64_t ps = st + hm, fe = ps + d.payload_len;
+            const uint32_t key = d.mask ? d.masking_key : 0u;
+#pragma unroll
+            for (int v = 0; v < VPT; ++v)
+                if (fe > oa[v] && st < oa[v] + 16) build_vector(b, oa[v], st, ps, fe, d.payload_off, key, img, out[v]);
+        }
+    }
+    for (uint32_t base = f0; f1 - f0 >= 2 && base <= f1; base += BLOCK) {
         const uint32_t cnt = (f1 - base + 1) < (uint32_t)BLOCK ? (f1 - base + 1) : BLOCK;
         __syncthreads();
         if (threadIdx.x < cnt) {
             const uint32_t f = base + threadIdx.x;
             const uvhttp_ws_build_desc_t d = b.frames[f];
-            const uint64_t p = d.payload_len;
-            const uint32_t hs = p < 126 ? 2 : p < 65536 ? 4 : 10;
-            const uint32_t m = d.mask ? 4 : 0;
-            uint8_t h[16] = {0};
-            h[0] = (uint8_t)((d.fin ? 0x80 : 0) | (d.opcode & 0x0F));
-            const uint8_t mb = d.mask ? 0x80 : 0;
-            if (hs == 2) {
-                h[1] = (uint8_t)(mb | p);
-            } else if (hs == 4) {
-                h[1] = (uint8_t)(mb | 126);
-                h[2] = (uint8_t)(p >> 8);
-                h[3] = (uint8_t)p;
-            } else {
-                h[1] = (uint8_t)(mb | 127);
-#pragma unroll
-                for (int k = 0; k < 8; ++k) h[2 + k] = (uint8_t)(p >> (56 - 8 * k));
-            }
-            if (m) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k) h[hs + k] = (uint8_t)(d.masking_key >> (8 * k));
-            }
-            u32x4 img;
-            __builtin_memcpy(&img, h, 16);
+            uint32_t hm;
+            const u32x4 img = build_header(d, &hm);
             const uint64_t st = b.out_off[f];
             s_start[threadIdx.x] = st;
-            s_pstart[threadIdx.x] = st + hs + m;
-            s_end[threadIdx.x] = st + hs + m + p;
+            s_pstart[threadIdx.x] = st + hm;
+            s_end[threadIdx.x] = st + hm + d.payload_len;
             s_src[threadIdx.x] = d.payload_off;
             s_key[threadIdx.x] = d.mask ? d.masking_key : 0u;
             s_hdr[threadIdx.x] = img;
@@ -1577,33 +1659,9 @@ __global__ __launch_bounds__(BLOCK) void kb_emit(BuildArgs b, uint64_t tile_base
                 }
             }
             for (; j >= 0; --j) {
-                const uint64_t fs = s_start[j], ps = s_pstart[j], fe = s_end[j];
-                if (fe <= oa[v]) break;
-                // header bytes [fs, ps) of the vector
-                if (ps > oa[v] && fs < oa[v] + 16) {
-                    const u32x4 img = s_hdr[j];
-                    const uint32_t iw[4] = {img.x, img.y, img.z, img.w};
-                    uint32_t ow[4] = {0, 0, 0, 0};
-                    for (int bq = 0; bq < 16; ++bq) {
-                        const uint64_t x = oa[v] + bq;
-                        if (x >= fs && x < ps) {
-                            const uint32_t k = (uint32_t)(x - fs);
-                            ow[bq >> 2] |= ((iw[k >> 2] >> (8 * (k & 3))) & 0xFF) << (8 * (bq & 3));
-                        }
-                    }
-                    out[v] |= u32x4{ow[0], ow[1], ow[2], ow[3]};
-                }
-                // payload bytes [ps, fe)
-                if (fe > ps && ps < oa[v] + 16) {
-                    const int lo_b = ps > oa[v] ? (int)(ps - oa[v]) : 0;
-                    const int hi_b = fe < oa[v] + 16 ? (int)(fe - oa[v]) : 16;
-                    const int64_t wstart = (int64_t)s_src[j] + ((int64_t)oa[v] - (int64_t)ps);
-                    const u32x4 w = load16_any(b.src, wstart, b.src_len);
-                    const uint32_t rk = rotr32(s_key[j], 8u * (uint32_t)((oa[v] - ps) & 3u));
-                    const u32x4 sel{lane_bytes(lo_b, hi_b, 0), lane_bytes(lo_b, hi_b, 1),
-                                    lane_bytes(lo_b, hi_b, 2), lane_bytes(lo_b, hi_b, 3)};
-                    out[v] |= (w ^ u32x4{rk, rk, rk, rk}) & sel;
-                }
+                if (s_end[j] <= oa[v]) break;
+                build_vector(b, oa[v], s_start[j], s_pstart[j], s_end[j], s_src[j], s_key[j],
+                             s_hdr[j], out[v]);
             }
         }
     }
@@ -1751,6 +1809,11 @@ int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out) {
     e->store_aux = 18;
     if (const char* sp = getenv("UVHTTP_WS_STORE_POLICY")) e->store_aux = atoi(sp) == 18 ? 18 : 0;
     if (const char* fp = getenv("UVHTTP_WS_PLAN_FPT")) e->plan_fpt = atoi(fp);
+    // test hook: start near the end of the epoch space to exercise the wrap-around clear
+    if (const char* ep = getenv("UVHTTP_WS_EPOCH_START")) {
+        const unsigned long v = strtoul(ep, nullptr, 0);
+        e->epoch = v < kMaxEpoch ? (uint32_t)v : 0;
+    }
     if (const char* wm = getenv("UVHTTP_WS_WALK"))
         e->walk_mode = strcmp(wm, "lane") == 0 ? 1 : strcmp(wm, "wave") == 0 ? 2 : 0;
     *out = e;
@@ -1900,10 +1963,9 @@ static void timing_end(uvhttp_ws_gpu_engine_t* e, int k, hipStream_t s) {
     e->ev_used = k + 1;
 }
 
-// Flags hold the epoch in 30 bits.  When the epoch space is used up the workspace is cleared
-// on the call's stream (once per 2^30 - 1 calls), so no entry left by an earlier call can
-// carry a live tag.
-constexpr uint32_t kMaxEpoch = (1u << 30) - 1;
+// Record tags hold the epoch in 30 bits.  When the epoch space is used up the workspace is
+// cleared on the call's stream (once per 2^30 - 1 calls), so no entry left by an earlier call
+// can carry a live tag.
 
 static uint32_t next_epoch(uvhttp_ws_gpu_engine_t* e, hipStream_t s) {
     if (e->epoch >= kMaxEpoch) {
