@@ -71,7 +71,8 @@ def main():
                     kern[k].append(ms / max(cnt, 1))
         for k in (0, 1):
             s = engs[k].read_summary(outs[k][1])
-            assert s["n_delivered"] == n and s["status"] == 0, (names[k], s)
+            if not os.environ.get("AB_NOCHECK"):  # experiment builds may decode wrongly
+                assert s["n_delivered"] == n and s["status"] == 0, (names[k], s)
         ms = [statistics.median(x) for x in step]
         ks = [statistics.median(x) for x in kern]
         print(f"{cfg} {mode:8s} step A {ms[0]*1e3:9.1f} us  B {ms[1]*1e3:9.1f} us  "

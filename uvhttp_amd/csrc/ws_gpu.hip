@@ -319,12 +319,11 @@ __device__ inline u32x4 load_header(const BatchArgs& a, uint64_t o) {
     return u32x4{t[0], t[1], t[2], t[3]};
 }
 
-__device__ inline ScanElem parse_hdr(const BatchArgs& a, uvhttp_ws_frame_desc_t* desc, uint32_t i,
-                                     const SegInfo& g, uint64_t o, u32x4 hv) {
+__device__ inline ScanElem parse_hdr(const BatchArgs& a, uint32_t i, const SegInfo& g, uint64_t o,
+                                     u32x4 hv, uvhttp_ws_frame_desc_t& d) {
     const uint64_t slot = g.end > o ? g.end - o : 0;
     const bool last = g.last;
 
-    uvhttp_ws_frame_desc_t d;
     d.payload_off = o;  // frames that do not parse keep a monotonic (empty) payload
     d.payload_len = 0;
     d.masking_key = 0;
@@ -408,17 +407,16 @@ __device__ inline ScanElem parse_hdr(const BatchArgs& a, uvhttp_ws_frame_desc_t*
         else if (fed < wlen) st = UVHTTP_WS_FRAME_INCOMPLETE;
     }
     d.status = (int8_t)st;
-    desc[i] = d;
     ScanElem elem = scan_identity();
     if (st == UVHTTP_WS_FRAME_OK) elem = scan_elem_of(d, (int32_t)i, g.head);
     else if (g.head) elem.bits = kHead;
     return elem;
 }
 
-__device__ inline ScanElem parse_one(const BatchArgs& a, uvhttp_ws_frame_desc_t* desc, uint32_t i,
-                                     const SegInfo& g) {
+__device__ inline ScanElem parse_one(const BatchArgs& a, uint32_t i, const SegInfo& g,
+                                     uvhttp_ws_frame_desc_t& d) {
     const uint64_t o = frame_start(a, i);
-    return parse_hdr(a, desc, i, g, o, load_header(a, o));
+    return parse_hdr(a, i, g, o, load_header(a, o), d);
 }
 
 // resolve_one: frame i's state-machine step.  With E = scan over the frames of the same
@@ -427,10 +425,10 @@ __device__ inline ScanElem parse_one(const BatchArgs& a, uvhttp_ws_frame_desc_t*
 // is not a zero-length start (a zero-length first fragment allocates nothing, so
 // fragmented_message stays NULL, src/uvhttp_websocket.c:794-816 + :964).  With no data
 // frame before i in its connection, the state is the connection's initial one.
-__device__ inline void resolve_one(const BatchArgs& a, uvhttp_ws_frame_desc_t* desc,
-                                   uvhttp_ws_message_desc_t* msgs, const Workspace& ws,
-                                   uint32_t i, uint32_t n, const SegInfo& g, ScanElem ex,
-                                   uvhttp_ws_frame_desc_t d) {
+// d: the frame's parsed descriptor (registers), completed here; the caller stores it once
+__device__ inline void resolve_one(const BatchArgs& a, uvhttp_ws_message_desc_t* msgs,
+                                   const Workspace& ws, uint32_t i, uint32_t n, const SegInfo& g,
+                                   ScanElem ex, uvhttp_ws_frame_desc_t& d) {
     if (g.head) ex = scan_identity();  // nothing of this connection precedes its first frame
 
     // in-place tiles whose start byte lies in this frame's span up to the next frame (frame
@@ -491,10 +489,7 @@ __device__ inline void resolve_one(const BatchArgs& a, uvhttp_ws_frame_desc_t* d
                     tag_claim(&ws.arena_first[t], a.epoch, i);
             }
         }
-        desc[i].status = (int8_t)st;
-        desc[i].message = d.message;
-        desc[i].payload_off = d.payload_off;
-        desc[i].flags = d.flags;
+        d.status = (int8_t)st;
     }
     if (a.open_after) a.open_after[i] = open_after;
     if (st != UVHTTP_WS_FRAME_OK) {
@@ -666,19 +661,25 @@ __global__ __launch_bounds__(kBlock) void k_plan(BatchArgs a, uvhttp_ws_frame_de
     const uint32_t i0 = (b * kBlock + threadIdx.x) * FPT;
     if (FPT == 1) {
         SegInfo g;
+        uvhttp_ws_frame_desc_t d;
         ScanElem elem = scan_identity();
         if (i0 < n) {
             g = seg_info(a, i0, n);
-            elem = parse_one(a, desc, i0, g);
+            elem = parse_one(a, i0, g, d);
         }
         ScanElem agg;
         const ScanElem local = block_exclusive_scan(elem, &agg);
         const ScanElem pre = lookback_prefix(ws, b, agg, a.epoch);
-        if (i0 < n) resolve_one(a, desc, msgs, ws, i0, n, g, scan_combine(pre, local), desc[i0]);
+        if (i0 < n) {
+            resolve_one(a, msgs, ws, i0, n, g, scan_combine(pre, local), d);
+            desc[i0] = d;
+        }
         return;
     }
-    // pass 1: all header loads of the lane's frames in flight together, then parse
+    // pass 1: all header loads of the lane's frames in flight together, then parse into
+    // registers (descriptors are stored once, after the state machine)
     ScanElem tagg = scan_identity();
+    uvhttp_ws_frame_desc_t dv[FPT];
     {
         uint64_t o[FPT];
         u32x4 hv[FPT];
@@ -689,18 +690,13 @@ __global__ __launch_bounds__(kBlock) void k_plan(BatchArgs a, uvhttp_ws_frame_de
 #pragma unroll
         for (int k = 0; k < FPT; ++k) {
             const uint32_t i = i0 + k;
-            if (i < n) tagg = scan_combine(tagg, parse_hdr(a, desc, i, seg_info(a, i, n), o[k], hv[k]));
+            if (i < n) tagg = scan_combine(tagg, parse_hdr(a, i, seg_info(a, i, n), o[k], hv[k], dv[k]));
         }
     }
     ScanElem agg;
     const ScanElem local = block_exclusive_scan(tagg, &agg);
     ScanElem run = scan_combine(lookback_prefix(ws, b, agg, a.epoch), local);
-    // pass 2: the lane's descriptors (its own pass-1 stores) loaded together, then the state
-    // machine in frame order
-    uvhttp_ws_frame_desc_t dv[FPT];
-#pragma unroll
-    for (int k = 0; k < FPT; ++k)
-        if (i0 + k < n) dv[k] = desc[i0 + k];
+    // pass 2: the state machine in frame order
 #pragma unroll
     for (int k = 0; k < FPT; ++k) {
         const uint32_t i = i0 + k;
@@ -709,7 +705,8 @@ __global__ __launch_bounds__(kBlock) void k_plan(BatchArgs a, uvhttp_ws_frame_de
             ScanElem e = scan_identity();
             if (dv[k].status == UVHTTP_WS_FRAME_OK) e = scan_elem_of(dv[k], (int32_t)i, g.head);
             else if (g.head) e.bits = kHead;
-            resolve_one(a, desc, msgs, ws, i, n, g, run, dv[k]);
+            resolve_one(a, msgs, ws, i, n, g, run, dv[k]);
+            desc[i] = dv[k];
             run = scan_combine(run, e);
         }
     }
