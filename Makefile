@@ -30,7 +30,7 @@ oracle:
 
 asm: uvhttp_amd/csrc/ws_gpu.hip
 	@mkdir -p $(BUILD)
-	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o $(BUILD)/ws_gpu.s $<
+	$(HIPCC) $(HIPFLAGS) -Wno-unused-command-line-argument --cuda-device-only -S -o $(BUILD)/ws_gpu.s $<
 
 clean:
 	rm -rf $(BUILD) uvhttp_amd/lib

@@ -65,14 +65,17 @@ def _rand_frames(rng, src_len, n, sizes):
     return fr
 
 
+# cap_extra moves the caller's capacity per frame, which picks the emit shape and the output
+# map granularity: every shape must handle frames much smaller and much larger than its map tile
+@pytest.mark.parametrize("cap_extra", [64, 1 << 22])
 @pytest.mark.parametrize("seed", range(8))
-def test_build_matches_oracle(torch, eng, seed):
+def test_build_matches_oracle(torch, eng, seed, cap_extra):
     rng = random.Random(seed)
     src = np.frombuffer(rng.randbytes(300000), np.uint8).copy()
     sizes = [[0, 1, 5, 125, 126, 127, 200], [1000, 4095, 65535, 65536, 70000],
              [0, 3, 300, 65536]][seed % 3]
     frames = _rand_frames(rng, src.size, rng.choice([1, 17, 300, 2000]), sizes)
-    exp, total, out, off = _build(torch, eng, src, frames)
+    exp, total, out, off = _build(torch, eng, src, frames, cap_extra=cap_extra)
     assert int(off[len(frames)]) == total
     assert np.array_equal(off[:len(frames)], np.cumsum([0] + [len(b) for b in exp[:-1]]))
     assert out[:total].tobytes() == b"".join(exp)

@@ -1433,6 +1433,23 @@ __global__ __launch_bounds__(kBlock) void k_stream_mark(BatchArgs a, uvhttp_ws_f
 // LDS) and its payload (one unaligned 16-byte source window, XORed with the rotated key
 // for client frames).  Bytes per frame: P read + (H + 4m + P) written.
 // ------------------------------------------------------------------------------------
+// Emit record of one built frame, copied by kb_offsets into every 16 KiB output-map tile whose
+// first byte the frame covers (exactly one frame covers a byte, so each tile has one writer
+// and no atomics).  64 bytes = one scalar s_load_dwordx16 in kb_emit, so a tile's lookup is a
+// single dependent round trip before its payload loads.
+struct __attribute__((aligned(64))) BuildRec {
+    uint64_t st;     // frame start in out
+    uint64_t ps;     // payload start in out
+    uint64_t fe;     // frame end in out
+    uint64_t src;    // payload offset in src
+    u32x4 img;       // header image (<= 14 bytes)
+    uint32_t key;    // 0 for server frames (XOR no-op)
+    uint32_t frame;  // frame index
+    uint32_t tag;    // epoch of the call that wrote it
+    uint32_t pad;
+};
+static_assert(sizeof(BuildRec) == 64, "one s_load_dwordx16");
+
 struct BuildArgs {
     const uint8_t* src;
     uint64_t src_len;
@@ -1443,8 +1460,10 @@ struct BuildArgs {
     uint64_t* out_off;   // [n + 1]
     uint64_t* blk;       // per-block sums -> prefixes (u64 scratch)
     uint64_t* grp;       // per-group sums -> prefixes, [n_groups] = total
-    uint32_t* map;       // output tile (16 KiB) -> first frame
+    BuildRec* mrec;      // output map tile -> record of the frame covering its first byte
     uint64_t n_map;
+    uint32_t map_shift;  // log2 of the map tile (>= the emit tile; ~ the average frame size)
+    uint32_t epoch;      // tag of this call's map records (stale records never match)
 };
 
 __device__ inline uint64_t build_size(const uvhttp_ws_build_desc_t& f) {
@@ -1479,8 +1498,6 @@ __global__ __launch_bounds__(kBlock) void kb_size(BuildArgs b) {
     uint64_t total;
     (void)block_exclusive_sum_u64(sz, &total);
     if (threadIdx.x == 0) b.blk[blockIdx.x] = total;
-    const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    for (uint64_t t = gtid; t < b.n_map; t += (uint64_t)gridDim.x * kBlock) b.map[t] = kNoFrame;
 }
 
 __global__ __launch_bounds__(kBlock) void kb_scan_groups(BuildArgs b, uint32_t n_blocks) {
@@ -1512,20 +1529,6 @@ __global__ __launch_bounds__(kBlock) void kb_scan_top(BuildArgs b, uint32_t n_gr
     if (threadIdx.x == 0) b.grp[n_groups] = total;
 }
 
-__global__ __launch_bounds__(kBlock) void kb_offsets(BuildArgs b, uint32_t n_groups) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    const uint64_t sz = i < b.n ? build_size(b.frames[i]) : 0;
-    uint64_t total;
-    const uint64_t local = block_exclusive_sum_u64(sz, &total);
-    if (i >= b.n) return;
-    const uint64_t off = b.grp[blockIdx.x / kBlock] + b.blk[blockIdx.x] + local;
-    b.out_off[i] = off;
-    if (i + 1 == b.n) b.out_off[b.n] = b.grp[n_groups];
-    if (b.grp[n_groups] > b.out_cap) return;  // nothing will be written
-    for (uint64_t t = (off + kMapTile - 1) / kMapTile; t * kMapTile < off + sz && t < b.n_map; ++t)
-        atomicMin(&b.map[t], i);
-}
-
 // header image of a built frame (<= 14 bytes: byte 0, byte 1, extended length, key)
 __device__ inline u32x4 build_header(const uvhttp_ws_build_desc_t& d, uint32_t* hsz) {
     const uint64_t p = d.payload_len;
@@ -1553,22 +1556,51 @@ __device__ inline u32x4 build_header(const uvhttp_ws_build_desc_t& d, uint32_t* 
     return u32x4{w[0], w[1], w[2], w[3]};
 }
 
+__global__ __launch_bounds__(kBlock) void kb_offsets(BuildArgs b, uint32_t n_groups) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t sz = i < b.n ? build_size(b.frames[i]) : 0;
+    uint64_t total;
+    const uint64_t local = block_exclusive_sum_u64(sz, &total);
+    if (i >= b.n) return;
+    const uint64_t off = b.grp[blockIdx.x / kBlock] + b.blk[blockIdx.x] + local;
+    b.out_off[i] = off;
+    if (i + 1 == b.n) b.out_off[b.n] = b.grp[n_groups];
+    if (b.grp[n_groups] > b.out_cap) return;  // nothing will be written (no record is tagged)
+    const uvhttp_ws_build_desc_t d = b.frames[i];
+    BuildRec r;
+    uint32_t hm;
+    r.img = build_header(d, &hm);
+    r.st = off;
+    r.ps = off + hm;
+    r.fe = r.ps + d.payload_len;
+    r.src = d.payload_off;
+    r.key = d.mask ? d.masking_key : 0u;
+    r.frame = i;
+    r.tag = b.epoch;
+    r.pad = 0;
+    const uint64_t g = 1ull << b.map_shift;
+    for (uint64_t t = (off + g - 1) >> b.map_shift; (t << b.map_shift) < off + sz && t < b.n_map; ++t)
+        b.mrec[t] = r;
+}
+
 // bytes of output vector [oa, oa + 16) that belong to frame (header image img over
 // [fs, ps), payload src[sp ...] over [ps, fe), key for client frames)
 __device__ inline void build_vector(const BuildArgs& b, uint64_t oa, uint64_t fs, uint64_t ps,
                                     uint64_t fe, uint64_t sp, uint32_t key, const u32x4& img,
                                     u32x4& out) {
     if (ps > oa && fs < oa + 16) {
-        const uint32_t iw[4] = {img.x, img.y, img.z, img.w};
-        uint32_t ow[4] = {0, 0, 0, 0};
-        for (int bq = 0; bq < 16; ++bq) {
-            const uint64_t x = oa + bq;
-            if (x >= fs && x < ps) {
-                const uint32_t k = (uint32_t)(x - fs);
-                ow[bq >> 2] |= ((iw[k >> 2] >> (8 * (k & 3))) & 0xFF) << (8 * (bq & 3));
-            }
-        }
-        out |= u32x4{ow[0], ow[1], ow[2], ow[3]};
+        // the header image moved to the vector's byte phase: output byte q = image byte
+        // q - (fs - oa), one 128-bit shift instead of a byte loop
+        const int64_t d = (int64_t)fs - (int64_t)oa;  // -13 .. 15
+        unsigned __int128 v = ((unsigned __int128)(((uint64_t)img.w << 32) | img.z) << 64) |
+                              (((uint64_t)img.y << 32) | img.x);
+        v = d >= 0 ? v << (8 * d) : v >> (-8 * d);
+        const int lo_b = d > 0 ? (int)d : 0;
+        const int hi_b = ps < oa + 16 ? (int)(ps - oa) : 16;
+        const u32x4 sel{lane_bytes(lo_b, hi_b, 0), lane_bytes(lo_b, hi_b, 1),
+                        lane_bytes(lo_b, hi_b, 2), lane_bytes(lo_b, hi_b, 3)};
+        const uint64_t lo = (uint64_t)v, hi = (uint64_t)(v >> 64);
+        out |= u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)} & sel;
     }
     if (fe > ps && ps < oa + 16 && fe > oa) {
         const int lo_b = ps > oa ? (int)(ps - oa) : 0;
@@ -1592,16 +1624,19 @@ __global__ __launch_bounds__(BLOCK) void kb_emit(BuildArgs b, uint64_t tile_base
     __shared__ uint32_t s_key[BLOCK];    // 0 for server frames (XOR no-op)
     __shared__ u32x4 s_hdr[BLOCK];       // header image (<= 14 bytes)
 
-    const uint64_t total = b.out_off[b.n];
-    if (total > b.out_cap || b.n == 0) return;
     const uint64_t t0 = (tile_base + blockIdx.x) * kT;
-    if (t0 >= total) return;
-    const uint64_t c0 = t0 / kMapTile, c1 = (t0 + kT - 1) / kMapTile + 1;
-    const uint32_t last = b.n - 1;
-    uint32_t f0 = b.map[c0];
-    if (f0 > last) f0 = 0;  // cannot happen for t0 < total; stay in bounds regardless
-    uint32_t f1 = (c1 < b.n_map) ? b.map[c1] : last;
-    if (f1 > last || f1 < f0) f1 = last;
+    // map tiles are a power of two >= kT (host), so the tile lies inside map tile c0
+    const uint64_t c0 = t0 >> b.map_shift, c1 = c0 + 1;
+    if (c0 >= b.n_map) return;
+    // both records in one round trip (the map has a spare entry past n_map, never tagged);
+    // the empty asm makes the compiler issue every field's load before the tag test
+    const BuildRec r0 = b.mrec[c0];
+    const BuildRec r1 = b.mrec[c0 + 1];
+    asm volatile("" ::"s"(r0.st), "s"(r0.ps), "s"(r0.fe), "s"(r0.src), "s"(r0.key),
+                 "s"(r1.st), "s"(r1.ps), "s"(r1.fe), "s"(r1.src), "s"(r1.key), "s"(r1.frame),
+                 "s"(r1.tag));
+    if (r0.tag != b.epoch) return;  // tile past the end of the output (or over capacity)
+    const bool v1 = c1 < b.n_map && r1.tag == b.epoch;
 
     uint64_t oa[VPT];
     u32x4 out[VPT];
@@ -1610,22 +1645,31 @@ __global__ __launch_bounds__(BLOCK) void kb_emit(BuildArgs b, uint64_t tile_base
         oa[v] = t0 + ((uint64_t)v * BLOCK + threadIdx.x) * 16u;
         out[v] = u32x4{0, 0, 0, 0};
     }
-    if (f1 - f0 < 2) {
-        // fast path (frames of ~4 KiB and up): at most two frames touch the tile; their
-        // descriptors are uniform scalar loads, no LDS staging
-        for (uint32_t f = f0; f <= f1; ++f) {
-            const uvhttp_ws_build_desc_t d = b.frames[f];
-            uint32_t hm;
-            const u32x4 img = build_header(d, &hm);
-            const uint64_t st = b.out_off[f];
-            const uint64_t ps = st + hm, fe = ps + d.payload_len;
-            const uint32_t key = d.mask ? d.masking_key : 0u;
+    if (v1 && r1.frame - r0.frame < 2) {
+        // fast path (frames of ~4 KiB and up): the frame covering the tile start and the one
+        // covering the next map tile's start cover every byte of the tile, and both records
+        // arrived with the lookup — every vector is whole, no bound check
+#pragma unroll
+        for (int v = 0; v < VPT; ++v)
+            if (r0.fe > oa[v])
+                build_vector(b, oa[v], r0.st, r0.ps, r0.fe, r0.src, r0.key, r0.img, out[v]);
+        if (r1.frame != r0.frame) {
 #pragma unroll
             for (int v = 0; v < VPT; ++v)
-                if (fe > oa[v] && st < oa[v] + 16) build_vector(b, oa[v], st, ps, fe, d.payload_off, key, img, out[v]);
+                if (r1.st < oa[v] + 16)
+                    build_vector(b, oa[v], r1.st, r1.ps, r1.fe, r1.src, r1.key, r1.img, out[v]);
         }
+#pragma unroll
+        for (int v = 0; v < VPT; ++v)
+            __builtin_nontemporal_store(out[v], reinterpret_cast<u32x4*>(b.out + oa[v]));
+        return;
     }
-    for (uint32_t base = f0; f1 - f0 >= 2 && base <= f1; base += BLOCK) {
+    const uint64_t total = b.out_off[b.n];
+    const uint32_t last = b.n - 1;
+    const uint32_t f0 = r0.frame;
+    uint32_t f1 = v1 ? r1.frame : last;
+    if (f1 > last || f1 < f0) f1 = last;
+    for (uint32_t base = f0; base <= f1; base += BLOCK) {
         const uint32_t cnt = (f1 - base + 1) < (uint32_t)BLOCK ? (f1 - base + 1) : BLOCK;
         __syncthreads();
         if (threadIdx.x < cnt) {
@@ -1770,6 +1814,9 @@ struct uvhttp_ws_gpu_engine {
     void* ss_mem;              // stream-decode scratch
     uint32_t ss_frames, ss_streams;
     StreamScratch ss;
+    void* bs_mem;              // send-side output-map records (BuildRec per map tile)
+    uint64_t bs_tiles;
+    int build_small;           // emit shape for frames < 4 KiB (UVHTTP_WS_BUILD_SMALL, tuning)
     hipEvent_t ev[2 * 1024];
     int ev_created;
     int ev_used;       // event pairs recorded and not yet harvested
@@ -1781,6 +1828,17 @@ struct uvhttp_ws_gpu_engine {
 static int set_err(uvhttp_ws_gpu_engine_t* e, int code, const char* what, hipError_t h) {
     if (e) snprintf(e->err, sizeof(e->err), "%s: %s", what, h == hipSuccess ? "" : hipGetErrorString(h));
     return code;
+}
+
+template <int BLOCK, int VPT>
+static void launch_emit(const BuildArgs& b, uint32_t n_frames, uint64_t out_cap, hipStream_t s) {
+    const uint64_t tile_bytes = (uint64_t)BLOCK * VPT * 16;
+    const uint64_t n_ptiles = (out_cap + tile_bytes - 1) / tile_bytes;
+    const uint64_t max_tiles = (1ull << 24);
+    for (uint64_t tb = 0; n_frames && tb < n_ptiles; tb += max_tiles) {
+        const uint32_t grid_p = (uint32_t)((n_ptiles - tb) < max_tiles ? (n_ptiles - tb) : max_tiles);
+        hipLaunchKernelGGL((kb_emit<BLOCK, VPT>), dim3(grid_p), dim3(BLOCK), 0, s, b, tb);
+    }
 }
 
 extern "C" {
@@ -1811,6 +1869,7 @@ int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out) {
         const unsigned long v = strtoul(ep, nullptr, 0);
         e->epoch = v < kMaxEpoch ? (uint32_t)v : 0;
     }
+    if (const char* bs = getenv("UVHTTP_WS_BUILD_SMALL")) e->build_small = atoi(bs);
     if (const char* wm = getenv("UVHTTP_WS_WALK"))
         e->walk_mode = strcmp(wm, "lane") == 0 ? 1 : strcmp(wm, "wave") == 0 ? 2 : 0;
     *out = e;
@@ -1824,6 +1883,7 @@ void uvhttp_ws_gpu_engine_free(uvhttp_ws_gpu_engine_t* e) {
     (void)hipSetDevice(e->device);
     if (e->ws_mem) (void)hipFree(e->ws_mem);
     if (e->ss_mem) (void)hipFree(e->ss_mem);
+    if (e->bs_mem) (void)hipFree(e->bs_mem);
     for (int k = 0; k < e->ev_created; ++k) (void)hipEventDestroy(e->ev[k]);
     (void)hipSetDevice(prev);
     free(e);
@@ -1967,6 +2027,7 @@ static void timing_end(uvhttp_ws_gpu_engine_t* e, int k, hipStream_t s) {
 static uint32_t next_epoch(uvhttp_ws_gpu_engine_t* e, hipStream_t s) {
     if (e->epoch >= kMaxEpoch) {
         (void)hipMemsetAsync(e->ws_mem, 0, e->ws_bytes, s);
+        if (e->bs_mem) (void)hipMemsetAsync(e->bs_mem, 0, e->bs_tiles * sizeof(BuildRec), s);
         e->epoch = 0;
     }
     return ++e->epoch;
@@ -2239,7 +2300,7 @@ int uvhttp_ws_gpu_build_frames(uvhttp_ws_gpu_engine_t* e, const uint8_t* d_src, 
         return set_err(e, UVHTTP_WS_GPU_EINVAL, "out must be 16-byte aligned", hipSuccess);
     if (n_frames > kMaxFrames) return set_err(e, UVHTTP_WS_GPU_EINVAL, "too many frames", hipSuccess);
     // scratch: reuse the engine workspace (block/group aggregates as u64, arena map)
-    int rc = uvhttp_ws_gpu_engine_reserve(e, n_frames ? n_frames : 1, 0, out_cap);
+    int rc = uvhttp_ws_gpu_engine_reserve(e, n_frames ? n_frames : 1, 0, 0);
     if (rc) return rc;
     int prev = 0;
     (void)hipGetDevice(&prev);
@@ -2255,8 +2316,40 @@ int uvhttp_ws_gpu_build_frames(uvhttp_ws_gpu_engine_t* e, const uint8_t* d_src, 
     b.out_off = d_out_off;
     b.blk = reinterpret_cast<uint64_t*>(e->ws.block_agg);
     b.grp = reinterpret_cast<uint64_t*>(e->ws.group_agg);
-    b.map = reinterpret_cast<uint32_t*>(e->ws.arena_first);
-    b.n_map = (out_cap + kMapTile - 1) / kMapTile;
+    // emit shape and map granularity from the average frame (the caller's capacity per frame):
+    // frames >= 4 KiB take 2 KiB tiles whose two map records (the frame covering the tile's map
+    // tile and the next one's) usually cover the whole tile; smaller frames take 16 KiB tiles
+    // that stage their frames in LDS.  Map tile = largest power of two <= the average frame,
+    // clamped to [tile, 64 KiB], so consecutive map records are at most one frame apart.
+    const uint64_t avg = n_frames ? out_cap / n_frames : out_cap;
+    const bool small = avg < 4096;
+    // small-frame tile: 0 = 64 x 2 (2 KiB, default), 1 = 64 x 4, 2 = 128 x 2, 3 = 256 x 4
+    const int sh = small ? e->build_small : 0;
+    const uint32_t tile_shift = sh == 3 ? 14 : (sh == 1 || sh == 2) ? 12 : 11;
+    uint32_t shift = small ? 14 : 11;
+    if (shift < tile_shift) shift = tile_shift;
+    while (shift < 16 && (2ull << shift) <= avg) ++shift;
+    b.map_shift = shift;
+    b.n_map = (out_cap + (1ull << shift) - 1) >> shift;
+    if (b.n_map + 1 > e->bs_tiles) {
+        if (e->bs_mem) (void)hipFree(e->bs_mem);
+        e->bs_mem = nullptr;
+        e->bs_tiles = 0;
+        // + 1: kb_emit reads the record after its tile's; that spare entry is never tagged
+        hipError_t h = hipMalloc(&e->bs_mem, (b.n_map + 1) * sizeof(BuildRec));
+        // zero: tag 0 never matches a live epoch (epochs >= 1)
+        if (h == hipSuccess) h = hipMemset(e->bs_mem, 0, (b.n_map + 1) * sizeof(BuildRec));
+        if (h == hipSuccess) h = hipDeviceSynchronize();
+        if (h != hipSuccess) {
+            if (e->bs_mem) (void)hipFree(e->bs_mem);
+            e->bs_mem = nullptr;
+            if (prev != e->device) (void)hipSetDevice(prev);
+            return set_err(e, UVHTTP_WS_GPU_ENOMEM, "hipMalloc build map", h);
+        }
+        e->bs_tiles = b.n_map + 1;
+    }
+    b.mrec = reinterpret_cast<BuildRec*>(e->bs_mem);
+    b.epoch = next_epoch(e, s);
     const uint32_t grid_f = n_frames ? (n_frames + kBlock - 1) / kBlock : 1;
     const uint32_t n_groups = (grid_f + kBlock - 1) / kBlock;
     hipLaunchKernelGGL(kb_size, dim3(grid_f), dim3(kBlock), 0, s, b);
@@ -2267,15 +2360,11 @@ int uvhttp_ws_gpu_build_frames(uvhttp_ws_gpu_engine_t* e, const uint8_t* d_src, 
         // d_out_off[0] = 0 (total) for an empty batch
         (void)hipMemsetAsync(d_out_off, 0, 8, s);
     }
-    constexpr int kB = 64, kV = 2;
-    const uint64_t tile_bytes = (uint64_t)kB * kV * 16;
-    const uint64_t n_ptiles = (out_cap + tile_bytes - 1) / tile_bytes;
-    const uint64_t max_tiles = (1ull << 24);
     const int tk = timing_begin(e, s);
-    for (uint64_t tb = 0; n_frames && tb < n_ptiles; tb += max_tiles) {
-        const uint32_t grid_p = (uint32_t)((n_ptiles - tb) < max_tiles ? (n_ptiles - tb) : max_tiles);
-        hipLaunchKernelGGL((kb_emit<kB, kV>), dim3(grid_p), dim3(kB), 0, s, b, tb);
-    }
+    if (sh == 3) launch_emit<256, 4>(b, n_frames, out_cap, s);
+    else if (sh == 2) launch_emit<128, 2>(b, n_frames, out_cap, s);
+    else if (sh == 1) launch_emit<64, 4>(b, n_frames, out_cap, s);
+    else launch_emit<64, 2>(b, n_frames, out_cap, s);
     timing_end(e, tk, s);
     const hipError_t h = hipGetLastError();
     if (prev != e->device) (void)hipSetDevice(prev);
