@@ -216,3 +216,107 @@ def build_frame(payload: bytes, opcode, mask, fin, key=b"\x00\x00\x00\x00", cap=
     rc = L.oracle_build_frame(out, cap, src if payload else None, len(payload), opcode, mask,
                               fin, kb)
     return rc, bytes(out)[: max(rc, 0)]
+
+
+# ---- TLS record layer (oracle/tls_oracle.c), layouts of include/uvhttp_tls_amd.h ----------
+
+TLS_KEY_DT = np.dtype([("key", "u1", 32), ("iv", "u1", 12), ("key_len", "<u4"),
+                       ("version", "<u4"), ("reserved", "<u4", 3)])
+TLS_STREAM_DT = np.dtype([("begin", "<u8"), ("len", "<u8"), ("seq", "<u8"), ("key", "<u4"),
+                          ("reserved", "<u4")])
+TLS_RECORD_DT = np.dtype([("rec_off", "<u8"), ("out_off", "<u8"), ("content_len", "<u4"),
+                          ("stream", "<u4"), ("type", "u1"), ("status", "i1"),
+                          ("reserved", "<u2"), ("reserved2", "<u4")])
+TLS_RESULT_DT = np.dtype([("first_record", "<u4"), ("n_records", "<u4"),
+                          ("n_delivered", "<u4"), ("status", "<i4"), ("first_status", "<i4"),
+                          ("reserved", "<u4"), ("consumed_bytes", "<u8"), ("next_seq", "<u8"),
+                          ("out_off", "<u8"), ("plain_len", "<u8"), ("reserved3", "<u8")])
+TLS_SEAL_DT = np.dtype([("src_off", "<u8"), ("out_off", "<u8"), ("seq", "<u8"),
+                        ("plain_len", "<u4"), ("key", "<u2"), ("type", "u1"),
+                        ("reserved", "u1")])
+assert TLS_KEY_DT.itemsize == 64 and TLS_STREAM_DT.itemsize == 32
+assert TLS_RECORD_DT.itemsize == 32 and TLS_RESULT_DT.itemsize == 64
+assert TLS_SEAL_DT.itemsize == 32
+
+TLS12, TLS13 = 0x0303, 0x0304
+REC_OK, REC_SKIPPED, REC_CONTROL = 0, 2, 3
+REC_OVERFLOW, REC_BAD_MAC, REC_BAD_TYPE, REC_VERSION = -1, -2, -3, -4
+REC_EMPTY, REC_CAPACITY, REC_KEY = -5, -6, -7
+
+
+def _tls_sigs(L):
+    vp, u32, u64, sz = C.c_void_p, C.c_uint32, C.c_uint64, C.c_size_t
+    for name, res, args in [
+        ("oracle_aes_encrypt_block", C.c_int, [vp, C.c_int, vp, vp]),
+        ("oracle_aes_sbox", C.c_uint8, [C.c_uint8]),
+        ("oracle_gf_mult", None, [vp, vp, vp]),
+        ("oracle_gcm", C.c_int, [vp, C.c_int, vp, vp, sz, vp, sz, vp, vp, C.c_int]),
+        ("oracle_tls_open_batch", u64, [vp, u64, vp, u32, vp, u32, vp, u32, vp, vp, u64]),
+        ("oracle_tls_seal_record", u64, [vp, u64, C.c_uint8, vp, u32, u32, vp]),
+        ("oracle_tls_open_stream_bytes", u64, [vp, u64, vp, u64, vp]),
+    ]:
+        fn = getattr(L, name)
+        fn.restype, fn.argtypes = res, args
+    return L
+
+
+def _buf(b: bytes):
+    return (C.c_uint8 * max(1, len(b))).from_buffer_copy(bytes(b) or b"\0")
+
+
+def aes_encrypt_block(key: bytes, block: bytes) -> bytes:
+    L = _tls_sigs(load())
+    out = (C.c_uint8 * 16)()
+    assert L.oracle_aes_encrypt_block(_buf(key), len(key), _buf(block), out) == 0
+    return bytes(out)
+
+
+def gcm(key: bytes, iv: bytes, aad: bytes, data: bytes, tag: bytes = None, decrypt=False):
+    """AES-GCM: encrypt -> (ct, tag); decrypt -> (rc, pt) (rc -2 on a tag mismatch)"""
+    L = _tls_sigs(load())
+    out = (C.c_uint8 * max(1, len(data)))()
+    t = _buf(tag or bytes(16))
+    rc = L.oracle_gcm(_buf(key), len(key), _buf(iv), _buf(aad), len(aad), _buf(data),
+                      len(data), out, t, 1 if decrypt else 0)
+    if decrypt:
+        return rc, bytes(out)[:len(data)]
+    return bytes(out)[:len(data)], bytes(t)
+
+
+def tls_key(key: bytes, iv: bytes, version):
+    k = np.zeros(1, TLS_KEY_DT)
+    k[0]["key"][:len(key)] = np.frombuffer(key, np.uint8)
+    k[0]["iv"][:] = np.frombuffer(iv.ljust(12, b"\0"), np.uint8)
+    k[0]["key_len"] = len(key)
+    k[0]["version"] = version
+    return k
+
+
+def tls_seal(keyrec, seq, type_, content: bytes, pad=0) -> bytes:
+    L = _tls_sigs(load())
+    out = (C.c_uint8 * (len(content) + pad + 64))()
+    n = L.oracle_tls_seal_record(_ptr(keyrec), seq, type_, _buf(content), len(content), pad, out)
+    assert n > 0
+    return bytes(out)[:n]
+
+
+def tls_open_batch(wire: np.ndarray, keys: np.ndarray, streams: np.ndarray, max_records=None,
+                   out_cap=None):
+    """Oracle of uvhttp_tls_gpu_open_records -> (records, results, out)"""
+    L = _tls_sigs(load())
+    w = np.ascontiguousarray(wire, dtype=np.uint8)
+    max_records = max(1, w.size // 5 + 1) if max_records is None else max_records
+    out_cap = w.size if out_cap is None else out_cap
+    recs = np.zeros(max(1, max_records), TLS_RECORD_DT)
+    res = np.zeros(max(1, len(streams)), TLS_RESULT_DT)
+    out = np.zeros(max(1, out_cap), np.uint8)
+    n = L.oracle_tls_open_batch(_ptr(w), w.size, _ptr(keys), len(keys), _ptr(streams),
+                                len(streams), _ptr(recs), max_records, _ptr(res), _ptr(out),
+                                out_cap)
+    return recs[:n], res[:len(streams)], out
+
+
+def tls_open_stream_bytes(keyrec, seq, wire: np.ndarray, out: np.ndarray) -> int:
+    L = _tls_sigs(load())
+    return int(L.oracle_tls_open_stream_bytes(_ptr(keyrec), seq, _ptr(wire), wire.size,
+                                              _ptr(out)))
