@@ -17,20 +17,25 @@ $(BUILD)/ws_gpu.o: uvhttp_amd/csrc/ws_gpu.hip include/uvhttp_ws_amd.h
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
+$(BUILD)/tls_gpu.o: uvhttp_amd/csrc/tls_gpu.hip include/uvhttp_tls_amd.h
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
 $(BUILD)/ws_host.o: uvhttp_amd/csrc/ws_host.c include/uvhttp_ws_amd.h
 	@mkdir -p $(BUILD)
 	$(CC) $(CFLAGS) -c -o $@ $<
 
-$(LIB): $(BUILD)/ws_gpu.o $(BUILD)/ws_host.o
+$(LIB): $(BUILD)/ws_gpu.o $(BUILD)/tls_gpu.o $(BUILD)/ws_host.o
 	@mkdir -p $(dir $@)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
 oracle:
 	$(MAKE) -C oracle
 
-asm: uvhttp_amd/csrc/ws_gpu.hip
+asm: uvhttp_amd/csrc/ws_gpu.hip uvhttp_amd/csrc/tls_gpu.hip
 	@mkdir -p $(BUILD)
-	$(HIPCC) $(HIPFLAGS) -Wno-unused-command-line-argument --cuda-device-only -S -o $(BUILD)/ws_gpu.s $<
+	$(HIPCC) $(HIPFLAGS) -Wno-unused-command-line-argument --cuda-device-only -S -o $(BUILD)/ws_gpu.s uvhttp_amd/csrc/ws_gpu.hip
+	$(HIPCC) $(HIPFLAGS) -Wno-unused-command-line-argument --cuda-device-only -S -o $(BUILD)/tls_gpu.s uvhttp_amd/csrc/tls_gpu.hip
 
 clean:
 	rm -rf $(BUILD) uvhttp_amd/lib

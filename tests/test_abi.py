@@ -48,8 +48,11 @@ def test_no_gpu_means_enodev():
         pytest.skip("GPU present")
     h = C.c_void_p()
     assert U.lib().uvhttp_ws_gpu_engine_create(0, C.byref(h)) == -2
+    assert U.lib().uvhttp_tls_gpu_engine_create(0, C.byref(h)) == -2
     with pytest.raises(U.GpuError):
         U.GpuEngine(0)
+    with pytest.raises(U.GpuError):
+        U.TlsEngine(0)
 
 
 def test_product_does_not_reference_oracle():

@@ -207,6 +207,16 @@ def load_library(path: str) -> C.CDLL:
                                                C.POINTER(Stream), C.POINTER(StreamResult)]),
         "uvhttp_ws_gpu_gen_frames": (C.c_int, [vp, vp, u32, u64, u64, C.c_int, C.c_int, C.c_int,
                                                vp]),
+        # TLS record layer (include/uvhttp_tls_amd.h)
+        "uvhttp_tls_gpu_engine_create": (C.c_int, [C.c_int, C.POINTER(vp)]),
+        "uvhttp_tls_gpu_engine_free": (None, [vp]),
+        "uvhttp_tls_gpu_engine_last_error": (C.c_char_p, [vp]),
+        "uvhttp_tls_gpu_engine_set_timing": (C.c_int, [vp, C.c_int]),
+        "uvhttp_tls_gpu_engine_kernel_time": (C.c_int, [vp, C.POINTER(C.c_double),
+                                                        C.POINTER(u64)]),
+        "uvhttp_tls_gpu_open_records": (C.c_int, [vp, vp, u64, vp, u32, vp, u32, vp, u32, vp, vp,
+                                                  u64, vp]),
+        "uvhttp_tls_gpu_seal_records": (C.c_int, [vp, vp, u64, vp, u32, vp, u32, vp, u64, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -550,3 +560,79 @@ class GpuPipeline:
             self.close()
         except Exception:
             pass
+
+
+# ---- TLS record layer (include/uvhttp_tls_amd.h) -----------------------------------------
+
+TLS_RECORD_BYTES, TLS_RESULT_BYTES = 32, 64
+
+
+class TlsEngine:
+    """Owns a uvhttp_tls_gpu_engine_t.  Keys, streams, records, results and seal descriptors
+    are device uint8 tensors holding the C structs of include/uvhttp_tls_amd.h."""
+
+    def __init__(self, device: int = 0, library: C.CDLL = None):
+        import torch
+        self.torch = torch
+        L = library or lib()
+        self._L = L
+        self.device = device
+        h = C.c_void_p()
+        rc = L.uvhttp_tls_gpu_engine_create(device, C.byref(h))
+        if rc != 0:
+            raise GpuError(f"uvhttp_tls_gpu_engine_create({device}) failed rc={rc} "
+                           "(needs an MI355X / gfx950 and the HIP runtime)")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._L.uvhttp_tls_gpu_engine_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != 0:
+            err = self._L.uvhttp_tls_gpu_engine_last_error(self.h)
+            raise GpuError(f"{what} rc={rc}: {err.decode() if err else ''}")
+
+    def _stream(self, stream):
+        if stream is None:
+            stream = self.torch.cuda.current_stream(self.device)
+        return C.c_void_p(stream.cuda_stream)
+
+    def set_timing(self, on: bool):
+        self._check(self._L.uvhttp_tls_gpu_engine_set_timing(self.h, 1 if on else 0), "timing")
+
+    def kernel_time(self):
+        ms, n = C.c_double(0), C.c_uint64(0)
+        self._check(self._L.uvhttp_tls_gpu_engine_kernel_time(self.h, C.byref(ms), C.byref(n)),
+                    "kernel_time")
+        return ms.value, n.value
+
+    def open_records(self, wire, keys, n_keys, streams, n_streams, max_records, out,
+                     records=None, results=None, wire_len=None, stream=None):
+        """uvhttp_tls_gpu_open_records -> (records, results) device tensors"""
+        t = self.torch
+        dev = f"cuda:{self.device}"
+        if records is None:
+            records = t.zeros(max(1, max_records) * TLS_RECORD_BYTES, dtype=t.uint8, device=dev)
+        if results is None:
+            results = t.zeros(max(1, n_streams) * TLS_RESULT_BYTES, dtype=t.uint8, device=dev)
+        self._check(self._L.uvhttp_tls_gpu_open_records(
+            self.h, C.c_void_p(wire.data_ptr()), wire.numel() if wire_len is None else wire_len,
+            C.c_void_p(keys.data_ptr()), n_keys, C.c_void_p(streams.data_ptr()), n_streams,
+            C.c_void_p(records.data_ptr()), max_records, C.c_void_p(results.data_ptr()),
+            C.c_void_p(out.data_ptr()), out.numel(), self._stream(stream)), "open_records")
+        return records, results
+
+    def seal_records(self, src, recs, n_records, keys, n_keys, out, stream=None):
+        """uvhttp_tls_gpu_seal_records (recs: device tensor of uvhttp_tls_seal_t)"""
+        self._check(self._L.uvhttp_tls_gpu_seal_records(
+            self.h, C.c_void_p(src.data_ptr()), src.numel(), C.c_void_p(recs.data_ptr()),
+            n_records, C.c_void_p(keys.data_ptr()), n_keys, C.c_void_p(out.data_ptr()),
+            out.numel(), self._stream(stream)), "seal_records")

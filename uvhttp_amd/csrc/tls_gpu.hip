@@ -1,0 +1,1062 @@
+// tls_gpu.hip — batched TLS record open / seal (AES-128/256-GCM) for gfx950 (MI355X).
+//
+// the record decrypt that runs ahead of the WebSocket decoder in the
+// reference (mbedtls_ssl_read in on_websocket_read, src/uvhttp_connection.c:1122-1159).  The
+// contract is in include/uvhttp_tls_amd.h and is restated on the CPU by oracle/tls_oracle.c.
+//
+// One call = key schedules -> record walk (count, scan, write) -> record crypto -> finalize
+// (stop rules, final content offsets) -> left-shift fix-up for connections whose TLS 1.3
+// records carried padding.  All on one stream, no host synchronisation.
+//
+// Record crypto (k_tls_crypt): AES-GCM is integer/bitwise work with no matrix shape — no MFMA.
+// One wavefront per record (<= 1028 GHASH blocks):
+//   * block i of the record's GHASH sequence (AAD, ciphertext blocks, length block; left-padded
+//     with zero blocks to a multiple of 64) goes to lane i % 64, so every load and store of the
+//     wave is one contiguous 1 KiB run of ciphertext;
+//   * AES-CTR with the T-table round (four lookups + XORs per column) from ONE 1 KiB table
+//     replicated 32 times in LDS (copy = lane % 32, word = x * 32 + copy): ds_read_b32 banks
+//     are (addr / 4) % 32 per 32-lane half, so every lookup of a wave is conflict-free; the
+//     other three tables are byte rotations;
+//   * GHASH: each lane runs Horner with multiplier H^64 over its strided blocks, then a
+//     6-level shuffle tree (multipliers H, H^2 ... H^32) and a final x H combine the lanes.
+//     Every multiply is Shoup's 4-bit table method: a 256-byte table of P * (4-bit
+//     polynomials) per multiplier P — 16 entries of 16 B fill one LDS bank row, so the
+//     ds_read_b128 lookups of a 16-lane group never conflict.  The 7 tables (H^(2^k),
+//     k = 0..6) are built once per key by k_tls_keys.
+//   * the lane holding the AAD block computes E(K, J0) for the tag instead of a keystream
+//     block; TLS 1.3's content type is the last non-zero inner byte, found by a wave max.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "uvhttp_tls_amd.h"
+
+namespace {
+
+constexpr int kBlock = 256;            // walk / finalize kernels: one lane per connection
+constexpr int kCryptWG = 256;          // crypto kernel: 4 waves, one record per wave
+constexpr int kCryptWaves = kCryptWG / 64;
+constexpr uint32_t kMaxLen13 = 16384 + 1 + 16;  // TLSCiphertext.length limits
+constexpr uint32_t kMaxLen12 = 16384 + 8 + 16;
+
+struct U128 {  // a GCM block as a big-endian 128-bit value (bit 0 of the spec = MSB of hi)
+    uint64_t hi, lo;
+};
+
+// Per key slot, built by k_tls_keys (2 KiB).
+struct __attribute__((aligned(64))) KeySched {
+    U128 tab[7][16];   // 4-bit Shoup tables of H^(2^k), k = 0..6
+    uint32_t rk[60];   // FIPS-197 round-key words, big-endian
+    uint32_t nr;       // 10 / 14; 0 = invalid key
+    uint32_t version;  // UVHTTP_TLS_VERSION_12 / _13
+    uint32_t iv[3];    // iv as big-endian words
+    uint32_t pad[11];
+};
+static_assert(sizeof(KeySched) == 2112, "key schedule layout");
+
+// One counted record (walk -> crypto -> finalize).
+struct RecWork {
+    uint64_t rec_off;     // header offset in wire
+    uint64_t spec_off;    // content position in out if every earlier record fills its reservation
+    uint64_t seq;         // sequence number
+    uint32_t len;         // TLSCiphertext.length
+    uint32_t stream;
+    uint32_t key;
+    int32_t status;       // header status from the walk, then the open result
+    uint32_t content_len;
+    uint32_t type;
+};
+static_assert(sizeof(RecWork) == 48, "record work layout");
+
+struct StreamWork {       // walk pass 1 -> pass 2
+    uint32_t n_rec;
+    uint32_t key_bad;
+    uint64_t cap;
+};
+
+struct TlsArgs {
+    const uint8_t* wire;
+    uint64_t wire_len;
+    const uvhttp_tls_key_t* keys;
+    uint32_t n_keys;
+    const uvhttp_tls_stream_t* streams;
+    uint32_t n_streams;
+    uvhttp_tls_record_t* records;
+    uint32_t max_records;
+    uvhttp_tls_result_t* results;
+    uint8_t* out;
+    uint64_t out_cap;
+    const KeySched* sched;
+    RecWork* work;
+    StreamWork* sw;
+    uint64_t* blk;        // per-256-stream block: [2b] records, [2b+1] reserved bytes
+    uint32_t* n_total;    // [0] records to open (0 on capacity failure), [1] capacity failed
+    uint32_t* fix;        // per connection: 1 = content must move left (padding)
+    const uint32_t* te0;  // AES T-table (1 KiB), built once per engine
+};
+
+// ---- GF(2^128) ------------------------------------------------------------------------
+
+__device__ inline U128 gf_xor(U128 a, U128 b) { return U128{a.hi ^ b.hi, a.lo ^ b.lo}; }
+
+// multiply by x (SP 800-38D: right shift, reduce with R = 0xE1 || 0^120)
+__device__ inline U128 gf_mulx(U128 v) {
+    const uint64_t lsb = v.lo & 1;
+    v.lo = (v.lo >> 1) | (v.hi << 63);
+    v.hi = (v.hi >> 1) ^ (lsb ? 0xE100000000000000ull : 0ull);
+    return v;
+}
+
+// generic bit-serial multiply (SP 800-38D Algorithm 1): key setup only
+__device__ U128 gf_mul_slow(U128 x, U128 y) {
+    U128 z{0, 0};
+    for (int i = 0; i < 128; ++i) {
+        const uint64_t bit = i < 64 ? (x.hi >> (63 - i)) & 1 : (x.lo >> (127 - i)) & 1;
+        if (bit) z = gf_xor(z, y);
+        y = gf_mulx(y);
+    }
+    return z;
+}
+
+// Shoup 4-bit table of P: T[8] = P, T[4] = P.x, T[2] = P.x^2, T[1] = P.x^3, T[a ^ b] = T[a] ^ T[b]
+__device__ void gf_table(U128 p, U128* t) {
+    U128 b[4];
+    b[3] = p;  // index 8
+    for (int k = 2; k >= 0; --k) b[k] = gf_mulx(b[k + 1]);  // b[2] = idx 4, b[1] = 2, b[0] = 1
+    for (int v = 0; v < 16; ++v) {
+        U128 r{0, 0};
+        for (int k = 0; k < 4; ++k)
+            if (v & (1 << k)) r = gf_xor(r, b[k]);
+        t[v] = r;
+    }
+}
+
+// reduction of the four bits shifted out by a multiply by x^4 (bits 112..127 of hi)
+__device__ inline uint64_t gf_last4(uint32_t r) {
+    return (uint64_t)(((r & 1) ? 0x1C20u : 0u) ^ ((r & 2) ? 0x3840u : 0u) ^
+                      ((r & 4) ? 0x7080u : 0u) ^ ((r & 8) ? 0xE100u : 0u)) << 48;
+}
+
+// X . P with P's 4-bit table T (in LDS): Horner in x^4 from the last nibble of X
+__device__ inline U128 gf_mul_tab(U128 x, const U128* __restrict__ t) {
+    U128 z = t[x.lo & 0xF];
+#pragma unroll
+    for (int k = 30; k >= 0; --k) {
+        const uint32_t n = k >= 16 ? (uint32_t)(x.lo >> ((31 - k) * 4)) & 0xF
+                                   : (uint32_t)(x.hi >> ((15 - k) * 4)) & 0xF;
+        const uint32_t r = (uint32_t)z.lo & 0xF;
+        z.lo = (z.lo >> 4) | (z.hi << 60);
+        z.hi = (z.hi >> 4) ^ gf_last4(r);
+        const U128 e = t[n];
+        z.hi ^= e.hi;
+        z.lo ^= e.lo;
+    }
+    return z;
+}
+
+// ---- AES ----------------------------------------------------------------------------------
+
+__device__ inline uint32_t ror32(uint32_t x, int s) { return (x >> s) | (x << (32 - s)); }
+__device__ inline uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+// one AES encryption with the T-table accessor te(x) (Te0[x]); rk = big-endian round keys.
+// NR is a template argument so every round-key index is a constant (the keys stay in scalar
+// registers when rk is wave-uniform).
+template <int NR, typename TE>
+__device__ inline void aes_enc(const uint32_t* __restrict__ rk, uint32_t in[4], TE te) {
+    constexpr uint32_t nr = NR;
+    uint32_t s0 = in[0] ^ rk[0], s1 = in[1] ^ rk[1], s2 = in[2] ^ rk[2], s3 = in[3] ^ rk[3];
+#pragma unroll
+    for (uint32_t r = 1; r < nr; ++r) {
+        const uint32_t t0 = te(s0 >> 24) ^ ror32(te((s1 >> 16) & 0xFF), 8) ^
+                            ror32(te((s2 >> 8) & 0xFF), 16) ^ ror32(te(s3 & 0xFF), 24) ^ rk[4 * r];
+        const uint32_t t1 = te(s1 >> 24) ^ ror32(te((s2 >> 16) & 0xFF), 8) ^
+                            ror32(te((s3 >> 8) & 0xFF), 16) ^ ror32(te(s0 & 0xFF), 24) ^ rk[4 * r + 1];
+        const uint32_t t2 = te(s2 >> 24) ^ ror32(te((s3 >> 16) & 0xFF), 8) ^
+                            ror32(te((s0 >> 8) & 0xFF), 16) ^ ror32(te(s1 & 0xFF), 24) ^ rk[4 * r + 2];
+        const uint32_t t3 = te(s3 >> 24) ^ ror32(te((s0 >> 16) & 0xFF), 8) ^
+                            ror32(te((s1 >> 8) & 0xFF), 16) ^ ror32(te(s2 & 0xFF), 24) ^ rk[4 * r + 3];
+        s0 = t0, s1 = t1, s2 = t2, s3 = t3;
+    }
+    // last round: S-box byte = bits 16..23 of Te0
+    auto sb = [&](uint32_t x) { return (te(x) >> 16) & 0xFF; };
+    const uint32_t* k = rk + 4 * nr;
+    in[0] = ((sb(s0 >> 24) << 24) | (sb((s1 >> 16) & 0xFF) << 16) | (sb((s2 >> 8) & 0xFF) << 8) | sb(s3 & 0xFF)) ^ k[0];
+    in[1] = ((sb(s1 >> 24) << 24) | (sb((s2 >> 16) & 0xFF) << 16) | (sb((s3 >> 8) & 0xFF) << 8) | sb(s0 & 0xFF)) ^ k[1];
+    in[2] = ((sb(s2 >> 24) << 24) | (sb((s3 >> 16) & 0xFF) << 16) | (sb((s0 >> 8) & 0xFF) << 8) | sb(s1 & 0xFF)) ^ k[2];
+    in[3] = ((sb(s3 >> 24) << 24) | (sb((s0 >> 16) & 0xFF) << 16) | (sb((s1 >> 8) & 0xFF) << 8) | sb(s2 & 0xFF)) ^ k[3];
+}
+
+template <typename TE>
+__device__ inline void aes_encrypt(const uint32_t* __restrict__ rk, uint32_t nr, uint32_t in[4], TE te) {
+    if (nr == 10)
+        aes_enc<10>(rk, in, te);
+    else
+        aes_enc<14>(rk, in, te);
+}
+
+// S-box (FIPS-197 §5.1.1: inverse in GF(2^8), then the affine map) and Te0, one thread
+__global__ void k_tls_te0(uint32_t* te0) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    uint8_t sbox[256];
+    uint8_t p = 1, q = 1;
+    do {
+        p = (uint8_t)(p ^ (uint8_t)(p << 1) ^ ((p & 0x80) ? 0x1B : 0));
+        q ^= (uint8_t)(q << 1);
+        q ^= (uint8_t)(q << 2);
+        q ^= (uint8_t)(q << 4);
+        if (q & 0x80) q ^= 0x09;
+        const uint8_t x = (uint8_t)(q ^ (uint8_t)((q << 1) | (q >> 7)) ^ (uint8_t)((q << 2) | (q >> 6)) ^
+                                    (uint8_t)((q << 3) | (q >> 5)) ^ (uint8_t)((q << 4) | (q >> 4)));
+        sbox[p] = (uint8_t)(x ^ 0x63);
+    } while (p != 1);
+    sbox[0] = 0x63;
+    for (int x = 0; x < 256; ++x) {
+        const uint32_t s = sbox[x];
+        const uint32_t s2 = ((s << 1) ^ ((s & 0x80) ? 0x1B : 0)) & 0xFF;
+        te0[x] = (s2 << 24) | (s << 16) | (s << 8) | (s2 ^ s);
+    }
+}
+
+// key slot -> round keys, H = E(K, 0^128), tables of H^(2^k); one lane per slot
+__global__ __launch_bounds__(kBlock) void k_tls_keys(const uvhttp_tls_key_t* keys, uint32_t n,
+                                                     const uint32_t* te0, KeySched* ks) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uvhttp_tls_key_t k = keys[i];
+    KeySched* o = ks + i;
+    const bool ok = (k.key_len == 16 || k.key_len == 32) &&
+                    (k.version == UVHTTP_TLS_VERSION_12 || k.version == UVHTTP_TLS_VERSION_13);
+    if (!ok) {
+        o->nr = 0;
+        o->version = 0;
+        return;
+    }
+    auto sb = [&](uint32_t x) { return (te0[x] >> 16) & 0xFF; };
+    const uint32_t nk = k.key_len / 4, nr = nk + 6, total = 4 * (nr + 1);
+    uint32_t w[60];
+    for (uint32_t j = 0; j < nk; ++j)
+        w[j] = ((uint32_t)k.key[4 * j] << 24) | ((uint32_t)k.key[4 * j + 1] << 16) |
+               ((uint32_t)k.key[4 * j + 2] << 8) | k.key[4 * j + 3];
+    uint32_t rcon = 1;
+    for (uint32_t j = nk; j < total; ++j) {
+        uint32_t t = w[j - 1];
+        if (j % nk == 0) {
+            t = (sb((t >> 16) & 0xFF) << 24) | (sb((t >> 8) & 0xFF) << 16) | (sb(t & 0xFF) << 8) |
+                sb(t >> 24);
+            t ^= rcon << 24;
+            rcon = ((rcon << 1) ^ ((rcon & 0x80) ? 0x1B : 0)) & 0xFF;
+        } else if (nk > 6 && j % nk == 4) {
+            t = (sb(t >> 24) << 24) | (sb((t >> 16) & 0xFF) << 16) | (sb((t >> 8) & 0xFF) << 8) |
+                sb(t & 0xFF);
+        }
+        w[j] = w[j - nk] ^ t;
+    }
+    for (uint32_t j = 0; j < total; ++j) o->rk[j] = w[j];
+    o->nr = nr;
+    o->version = k.version;
+    for (int j = 0; j < 3; ++j)
+        o->iv[j] = ((uint32_t)k.iv[4 * j] << 24) | ((uint32_t)k.iv[4 * j + 1] << 16) |
+                   ((uint32_t)k.iv[4 * j + 2] << 8) | k.iv[4 * j + 3];
+    uint32_t z[4] = {0, 0, 0, 0};
+    aes_encrypt(w, nr, z, [&](uint32_t x) { return te0[x]; });
+    U128 p{((uint64_t)z[0] << 32) | z[1], ((uint64_t)z[2] << 32) | z[3]};
+    for (int l = 0; l < 7; ++l) {
+        U128 t[16];
+        gf_table(p, t);
+        for (int v = 0; v < 16; ++v) o->tab[l][v] = t[v];
+        p = gf_mul_slow(p, p);
+    }
+}
+
+// ---- record walk ------------------------------------------------------------------------
+
+__device__ inline uint32_t be16(const uint8_t* p) { return ((uint32_t)p[0] << 8) | p[1]; }
+
+// header checks in contract order; 0 or the record status
+__device__ inline int32_t header_status(uint32_t version, uint32_t type, uint32_t ver, uint32_t len) {
+    if (ver != 0x0303) return UVHTTP_TLS_REC_ERR_VERSION;
+    if (version == UVHTTP_TLS_VERSION_13 ? type != 23 : (type < 21 || type > 23))
+        return UVHTTP_TLS_REC_ERR_BAD_TYPE;
+    if (len > (version == UVHTTP_TLS_VERSION_13 ? kMaxLen13 : kMaxLen12))
+        return UVHTTP_TLS_REC_ERR_OVERFLOW;
+    if (len < (version == UVHTTP_TLS_VERSION_13 ? 16u : 24u)) return UVHTTP_TLS_REC_ERR_BAD_MAC;
+    return 0;
+}
+
+__device__ inline uint64_t record_cap(uint32_t version, uint32_t len) {
+    const uint32_t over = version == UVHTTP_TLS_VERSION_13 ? 17 : 24;
+    return len > over ? len - over : 0;
+}
+
+__device__ inline bool key_valid(const uvhttp_tls_key_t& k) {
+    return (k.key_len == 16 || k.key_len == 32) &&
+           (k.version == UVHTTP_TLS_VERSION_12 || k.version == UVHTTP_TLS_VERSION_13);
+}
+
+// walk one connection's records; WRITE fills RecWork from index `first` (spec offsets from base)
+template <bool WRITE>
+__device__ inline uint32_t walk(const TlsArgs& a, uint32_t s, uint64_t* cap_out, uint32_t first,
+                                uint64_t base) {
+    const uvhttp_tls_stream_t st = a.streams[s];
+    *cap_out = 0;
+    if (st.key >= a.n_keys) return 0;
+    const uvhttp_tls_key_t k = a.keys[st.key];
+    if (!key_valid(k)) return 0;
+    const uint64_t L = st.begin + st.len <= a.wire_len ? st.len : 0;
+    const uint8_t* p = a.wire + st.begin;
+    uint32_t n = 0;
+    uint64_t pos = 0, cap = 0;
+    while (L - pos >= 5) {
+        const uint32_t type = p[pos], ver = be16(p + pos + 1), len = be16(p + pos + 3);
+        const int32_t hs = header_status(k.version, type, ver, len);
+        if (!hs && L - pos - 5 < len) break;  // incomplete: waits for more bytes
+        if (WRITE) {
+            RecWork w;
+            w.rec_off = st.begin + pos;
+            w.spec_off = base + cap;
+            w.seq = st.seq + n;
+            w.len = len;
+            w.stream = s;
+            w.key = st.key;
+            w.status = hs;
+            w.content_len = 0;
+            w.type = 0;
+            a.work[first + n] = w;
+        }
+        ++n;
+        if (hs) break;
+        cap += record_cap(k.version, len);
+        pos += 5 + (uint64_t)len;
+    }
+    *cap_out = cap;
+    return n;
+}
+
+template <typename T>
+__device__ inline T block_exclusive_sum(T v, T* total) {
+    __shared__ T wsum[kBlock / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    T inc = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const T o = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += o;
+    }
+    if (lane == 63) wsum[wave] = inc;
+    __syncthreads();
+    T pre = 0, all = 0;
+    for (int k = 0; k < kBlock / 64; ++k) {
+        if (k < wave) pre += wsum[k];
+        all += wsum[k];
+    }
+    __syncthreads();
+    *total = all;
+    return pre + inc - v;
+}
+
+__global__ __launch_bounds__(kBlock) void k_tls_walk_count(TlsArgs a) {
+    const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
+    uint64_t cap = 0;
+    uint32_t n = 0;
+    if (s < a.n_streams) {
+        n = walk<false>(a, s, &cap, 0, 0);
+        a.sw[s] = StreamWork{n, 0u, cap};
+    }
+    uint64_t tn, tc;
+    (void)block_exclusive_sum<uint64_t>(n, &tn);
+    (void)block_exclusive_sum<uint64_t>(cap, &tc);
+    if (threadIdx.x == 0) {
+        a.blk[2 * blockIdx.x] = tn;
+        a.blk[2 * blockIdx.x + 1] = tc;
+    }
+}
+
+// exclusive prefix of the per-block (records, bytes) pairs; capacity decision
+__global__ __launch_bounds__(kBlock) void k_tls_walk_scan(TlsArgs a, uint32_t n_blocks) {
+    const uint32_t per = (n_blocks + kBlock - 1) / kBlock;
+    const uint32_t beg = threadIdx.x * per;
+    const uint32_t fin = beg + per < n_blocks ? beg + per : n_blocks;
+    uint64_t rn = 0, rc = 0;
+    for (uint32_t b = beg; b < fin; ++b) rn += a.blk[2 * b], rc += a.blk[2 * b + 1];
+    uint64_t tn, tc;
+    uint64_t pn = block_exclusive_sum<uint64_t>(rn, &tn);
+    uint64_t pc = block_exclusive_sum<uint64_t>(rc, &tc);
+    for (uint32_t b = beg; b < fin; ++b) {
+        const uint64_t vn = a.blk[2 * b], vc = a.blk[2 * b + 1];
+        a.blk[2 * b] = pn;
+        a.blk[2 * b + 1] = pc;
+        pn += vn;
+        pc += vc;
+    }
+    if (threadIdx.x == 0) {
+        const bool fail = tn > a.max_records || tc > a.out_cap;
+        a.n_total[0] = fail ? 0u : (uint32_t)tn;
+        a.n_total[1] = fail ? 1u : 0u;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_tls_walk_write(TlsArgs a) {
+    const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
+    const StreamWork sw = s < a.n_streams ? a.sw[s] : StreamWork{0, 0, 0};
+    uint64_t tn, tc;
+    const uint64_t first = a.blk[2 * blockIdx.x] + block_exclusive_sum<uint64_t>(sw.n_rec, &tn);
+    const uint64_t base = a.blk[2 * blockIdx.x + 1] + block_exclusive_sum<uint64_t>(sw.cap, &tc);
+    if (s >= a.n_streams || a.n_total[1]) return;
+    uint64_t cap;
+    (void)walk<true>(a, s, &cap, (uint32_t)first, base);
+    a.sw[s].key_bad = (uint32_t)first;  // reused: first record index for finalize
+    a.sw[s].cap = base;                 // reused: the connection's base in out
+}
+
+// ---- record crypto ---------------------------------------------------------------------------
+
+// 16 bytes at p + [lo, hi) of a 16-byte window (others zero); little-endian words
+__device__ inline void load_part(const uint8_t* p, int lo, int hi, uint32_t w[4]) {
+    if (lo == 0 && hi == 16) {
+        __builtin_memcpy(w, p, 16);
+        return;
+    }
+    w[0] = w[1] = w[2] = w[3] = 0;
+    for (int b = lo; b < hi; ++b) w[b >> 2] |= (uint32_t)p[b] << (8 * (b & 3));
+}
+
+__device__ inline void store_part(uint8_t* p, int n, const uint32_t w[4]) {
+    if (n == 16) {
+        __builtin_memcpy(p, w, 16);
+        return;
+    }
+    for (int b = 0; b < n; ++b) p[b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+}
+
+__device__ inline U128 le_to_block(const uint32_t w[4]) {
+    return U128{((uint64_t)bswap32(w[0]) << 32) | bswap32(w[1]),
+                ((uint64_t)bswap32(w[2]) << 32) | bswap32(w[3])};
+}
+
+__device__ inline U128 shfl_down128(U128 v, int d) {
+    const uint32_t a = __shfl_down((uint32_t)v.hi, d, 64), b = __shfl_down((uint32_t)(v.hi >> 32), d, 64);
+    const uint32_t c = __shfl_down((uint32_t)v.lo, d, 64), e = __shfl_down((uint32_t)(v.lo >> 32), d, 64);
+    return U128{((uint64_t)b << 32) | a, ((uint64_t)e << 32) | c};
+}
+
+struct SealArgs {
+    const uint8_t* src;
+    uint64_t src_len;
+    const uvhttp_tls_seal_t* recs;
+    uint32_t n;
+    uint8_t* out;
+    uint64_t out_cap;
+    const KeySched* sched;
+    uint32_t n_keys;
+    const uint32_t* te0;
+};
+
+// One record's GCM on one wave.  OPEN: ciphertext at ct[0, clen) -> plaintext content to
+// dst[0, wlen) (wlen = bytes to keep), returns tag match + (TLS 1.3) the last non-zero byte.
+// SEAL: plaintext from the (content, type) generator -> ciphertext at ct, tag after it.
+struct CryptOut {
+    bool tag_ok;
+    uint32_t last_nz;  // (index + 1) << 8 | byte of the last non-zero inner byte, 0 if none
+};
+
+template <bool SEAL>
+__device__ CryptOut gcm_record(const KeySched* __restrict__ ks, const uint32_t* te, uint32_t lane32,
+                               const U128 (*tabs)[16], const uint32_t nonce[3], U128 aad,
+                               uint32_t alen, const uint8_t* ct_in, uint8_t* ct_out, uint32_t clen,
+                               uint8_t* dst, uint32_t wlen, const uint8_t* src, uint32_t src_n,
+                               uint32_t inner_type, bool is13) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t nr = ks->nr;
+    const uint32_t nblk = (clen + 15) / 16;
+    const uint32_t m = nblk + 2;             // AAD, ciphertext blocks, length block
+    const uint32_t J = (m + 63) / 64;
+    const uint32_t pad = 64 * J - m;
+    auto te_lds = [&](uint32_t x) { return te[(x << 5) | lane32]; };
+    const uint32_t* __restrict__ rk = ks->rk;
+    U128 acc{0, 0};
+    uint32_t ej0[4] = {0, 0, 0, 0};
+    uint32_t last_nz = 0;
+    for (uint32_t j = 0; j < J; ++j) {
+        const int32_t q = (int32_t)(64 * j + lane) - (int32_t)pad;  // position in the sequence
+        U128 x{0, 0};
+        // counter block: J0 for the AAD lane (tag mask), J0 + 1 + k for ciphertext block k
+        uint32_t cb[4] = {nonce[0], nonce[1], nonce[2], q <= 0 ? 1u : (uint32_t)q + 1u};
+        aes_encrypt(rk, nr, cb, te_lds);
+        if (q == 0) {
+            x = aad;
+            ej0[0] = cb[0], ej0[1] = cb[1], ej0[2] = cb[2], ej0[3] = cb[3];
+        } else if (q > 0 && (uint32_t)q <= nblk) {
+            const uint32_t k = (uint32_t)q - 1;
+            const uint32_t off = 16 * k;
+            const int n = clen - off < 16 ? (int)(clen - off) : 16;
+            uint32_t d[4];
+            const uint32_t ks4[4] = {bswap32(cb[0]), bswap32(cb[1]), bswap32(cb[2]), bswap32(cb[3])};
+            if (!SEAL) {
+                load_part(ct_in + off, 0, n, d);
+                x = le_to_block(d);
+                uint32_t pt[4];
+                for (int b = 0; b < 4; ++b) pt[b] = d[b] ^ ks4[b];
+                if (n < 16) {  // keep zero beyond the record
+                    for (int b = 0; b < 4; ++b) {
+                        const int lo = 4 * b;
+                        const uint32_t msk = n >= lo + 4 ? 0xFFFFFFFFu : n <= lo ? 0u : ((1u << (8 * (n - lo))) - 1u);
+                        pt[b] &= msk;
+                    }
+                }
+                if (is13) {
+                    for (int b = 3; b >= 0; --b) {
+                        if (pt[b]) {
+                            const uint32_t byte_i = 4 * b + (31 - __builtin_clz(pt[b])) / 8;
+                            const uint32_t v = ((off + byte_i + 1) << 8) | ((pt[b] >> (8 * (byte_i & 3))) & 0xFF);
+                            if (v > last_nz) last_nz = v;
+                            break;
+                        }
+                    }
+                }
+                if (off < wlen) store_part(dst + off, wlen - off < 16 ? (int)(wlen - off) : 16, pt);
+            } else {
+                // inner plaintext byte b of the record = content b (< src_n), type (== src_n), 0
+                const int cn = src_n > off ? (src_n - off < 16 ? (int)(src_n - off) : 16) : 0;
+                load_part(src + off, 0, cn, d);
+                if (is13 && src_n >= off && src_n < off + 16) {
+                    const uint32_t bq = src_n - off;
+                    d[bq >> 2] |= inner_type << (8 * (bq & 3));
+                }
+                for (int b = 0; b < 4; ++b) d[b] ^= ks4[b];
+                if (n < 16) {
+                    for (int b = 0; b < 4; ++b) {
+                        const int lo = 4 * b;
+                        const uint32_t msk = n >= lo + 4 ? 0xFFFFFFFFu : n <= lo ? 0u : ((1u << (8 * (n - lo))) - 1u);
+                        d[b] &= msk;
+                    }
+                }
+                store_part(ct_out + off, n, d);
+                x = le_to_block(d);
+            }
+        } else if ((uint32_t)q == m - 1) {
+            x = U128{(uint64_t)alen * 8, (uint64_t)clen * 8};
+        }
+        acc = j == 0 ? x : gf_xor(gf_mul_tab(acc, tabs[6]), x);  // Horner, multiplier H^64
+    }
+    // combine lanes: level t joins groups of 2^t lanes with multiplier H^(2^t)
+#pragma unroll
+    for (int t = 0; t < 6; ++t) {
+        const U128 right = shfl_down128(acc, 1 << t);
+        acc = gf_xor(gf_mul_tab(acc, tabs[t]), right);
+    }
+    acc = gf_mul_tab(acc, tabs[0]);  // lane 0: GHASH
+    // E(K, J0) lives in the lane that held the AAD block: lane pad % 64 of iteration pad / 64
+    const uint32_t src_lane = pad & 63;
+    uint32_t e[4];
+    for (int b = 0; b < 4; ++b) e[b] = __shfl(ej0[b], src_lane, 64);
+    const U128 tag{acc.hi ^ (((uint64_t)e[0] << 32) | e[1]), acc.lo ^ (((uint64_t)e[2] << 32) | e[3])};
+    CryptOut r{false, 0};
+    if (SEAL) {
+        if (lane == 0) {
+            const uint32_t w[4] = {bswap32((uint32_t)(tag.hi >> 32)), bswap32((uint32_t)tag.hi),
+                                   bswap32((uint32_t)(tag.lo >> 32)), bswap32((uint32_t)tag.lo)};
+            store_part(ct_out + clen, 16, w);
+        }
+        return r;
+    }
+    uint32_t t4[4];
+    load_part(ct_in + clen, 0, 16, t4);
+    const U128 want = le_to_block(t4);
+    r.tag_ok = want.hi == tag.hi && want.lo == tag.lo;  // lane 0's tag is the valid one
+    // wave max of last_nz
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint32_t o = __shfl_xor(last_nz, d, 64);
+        if (o > last_nz) last_nz = o;
+    }
+    r.last_nz = last_nz;
+    return r;
+}
+
+__device__ inline void load_tables(const KeySched* ks, U128 (*tabs)[16]) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint4* s = reinterpret_cast<const uint4*>(ks->tab);
+    uint4* d = reinterpret_cast<uint4*>(tabs);
+    for (uint32_t i = lane; i < 7 * 16; i += 64) d[i] = s[i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ inline void fill_te(const uint32_t* te0, uint32_t* te) {
+    for (uint32_t i = threadIdx.x; i < 256 * 32; i += blockDim.x) te[i] = te0[i >> 5];
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(kCryptWG) void k_tls_open(TlsArgs a) {
+    __shared__ uint32_t te[256 * 32];
+    __shared__ U128 tabs[kCryptWaves][7][16];
+    fill_te(a.te0, te);
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t n = a.n_total[0];
+    uint32_t cur = 0xFFFFFFFFu;
+    // r is wave-uniform: readfirstlane makes the record and key-schedule loads scalar
+    for (uint32_t r = __builtin_amdgcn_readfirstlane(blockIdx.x * kCryptWaves + wave); r < n;
+         r += gridDim.x * kCryptWaves) {
+        RecWork w = a.work[r];
+        if (w.status != 0) continue;  // header failure: nothing to open
+        const KeySched* ks = a.sched + w.key;
+        if (w.key != cur) {
+            load_tables(ks, tabs[wave]);
+            cur = w.key;
+        }
+        const bool is13 = ks->version == UVHTTP_TLS_VERSION_13;
+        const uint8_t* rec = a.wire + w.rec_off;
+        uint32_t nonce[3];
+        U128 aad;
+        uint32_t alen, clen;
+        const uint8_t* ct;
+        if (is13) {
+            nonce[0] = ks->iv[0];
+            nonce[1] = ks->iv[1] ^ (uint32_t)(w.seq >> 32);
+            nonce[2] = ks->iv[2] ^ (uint32_t)w.seq;
+            uint32_t h[4];
+            load_part(rec, 0, 5, h);
+            aad = le_to_block(h);
+            alen = 5;
+            clen = w.len - 16;
+            ct = rec + 5;
+        } else {
+            uint32_t ex[4];
+            load_part(rec + 5, 0, 8, ex);
+            nonce[0] = ks->iv[0];
+            nonce[1] = bswap32(ex[0]);
+            nonce[2] = bswap32(ex[1]);
+            clen = w.len - 24;
+            aad = U128{w.seq, ((uint64_t)rec[0] << 56) | (0x0303ull << 40) | ((uint64_t)clen << 24)};
+            alen = 13;
+            ct = rec + 13;
+        }
+        const uint32_t wlen = is13 ? (clen > 0 ? clen - 1 : 0) : clen;
+        const CryptOut co = gcm_record<false>(ks, te, lane & 31, tabs[wave], nonce, aad, alen, ct,
+                                              nullptr, clen, a.out + w.spec_off, wlen, nullptr, 0,
+                                              0, is13);
+        if (lane == 0) {
+            int32_t st;
+            uint32_t type = 0, cl = 0;
+            if (!co.tag_ok) {
+                st = UVHTTP_TLS_REC_ERR_BAD_MAC;
+            } else if (is13) {
+                if (co.last_nz == 0) {
+                    st = UVHTTP_TLS_REC_ERR_EMPTY;
+                } else {
+                    type = co.last_nz & 0xFF;
+                    cl = (co.last_nz >> 8) - 1;
+                    st = type == 23 ? UVHTTP_TLS_REC_OK : UVHTTP_TLS_REC_CONTROL;
+                }
+            } else {
+                type = rec[0];
+                cl = clen;
+                st = type == 23 ? UVHTTP_TLS_REC_OK : UVHTTP_TLS_REC_CONTROL;
+            }
+            a.work[r].status = st;
+            a.work[r].type = type;
+            a.work[r].content_len = cl;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kCryptWG) void k_tls_seal(SealArgs a) {
+    __shared__ uint32_t te[256 * 32];
+    __shared__ U128 tabs[kCryptWaves][7][16];
+    fill_te(a.te0, te);
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t cur = 0xFFFFFFFFu;
+    for (uint32_t r = __builtin_amdgcn_readfirstlane(blockIdx.x * kCryptWaves + wave); r < a.n;
+         r += gridDim.x * kCryptWaves) {
+        const uvhttp_tls_seal_t sr = a.recs[r];
+        if (sr.key >= a.n_keys) continue;
+        const KeySched* ks = a.sched + sr.key;
+        if (ks->nr == 0 || sr.plain_len > 16384) continue;
+        const bool is13 = ks->version == UVHTTP_TLS_VERSION_13;
+        const uint32_t clen = sr.plain_len + (is13 ? 1u : 0u);
+        const uint32_t rlen = clen + 16 + (is13 ? 0u : 8u);
+        if (sr.out_off + 5 + rlen > a.out_cap || sr.src_off + sr.plain_len > a.src_len) continue;
+        if (sr.key != cur) {
+            load_tables(ks, tabs[wave]);
+            cur = sr.key;
+        }
+        uint8_t* rec = a.out + sr.out_off;
+        const uint32_t otype = is13 ? 23u : sr.type;
+        uint32_t nonce[3];
+        U128 aad;
+        uint32_t alen;
+        uint8_t* ct;
+        if (is13) {
+            nonce[0] = ks->iv[0];
+            nonce[1] = ks->iv[1] ^ (uint32_t)(sr.seq >> 32);
+            nonce[2] = ks->iv[2] ^ (uint32_t)sr.seq;
+            aad = U128{((uint64_t)otype << 56) | (0x0303ull << 40) | ((uint64_t)rlen << 24), 0};
+            alen = 5;
+            ct = rec + 5;
+        } else {
+            nonce[0] = ks->iv[0];
+            nonce[1] = (uint32_t)(sr.seq >> 32);
+            nonce[2] = (uint32_t)sr.seq;
+            aad = U128{sr.seq, ((uint64_t)otype << 56) | (0x0303ull << 40) | ((uint64_t)clen << 24)};
+            alen = 13;
+            ct = rec + 13;
+        }
+        if (lane < 5) {
+            const uint32_t hb[5] = {otype, 3, 3, rlen >> 8, rlen & 0xFF};
+            rec[lane] = (uint8_t)hb[lane];
+        } else if (!is13 && lane < 13) {
+            rec[lane] = (uint8_t)(sr.seq >> (8 * (12 - lane)));
+        }
+        (void)gcm_record<true>(ks, te, lane & 31, tabs[wave], nonce, aad, alen, nullptr, ct, clen,
+                               nullptr, 0, a.src + sr.src_off, sr.plain_len, sr.type, is13);
+    }
+}
+
+// ---- finalize / fix-up ---------------------------------------------------------------------
+
+__global__ __launch_bounds__(kBlock) void k_tls_finalize(TlsArgs a) {
+    const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
+    if (s >= a.n_streams) return;
+    const uvhttp_tls_stream_t st = a.streams[s];
+    uvhttp_tls_result_t r;
+    memset(&r, 0, sizeof(r));
+    r.next_seq = st.seq;
+    a.fix[s] = 0;
+    if (a.n_total[1]) {  // capacity: nothing delivered anywhere
+        r.status = -1;
+        r.first_status = UVHTTP_TLS_REC_ERR_CAPACITY;
+        a.results[s] = r;
+        return;
+    }
+    const StreamWork sw = a.sw[s];
+    r.first_record = sw.key_bad;
+    r.n_records = sw.n_rec;
+    r.out_off = sw.cap;
+    const bool kbad = st.key >= a.n_keys || !key_valid(a.keys[st.key]);
+    if (kbad) {
+        r.status = -1;
+        r.first_status = UVHTTP_TLS_REC_ERR_KEY;
+        a.results[s] = r;
+        return;
+    }
+    uint64_t plain = 0;
+    bool stopped = false, moved = false;
+    for (uint32_t j = 0; j < sw.n_rec; ++j) {
+        const RecWork w = a.work[r.first_record + j];
+        uvhttp_tls_record_t o;
+        o.rec_off = w.rec_off;
+        o.out_off = 0;
+        o.content_len = 0;
+        o.stream = s;
+        o.type = 0;
+        o.reserved = 0;
+        o.reserved2 = 0;
+        if (stopped) {
+            o.status = UVHTTP_TLS_REC_SKIPPED;
+        } else {
+            o.status = (int8_t)w.status;
+            o.type = (uint8_t)w.type;
+            o.content_len = w.content_len;
+            if (w.status == UVHTTP_TLS_REC_OK) {
+                o.out_off = r.out_off + plain;
+                if (o.out_off != w.spec_off) moved = true;
+                plain += w.content_len;
+                r.n_delivered++;
+                r.consumed_bytes = w.rec_off - st.begin + 5 + w.len;
+            } else {
+                stopped = true;
+                r.first_status = w.status;
+                r.status = w.status < 0 ? -1 : 0;
+            }
+        }
+        a.records[r.first_record + j] = o;
+    }
+    r.next_seq = st.seq + r.n_delivered;
+    r.plain_len = plain;
+    a.results[s] = r;
+    a.fix[s] = moved ? 1u : 0u;
+}
+
+// Move the delivered contents of a connection with padded TLS 1.3 records to their final
+// (lower) offsets: records in order, each copied in WG-sized chunks read fully before written.
+__global__ __launch_bounds__(kBlock) void k_tls_fixup(TlsArgs a) {
+    const uint32_t s = blockIdx.x;
+    if (s >= a.n_streams || !a.fix[s]) return;
+    const uvhttp_tls_result_t r = a.results[s];
+    for (uint32_t j = 0; j < r.n_delivered; ++j) {
+        const RecWork w = a.work[r.first_record + j];
+        const uint64_t dst = a.records[r.first_record + j].out_off, src = w.spec_off;
+        if (dst == src) continue;
+        for (uint64_t c = 0; c < w.content_len; c += kBlock * 16) {
+            const uint64_t o = c + threadIdx.x * 16;
+            uint32_t v[4] = {0, 0, 0, 0};
+            const int n = o < w.content_len ? (w.content_len - o < 16 ? (int)(w.content_len - o) : 16) : 0;
+            if (n) load_part(a.out + src + o, 0, n, v);
+            __syncthreads();
+            if (n) store_part(a.out + dst + o, n, v);
+            __syncthreads();
+        }
+    }
+}
+
+}  // namespace
+
+// ---- engine ---------------------------------------------------------------------------------
+
+struct uvhttp_tls_gpu_engine {
+    int device;
+    uint32_t* te0;
+    void* ws;
+    size_t ws_bytes;
+    uint32_t cap_keys, cap_streams, cap_records;
+    KeySched* sched;
+    RecWork* work;
+    StreamWork* sw;
+    uint64_t* blk;
+    uint32_t* n_total;
+    uint32_t* fix;
+    int timing;
+    hipEvent_t ev[2 * 256];
+    int ev_created, ev_used;
+    double time_ms;
+    uint64_t launches;
+    int crypt_grid;
+    char err[256];
+};
+
+static int tls_err(uvhttp_tls_gpu_engine_t* e, int code, const char* what, hipError_t h) {
+    if (e) snprintf(e->err, sizeof(e->err), "%s: %s", what, h == hipSuccess ? "" : hipGetErrorString(h));
+    return code;
+}
+
+static size_t al(size_t x) { return (x + 255) / 256 * 256; }
+
+static int tls_reserve(uvhttp_tls_gpu_engine_t* e, uint32_t keys, uint32_t streams, uint32_t records) {
+    if (e->ws && keys <= e->cap_keys && streams <= e->cap_streams && records <= e->cap_records)
+        return UVHTTP_TLS_GPU_OK;
+    keys = keys > e->cap_keys ? keys : e->cap_keys;
+    streams = streams > e->cap_streams ? streams : e->cap_streams;
+    records = records > e->cap_records ? records : e->cap_records;
+    const size_t nblk = (streams + kBlock - 1) / kBlock + 1;
+    const size_t o_sched = 0;
+    const size_t o_work = al(o_sched + (size_t)(keys ? keys : 1) * sizeof(KeySched));
+    const size_t o_sw = al(o_work + (size_t)(records ? records : 1) * sizeof(RecWork));
+    const size_t o_blk = al(o_sw + (size_t)(streams ? streams : 1) * sizeof(StreamWork));
+    const size_t o_tot = al(o_blk + 2 * nblk * sizeof(uint64_t));
+    const size_t o_fix = al(o_tot + 16);
+    const size_t bytes = al(o_fix + (size_t)(streams ? streams : 1) * sizeof(uint32_t));
+    if (e->ws) (void)hipFree(e->ws);
+    e->ws = nullptr;
+    const hipError_t h = hipMalloc(&e->ws, bytes);
+    if (h != hipSuccess) {
+        e->cap_keys = e->cap_streams = e->cap_records = 0;
+        return tls_err(e, UVHTTP_TLS_GPU_ENOMEM, "hipMalloc tls workspace", h);
+    }
+    char* b = (char*)e->ws;
+    e->sched = (KeySched*)(b + o_sched);
+    e->work = (RecWork*)(b + o_work);
+    e->sw = (StreamWork*)(b + o_sw);
+    e->blk = (uint64_t*)(b + o_blk);
+    e->n_total = (uint32_t*)(b + o_tot);
+    e->fix = (uint32_t*)(b + o_fix);
+    e->ws_bytes = bytes;
+    e->cap_keys = keys;
+    e->cap_streams = streams;
+    e->cap_records = records;
+    return UVHTTP_TLS_GPU_OK;
+}
+
+static void tls_harvest(uvhttp_tls_gpu_engine_t* e) {
+    for (int k = 0; k < e->ev_used; ++k) {
+        float ms = 0;
+        if (hipEventSynchronize(e->ev[2 * k + 1]) == hipSuccess &&
+            hipEventElapsedTime(&ms, e->ev[2 * k], e->ev[2 * k + 1]) == hipSuccess) {
+            e->time_ms += ms;
+            e->launches++;
+        }
+    }
+    e->ev_used = 0;
+}
+
+static int tls_timing_begin(uvhttp_tls_gpu_engine_t* e, hipStream_t s) {
+    if (!e->timing) return -1;
+    if (e->ev_used * 2 + 2 > (int)(sizeof(e->ev) / sizeof(e->ev[0]))) tls_harvest(e);
+    const int k = e->ev_used;
+    while (e->ev_created < 2 * k + 2) {
+        if (hipEventCreate(&e->ev[e->ev_created]) != hipSuccess) return -1;
+        e->ev_created++;
+    }
+    (void)hipEventRecord(e->ev[2 * k], s);
+    return k;
+}
+
+static void tls_timing_end(uvhttp_tls_gpu_engine_t* e, int k, hipStream_t s) {
+    if (k < 0) return;
+    (void)hipEventRecord(e->ev[2 * k + 1], s);
+    e->ev_used = k + 1;
+}
+
+extern "C" {
+
+int uvhttp_tls_gpu_engine_create(int device, uvhttp_tls_gpu_engine_t** out) {
+    if (!out) return UVHTTP_TLS_GPU_EINVAL;
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0 || device < 0 || device >= count)
+        return UVHTTP_TLS_GPU_ENODEV;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return UVHTTP_TLS_GPU_ENODEV;
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return UVHTTP_TLS_GPU_ENODEV;
+    uvhttp_tls_gpu_engine_t* e = (uvhttp_tls_gpu_engine_t*)calloc(1, sizeof(*e));
+    if (!e) return UVHTTP_TLS_GPU_ENOMEM;
+    e->device = device;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(device);
+    hipError_t h = hipMalloc(&e->te0, 256 * sizeof(uint32_t));
+    if (h == hipSuccess) {
+        hipLaunchKernelGGL(k_tls_te0, dim3(1), dim3(64), 0, 0, e->te0);
+        h = hipDeviceSynchronize();
+    }
+    // crypto grid: enough 4-wave workgroups for every CU several times over
+    e->crypt_grid = prop.multiProcessorCount * 8;
+    if (const char* g = getenv("UVHTTP_TLS_CRYPT_GRID")) e->crypt_grid = atoi(g) > 0 ? atoi(g) : e->crypt_grid;
+    (void)hipSetDevice(prev);
+    if (h != hipSuccess) {
+        if (e->te0) (void)hipFree(e->te0);
+        free(e);
+        return UVHTTP_TLS_GPU_ENODEV;
+    }
+    *out = e;
+    return UVHTTP_TLS_GPU_OK;
+}
+
+void uvhttp_tls_gpu_engine_free(uvhttp_tls_gpu_engine_t* e) {
+    if (!e) return;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(e->device);
+    if (e->ws) (void)hipFree(e->ws);
+    if (e->te0) (void)hipFree(e->te0);
+    for (int k = 0; k < e->ev_created; ++k) (void)hipEventDestroy(e->ev[k]);
+    (void)hipSetDevice(prev);
+    free(e);
+}
+
+const char* uvhttp_tls_gpu_engine_last_error(const uvhttp_tls_gpu_engine_t* e) {
+    return e ? e->err : "no engine";
+}
+
+int uvhttp_tls_gpu_engine_set_timing(uvhttp_tls_gpu_engine_t* e, int enable) {
+    if (!e) return UVHTTP_TLS_GPU_EINVAL;
+    e->timing = enable ? 1 : 0;
+    return UVHTTP_TLS_GPU_OK;
+}
+
+int uvhttp_tls_gpu_engine_kernel_time(uvhttp_tls_gpu_engine_t* e, double* ms, uint64_t* launches) {
+    if (!e || !ms || !launches) return UVHTTP_TLS_GPU_EINVAL;
+    tls_harvest(e);
+    *ms = e->time_ms;
+    *launches = e->launches;
+    e->time_ms = 0;
+    e->launches = 0;
+    return UVHTTP_TLS_GPU_OK;
+}
+
+int uvhttp_tls_gpu_open_records(uvhttp_tls_gpu_engine_t* e, const uint8_t* wire, uint64_t wire_len,
+                                const uvhttp_tls_key_t* keys, uint32_t n_keys,
+                                const uvhttp_tls_stream_t* streams, uint32_t n_streams,
+                                uvhttp_tls_record_t* records, uint32_t max_records,
+                                uvhttp_tls_result_t* results, uint8_t* out, uint64_t out_cap,
+                                void* stream) {
+    if (!e || (!wire && wire_len) || (!keys && n_keys) || (!streams && n_streams) ||
+        (!records && max_records) || (!results && n_streams) || (!out && out_cap))
+        return UVHTTP_TLS_GPU_EINVAL;
+    if (n_streams > (1u << 26) || max_records > (1u << 28))
+        return tls_err(e, UVHTTP_TLS_GPU_EINVAL, "too many streams / records", hipSuccess);
+    if (!n_streams) return UVHTTP_TLS_GPU_OK;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    if (prev != e->device) (void)hipSetDevice(e->device);
+    int rc = tls_reserve(e, n_keys, n_streams, max_records);
+    if (rc) {
+        if (prev != e->device) (void)hipSetDevice(prev);
+        return rc;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    TlsArgs a;
+    a.wire = wire;
+    a.wire_len = wire_len;
+    a.keys = keys;
+    a.n_keys = n_keys;
+    a.streams = streams;
+    a.n_streams = n_streams;
+    a.records = records;
+    a.max_records = max_records;
+    a.results = results;
+    a.out = out;
+    a.out_cap = out_cap;
+    a.sched = e->sched;
+    a.work = e->work;
+    a.sw = e->sw;
+    a.blk = e->blk;
+    a.n_total = e->n_total;
+    a.fix = e->fix;
+    a.te0 = e->te0;
+    const uint32_t nb = (n_streams + kBlock - 1) / kBlock;
+    if (n_keys)
+        hipLaunchKernelGGL(k_tls_keys, dim3((n_keys + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
+                           keys, n_keys, (const uint32_t*)e->te0, e->sched);
+    hipLaunchKernelGGL(k_tls_walk_count, dim3(nb), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(k_tls_walk_scan, dim3(1), dim3(kBlock), 0, s, a, nb);
+    hipLaunchKernelGGL(k_tls_walk_write, dim3(nb), dim3(kBlock), 0, s, a);
+    const uint32_t need = (max_records + kCryptWaves - 1) / kCryptWaves;
+    const uint32_t grid = need < (uint32_t)e->crypt_grid ? (need ? need : 1) : (uint32_t)e->crypt_grid;
+    const int tk = tls_timing_begin(e, s);
+    hipLaunchKernelGGL(k_tls_open, dim3(grid), dim3(kCryptWG), 0, s, a);
+    tls_timing_end(e, tk, s);
+    hipLaunchKernelGGL(k_tls_finalize, dim3(nb), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(k_tls_fixup, dim3(n_streams), dim3(kBlock), 0, s, a);
+    const hipError_t h = hipGetLastError();
+    if (prev != e->device) (void)hipSetDevice(prev);
+    if (h != hipSuccess) return tls_err(e, UVHTTP_TLS_GPU_ELAUNCH, "launch", h);
+    return UVHTTP_TLS_GPU_OK;
+}
+
+int uvhttp_tls_gpu_seal_records(uvhttp_tls_gpu_engine_t* e, const uint8_t* src, uint64_t src_len,
+                                const uvhttp_tls_seal_t* recs, uint32_t n_records,
+                                const uvhttp_tls_key_t* keys, uint32_t n_keys, uint8_t* out,
+                                uint64_t out_cap, void* stream) {
+    if (!e || (!src && src_len) || (!recs && n_records) || (!keys && n_keys) || (!out && out_cap))
+        return UVHTTP_TLS_GPU_EINVAL;
+    if (!n_records) return UVHTTP_TLS_GPU_OK;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    if (prev != e->device) (void)hipSetDevice(e->device);
+    int rc = tls_reserve(e, n_keys, 1, 1);
+    if (rc) {
+        if (prev != e->device) (void)hipSetDevice(prev);
+        return rc;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    if (n_keys)
+        hipLaunchKernelGGL(k_tls_keys, dim3((n_keys + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
+                           keys, n_keys, (const uint32_t*)e->te0, e->sched);
+    SealArgs a{src, src_len, recs, n_records, out, out_cap, e->sched, n_keys, e->te0};
+    const uint32_t need = (n_records + kCryptWaves - 1) / kCryptWaves;
+    const uint32_t grid = need < (uint32_t)e->crypt_grid ? need : (uint32_t)e->crypt_grid;
+    const int tk = tls_timing_begin(e, s);
+    hipLaunchKernelGGL(k_tls_seal, dim3(grid), dim3(kCryptWG), 0, s, a);
+    tls_timing_end(e, tk, s);
+    const hipError_t h = hipGetLastError();
+    if (prev != e->device) (void)hipSetDevice(prev);
+    if (h != hipSuccess) return tls_err(e, UVHTTP_TLS_GPU_ELAUNCH, "launch", h);
+    return UVHTTP_TLS_GPU_OK;
+}
+
+}  // extern "C"
