@@ -14,15 +14,17 @@
 //     with zero blocks to a multiple of 64) goes to lane i % 64, so every load and store of the
 //     wave is one contiguous 1 KiB run of ciphertext;
 //   * AES-CTR with the T-table round (four lookups + XORs per column) from ONE 1 KiB table
-//     replicated 32 times in LDS (copy = lane % 32, word = x * 32 + copy): ds_read_b32 banks
-//     are (addr / 4) % 32 per 32-lane half, so every lookup of a wave is conflict-free; the
+//     replicated in LDS (copy = lane % copies, word = x * copies + copy): ds_read_b32 banks
+//     are (addr / 4) % 32 per 32-lane half, so 32 copies are conflict-free and 16 copies cost
+//     at most 2-way; 16 copies leave room for 3 workgroups per CU and measured faster; the
 //     other three tables are byte rotations;
 //   * GHASH: each lane runs Horner with multiplier H^64 over its strided blocks, then a
 //     6-level shuffle tree (multipliers H, H^2 ... H^32) and a final x H combine the lanes.
-//     Every multiply is Shoup's 4-bit table method: a 256-byte table of P * (4-bit
-//     polynomials) per multiplier P — 16 entries of 16 B fill one LDS bank row, so the
-//     ds_read_b128 lookups of a 16-lane group never conflict.  The 7 tables (H^(2^k),
-//     k = 0..6) are built once per key by k_tls_keys.
+//     Multiplies use Shoup's table method: 4-bit tables (256 B per multiplier P: 16 entries of
+//     16 B fill one LDS bank row, so a 16-lane group's ds_read_b128 never conflicts) for
+//     H^(2^k), k = 0..6, built once per key by k_tls_keys; the Horner multiplier H^64 also
+//     gets an 8-bit table (4 KiB, built per wave from its 4-bit table when the key changes),
+//     which halves the steps of the dominant multiply.
 //   * the lane holding the AAD block computes E(K, J0) for the tag instead of a keystream
 //     block; TLS 1.3's content type is the last non-zero inner byte, found by a wave max.
 #include <hip/hip_runtime.h>
@@ -39,6 +41,25 @@ namespace {
 constexpr int kBlock = 256;            // walk / finalize kernels: one lane per connection
 constexpr int kCryptWG = 256;          // crypto kernel: 4 waves, one record per wave
 constexpr int kCryptWaves = kCryptWG / 64;
+// tuning switches (tools/build_variant.sh -D...; defaults = the shipped configuration)
+// (A/B on MI355X, tools/tls_ab.sh, 65 536 x 4 x 16 KiB TLS 1.3 AES-128-GCM; kernel GB/s of
+// plaintext: 4-bit Horner + 32 copies 310, 8-bit Horner + 32 copies 355, 8-bit + 16 copies 394,
+// 8-bit + 8 copies 379; forcing 4 waves/SIMD spills and loses)
+#ifndef TLS_TE_COPIES
+#define TLS_TE_COPIES 16   // copies of Te0 in LDS (32: conflict-free; 16: 3 workgroups per CU)
+#endif
+#ifndef TLS_GHASH8
+#define TLS_GHASH8 1       // 1: Horner multiplier H^64 through an 8-bit table (4 KiB per wave)
+#endif
+#ifndef TLS_WPE
+#define TLS_WPE 0          // >0: amdgpu_waves_per_eu hint for the crypto kernels
+#endif
+#if TLS_WPE > 0
+#define CRYPT_ATTR __launch_bounds__(kCryptWG) __attribute__((amdgpu_waves_per_eu(TLS_WPE)))
+#else
+#define CRYPT_ATTR __launch_bounds__(kCryptWG)
+#endif
+constexpr uint32_t kTeShift = TLS_TE_COPIES == 32 ? 5 : TLS_TE_COPIES == 16 ? 4 : 3;
 constexpr uint32_t kMaxLen13 = 16384 + 1 + 16;  // TLSCiphertext.length limits
 constexpr uint32_t kMaxLen12 = 16384 + 8 + 16;
 
@@ -134,10 +155,15 @@ __device__ void gf_table(U128 p, U128* t) {
     }
 }
 
-// reduction of the four bits shifted out by a multiply by x^4 (bits 112..127 of hi)
+// reduction of the four bits shifted out by a multiply by x^4 (bits 112..127 of hi): bit p of
+// r (p = 0 is b_127) becomes x^(128 + 3 - p) -> R >> (3 - p), i.e. carry-less r * 0x1C20
 __device__ inline uint64_t gf_last4(uint32_t r) {
-    return (uint64_t)(((r & 1) ? 0x1C20u : 0u) ^ ((r & 2) ? 0x3840u : 0u) ^
-                      ((r & 4) ? 0x7080u : 0u) ^ ((r & 8) ? 0xE100u : 0u)) << 48;
+    return (uint64_t)((r << 5) ^ (r << 10) ^ (r << 11) ^ (r << 12)) << 48;
+}
+
+// the same for the eight bits shifted out by x^8: carry-less r * 0x1C2 (0x1C2 = 0xE100 >> 7)
+__device__ inline uint64_t gf_last8(uint32_t r) {
+    return (uint64_t)((r << 1) ^ (r << 6) ^ (r << 7) ^ (r << 8)) << 48;
 }
 
 // X . P with P's 4-bit table T (in LDS): Horner in x^4 from the last nibble of X
@@ -155,6 +181,39 @@ __device__ inline U128 gf_mul_tab(U128 x, const U128* __restrict__ t) {
         z.lo ^= e.lo;
     }
     return z;
+}
+
+// X . P with P's 8-bit table T8 (256 entries of P * (byte polynomials)): Horner in x^8
+[[maybe_unused]] __device__ inline U128 gf_mul_tab8(U128 x, const U128* __restrict__ t) {
+    U128 z = t[x.lo & 0xFF];
+#pragma unroll
+    for (int k = 14; k >= 0; --k) {
+        const uint32_t n = k >= 8 ? (uint32_t)(x.lo >> ((15 - k) * 8)) & 0xFF
+                                  : (uint32_t)(x.hi >> ((7 - k) * 8)) & 0xFF;
+        const uint32_t r = (uint32_t)z.lo & 0xFF;
+        z.lo = (z.lo >> 8) | (z.hi << 56);
+        z.hi = (z.hi >> 8) ^ gf_last8(r);
+        const U128 e = t[n];
+        z.hi ^= e.hi;
+        z.lo ^= e.lo;
+    }
+    return z;
+}
+
+// 8-bit table from the 4-bit one: byte v = (high nibble: x^0..x^3)(low nibble: x^4..x^7), so
+// T8[v] = T4[v >> 4] ^ T4[v & 15] . x^4; one wave fills the 256 entries
+[[maybe_unused]] __device__ inline void gf_table8(const U128* t4, U128* t8) {
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t v = lane; v < 256; v += 64) {
+        U128 lo = t4[v & 15];
+        const uint32_t r = (uint32_t)lo.lo & 0xF;
+        lo.lo = (lo.lo >> 4) | (lo.hi << 60);
+        lo.hi = (lo.hi >> 4) ^ gf_last4(r);
+        t8[v] = gf_xor(t4[v >> 4], lo);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // ---- AES ----------------------------------------------------------------------------------
@@ -465,7 +524,7 @@ struct CryptOut {
 
 template <bool SEAL>
 __device__ CryptOut gcm_record(const KeySched* __restrict__ ks, const uint32_t* te, uint32_t lane32,
-                               const U128 (*tabs)[16], const uint32_t nonce[3], U128 aad,
+                               const U128 (*tabs)[16], const U128* t8, const uint32_t nonce[3], U128 aad,
                                uint32_t alen, const uint8_t* ct_in, uint8_t* ct_out, uint32_t clen,
                                uint8_t* dst, uint32_t wlen, const uint8_t* src, uint32_t src_n,
                                uint32_t inner_type, bool is13) {
@@ -475,7 +534,7 @@ __device__ CryptOut gcm_record(const KeySched* __restrict__ ks, const uint32_t* 
     const uint32_t m = nblk + 2;             // AAD, ciphertext blocks, length block
     const uint32_t J = (m + 63) / 64;
     const uint32_t pad = 64 * J - m;
-    auto te_lds = [&](uint32_t x) { return te[(x << 5) | lane32]; };
+    auto te_lds = [&](uint32_t x) { return te[(x << kTeShift) | lane32]; };
     const uint32_t* __restrict__ rk = ks->rk;
     U128 acc{0, 0};
     uint32_t ej0[4] = {0, 0, 0, 0};
@@ -540,7 +599,11 @@ __device__ CryptOut gcm_record(const KeySched* __restrict__ ks, const uint32_t* 
         } else if ((uint32_t)q == m - 1) {
             x = U128{(uint64_t)alen * 8, (uint64_t)clen * 8};
         }
+#if TLS_GHASH8
+        acc = j == 0 ? x : gf_xor(gf_mul_tab8(acc, t8), x);  // Horner, multiplier H^64
+#else
         acc = j == 0 ? x : gf_xor(gf_mul_tab(acc, tabs[6]), x);  // Horner, multiplier H^64
+#endif
     }
     // combine lanes: level t joins groups of 2^t lanes with multiplier H^(2^t)
 #pragma unroll
@@ -588,13 +651,19 @@ __device__ inline void load_tables(const KeySched* ks, U128 (*tabs)[16]) {
 }
 
 __device__ inline void fill_te(const uint32_t* te0, uint32_t* te) {
-    for (uint32_t i = threadIdx.x; i < 256 * 32; i += blockDim.x) te[i] = te0[i >> 5];
+    for (uint32_t i = threadIdx.x; i < 256 * TLS_TE_COPIES; i += blockDim.x) te[i] = te0[i >> kTeShift];
     __syncthreads();
 }
 
-__global__ __launch_bounds__(kCryptWG) void k_tls_open(TlsArgs a) {
-    __shared__ uint32_t te[256 * 32];
+__global__ CRYPT_ATTR void k_tls_open(TlsArgs a) {
+    __shared__ uint32_t te[256 * TLS_TE_COPIES];
     __shared__ U128 tabs[kCryptWaves][7][16];
+#if TLS_GHASH8
+    __shared__ U128 t8s[kCryptWaves][256];
+    U128* t8 = t8s[threadIdx.x >> 6];
+#else
+    U128* t8 = nullptr;
+#endif
     fill_te(a.te0, te);
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t n = a.n_total[0];
@@ -607,6 +676,7 @@ __global__ __launch_bounds__(kCryptWG) void k_tls_open(TlsArgs a) {
         const KeySched* ks = a.sched + w.key;
         if (w.key != cur) {
             load_tables(ks, tabs[wave]);
+            if (TLS_GHASH8) gf_table8(tabs[wave][6], t8);
             cur = w.key;
         }
         const bool is13 = ks->version == UVHTTP_TLS_VERSION_13;
@@ -637,7 +707,7 @@ __global__ __launch_bounds__(kCryptWG) void k_tls_open(TlsArgs a) {
             ct = rec + 13;
         }
         const uint32_t wlen = is13 ? (clen > 0 ? clen - 1 : 0) : clen;
-        const CryptOut co = gcm_record<false>(ks, te, lane & 31, tabs[wave], nonce, aad, alen, ct,
+        const CryptOut co = gcm_record<false>(ks, te, lane & (TLS_TE_COPIES - 1), tabs[wave], t8, nonce, aad, alen, ct,
                                               nullptr, clen, a.out + w.spec_off, wlen, nullptr, 0,
                                               0, is13);
         if (lane == 0) {
@@ -665,9 +735,15 @@ __global__ __launch_bounds__(kCryptWG) void k_tls_open(TlsArgs a) {
     }
 }
 
-__global__ __launch_bounds__(kCryptWG) void k_tls_seal(SealArgs a) {
-    __shared__ uint32_t te[256 * 32];
+__global__ CRYPT_ATTR void k_tls_seal(SealArgs a) {
+    __shared__ uint32_t te[256 * TLS_TE_COPIES];
     __shared__ U128 tabs[kCryptWaves][7][16];
+#if TLS_GHASH8
+    __shared__ U128 t8s[kCryptWaves][256];
+    U128* t8 = t8s[threadIdx.x >> 6];
+#else
+    U128* t8 = nullptr;
+#endif
     fill_te(a.te0, te);
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t cur = 0xFFFFFFFFu;
@@ -683,6 +759,7 @@ __global__ __launch_bounds__(kCryptWG) void k_tls_seal(SealArgs a) {
         if (sr.out_off + 5 + rlen > a.out_cap || sr.src_off + sr.plain_len > a.src_len) continue;
         if (sr.key != cur) {
             load_tables(ks, tabs[wave]);
+            if (TLS_GHASH8) gf_table8(tabs[wave][6], t8);
             cur = sr.key;
         }
         uint8_t* rec = a.out + sr.out_off;
@@ -712,7 +789,7 @@ __global__ __launch_bounds__(kCryptWG) void k_tls_seal(SealArgs a) {
         } else if (!is13 && lane < 13) {
             rec[lane] = (uint8_t)(sr.seq >> (8 * (12 - lane)));
         }
-        (void)gcm_record<true>(ks, te, lane & 31, tabs[wave], nonce, aad, alen, nullptr, ct, clen,
+        (void)gcm_record<true>(ks, te, lane & (TLS_TE_COPIES - 1), tabs[wave], t8, nonce, aad, alen, nullptr, ct, clen,
                                nullptr, 0, a.src + sr.src_off, sr.plain_len, sr.type, is13);
     }
 }
