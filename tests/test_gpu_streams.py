@@ -27,20 +27,24 @@ def torch():
     return t
 
 
-@pytest.fixture(scope="module", params=["lane", "wave"])
+@pytest.fixture(scope="module", params=["lane", "wave", "wave-twopass"])
 def eng(torch, request):
-    """Both frame-discovery walks (a lane or a wave per connection) must decode alike."""
+    """Every frame-discovery walk (a lane per connection; a wave per connection, single pass
+    through the offset scratch or the two-walk fallback) must decode alike."""
     import os
     import uvhttp_amd as U
-    old = os.environ.get("UVHTTP_WS_WALK")
-    os.environ["UVHTTP_WS_WALK"] = request.param
+    env = {"UVHTTP_WS_WALK": request.param.split("-")[0],
+           "UVHTTP_WS_WALK_SINGLE": "0" if request.param.endswith("twopass") else "1"}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         e = U.GpuEngine(0)
     finally:
-        if old is None:
-            os.environ.pop("UVHTTP_WS_WALK", None)
-        else:
-            os.environ["UVHTTP_WS_WALK"] = old
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     yield e
     e.close()
 
@@ -116,12 +120,9 @@ def _conn_case(rng, U, bad):
     return prod, orc, new
 
 
-@pytest.mark.parametrize("seed", range(10))
-def test_streams_match_process_data(torch, eng, hooks, seed):
-    import uvhttp_amd as U
-    rng = random.Random(9000 + seed)
-    bad = seed % 2 == 1
-    cases = [c for c in (_conn_case(rng, U, bad) for _ in range(rng.choice([1, 5, 40, 200]))) if c]
+def _run_cases(torch, eng, U, cases, rng, max_frames):
+    """One decode_streams call over every (product conn, oracle conn, new bytes) case, then the
+    reference semantics: deliver_stream on the product side vs process_data on the oracle."""
     # batch wire: each connection's buffered bytes + new read, 16-B aligned starts, gaps allowed
     chunks, streams, pos = [], [], 0
     for prod, orc, new in cases:
@@ -142,7 +143,6 @@ def test_streams_match_process_data(torch, eng, hooks, seed):
     sbytes = b"".join(bytes(s) for s in streams)
     dev_streams = torch.from_numpy(np.frombuffer(sbytes, np.uint8).copy()).to("cuda")
     dw = torch.from_numpy(wire.copy()).to("cuda")
-    max_frames = 4096
     desc, res = eng.decode_streams(dw, dev_streams, n, max_frames, wire_len=pos)
     torch.cuda.synchronize()
     results = eng.read_stream_results(res, n)
@@ -174,6 +174,15 @@ def test_streams_match_process_data(torch, eng, hooks, seed):
         assert sink == exp[len(exp) - len(sink):], k
 
 
+@pytest.mark.parametrize("seed", range(10))
+def test_streams_match_process_data(torch, eng, hooks, seed):
+    import uvhttp_amd as U
+    rng = random.Random(9000 + seed)
+    bad = seed % 2 == 1
+    cases = [c for c in (_conn_case(rng, U, bad) for _ in range(rng.choice([1, 5, 40, 200]))) if c]
+    _run_cases(torch, eng, U, cases, rng, 4096)
+
+
 def test_streams_capacity_overflow(torch, eng):
     import uvhttp_amd as U
     frames = b"".join(_frame(2, 1, b"x", b"\x00\x00\x00\x01") for _ in range(50))
@@ -189,3 +198,24 @@ def test_streams_capacity_overflow(torch, eng):
     r = eng.read_stream_results(res, 1)[0]
     assert r.status == -1 and r.first_status == -10
     assert torch.equal(dw, before)
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_streams_many_small_frames(torch, eng, hooks, seed):
+    """Connections with hundreds of frames: the wave walk crosses many 4 KiB blocks through
+    its prefetch ring, and jumps over blocks on the larger frames."""
+    import uvhttp_amd as U
+    rng = random.Random(777 + seed)
+    cases = []
+    for _ in range(9):
+        prod = U.WsConnection(1, 16 * 1024 * 1024, 64 * 1024 * 1024, user_data=True)
+        orc = _oracle.OracleConn(1, 16 * 1024 * 1024, 64 * 1024 * 1024, record=1, wrapper=True)
+        frames = []
+        for _ in range(rng.randint(200, 1200)):
+            payload = rng.randbytes(rng.choice([0, 1, 125, 126, 200, 260, 700, 4000, 9000]))
+            frames.append(_frame(2, 1, payload, rng.randbytes(4), True, 0))
+        new = b"".join(frames)
+        if rng.random() < 0.5:
+            new = new[: rng.randint(1, len(new))]
+        cases.append((prod, orc, new))
+    _run_cases(torch, eng, U, cases, rng, 16384)

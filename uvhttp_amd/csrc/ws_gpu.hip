@@ -219,6 +219,13 @@ struct StreamScratch {
     uint32_t* seg_bad;     // [n_streams] first undelivered frame of each connection
     uint32_t* walk_agg;    // [stream blocks + 1] frame counts per block, then prefixes
     uint32_t* n_total;     // [1] frames found (device-side frame count)
+    // single-pass wave walk: each connection's frame starts (relative u32) go to its slice of
+    // walk_tmp during the counting walk, then are copied into place (no second walk)
+    uint32_t* walk_tmp;    // [tmp_cap]
+    uint64_t tmp_cap;      // 0 = single pass unavailable
+    uint64_t* walk_base;   // [n_streams] slice start within its 256-connection block
+    uint64_t* bound_blk;   // [stream blocks + 1] slice totals, then prefixes; [nb] = total
+    uint32_t* walk_single; // [1] 1 when every slice fits walk_tmp
 };
 
 struct BatchArgs {
@@ -1220,6 +1227,27 @@ __device__ inline uint32_t walk_stream(const WalkArgs& w, uint32_t s, uint32_t f
     return count;
 }
 
+__device__ inline uint64_t block_exclusive_sum_u64(uint64_t v, uint64_t* total) {
+    __shared__ uint64_t wsum[kBlock / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint64_t inc = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t o = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += o;
+    }
+    if (lane == 63) wsum[wave] = inc;
+    __syncthreads();
+    uint64_t pre = 0, all = 0;
+    for (int k = 0; k < kBlock / 64; ++k) {
+        if (k < wave) pre += wsum[k];
+        all += wsum[k];
+    }
+    __syncthreads();
+    *total = all;
+    return pre + inc - v;
+}
+
 __device__ inline uint32_t block_exclusive_sum_u32(uint32_t v, uint32_t* total) {
     __shared__ uint32_t wsum[kBlock / 64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1241,17 +1269,53 @@ __device__ inline uint32_t block_exclusive_sum_u32(uint32_t v, uint32_t* total) 
     return pre + inc - v;
 }
 
-// Wave-per-connection walk (connections with many small frames): the 64 lanes stage a
-// 2 KiB window of the connection's bytes in LDS with one coalesced 16-byte load each (x2),
-// then every lane parses the same headers from LDS (broadcast reads) — a hop costs an LDS
-// round trip instead of dependent global byte loads, and a window reload is one memory
-// round trip for ~8 frames of 256 B.  Same decisions as walk_stream, byte for byte.
-constexpr int kWinVec = 2;
-constexpr uint32_t kWin = 64u * 16u * kWinVec;
+// Wave-per-connection walk (connections with many small frames).  The connection's bytes are
+// read in aligned 4 KiB blocks: LDS holds the block of the current header and the next one (a
+// two-slot ring, so a header straddling a block end is readable), and the block after those is
+// already in flight in registers (one 16-byte load per lane x 4), issued when the walk entered
+// the current block.  (A second block in flight measured the same: the compiler's waitcnt at
+// the loop head drains both.)  Every lane parses the same header from LDS (broadcast reads): the ten
+// bytes a header can need are independent ds_read_u8, one LDS round trip per hop.  A frame
+// longer than a block (the walk jumps) reloads the ring at the new position.  Same decisions
+// as walk_stream, byte for byte.
+constexpr uint32_t kWalkBlk = 4096;
+constexpr int kWalkVec = (int)(kWalkBlk / (64u * 16u));  // 16-byte loads per lane per block
 
-template <bool WRITE>
-__device__ inline uint32_t walk_stream_wave(const WalkArgs& w, uint32_t s, uint32_t first,
-                                            uint8_t* win) {
+__device__ inline void walk_load_block(const WalkArgs& w, uint64_t blk, u32x4 v[kWalkVec]) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < kWalkVec; ++k) {
+        const uint64_t src = blk * kWalkBlk + (uint64_t)(k * 64 + lane) * 16u;
+        if (src + 16 <= w.wire_len) {
+            v[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(w.wire + src));
+        } else {
+            uint32_t t[4] = {0, 0, 0, 0};
+            for (uint32_t q = 0; q < 16 && src + q < w.wire_len; ++q)
+                t[q >> 2] |= (uint32_t)w.wire[src + q] << (8 * (q & 3));
+            v[k] = u32x4{t[0], t[1], t[2], t[3]};
+        }
+    }
+}
+
+__device__ inline void walk_store_block(uint8_t* ring, uint64_t blk, const u32x4 v[kWalkVec]) {
+    const int lane = threadIdx.x & 63;
+    uint8_t* slot = ring + (blk & 1) * kWalkBlk;
+#pragma unroll
+    for (int k = 0; k < kWalkVec; ++k)
+        *reinterpret_cast<u32x4*>(slot + (uint32_t)(k * 64 + lane) * 16u) = v[k];
+}
+
+__device__ inline void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// MODE 0: count; 1: write frame_off / frame_seg from `first`; 2: write starts relative to
+// the connection into walk_tmp from `first` (a slice index)
+template <int MODE>
+__device__ inline uint32_t walk_stream_wave(const WalkArgs& w, uint32_t s, uint64_t first,
+                                            uint8_t* ring) {
     const int lane = threadIdx.x & 63;
     const uvhttp_ws_stream_t st = w.streams[s];
     const uint64_t L = st.begin + st.len <= w.wire_len ? st.len : 0;
@@ -1260,51 +1324,52 @@ __device__ inline uint32_t walk_stream_wave(const WalkArgs& w, uint32_t s, uint3
     const uint64_t mf = (uint64_t)(int64_t)st.max_frame_size;
     uint32_t count = 0;
     uint64_t pos = 0;
-    uint64_t wb = 0;
-    bool have = false;
+    uint64_t cur = ~0ull;  // block of the current header; LDS holds cur and cur + 1
+    u32x4 pf[kWalkVec];    // block cur + 2, in flight
+    auto byte_at = [&](uint64_t x) { return (uint32_t)ring[((x / kWalkBlk) & 1) * kWalkBlk + x % kWalkBlk]; };
     while (L - pos >= 2) {
         const uint64_t at = st.begin + pos;
-        if (!have || at < wb || at + 10 > wb + kWin) {
-            wb = at & ~(uint64_t)15;
-            have = true;
-#pragma unroll
-            for (int v = 0; v < kWinVec; ++v) {
-                const uint32_t o = (uint32_t)(v * 64 + lane) * 16u;
-                const uint64_t src = wb + o;
-                u32x4 x;
-                if (src + 16 <= w.wire_len) {
-                    x = *reinterpret_cast<const u32x4*>(w.wire + src);
-                } else {
-                    uint32_t t[4] = {0, 0, 0, 0};
-                    for (uint32_t k = 0; k < 16 && src + k < w.wire_len; ++k)
-                        t[k >> 2] |= (uint32_t)w.wire[src + k] << (8 * (k & 3));
-                    x = u32x4{t[0], t[1], t[2], t[3]};
-                }
-                *reinterpret_cast<u32x4*>(win + o) = x;
+        const uint64_t blk = at / kWalkBlk;
+        if (blk != cur) {
+            if (cur != ~0ull && blk == cur + 1) {
+                walk_store_block(ring, blk + 1, pf);  // the prefetched block joins the ring
+            } else {
+                u32x4 t[kWalkVec];
+                walk_load_block(w, blk, t);
+                walk_load_block(w, blk + 1, pf);
+                walk_store_block(ring, blk, t);
+                walk_store_block(ring, blk + 1, pf);
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            walk_load_block(w, blk + 2, pf);
+            cur = blk;
+            wave_sync_lds();
         }
-        const uint8_t* h = win + (at - wb);
-        const uint32_t b0 = h[0], b1 = h[1];
+        // the ten bytes a header can use, all independent LDS reads
+        uint32_t hb[10];
+#pragma unroll
+        for (int k = 0; k < 10; ++k) hb[k] = byte_at(at + k);
+        const uint32_t b0 = hb[0], b1 = hb[1];
         const uint32_t code = b1 & 0x7F;
         const uint32_t need = code == 126 ? 4 : code == 127 ? 10 : 2;
         if (L - pos < need) break;
         uint64_t plen = code;
-        if (need > 2) {
+        if (need == 4) {
+            plen = (hb[2] << 8) | hb[3];
+        } else if (need == 10) {
             plen = 0;
-            for (uint32_t k = 2; k < need; ++k) plen = (plen << 8) | h[k];
+#pragma unroll
+            for (int k = 2; k < 10; ++k) plen = (plen << 8) | hb[k];
         }
         const bool bad = (need == 10 && (plen >> 63)) || (b0 & 0x70) ||
                          ((b0 & 0x0F) >= 8 && (plen > 125 || !(b0 & 0x80))) ||
                          (st.is_server && !(b1 & 0x80)) || plen > mf;
         const uint64_t wl = need + ((b1 & 0x80) ? 4u : 0u) + plen;
         if (!bad && L - pos < wl) break;  // incomplete: waits for more bytes
-        if (WRITE && lane == 0 && first + count < w.max_frames) {
+        if (MODE == 1 && lane == 0 && first + count < w.max_frames) {
             w.sc.frame_off[first + count] = at;
             w.sc.frame_seg[first + count] = s;
         }
+        if (MODE == 2 && lane == 0) w.sc.walk_tmp[first + count] = (uint32_t)pos;
         ++count;
         if (bad) break;  // process_data returns at this frame
         pos += wl;
@@ -1312,13 +1377,76 @@ __device__ inline uint32_t walk_stream_wave(const WalkArgs& w, uint32_t s, uint3
     return count;
 }
 
-// wave mode pass 1: frames per connection (one wave each)
-__global__ __launch_bounds__(kBlock) void k_walk_count_wave(WalkArgs w) {
-    __shared__ __attribute__((aligned(16))) uint8_t win[kBlock / 64][kWin];
+// single-pass wave walk, step 1: each connection's slice of walk_tmp, an upper bound on the
+// frames the walk can count: every counted frame but the last (failing) one is >= 2 bytes,
+// and >= 6 on a server connection (unmasked frames fail there, :910-912)
+__global__ __launch_bounds__(kBlock) void k_walk_bound(WalkArgs w) {
+    const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
+    uint64_t b = 0;
+    if (s < w.n_streams) {
+        const uvhttp_ws_stream_t st = w.streams[s];
+        const uint64_t L = st.begin + st.len <= w.wire_len ? st.len : 0;
+        b = L / (st.is_server ? 6 : 2) + 1;
+    }
+    uint64_t total;
+    const uint64_t local = block_exclusive_sum_u64(b, &total);
+    if (s < w.n_streams) w.sc.walk_base[s] = local;
+    if (threadIdx.x == 0) w.sc.bound_blk[blockIdx.x] = total;
+}
+
+// step 2: slice prefixes over the blocks; single pass only if every slice fits
+__global__ __launch_bounds__(kBlock) void k_walk_bound_scan(WalkArgs w, uint32_t n_blocks) {
+    const uint32_t per = (n_blocks + kBlock - 1) / kBlock;
+    const uint32_t beg = threadIdx.x * per;
+    const uint32_t fin = beg + per < n_blocks ? beg + per : n_blocks;
+    uint64_t run = 0;
+    for (uint32_t b = beg; b < fin; ++b) run += w.sc.bound_blk[b];
+    uint64_t total;
+    uint64_t pre = block_exclusive_sum_u64(run, &total);
+    for (uint32_t b = beg; b < fin; ++b) {
+        const uint64_t v = w.sc.bound_blk[b];
+        w.sc.bound_blk[b] = pre;
+        pre += v;
+    }
+    if (threadIdx.x == 0) *w.sc.walk_single = total <= w.sc.tmp_cap ? 1u : 0u;
+}
+
+// step 3: the one walk — counts, and records the starts in the connection's slice
+__global__ __launch_bounds__(kBlock) void k_walk_once_wave(WalkArgs w) {
+    __shared__ __attribute__((aligned(16))) uint8_t win[kBlock / 64][2 * kWalkBlk];
     const uint32_t wave = threadIdx.x >> 6;
     const uint32_t s = blockIdx.x * (kBlock / 64) + wave;
     if (s >= w.n_streams) return;
-    const uint32_t c = walk_stream_wave<false>(w, s, 0, win[wave]);
+    const uint32_t c = *w.sc.walk_single
+        ? walk_stream_wave<2>(w, s, w.sc.walk_base[s] + w.sc.bound_blk[s / kBlock], win[wave])
+        : walk_stream_wave<0>(w, s, 0, win[wave]);
+    if ((threadIdx.x & 63) == 0) w.results[s].n_frames = c;
+}
+
+// step 5 (after the count scan placed each connection's first frame): copy the slice into
+// frame_off / frame_seg, coalesced
+__global__ __launch_bounds__(kBlock) void k_walk_compact(WalkArgs w) {
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t s = blockIdx.x * (kBlock / 64) + wave;
+    if (s >= w.n_streams || !*w.sc.walk_single) return;
+    const uvhttp_ws_stream_result_t r = w.results[s];
+    const uint64_t base = w.sc.walk_base[s] + w.sc.bound_blk[s / kBlock];
+    const uint64_t begin = w.streams[s].begin;
+    for (uint32_t k = lane; k < r.n_frames; k += 64) {
+        const uint64_t f = (uint64_t)r.first_frame + k;
+        if (f >= w.max_frames) break;
+        w.sc.frame_off[f] = begin + w.sc.walk_tmp[base + k];
+        w.sc.frame_seg[f] = s;
+    }
+}
+
+// wave mode pass 1: frames per connection (one wave each)
+__global__ __launch_bounds__(kBlock) void k_walk_count_wave(WalkArgs w) {
+    __shared__ __attribute__((aligned(16))) uint8_t win[kBlock / 64][2 * kWalkBlk];
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t s = blockIdx.x * (kBlock / 64) + wave;
+    if (s >= w.n_streams) return;
+    const uint32_t c = walk_stream_wave<0>(w, s, 0, win[wave]);
     if ((threadIdx.x & 63) == 0) w.results[s].n_frames = c;
 }
 
@@ -1333,12 +1461,13 @@ __global__ __launch_bounds__(kBlock) void k_walk_agg(WalkArgs w) {
 
 // wave mode pass 2: offsets, after k_walk_write<false> placed each connection's first frame
 __global__ __launch_bounds__(kBlock) void k_walk_write_wave(WalkArgs w) {
-    __shared__ __attribute__((aligned(16))) uint8_t win[kBlock / 64][kWin];
+    __shared__ __attribute__((aligned(16))) uint8_t win[kBlock / 64][2 * kWalkBlk];
     const uint32_t wave = threadIdx.x >> 6;
     const uint32_t s = blockIdx.x * (kBlock / 64) + wave;
     if (s >= w.n_streams) return;
+    if (w.sc.tmp_cap && *w.sc.walk_single) return;  // the single pass already has the starts
     const uvhttp_ws_stream_result_t r = w.results[s];
-    if (r.n_frames) (void)walk_stream_wave<true>(w, s, r.first_frame, win[wave]);
+    if (r.n_frames) (void)walk_stream_wave<1>(w, s, r.first_frame, win[wave]);
 }
 
 
@@ -1471,26 +1600,6 @@ __device__ inline uint64_t build_size(const uvhttp_ws_build_desc_t& f) {
     return (p < 126 ? 2 : p < 65536 ? 4 : 10) + (f.mask ? 4 : 0) + p;
 }
 
-__device__ inline uint64_t block_exclusive_sum_u64(uint64_t v, uint64_t* total) {
-    __shared__ uint64_t wsum[kBlock / 64];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint64_t inc = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint64_t o = __shfl_up(inc, d, 64);
-        if (lane >= d) inc += o;
-    }
-    if (lane == 63) wsum[wave] = inc;
-    __syncthreads();
-    uint64_t pre = 0, all = 0;
-    for (int k = 0; k < kBlock / 64; ++k) {
-        if (k < wave) pre += wsum[k];
-        all += wsum[k];
-    }
-    __syncthreads();
-    *total = all;
-    return pre + inc - v;
-}
 
 __global__ __launch_bounds__(kBlock) void kb_size(BuildArgs b) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
@@ -1814,6 +1923,9 @@ struct uvhttp_ws_gpu_engine {
     void* ss_mem;              // stream-decode scratch
     uint32_t ss_frames, ss_streams;
     StreamScratch ss;
+    void* wt_mem;              // single-pass walk scratch (frame starts per connection slice)
+    uint64_t wt_cap;
+    int walk_single_off;       // UVHTTP_WS_WALK_SINGLE=0: always walk twice (tests, A/B)
     void* bs_mem;              // send-side output-map records (BuildRec per map tile)
     uint64_t bs_tiles;
     int build_small;           // emit shape for frames < 4 KiB (UVHTTP_WS_BUILD_SMALL, tuning)
@@ -1870,6 +1982,7 @@ int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out) {
         e->epoch = v < kMaxEpoch ? (uint32_t)v : 0;
     }
     if (const char* bs = getenv("UVHTTP_WS_BUILD_SMALL")) e->build_small = atoi(bs);
+    if (const char* ws = getenv("UVHTTP_WS_WALK_SINGLE")) e->walk_single_off = atoi(ws) == 0;
     if (const char* wm = getenv("UVHTTP_WS_WALK"))
         e->walk_mode = strcmp(wm, "lane") == 0 ? 1 : strcmp(wm, "wave") == 0 ? 2 : 0;
     *out = e;
@@ -1884,6 +1997,7 @@ void uvhttp_ws_gpu_engine_free(uvhttp_ws_gpu_engine_t* e) {
     if (e->ws_mem) (void)hipFree(e->ws_mem);
     if (e->ss_mem) (void)hipFree(e->ss_mem);
     if (e->bs_mem) (void)hipFree(e->bs_mem);
+    if (e->wt_mem) (void)hipFree(e->wt_mem);
     for (int k = 0; k < e->ev_created; ++k) (void)hipEventDestroy(e->ev[k]);
     (void)hipSetDevice(prev);
     free(e);
@@ -2178,7 +2292,10 @@ static int reserve_streams(uvhttp_ws_gpu_engine_t* e, uint32_t frames, uint32_t 
     size_t o_bad = align_up(o_open + (size_t)fr * 8, 256);
     size_t o_agg = align_up(o_bad + (size_t)sn * 4, 256);
     size_t o_tot = align_up(o_agg + sblk * 4, 256);
-    size_t bytes = align_up(o_tot + 16, 256);
+    size_t o_wbase = align_up(o_tot + 16, 256);
+    size_t o_bblk = align_up(o_wbase + (size_t)sn * 8, 256);
+    size_t o_single = align_up(o_bblk + sblk * 8, 256);
+    size_t bytes = align_up(o_single + 16, 256);
     int prev = 0;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(e->device);
@@ -2197,6 +2314,9 @@ static int reserve_streams(uvhttp_ws_gpu_engine_t* e, uint32_t frames, uint32_t 
     e->ss.seg_bad = (uint32_t*)(b + o_bad);
     e->ss.walk_agg = (uint32_t*)(b + o_agg);
     e->ss.n_total = (uint32_t*)(b + o_tot);
+    e->ss.walk_base = (uint64_t*)(b + o_wbase);
+    e->ss.bound_blk = (uint64_t*)(b + o_bblk);
+    e->ss.walk_single = (uint32_t*)(b + o_single);
     e->ss_frames = fr;
     e->ss_streams = sn;
     return UVHTTP_WS_GPU_OK;
@@ -2237,11 +2357,29 @@ int uvhttp_ws_gpu_decode_streams(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uin
     const bool wave_walk = e->walk_mode ? e->walk_mode == 2 : n_streams <= 16384;
     if (wave_walk) {
         const uint32_t nwb = (n_streams + kBlock / 64 - 1) / (kBlock / 64);
-        hipLaunchKernelGGL(k_walk_count_wave, dim3(nwb), dim3(kBlock), 0, s, w);
+        // single pass when the offset scratch fits: bound <= wire/2 + one per connection
+        // (4-byte entries, so at most 2 bytes per wire byte; capped at 8 GiB)
+        const uint64_t want = wire_len / 2 + n_streams + 1;
+        if (e->walk_single_off == 0 && want * 4 <= (8ull << 30) && want > e->wt_cap) {
+            if (e->wt_mem) (void)hipFree(e->wt_mem);
+            e->wt_mem = nullptr;
+            e->wt_cap = 0;
+            if (hipMalloc(&e->wt_mem, want * 4) == hipSuccess) e->wt_cap = want;
+        }
+        w.sc.walk_tmp = (uint32_t*)e->wt_mem;
+        w.sc.tmp_cap = e->walk_single_off ? 0 : e->wt_cap;
+        if (w.sc.tmp_cap) {
+            hipLaunchKernelGGL(k_walk_bound, dim3(nsb), dim3(kBlock), 0, s, w);
+            hipLaunchKernelGGL(k_walk_bound_scan, dim3(1), dim3(kBlock), 0, s, w, nsb);
+            hipLaunchKernelGGL(k_walk_once_wave, dim3(nwb), dim3(kBlock), 0, s, w);
+        } else {
+            hipLaunchKernelGGL(k_walk_count_wave, dim3(nwb), dim3(kBlock), 0, s, w);
+        }
         hipLaunchKernelGGL(k_walk_agg, dim3(nsb), dim3(kBlock), 0, s, w);
         hipLaunchKernelGGL(k_walk_scan, dim3(1), dim3(kBlock), 0, s, w, nsb);
         hipLaunchKernelGGL(k_walk_write<false>, dim3(nsb), dim3(kBlock), 0, s, w);
-        hipLaunchKernelGGL(k_walk_write_wave, dim3(nwb), dim3(kBlock), 0, s, w);
+        if (w.sc.tmp_cap) hipLaunchKernelGGL(k_walk_compact, dim3(nwb), dim3(kBlock), 0, s, w);
+        hipLaunchKernelGGL(k_walk_write_wave, dim3(nwb), dim3(kBlock), 0, s, w);  // fallback
     } else {
         hipLaunchKernelGGL(k_walk_count, dim3(nsb), dim3(kBlock), 0, s, w);
         hipLaunchKernelGGL(k_walk_scan, dim3(1), dim3(kBlock), 0, s, w, nsb);
