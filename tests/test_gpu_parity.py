@@ -490,3 +490,33 @@ def test_epoch_wraparound(torch, monkeypatch):
                 _compare(ref, got, compact)
     finally:
         e.close()
+
+
+@pytest.mark.parametrize("compact", [False, True])
+@pytest.mark.parametrize("plen", [0, 3, 60, 200, 1000])
+def test_stride_layouts(torch, eng, plen, compact):
+    """Fixed-stride batches of small frames (the payload kernels find a vector's frame by
+    arithmetic there): uniform frames, a longer last frame, a wrong-sized frame (LAYOUT), a cut
+    last frame, a failing frame in the middle, mixed opcodes of the same wire size."""
+    rng = random.Random(plen)
+    k = lambda: rng.randbytes(4)  # noqa: E731
+    n = 600
+    base = [_frame(rng.choice([1, 2]), 1, rng.randbytes(plen), k()) for _ in range(n)]
+    stride = len(base[0])
+    variants = {"uniform": base,
+                "long_last": base[:-1] + [_frame(2, 1, rng.randbytes(plen + 777), k())],
+                "layout": base[:300] + [_frame(2, 1, rng.randbytes(plen + 1), k())] + base[301:],
+                "rsv": base[:200] + [_frame(2, 1, rng.randbytes(plen), k(), rsv=4)] + base[201:]}
+    if plen <= 125:  # same wire size: PING / CONT fragments / TEXT mixed
+        mix = []
+        for i in range(n):
+            # PING, TEXT start, CONT end, BINARY, PONG
+            mix.append(_frame([9, 1, 0, 2, 10][i % 5], 0 if i % 5 == 1 else 1,
+                              rng.randbytes(plen), k()))
+        variants["mixed"] = mix
+    for name, frames in variants.items():
+        wire = np.frombuffer(b"".join(frames), np.uint8).copy()
+        for wl in (wire.size, wire.size - 1 - rng.randrange(min(stride, 30))):
+            ref, got = _run_both(torch, eng, wire, len(frames), stride=stride, wire_len=wl,
+                                 compact=compact)
+            _compare(ref, got, compact)
