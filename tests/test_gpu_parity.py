@@ -26,10 +26,21 @@ def torch():
     return t
 
 
-@pytest.fixture(scope="module")
-def eng(torch):
+@pytest.fixture(scope="module", params=["gather", "scatter"])
+def eng(torch, request):
+    """Both compact-decode kernels (arena-driven gather, wire-driven scatter; the engine picks
+    by average frame size) must produce the same arena; in-place runs are unaffected."""
+    import os
     import uvhttp_amd as U
-    e = U.GpuEngine(0)
+    old = os.environ.get("UVHTTP_WS_COMPACT")
+    os.environ["UVHTTP_WS_COMPACT"] = request.param
+    try:
+        e = U.GpuEngine(0)
+    finally:
+        if old is None:
+            os.environ.pop("UVHTTP_WS_COMPACT", None)
+        else:
+            os.environ["UVHTTP_WS_COMPACT"] = old
     yield e
     e.close()
 

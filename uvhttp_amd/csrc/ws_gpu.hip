@@ -31,6 +31,7 @@ namespace {
 
 constexpr int kBlock = 256;                 // threads per workgroup (4 waves of 64)
 constexpr uint64_t kMapTile = 16384;        // granularity of the tile -> first-frame maps
+constexpr uint64_t kScatterAvg = 16384;     // compact decode: wire-driven below this frame size
 constexpr uint32_t kMaxFrames = 1u << 26;   // k_scan handles <= 2^18 block aggregates
 constexpr uint32_t kNoFrame = 0xFFFFFFFFu;  // tile map entry no frame claimed this call
 constexpr uint32_t kMaxEpoch = (1u << 30) - 1;  // decode-call tags run 1 .. kMaxEpoch
@@ -1157,6 +1158,137 @@ __global__ __launch_bounds__(BLOCK) void k_gather_compact(
 }
 
 // ------------------------------------------------------------------------------------
+// k_scatter_compact: the compact decode for small frames, driven by the WIRE instead of the
+// arena.  The arena-driven gather must find a tile's frames before it knows what to load (map
+// -> descriptors -> source loads: three dependent round trips per workgroup), which leaves
+// frames of a few hundred bytes at ~4 TB/s.  Here each workgroup takes a wire tile like the
+// in-place kernel: its loads are issued first, the frames come from the in-place tile map
+// (staged in LDS, binary search per vector) while they are in flight, and each vector's
+// payload bytes of a delivered data frame are unmasked and stored at the frame's arena offset
+// (unaligned 16-byte stores; the bytes at a payload's edges by 8/4/2/1-byte pieces).
+// ------------------------------------------------------------------------------------
+// bytes [0, n) of v (little-endian) to p, n <= 16
+__device__ inline void store_lo_bytes(uint8_t* p, unsigned __int128 v, int n) {
+    if (n == 16) {
+        __builtin_memcpy(p, &v, 16);
+        return;
+    }
+    if (n & 8) {
+        const uint64_t w = (uint64_t)v;
+        __builtin_memcpy(p, &w, 8);
+        p += 8;
+        v >>= 64;
+    }
+    if (n & 4) {
+        const uint32_t w = (uint32_t)v;
+        __builtin_memcpy(p, &w, 4);
+        p += 4;
+        v >>= 32;
+    }
+    if (n & 2) {
+        const uint16_t w = (uint16_t)v;
+        __builtin_memcpy(p, &w, 2);
+        p += 2;
+        v >>= 16;
+    }
+    if (n & 1) *p = (uint8_t)v;
+}
+
+template <int BLOCK, int VPT>
+__global__ __launch_bounds__(BLOCK) void k_scatter_compact(
+    BatchArgs a, const uvhttp_ws_frame_desc_t* __restrict__ desc, Workspace ws,
+    uint64_t arena_bytes_cap, uint64_t tile_base) {
+    constexpr uint64_t kT = (uint64_t)BLOCK * VPT * 16;
+    __shared__ uint64_t s_ps[BLOCK];  // wire offset of the payload
+    __shared__ uint64_t s_pe[BLOCK];  // its end (== start: not a delivered data frame)
+    __shared__ uint64_t s_ao[BLOCK];  // arena offset
+    __shared__ uint32_t s_key[BLOCK];
+
+    const uint64_t t0 = (tile_base + blockIdx.x) * kT;
+    const uint64_t vend = a.wire_len;
+    const uint64_t full_end = vend & ~(uint64_t)15;
+    const uint64_t clamp_va = full_end ? full_end - 16 : 0;
+    u32x4 data[VPT];
+    uint64_t va[VPT];
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {
+        va[v] = t0 + ((uint64_t)v * BLOCK + threadIdx.x) * 16u;
+        const uint64_t la = va[v] < full_end ? va[v] : clamp_va;
+        data[v] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.wire + la));
+    }
+    // the one vector straddling the end of the wire: its bytes individually (the clamped
+    // load above read the previous vector)
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {
+        if (va[v] == full_end && full_end < vend) {
+            uint32_t t[4] = {0, 0, 0, 0};
+            for (uint64_t q = 0; full_end + q < vend; ++q)
+                t[q >> 2] |= (uint32_t)a.wire[full_end + q] << (8 * (q & 3));
+            data[v] = u32x4{t[0], t[1], t[2], t[3]};
+        }
+    }
+    const uint32_t n = nframes(a);
+    const uint32_t nb = first_bad_of(a, ws, n);
+    if (nb == 0 || n == 0 || t0 >= vend) return;
+    const uint32_t last = (nb < n ? nb : n) - 1;
+    const uint64_t c0 = t0 / kMapTile, c1 = (t0 + kT - 1) / kMapTile + 1;
+    const uint32_t f0 = tag_get(ws.tile_first[c0], a.epoch, kNoFrame);
+    uint32_t f1 = (c1 < a.n_tiles) ? tag_get(ws.tile_first[c1], a.epoch, kNoFrame) : last;
+    if (f0 > last) return;
+    if (f1 > last || f1 < f0) f1 = last;
+
+    for (uint32_t base = f0; base <= f1; base += BLOCK) {
+        const uint32_t cnt = (f1 - base + 1) < (uint32_t)BLOCK ? (f1 - base + 1) : BLOCK;
+        __syncthreads();
+        if (threadIdx.x < cnt) {
+            const uint32_t f = base + threadIdx.x;
+            const uvhttp_ws_frame_desc_t d = desc[f];
+            const uint64_t ps = frame_start(a, f) + d.header_size + ((d.flags & UVHTTP_WS_FLAG_MASK) ? 4u : 0u);
+            const bool data_frame = d.opcode <= 2;
+            s_ps[threadIdx.x] = ps;
+            s_pe[threadIdx.x] = ps + (data_frame ? d.payload_len : 0);
+            s_ao[threadIdx.x] = d.payload_off;
+            s_key[threadIdx.x] = d.masking_key;
+        }
+        __syncthreads();
+        if (s_ps[0] >= t0 + kT) break;
+#pragma unroll
+        for (int v = 0; v < VPT; ++v) {
+            if (va[v] >= vend) continue;
+            int lo = 0, hi = (int)cnt - 1, j = -1;
+            while (lo <= hi) {
+                const int mid = (lo + hi) >> 1;
+                if (s_ps[mid] < va[v] + 16) {
+                    j = mid;
+                    lo = mid + 1;
+                } else {
+                    hi = mid - 1;
+                }
+            }
+            for (; j >= 0; --j) {
+                const uint64_t ps = s_ps[j], pe = s_pe[j];
+                if (pe <= va[v]) {
+                    if (pe != ps) break;  // empty / control payloads don't end the walk
+                    continue;
+                }
+                const int b0 = ps > va[v] ? (int)(ps - va[v]) : 0;
+                int b1 = pe < va[v] + 16 ? (int)(pe - va[v]) : 16;
+                if (va[v] + b1 > vend) b1 = (int)(vend - va[v]);
+                const uint64_t dst = s_ao[j] + (va[v] + b0 - ps);
+                if (dst >= arena_bytes_cap || b1 <= b0) continue;
+                const int len = (int)(dst + (b1 - b0) <= arena_bytes_cap ? b1 - b0 : arena_bytes_cap - dst);
+                const uint32_t rk = rotr32(s_key[j], 8u * (uint32_t)((va[v] - ps) & 3u));
+                const u32x4 x = data[v] ^ u32x4{rk, rk, rk, rk};
+                unsigned __int128 w = ((unsigned __int128)(((uint64_t)x.w << 32) | x.z) << 64) |
+                                      (((uint64_t)x.y << 32) | x.x);
+                w >>= 8 * b0;
+                store_lo_bytes(a.arena + dst, w, len);
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // stream decode: frame discovery.  One lane per connection walks its buffered bytes header
 // by header exactly as process_data's loop does (:872-932) and stops where process_data
 // stops: fewer bytes than a header needs, a frame process_data rejects before unmasking
@@ -1932,6 +2064,7 @@ struct uvhttp_ws_gpu_engine {
     void* bs_mem;              // send-side output-map records (BuildRec per map tile)
     uint64_t bs_tiles;
     int build_small;           // emit shape for frames < 4 KiB (UVHTTP_WS_BUILD_SMALL, tuning)
+    int compact_mode;          // 0 automatic, 1 arena-driven gather, 2 wire-driven scatter
     hipEvent_t ev[2 * 1024];
     int ev_created;
     int ev_used;       // event pairs recorded and not yet harvested
@@ -1985,6 +2118,8 @@ int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out) {
         e->epoch = v < kMaxEpoch ? (uint32_t)v : 0;
     }
     if (const char* bs = getenv("UVHTTP_WS_BUILD_SMALL")) e->build_small = atoi(bs);
+    if (const char* cm = getenv("UVHTTP_WS_COMPACT"))
+        e->compact_mode = strcmp(cm, "gather") == 0 ? 1 : strcmp(cm, "scatter") == 0 ? 2 : 0;
     if (const char* ws = getenv("UVHTTP_WS_WALK_SINGLE")) e->walk_single_off = atoi(ws) == 0;
     if (const char* wm = getenv("UVHTTP_WS_WALK"))
         e->walk_mode = strcmp(wm, "lane") == 0 ? 1 : strcmp(wm, "wave") == 0 ? 2 : 0;
@@ -2223,9 +2358,12 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
     // payload kernel tile shape: explicit (set_tile) or by average wire bytes per frame
     // (auto shapes from tools/tile_sweep.py on MI355X, profiles/r01_tile_sweep.txt)
     int blk = e->tile_block, vpt = e->tile_vpt;
+    const uint64_t avg = a.n ? b->wire_len / a.n : 0;
+    // compact decode: frames below kScatterAvg wire bytes on average take the wire-driven
+    // scatter kernel, larger ones the arena-driven gather (UVHTTP_WS_COMPACT=gather|scatter)
+    const bool scatter = arena && (e->compact_mode ? e->compact_mode == 2 : avg < kScatterAvg);
     if (!blk) {
-        const uint64_t avg = a.n ? b->wire_len / a.n : 0;
-        if (!arena) {
+        if (!arena || scatter) {
             blk = avg >= 32768 ? 64 : 256;
             vpt = avg >= 32768 ? 1 : avg >= 2048 ? 2 : 4;
         } else {
@@ -2233,7 +2371,7 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
             vpt = 2;
         }
     }
-    const uint64_t span = arena ? n_atiles * kMapTile : b->wire_len;
+    const uint64_t span = arena && !scatter ? n_atiles * kMapTile : b->wire_len;
     const uint64_t tile_bytes = (uint64_t)blk * vpt * 16;
     const uint64_t n_ptiles = (span + tile_bytes - 1) / tile_bytes;
     // the dispatch packet counts work-items in 32 bits: split very large passes
@@ -2249,6 +2387,9 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
         else if (!arena)                                                                         \
             hipLaunchKernelGGL((k_unmask_inplace<B, V>), dim3(grid_p), dim3(B), 0, s, a, d_desc, \
                                e->ws, tb);                                                       \
+        else if (scatter)                                                                        \
+            hipLaunchKernelGGL((k_scatter_compact<B, V>), dim3(grid_p), dim3(B), 0, s, a,        \
+                               d_desc, e->ws, arena_cap, tb);                                    \
         else                                                                                     \
             hipLaunchKernelGGL((k_gather_compact<B, V>), dim3(grid_p), dim3(B), 0, s, a, d_desc, \
                                e->ws, arena_cap, tb);                                            \
