@@ -514,20 +514,28 @@ struct SealArgs {
     const uint32_t* te0;
 };
 
-// One record's GCM on one wave.  OPEN: ciphertext at ct[0, clen) -> plaintext content to
-// dst[0, wlen) (wlen = bytes to keep), returns tag match + (TLS 1.3) the last non-zero byte.
-// SEAL: plaintext from the (content, type) generator -> ciphertext at ct, tag after it.
+// One record's GCM on one wave, in two parts around the lane combine.  OPEN: ciphertext at
+// ct[0, clen) -> plaintext content to dst[0, wlen) (wlen = bytes to keep), then tag match +
+// (TLS 1.3) the last non-zero byte.  SEAL: plaintext from the (content, type) generator ->
+// ciphertext at ct, tag after it.
 struct CryptOut {
     bool tag_ok;
     uint32_t last_nz;  // (index + 1) << 8 | byte of the last non-zero inner byte, 0 if none
 };
 
+struct Lanes {          // per-lane state after the Horner pass
+    U128 acc;           // the lane's Horner sum (multiplier H^64)
+    uint32_t ej0[4];    // E(K, J0) in the lane that held the AAD block
+    uint32_t last_nz;
+    uint32_t src_lane;  // that lane
+};
+
 template <bool SEAL>
-__device__ CryptOut gcm_record(const KeySched* __restrict__ ks, const uint32_t* te, uint32_t lane32,
-                               const U128 (*tabs)[16], const U128* t8, const uint32_t nonce[3], U128 aad,
-                               uint32_t alen, const uint8_t* ct_in, uint8_t* ct_out, uint32_t clen,
-                               uint8_t* dst, uint32_t wlen, const uint8_t* src, uint32_t src_n,
-                               uint32_t inner_type, bool is13) {
+__device__ Lanes gcm_lanes(const KeySched* __restrict__ ks, const uint32_t* te, uint32_t lane32,
+                           const U128 (*tabs)[16], const U128* t8, const uint32_t nonce[3], U128 aad,
+                           uint32_t alen, const uint8_t* ct_in, uint8_t* ct_out, uint32_t clen,
+                           uint8_t* dst, uint32_t wlen, const uint8_t* src, uint32_t src_n,
+                           uint32_t inner_type, bool is13) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t nr = ks->nr;
     const uint32_t nblk = (clen + 15) / 16;
@@ -605,17 +613,47 @@ __device__ CryptOut gcm_record(const KeySched* __restrict__ ks, const uint32_t* 
         acc = j == 0 ? x : gf_xor(gf_mul_tab(acc, tabs[6]), x);  // Horner, multiplier H^64
 #endif
     }
-    // combine lanes: level t joins groups of 2^t lanes with multiplier H^(2^t)
+    // E(K, J0) lives in the lane that held the AAD block: lane pad % 64 of iteration pad / 64
+    return Lanes{acc, {ej0[0], ej0[1], ej0[2], ej0[3]}, last_nz, pad & 63};
+}
+
+// combine one wave's lanes: level t joins groups of 2^t lanes with multiplier H^(2^t); lane 0
+// ends with the GHASH
+[[maybe_unused]] __device__ inline U128 wave_tree(U128 acc, const U128 (*tabs)[16]) {
 #pragma unroll
     for (int t = 0; t < 6; ++t) {
         const U128 right = shfl_down128(acc, 1 << t);
         acc = gf_xor(gf_mul_tab(acc, tabs[t]), right);
     }
-    acc = gf_mul_tab(acc, tabs[0]);  // lane 0: GHASH
-    // E(K, J0) lives in the lane that held the AAD block: lane pad % 64 of iteration pad / 64
-    const uint32_t src_lane = pad & 63;
+    return gf_mul_tab(acc, tabs[0]);
+}
+
+// the same combine for the workgroup's four records at once, through LDS: at level t the
+// 4 x 32 / 2^t pairs are spread over the workgroup's threads, so the four trees cost about two
+// wave-wide multiplies per record instead of seven (s_acc[w][l] = record w, lane l)
+[[maybe_unused]] __device__ inline void wg_tree(U128 (*s_acc)[64], const U128 (*tabs)[7][16]) {
+#pragma unroll
+    for (int t = 0; t < 6; ++t) {
+        const uint32_t per = 32u >> t;  // pairs per record at this level
+        if (threadIdx.x < kCryptWaves * per) {
+            const uint32_t w = threadIdx.x / per, p = threadIdx.x % per;
+            const uint32_t l = p << (t + 1), r = l + (1u << t);
+            s_acc[w][l] = gf_xor(gf_mul_tab(s_acc[w][l], tabs[w][t]), s_acc[w][r]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x < kCryptWaves) s_acc[threadIdx.x][0] = gf_mul_tab(s_acc[threadIdx.x][0], tabs[threadIdx.x][0]);
+    __syncthreads();
+}
+
+// tag from the GHASH (valid in lane 0): SEAL stores it after the ciphertext, OPEN compares
+template <bool SEAL>
+__device__ CryptOut gcm_finish(const Lanes& L, U128 acc, const uint8_t* ct_in, uint8_t* ct_out,
+                               uint32_t clen) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t last_nz = L.last_nz;
     uint32_t e[4];
-    for (int b = 0; b < 4; ++b) e[b] = __shfl(ej0[b], src_lane, 64);
+    for (int b = 0; b < 4; ++b) e[b] = __shfl(L.ej0[b], L.src_lane, 64);
     const U128 tag{acc.hi ^ (((uint64_t)e[0] << 32) | e[1]), acc.lo ^ (((uint64_t)e[2] << 32) | e[3])};
     CryptOut r{false, 0};
     if (SEAL) {
@@ -655,6 +693,10 @@ __device__ inline void fill_te(const uint32_t* te0, uint32_t* te) {
     __syncthreads();
 }
 
+#ifndef TLS_WG_TREE
+#define TLS_WG_TREE 1      // 1: the lane combine of the workgroup's 4 records shared through LDS
+#endif
+
 __global__ CRYPT_ATTR void k_tls_open(TlsArgs a) {
     __shared__ uint32_t te[256 * TLS_TE_COPIES];
     __shared__ U128 tabs[kCryptWaves][7][16];
@@ -664,52 +706,75 @@ __global__ CRYPT_ATTR void k_tls_open(TlsArgs a) {
 #else
     U128* t8 = nullptr;
 #endif
+#if TLS_WG_TREE
+    __shared__ U128 s_acc[kCryptWaves][64];
+#endif
     fill_te(a.te0, te);
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t n = a.n_total[0];
     uint32_t cur = 0xFFFFFFFFu;
-    // r is wave-uniform: readfirstlane makes the record and key-schedule loads scalar
-    for (uint32_t r = __builtin_amdgcn_readfirstlane(blockIdx.x * kCryptWaves + wave); r < n;
-         r += gridDim.x * kCryptWaves) {
-        RecWork w = a.work[r];
-        if (w.status != 0) continue;  // header failure: nothing to open
-        const KeySched* ks = a.sched + w.key;
-        if (w.key != cur) {
-            load_tables(ks, tabs[wave]);
-            if (TLS_GHASH8) gf_table8(tabs[wave][6], t8);
-            cur = w.key;
+    // rounds are workgroup-uniform (the shared combine has barriers); r is wave-uniform:
+    // readfirstlane makes the record and key-schedule loads scalar
+    for (uint32_t rb = blockIdx.x * kCryptWaves; rb < n; rb += gridDim.x * kCryptWaves) {
+        const uint32_t r = __builtin_amdgcn_readfirstlane(rb + wave);
+        RecWork w;
+        bool active = r < n;
+        if (active) {
+            w = a.work[r];
+            active = w.status == 0;  // header failure: nothing to open
         }
-        const bool is13 = ks->version == UVHTTP_TLS_VERSION_13;
-        const uint8_t* rec = a.wire + w.rec_off;
-        uint32_t nonce[3];
-        U128 aad;
-        uint32_t alen, clen;
-        const uint8_t* ct;
-        if (is13) {
-            nonce[0] = ks->iv[0];
-            nonce[1] = ks->iv[1] ^ (uint32_t)(w.seq >> 32);
-            nonce[2] = ks->iv[2] ^ (uint32_t)w.seq;
-            uint32_t h[4];
-            load_part(rec, 0, 5, h);
-            aad = le_to_block(h);
-            alen = 5;
-            clen = w.len - 16;
-            ct = rec + 5;
-        } else {
-            uint32_t ex[4];
-            load_part(rec + 5, 0, 8, ex);
-            nonce[0] = ks->iv[0];
-            nonce[1] = bswap32(ex[0]);
-            nonce[2] = bswap32(ex[1]);
-            clen = w.len - 24;
-            aad = U128{w.seq, ((uint64_t)rec[0] << 56) | (0x0303ull << 40) | ((uint64_t)clen << 24)};
-            alen = 13;
-            ct = rec + 13;
+        Lanes L{U128{0, 0}, {0, 0, 0, 0}, 0, 0};
+        const KeySched* ks = a.sched + (active ? w.key : 0);
+        const uint8_t* rec = a.wire + (active ? w.rec_off : 0);
+        bool is13 = false;
+        uint32_t clen = 0;
+        const uint8_t* ct = rec;
+        if (active) {
+            if (w.key != cur) {
+                load_tables(ks, tabs[wave]);
+                if (TLS_GHASH8) gf_table8(tabs[wave][6], t8);
+                cur = w.key;
+            }
+            is13 = ks->version == UVHTTP_TLS_VERSION_13;
+            uint32_t nonce[3];
+            U128 aad;
+            uint32_t alen;
+            if (is13) {
+                nonce[0] = ks->iv[0];
+                nonce[1] = ks->iv[1] ^ (uint32_t)(w.seq >> 32);
+                nonce[2] = ks->iv[2] ^ (uint32_t)w.seq;
+                uint32_t h[4];
+                load_part(rec, 0, 5, h);
+                aad = le_to_block(h);
+                alen = 5;
+                clen = w.len - 16;
+                ct = rec + 5;
+            } else {
+                uint32_t ex[4];
+                load_part(rec + 5, 0, 8, ex);
+                nonce[0] = ks->iv[0];
+                nonce[1] = bswap32(ex[0]);
+                nonce[2] = bswap32(ex[1]);
+                clen = w.len - 24;
+                aad = U128{w.seq, ((uint64_t)rec[0] << 56) | (0x0303ull << 40) | ((uint64_t)clen << 24)};
+                alen = 13;
+                ct = rec + 13;
+            }
+            const uint32_t wlen = is13 ? (clen > 0 ? clen - 1 : 0) : clen;
+            L = gcm_lanes<false>(ks, te, lane & (TLS_TE_COPIES - 1), tabs[wave], t8, nonce, aad,
+                                 alen, ct, nullptr, clen, a.out + w.spec_off, wlen, nullptr, 0, 0,
+                                 is13);
         }
-        const uint32_t wlen = is13 ? (clen > 0 ? clen - 1 : 0) : clen;
-        const CryptOut co = gcm_record<false>(ks, te, lane & (TLS_TE_COPIES - 1), tabs[wave], t8, nonce, aad, alen, ct,
-                                              nullptr, clen, a.out + w.spec_off, wlen, nullptr, 0,
-                                              0, is13);
+#if TLS_WG_TREE
+        s_acc[wave][lane] = L.acc;
+        __syncthreads();
+        wg_tree(s_acc, tabs);
+        const U128 ghash = s_acc[wave][0];
+#else
+        const U128 ghash = active ? wave_tree(L.acc, tabs[wave]) : U128{0, 0};
+#endif
+        if (!active) continue;
+        const CryptOut co = gcm_finish<false>(L, ghash, ct, nullptr, clen);
         if (lane == 0) {
             int32_t st;
             uint32_t type = 0, cl = 0;
@@ -744,53 +809,80 @@ __global__ CRYPT_ATTR void k_tls_seal(SealArgs a) {
 #else
     U128* t8 = nullptr;
 #endif
+#if TLS_WG_TREE
+    __shared__ U128 s_acc[kCryptWaves][64];
+#endif
     fill_te(a.te0, te);
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t cur = 0xFFFFFFFFu;
-    for (uint32_t r = __builtin_amdgcn_readfirstlane(blockIdx.x * kCryptWaves + wave); r < a.n;
-         r += gridDim.x * kCryptWaves) {
-        const uvhttp_tls_seal_t sr = a.recs[r];
-        if (sr.key >= a.n_keys) continue;
-        const KeySched* ks = a.sched + sr.key;
-        if (ks->nr == 0 || sr.plain_len > 16384) continue;
-        const bool is13 = ks->version == UVHTTP_TLS_VERSION_13;
-        const uint32_t clen = sr.plain_len + (is13 ? 1u : 0u);
-        const uint32_t rlen = clen + 16 + (is13 ? 0u : 8u);
-        if (sr.out_off + 5 + rlen > a.out_cap || sr.src_off + sr.plain_len > a.src_len) continue;
-        if (sr.key != cur) {
-            load_tables(ks, tabs[wave]);
-            if (TLS_GHASH8) gf_table8(tabs[wave][6], t8);
-            cur = sr.key;
+    for (uint32_t rb = blockIdx.x * kCryptWaves; rb < a.n; rb += gridDim.x * kCryptWaves) {
+        const uint32_t r = __builtin_amdgcn_readfirstlane(rb + wave);
+        uvhttp_tls_seal_t sr;
+        bool active = r < a.n;
+        const KeySched* ks = a.sched;
+        bool is13 = false;
+        uint32_t clen = 0, rlen = 0;
+        if (active) {
+            sr = a.recs[r];
+            active = sr.key < a.n_keys;
+            if (active) {
+                ks = a.sched + sr.key;
+                active = ks->nr != 0 && sr.plain_len <= 16384;
+            }
+            if (active) {
+                is13 = ks->version == UVHTTP_TLS_VERSION_13;
+                clen = sr.plain_len + (is13 ? 1u : 0u);
+                rlen = clen + 16 + (is13 ? 0u : 8u);
+                active = sr.out_off + 5 + rlen <= a.out_cap && sr.src_off + sr.plain_len <= a.src_len;
+            }
         }
-        uint8_t* rec = a.out + sr.out_off;
-        const uint32_t otype = is13 ? 23u : sr.type;
-        uint32_t nonce[3];
-        U128 aad;
-        uint32_t alen;
-        uint8_t* ct;
-        if (is13) {
-            nonce[0] = ks->iv[0];
-            nonce[1] = ks->iv[1] ^ (uint32_t)(sr.seq >> 32);
-            nonce[2] = ks->iv[2] ^ (uint32_t)sr.seq;
-            aad = U128{((uint64_t)otype << 56) | (0x0303ull << 40) | ((uint64_t)rlen << 24), 0};
-            alen = 5;
-            ct = rec + 5;
-        } else {
-            nonce[0] = ks->iv[0];
-            nonce[1] = (uint32_t)(sr.seq >> 32);
-            nonce[2] = (uint32_t)sr.seq;
-            aad = U128{sr.seq, ((uint64_t)otype << 56) | (0x0303ull << 40) | ((uint64_t)clen << 24)};
-            alen = 13;
-            ct = rec + 13;
+        Lanes L{U128{0, 0}, {0, 0, 0, 0}, 0, 0};
+        uint8_t* ct = a.out;
+        if (active) {
+            if (sr.key != cur) {
+                load_tables(ks, tabs[wave]);
+                if (TLS_GHASH8) gf_table8(tabs[wave][6], t8);
+                cur = sr.key;
+            }
+            uint8_t* rec = a.out + sr.out_off;
+            const uint32_t otype = is13 ? 23u : sr.type;
+            uint32_t nonce[3];
+            U128 aad;
+            uint32_t alen;
+            if (is13) {
+                nonce[0] = ks->iv[0];
+                nonce[1] = ks->iv[1] ^ (uint32_t)(sr.seq >> 32);
+                nonce[2] = ks->iv[2] ^ (uint32_t)sr.seq;
+                aad = U128{((uint64_t)otype << 56) | (0x0303ull << 40) | ((uint64_t)rlen << 24), 0};
+                alen = 5;
+                ct = rec + 5;
+            } else {
+                nonce[0] = ks->iv[0];
+                nonce[1] = (uint32_t)(sr.seq >> 32);
+                nonce[2] = (uint32_t)sr.seq;
+                aad = U128{sr.seq, ((uint64_t)otype << 56) | (0x0303ull << 40) | ((uint64_t)clen << 24)};
+                alen = 13;
+                ct = rec + 13;
+            }
+            if (lane < 5) {
+                const uint32_t hb[5] = {otype, 3, 3, rlen >> 8, rlen & 0xFF};
+                rec[lane] = (uint8_t)hb[lane];
+            } else if (!is13 && lane < 13) {
+                rec[lane] = (uint8_t)(sr.seq >> (8 * (12 - lane)));
+            }
+            L = gcm_lanes<true>(ks, te, lane & (TLS_TE_COPIES - 1), tabs[wave], t8, nonce, aad,
+                                alen, nullptr, ct, clen, nullptr, 0, a.src + sr.src_off,
+                                sr.plain_len, sr.type, is13);
         }
-        if (lane < 5) {
-            const uint32_t hb[5] = {otype, 3, 3, rlen >> 8, rlen & 0xFF};
-            rec[lane] = (uint8_t)hb[lane];
-        } else if (!is13 && lane < 13) {
-            rec[lane] = (uint8_t)(sr.seq >> (8 * (12 - lane)));
-        }
-        (void)gcm_record<true>(ks, te, lane & (TLS_TE_COPIES - 1), tabs[wave], t8, nonce, aad, alen, nullptr, ct, clen,
-                               nullptr, 0, a.src + sr.src_off, sr.plain_len, sr.type, is13);
+#if TLS_WG_TREE
+        s_acc[wave][lane] = L.acc;
+        __syncthreads();
+        wg_tree(s_acc, tabs);
+        const U128 ghash = s_acc[wave][0];
+#else
+        const U128 ghash = active ? wave_tree(L.acc, tabs[wave]) : U128{0, 0};
+#endif
+        if (active) (void)gcm_finish<true>(L, ghash, nullptr, ct, clen);
     }
 }
 
