@@ -1,6 +1,6 @@
 /*
- * uvhttp_tls_amd.h — batched TLS record open (AES-GCM) on MI355X, ahead of the WebSocket
- * decoder.
+ * uvhttp_tls_amd.h — batched TLS record open (AES-GCM, ChaCha20-Poly1305) on MI355X, ahead of
+ * the WebSocket decoder.
  *
  * What it replaces.  For a TLS connection the reference's WebSocket read callback decrypts
  * with mbedtls before framing: on_websocket_read (src/uvhttp_connection.c:1122-1159) calls
@@ -8,7 +8,8 @@
  * uvhttp_ws_process_data (:1152-1153), closes the WebSocket on PEER_CLOSE_NOTIFY (:1136-1138)
  * and on any other negative return (:1139-1144).  mbedtls (an un-vendored submodule,
  * .gitmodules; absent here) opens each record with the negotiated AEAD — for the TLS 1.2/1.3
- * AES suites, AES-128/256-GCM (NIST SP 800-38D, RFC 5288, RFC 8446 §5.2-5.3).  This surface
+ * AEAD suites, AES-128/256-GCM (NIST SP 800-38D, RFC 5288) and ChaCha20-Poly1305 (RFC 8439,
+ * RFC 7905), TLS 1.3 (RFC 8446 §5.2-5.3) and TLS 1.2.  This surface
  * opens the application-data records of many connections in one device call and leaves each
  * connection's plaintext contiguous in device memory, where uvhttp_ws_gpu_decode_streams
  * (include/uvhttp_ws_amd.h) takes it as its wire stream.
@@ -30,20 +31,21 @@
  *   - at a record whose header fails a check, in this order (the record is counted, with its
  *     status): version != 0x0303 (ERR_VERSION); type not application_data (TLS 1.3) / not
  *     alert, handshake or application_data (TLS 1.2) (ERR_BAD_TYPE); length over the limit
- *     (ERR_OVERFLOW: TLS 1.3 2^14 + 1 inner-plaintext bytes + 16-byte tag; TLS 1.2 2^14 +
- *     8-byte explicit nonce + tag); length below the AEAD overhead (ERR_BAD_MAC: TLS 1.3 16,
- *     TLS 1.2 24).
- * Counted record k of connection s is opened with sequence number seq + k.  TLS 1.3: nonce =
- * iv XOR (0^32 || be64(seq)), AAD = the 5 header bytes, inner plaintext = content || type ||
- * zero padding (type = last non-zero byte; none = ERR_EMPTY).  TLS 1.2 (RFC 5288): nonce =
- * iv[0..3] || the 8 explicit-nonce bytes after the header, AAD = be64(seq) || type ||
- * 0x03 0x03 || be16(plaintext length).  A record is delivered if it authenticates (else
+ *     (ERR_OVERFLOW: 2^14 content bytes (+ 1 inner type byte for TLS 1.3) + the AEAD
+ *     overhead); length below the AEAD overhead (ERR_BAD_MAC).  The overhead is the 16-byte
+ *     tag, plus the 8-byte explicit nonce of TLS 1.2 AES-GCM.
+ * Counted record k of connection s is opened with sequence number seq + k.  Nonce: iv XOR
+ * (0^32 || be64(seq)) for TLS 1.3 and for TLS 1.2 ChaCha20-Poly1305 (RFC 7905); iv[0..3] ||
+ * the 8 explicit-nonce bytes after the header for TLS 1.2 AES-GCM (RFC 5288).  AAD: the 5
+ * header bytes (TLS 1.3); be64(seq) || type || 0x03 0x03 || be16(plaintext length) (TLS 1.2).
+ * TLS 1.3 inner plaintext = content || type || zero padding (type = last non-zero byte; none
+ * = ERR_EMPTY).  A record is delivered if it authenticates (else
  * ERR_BAD_MAC) and its (inner) type is application_data (23), else it is CONTROL.  The first
  * record not delivered stops the connection; the records after it are SKIPPED.
  *
  * Output.  Connection s's delivered content is contiguous at out[out_off, out_off + plain_len)
  * in record order.  out_off is the connection's base in a layout where every counted record
- * reserves its largest possible content (TLS 1.3: length - 17, TLS 1.2: length - 24, never
+ * reserves its largest possible content (length - overhead, - 1 more for TLS 1.3, never
  * below 0), connections in index order from 0; out_cap >= the total wire bytes of the
  * connections always suffices.  Bytes of out outside the delivered ranges are unspecified.
  * The ciphertext in wire is not modified.
@@ -81,16 +83,22 @@ extern "C" {
 #define UVHTTP_TLS_REC_ERR_VERSION (-4)   /* legacy_record_version != 0x0303 */
 #define UVHTTP_TLS_REC_ERR_EMPTY (-5)     /* TLS 1.3 inner plaintext has no content type */
 #define UVHTTP_TLS_REC_ERR_CAPACITY (-6)  /* records / layout exceed records[] or out_cap */
-#define UVHTTP_TLS_REC_ERR_KEY (-7)       /* key slot out of range, or key_len / version invalid
+#define UVHTTP_TLS_REC_ERR_KEY (-7)       /* key slot out of range, or key_len / version / cipher invalid
                                              (connection result only; no record counted) */
+
+/* AEAD of a key slot (uvhttp_tls_key_t.cipher). */
+#define UVHTTP_TLS_CIPHER_AES_GCM 0u            /* AES-128/256-GCM (key_len 16 / 32) */
+#define UVHTTP_TLS_CIPHER_CHACHA20_POLY1305 1u  /* RFC 8439 (key_len 32) */
 
 /* Keys of one connection direction (64 bytes). */
 typedef struct {
-    uint8_t key[32];   /* AES key, key_len bytes used */
-    uint8_t iv[12];    /* TLS 1.3: the write iv; TLS 1.2: salt = iv[0..3], rest ignored */
-    uint32_t key_len;  /* 16 (AES-128-GCM) or 32 (AES-256-GCM) */
+    uint8_t key[32];   /* key_len bytes used */
+    uint8_t iv[12];    /* TLS 1.3 and TLS 1.2 ChaCha20-Poly1305: the write iv (nonce = iv XOR
+                          seq); TLS 1.2 AES-GCM: salt = iv[0..3], rest ignored */
+    uint32_t key_len;  /* 16 or 32 (AES-GCM), 32 (ChaCha20-Poly1305) */
     uint32_t version;  /* UVHTTP_TLS_VERSION_12 or UVHTTP_TLS_VERSION_13 */
-    uint32_t reserved[3];
+    uint32_t cipher;   /* UVHTTP_TLS_CIPHER_* (0 = AES-GCM) */
+    uint32_t reserved[2];
 } uvhttp_tls_key_t;
 
 /* One connection's buffered ciphertext (32 bytes). */
@@ -164,7 +172,7 @@ int uvhttp_tls_gpu_open_records(uvhttp_tls_gpu_engine_t* eng, const uint8_t* wir
                                 void* stream);
 
 /* Seal records (the send side, and the bench's input generator).  Record i: header (type 23
- * for TLS 1.3, `type` for TLS 1.2), TLS 1.2 explicit nonce = be64(seq), ciphertext, tag; the
+ * for TLS 1.3, `type` for TLS 1.2), TLS 1.2 AES-GCM explicit nonce = be64(seq), ciphertext, tag; the
  * TLS 1.3 inner plaintext is content || type with no padding.  Device pointers throughout;
  * records must not overlap src. */
 int uvhttp_tls_gpu_seal_records(uvhttp_tls_gpu_engine_t* eng, const uint8_t* src,

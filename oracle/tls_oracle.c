@@ -5,22 +5,27 @@
  * reference: on_websocket_read (src/uvhttp_connection.c:1122-1159)
  * decrypts every record with mbedtls_ssl_read before uvhttp_ws_process_data sees the bytes.
  * mbedtls itself is an un-vendored submodule (.gitmodules, deps/mbedtls: empty here), so the
- * AEAD it runs for the AES suites is restated from the published standards it implements:
+ * AEADs it runs (AES-GCM, ChaCha20-Poly1305) are restated from the published standards:
  *   aes_*         FIPS-197 (key expansion §5.2, cipher §5.1), byte-oriented, S-box generated
  *   gf_mult       NIST SP 800-38D §6.3 Algorithm 1 (bit-serial multiply in GF(2^128))
  *   gcm_crypt     NIST SP 800-38D §7.1/7.2 with a 96-bit IV (J0 = IV || 0^31 || 1)
- *   tls13_*       RFC 8446 §5.2 (TLSInnerPlaintext, AAD = record header) and §5.3 (nonce)
- *   tls12_*       RFC 5288 §3 (salt || explicit nonce, AAD = seq || type || version || len)
+ *   chacha20_*    RFC 8439 §2.3 (block function)
+ *   poly_*        RFC 8439 §2.5 (Poly1305, plain 130-bit arithmetic)
+ *   chachapoly_*  RFC 8439 §2.8 (AEAD_CHACHA20_POLY1305)
+ *   TLS records   RFC 8446 §5.2 (TLSInnerPlaintext, AAD = record header) and §5.3 (nonce);
+ *                 RFC 5288 §3 (TLS 1.2 AES-GCM: salt || explicit nonce, AAD = seq || type ||
+ *                 version || len); RFC 7905 §2 (TLS 1.2 ChaCha20-Poly1305: iv XOR seq)
  *   oracle_tls_open_batch  the batch contract of include/uvhttp_tls_amd.h (walk, open,
  *                 stop at the first record that is not delivered application data, layout)
  * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg load it; the product
  * library never links or calls anything here.
  *
- * Pinning: FIPS-197 Appendix C.1/C.3 and the GCM specification's test cases
- * (tests/golden/tls_known_answers.json), and records written by a real TLS stack — OpenSSL
- * 3.0.2's libssl in this container, TLS 1.3 and TLS 1.2 AES-GCM sessions over memory BIOs
- * with their keys recovered from the key log (tests/golden/make_tls_vectors.py ->
- * tests/golden/tls_openssl_records.json).  tests/test_tls_oracle.py checks both.
+ * Pinning: FIPS-197 Appendix C.1/C.3, the GCM specification's test cases and RFC 8439's
+ * ChaCha20 / Poly1305 / AEAD test vectors (tests/golden/tls_known_answers.json), and records
+ * written by a real TLS stack — OpenSSL 3.0.2's libssl in this container, TLS 1.3 and TLS 1.2
+ * sessions with AES-GCM and ChaCha20-Poly1305 over memory BIOs, keys recovered from the key
+ * log (tests/golden/make_tls_vectors.py -> tests/golden/tls_openssl_records.json).
+ * tests/test_tls_oracle.py checks both.
  */
 #include <stdint.h>
 #include <stdlib.h>
@@ -192,14 +197,185 @@ int oracle_gcm(const uint8_t* key, int klen, const uint8_t iv[12], const uint8_t
     return 0;
 }
 
-/* ---- TLS records (RFC 8446 §5.2-5.3, RFC 5288 §3) ------------------------------------- */
+/* ---- ChaCha20 and Poly1305 (RFC 8439) ------------------------------------------------ */
+
+static uint32_t rotl32(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+static uint32_t le32(const uint8_t* p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+/* §2.3: the 64-byte block for (key, counter, nonce) */
+static void chacha20_block(const uint8_t key[32], uint32_t counter, const uint8_t nonce[12],
+                           uint8_t out[64]) {
+    uint32_t st[16], x[16];
+    st[0] = 0x61707865, st[1] = 0x3320646e, st[2] = 0x79622d32, st[3] = 0x6b206574;
+    for (int i = 0; i < 8; i++) st[4 + i] = le32(key + 4 * i);
+    st[12] = counter;
+    for (int i = 0; i < 3; i++) st[13 + i] = le32(nonce + 4 * i);
+    memcpy(x, st, sizeof(x));
+#define QR(a, b, c, d)                                                                          \
+    x[a] += x[b], x[d] ^= x[a], x[d] = rotl32(x[d], 16), x[c] += x[d], x[b] ^= x[c],            \
+        x[b] = rotl32(x[b], 12), x[a] += x[b], x[d] ^= x[a], x[d] = rotl32(x[d], 8),           \
+        x[c] += x[d], x[b] ^= x[c], x[b] = rotl32(x[b], 7)
+    for (int r = 0; r < 10; r++) {
+        QR(0, 4, 8, 12), QR(1, 5, 9, 13), QR(2, 6, 10, 14), QR(3, 7, 11, 15);
+        QR(0, 5, 10, 15), QR(1, 6, 11, 12), QR(2, 7, 8, 13), QR(3, 4, 9, 14);
+    }
+#undef QR
+    for (int i = 0; i < 16; i++) {
+        const uint32_t v = x[i] + st[i];
+        out[4 * i] = (uint8_t)v, out[4 * i + 1] = (uint8_t)(v >> 8);
+        out[4 * i + 2] = (uint8_t)(v >> 16), out[4 * i + 3] = (uint8_t)(v >> 24);
+    }
+}
+
+void oracle_chacha20_block(const uint8_t key[32], uint32_t counter, const uint8_t nonce[12],
+                           uint8_t out[64]) {
+    chacha20_block(key, counter, nonce, out);
+}
+
+/* §2.5: Poly1305 with plain 130-bit arithmetic (three 64-bit limbs, 128-bit products) */
+typedef struct {
+    uint64_t r0, r1, s0, s1;
+    uint64_t h0, h1, h2;
+} orc_poly_t;
+
+static void poly_init(orc_poly_t* p, const uint8_t k[32]) {
+    uint64_t r0 = 0, r1 = 0, s0 = 0, s1 = 0;
+    for (int i = 7; i >= 0; i--) {
+        r0 = (r0 << 8) | k[i];
+        r1 = (r1 << 8) | k[8 + i];
+        s0 = (s0 << 8) | k[16 + i];
+        s1 = (s1 << 8) | k[24 + i];
+    }
+    p->r0 = r0 & 0x0ffffffc0fffffffull;  /* clamp: r &= 0x0ffffffc0ffffffc0ffffffc0fffffff */
+    p->r1 = r1 & 0x0ffffffc0ffffffcull;
+    p->s0 = s0, p->s1 = s1;
+    p->h0 = p->h1 = p->h2 = 0;
+}
+
+/* h = (h + n) * r mod 2^130 - 5, n = 16 bytes of m (+ 2^(8 len) : the appended 0x01) */
+static void poly_block(orc_poly_t* p, const uint8_t* m, size_t len) {
+    uint8_t b[17] = {0};
+    memcpy(b, m, len);
+    b[len] = 1;
+    uint64_t n0 = 0, n1 = 0;
+    for (int i = 7; i >= 0; i--) n0 = (n0 << 8) | b[i], n1 = (n1 << 8) | b[8 + i];
+    unsigned __int128 t = (unsigned __int128)p->h0 + n0;
+    uint64_t a0 = (uint64_t)t;
+    t = (t >> 64) + p->h1 + n1;
+    uint64_t a1 = (uint64_t)t;
+    uint64_t a2 = (uint64_t)(t >> 64) + p->h2 + b[16];
+    /* (a2:a1:a0) * (r1:r0): a2 < 8, r < 2^124 */
+    unsigned __int128 m00 = (unsigned __int128)a0 * p->r0;
+    unsigned __int128 m01 = (unsigned __int128)a0 * p->r1;
+    unsigned __int128 m10 = (unsigned __int128)a1 * p->r0;
+    unsigned __int128 m11 = (unsigned __int128)a1 * p->r1;
+    unsigned __int128 m20 = (unsigned __int128)a2 * p->r0;
+    unsigned __int128 m21 = (unsigned __int128)a2 * p->r1;
+    uint64_t d0 = (uint64_t)m00;
+    unsigned __int128 c = (m00 >> 64) + (uint64_t)m01 + (uint64_t)m10;
+    uint64_t d1 = (uint64_t)c;
+    c = (c >> 64) + (m01 >> 64) + (m10 >> 64) + (uint64_t)m11 + (uint64_t)m20;
+    uint64_t d2 = (uint64_t)c;
+    c = (c >> 64) + (m11 >> 64) + (m20 >> 64) + (uint64_t)m21;
+    uint64_t d3 = (uint64_t)c;  /* product < 2^255: fits d3:d2:d1:d0 with (m21 >> 64) == 0 */
+    /* fold: x = lo130 + hi * 2^130 == lo130 + 5 * hi (mod p) */
+    uint64_t l0 = d0, l1 = d1, l2 = d2 & 3;
+    uint64_t h0 = (d2 >> 2) | (d3 << 62), h1 = d3 >> 2;  /* hi = x >> 130 */
+    unsigned __int128 u = (unsigned __int128)l0 + (unsigned __int128)h0 * 5;
+    l0 = (uint64_t)u;
+    u = (u >> 64) + l1 + (unsigned __int128)h1 * 5;
+    l1 = (uint64_t)u;
+    l2 += (uint64_t)(u >> 64);
+    /* once more for the bits above 2^130 (l2 < 2^64 small) */
+    const uint64_t top = l2 >> 2;
+    l2 &= 3;
+    u = (unsigned __int128)l0 + top * 5;
+    l0 = (uint64_t)u;
+    u = (u >> 64) + l1;
+    l1 = (uint64_t)u;
+    l2 += (uint64_t)(u >> 64);
+    p->h0 = l0, p->h1 = l1, p->h2 = l2;
+}
+
+static void poly_finish(orc_poly_t* p, uint8_t tag[16]) {
+    /* full reduction mod p = 2^130 - 5: h < 2^131 here, subtract p while h >= p */
+    for (int k = 0; k < 2; k++) {
+        /* g = h + 5; if g >= 2^130 then h - p = g - 2^130 */
+        unsigned __int128 g = (unsigned __int128)p->h0 + 5;
+        const uint64_t g0 = (uint64_t)g;
+        g = (g >> 64) + p->h1;
+        const uint64_t g1 = (uint64_t)g;
+        const uint64_t g2 = p->h2 + (uint64_t)(g >> 64);
+        if (g2 >= 4) p->h0 = g0, p->h1 = g1, p->h2 = g2 - 4;
+    }
+    unsigned __int128 t = (unsigned __int128)p->h0 + p->s0;
+    const uint64_t t0 = (uint64_t)t;
+    const uint64_t t1 = (uint64_t)((t >> 64) + p->h1 + p->s1);
+    for (int i = 0; i < 8; i++) tag[i] = (uint8_t)(t0 >> (8 * i)), tag[8 + i] = (uint8_t)(t1 >> (8 * i));
+}
+
+void oracle_poly1305(const uint8_t key[32], const uint8_t* m, size_t n, uint8_t tag[16]) {
+    orc_poly_t p;
+    poly_init(&p, key);
+    for (size_t off = 0; off < n; off += 16) poly_block(&p, m + off, n - off < 16 ? n - off : 16);
+    poly_finish(&p, tag);
+}
+
+/* §2.8 AEAD_CHACHA20_POLY1305: encrypt/decrypt in place-safe, tag over AAD || pad || CT || pad
+ * || le64(aad len) || le64(ct len) */
+static void chachapoly_crypt(const uint8_t key[32], const uint8_t nonce[12], const uint8_t* aad,
+                             size_t alen, const uint8_t* in, size_t n, uint8_t* out,
+                             uint8_t tag[16], int decrypt) {
+    uint8_t blk[64], otk[64], lens[16];
+    chacha20_block(key, 0, nonce, otk);
+    orc_poly_t p;
+    poly_init(&p, otk);
+    for (size_t off = 0; off < alen; off += 16) {
+        uint8_t b[16] = {0};
+        memcpy(b, aad + off, alen - off < 16 ? alen - off : 16);
+        poly_block(&p, b, 16);
+    }
+    if (decrypt)
+        for (size_t off = 0; off < n; off += 16) {
+            uint8_t b[16] = {0};
+            memcpy(b, in + off, n - off < 16 ? n - off : 16);
+            poly_block(&p, b, 16);
+        }
+    for (size_t off = 0, c = 1; off < n; off += 64, c++) {
+        chacha20_block(key, (uint32_t)c, nonce, blk);
+        const size_t m = n - off < 64 ? n - off : 64;
+        for (size_t k = 0; k < m; k++) out[off + k] = (uint8_t)(in[off + k] ^ blk[k]);
+    }
+    if (!decrypt)
+        for (size_t off = 0; off < n; off += 16) {
+            uint8_t b[16] = {0};
+            memcpy(b, out + off, n - off < 16 ? n - off : 16);
+            poly_block(&p, b, 16);
+        }
+    for (int i = 0; i < 8; i++) lens[i] = (uint8_t)((uint64_t)alen >> (8 * i)), lens[8 + i] = (uint8_t)((uint64_t)n >> (8 * i));
+    poly_block(&p, lens, 16);
+    poly_finish(&p, tag);
+}
+
+int oracle_chachapoly(const uint8_t key[32], const uint8_t nonce[12], const uint8_t* aad, size_t alen,
+                      const uint8_t* in, size_t n, uint8_t* out, uint8_t tag[16], int decrypt) {
+    uint8_t t[16];
+    chachapoly_crypt(key, nonce, aad, alen, in, n, out, t, decrypt);
+    if (decrypt) return memcmp(t, tag, 16) ? -2 : 0;
+    memcpy(tag, t, 16);
+    return 0;
+}
+
+/* ---- TLS records (RFC 8446 §5.2-5.3, RFC 5288 §3, RFC 7905 §2) ------------------------ */
 
 /* layouts identical to include/uvhttp_tls_amd.h (kept separate: the oracle does not depend
  * on the product's headers) */
 typedef struct {
     uint8_t key[32];
     uint8_t iv[12];
-    uint32_t key_len, version, reserved[3];
+    uint32_t key_len, version, cipher, reserved[2];
 } orc_tls_key_t;
 typedef struct {
     uint64_t begin, len, seq;
@@ -227,84 +403,114 @@ enum {
 };
 #define V12 0x0303u
 #define V13 0x0304u
+#define C_AESGCM 0u
+#define C_CHACHA 1u
 
 static int key_ok(const orc_tls_key_t* k) {
-    return (k->key_len == 16 || k->key_len == 32) && (k->version == V12 || k->version == V13);
+    if (k->version != V12 && k->version != V13) return 0;
+    if (k->cipher == C_AESGCM) return k->key_len == 16 || k->key_len == 32;
+    return k->cipher == C_CHACHA && k->key_len == 32;
 }
 
-/* nonce of record `seq` (RFC 8446 §5.3 / RFC 5288 §3) */
+/* bytes of explicit nonce after the header: TLS 1.2 AES-GCM only (RFC 5288); the TLS 1.2
+ * ChaCha20-Poly1305 nonce is implicit (RFC 7905) */
+static uint32_t explicit_len(const orc_tls_key_t* k) {
+    return k->version == V12 && k->cipher == C_AESGCM ? 8u : 0u;
+}
+
+typedef struct {
+    orc_aes_t aes;
+    const orc_tls_key_t* k;
+} orc_aead_t;
+
+static int aead_init(orc_aead_t* a, const orc_tls_key_t* k) {
+    a->k = k;
+    if (!key_ok(k)) return -1;
+    return k->cipher == C_AESGCM ? aes_setkey(&a->aes, k->key, (int)k->key_len) : 0;
+}
+
+static void aead_crypt(const orc_aead_t* a, const uint8_t nonce[12], const uint8_t* aad,
+                       size_t alen, const uint8_t* in, size_t n, uint8_t* out, uint8_t tag[16],
+                       int decrypt) {
+    if (a->k->cipher == C_AESGCM) gcm_crypt(&a->aes, nonce, aad, alen, in, n, out, tag, decrypt);
+    else chachapoly_crypt(a->k->key, nonce, aad, alen, in, n, out, tag, decrypt);
+}
+
+/* nonce of record `seq`: iv XOR (0^32 || be64(seq)) (TLS 1.3, RFC 8446 §5.3; TLS 1.2
+ * ChaCha20-Poly1305, RFC 7905 §2), or salt || explicit nonce (TLS 1.2 AES-GCM) */
 static void tls_nonce(const orc_tls_key_t* k, uint64_t seq, const uint8_t* explicit8,
                       uint8_t nonce[12]) {
-    if (k->version == V13) {
-        memcpy(nonce, k->iv, 12);
-        for (int b = 0; b < 8; b++) nonce[4 + b] ^= (uint8_t)(seq >> (56 - 8 * b));
-    } else {
+    if (explicit_len(k)) {
         memcpy(nonce, k->iv, 4);
         memcpy(nonce + 4, explicit8, 8);
+    } else {
+        memcpy(nonce, k->iv, 12);
+        for (int b = 0; b < 8; b++) nonce[4 + b] ^= (uint8_t)(seq >> (56 - 8 * b));
     }
 }
 
 /* header checks of the walk, in contract order; returns 0 or the record's status */
-static int header_status(uint32_t version, const uint8_t* h) {
+static int header_status(const orc_tls_key_t* k, const uint8_t* h) {
     const uint32_t type = h[0], ver = ((uint32_t)h[1] << 8) | h[2];
     const uint32_t len = ((uint32_t)h[3] << 8) | h[4];
+    const uint32_t over = explicit_len(k) + 16;
     if (ver != 0x0303) return T_VERSION;
-    if (version == V13 ? type != 23 : (type < 21 || type > 23)) return T_BAD_TYPE;
-    if (len > (version == V13 ? 16384u + 1 + 16 : 16384u + 8 + 16)) return T_OVERFLOW;
-    if (len < (version == V13 ? 16u : 24u)) return T_BAD_MAC;
+    if (k->version == V13 ? type != 23 : (type < 21 || type > 23)) return T_BAD_TYPE;
+    if (len > 16384u + (k->version == V13 ? 1u : 0u) + over) return T_OVERFLOW;
+    if (len < over) return T_BAD_MAC;
     return 0;
 }
 
 /* reserved content bytes of a counted record (largest content it can deliver) */
-static uint64_t record_cap(uint32_t version, uint32_t len) {
-    const uint32_t over = version == V13 ? 17 : 24;
+static uint64_t record_cap(const orc_tls_key_t* k, uint32_t len) {
+    const uint32_t over = explicit_len(k) + 16 + (k->version == V13 ? 1u : 0u);
     return len > over ? len - over : 0;
 }
 
 /* open one complete record whose header passed; writes its content to out (content_len
  * bytes), returns the status, sets *type and *content_len */
-static int open_record(const orc_aes_t* a, const orc_tls_key_t* k, uint64_t seq,
-                       const uint8_t* rec, uint8_t* out, uint8_t* type, uint32_t* content_len) {
+static int open_record(const orc_aead_t* a, uint64_t seq, const uint8_t* rec, uint8_t* out,
+                       uint8_t* type, uint32_t* content_len) {
+    const orc_tls_key_t* k = a->k;
     const uint32_t len = ((uint32_t)rec[3] << 8) | rec[4];
+    const uint32_t ex = explicit_len(k);
+    const uint32_t clen = len - ex - 16;
+    const uint8_t* ct = rec + 5 + ex;
     uint8_t nonce[12], tag[16], aad[13];
+    size_t alen;
     *type = 0;
     *content_len = 0;
+    tls_nonce(k, seq, rec + 5, nonce);
     if (k->version == V13) {
-        const uint32_t clen = len - 16;
-        uint8_t* inner = (uint8_t*)malloc(clen ? clen : 1);
-        tls_nonce(k, seq, NULL, nonce);
-        gcm_crypt(a, nonce, rec, 5, rec + 5, clen, inner, tag, 1);
-        if (memcmp(tag, rec + 5 + clen, 16)) {
-            free(inner);
-            return T_BAD_MAC;
-        }
-        uint32_t i = clen;
-        while (i > 0 && inner[i - 1] == 0) i--;
-        if (i == 0) {
-            free(inner);
-            return T_EMPTY;
-        }
-        *type = inner[i - 1];
-        *content_len = i - 1;
-        memcpy(out, inner, i - 1);
-        free(inner);
+        memcpy(aad, rec, 5);
+        alen = 5;
     } else {
-        const uint32_t clen = len - 24;
-        tls_nonce(k, seq, rec + 5, nonce);
         put_be64(aad, seq);
         aad[8] = rec[0], aad[9] = 3, aad[10] = 3;
         aad[11] = (uint8_t)(clen >> 8), aad[12] = (uint8_t)clen;
-        uint8_t* plain = (uint8_t*)malloc(clen ? clen : 1);
-        gcm_crypt(a, nonce, aad, 13, rec + 13, clen, plain, tag, 1);
-        if (memcmp(tag, rec + 13 + clen, 16)) {
+        alen = 13;
+    }
+    uint8_t* plain = (uint8_t*)malloc(clen ? clen : 1);
+    aead_crypt(a, nonce, aad, alen, ct, clen, plain, tag, 1);
+    if (memcmp(tag, ct + clen, 16)) {
+        free(plain);
+        return T_BAD_MAC;
+    }
+    if (k->version == V13) {
+        uint32_t i = clen;
+        while (i > 0 && plain[i - 1] == 0) i--;
+        if (i == 0) {
             free(plain);
-            return T_BAD_MAC;
+            return T_EMPTY;
         }
+        *type = plain[i - 1];
+        *content_len = i - 1;
+    } else {
         *type = rec[0];
         *content_len = clen;
-        memcpy(out, plain, clen);
-        free(plain);
     }
+    memcpy(out, plain, *content_len);
+    free(plain);
     return *type == 23 ? T_OK : T_CONTROL;
 }
 
@@ -316,17 +522,17 @@ static void walk_stream(const uint8_t* wire, uint64_t wire_len, const orc_tls_st
     *cap = 0;
     *key_bad = st->key >= n_keys || !key_ok(&keys[st->key]);
     if (*key_bad) return;
-    const uint32_t version = keys[st->key].version;
+    const orc_tls_key_t* k = &keys[st->key];
     const uint64_t L = st->begin + st->len <= wire_len ? st->len : 0;
     const uint8_t* p = wire + st->begin;
     uint64_t pos = 0;
     while (L - pos >= 5) {
-        const int hs = header_status(version, p + pos);
+        const int hs = header_status(k, p + pos);
         const uint32_t len = ((uint32_t)p[pos + 3] << 8) | p[pos + 4];
         if (!hs && L - pos - 5 < len) break;  /* incomplete: waits for more bytes */
         ++*n_rec;
         if (hs) break;
-        *cap += record_cap(version, len);
+        *cap += record_cap(k, len);
         pos += 5 + (uint64_t)len;
     }
 }
@@ -376,8 +582,8 @@ uint64_t oracle_tls_open_batch(const uint8_t* wire, uint64_t wire_len, const orc
             continue;
         }
         const orc_tls_key_t* k = &keys[st->key];
-        orc_aes_t a;
-        aes_setkey(&a, k->key, (int)k->key_len);
+        orc_aead_t a;
+        aead_init(&a, k);
         const uint8_t* p = wire + st->begin;
         uint64_t pos = 0, plain = 0;
         int stopped = 0;
@@ -390,12 +596,12 @@ uint64_t oracle_tls_open_batch(const uint8_t* wire, uint64_t wire_len, const orc
             if (stopped) {
                 rec->status = T_SKIPPED;
             } else {
-                int status = header_status(k->version, p + pos);
+                int status = header_status(k, p + pos);
                 if (!status) {
                     uint8_t type;
                     uint32_t clen;
-                    status = open_record(&a, k, st->seq + j, p + pos, out + out_base + plain,
-                                         &type, &clen);
+                    status = open_record(&a, st->seq + j, p + pos, out + out_base + plain, &type,
+                                         &clen);
                     rec->type = type;
                     rec->content_len = clen;
                 }
@@ -422,51 +628,48 @@ uint64_t oracle_tls_open_batch(const uint8_t* wire, uint64_t wire_len, const orc
 }
 
 /* Seal one record (send side / test-data generator): returns its length, or 0 on bad input.
- * TLS 1.3: outer type 23, inner = content || type (no padding) + `pad` zero bytes;
- * TLS 1.2: outer type = type, explicit nonce = be64(seq). */
+ * TLS 1.3: outer type 23, inner = content || type + `pad` zero bytes; TLS 1.2: outer type =
+ * type, AES-GCM explicit nonce = be64(seq). */
 uint64_t oracle_tls_seal_record(const orc_tls_key_t* k, uint64_t seq, uint8_t type,
                                 const uint8_t* content, uint32_t n, uint32_t pad, uint8_t* rec) {
-    orc_aes_t a;
-    if (!key_ok(k) || aes_setkey(&a, k->key, (int)k->key_len)) return 0;
+    orc_aead_t a;
+    if (aead_init(&a, k)) return 0;
+    const uint32_t ex = explicit_len(k);
+    const uint32_t clen = k->version == V13 ? n + 1 + pad : n;
+    const uint32_t len = ex + clen + 16;
+    if (len > 0xFFFF) return 0;
     uint8_t nonce[12], aad[13];
+    rec[0] = k->version == V13 ? 23 : type, rec[1] = 3, rec[2] = 3;
+    rec[3] = (uint8_t)(len >> 8), rec[4] = (uint8_t)len;
+    if (ex) put_be64(rec + 5, seq);
+    uint8_t* ct = rec + 5 + ex;
+    memmove(ct, content, n);
     if (k->version == V13) {
-        const uint32_t clen = n + 1 + pad;
-        if (clen + 16 > 0xFFFF) return 0;
-        rec[0] = 23, rec[1] = 3, rec[2] = 3;
-        rec[3] = (uint8_t)((clen + 16) >> 8), rec[4] = (uint8_t)(clen + 16);
-        uint8_t* inner = rec + 5;
-        memmove(inner, content, n);
-        inner[n] = type;
-        memset(inner + n + 1, 0, pad);
-        tls_nonce(k, seq, NULL, nonce);
-        gcm_crypt(&a, nonce, rec, 5, inner, clen, inner, inner + clen, 0);
-        return 5 + (uint64_t)clen + 16;
+        ct[n] = type;
+        memset(ct + n + 1, 0, pad);
+        memcpy(aad, rec, 5);
+    } else {
+        put_be64(aad, seq);
+        aad[8] = type, aad[9] = 3, aad[10] = 3, aad[11] = (uint8_t)(n >> 8), aad[12] = (uint8_t)n;
     }
-    if (n + 24 > 0xFFFF) return 0;
-    rec[0] = type, rec[1] = 3, rec[2] = 3;
-    rec[3] = (uint8_t)((n + 24) >> 8), rec[4] = (uint8_t)(n + 24);
-    put_be64(rec + 5, seq);
     tls_nonce(k, seq, rec + 5, nonce);
-    put_be64(aad, seq);
-    aad[8] = type, aad[9] = 3, aad[10] = 3, aad[11] = (uint8_t)(n >> 8), aad[12] = (uint8_t)n;
-    memmove(rec + 13, content, n);
-    gcm_crypt(&a, nonce, aad, 13, rec + 13, n, rec + 13, rec + 13 + n, 0);
-    return 13 + (uint64_t)n + 16;
+    aead_crypt(&a, nonce, aad, k->version == V13 ? 5 : 13, ct, clen, ct, ct + clen, 0);
+    return 5 + (uint64_t)len;
 }
 
 /* CPU baseline: open `n` complete TLS records laid out back to back (one connection, one
  * key, sequence numbers from seq); returns the content bytes delivered */
 uint64_t oracle_tls_open_stream_bytes(const orc_tls_key_t* k, uint64_t seq, const uint8_t* wire,
                                       uint64_t len, uint8_t* out) {
-    orc_aes_t a;
-    if (!key_ok(k) || aes_setkey(&a, k->key, (int)k->key_len)) return 0;
+    orc_aead_t a;
+    if (aead_init(&a, k)) return 0;
     uint64_t pos = 0, plain = 0;
     while (len - pos >= 5) {
         const uint32_t rl = ((uint32_t)wire[pos + 3] << 8) | wire[pos + 4];
-        if (header_status(k->version, wire + pos) || len - pos - 5 < rl) break;
+        if (header_status(k, wire + pos) || len - pos - 5 < rl) break;
         uint8_t type;
         uint32_t clen;
-        if (open_record(&a, k, seq++, wire + pos, out + plain, &type, &clen) != T_OK) break;
+        if (open_record(&a, seq++, wire + pos, out + plain, &type, &clen) != T_OK) break;
         plain += clen;
         pos += 5 + (uint64_t)rl;
     }

@@ -221,7 +221,7 @@ def build_frame(payload: bytes, opcode, mask, fin, key=b"\x00\x00\x00\x00", cap=
 # ---- TLS record layer (oracle/tls_oracle.c), layouts of include/uvhttp_tls_amd.h ----------
 
 TLS_KEY_DT = np.dtype([("key", "u1", 32), ("iv", "u1", 12), ("key_len", "<u4"),
-                       ("version", "<u4"), ("reserved", "<u4", 3)])
+                       ("version", "<u4"), ("cipher", "<u4"), ("reserved", "<u4", 2)])
 TLS_STREAM_DT = np.dtype([("begin", "<u8"), ("len", "<u8"), ("seq", "<u8"), ("key", "<u4"),
                           ("reserved", "<u4")])
 TLS_RECORD_DT = np.dtype([("rec_off", "<u8"), ("out_off", "<u8"), ("content_len", "<u4"),
@@ -239,6 +239,7 @@ assert TLS_RECORD_DT.itemsize == 32 and TLS_RESULT_DT.itemsize == 64
 assert TLS_SEAL_DT.itemsize == 32
 
 TLS12, TLS13 = 0x0303, 0x0304
+AES_GCM, CHACHA = 0, 1
 REC_OK, REC_SKIPPED, REC_CONTROL = 0, 2, 3
 REC_OVERFLOW, REC_BAD_MAC, REC_BAD_TYPE, REC_VERSION = -1, -2, -3, -4
 REC_EMPTY, REC_CAPACITY, REC_KEY = -5, -6, -7
@@ -254,6 +255,9 @@ def _tls_sigs(L):
         ("oracle_tls_open_batch", u64, [vp, u64, vp, u32, vp, u32, vp, u32, vp, vp, u64]),
         ("oracle_tls_seal_record", u64, [vp, u64, C.c_uint8, vp, u32, u32, vp]),
         ("oracle_tls_open_stream_bytes", u64, [vp, u64, vp, u64, vp]),
+        ("oracle_chacha20_block", None, [vp, u32, vp, vp]),
+        ("oracle_poly1305", None, [vp, vp, sz, vp]),
+        ("oracle_chachapoly", C.c_int, [vp, vp, vp, sz, vp, sz, vp, vp, C.c_int]),
     ]:
         fn = getattr(L, name)
         fn.restype, fn.argtypes = res, args
@@ -283,13 +287,41 @@ def gcm(key: bytes, iv: bytes, aad: bytes, data: bytes, tag: bytes = None, decry
     return bytes(out)[:len(data)], bytes(t)
 
 
-def tls_key(key: bytes, iv: bytes, version):
+def tls_key(key: bytes, iv: bytes, version, cipher=AES_GCM):
     k = np.zeros(1, TLS_KEY_DT)
     k[0]["key"][:len(key)] = np.frombuffer(key, np.uint8)
     k[0]["iv"][:] = np.frombuffer(iv.ljust(12, b"\0"), np.uint8)
     k[0]["key_len"] = len(key)
     k[0]["version"] = version
+    k[0]["cipher"] = cipher
     return k
+
+
+def chacha20_block(key: bytes, counter: int, nonce: bytes) -> bytes:
+    L = _tls_sigs(load())
+    out = (C.c_uint8 * 64)()
+    L.oracle_chacha20_block(_buf(key), counter, _buf(nonce), out)
+    return bytes(out)
+
+
+def poly1305(key: bytes, msg: bytes) -> bytes:
+    L = _tls_sigs(load())
+    out = (C.c_uint8 * 16)()
+    L.oracle_poly1305(_buf(key), _buf(msg), len(msg), out)
+    return bytes(out)
+
+
+def chachapoly(key: bytes, nonce: bytes, aad: bytes, data: bytes, tag: bytes = None,
+               decrypt=False):
+    """AEAD_CHACHA20_POLY1305: encrypt -> (ct, tag); decrypt -> (rc, pt)"""
+    L = _tls_sigs(load())
+    out = (C.c_uint8 * max(1, len(data)))()
+    t = _buf(tag or bytes(16))
+    rc = L.oracle_chachapoly(_buf(key), _buf(nonce), _buf(aad), len(aad), _buf(data), len(data),
+                             out, t, 1 if decrypt else 0)
+    if decrypt:
+        return rc, bytes(out)[:len(data)]
+    return bytes(out)[:len(data)], bytes(t)
 
 
 def tls_seal(keyrec, seq, type_, content: bytes, pad=0) -> bytes:

@@ -5,7 +5,8 @@ Runs in the build container only (not on the GPU box, not by the tests): drives 
 memory BIOs — a client and a server in one process, a throw-away self-signed P-256 certificate
 made with the `openssl` CLI — and captures the client -> server bytes after the handshake:
 application-data records of several sizes (a write over 2^14 bytes spans two records), and
-the encrypted close_notify alert at the end.  The read keys are recovered from OpenSSL's key
+the encrypted close_notify alert at the end — TLS 1.3 and TLS 1.2, AES-GCM and
+ChaCha20-Poly1305.  The read keys are recovered from OpenSSL's key
 log (TLS 1.3: CLIENT_TRAFFIC_SECRET_0 -> HKDF-Expand-Label "key"/"iv", RFC 8446 §7.1/7.3;
 TLS 1.2: CLIENT_RANDOM master secret -> PRF "key expansion" key block, RFC 5246 §6.3), so the
 fixture pins the record layer of tls_oracle.c (nonce, AAD, inner plaintext, padding) against
@@ -92,7 +93,7 @@ def prf(secret, label, seed, length, h):
     return out[:length]
 
 
-def session(version, suite, klen, h, writes, padding=0):
+def session(version, suite, klen, h, writes, padding=0, cipher=0):
     tmp = tempfile.mkdtemp()
     cert, key = os.path.join(tmp, "c.pem"), os.path.join(tmp, "k.pem")
     subprocess.run(["openssl", "req", "-x509", "-newkey", "ec", "-pkeyopt",
@@ -173,15 +174,16 @@ def session(version, suite, klen, h, writes, padding=0):
         seq0 = 0
     else:
         ms = bytes.fromhex(kl["CLIENT_RANDOM"][2])
-        kb = prf(ms, b"key expansion", sr.raw + cr.raw, 2 * klen + 8, h)
-        wkey, wiv = kb[:klen], kb[2 * klen:2 * klen + 4] + bytes(8)
+        ivlen = 12 if cipher else 4  # ChaCha20-Poly1305: 12-byte fixed iv (RFC 7905)
+        kb = prf(ms, b"key expansion", sr.raw + cr.raw, 2 * klen + 2 * ivlen, h)
+        wkey, wiv = kb[:klen], (kb[2 * klen:2 * klen + ivlen] + bytes(12))[:12]
         seq0 = 1  # seq 0 was the client's Finished
     ssl.SSL_free(cli)  # frees its BIOs
     ssl.SSL_free(srv)
     ssl.SSL_CTX_free(sctx)
     ssl.SSL_CTX_free(cctx)
     return {
-        "version": version, "suite": suite_name,
+        "version": version, "suite": suite_name, "cipher": cipher,
         "key": wkey.hex(), "iv": wiv.hex(), "seq": seq0, "padding": padding,
         "writes": writes, "wire_b64": base64.b64encode(wire).decode(),
         "plaintext_len": len(got), "plaintext_sha256": hashlib.sha256(got).hexdigest(),
@@ -197,6 +199,8 @@ def main():
         session(0x0304, "TLS_AES_128_GCM_SHA256", 16, hashlib.sha256, writes, padding=256),
         session(0x0303, "ECDHE-ECDSA-AES128-GCM-SHA256", 16, hashlib.sha256, writes),
         session(0x0303, "ECDHE-ECDSA-AES256-GCM-SHA384", 32, hashlib.sha384, writes),
+        session(0x0304, "TLS_CHACHA20_POLY1305_SHA256", 32, hashlib.sha256, writes, cipher=1),
+        session(0x0303, "ECDHE-ECDSA-CHACHA20-POLY1305", 32, hashlib.sha256, writes, cipher=1),
     ]
     with open(OUT, "w") as f:
         json.dump({"generator": "tests/golden/make_tls_vectors.py",
