@@ -1,7 +1,8 @@
 """TLS record open / seal on the MI355X against the CPU oracle
 (oracle/tls_oracle.c): OpenSSL-written sessions, randomized multi-connection batches with every
 stop rule of include/uvhttp_tls_amd.h, device seal vs oracle seal byte for byte, and a large
-seal -> open round trip.  Bit-exact: records, connection results and the delivered plaintext."""
+seal -> open round trip — AES-128/256-GCM and ChaCha20-Poly1305, TLS 1.3 and 1.2.  Bit-exact:
+records, connection results and the delivered plaintext."""
 import base64
 import hashlib
 import json
@@ -72,12 +73,14 @@ def _sessions():
 
 
 def test_openssl_sessions(torch, eng):
-    """Every OpenSSL session alone, then all five in one batch (five keys, both versions)."""
+    """Every OpenSSL session alone, then all seven in one batch (seven keys: both versions,
+    AES-GCM and ChaCha20-Poly1305)."""
     wires, keys, sts = [], [], []
     base = 0
     for i, s in enumerate(_sessions()):
         w = np.frombuffer(base64.b64decode(s["wire_b64"]), np.uint8)
-        k = O.tls_key(bytes.fromhex(s["key"]), bytes.fromhex(s["iv"]), s["version"])
+        k = O.tls_key(bytes.fromhex(s["key"]), bytes.fromhex(s["iv"]), s["version"],
+                      s.get("cipher", 0))
         st = np.zeros(1, O.TLS_STREAM_DT)
         st[0]["len"], st[0]["seq"] = w.size, s["seq"]
         _, so, oo = check(torch, eng, w, k, st)
@@ -92,10 +95,16 @@ def test_openssl_sessions(torch, eng):
     check(torch, eng, np.concatenate(wires), np.concatenate(keys), np.concatenate(sts))
 
 
+def _key_set(rng):
+    """AES-128-GCM, AES-256-GCM, ChaCha20-Poly1305 x TLS 1.3, TLS 1.2"""
+    return np.concatenate([O.tls_key(rng.randbytes(kl), rng.randbytes(12), v, c)
+                           for kl, c in ((16, O.AES_GCM), (32, O.AES_GCM), (32, O.CHACHA))
+                           for v in (O.TLS13, O.TLS12)])
+
+
 def _random_batch(seed, n_streams, sizes, faults=True):
     rng = random.Random(seed)
-    keys = np.concatenate([O.tls_key(rng.randbytes(kl), rng.randbytes(12), v)
-                           for kl in (16, 32) for v in (O.TLS13, O.TLS12)])
+    keys = _key_set(rng)
     wire, st = bytearray(), np.zeros(n_streams, O.TLS_STREAM_DT)
     for s in range(n_streams):
         k = rng.randrange(len(keys))
@@ -131,6 +140,8 @@ def test_key_and_capacity_errors(torch, eng):
     wire, keys, st = _random_batch(77, 20, [50, 500], faults=False)
     keys[1]["key_len"] = 24      # invalid key length
     keys[2]["version"] = 0x0302  # invalid version
+    keys[5]["key_len"] = 16      # ChaCha20-Poly1305 with a 16-byte key
+    keys[4]["cipher"] = 7        # unknown cipher
     st[3]["key"] = 99            # slot out of range
     check(torch, eng, wire, keys, st)
     n = int(O.tls_open_batch(wire, keys, st)[1]["n_records"].sum())
@@ -148,8 +159,7 @@ def _seal_dev(torch, eng, src, descs, keys, out_bytes):
 
 def test_seal_matches_oracle(torch, eng):
     rng = random.Random(9)
-    keys = np.concatenate([O.tls_key(rng.randbytes(kl), rng.randbytes(12), v)
-                           for kl in (16, 32) for v in (O.TLS13, O.TLS12)])
+    keys = _key_set(rng)
     src = np.frombuffer(rng.randbytes(1 << 18), np.uint8)
     sizes = [0, 1, 15, 16, 17, 100, 1023, 4096, 16383, 16384]
     n = 200
@@ -176,8 +186,9 @@ def test_seal_open_roundtrip_large(torch, eng):
     t = torch
     rng = random.Random(21)
     n_conn, per = 4096, 4
-    keys = np.concatenate([O.tls_key(rng.randbytes(16 if i % 2 else 32), rng.randbytes(12),
-                                     O.TLS13 if i % 3 else O.TLS12) for i in range(n_conn)])
+    keys = np.concatenate([O.tls_key(rng.randbytes(16 if i % 2 and i % 5 else 32), rng.randbytes(12),
+                                     O.TLS13 if i % 3 else O.TLS12,
+                                     O.AES_GCM if i % 5 else O.CHACHA) for i in range(n_conn)])
     plen = 16384
     src = t.randint(0, 256, (n_conn * per * plen,), dtype=t.uint8, device="cuda")
     descs = np.zeros(n_conn * per, O.TLS_SEAL_DT)
@@ -185,7 +196,7 @@ def test_seal_open_roundtrip_large(torch, eng):
     off = 0
     for c in range(n_conn):
         v = int(keys[c]["version"])
-        rl = 5 + plen + 16 + (1 if v == O.TLS13 else 8)
+        rl = 5 + plen + 16 + (1 if v == O.TLS13 else 8 if keys[c]["cipher"] == O.AES_GCM else 0)
         st[c] = (off, rl * per, 1000 + c, c, 0)
         for j in range(per):
             i = c * per + j

@@ -4,8 +4,8 @@ reference (src/uvhttp_connection.c:1122-1159: mbedtls_ssl_read, then uvhttp_ws_p
 each decrypted chunk) for many connections in two device calls.
 
 Each connection's client WebSocket frames are cut into TLS records at random points (frames
-straddle records), sealed with the CPU oracle under its own key (TLS 1.3 and 1.2, AES-128 and
-AES-256), and the ciphertext may end inside a record.  The device opens the records; each
+straddle records), sealed with the CPU oracle under its own key (TLS 1.3 and 1.2, AES-128-GCM,
+AES-256-GCM and ChaCha20-Poly1305), and the ciphertext may end inside a record.  The device opens the records; each
 connection's plaintext (contiguous at its out_off) is handed as that connection's wire stream
 to uvhttp_ws_gpu_decode_streams; uvhttp_ws_deliver_stream replays the callbacks.  The oracle
 side: tls_oracle.c opens the same records and oracle process_data decodes the plaintext.  Both
@@ -51,8 +51,9 @@ def test_tls_then_websocket(torch, seed):
     t = torch
     rng = random.Random(4242 + seed)
     n_conn = [6, 40, 120][seed]
-    keys = np.concatenate([O.tls_key(rng.randbytes(rng.choice([16, 32])), rng.randbytes(12),
-                                     rng.choice([O.TLS13, O.TLS12])) for _ in range(n_conn)])
+    ciphers = [(16, O.AES_GCM), (32, O.AES_GCM), (32, O.CHACHA)]
+    keys = np.concatenate([O.tls_key(rng.randbytes(kl), rng.randbytes(12), rng.choice([O.TLS13, O.TLS12]), c)
+                           for kl, c in (rng.choice(ciphers) for _ in range(n_conn))])
     wire, st = bytearray(), np.zeros(n_conn, O.TLS_STREAM_DT)
     for c in range(n_conn):
         plain = _ws_frames(rng, rng.randint(0, 12))

@@ -3,15 +3,18 @@
 
 Workload: `--conns` connections, each with `--records` application-data records of `--plen`
 content bytes (default 65 536 x 4 x 16 KiB: 64 KiB of plaintext per connection, the C3 shape),
-TLS 1.3 (or --version 12), AES-128-GCM (or --klen 32), one key per connection.  The records
+TLS 1.3 (or --version 12), AES-128-GCM (or --klen 32, or --cipher chacha: ChaCha20-Poly1305),
+one key per connection.  The records
 are sealed on the device (uvhttp_tls_gpu_seal_records), then each timed step opens all of them
 (uvhttp_tls_gpu_open_records: key schedules, walk, crypto, finalize) with inputs resident in
 HBM.  Prints one JSON line: plaintext GiB/s per step, the crypto kernel's time (HIP events),
 its bytes moved (ciphertext read + plaintext written), and two single-core CPU baselines on a
 bounded sample: the oracle restatement (byte-oriented C, the parity checker) and OpenSSL 3.0
-EVP AES-GCM from the system libcrypto (AES-NI + PCLMUL: what a production CPU stack does).
+EVP AES-GCM / ChaCha20-Poly1305 from the system libcrypto (AES-NI + PCLMUL / AVX2: what a
+production CPU stack does).
 
     python tools/bench_tls.py [--conns N] [--records R] [--plen P] [--version 13|12] [--klen 16|32]
+                              [--cipher aes|chacha]
 """
 import argparse
 import ctypes as C
@@ -28,8 +31,8 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 GIB = float(1 << 30)
 
 
-def openssl_baseline(keyrec, seq, wire, n_rec, rlen, version, seconds):
-    """OpenSSL EVP AES-GCM decrypt of the same records, 1 thread (libcrypto.so.3)."""
+def openssl_baseline(keyrec, seq, wire, n_rec, rlen, version, seconds, chacha=False):
+    """OpenSSL EVP AEAD decrypt of the same records, 1 thread (libcrypto.so.3)."""
     try:
         L = C.CDLL("libcrypto.so.3")
     except OSError:
@@ -37,6 +40,7 @@ def openssl_baseline(keyrec, seq, wire, n_rec, rlen, version, seconds):
     vp, ip = C.c_void_p, C.c_int
     for name, res, args in [("EVP_CIPHER_CTX_new", vp, []), ("EVP_CIPHER_CTX_free", None, [vp]),
                             ("EVP_aes_128_gcm", vp, []), ("EVP_aes_256_gcm", vp, []),
+                            ("EVP_chacha20_poly1305", vp, []),
                             ("EVP_DecryptInit_ex", ip, [vp, vp, vp, vp, vp]),
                             ("EVP_DecryptUpdate", ip, [vp, vp, C.POINTER(ip), vp, ip]),
                             ("EVP_DecryptFinal_ex", ip, [vp, vp, C.POINTER(ip)]),
@@ -46,7 +50,8 @@ def openssl_baseline(keyrec, seq, wire, n_rec, rlen, version, seconds):
     klen = int(keyrec["key_len"])
     key = bytes(keyrec["key"][:klen])
     iv = bytes(keyrec["iv"])
-    cipher = L.EVP_aes_128_gcm() if klen == 16 else L.EVP_aes_256_gcm()
+    cipher = (L.EVP_chacha20_poly1305() if chacha else
+              L.EVP_aes_128_gcm() if klen == 16 else L.EVP_aes_256_gcm())
     ctx = L.EVP_CIPHER_CTX_new()
     out = C.create_string_buffer(rlen)
     outl = ip(0)
@@ -59,6 +64,10 @@ def openssl_baseline(keyrec, seq, wire, n_rec, rlen, version, seconds):
             if version == 0x0304:
                 nonce = bytes(a ^ b for a, b in zip(iv, bytes(4) + s.to_bytes(8, "big")))
                 aad, ct = rec[:5], rec[5:5 + rlen - 16]
+            elif chacha:  # RFC 7905: implicit nonce
+                nonce = bytes(a ^ b for a, b in zip(iv, bytes(4) + s.to_bytes(8, "big")))
+                ct = rec[5:5 + rlen - 16]
+                aad = s.to_bytes(8, "big") + rec[:3] + len(ct).to_bytes(2, "big")
             else:
                 nonce = iv[:4] + rec[5:13]
                 ct = rec[13:5 + rlen - 16]
@@ -84,6 +93,7 @@ def main():
     ap.add_argument("--plen", type=int, default=16384)
     ap.add_argument("--version", type=int, default=13, choices=[12, 13])
     ap.add_argument("--klen", type=int, default=16, choices=[16, 32])
+    ap.add_argument("--cipher", default="aes", choices=["aes", "chacha"])
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--cpu-seconds", type=float, default=4.0)
@@ -101,8 +111,12 @@ def main():
     keys = np.zeros(n, O.TLS_KEY_DT)
     keys["key"] = rng.integers(0, 256, (n, 32), dtype=np.uint8)
     keys["iv"] = rng.integers(0, 256, (n, 12), dtype=np.uint8)
-    keys["key_len"], keys["version"] = args.klen, ver
-    rlen = plen + 16 + (1 if ver == 0x0304 else 8)  # TLSCiphertext.length
+    chacha = args.cipher == "chacha"
+    keys["key_len"], keys["version"] = (32 if chacha else args.klen), ver
+    keys["cipher"] = O.CHACHA if chacha else O.AES_GCM
+    # TLSCiphertext.length: content + tag + (TLS 1.3 type byte | TLS 1.2 AES-GCM explicit nonce)
+    rlen = plen + 16 + (1 if ver == 0x0304 else 0 if chacha else 8)
+    aead = "ChaCha20-Poly1305" if chacha else f"AES-{args.klen * 8}-GCM"
     stride = 5 + rlen
     idx = np.arange(n * per, dtype=np.uint64)
     seals = np.zeros(n * per, O.TLS_SEAL_DT)
@@ -156,9 +170,9 @@ def main():
         "metric": "TLS record open GiB/s (device-resident)", "value": round(plain * args.steps / el / GIB, 2),
         "unit": "GiB/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(el / args.steps * 1e3, 4), "higher_is_better": True,
-        "dtype": "u8/u32 (AES-GCM)", "data": "synthetic (random plaintext sealed on the device)",
+        "dtype": "u8/u32 (ChaCha20-Poly1305)" if chacha else "u8/u32 (AES-GCM)", "data": "synthetic (random plaintext sealed on the device)",
         "config": {"workload": f"{n} connections x {per} x {plen} B TLS 1.{args.version % 10} "
-                               f"AES-{args.klen * 8}-GCM records", "conns": n, "records": per,
+                               f"{aead} records", "conns": n, "records": per,
                    "plen": plen},
         "kernel": {"name": "k_tls_open", "avg_us": round(kus, 2),
                    "plaintext_gbs": round(plain / (kus * 1e-6) / 1e9, 1),
@@ -178,7 +192,7 @@ def main():
         line["cpu_baseline"] = {
             "oracle": {"value": round(done / el1 / GIB, 4), "unit": "GiB/s", "cores": 1,
                        "kind": "port", "sample": f"{m} records of connection 0, {el1:.1f} s"},
-            "openssl": openssl_baseline(keys[0], 0, sample, m, rlen, ver, args.cpu_seconds),
+            "openssl": openssl_baseline(keys[0], 0, sample, m, rlen, ver, args.cpu_seconds, chacha),
         }
     print(json.dumps(line))
 

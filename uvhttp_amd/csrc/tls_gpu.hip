@@ -1,4 +1,5 @@
-// tls_gpu.hip — batched TLS record open / seal (AES-128/256-GCM) for gfx950 (MI355X).
+// tls_gpu.hip — batched TLS record open / seal (AES-128/256-GCM, ChaCha20-Poly1305) for
+// gfx950 (MI355X).
 //
 // the record decrypt that runs ahead of the WebSocket decoder in the
 // reference (mbedtls_ssl_read in on_websocket_read, src/uvhttp_connection.c:1122-1159).  The
@@ -60,8 +61,6 @@ constexpr int kCryptWaves = kCryptWG / 64;
 #define CRYPT_ATTR __launch_bounds__(kCryptWG)
 #endif
 constexpr uint32_t kTeShift = TLS_TE_COPIES == 32 ? 5 : TLS_TE_COPIES == 16 ? 4 : 3;
-constexpr uint32_t kMaxLen13 = 16384 + 1 + 16;  // TLSCiphertext.length limits
-constexpr uint32_t kMaxLen12 = 16384 + 8 + 16;
 
 struct U128 {  // a GCM block as a big-endian 128-bit value (bit 0 of the spec = MSB of hi)
     uint64_t hi, lo;
@@ -69,12 +68,13 @@ struct U128 {  // a GCM block as a big-endian 128-bit value (bit 0 of the spec =
 
 // Per key slot, built by k_tls_keys (2 KiB).
 struct __attribute__((aligned(64))) KeySched {
-    U128 tab[7][16];   // 4-bit Shoup tables of H^(2^k), k = 0..6
-    uint32_t rk[60];   // FIPS-197 round-key words, big-endian
-    uint32_t nr;       // 10 / 14; 0 = invalid key
+    U128 tab[7][16];   // AES-GCM: 4-bit Shoup tables of H^(2^k), k = 0..6
+    uint32_t rk[60];   // AES: FIPS-197 round-key words, big-endian; ChaCha20: key words [0..7], LE
+    uint32_t nr;       // 10 / 14 (AES), 20 (ChaCha20); 0 = invalid key
     uint32_t version;  // UVHTTP_TLS_VERSION_12 / _13
-    uint32_t iv[3];    // iv as big-endian words
-    uint32_t pad[11];
+    uint32_t iv[3];    // AES-GCM: iv as big-endian words; ChaCha20: little-endian words
+    uint32_t cipher;   // UVHTTP_TLS_CIPHER_*
+    uint32_t pad[10];
 };
 static_assert(sizeof(KeySched) == 2112, "key schedule layout");
 
@@ -280,18 +280,40 @@ __global__ void k_tls_te0(uint32_t* te0) {
     }
 }
 
-// key slot -> round keys, H = E(K, 0^128), tables of H^(2^k); one lane per slot
+__device__ inline bool key_valid(const uvhttp_tls_key_t& k) {
+    if (k.version != UVHTTP_TLS_VERSION_12 && k.version != UVHTTP_TLS_VERSION_13) return false;
+    if (k.cipher == UVHTTP_TLS_CIPHER_AES_GCM) return k.key_len == 16 || k.key_len == 32;
+    return k.cipher == UVHTTP_TLS_CIPHER_CHACHA20_POLY1305 && k.key_len == 32;
+}
+
+// explicit nonce bytes after the header: TLS 1.2 AES-GCM only (RFC 5288; RFC 7905 has none)
+__device__ inline uint32_t explicit_len(uint32_t version, uint32_t cipher) {
+    return version == UVHTTP_TLS_VERSION_12 && cipher == UVHTTP_TLS_CIPHER_AES_GCM ? 8u : 0u;
+}
+
+// key slot -> AES round keys, H = E(K, 0^128), tables of H^(2^k) (AES-GCM), or the ChaCha20
+// key / iv words; one lane per slot
 __global__ __launch_bounds__(kBlock) void k_tls_keys(const uvhttp_tls_key_t* keys, uint32_t n,
                                                      const uint32_t* te0, KeySched* ks) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     const uvhttp_tls_key_t k = keys[i];
     KeySched* o = ks + i;
-    const bool ok = (k.key_len == 16 || k.key_len == 32) &&
-                    (k.version == UVHTTP_TLS_VERSION_12 || k.version == UVHTTP_TLS_VERSION_13);
-    if (!ok) {
+    if (!key_valid(k)) {
         o->nr = 0;
         o->version = 0;
+        return;
+    }
+    o->cipher = k.cipher;
+    o->version = k.version;
+    if (k.cipher == UVHTTP_TLS_CIPHER_CHACHA20_POLY1305) {  // RFC 8439: little-endian words
+        for (int j = 0; j < 8; ++j)
+            o->rk[j] = (uint32_t)k.key[4 * j] | ((uint32_t)k.key[4 * j + 1] << 8) |
+                       ((uint32_t)k.key[4 * j + 2] << 16) | ((uint32_t)k.key[4 * j + 3] << 24);
+        for (int j = 0; j < 3; ++j)
+            o->iv[j] = (uint32_t)k.iv[4 * j] | ((uint32_t)k.iv[4 * j + 1] << 8) |
+                       ((uint32_t)k.iv[4 * j + 2] << 16) | ((uint32_t)k.iv[4 * j + 3] << 24);
+        o->nr = 20;
         return;
     }
     auto sb = [&](uint32_t x) { return (te0[x] >> 16) & 0xFF; };
@@ -316,7 +338,6 @@ __global__ __launch_bounds__(kBlock) void k_tls_keys(const uvhttp_tls_key_t* key
     }
     for (uint32_t j = 0; j < total; ++j) o->rk[j] = w[j];
     o->nr = nr;
-    o->version = k.version;
     for (int j = 0; j < 3; ++j)
         o->iv[j] = ((uint32_t)k.iv[4 * j] << 24) | ((uint32_t)k.iv[4 * j + 1] << 16) |
                    ((uint32_t)k.iv[4 * j + 2] << 8) | k.iv[4 * j + 3];
@@ -335,25 +356,23 @@ __global__ __launch_bounds__(kBlock) void k_tls_keys(const uvhttp_tls_key_t* key
 
 __device__ inline uint32_t be16(const uint8_t* p) { return ((uint32_t)p[0] << 8) | p[1]; }
 
-// header checks in contract order; 0 or the record status
-__device__ inline int32_t header_status(uint32_t version, uint32_t type, uint32_t ver, uint32_t len) {
+// header checks in contract order; 0 or the record status.  AEAD overhead = 16-byte tag +
+// explicit nonce; the limit is 2^14 content bytes (+ the TLS 1.3 inner type byte) + overhead
+__device__ inline int32_t header_status(uint32_t version, uint32_t cipher, uint32_t type,
+                                        uint32_t ver, uint32_t len) {
+    const uint32_t over = 16 + explicit_len(version, cipher);
     if (ver != 0x0303) return UVHTTP_TLS_REC_ERR_VERSION;
     if (version == UVHTTP_TLS_VERSION_13 ? type != 23 : (type < 21 || type > 23))
         return UVHTTP_TLS_REC_ERR_BAD_TYPE;
-    if (len > (version == UVHTTP_TLS_VERSION_13 ? kMaxLen13 : kMaxLen12))
+    if (len > 16384u + (version == UVHTTP_TLS_VERSION_13 ? 1u : 0u) + over)
         return UVHTTP_TLS_REC_ERR_OVERFLOW;
-    if (len < (version == UVHTTP_TLS_VERSION_13 ? 16u : 24u)) return UVHTTP_TLS_REC_ERR_BAD_MAC;
+    if (len < over) return UVHTTP_TLS_REC_ERR_BAD_MAC;
     return 0;
 }
 
-__device__ inline uint64_t record_cap(uint32_t version, uint32_t len) {
-    const uint32_t over = version == UVHTTP_TLS_VERSION_13 ? 17 : 24;
+__device__ inline uint64_t record_cap(uint32_t version, uint32_t cipher, uint32_t len) {
+    const uint32_t over = 16 + explicit_len(version, cipher) + (version == UVHTTP_TLS_VERSION_13 ? 1u : 0u);
     return len > over ? len - over : 0;
-}
-
-__device__ inline bool key_valid(const uvhttp_tls_key_t& k) {
-    return (k.key_len == 16 || k.key_len == 32) &&
-           (k.version == UVHTTP_TLS_VERSION_12 || k.version == UVHTTP_TLS_VERSION_13);
 }
 
 // walk one connection's records; WRITE fills RecWork from index `first` (spec offsets from base)
@@ -371,7 +390,7 @@ __device__ inline uint32_t walk(const TlsArgs& a, uint32_t s, uint64_t* cap_out,
     uint64_t pos = 0, cap = 0;
     while (L - pos >= 5) {
         const uint32_t type = p[pos], ver = be16(p + pos + 1), len = be16(p + pos + 3);
-        const int32_t hs = header_status(k.version, type, ver, len);
+        const int32_t hs = header_status(k.version, k.cipher, type, ver, len);
         if (!hs && L - pos - 5 < len) break;  // incomplete: waits for more bytes
         if (WRITE) {
             RecWork w;
@@ -388,7 +407,7 @@ __device__ inline uint32_t walk(const TlsArgs& a, uint32_t s, uint64_t* cap_out,
         }
         ++n;
         if (hs) break;
-        cap += record_cap(k.version, len);
+        cap += record_cap(k.version, k.cipher, len);
         pos += 5 + (uint64_t)len;
     }
     *cap_out = cap;
@@ -523,6 +542,30 @@ struct CryptOut {
     uint32_t last_nz;  // (index + 1) << 8 | byte of the last non-zero inner byte, 0 if none
 };
 
+// TLS 1.3 content type: each lane keeps the last (highest-offset) non-zero 16-byte block of
+// inner plaintext it saw (blocks arrive in increasing order per lane) and resolves the byte
+// once at the end: (index + 1) << 8 | byte, 0 if none — the wave max is the last non-zero byte
+struct LastNz {
+    uint32_t off1;  // block offset + 1, 0 = none
+    uint32_t w[4];
+    __device__ inline void see(uint32_t off, const uint32_t pt[4]) {
+        if (pt[0] | pt[1] | pt[2] | pt[3]) {
+            off1 = off + 1;
+            w[0] = pt[0], w[1] = pt[1], w[2] = pt[2], w[3] = pt[3];
+        }
+    }
+    __device__ inline uint32_t resolve() const {
+        if (!off1) return 0;
+        for (int b = 3; b >= 0; --b) {
+            if (w[b]) {
+                const uint32_t byte_i = 4 * b + (31 - __builtin_clz(w[b])) / 8;
+                return ((off1 + byte_i) << 8) | ((w[b] >> (8 * (byte_i & 3))) & 0xFF);
+            }
+        }
+        return 0;
+    }
+};
+
 struct Lanes {          // per-lane state after the Horner pass
     U128 acc;           // the lane's Horner sum (multiplier H^64)
     uint32_t ej0[4];    // E(K, J0) in the lane that held the AAD block
@@ -546,7 +589,7 @@ __device__ Lanes gcm_lanes(const KeySched* __restrict__ ks, const uint32_t* te, 
     const uint32_t* __restrict__ rk = ks->rk;
     U128 acc{0, 0};
     uint32_t ej0[4] = {0, 0, 0, 0};
-    uint32_t last_nz = 0;
+    LastNz nz{0, {0, 0, 0, 0}};
     for (uint32_t j = 0; j < J; ++j) {
         const int32_t q = (int32_t)(64 * j + lane) - (int32_t)pad;  // position in the sequence
         U128 x{0, 0};
@@ -574,16 +617,7 @@ __device__ Lanes gcm_lanes(const KeySched* __restrict__ ks, const uint32_t* te, 
                         pt[b] &= msk;
                     }
                 }
-                if (is13) {
-                    for (int b = 3; b >= 0; --b) {
-                        if (pt[b]) {
-                            const uint32_t byte_i = 4 * b + (31 - __builtin_clz(pt[b])) / 8;
-                            const uint32_t v = ((off + byte_i + 1) << 8) | ((pt[b] >> (8 * (byte_i & 3))) & 0xFF);
-                            if (v > last_nz) last_nz = v;
-                            break;
-                        }
-                    }
-                }
+                if (is13) nz.see(off, pt);
                 if (off < wlen) store_part(dst + off, wlen - off < 16 ? (int)(wlen - off) : 16, pt);
             } else {
                 // inner plaintext byte b of the record = content b (< src_n), type (== src_n), 0
@@ -614,7 +648,7 @@ __device__ Lanes gcm_lanes(const KeySched* __restrict__ ks, const uint32_t* te, 
 #endif
     }
     // E(K, J0) lives in the lane that held the AAD block: lane pad % 64 of iteration pad / 64
-    return Lanes{acc, {ej0[0], ej0[1], ej0[2], ej0[3]}, last_nz, pad & 63};
+    return Lanes{acc, {ej0[0], ej0[1], ej0[2], ej0[3]}, nz.resolve(), pad & 63};
 }
 
 // combine one wave's lanes: level t joins groups of 2^t lanes with multiplier H^(2^t); lane 0
@@ -678,6 +712,276 @@ __device__ CryptOut gcm_finish(const Lanes& L, U128 acc, const uint8_t* ct_in, u
     return r;
 }
 
+// ---- ChaCha20-Poly1305 (RFC 8439) -------------------------------------------------------
+//
+// One wavefront per record, like AES-GCM.  ChaCha20: lane l of round j produces the 64-byte
+// keystream block of ciphertext chunk 64 j + l (counter chunk + 1): twenty ARX rounds in
+// registers, no tables.  The chunk's ciphertext (read, or produced when sealing) goes to a
+// 4 KiB LDS window per wave, from which Poly1305 reads it with a 16-byte-block-per-lane
+// mapping: ciphertext block k -> lane k % 64.  Poly1305 in radix 2^26 (five limbs, 25
+// 32x32->64 multiplies per block): each lane runs Horner with multiplier r^64 over its blocks,
+// the AAD block is folded into lane 0's first step (multiplier r), and the lanes combine in a
+// shuffle tree after a rotation that orders them by exponent; the length block ends it.
+
+struct P130 {  // a Poly1305 field element, radix 2^26 (limbs may exceed 26 bits between carries)
+    uint32_t h[5];
+};
+
+__device__ inline P130 p_from_le16(const uint32_t w[4], uint32_t hibit) {
+    P130 r;
+    r.h[0] = w[0] & 0x3ffffff;
+    r.h[1] = ((w[0] >> 26) | (w[1] << 6)) & 0x3ffffff;
+    r.h[2] = ((w[1] >> 20) | (w[2] << 12)) & 0x3ffffff;
+    r.h[3] = ((w[2] >> 14) | (w[3] << 18)) & 0x3ffffff;
+    r.h[4] = (w[3] >> 8) | hibit;
+    return r;
+}
+
+__device__ inline P130 p_add(P130 a, const P130& b) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) a.h[i] += b.h[i];
+    return a;
+}
+
+// a * b mod 2^130 - 5, result limbs carried (h1 may carry one extra bit)
+__device__ inline P130 p_mul(const P130& a, const P130& b) {
+    const uint32_t b1s = b.h[1] * 5, b2s = b.h[2] * 5, b3s = b.h[3] * 5, b4s = b.h[4] * 5;
+    auto m = [](uint32_t x, uint32_t y) { return (uint64_t)x * y; };
+    uint64_t d0 = m(a.h[0], b.h[0]) + m(a.h[1], b4s) + m(a.h[2], b3s) + m(a.h[3], b2s) + m(a.h[4], b1s);
+    uint64_t d1 = m(a.h[0], b.h[1]) + m(a.h[1], b.h[0]) + m(a.h[2], b4s) + m(a.h[3], b3s) + m(a.h[4], b2s);
+    uint64_t d2 = m(a.h[0], b.h[2]) + m(a.h[1], b.h[1]) + m(a.h[2], b.h[0]) + m(a.h[3], b4s) + m(a.h[4], b3s);
+    uint64_t d3 = m(a.h[0], b.h[3]) + m(a.h[1], b.h[2]) + m(a.h[2], b.h[1]) + m(a.h[3], b.h[0]) + m(a.h[4], b4s);
+    uint64_t d4 = m(a.h[0], b.h[4]) + m(a.h[1], b.h[3]) + m(a.h[2], b.h[2]) + m(a.h[3], b.h[1]) + m(a.h[4], b.h[0]);
+    P130 r;
+    uint64_t c = d0 >> 26;
+    r.h[0] = (uint32_t)d0 & 0x3ffffff;
+    d1 += c, c = d1 >> 26, r.h[1] = (uint32_t)d1 & 0x3ffffff;
+    d2 += c, c = d2 >> 26, r.h[2] = (uint32_t)d2 & 0x3ffffff;
+    d3 += c, c = d3 >> 26, r.h[3] = (uint32_t)d3 & 0x3ffffff;
+    d4 += c, c = d4 >> 26, r.h[4] = (uint32_t)d4 & 0x3ffffff;
+    const uint64_t t = (uint64_t)r.h[0] + c * 5;
+    r.h[0] = (uint32_t)t & 0x3ffffff;
+    r.h[1] += (uint32_t)(t >> 26);
+    return r;
+}
+
+// (h mod 2^130 - 5) + s mod 2^128, as four little-endian words (RFC 8439 §2.5.1 final step)
+__device__ inline void p_tag(P130 h, const uint32_t s[4], uint32_t out[4]) {
+    uint32_t c;
+    for (int pass = 0; pass < 2; ++pass) {  // two full carry passes: every limb < 2^26
+        c = h.h[0] >> 26, h.h[0] &= 0x3ffffff, h.h[1] += c;
+        c = h.h[1] >> 26, h.h[1] &= 0x3ffffff, h.h[2] += c;
+        c = h.h[2] >> 26, h.h[2] &= 0x3ffffff, h.h[3] += c;
+        c = h.h[3] >> 26, h.h[3] &= 0x3ffffff, h.h[4] += c;
+        c = h.h[4] >> 26, h.h[4] &= 0x3ffffff, h.h[0] += c * 5;
+    }
+    c = h.h[0] >> 26, h.h[0] &= 0x3ffffff, h.h[1] += c;
+    // g = h + 5 - 2^130; take g when it does not borrow (h >= p)
+    uint32_t g[5];
+    c = h.h[0] + 5, g[0] = c & 0x3ffffff, c >>= 26;
+    c += h.h[1], g[1] = c & 0x3ffffff, c >>= 26;
+    c += h.h[2], g[2] = c & 0x3ffffff, c >>= 26;
+    c += h.h[3], g[3] = c & 0x3ffffff, c >>= 26;
+    g[4] = h.h[4] + c - (1u << 26);
+    const uint32_t keep_g = (g[4] >> 31) - 1u;  // all ones if g did not borrow
+    for (int i = 0; i < 5; ++i) h.h[i] = (h.h[i] & ~keep_g) | (g[i] & keep_g);
+    const uint32_t w0 = h.h[0] | (h.h[1] << 26), w1 = (h.h[1] >> 6) | (h.h[2] << 20);
+    const uint32_t w2 = (h.h[2] >> 12) | (h.h[3] << 14), w3 = (h.h[3] >> 18) | (h.h[4] << 8);
+    uint64_t f = (uint64_t)w0 + s[0];
+    out[0] = (uint32_t)f;
+    f = (uint64_t)w1 + s[1] + (f >> 32), out[1] = (uint32_t)f;
+    f = (uint64_t)w2 + s[2] + (f >> 32), out[2] = (uint32_t)f;
+    f = (uint64_t)w3 + s[3] + (f >> 32), out[3] = (uint32_t)f;
+}
+
+__device__ inline uint32_t rotl(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+
+// RFC 8439 §2.3 block function: x[16] = keystream words (little-endian byte order)
+__device__ inline void chacha_block(const uint32_t* __restrict__ key, uint32_t counter,
+                                    const uint32_t nonce[3], uint32_t x[16]) {
+    uint32_t st[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u,
+                       key[0], key[1], key[2], key[3], key[4], key[5], key[6], key[7],
+                       counter, nonce[0], nonce[1], nonce[2]};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x[i] = st[i];
+#define CQR(a, b, c, d)                                                                       \
+    x[a] += x[b], x[d] = rotl(x[d] ^ x[a], 16), x[c] += x[d], x[b] = rotl(x[b] ^ x[c], 12),  \
+    x[a] += x[b], x[d] = rotl(x[d] ^ x[a], 8), x[c] += x[d], x[b] = rotl(x[b] ^ x[c], 7)
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        CQR(0, 4, 8, 12); CQR(1, 5, 9, 13); CQR(2, 6, 10, 14); CQR(3, 7, 11, 15);
+        CQR(0, 5, 10, 15); CQR(1, 6, 11, 12); CQR(2, 7, 8, 13); CQR(3, 4, 9, 14);
+    }
+#undef CQR
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x[i] += st[i];
+}
+
+__device__ inline P130 shfl_p(const P130& v, int src) {
+    P130 r;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) r.h[i] = __shfl(v.h[i], src, 64);
+    return r;
+}
+
+// One record on one wave.  OPEN: ct[0, clen) -> content dst[0, wlen), tag compared with
+// ct[clen, +16); SEAL: plaintext from (src, src_n, inner_type) -> ciphertext at ct_out, tag
+// stored after it.  aad16: the AAD block (<= 13 bytes) as four little-endian words.
+#ifndef TLS_POLY_SGPR
+#define TLS_POLY_SGPR 1    // 1: the Poly1305 key powers r^(2^t) in scalar registers
+#endif
+#ifndef TLS_CHACHA_WPE
+#define TLS_CHACHA_WPE 0   // >0: amdgpu_waves_per_eu hint for the ChaCha20-Poly1305 kernels
+#endif
+#if TLS_CHACHA_WPE > 0
+#define CHACHA_ATTR __launch_bounds__(kCryptWG) __attribute__((amdgpu_waves_per_eu(TLS_CHACHA_WPE)))
+#else
+#define CHACHA_ATTR __launch_bounds__(kCryptWG)
+#endif
+
+template <bool SEAL>
+__device__ CryptOut chacha_record(const KeySched* __restrict__ ks, const uint32_t nonce[3],
+                                  const uint32_t aad16[4], uint32_t alen, const uint8_t* ct_in,
+                                  uint8_t* ct_out, uint32_t clen, uint8_t* dst, uint32_t wlen,
+                                  const uint8_t* src, uint32_t src_n, uint32_t inner_type,
+                                  bool is13, uint8_t* win) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t* __restrict__ key = ks->rk;
+    // one-time Poly1305 key: block 0 (every lane computes it: one uniform extra block)
+    uint32_t x[16];
+    chacha_block(key, 0, nonce, x);
+    // wave-uniform: held in scalar registers (readfirstlane), freeing vector registers
+    const uint32_t rw[4] = {x[0] & 0x0fffffffu, x[1] & 0x0ffffffcu, x[2] & 0x0ffffffcu, x[3] & 0x0ffffffcu};
+    uint32_t sw[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sw[i] = __builtin_amdgcn_readfirstlane(x[4 + i]);
+    P130 pr[7];  // r^(2^t), t = 0..6
+    pr[0] = p_from_le16(rw, 0);
+#pragma unroll
+    for (int t = 1; t < 7; ++t) pr[t] = p_mul(pr[t - 1], pr[t - 1]);
+#if TLS_POLY_SGPR
+#pragma unroll
+    for (int t = 0; t < 7; ++t)
+#pragma unroll
+        for (int i = 0; i < 5; ++i) pr[t].h[i] = __builtin_amdgcn_readfirstlane(pr[t].h[i]);
+#endif
+    const uint32_t nct = (clen + 15) / 16;       // ciphertext Poly blocks
+    const uint32_t nchunk = (clen + 63) / 64;    // ChaCha blocks (counter 1 ..)
+    const uint32_t J = (nchunk + 63) / 64;       // rounds of 64 chunks = 4 KiB of ciphertext
+    P130 acc{{0, 0, 0, 0, 0}};
+    LastNz nz{0, {0, 0, 0, 0}};
+    for (uint32_t j = 0; j < J; ++j) {
+        const uint32_t chunk = 64 * j + lane;
+        const uint32_t off = 64 * chunk;
+        // ChaCha20 over the lane's 64-byte chunk (a variant that loaded the next round's chunk
+        // ahead, into 16 more registers, measured 22% slower)
+        uint32_t d[16];
+        if (chunk < nchunk) {
+            chacha_block(key, chunk + 1, nonce, x);
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const uint32_t o = off + 16 * v;
+                const int n = o >= clen ? 0 : (clen - o < 16 ? (int)(clen - o) : 16);
+                uint32_t w[4] = {0, 0, 0, 0};
+                if (!SEAL) {
+                    if (n) load_part(ct_in + o, 0, n, w);
+                    uint32_t pt[4];
+                    for (int b = 0; b < 4; ++b) pt[b] = w[b] ^ x[4 * v + b];
+                    if (n < 16) {
+                        for (int b = 0; b < 4; ++b) {
+                            const int lo = 4 * b;
+                            pt[b] &= n >= lo + 4 ? 0xFFFFFFFFu : n <= lo ? 0u : ((1u << (8 * (n - lo))) - 1u);
+                        }
+                    }
+                    if (is13) nz.see(o, pt);
+                    if (n && o < wlen) store_part(dst + o, wlen - o < 16 ? (int)(wlen - o) : 16, pt);
+                } else {
+                    const int cn = src_n > o ? (src_n - o < 16 ? (int)(src_n - o) : 16) : 0;
+                    if (cn) load_part(src + o, 0, cn, w);
+                    if (is13 && src_n >= o && src_n < o + 16) {
+                        const uint32_t bq = src_n - o;
+                        w[bq >> 2] |= inner_type << (8 * (bq & 3));
+                    }
+                    for (int b = 0; b < 4; ++b) w[b] ^= x[4 * v + b];
+                    if (n < 16) {
+                        for (int b = 0; b < 4; ++b) {
+                            const int lo = 4 * b;
+                            w[b] &= n >= lo + 4 ? 0xFFFFFFFFu : n <= lo ? 0u : ((1u << (8 * (n - lo))) - 1u);
+                        }
+                    }
+                    if (n) store_part(ct_out + o, n, w);
+                }
+                d[4 * v] = w[0], d[4 * v + 1] = w[1], d[4 * v + 2] = w[2], d[4 * v + 3] = w[3];
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) d[i] = 0;
+        }
+        // the round's 4 KiB of ciphertext through LDS: chunk order in, block-per-lane out
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+            *reinterpret_cast<uint4*>(win + 64 * lane + 16 * v) = uint4{d[4 * v], d[4 * v + 1], d[4 * v + 2], d[4 * v + 3]};
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t k = 256 * j + 64 * q + lane;  // ciphertext block
+            if (k < nct) {
+                const uint4 c4 = *reinterpret_cast<const uint4*>(win + 16 * (64 * q + lane));
+                const uint32_t cw[4] = {c4.x, c4.y, c4.z, c4.w};
+                P130 c = p_from_le16(cw, 1u << 24);
+                if (k == 0) {  // lane 0's first block: the AAD block comes first (multiplier r)
+                    const P130 a = p_from_le16(aad16, 1u << 24);
+                    c = p_add(p_mul(a, pr[0]), c);
+                }
+                acc = (k < 64) ? c : p_add(p_mul(acc, pr[6]), c);
+            }
+        }
+    }
+    // Tag = (T r + c_LEN) r with T = c_AAD r^nct + sum_k c_k r^(nct-1-k).  Lane l's Horner sum
+    // A_l ends at its last block K_l, so T = sum_l A_l r^(nct-1-K_l); with R = nct - 64 (Jb-1)
+    // blocks in the last round that exponent is (R - 1 - l) mod 64: every value 0..63 once.
+    // Rank i = 63 - exponent is lane (i + R) mod 64, and a 6-level tree over ranks with
+    // multipliers r^(2^t) leaves T in lane 0.
+    P130 total;
+    if (nct == 0) {
+        total = p_mul(p_from_le16(aad16, 1u << 24), pr[0]);  // T = c_AAD
+    } else {
+        const uint32_t R = nct - 64 * ((nct - 1) / 64);
+        P130 b = shfl_p(acc, (int)((lane + R) & 63));
+#pragma unroll
+        for (int t = 0; t < 6; ++t) {
+            P130 right;
+#pragma unroll
+            for (int i = 0; i < 5; ++i) right.h[i] = __shfl_down(b.h[i], 1 << t, 64);
+            b = p_add(p_mul(b, pr[t]), right);
+        }
+        total = p_mul(b, pr[0]);  // T r
+    }
+    const uint32_t lens[4] = {alen, 0, clen, 0};
+    total = p_mul(p_add(total, p_from_le16(lens, 1u << 24)), pr[0]);
+    uint32_t tag[4];
+    p_tag(total, sw, tag);
+    CryptOut r{false, 0};
+    if (SEAL) {
+        if (lane == 0) store_part(ct_out + clen, 16, tag);
+        return r;
+    }
+    uint32_t t4[4];
+    load_part(ct_in + clen, 0, 16, t4);
+    r.tag_ok = t4[0] == tag[0] && t4[1] == tag[1] && t4[2] == tag[2] && t4[3] == tag[3];
+    uint32_t last_nz = nz.resolve();
+#pragma unroll
+    for (int dd = 32; dd >= 1; dd >>= 1) {
+        const uint32_t o = __shfl_xor(last_nz, dd, 64);
+        if (o > last_nz) last_nz = o;
+    }
+    r.last_nz = last_nz;
+    return r;
+}
+
 __device__ inline void load_tables(const KeySched* ks, U128 (*tabs)[16]) {
     const uint32_t lane = threadIdx.x & 63;
     const uint4* s = reinterpret_cast<const uint4*>(ks->tab);
@@ -696,6 +1000,32 @@ __device__ inline void fill_te(const uint32_t* te0, uint32_t* te) {
 #ifndef TLS_WG_TREE
 #define TLS_WG_TREE 1      // 1: the lane combine of the workgroup's 4 records shared through LDS
 #endif
+
+// record status from the AEAD result (lane 0): TLS 1.3 type = last non-zero inner byte
+__device__ inline void open_status(const TlsArgs& a, uint32_t r, const CryptOut& co, bool is13,
+                                   uint32_t clen, uint32_t outer_type) {
+    if ((threadIdx.x & 63) != 0) return;
+    int32_t st;
+    uint32_t type = 0, cl = 0;
+    if (!co.tag_ok) {
+        st = UVHTTP_TLS_REC_ERR_BAD_MAC;
+    } else if (is13) {
+        if (co.last_nz == 0) {
+            st = UVHTTP_TLS_REC_ERR_EMPTY;
+        } else {
+            type = co.last_nz & 0xFF;
+            cl = (co.last_nz >> 8) - 1;
+            st = type == 23 ? UVHTTP_TLS_REC_OK : UVHTTP_TLS_REC_CONTROL;
+        }
+    } else {
+        type = outer_type;
+        cl = clen;
+        st = type == 23 ? UVHTTP_TLS_REC_OK : UVHTTP_TLS_REC_CONTROL;
+    }
+    a.work[r].status = st;
+    a.work[r].type = type;
+    a.work[r].content_len = cl;
+}
 
 __global__ CRYPT_ATTR void k_tls_open(TlsArgs a) {
     __shared__ uint32_t te[256 * TLS_TE_COPIES];
@@ -729,6 +1059,7 @@ __global__ CRYPT_ATTR void k_tls_open(TlsArgs a) {
         bool is13 = false;
         uint32_t clen = 0;
         const uint8_t* ct = rec;
+        if (active) active = ks->cipher == UVHTTP_TLS_CIPHER_AES_GCM;  // else k_tls_open_chacha
         if (active) {
             if (w.key != cur) {
                 load_tables(ks, tabs[wave]);
@@ -766,38 +1097,72 @@ __global__ CRYPT_ATTR void k_tls_open(TlsArgs a) {
                                  is13);
         }
 #if TLS_WG_TREE
-        s_acc[wave][lane] = L.acc;
-        __syncthreads();
-        wg_tree(s_acc, tabs);
-        const U128 ghash = s_acc[wave][0];
+        // a round with no AES-GCM record in the workgroup (ChaCha20-Poly1305 records, header
+        // failures) skips the combine: its serial multiplies are pure latency
+        U128 ghash{0, 0};
+        if (__syncthreads_or(active)) {
+            s_acc[wave][lane] = L.acc;
+            __syncthreads();
+            wg_tree(s_acc, tabs);
+            ghash = s_acc[wave][0];
+        }
 #else
         const U128 ghash = active ? wave_tree(L.acc, tabs[wave]) : U128{0, 0};
 #endif
         if (!active) continue;
-        const CryptOut co = gcm_finish<false>(L, ghash, ct, nullptr, clen);
-        if (lane == 0) {
-            int32_t st;
-            uint32_t type = 0, cl = 0;
-            if (!co.tag_ok) {
-                st = UVHTTP_TLS_REC_ERR_BAD_MAC;
-            } else if (is13) {
-                if (co.last_nz == 0) {
-                    st = UVHTTP_TLS_REC_ERR_EMPTY;
-                } else {
-                    type = co.last_nz & 0xFF;
-                    cl = (co.last_nz >> 8) - 1;
-                    st = type == 23 ? UVHTTP_TLS_REC_OK : UVHTTP_TLS_REC_CONTROL;
-                }
-            } else {
-                type = rec[0];
-                cl = clen;
-                st = type == 23 ? UVHTTP_TLS_REC_OK : UVHTTP_TLS_REC_CONTROL;
-            }
-            a.work[r].status = st;
-            a.work[r].type = type;
-            a.work[r].content_len = cl;
-        }
+        open_status(a, r, gcm_finish<false>(L, ghash, ct, nullptr, clen), is13, clen, rec[0]);
     }
+}
+
+// ChaCha20-Poly1305 records (the AES-GCM kernel skips them): one wave per record, no shared
+// tables and no workgroup barriers, so waves take records independently
+__global__ CHACHA_ATTR void k_tls_open_chacha(TlsArgs a) {
+    __shared__ uint4 wins[kCryptWaves][256];
+    uint8_t* win = reinterpret_cast<uint8_t*>(wins[threadIdx.x >> 6]);
+    const uint32_t n = a.n_total[0];
+    // the record index is wave-uniform by construction (readfirstlane of the wave id): a
+    // per-lane loop bound would make every branch of the record code divergent
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (uint32_t r = blockIdx.x * kCryptWaves + wave; r < n; r += gridDim.x * kCryptWaves) {
+        const RecWork w = a.work[r];
+        if (w.status != 0) continue;
+        const KeySched* ks = a.sched + w.key;
+        if (ks->cipher != UVHTTP_TLS_CIPHER_CHACHA20_POLY1305) continue;
+        // RFC 8439 AEAD; nonce = iv XOR be64(seq) for TLS 1.3 and TLS 1.2 (RFC 7905)
+        const uint8_t* rec = a.wire + w.rec_off;
+        const bool is13 = ks->version == UVHTTP_TLS_VERSION_13;
+        const uint32_t nonce[3] = {ks->iv[0], ks->iv[1] ^ bswap32((uint32_t)(w.seq >> 32)),
+                                   ks->iv[2] ^ bswap32((uint32_t)w.seq)};
+        const uint32_t clen = w.len - 16;
+        uint32_t aad16[4];
+        if (is13) {
+            load_part(rec, 0, 5, aad16);
+        } else {
+            aad16[0] = bswap32((uint32_t)(w.seq >> 32));
+            aad16[1] = bswap32((uint32_t)w.seq);
+            aad16[2] = (uint32_t)rec[0] | 0x030300u | ((clen >> 8) << 24);
+            aad16[3] = clen & 0xFF;
+        }
+        const uint32_t wlen = is13 ? (clen > 0 ? clen - 1 : 0) : clen;
+        const CryptOut co = chacha_record<false>(ks, nonce, aad16, is13 ? 5u : 13u, rec + 5, nullptr,
+                                                 clen, a.out + w.spec_off, wlen, nullptr, 0, 0, is13, win);
+        open_status(a, r, co, is13, clen, rec[0]);
+    }
+}
+
+// seal descriptor r checked against the contract (key slot, key, content size, buffers) and
+// the AEAD a kernel handles; record sizes out
+__device__ inline bool seal_prep(const SealArgs& a, uint32_t r, uint32_t cipher, uvhttp_tls_seal_t* sr,
+                                 const KeySched** ks, bool* is13, uint32_t* clen, uint32_t* rlen) {
+    *sr = a.recs[r];
+    if (sr->key >= a.n_keys) return false;
+    const KeySched* k = a.sched + sr->key;
+    if (k->nr == 0 || k->cipher != cipher || sr->plain_len > 16384) return false;
+    *ks = k;
+    *is13 = k->version == UVHTTP_TLS_VERSION_13;
+    *clen = sr->plain_len + (*is13 ? 1u : 0u);
+    *rlen = *clen + 16 + explicit_len(k->version, cipher);
+    return sr->out_off + 5 + *rlen <= a.out_cap && sr->src_off + sr->plain_len <= a.src_len;
 }
 
 __global__ CRYPT_ATTR void k_tls_seal(SealArgs a) {
@@ -818,24 +1183,10 @@ __global__ CRYPT_ATTR void k_tls_seal(SealArgs a) {
     for (uint32_t rb = blockIdx.x * kCryptWaves; rb < a.n; rb += gridDim.x * kCryptWaves) {
         const uint32_t r = __builtin_amdgcn_readfirstlane(rb + wave);
         uvhttp_tls_seal_t sr;
-        bool active = r < a.n;
         const KeySched* ks = a.sched;
         bool is13 = false;
         uint32_t clen = 0, rlen = 0;
-        if (active) {
-            sr = a.recs[r];
-            active = sr.key < a.n_keys;
-            if (active) {
-                ks = a.sched + sr.key;
-                active = ks->nr != 0 && sr.plain_len <= 16384;
-            }
-            if (active) {
-                is13 = ks->version == UVHTTP_TLS_VERSION_13;
-                clen = sr.plain_len + (is13 ? 1u : 0u);
-                rlen = clen + 16 + (is13 ? 0u : 8u);
-                active = sr.out_off + 5 + rlen <= a.out_cap && sr.src_off + sr.plain_len <= a.src_len;
-            }
-        }
+        bool active = r < a.n && seal_prep(a, r, UVHTTP_TLS_CIPHER_AES_GCM, &sr, &ks, &is13, &clen, &rlen);
         Lanes L{U128{0, 0}, {0, 0, 0, 0}, 0, 0};
         uint8_t* ct = a.out;
         if (active) {
@@ -875,14 +1226,54 @@ __global__ CRYPT_ATTR void k_tls_seal(SealArgs a) {
                                 sr.plain_len, sr.type, is13);
         }
 #if TLS_WG_TREE
-        s_acc[wave][lane] = L.acc;
-        __syncthreads();
-        wg_tree(s_acc, tabs);
-        const U128 ghash = s_acc[wave][0];
+        // a round with no AES-GCM record in the workgroup (ChaCha20-Poly1305 records, header
+        // failures) skips the combine: its serial multiplies are pure latency
+        U128 ghash{0, 0};
+        if (__syncthreads_or(active)) {
+            s_acc[wave][lane] = L.acc;
+            __syncthreads();
+            wg_tree(s_acc, tabs);
+            ghash = s_acc[wave][0];
+        }
 #else
         const U128 ghash = active ? wave_tree(L.acc, tabs[wave]) : U128{0, 0};
 #endif
         if (active) (void)gcm_finish<true>(L, ghash, nullptr, ct, clen);
+    }
+}
+
+__global__ CHACHA_ATTR void k_tls_seal_chacha(SealArgs a) {
+    __shared__ uint4 wins[kCryptWaves][256];
+    uint8_t* win = reinterpret_cast<uint8_t*>(wins[threadIdx.x >> 6]);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (uint32_t r = blockIdx.x * kCryptWaves + wave; r < a.n; r += gridDim.x * kCryptWaves) {
+        uvhttp_tls_seal_t sr;
+        const KeySched* ks;
+        bool is13;
+        uint32_t clen, rlen;
+        if (!seal_prep(a, r, UVHTTP_TLS_CIPHER_CHACHA20_POLY1305, &sr, &ks, &is13, &clen, &rlen)) continue;
+        uint8_t* rec = a.out + sr.out_off;
+        const uint32_t otype = is13 ? 23u : sr.type;
+        const uint32_t nonce[3] = {ks->iv[0], ks->iv[1] ^ bswap32((uint32_t)(sr.seq >> 32)),
+                                   ks->iv[2] ^ bswap32((uint32_t)sr.seq)};
+        uint32_t aad16[4];
+        if (is13) {
+            aad16[0] = otype | 0x030300u | ((rlen >> 8) << 24);
+            aad16[1] = rlen & 0xFF;
+            aad16[2] = aad16[3] = 0;
+        } else {
+            aad16[0] = bswap32((uint32_t)(sr.seq >> 32));
+            aad16[1] = bswap32((uint32_t)sr.seq);
+            aad16[2] = otype | 0x030300u | ((clen >> 8) << 24);
+            aad16[3] = clen & 0xFF;
+        }
+        if (lane < 5) {
+            const uint32_t hb[5] = {otype, 3, 3, rlen >> 8, rlen & 0xFF};
+            rec[lane] = (uint8_t)hb[lane];
+        }
+        (void)chacha_record<true>(ks, nonce, aad16, is13 ? 5u : 13u, nullptr, rec + 5, clen, nullptr,
+                                  0, a.src + sr.src_off, sr.plain_len, sr.type, is13, win);
     }
 }
 
@@ -1188,6 +1579,7 @@ int uvhttp_tls_gpu_open_records(uvhttp_tls_gpu_engine_t* e, const uint8_t* wire,
     const uint32_t grid = need < (uint32_t)e->crypt_grid ? (need ? need : 1) : (uint32_t)e->crypt_grid;
     const int tk = tls_timing_begin(e, s);
     hipLaunchKernelGGL(k_tls_open, dim3(grid), dim3(kCryptWG), 0, s, a);
+    hipLaunchKernelGGL(k_tls_open_chacha, dim3(grid), dim3(kCryptWG), 0, s, a);
     tls_timing_end(e, tk, s);
     hipLaunchKernelGGL(k_tls_finalize, dim3(nb), dim3(kBlock), 0, s, a);
     hipLaunchKernelGGL(k_tls_fixup, dim3(n_streams), dim3(kBlock), 0, s, a);
@@ -1221,6 +1613,7 @@ int uvhttp_tls_gpu_seal_records(uvhttp_tls_gpu_engine_t* e, const uint8_t* src, 
     const uint32_t grid = need < (uint32_t)e->crypt_grid ? need : (uint32_t)e->crypt_grid;
     const int tk = tls_timing_begin(e, s);
     hipLaunchKernelGGL(k_tls_seal, dim3(grid), dim3(kCryptWG), 0, s, a);
+    hipLaunchKernelGGL(k_tls_seal_chacha, dim3(grid), dim3(kCryptWG), 0, s, a);
     tls_timing_end(e, tk, s);
     const hipError_t h = hipGetLastError();
     if (prev != e->device) (void)hipSetDevice(prev);
