@@ -60,6 +60,17 @@ constexpr int kCryptWaves = kCryptWG / 64;
 #else
 #define CRYPT_ATTR __launch_bounds__(kCryptWG)
 #endif
+#ifndef TLS_POLY_SGPR
+#define TLS_POLY_SGPR 1    // 1: the Poly1305 key powers r^(2^t) in scalar registers
+#endif
+#ifndef TLS_CHACHA_WPE
+#define TLS_CHACHA_WPE 4   // >0: amdgpu_waves_per_eu hint for the ChaCha20-Poly1305 kernels (4: 975 vs 960 GB/s at 3)
+#endif
+#if TLS_CHACHA_WPE > 0
+#define CHACHA_ATTR __launch_bounds__(kCryptWG) __attribute__((amdgpu_waves_per_eu(TLS_CHACHA_WPE)))
+#else
+#define CHACHA_ATTR __launch_bounds__(kCryptWG)
+#endif
 constexpr uint32_t kTeShift = TLS_TE_COPIES == 32 ? 5 : TLS_TE_COPIES == 16 ? 4 : 3;
 
 struct U128 {  // a GCM block as a big-endian 128-bit value (bit 0 of the spec = MSB of hi)
@@ -595,6 +606,8 @@ __device__ Lanes gcm_lanes(const KeySched* __restrict__ ks, const uint32_t* te, 
         U128 x{0, 0};
         // counter block: J0 for the AAD lane (tag mask), J0 + 1 + k for ciphertext block k
         uint32_t cb[4] = {nonce[0], nonce[1], nonce[2], q <= 0 ? 1u : (uint32_t)q + 1u};
+        // (loading the ciphertext block ahead of the rounds, pinned by a sched_barrier, measured
+        // neutral here — 410 GB/s either way — unlike ChaCha20-Poly1305, where it gained 20%)
         aes_encrypt(rk, nr, cb, te_lds);
         if (q == 0) {
             x = aad;
@@ -827,17 +840,6 @@ __device__ inline P130 shfl_p(const P130& v, int src) {
 // One record on one wave.  OPEN: ct[0, clen) -> content dst[0, wlen), tag compared with
 // ct[clen, +16); SEAL: plaintext from (src, src_n, inner_type) -> ciphertext at ct_out, tag
 // stored after it.  aad16: the AAD block (<= 13 bytes) as four little-endian words.
-#ifndef TLS_POLY_SGPR
-#define TLS_POLY_SGPR 1    // 1: the Poly1305 key powers r^(2^t) in scalar registers
-#endif
-#ifndef TLS_CHACHA_WPE
-#define TLS_CHACHA_WPE 0   // >0: amdgpu_waves_per_eu hint for the ChaCha20-Poly1305 kernels
-#endif
-#if TLS_CHACHA_WPE > 0
-#define CHACHA_ATTR __launch_bounds__(kCryptWG) __attribute__((amdgpu_waves_per_eu(TLS_CHACHA_WPE)))
-#else
-#define CHACHA_ATTR __launch_bounds__(kCryptWG)
-#endif
 
 template <bool SEAL>
 __device__ CryptOut chacha_record(const KeySched* __restrict__ ks, const uint32_t nonce[3],
@@ -873,10 +875,37 @@ __device__ CryptOut chacha_record(const KeySched* __restrict__ ks, const uint32_
     for (uint32_t j = 0; j < J; ++j) {
         const uint32_t chunk = 64 * j + lane;
         const uint32_t off = 64 * chunk;
-        // ChaCha20 over the lane's 64-byte chunk (a variant that loaded the next round's chunk
-        // ahead, into 16 more registers, measured 22% slower)
+        // ChaCha20 over the lane's 64-byte chunk.  Full chunks (all but a record's last) load
+        // their 64 bytes unconditionally before the block function, so the loads' latency runs
+        // under the twenty rounds; the byte-exact path below handles the last chunk.  (A variant
+        // that loaded the next round's chunk a round ahead measured 22% slower.)
         uint32_t d[16];
-        if (chunk < nchunk) {
+        if (chunk < nchunk && off + 64 <= (SEAL ? src_n : clen)) {
+            uint32_t in[16];
+            const uint8_t* ip = (SEAL ? src : ct_in) + off;
+#pragma unroll
+            for (int v = 0; v < 4; ++v) __builtin_memcpy(in + 4 * v, ip + 16 * v, 16);
+            __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of the rounds
+            chacha_block(key, chunk + 1, nonce, x);
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const uint32_t o = off + 16 * v;
+                uint32_t w[4];
+#pragma unroll
+                for (int b = 0; b < 4; ++b) w[b] = in[4 * v + b] ^ x[4 * v + b];
+                if (!SEAL) {  // w = plaintext; Poly1305 reads the ciphertext
+                    if (is13) nz.see(o, w);
+                    if (o + 16 <= wlen) __builtin_memcpy(dst + o, w, 16);
+                    else if (o < wlen) store_part(dst + o, (int)(wlen - o), w);
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) d[4 * v + b] = in[4 * v + b];
+                } else {      // w = ciphertext
+                    __builtin_memcpy(ct_out + o, w, 16);
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) d[4 * v + b] = w[b];
+                }
+            }
+        } else if (chunk < nchunk) {
             chacha_block(key, chunk + 1, nonce, x);
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
