@@ -125,7 +125,8 @@ struct TlsArgs {
     RecWork* work;
     StreamWork* sw;
     uint64_t* blk;        // per-256-stream block: [2b] records, [2b+1] reserved bytes
-    uint32_t* n_total;    // [0] records to open (0 on capacity failure), [1] capacity failed
+    uint32_t* n_total;    // [0] records to open (0 on capacity failure), [1] capacity failed,
+                          // [2] bit c set: some record under cipher c (UVHTTP_TLS_CIPHER_*)
     uint32_t* fix;        // per connection: 1 = content must move left (padding)
     const uint32_t* te0;  // AES T-table (1 KiB), built once per engine
 };
@@ -450,16 +451,21 @@ __device__ inline T block_exclusive_sum(T v, T* total) {
 __global__ __launch_bounds__(kBlock) void k_tls_walk_count(TlsArgs a) {
     const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
     uint64_t cap = 0;
-    uint32_t n = 0;
+    uint32_t n = 0, cipher = 0;
     if (s < a.n_streams) {
         n = walk<false>(a, s, &cap, 0, 0);
         a.sw[s] = StreamWork{n, 0u, cap};
+        if (n) cipher = a.keys[a.streams[s].key].cipher;  // walk counted records: key valid
     }
     uint64_t tn, tc;
     (void)block_exclusive_sum<uint64_t>(n, &tn);
     (void)block_exclusive_sum<uint64_t>(cap, &tc);
+    // which AEADs the block's records use, in the top byte of its record count: the crypto
+    // kernel of an AEAD no record uses returns at once
+    const uint64_t m = (__syncthreads_or(n && cipher == UVHTTP_TLS_CIPHER_AES_GCM) ? 1u : 0u) |
+                       (__syncthreads_or(n && cipher == UVHTTP_TLS_CIPHER_CHACHA20_POLY1305) ? 2u : 0u);
     if (threadIdx.x == 0) {
-        a.blk[2 * blockIdx.x] = tn;
+        a.blk[2 * blockIdx.x] = tn | (m << 56);
         a.blk[2 * blockIdx.x + 1] = tc;
     }
 }
@@ -469,13 +475,19 @@ __global__ __launch_bounds__(kBlock) void k_tls_walk_scan(TlsArgs a, uint32_t n_
     const uint32_t per = (n_blocks + kBlock - 1) / kBlock;
     const uint32_t beg = threadIdx.x * per;
     const uint32_t fin = beg + per < n_blocks ? beg + per : n_blocks;
+    constexpr uint64_t kCount = (1ull << 56) - 1;
     uint64_t rn = 0, rc = 0;
-    for (uint32_t b = beg; b < fin; ++b) rn += a.blk[2 * b], rc += a.blk[2 * b + 1];
+    uint32_t m = 0;
+    for (uint32_t b = beg; b < fin; ++b) {
+        rn += a.blk[2 * b] & kCount, rc += a.blk[2 * b + 1];
+        m |= (uint32_t)(a.blk[2 * b] >> 56);
+    }
     uint64_t tn, tc;
     uint64_t pn = block_exclusive_sum<uint64_t>(rn, &tn);
     uint64_t pc = block_exclusive_sum<uint64_t>(rc, &tc);
+    const uint32_t mask = (__syncthreads_or(m & 1) ? 1u : 0u) | (__syncthreads_or(m & 2) ? 2u : 0u);
     for (uint32_t b = beg; b < fin; ++b) {
-        const uint64_t vn = a.blk[2 * b], vc = a.blk[2 * b + 1];
+        const uint64_t vn = a.blk[2 * b] & kCount, vc = a.blk[2 * b + 1];
         a.blk[2 * b] = pn;
         a.blk[2 * b + 1] = pc;
         pn += vn;
@@ -485,6 +497,7 @@ __global__ __launch_bounds__(kBlock) void k_tls_walk_scan(TlsArgs a, uint32_t n_
         const bool fail = tn > a.max_records || tc > a.out_cap;
         a.n_total[0] = fail ? 0u : (uint32_t)tn;
         a.n_total[1] = fail ? 1u : 0u;
+        a.n_total[2] = mask;
     }
 }
 
@@ -1068,6 +1081,7 @@ __global__ CRYPT_ATTR void k_tls_open(TlsArgs a) {
 #if TLS_WG_TREE
     __shared__ U128 s_acc[kCryptWaves][64];
 #endif
+    if (!(a.n_total[2] & (1u << UVHTTP_TLS_CIPHER_AES_GCM))) return;  // no AES-GCM record
     fill_te(a.te0, te);
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t n = a.n_total[0];
@@ -1148,6 +1162,7 @@ __global__ CRYPT_ATTR void k_tls_open(TlsArgs a) {
 __global__ CHACHA_ATTR void k_tls_open_chacha(TlsArgs a) {
     __shared__ uint4 wins[kCryptWaves][256];
     uint8_t* win = reinterpret_cast<uint8_t*>(wins[threadIdx.x >> 6]);
+    if (!(a.n_total[2] & (1u << UVHTTP_TLS_CIPHER_CHACHA20_POLY1305))) return;
     const uint32_t n = a.n_total[0];
     // the record index is wave-uniform by construction (readfirstlane of the wave id): a
     // per-lane loop bound would make every branch of the record code divergent
