@@ -23,10 +23,28 @@ def torch():
     return t
 
 
-@pytest.fixture(scope="module")
-def eng(torch):
+# emit path: the engine's automatic choice, the frame-grouped LDS kernel (kb_emit_frames) for
+# every batch (including frames far larger than its LDS window), or the output-tile kernels
+# (kb_emit) for every batch; UVHTTP_WS_BUILD_FRAMES is read when the engine is created
+_PATHS = {"auto": None, "grouped": str(1 << 62), "tiles": "0"}
+
+
+@pytest.fixture(scope="module", params=list(_PATHS))
+def eng(torch, request):
+    import os
     import uvhttp_amd as U
-    e = U.GpuEngine(0)
+    old = os.environ.get("UVHTTP_WS_BUILD_FRAMES")
+    if _PATHS[request.param] is None:
+        os.environ.pop("UVHTTP_WS_BUILD_FRAMES", None)
+    else:
+        os.environ["UVHTTP_WS_BUILD_FRAMES"] = _PATHS[request.param]
+    try:
+        e = U.GpuEngine(0)
+    finally:
+        if old is None:
+            os.environ.pop("UVHTTP_WS_BUILD_FRAMES", None)
+        else:
+            os.environ["UVHTTP_WS_BUILD_FRAMES"] = old
     yield e
     e.close()
 

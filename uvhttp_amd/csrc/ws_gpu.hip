@@ -1728,6 +1728,7 @@ struct BuildArgs {
     uint64_t n_map;
     uint32_t map_shift;  // log2 of the map tile (>= the emit tile; ~ the average frame size)
     uint32_t epoch;      // tag of this call's map records (stale records never match)
+    uint32_t group;      // kb_emit_frames: frames per workgroup (<= kEmitF)
 };
 
 __device__ inline uint64_t build_size(const uvhttp_ws_build_desc_t& f) {
@@ -1963,6 +1964,192 @@ __global__ __launch_bounds__(BLOCK) void kb_emit(BuildArgs b, uint64_t tile_base
     }
 }
 
+// Small-frame emit: one workgroup per kEmitF consecutive frames.  Their output [A, B) is
+// contiguous; it is assembled in an LDS window (zeroed; header bytes and the edge vectors of
+// each payload OR-ed in, interior payload vectors written whole) and then stored as aligned
+// 16-byte vectors, so every global store is a full coalesced vector except the two partial
+// vectors at the range's ends (their other bytes belong to the neighbouring workgroups).
+// Work items are (frame, aligned output vector of its payload) pairs, flattened by a prefix
+// over the workgroup's frames; a window takes the contiguous item range whose vectors fall
+// inside it.  Per frame: one descriptor load and one offset load; per payload vector: one
+// unaligned 16-byte source load — no per-tile map records and no per-vector frame search
+// over the whole tile.
+constexpr uint32_t kEmitF = 256;         // frames per workgroup at most (one per thread; FMAX)
+constexpr uint32_t kEmitWin = 20480;     // LDS window bytes (64 frames of <= 300 bytes: one window)
+constexpr uint32_t kEmitItems = 1280;    // item -> frame table entries (one-window workgroups; 5 per thread)
+
+template <int BLOCK, int FMAX>
+__global__ __launch_bounds__(BLOCK) void kb_emit_frames(BuildArgs b) {
+    __shared__ u32x4 s_win[kEmitWin / 16];
+    __shared__ uint64_t s_ps[FMAX], s_fe[FMAX], s_sp[FMAX], s_st[FMAX];
+    __shared__ uint32_t s_key[FMAX];
+    __shared__ u32x4 s_img[FMAX];
+    __shared__ uint32_t s_cp[FMAX + 1];  // items of frames [0, j)
+    __shared__ uint32_t s_q[2];
+    __shared__ uint8_t s_fof[kEmitItems];  // frame of item q (a workgroup with one window)
+    __shared__ uint32_t s_wsum[BLOCK / 64];
+
+    const uint64_t total = b.out_off[b.n];
+    if (total > b.out_cap) return;  // nothing is written (as kb_emit)
+    const uint32_t f0 = blockIdx.x * b.group;
+    if (f0 >= b.n) return;
+    const uint32_t nf = b.n - f0 < b.group ? b.n - f0 : b.group;
+    static_assert(BLOCK >= FMAX && FMAX <= 256, "one thread per frame; frame ids fit a byte");
+    {
+        const uint32_t j = threadIdx.x, lane = j & 63, wave = j >> 6;
+        uint32_t nv = 0;
+        if (j < nf) {
+            const uvhttp_ws_build_desc_t d = b.frames[f0 + j];
+            const uint64_t st = b.out_off[f0 + j];
+            uint32_t hm;
+            s_img[j] = build_header(d, &hm);
+            s_st[j] = st;
+            s_ps[j] = st + hm;
+            s_fe[j] = st + hm + d.payload_len;
+            s_sp[j] = d.payload_off;
+            s_key[j] = d.mask ? d.masking_key : 0u;
+            if (d.payload_len) nv = (uint32_t)(((st + hm + d.payload_len - 1) >> 4) - ((st + hm) >> 4) + 1);
+        }
+        uint32_t inc = nv;  // block-inclusive scan of the item counts
+#pragma unroll
+        for (int dd = 1; dd < 64; dd <<= 1) {
+            const uint32_t o = __shfl_up(inc, dd, 64);
+            if ((int)lane >= dd) inc += o;
+        }
+        if (lane == 63) s_wsum[wave] = inc;
+        __syncthreads();
+        for (uint32_t w = 0; w < wave; ++w) inc += s_wsum[w];
+        if (j < FMAX) s_cp[j + 1] = inc;
+        if (j == 0) s_cp[0] = 0;
+    }
+    __syncthreads();
+    const uint64_t A = s_st[0], B = s_fe[nf - 1];
+    const uint32_t nitems = s_cp[nf];
+    // the common case: the whole range in one window and an item table that fits — each
+    // frame's lane fills its items' entries, so an item finds its frame in one LDS read
+    const bool one = B - (A & ~15ull) <= kEmitWin && nitems <= kEmitItems;
+    if (one && threadIdx.x < nf)
+        for (uint32_t q = s_cp[threadIdx.x]; q < s_cp[threadIdx.x + 1]; ++q) s_fof[q] = (uint8_t)threadIdx.x;
+    // frame of item q: the last j with s_cp[j] <= q
+    auto frame_of = [&](uint32_t q) {
+        uint32_t lo = 0, hi = nf - 1;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (s_cp[mid] <= q) lo = mid;
+            else hi = mid - 1;
+        }
+        return lo;
+    };
+    auto item_oa = [&](uint32_t q, uint32_t j) { return ((s_ps[j] >> 4) + (q - s_cp[j])) << 4; };
+    uint32_t* win32 = reinterpret_cast<uint32_t*>(s_win);
+    for (uint64_t wlo = A & ~15ull; wlo < B; wlo += kEmitWin) {
+        const uint64_t whi = wlo + kEmitWin;
+        for (uint32_t v = threadIdx.x; v < kEmitWin / 16; v += BLOCK) s_win[v] = u32x4{0, 0, 0, 0};
+        if (one) {
+            if (threadIdx.x == 0) s_q[0] = 0, s_q[1] = nitems;
+        } else if (threadIdx.x == 0) {  // items whose vectors lie in the window: [first oa >= wlo, first oa >= whi)
+            uint32_t q0 = 0, q1 = nitems;
+            for (int k = 0; k < 2; ++k) {
+                const uint64_t bound = k ? whi : wlo;
+                uint32_t lo = 0, hi = nitems;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (item_oa(mid, frame_of(mid)) < bound) lo = mid + 1;
+                    else hi = mid;
+                }
+                (k ? q1 : q0) = lo;
+            }
+            s_q[0] = q0;
+            s_q[1] = q1;
+        }
+        __syncthreads();
+        // a payload item's source window and its LDS update (interior vectors whole, edges OR-ed)
+        auto item_src = [&](uint32_t q, uint32_t j, uint64_t* oa) {
+            *oa = item_oa(q, j);
+            return (int64_t)s_sp[j] + ((int64_t)*oa - (int64_t)s_ps[j]);
+        };
+        auto put_item = [&](uint32_t j, uint64_t oa, u32x4 w) {
+            const uint64_t ps = s_ps[j], fe = s_fe[j];
+            const int lo_b = ps > oa ? (int)(ps - oa) : 0;
+            const int hi_b = fe < oa + 16 ? (int)(fe - oa) : 16;
+            const uint32_t rk = rotr32(s_key[j], 8u * (uint32_t)((oa - ps) & 3u));
+            w = w ^ u32x4{rk, rk, rk, rk};
+            const uint32_t wv = (uint32_t)((oa - wlo) >> 4);
+            if (lo_b == 0 && hi_b == 16) {
+                s_win[wv] = w;
+            } else {
+                const u32x4 sel{lane_bytes(lo_b, hi_b, 0), lane_bytes(lo_b, hi_b, 1),
+                                lane_bytes(lo_b, hi_b, 2), lane_bytes(lo_b, hi_b, 3)};
+                const u32x4 m = w & sel;
+                if (m.x) atomicOr(&win32[4 * wv + 0], m.x);
+                if (m.y) atomicOr(&win32[4 * wv + 1], m.y);
+                if (m.z) atomicOr(&win32[4 * wv + 2], m.z);
+                if (m.w) atomicOr(&win32[4 * wv + 3], m.w);
+            }
+        };
+        auto put_headers = [&]() {  // header bytes (one lane per frame)
+            if (threadIdx.x >= nf) return;
+            const uint32_t j = threadIdx.x;
+            const uint64_t st = s_st[j], ps = s_ps[j];
+            const u32x4 img = s_img[j];
+            const uint32_t iw[4] = {img.x, img.y, img.z, img.w};
+            for (uint64_t k = st; k < ps; ++k) {
+                if (k < wlo || k >= whi) continue;
+                const uint32_t ib = (uint32_t)(k - st), wb = (uint32_t)(k - wlo);
+                atomicOr(&win32[wb >> 2], ((iw[ib >> 2] >> (8 * (ib & 3))) & 0xFFu) << (8 * (wb & 3)));
+            }
+        };
+        if (one && b.src_len >= 16) {
+            // every item's 16-byte source load issued before any LDS work (an out-of-range
+            // window loads from offset 0 and is redone bytewise below)
+            constexpr int kIpt = kEmitItems / BLOCK;
+            u32x4 w[kIpt];
+            uint64_t oa[kIpt];
+            int64_t ws[kIpt];
+#pragma unroll
+            for (int k = 0; k < kIpt; ++k) {
+                const uint32_t q = threadIdx.x + k * BLOCK;
+                const uint32_t j = q < nitems ? s_fof[q] : 0;
+                ws[k] = item_src(q < nitems ? q : s_cp[0], j, &oa[k]);
+                const bool ok = ws[k] >= 0 && (uint64_t)ws[k] + 16 <= b.src_len;
+                __builtin_memcpy(&w[k], b.src + (ok ? ws[k] : 0), 16);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            put_headers();
+#pragma unroll
+            for (int k = 0; k < kIpt; ++k) {
+                const uint32_t q = threadIdx.x + k * BLOCK;
+                if (q >= nitems) continue;
+                if (!(ws[k] >= 0 && (uint64_t)ws[k] + 16 <= b.src_len)) w[k] = load16_any(b.src, ws[k], b.src_len);
+                put_item(s_fof[q], oa[k], w[k]);
+            }
+        } else {
+            put_headers();
+            const uint32_t q0 = s_q[0], q1 = s_q[1];
+            for (uint32_t q = q0 + threadIdx.x; q < q1; q += BLOCK) {
+                const uint32_t j = one ? s_fof[q] : frame_of(q);
+                uint64_t oa;
+                const int64_t wsrc = item_src(q, j, &oa);
+                put_item(j, oa, load16_any(b.src, wsrc, b.src_len));
+            }
+        }
+        __syncthreads();
+        // store the window's part of [A, B)
+        const uint64_t lo = A > wlo ? A : wlo, hi = B < whi ? B : whi;
+        for (uint64_t oa = (lo & ~15ull) + 16ull * threadIdx.x; oa < hi; oa += 16ull * BLOCK) {
+            const u32x4 v = s_win[(oa - wlo) >> 4];
+            if (oa >= lo && oa + 16 <= hi) {
+                __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(b.out + oa));
+            } else {
+                const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+                for (uint32_t k = 0; k < 16; ++k)
+                    if (oa + k >= lo && oa + k < hi) b.out[oa + k] = (uint8_t)(vw[k >> 2] >> (8 * (k & 3)));
+            }
+        }
+        __syncthreads();
+    }
+}
+
 // plain unmask of one buffer with one key (uvhttp_ws_apply_mask over device memory)
 __global__ __launch_bounds__(kBlock) void k_apply_mask(uint8_t* data, uint64_t len, uint32_t key,
                                                        uint64_t head) {
@@ -2064,6 +2251,7 @@ struct uvhttp_ws_gpu_engine {
     void* bs_mem;              // send-side output-map records (BuildRec per map tile)
     uint64_t bs_tiles;
     int build_small;           // emit shape for frames < 4 KiB (UVHTTP_WS_BUILD_SMALL, tuning)
+    uint64_t build_frames_max; // frame-grouped LDS emit below this average frame (UVHTTP_WS_BUILD_FRAMES; 0 = off)
     int compact_mode;          // 0 automatic, 1 arena-driven gather, 2 wire-driven scatter
     hipEvent_t ev[2 * 1024];
     int ev_created;
@@ -2118,6 +2306,8 @@ int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out) {
         e->epoch = v < kMaxEpoch ? (uint32_t)v : 0;
     }
     if (const char* bs = getenv("UVHTTP_WS_BUILD_SMALL")) e->build_small = atoi(bs);
+    e->build_frames_max = 4096;
+    if (const char* bf = getenv("UVHTTP_WS_BUILD_FRAMES")) e->build_frames_max = strtoull(bf, nullptr, 10);
     if (const char* cm = getenv("UVHTTP_WS_COMPACT"))
         e->compact_mode = strcmp(cm, "gather") == 0 ? 1 : strcmp(cm, "scatter") == 0 ? 2 : 0;
     if (const char* ws = getenv("UVHTTP_WS_WALK_SINGLE")) e->walk_single_off = atoi(ws) == 0;
@@ -2589,6 +2779,7 @@ int uvhttp_ws_gpu_build_frames(uvhttp_ws_gpu_engine_t* e, const uint8_t* d_src, 
     if (prev != e->device) (void)hipSetDevice(e->device);
     hipStream_t s = (hipStream_t)stream;
     BuildArgs b;
+    b.group = kEmitF;
     b.src = d_src;
     b.src_len = src_len;
     b.frames = d_frames;
@@ -2605,6 +2796,8 @@ int uvhttp_ws_gpu_build_frames(uvhttp_ws_gpu_engine_t* e, const uint8_t* d_src, 
     // clamped to [tile, 64 KiB], so consecutive map records are at most one frame apart.
     const uint64_t avg = n_frames ? out_cap / n_frames : out_cap;
     const bool small = avg < 4096;
+    // below build_frames_max the frame-grouped kernel (kb_emit_frames) replaces the tiles
+    const bool grouped = n_frames && avg < e->build_frames_max;
     // small-frame tile: 0 = 64 x 2 (2 KiB, default), 1 = 64 x 4, 2 = 128 x 2, 3 = 256 x 4
     const int sh = small ? e->build_small : 0;
     const uint32_t tile_shift = sh == 3 ? 14 : (sh == 1 || sh == 2) ? 12 : 11;
@@ -2612,8 +2805,8 @@ int uvhttp_ws_gpu_build_frames(uvhttp_ws_gpu_engine_t* e, const uint8_t* d_src, 
     if (shift < tile_shift) shift = tile_shift;
     while (shift < 16 && (2ull << shift) <= avg) ++shift;
     b.map_shift = shift;
-    b.n_map = (out_cap + (1ull << shift) - 1) >> shift;
-    if (b.n_map + 1 > e->bs_tiles) {
+    b.n_map = grouped ? 0 : (out_cap + (1ull << shift) - 1) >> shift;  // grouped: no map records
+    if (!grouped && b.n_map + 1 > e->bs_tiles) {
         if (e->bs_mem) (void)hipFree(e->bs_mem);
         e->bs_mem = nullptr;
         e->bs_tiles = 0;
@@ -2643,7 +2836,23 @@ int uvhttp_ws_gpu_build_frames(uvhttp_ws_gpu_engine_t* e, const uint8_t* d_src, 
         (void)hipMemsetAsync(d_out_off, 0, 8, s);
     }
     const int tk = timing_begin(e, s);
-    if (sh == 3) launch_emit<256, 4>(b, n_frames, out_cap, s);
+    if (grouped) {
+        // frames per workgroup: as many as keep an average group inside one LDS window and
+        // the item table (payload vectors ~ avg / 16 + 1 per frame)
+        uint64_t g = kEmitItems / (avg / 16 + 2);
+        if (g > kEmitF) g = kEmitF;
+        if (g < 1) g = 1;
+        // up to 64 frames the smaller LDS footprint keeps 6 workgroups per CU (256-byte frames:
+        // 100 us with 64 per group vs 116 with 71 in the large footprint); tiny frames (room for
+        // >= 128 per group) take up to 256 (64-byte frames: 287 -> 149 us)
+        const bool wide = g >= 128;
+        if (!wide && g > 64) g = 64;
+        b.group = (uint32_t)g;
+        const dim3 grid((n_frames + b.group - 1) / b.group);
+        if (wide) hipLaunchKernelGGL((kb_emit_frames<256, 256>), grid, dim3(256), 0, s, b);
+        else hipLaunchKernelGGL((kb_emit_frames<256, 64>), grid, dim3(256), 0, s, b);
+    }
+    else if (sh == 3) launch_emit<256, 4>(b, n_frames, out_cap, s);
     else if (sh == 2) launch_emit<128, 2>(b, n_frames, out_cap, s);
     else if (sh == 1) launch_emit<64, 4>(b, n_frames, out_cap, s);
     else launch_emit<64, 2>(b, n_frames, out_cap, s);
