@@ -689,12 +689,40 @@ __global__ __launch_bounds__(kBlock) void k_plan(BatchArgs a, uvhttp_ws_frame_de
     ScanElem tagg = scan_identity();
     uvhttp_ws_frame_desc_t dv[FPT];
     {
+        // every load unconditional (indices clamped to the last frame, header windows to the
+        // last 16 wire bytes) so all of them are in flight together: under per-frame branches
+        // the compiler waited for each load before issuing the next (32 round trips per lane)
         uint64_t o[FPT];
         u32x4 hv[FPT];
+        const uint32_t ilast = n ? n - 1 : 0;
+        if (a.frame_off) {
 #pragma unroll
-        for (int k = 0; k < FPT; ++k) o[k] = i0 + k < n ? frame_start(a, i0 + k) : 0;
+            for (int k = 0; k < FPT; ++k) o[k] = a.frame_off[i0 + k < n ? i0 + k : ilast];
+        } else {
 #pragma unroll
-        for (int k = 0; k < FPT; ++k) hv[k] = i0 + k < n ? load_header(a, o[k]) : u32x4{0, 0, 0, 0};
+            for (int k = 0; k < FPT; ++k) o[k] = (uint64_t)(i0 + k < n ? i0 + k : ilast) * a.frame_stride;
+        }
+        if (a.wire_len >= 16) {
+#pragma unroll
+            for (int k = 0; k < FPT; ++k) {
+                const uint64_t oc = o[k] + 16 <= a.wire_len ? o[k] : a.wire_len - 16;
+                __builtin_memcpy(&hv[k], a.wire + oc, 16);
+            }
+            // a header within 16 bytes of the wire's end: its bytes sit d = o - oc bytes into
+            // the clamped window; shift them down, zeros past the end (as load_header)
+#pragma unroll
+            for (int k = 0; k < FPT; ++k) {
+                const uint64_t oc = o[k] + 16 <= a.wire_len ? o[k] : a.wire_len - 16;
+                const uint64_t d = o[k] - oc;
+                unsigned __int128 v = ((unsigned __int128)(((uint64_t)hv[k].w << 32) | hv[k].z) << 64) |
+                                      (((uint64_t)hv[k].y << 32) | hv[k].x);
+                v = d >= 16 ? 0 : v >> (8 * d);
+                hv[k] = u32x4{(uint32_t)v, (uint32_t)(v >> 32), (uint32_t)(v >> 64), (uint32_t)(v >> 96)};
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < FPT; ++k) hv[k] = load_header(a, o[k]);
+        }
 #pragma unroll
         for (int k = 0; k < FPT; ++k) {
             const uint32_t i = i0 + k;
@@ -2475,15 +2503,17 @@ static uint32_t next_epoch(uvhttp_ws_gpu_engine_t* e, hipStream_t s) {
     return ++e->epoch;
 }
 
-// k_plan launch: frames per lane chosen so the grid stays within ~256 blocks (the look-back
-// sees every predecessor in one window); UVHTTP_WS_PLAN_FPT pins it for tuning
+// k_plan launch: frames per lane chosen so the grid stays within ~512 blocks — every block
+// costs a ticket atomic and a look-back round on device-coherent records, so the call's time
+// grows with the block count (C4, 1 048 576 frames: 4096 blocks 148 us, 2048 96, 1024 82,
+// 512 64, 256 68 for k_plan + k_finalize); UVHTTP_WS_PLAN_FPT pins it for tuning
 static void launch_plan(uvhttp_ws_gpu_engine_t* e, BatchArgs& a, uint32_t n_cap,
                         uvhttp_ws_frame_desc_t* d_desc, uvhttp_ws_message_desc_t* d_msgs,
                         hipStream_t s) {
     int fpt = e->plan_fpt;
     if (fpt != 1 && fpt != 2 && fpt != 4 && fpt != 8 && fpt != 16) {
         fpt = 1;
-        while (fpt < 16 && ((uint64_t)n_cap + kBlock * fpt - 1) / (kBlock * fpt) > 256) fpt *= 2;
+        while (fpt < 16 && ((uint64_t)n_cap + kBlock * fpt - 1) / (kBlock * fpt) > 512) fpt *= 2;
     }
     const uint32_t per = kBlock * fpt;
     a.plan_frames = per;
