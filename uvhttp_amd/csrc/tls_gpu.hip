@@ -1085,7 +1085,7 @@ __global__ CRYPT_ATTR void k_tls_open(TlsArgs a) {
     fill_te(a.te0, te);
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t n = a.n_total[0];
-    uint32_t cur = 0xFFFFFFFFu;
+    uint32_t cur = 0xFFFFFFFFu, cur8 = 0xFFFFFFFFu;  // key slots of the wave's 4-bit / 8-bit tables
     // rounds are workgroup-uniform (the shared combine has barriers); r is wave-uniform:
     // readfirstlane makes the record and key-schedule loads scalar
     for (uint32_t rb = blockIdx.x * kCryptWaves; rb < n; rb += gridDim.x * kCryptWaves) {
@@ -1106,8 +1106,14 @@ __global__ CRYPT_ATTR void k_tls_open(TlsArgs a) {
         if (active) {
             if (w.key != cur) {
                 load_tables(ks, tabs[wave]);
-                if (TLS_GHASH8) gf_table8(tabs[wave][6], t8);
                 cur = w.key;
+            }
+            // the 8-bit table serves only the Horner steps of records over 62 blocks: a run of
+            // small records under changing keys skips building it
+            const uint32_t cl = w.len - (ks->version == UVHTTP_TLS_VERSION_13 ? 16u : 24u);
+            if (TLS_GHASH8 && (cl + 15) / 16 + 2 > 64 && cur8 != w.key) {
+                gf_table8(tabs[wave][6], t8);
+                cur8 = w.key;
             }
             is13 = ks->version == UVHTTP_TLS_VERSION_13;
             uint32_t nonce[3];
@@ -1223,7 +1229,7 @@ __global__ CRYPT_ATTR void k_tls_seal(SealArgs a) {
 #endif
     fill_te(a.te0, te);
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t cur = 0xFFFFFFFFu;
+    uint32_t cur = 0xFFFFFFFFu, cur8 = 0xFFFFFFFFu;  // key slots of the wave's 4-bit / 8-bit tables
     for (uint32_t rb = blockIdx.x * kCryptWaves; rb < a.n; rb += gridDim.x * kCryptWaves) {
         const uint32_t r = __builtin_amdgcn_readfirstlane(rb + wave);
         uvhttp_tls_seal_t sr;
@@ -1236,8 +1242,11 @@ __global__ CRYPT_ATTR void k_tls_seal(SealArgs a) {
         if (active) {
             if (sr.key != cur) {
                 load_tables(ks, tabs[wave]);
-                if (TLS_GHASH8) gf_table8(tabs[wave][6], t8);
                 cur = sr.key;
+            }
+            if (TLS_GHASH8 && (clen + 15) / 16 + 2 > 64 && cur8 != sr.key) {
+                gf_table8(tabs[wave][6], t8);
+                cur8 = sr.key;
             }
             uint8_t* rec = a.out + sr.out_off;
             const uint32_t otype = is13 ? 23u : sr.type;
