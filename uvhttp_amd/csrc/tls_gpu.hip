@@ -60,6 +60,9 @@ constexpr int kCryptWaves = kCryptWG / 64;
 #else
 #define CRYPT_ATTR __launch_bounds__(kCryptWG)
 #endif
+#ifndef TLS_PACK_WPE
+#define TLS_PACK_WPE 2     // amdgpu_waves_per_eu of the packed ChaCha20-Poly1305 kernel
+#endif
 #ifndef TLS_POLY_SGPR
 #define TLS_POLY_SGPR 1    // 1: the Poly1305 key powers r^(2^t) in scalar registers
 #endif
@@ -388,9 +391,15 @@ __device__ inline uint64_t record_cap(uint32_t version, uint32_t cipher, uint32_
 }
 
 // walk one connection's records; WRITE fills RecWork from index `first` (spec offsets from base)
+// ChaCha20-Poly1305 records up to this TLSCiphertext.length (8 KiB of content + the TLS 1.3 type
+// byte) are opened kPack to a wave (k_tls_open_chacha_packed), longer ones one per wave
+// (measured, TLS 1.3 GiB/s per-record -> packed: 256 B 34 -> 122, 1 KiB 128 -> 323, 2 KiB
+// 249 -> 466, 4 KiB 463 -> 599, 8 KiB 698 -> 726; 16 KiB 913 -> 812, so 16 KiB stays per record)
+constexpr uint32_t kPackMaxLen = 8192 + 1 + 16;
+
 template <bool WRITE>
 __device__ inline uint32_t walk(const TlsArgs& a, uint32_t s, uint64_t* cap_out, uint32_t first,
-                                uint64_t base) {
+                                uint64_t base, uint32_t* size_bits = nullptr) {
     const uvhttp_tls_stream_t st = a.streams[s];
     *cap_out = 0;
     if (st.key >= a.n_keys) return 0;
@@ -404,6 +413,7 @@ __device__ inline uint32_t walk(const TlsArgs& a, uint32_t s, uint64_t* cap_out,
         const uint32_t type = p[pos], ver = be16(p + pos + 1), len = be16(p + pos + 3);
         const int32_t hs = header_status(k.version, k.cipher, type, ver, len);
         if (!hs && L - pos - 5 < len) break;  // incomplete: waits for more bytes
+        if (size_bits && !hs) *size_bits |= len <= kPackMaxLen ? 1u : 2u;
         if (WRITE) {
             RecWork w;
             w.rec_off = st.begin + pos;
@@ -451,9 +461,9 @@ __device__ inline T block_exclusive_sum(T v, T* total) {
 __global__ __launch_bounds__(kBlock) void k_tls_walk_count(TlsArgs a) {
     const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
     uint64_t cap = 0;
-    uint32_t n = 0, cipher = 0;
+    uint32_t n = 0, cipher = 0, sizes = 0;
     if (s < a.n_streams) {
-        n = walk<false>(a, s, &cap, 0, 0);
+        n = walk<false>(a, s, &cap, 0, 0, &sizes);
         a.sw[s] = StreamWork{n, 0u, cap};
         if (n) cipher = a.keys[a.streams[s].key].cipher;  // walk counted records: key valid
     }
@@ -462,8 +472,12 @@ __global__ __launch_bounds__(kBlock) void k_tls_walk_count(TlsArgs a) {
     (void)block_exclusive_sum<uint64_t>(cap, &tc);
     // which AEADs the block's records use, in the top byte of its record count: the crypto
     // kernel of an AEAD no record uses returns at once
+    // (bit 0 AES-GCM, bit 1 ChaCha20-Poly1305, bits 2 / 3: ChaCha records short / long enough
+    // for the packed / per-record kernel)
+    const bool cc = n && cipher == UVHTTP_TLS_CIPHER_CHACHA20_POLY1305;
     const uint64_t m = (__syncthreads_or(n && cipher == UVHTTP_TLS_CIPHER_AES_GCM) ? 1u : 0u) |
-                       (__syncthreads_or(n && cipher == UVHTTP_TLS_CIPHER_CHACHA20_POLY1305) ? 2u : 0u);
+                       (__syncthreads_or(cc) ? 2u : 0u) | (__syncthreads_or(cc && (sizes & 1)) ? 4u : 0u) |
+                       (__syncthreads_or(cc && (sizes & 2)) ? 8u : 0u);
     if (threadIdx.x == 0) {
         a.blk[2 * blockIdx.x] = tn | (m << 56);
         a.blk[2 * blockIdx.x + 1] = tc;
@@ -485,7 +499,9 @@ __global__ __launch_bounds__(kBlock) void k_tls_walk_scan(TlsArgs a, uint32_t n_
     uint64_t tn, tc;
     uint64_t pn = block_exclusive_sum<uint64_t>(rn, &tn);
     uint64_t pc = block_exclusive_sum<uint64_t>(rc, &tc);
-    const uint32_t mask = (__syncthreads_or(m & 1) ? 1u : 0u) | (__syncthreads_or(m & 2) ? 2u : 0u);
+    uint32_t mask = 0;
+#pragma unroll
+    for (int bit = 0; bit < 4; ++bit) mask |= __syncthreads_or(m & (1u << bit)) ? 1u << bit : 0u;
     for (uint32_t b = beg; b < fin; ++b) {
         const uint64_t vn = a.blk[2 * b] & kCount, vc = a.blk[2 * b + 1];
         a.blk[2 * b] = pn;
@@ -1163,17 +1179,224 @@ __global__ CRYPT_ATTR void k_tls_open(TlsArgs a) {
     }
 }
 
+// Packed ChaCha20-Poly1305 open for records up to 8 KiB: a group of kPack consecutive work
+// items shares one wave, kSeg lanes per record (segment k = lanes [k kSeg, (k+1) kSeg)), so a
+// small record no longer costs a whole wave round of the block function plus its own one-time
+// key, key powers and lane combine.  Same structure as chacha_record within each segment: lane
+// u of round j takes chunk kSeg j + u, the round's ciphertext goes through the wave's LDS window,
+// Poly1305 block b of the record is Horner-accumulated by lane b % kSeg (multiplier r^kSeg),
+// and the segment's lanes combine after the rotation by R = nct mod kSeg in log2(kSeg) shuffle
+// levels confined to the segment.  Record parameters live in vector registers (they differ
+// between segments).
+constexpr int kSeg = 16;
+constexpr int kPack = 64 / kSeg;
+constexpr int kSegLog = 4;
+static_assert((1 << kSegLog) == kSeg, "segment size");
+
+__device__ inline P130 shfl_seg(const P130& v, int src) {
+    P130 r;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) r.h[i] = __shfl(v.h[i], src, kSeg);
+    return r;
+}
+
+// record status (lane u == 0 of each segment; open_status's rules)
+__device__ inline void open_status_at(const TlsArgs& a, uint32_t r, const CryptOut& co, bool is13,
+                                      uint32_t clen, uint32_t outer_type) {
+    int32_t st;
+    uint32_t type = 0, cl = 0;
+    if (!co.tag_ok) {
+        st = UVHTTP_TLS_REC_ERR_BAD_MAC;
+    } else if (is13) {
+        if (co.last_nz == 0) {
+            st = UVHTTP_TLS_REC_ERR_EMPTY;
+        } else {
+            type = co.last_nz & 0xFF;
+            cl = (co.last_nz >> 8) - 1;
+            st = type == 23 ? UVHTTP_TLS_REC_OK : UVHTTP_TLS_REC_CONTROL;
+        }
+    } else {
+        type = outer_type;
+        cl = clen;
+        st = type == 23 ? UVHTTP_TLS_REC_OK : UVHTTP_TLS_REC_CONTROL;
+    }
+    a.work[r].status = st;
+    a.work[r].type = type;
+    a.work[r].content_len = cl;
+}
+
+// does group g (work items [g kPack, g kPack + kPack)) hold a ChaCha record too long to pack?
+// (wave-uniform; both ChaCha kernels decide the same way)
+__device__ inline bool group_has_long(const TlsArgs& a, uint32_t g, uint32_t n) {
+    const uint32_t lane = threadIdx.x & 63;
+    bool big = false;
+    if (lane < kPack && g * kPack + lane < n) {
+        const RecWork w = a.work[g * kPack + lane];
+        big = w.status == 0 && w.len > kPackMaxLen &&
+              a.sched[w.key].cipher == UVHTTP_TLS_CIPHER_CHACHA20_POLY1305;
+    }
+    return __builtin_amdgcn_readfirstlane(__ballot(big) != 0 ? 1u : 0u) != 0;
+}
+
+__device__ void chacha_open_packed(const TlsArgs& a, uint32_t r0, uint8_t* win) {
+    const uint32_t lane = threadIdx.x & 63, k = lane / kSeg, u = lane % kSeg;
+    const uint32_t r = r0 + k;
+    bool act = r < a.n_total[0];
+    RecWork w;
+    if (act) {
+        w = a.work[r];
+        act = w.status == 0 && a.sched[w.key].cipher == UVHTTP_TLS_CIPHER_CHACHA20_POLY1305;
+    }
+    uint32_t key[8], nonce[3] = {0, 0, 0}, aad16[4] = {0, 0, 0, 0};
+    uint32_t clen = 0, wlen = 0, alen = 0, otype = 0;
+    bool is13 = false;
+    const uint8_t* rec = a.wire;
+    uint8_t* dst = a.out;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) key[i] = 0;
+    if (act) {
+        const KeySched* ks = a.sched + w.key;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) key[i] = ks->rk[i];
+        is13 = ks->version == UVHTTP_TLS_VERSION_13;
+        nonce[0] = ks->iv[0];
+        nonce[1] = ks->iv[1] ^ bswap32((uint32_t)(w.seq >> 32));
+        nonce[2] = ks->iv[2] ^ bswap32((uint32_t)w.seq);
+        rec = a.wire + w.rec_off;
+        dst = a.out + w.spec_off;
+        clen = w.len - 16;
+        otype = rec[0];
+        if (is13) {
+            load_part(rec, 0, 5, aad16);
+        } else {
+            aad16[0] = bswap32((uint32_t)(w.seq >> 32));
+            aad16[1] = bswap32((uint32_t)w.seq);
+            aad16[2] = otype | 0x030300u | ((clen >> 8) << 24);
+            aad16[3] = clen & 0xFF;
+        }
+        wlen = is13 ? (clen > 0 ? clen - 1 : 0) : clen;
+        alen = is13 ? 5u : 13u;
+    }
+    const uint8_t* ct_in = rec + 5;
+    uint32_t x[16];
+    chacha_block(key, 0, nonce, x);  // the segment's one-time key
+    const uint32_t rw[4] = {x[0] & 0x0fffffffu, x[1] & 0x0ffffffcu, x[2] & 0x0ffffffcu, x[3] & 0x0ffffffcu};
+    const uint32_t sw[4] = {x[4], x[5], x[6], x[7]};
+    P130 pr[kSegLog + 1];  // r^(2^t), t = 0..log2(kSeg)
+    pr[0] = p_from_le16(rw, 0);
+#pragma unroll
+    for (int t = 1; t <= kSegLog; ++t) pr[t] = p_mul(pr[t - 1], pr[t - 1]);
+    const uint32_t nct = (clen + 15) / 16;
+    const uint32_t nchunk = (clen + 63) / 64;
+    uint32_t J = (nchunk + kSeg - 1) / kSeg;  // rounds this segment needs; the wave runs the max
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint32_t o = __shfl_xor(J, d, 64);
+        if (o > J) J = o;
+    }
+    J = __builtin_amdgcn_readfirstlane(J);
+    P130 acc{{0, 0, 0, 0, 0}};
+    LastNz nz{0, {0, 0, 0, 0}};
+    for (uint32_t j = 0; j < J; ++j) {
+        const uint32_t chunk = kSeg * j + u;
+        const uint32_t off = 64 * chunk;
+        uint32_t d[16];
+        if (chunk < nchunk) {
+            const bool full = off + 64 <= clen;
+            uint32_t in[16];
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const uint32_t o = off + 16 * v;
+                const int nb = o >= clen ? 0 : (clen - o < 16 ? (int)(clen - o) : 16);
+                if (full) __builtin_memcpy(in + 4 * v, ct_in + o, 16);
+                else load_part(ct_in + o, 0, nb, in + 4 * v);
+            }
+            chacha_block(key, chunk + 1, nonce, x);
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const uint32_t o = off + 16 * v;
+                const int nb = o >= clen ? 0 : (clen - o < 16 ? (int)(clen - o) : 16);
+                uint32_t pt[4];
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const int lo = 4 * b;
+                    pt[b] = (in[4 * v + b] ^ x[4 * v + b]) &
+                            (nb >= lo + 4 ? 0xFFFFFFFFu : nb <= lo ? 0u : ((1u << (8 * (nb - lo))) - 1u));
+                    d[4 * v + b] = in[4 * v + b];
+                }
+                if (is13) nz.see(o, pt);
+                if (o + 16 <= wlen) __builtin_memcpy(dst + o, pt, 16);
+                else if (nb && o < wlen) store_part(dst + o, (int)(wlen - o), pt);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) d[i] = 0;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+            *reinterpret_cast<uint4*>(win + 64 * lane + 16 * v) = uint4{d[4 * v], d[4 * v + 1], d[4 * v + 2], d[4 * v + 3]};
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t blk = 4 * kSeg * j + kSeg * q + u;  // the record's Poly1305 block
+            if (blk < nct) {
+                const uint4 c4 = *reinterpret_cast<const uint4*>(win + 64 * kSeg * k + 16 * (kSeg * q + u));
+                const uint32_t cw[4] = {c4.x, c4.y, c4.z, c4.w};
+                P130 c = p_from_le16(cw, 1u << 24);
+                if (blk == 0) c = p_add(p_mul(p_from_le16(aad16, 1u << 24), pr[0]), c);
+                acc = blk < kSeg ? c : p_add(p_mul(acc, pr[kSegLog]), c);
+            }
+        }
+    }
+    // T = sum over the segment's lanes of A_u r^((R - 1 - u) mod kSeg); rank i = lane (i + R)
+    const uint32_t R = nct ? nct - kSeg * ((nct - 1) / kSeg) : 0;
+    P130 b = shfl_seg(acc, (int)((u + R) & (kSeg - 1)));
+#pragma unroll
+    for (int t = 0; t < kSegLog; ++t) {
+        P130 right;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) right.h[i] = __shfl_down(b.h[i], 1 << t, kSeg);
+        b = p_add(p_mul(b, pr[t]), right);
+    }
+    P130 total = nct ? p_mul(b, pr[0]) : p_mul(p_from_le16(aad16, 1u << 24), pr[0]);
+    const uint32_t lens[4] = {alen, 0, clen, 0};
+    total = p_mul(p_add(total, p_from_le16(lens, 1u << 24)), pr[0]);
+    uint32_t tag[4];
+    p_tag(total, sw, tag);
+    uint32_t last_nz = nz.resolve();
+#pragma unroll
+    for (int d = kSeg / 2; d >= 1; d >>= 1) {
+        const uint32_t o = __shfl_xor(last_nz, d, kSeg);
+        if (o > last_nz) last_nz = o;
+    }
+    if (act && u == 0) {
+        uint32_t t4[4];
+        load_part(ct_in + clen, 0, 16, t4);
+        CryptOut co{t4[0] == tag[0] && t4[1] == tag[1] && t4[2] == tag[2] && t4[3] == tag[3], last_nz};
+        open_status_at(a, r, co, is13, clen, otype);
+    }
+}
+
 // ChaCha20-Poly1305 records (the AES-GCM kernel skips them): one wave per record, no shared
 // tables and no workgroup barriers, so waves take records independently
 __global__ CHACHA_ATTR void k_tls_open_chacha(TlsArgs a) {
     __shared__ uint4 wins[kCryptWaves][256];
     uint8_t* win = reinterpret_cast<uint8_t*>(wins[threadIdx.x >> 6]);
-    if (!(a.n_total[2] & (1u << UVHTTP_TLS_CIPHER_CHACHA20_POLY1305))) return;
+    if (!(a.n_total[2] & 8u)) return;  // no long ChaCha20-Poly1305 record
     const uint32_t n = a.n_total[0];
     // the record index is wave-uniform by construction (readfirstlane of the wave id): a
     // per-lane loop bound would make every branch of the record code divergent
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    for (uint32_t r = blockIdx.x * kCryptWaves + wave; r < n; r += gridDim.x * kCryptWaves) {
+    // groups of kPack consecutive records: a group holding a long ChaCha record is opened here
+    // one record per wave, the others by k_tls_open_chacha_packed
+    for (uint32_t g = blockIdx.x * kCryptWaves + wave; g * kPack < n; g += gridDim.x * kCryptWaves) {
+        if (!group_has_long(a, g, n)) continue;
+        for (uint32_t r = g * kPack; r < g * kPack + kPack && r < n; ++r) {
         const RecWork w = a.work[r];
         if (w.status != 0) continue;
         const KeySched* ks = a.sched + w.key;
@@ -1198,6 +1421,18 @@ __global__ CHACHA_ATTR void k_tls_open_chacha(TlsArgs a) {
                                                  clen, a.out + w.spec_off, wlen, nullptr, 0, 0, is13, win);
         open_status(a, r, co, is13, clen, rec[0]);
     }
+    }
+}
+
+__global__ __launch_bounds__(kCryptWG) __attribute__((amdgpu_waves_per_eu(TLS_PACK_WPE))) void
+k_tls_open_chacha_packed(TlsArgs a) {
+    __shared__ uint4 wins[kCryptWaves][256];
+    uint8_t* win = reinterpret_cast<uint8_t*>(wins[threadIdx.x >> 6]);
+    if (!(a.n_total[2] & 4u)) return;  // no short ChaCha20-Poly1305 record
+    const uint32_t n = a.n_total[0];
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (uint32_t g = blockIdx.x * kCryptWaves + wave; g * kPack < n; g += gridDim.x * kCryptWaves)
+        if (!group_has_long(a, g, n)) chacha_open_packed(a, g * kPack, win);
 }
 
 // seal descriptor r checked against the contract (key slot, key, content size, buffers) and
@@ -1633,6 +1868,7 @@ int uvhttp_tls_gpu_open_records(uvhttp_tls_gpu_engine_t* e, const uint8_t* wire,
     const int tk = tls_timing_begin(e, s);
     hipLaunchKernelGGL(k_tls_open, dim3(grid), dim3(kCryptWG), 0, s, a);
     hipLaunchKernelGGL(k_tls_open_chacha, dim3(grid), dim3(kCryptWG), 0, s, a);
+    hipLaunchKernelGGL(k_tls_open_chacha_packed, dim3(grid), dim3(kCryptWG), 0, s, a);
     tls_timing_end(e, tk, s);
     hipLaunchKernelGGL(k_tls_finalize, dim3(nb), dim3(kBlock), 0, s, a);
     hipLaunchKernelGGL(k_tls_fixup, dim3(n_streams), dim3(kBlock), 0, s, a);
