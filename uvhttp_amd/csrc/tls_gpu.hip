@@ -396,6 +396,10 @@ __device__ inline uint64_t record_cap(uint32_t version, uint32_t cipher, uint32_
 // (measured, TLS 1.3 GiB/s per-record -> packed: 256 B 34 -> 122, 1 KiB 128 -> 323, 2 KiB
 // 249 -> 466, 4 KiB 463 -> 599, 8 KiB 698 -> 726; 16 KiB 913 -> 812, so 16 KiB stays per record)
 constexpr uint32_t kPackMaxLen = 8192 + 1 + 16;
+// AES-GCM records up to this length (4 KiB of content with either version's overhead) are
+// opened kPack to a wave (k_tls_open_aes_packed); measured TLS 1.3 GiB/s per-record -> packed:
+// 256 B 32 -> 79, 1 KiB 93 -> 163, 4 KiB 233 -> 264, 8 KiB 311 -> 297 (so 8 KiB stays per record)
+constexpr uint32_t kPackMaxLenAes = 4096 + 1 + 24;
 
 template <bool WRITE>
 __device__ inline uint32_t walk(const TlsArgs& a, uint32_t s, uint64_t* cap_out, uint32_t first,
@@ -413,7 +417,8 @@ __device__ inline uint32_t walk(const TlsArgs& a, uint32_t s, uint64_t* cap_out,
         const uint32_t type = p[pos], ver = be16(p + pos + 1), len = be16(p + pos + 3);
         const int32_t hs = header_status(k.version, k.cipher, type, ver, len);
         if (!hs && L - pos - 5 < len) break;  // incomplete: waits for more bytes
-        if (size_bits && !hs) *size_bits |= len <= kPackMaxLen ? 1u : 2u;
+        if (size_bits && !hs)
+            *size_bits |= len <= (k.cipher == UVHTTP_TLS_CIPHER_AES_GCM ? kPackMaxLenAes : kPackMaxLen) ? 1u : 2u;
         if (WRITE) {
             RecWork w;
             w.rec_off = st.begin + pos;
@@ -473,11 +478,14 @@ __global__ __launch_bounds__(kBlock) void k_tls_walk_count(TlsArgs a) {
     // which AEADs the block's records use, in the top byte of its record count: the crypto
     // kernel of an AEAD no record uses returns at once
     // (bit 0 AES-GCM, bit 1 ChaCha20-Poly1305, bits 2 / 3: ChaCha records short / long enough
-    // for the packed / per-record kernel)
+    // for the packed / per-record kernel, bits 4 / 5: the same for AES-GCM)
     const bool cc = n && cipher == UVHTTP_TLS_CIPHER_CHACHA20_POLY1305;
-    const uint64_t m = (__syncthreads_or(n && cipher == UVHTTP_TLS_CIPHER_AES_GCM) ? 1u : 0u) |
+    const bool ag = n && cipher == UVHTTP_TLS_CIPHER_AES_GCM;
+    const uint64_t m = (__syncthreads_or(ag) ? 1u : 0u) |
                        (__syncthreads_or(cc) ? 2u : 0u) | (__syncthreads_or(cc && (sizes & 1)) ? 4u : 0u) |
-                       (__syncthreads_or(cc && (sizes & 2)) ? 8u : 0u);
+                       (__syncthreads_or(cc && (sizes & 2)) ? 8u : 0u) |
+                       (__syncthreads_or(ag && (sizes & 1)) ? 16u : 0u) |
+                       (__syncthreads_or(ag && (sizes & 2)) ? 32u : 0u);
     if (threadIdx.x == 0) {
         a.blk[2 * blockIdx.x] = tn | (m << 56);
         a.blk[2 * blockIdx.x + 1] = tc;
@@ -501,7 +509,7 @@ __global__ __launch_bounds__(kBlock) void k_tls_walk_scan(TlsArgs a, uint32_t n_
     uint64_t pc = block_exclusive_sum<uint64_t>(rc, &tc);
     uint32_t mask = 0;
 #pragma unroll
-    for (int bit = 0; bit < 4; ++bit) mask |= __syncthreads_or(m & (1u << bit)) ? 1u << bit : 0u;
+    for (int bit = 0; bit < 6; ++bit) mask |= __syncthreads_or(m & (1u << bit)) ? 1u << bit : 0u;
     for (uint32_t b = beg; b < fin; ++b) {
         const uint64_t vn = a.blk[2 * b] & kCount, vc = a.blk[2 * b + 1];
         a.blk[2 * b] = pn;
@@ -1059,126 +1067,6 @@ __device__ inline void fill_te(const uint32_t* te0, uint32_t* te) {
 #define TLS_WG_TREE 1      // 1: the lane combine of the workgroup's 4 records shared through LDS
 #endif
 
-// record status from the AEAD result (lane 0): TLS 1.3 type = last non-zero inner byte
-__device__ inline void open_status(const TlsArgs& a, uint32_t r, const CryptOut& co, bool is13,
-                                   uint32_t clen, uint32_t outer_type) {
-    if ((threadIdx.x & 63) != 0) return;
-    int32_t st;
-    uint32_t type = 0, cl = 0;
-    if (!co.tag_ok) {
-        st = UVHTTP_TLS_REC_ERR_BAD_MAC;
-    } else if (is13) {
-        if (co.last_nz == 0) {
-            st = UVHTTP_TLS_REC_ERR_EMPTY;
-        } else {
-            type = co.last_nz & 0xFF;
-            cl = (co.last_nz >> 8) - 1;
-            st = type == 23 ? UVHTTP_TLS_REC_OK : UVHTTP_TLS_REC_CONTROL;
-        }
-    } else {
-        type = outer_type;
-        cl = clen;
-        st = type == 23 ? UVHTTP_TLS_REC_OK : UVHTTP_TLS_REC_CONTROL;
-    }
-    a.work[r].status = st;
-    a.work[r].type = type;
-    a.work[r].content_len = cl;
-}
-
-__global__ CRYPT_ATTR void k_tls_open(TlsArgs a) {
-    __shared__ uint32_t te[256 * TLS_TE_COPIES];
-    __shared__ U128 tabs[kCryptWaves][7][16];
-#if TLS_GHASH8
-    __shared__ U128 t8s[kCryptWaves][256];
-    U128* t8 = t8s[threadIdx.x >> 6];
-#else
-    U128* t8 = nullptr;
-#endif
-#if TLS_WG_TREE
-    __shared__ U128 s_acc[kCryptWaves][64];
-#endif
-    if (!(a.n_total[2] & (1u << UVHTTP_TLS_CIPHER_AES_GCM))) return;  // no AES-GCM record
-    fill_te(a.te0, te);
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t n = a.n_total[0];
-    uint32_t cur = 0xFFFFFFFFu, cur8 = 0xFFFFFFFFu;  // key slots of the wave's 4-bit / 8-bit tables
-    // rounds are workgroup-uniform (the shared combine has barriers); r is wave-uniform:
-    // readfirstlane makes the record and key-schedule loads scalar
-    for (uint32_t rb = blockIdx.x * kCryptWaves; rb < n; rb += gridDim.x * kCryptWaves) {
-        const uint32_t r = __builtin_amdgcn_readfirstlane(rb + wave);
-        RecWork w;
-        bool active = r < n;
-        if (active) {
-            w = a.work[r];
-            active = w.status == 0;  // header failure: nothing to open
-        }
-        Lanes L{U128{0, 0}, {0, 0, 0, 0}, 0, 0};
-        const KeySched* ks = a.sched + (active ? w.key : 0);
-        const uint8_t* rec = a.wire + (active ? w.rec_off : 0);
-        bool is13 = false;
-        uint32_t clen = 0;
-        const uint8_t* ct = rec;
-        if (active) active = ks->cipher == UVHTTP_TLS_CIPHER_AES_GCM;  // else k_tls_open_chacha
-        if (active) {
-            if (w.key != cur) {
-                load_tables(ks, tabs[wave]);
-                cur = w.key;
-            }
-            // the 8-bit table serves only the Horner steps of records over 62 blocks: a run of
-            // small records under changing keys skips building it
-            const uint32_t cl = w.len - (ks->version == UVHTTP_TLS_VERSION_13 ? 16u : 24u);
-            if (TLS_GHASH8 && (cl + 15) / 16 + 2 > 64 && cur8 != w.key) {
-                gf_table8(tabs[wave][6], t8);
-                cur8 = w.key;
-            }
-            is13 = ks->version == UVHTTP_TLS_VERSION_13;
-            uint32_t nonce[3];
-            U128 aad;
-            uint32_t alen;
-            if (is13) {
-                nonce[0] = ks->iv[0];
-                nonce[1] = ks->iv[1] ^ (uint32_t)(w.seq >> 32);
-                nonce[2] = ks->iv[2] ^ (uint32_t)w.seq;
-                uint32_t h[4];
-                load_part(rec, 0, 5, h);
-                aad = le_to_block(h);
-                alen = 5;
-                clen = w.len - 16;
-                ct = rec + 5;
-            } else {
-                uint32_t ex[4];
-                load_part(rec + 5, 0, 8, ex);
-                nonce[0] = ks->iv[0];
-                nonce[1] = bswap32(ex[0]);
-                nonce[2] = bswap32(ex[1]);
-                clen = w.len - 24;
-                aad = U128{w.seq, ((uint64_t)rec[0] << 56) | (0x0303ull << 40) | ((uint64_t)clen << 24)};
-                alen = 13;
-                ct = rec + 13;
-            }
-            const uint32_t wlen = is13 ? (clen > 0 ? clen - 1 : 0) : clen;
-            L = gcm_lanes<false>(ks, te, lane & (TLS_TE_COPIES - 1), tabs[wave], t8, nonce, aad,
-                                 alen, ct, nullptr, clen, a.out + w.spec_off, wlen, nullptr, 0, 0,
-                                 is13);
-        }
-#if TLS_WG_TREE
-        // a round with no AES-GCM record in the workgroup (ChaCha20-Poly1305 records, header
-        // failures) skips the combine: its serial multiplies are pure latency
-        U128 ghash{0, 0};
-        if (__syncthreads_or(active)) {
-            s_acc[wave][lane] = L.acc;
-            __syncthreads();
-            wg_tree(s_acc, tabs);
-            ghash = s_acc[wave][0];
-        }
-#else
-        const U128 ghash = active ? wave_tree(L.acc, tabs[wave]) : U128{0, 0};
-#endif
-        if (!active) continue;
-        open_status(a, r, gcm_finish<false>(L, ghash, ct, nullptr, clen), is13, clen, rec[0]);
-    }
-}
-
 // Packed ChaCha20-Poly1305 open for records up to 8 KiB: a group of kPack consecutive work
 // items shares one wave, kSeg lanes per record (segment k = lanes [k kSeg, (k+1) kSeg)), so a
 // small record no longer costs a whole wave round of the block function plus its own one-time
@@ -1227,13 +1115,14 @@ __device__ inline void open_status_at(const TlsArgs& a, uint32_t r, const CryptO
 
 // does group g (work items [g kPack, g kPack + kPack)) hold a ChaCha record too long to pack?
 // (wave-uniform; both ChaCha kernels decide the same way)
-__device__ inline bool group_has_long(const TlsArgs& a, uint32_t g, uint32_t n) {
+__device__ inline bool group_has_long(const TlsArgs& a, uint32_t g, uint32_t n,
+                                      uint32_t cipher = UVHTTP_TLS_CIPHER_CHACHA20_POLY1305) {
     const uint32_t lane = threadIdx.x & 63;
+    const uint32_t lim = cipher == UVHTTP_TLS_CIPHER_AES_GCM ? kPackMaxLenAes : kPackMaxLen;
     bool big = false;
     if (lane < kPack && g * kPack + lane < n) {
         const RecWork w = a.work[g * kPack + lane];
-        big = w.status == 0 && w.len > kPackMaxLen &&
-              a.sched[w.key].cipher == UVHTTP_TLS_CIPHER_CHACHA20_POLY1305;
+        big = w.status == 0 && w.len > lim && a.sched[w.key].cipher == cipher;
     }
     return __builtin_amdgcn_readfirstlane(__ballot(big) != 0 ? 1u : 0u) != 0;
 }
@@ -1380,6 +1269,281 @@ __device__ void chacha_open_packed(const TlsArgs& a, uint32_t r0, uint8_t* win) 
         CryptOut co{t4[0] == tag[0] && t4[1] == tag[1] && t4[2] == tag[2] && t4[3] == tag[3], last_nz};
         open_status_at(a, r, co, is13, clen, otype);
     }
+}
+
+// Packed AES-GCM open for records up to kPackMaxLenAes: a group of kPack consecutive work items
+// on one wave, kSeg lanes per record — the same segment layout as the packed ChaCha kernel.
+// Segment k stages its key's round keys and the 4-bit GHASH tables of H, H^2 ... H^16 in LDS
+// (the record's key differs per segment); lane u of round j takes GHASH position kSeg j + u of
+// the record's left-padded sequence (AAD, ciphertext blocks, length block), runs AES-CTR for it
+// from the shared T-table and Horner with multiplier H^16; the segment's lanes combine in four
+// shuffle levels (H, H^2, H^4, H^8) and a final x H.
+__device__ inline U128 shfl_down128_seg(U128 v, int d) {
+    const uint32_t a = __shfl_down((uint32_t)v.hi, d, kSeg), b = __shfl_down((uint32_t)(v.hi >> 32), d, kSeg);
+    const uint32_t c = __shfl_down((uint32_t)v.lo, d, kSeg), e = __shfl_down((uint32_t)(v.lo >> 32), d, kSeg);
+    return U128{((uint64_t)b << 32) | a, ((uint64_t)e << 32) | c};
+}
+
+__device__ void aes_open_packed(const TlsArgs& a, uint32_t r0, const uint32_t* te, uint32_t (*s_rk)[64],
+                                U128 (*s_tab)[kSegLog + 1][16]) {
+    const uint32_t lane = threadIdx.x & 63, k = lane / kSeg, u = lane % kSeg;
+    const uint32_t r = r0 + k;
+    bool act = r < a.n_total[0];
+    RecWork w;
+    if (act) {
+        w = a.work[r];
+        act = w.status == 0 && a.sched[w.key].cipher == UVHTTP_TLS_CIPHER_AES_GCM;
+    }
+    const KeySched* ks = a.sched + (act ? w.key : 0);
+    if (act) {  // the segment's round keys and H^(2^t) tables, t = 0..4
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (u + 16 * i < 60) s_rk[k][u + 16 * i] = ks->rk[u + 16 * i];
+#pragma unroll
+        for (int i = 0; i <= kSegLog; ++i) s_tab[k][i][u] = ks->tab[i][u];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint32_t nonce[3] = {0, 0, 0}, clen = 0, wlen = 0, alen = 0, nr = 10, otype = 0;
+    U128 aad{0, 0};
+    bool is13 = false;
+    const uint8_t* rec = a.wire;
+    const uint8_t* ct = a.wire;
+    uint8_t* dst = a.out;
+    if (act) {
+        is13 = ks->version == UVHTTP_TLS_VERSION_13;
+        nr = ks->nr;
+        rec = a.wire + w.rec_off;
+        dst = a.out + w.spec_off;
+        otype = rec[0];
+        if (is13) {
+            nonce[0] = ks->iv[0];
+            nonce[1] = ks->iv[1] ^ (uint32_t)(w.seq >> 32);
+            nonce[2] = ks->iv[2] ^ (uint32_t)w.seq;
+            uint32_t h[4];
+            load_part(rec, 0, 5, h);
+            aad = le_to_block(h);
+            alen = 5;
+            clen = w.len - 16;
+            ct = rec + 5;
+        } else {
+            uint32_t ex[4];
+            load_part(rec + 5, 0, 8, ex);
+            nonce[0] = ks->iv[0];
+            nonce[1] = bswap32(ex[0]);
+            nonce[2] = bswap32(ex[1]);
+            clen = w.len - 24;
+            aad = U128{w.seq, ((uint64_t)otype << 56) | (0x0303ull << 40) | ((uint64_t)clen << 24)};
+            alen = 13;
+            ct = rec + 13;
+        }
+        wlen = is13 ? (clen > 0 ? clen - 1 : 0) : clen;
+    }
+    const uint32_t nblk = (clen + 15) / 16;
+    const uint32_t m = act ? nblk + 2 : 0;             // AAD, ciphertext blocks, length block
+    const uint32_t Jr = (m + kSeg - 1) / kSeg;          // this segment's rounds
+    const uint32_t pad = kSeg * Jr - m;                 // left padding (< kSeg)
+    uint32_t J = Jr;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint32_t o = __shfl_xor(J, d, 64);
+        if (o > J) J = o;
+    }
+    J = __builtin_amdgcn_readfirstlane(J);
+    const uint32_t lane_te = lane & (TLS_TE_COPIES - 1);
+    auto te_lds = [&](uint32_t x) { return te[(x << kTeShift) | lane_te]; };
+    U128 acc{0, 0};
+    uint32_t ej0[4] = {0, 0, 0, 0};
+    LastNz nz{0, {0, 0, 0, 0}};
+    for (uint32_t j = 0; j < J; ++j) {
+        const int32_t q = (int32_t)(kSeg * j + u) - (int32_t)pad;
+        uint32_t cb[4] = {nonce[0], nonce[1], nonce[2], q <= 0 ? 1u : (uint32_t)q + 1u};
+        aes_encrypt(s_rk[k], nr, cb, te_lds);
+        if (j >= Jr) continue;
+        U128 x{0, 0};
+        if (q == 0) {
+            x = aad;
+            ej0[0] = cb[0], ej0[1] = cb[1], ej0[2] = cb[2], ej0[3] = cb[3];
+        } else if (q > 0 && (uint32_t)q <= nblk) {
+            const uint32_t off = 16 * ((uint32_t)q - 1);
+            const int nb = clen - off < 16 ? (int)(clen - off) : 16;
+            uint32_t d[4];
+            load_part(ct + off, 0, nb, d);
+            x = le_to_block(d);
+            uint32_t pt[4];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int lo = 4 * b;
+                pt[b] = (d[b] ^ bswap32(cb[b])) &
+                        (nb >= lo + 4 ? 0xFFFFFFFFu : nb <= lo ? 0u : ((1u << (8 * (nb - lo))) - 1u));
+            }
+            if (is13) nz.see(off, pt);
+            if (off < wlen) store_part(dst + off, wlen - off < 16 ? (int)(wlen - off) : 16, pt);
+        } else if ((uint32_t)q == m - 1) {
+            x = U128{(uint64_t)alen * 8, (uint64_t)clen * 8};
+        }
+        acc = j == 0 ? x : gf_xor(gf_mul_tab(acc, s_tab[k][kSegLog]), x);  // Horner, H^16
+    }
+#pragma unroll
+    for (int t = 0; t < kSegLog; ++t) acc = gf_xor(gf_mul_tab(acc, s_tab[k][t]), shfl_down128_seg(acc, 1 << t));
+    acc = gf_mul_tab(acc, s_tab[k][0]);
+    uint32_t e[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) e[b] = __shfl(ej0[b], (int)pad, kSeg);  // E(K, J0): round 0, lane pad
+    const U128 tag{acc.hi ^ (((uint64_t)e[0] << 32) | e[1]), acc.lo ^ (((uint64_t)e[2] << 32) | e[3])};
+    uint32_t last_nz = nz.resolve();
+#pragma unroll
+    for (int d = kSeg / 2; d >= 1; d >>= 1) {
+        const uint32_t o = __shfl_xor(last_nz, d, kSeg);
+        if (o > last_nz) last_nz = o;
+    }
+    if (act && u == 0) {
+        uint32_t t4[4];
+        load_part(ct + clen, 0, 16, t4);
+        const U128 want = le_to_block(t4);
+        const CryptOut co{want.hi == tag.hi && want.lo == tag.lo, last_nz};
+        open_status_at(a, r, co, is13, clen, otype);
+    }
+}
+
+// record status from the AEAD result (lane 0): TLS 1.3 type = last non-zero inner byte
+__device__ inline void open_status(const TlsArgs& a, uint32_t r, const CryptOut& co, bool is13,
+                                   uint32_t clen, uint32_t outer_type) {
+    if ((threadIdx.x & 63) != 0) return;
+    int32_t st;
+    uint32_t type = 0, cl = 0;
+    if (!co.tag_ok) {
+        st = UVHTTP_TLS_REC_ERR_BAD_MAC;
+    } else if (is13) {
+        if (co.last_nz == 0) {
+            st = UVHTTP_TLS_REC_ERR_EMPTY;
+        } else {
+            type = co.last_nz & 0xFF;
+            cl = (co.last_nz >> 8) - 1;
+            st = type == 23 ? UVHTTP_TLS_REC_OK : UVHTTP_TLS_REC_CONTROL;
+        }
+    } else {
+        type = outer_type;
+        cl = clen;
+        st = type == 23 ? UVHTTP_TLS_REC_OK : UVHTTP_TLS_REC_CONTROL;
+    }
+    a.work[r].status = st;
+    a.work[r].type = type;
+    a.work[r].content_len = cl;
+}
+
+__global__ CRYPT_ATTR void k_tls_open(TlsArgs a) {
+    __shared__ uint32_t te[256 * TLS_TE_COPIES];
+    __shared__ U128 tabs[kCryptWaves][7][16];
+#if TLS_GHASH8
+    __shared__ U128 t8s[kCryptWaves][256];
+    U128* t8 = t8s[threadIdx.x >> 6];
+#else
+    U128* t8 = nullptr;
+#endif
+#if TLS_WG_TREE
+    __shared__ U128 s_acc[kCryptWaves][64];
+#endif
+    if (!(a.n_total[2] & 32u)) return;  // no AES-GCM record too long to pack
+    fill_te(a.te0, te);
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t n = a.n_total[0];
+    uint32_t cur = 0xFFFFFFFFu, cur8 = 0xFFFFFFFFu;  // key slots of the wave's 4-bit / 8-bit tables
+    // a wave takes a group of kPack records holding a long AES-GCM record (the others go to
+    // k_tls_open_aes_packed) and opens them one per round; rounds are workgroup-uniform (the
+    // shared combine has barriers); r is wave-uniform: readfirstlane makes the record and
+    // key-schedule loads scalar
+    for (uint32_t gb = blockIdx.x * kCryptWaves; gb * kPack < n; gb += gridDim.x * kCryptWaves) {
+    const uint32_t g = __builtin_amdgcn_readfirstlane(gb + wave);
+    const bool grp = g * kPack < n && group_has_long(a, g, n, UVHTTP_TLS_CIPHER_AES_GCM);
+    for (uint32_t i = 0; i < kPack; ++i) {
+        const uint32_t r = g * kPack + i;
+        RecWork w;
+        bool active = grp && r < n;
+        if (active) {
+            w = a.work[r];
+            active = w.status == 0;  // header failure: nothing to open
+        }
+        Lanes L{U128{0, 0}, {0, 0, 0, 0}, 0, 0};
+        const KeySched* ks = a.sched + (active ? w.key : 0);
+        const uint8_t* rec = a.wire + (active ? w.rec_off : 0);
+        bool is13 = false;
+        uint32_t clen = 0;
+        const uint8_t* ct = rec;
+        if (active) active = ks->cipher == UVHTTP_TLS_CIPHER_AES_GCM;  // else k_tls_open_chacha
+        if (active) {
+            if (w.key != cur) {
+                load_tables(ks, tabs[wave]);
+                cur = w.key;
+            }
+            // the 8-bit table serves only the Horner steps of records over 62 blocks: a run of
+            // small records under changing keys skips building it
+            const uint32_t cl = w.len - (ks->version == UVHTTP_TLS_VERSION_13 ? 16u : 24u);
+            if (TLS_GHASH8 && (cl + 15) / 16 + 2 > 64 && cur8 != w.key) {
+                gf_table8(tabs[wave][6], t8);
+                cur8 = w.key;
+            }
+            is13 = ks->version == UVHTTP_TLS_VERSION_13;
+            uint32_t nonce[3];
+            U128 aad;
+            uint32_t alen;
+            if (is13) {
+                nonce[0] = ks->iv[0];
+                nonce[1] = ks->iv[1] ^ (uint32_t)(w.seq >> 32);
+                nonce[2] = ks->iv[2] ^ (uint32_t)w.seq;
+                uint32_t h[4];
+                load_part(rec, 0, 5, h);
+                aad = le_to_block(h);
+                alen = 5;
+                clen = w.len - 16;
+                ct = rec + 5;
+            } else {
+                uint32_t ex[4];
+                load_part(rec + 5, 0, 8, ex);
+                nonce[0] = ks->iv[0];
+                nonce[1] = bswap32(ex[0]);
+                nonce[2] = bswap32(ex[1]);
+                clen = w.len - 24;
+                aad = U128{w.seq, ((uint64_t)rec[0] << 56) | (0x0303ull << 40) | ((uint64_t)clen << 24)};
+                alen = 13;
+                ct = rec + 13;
+            }
+            const uint32_t wlen = is13 ? (clen > 0 ? clen - 1 : 0) : clen;
+            L = gcm_lanes<false>(ks, te, lane & (TLS_TE_COPIES - 1), tabs[wave], t8, nonce, aad,
+                                 alen, ct, nullptr, clen, a.out + w.spec_off, wlen, nullptr, 0, 0,
+                                 is13);
+        }
+#if TLS_WG_TREE
+        // a round with no AES-GCM record in the workgroup (ChaCha20-Poly1305 records, header
+        // failures) skips the combine: its serial multiplies are pure latency
+        U128 ghash{0, 0};
+        if (__syncthreads_or(active)) {
+            s_acc[wave][lane] = L.acc;
+            __syncthreads();
+            wg_tree(s_acc, tabs);
+            ghash = s_acc[wave][0];
+        }
+#else
+        const U128 ghash = active ? wave_tree(L.acc, tabs[wave]) : U128{0, 0};
+#endif
+        if (!active) continue;
+        open_status(a, r, gcm_finish<false>(L, ghash, ct, nullptr, clen), is13, clen, rec[0]);
+    }
+    }
+}
+
+__global__ CRYPT_ATTR void k_tls_open_aes_packed(TlsArgs a) {
+    __shared__ uint32_t te[256 * TLS_TE_COPIES];
+    __shared__ uint32_t s_rk[kCryptWaves][kPack][64];
+    __shared__ U128 s_tab[kCryptWaves][kPack][kSegLog + 1][16];
+    if (!(a.n_total[2] & 16u)) return;  // no short AES-GCM record
+    fill_te(a.te0, te);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t n = a.n_total[0];
+    for (uint32_t g = blockIdx.x * kCryptWaves + wave; g * kPack < n; g += gridDim.x * kCryptWaves)
+        if (!group_has_long(a, g, n, UVHTTP_TLS_CIPHER_AES_GCM))
+            aes_open_packed(a, g * kPack, te, s_rk[wave], s_tab[wave]);
 }
 
 // ChaCha20-Poly1305 records (the AES-GCM kernel skips them): one wave per record, no shared
@@ -1867,6 +2031,7 @@ int uvhttp_tls_gpu_open_records(uvhttp_tls_gpu_engine_t* e, const uint8_t* wire,
     const uint32_t grid = need < (uint32_t)e->crypt_grid ? (need ? need : 1) : (uint32_t)e->crypt_grid;
     const int tk = tls_timing_begin(e, s);
     hipLaunchKernelGGL(k_tls_open, dim3(grid), dim3(kCryptWG), 0, s, a);
+    hipLaunchKernelGGL(k_tls_open_aes_packed, dim3(grid), dim3(kCryptWG), 0, s, a);
     hipLaunchKernelGGL(k_tls_open_chacha, dim3(grid), dim3(kCryptWG), 0, s, a);
     hipLaunchKernelGGL(k_tls_open_chacha_packed, dim3(grid), dim3(kCryptWG), 0, s, a);
     tls_timing_end(e, tk, s);
