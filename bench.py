@@ -14,6 +14,12 @@ elapsed time over ranks is used.
 
 --config c5 runs BASELINE config C5 instead: 8 388 608 x 64 KiB frames in total, split into
 contiguous per-rank shards (strong scaling), each decoded in resident 1 048 576-frame passes.
+It is the default whenever more than one GPU runs (BASELINE config 5, "reported at 1/2/4/8
+GPUs"); the N=1 default (C3) also times C5 on its one GPU ("c5_1gpu") so the curve has a base.
+
+Launch: under torch.distributed.run (RANK/WORLD_SIZE set) every process is one rank.  Started
+directly with --gpus N > 1, this process spawns the N rank processes itself (before anything
+touches a GPU), waits for them and prints rank 0's line.
 
 Rank 0 prints ONE JSON line.  `roofline` comes from HIP events bracketing the payload kernel
 on its stream during the timed steps; `cpu_baseline` times the CPU port of the reference path
@@ -136,22 +142,27 @@ def cpu_baseline(cfg_name, target_s=10.0):
         "stream_decode_16k_reads": round(stream_gibs, 3),
         "stream_decode_sample": f"process_data fed 16 KiB reads, {spasses} passes in {el2:.1f} s",
         "compiler": cc.splitlines()[0] if cc else "gcc", "flags": "-O2 -DNDEBUG",
-        "cpu": cpu_model(), "host_threads": os.cpu_count(),
+        "cpu": cpu_model(), "machine_cpus": os.cpu_count(), "process_cpus": _cpu_share(),
         "multi_thread": mt,
     }
+
+
+def _cpu_share():
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
 
 
 def cpu_baseline_threads(L, orc, cfg_name, seconds):
     """SURVEY §8(d)'s all-cores variant: T threads, one independent connection stream each
     (its own ~32 MiB sample of the workload), header parse + apply_mask, timed together.
-    T = this process's CPU share (16 on the GPU box; UVHTTP_WS_CPU_THREADS overrides)."""
+    T = the CPUs this process may run on, at most 16 (the GPU box grants each job a 16-CPU
+    share of a larger machine, so "all cores" here means that share; machine_cpus in the
+    record is the whole host).  UVHTTP_WS_CPU_THREADS overrides."""
     import threading
     n, plen, frag, _ = CONFIGS[cfg_name]
-    try:
-        share = len(os.sched_getaffinity(0))
-    except AttributeError:
-        share = os.cpu_count() or 1
-    T = int(os.environ.get("UVHTTP_WS_CPU_THREADS", min(16, share)))
+    T = int(os.environ.get("UVHTTP_WS_CPU_THREADS", min(16, _cpu_share())))
     sample = max(1, min(n, (32 << 20) // max(plen, 1)))
     bufs = [orc.gen_frames(sample, plen, SEED + 1 + t, fragmented=frag, total=sample)
             for t in range(T)]
@@ -177,7 +188,8 @@ def cpu_baseline_threads(L, orc, cfg_name, seconds):
         x.join()
     el = time.perf_counter() - t0
     return {"value": round(sum(done) / el / GIB, 3), "unit": "GiB/s", "cores": T,
-            "sample": f"{T} threads x {sample} frames x {plen} B, {el:.1f} s"}
+            "sample": f"{T} threads x {sample} frames x {plen} B, {el:.1f} s",
+            "note": "all CPUs granted to this process (<= 16), one connection stream each"}
 
 
 def pmc_traffic(cfg_name, mode):
@@ -193,138 +205,264 @@ def pmc_traffic(cfg_name, mode):
         return None
 
 
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n):
+    """`python bench.py --gpus N` without a launcher: start N rank processes of this script
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, one GPU each), wait for all of them and
+    pass rank 0's JSON line through.  Called before anything in this process touches a GPU, so
+    the children are fresh processes, never an exec of a GPU-initialised one."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env, stdout=subprocess.PIPE if r == 0 else None,
+                                      text=True))
+    out0, _ = procs[0].communicate()
+    rcs = [p.wait() for p in procs]
+    sys.stdout.write(out0)
+    sys.stdout.flush()
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+class StubWorkload:
+    """--stub (tests only): the launcher, rank bootstrap, barrier, timing and reporting of the
+    real run with a host sleep as the step — no GPU, no library."""
+
+    def __init__(self, args, cfg, rank, world, local):
+        _, self.plen, _, _ = CONFIGS[cfg]
+        self.first, self.n, self.passes = shard_plan(cfg, rank, world)
+        self.stride = self.plen + header_size(self.plen) + 4
+        self.kernel = "stub"
+
+    def step(self):
+        time.sleep(0.001 * self.passes)
+
+    def sync(self):
+        pass
+
+    def set_timing(self, on):
+        pass
+
+    def kernel_time(self):
+        return 0.0, 0
+
+    def check(self):
+        pass
+
+    def close(self):
+        pass
+
+
+class GpuWorkload:
+    """One rank's shard of a config, resident in HBM, decoded through the C-ABI."""
+
+    def __init__(self, args, cfg, rank, world, local):
+        import torch
+        import uvhttp_amd as U
+        self.torch = torch
+        torch.cuda.set_device(local)
+        dev = f"cuda:{local}"
+        mode = args.mode
+        _, plen, frag, mm = CONFIGS[cfg]
+        first, n, passes = shard_plan(cfg, rank, world)
+        self.plen, self.n, self.passes, self.mode, self.mm = plen, n, passes, mode, mm
+        self.stride = stride = U.gen_frame_stride(plen)
+        self.wire_len = wire_len = stride * n
+        self.eng = eng = U.GpuEngine(local)
+        self.stream = stream = torch.cuda.current_stream(local)
+        self.wire = torch.empty(wire_len + 64, dtype=torch.uint8, device=dev)
+        eng.gen_frames(self.wire, n, plen, SEED + first, opcode0=2, fragmented=frag, stream=stream)
+        self.desc, self.summ = eng.alloc_outputs(n)
+        self.arena = self.msgs = None
+        if mode == "compact":
+            self.arena = torch.empty(n * plen + 64, dtype=torch.uint8, device=dev)
+            self.msgs = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+        eng.reserve(n, wire_len, n * plen if self.arena is not None else 0)
+        self.build_dev = self.streams_dev = None
+        self.kernel = {"compact": "k_gather_compact", "build": "kb_emit",
+                       "build_masked": "kb_emit"}.get(mode, "k_unmask_inplace")
+        if mode.startswith("build"):
+            # send side: frame n payloads of the config (server echo: unmasked; client: masked)
+            import numpy as np
+            fr = np.zeros(n, dtype=[("po", "<u8"), ("pl", "<u8"), ("key", "<u4"), ("op", "u1"),
+                                    ("fin", "u1"), ("mask", "u1"), ("r0", "u1"), ("r1", "<u8")])
+            fr["po"] = np.arange(n, dtype=np.uint64) * plen
+            fr["pl"] = plen
+            fr["key"] = np.arange(n, dtype=np.uint32) * 2654435761
+            fr["op"], fr["fin"] = 2, 1
+            fr["mask"] = 1 if mode == "build_masked" else 0
+            self.build_dev = torch.from_numpy(fr.view(np.uint8).copy()).to(dev)
+            self.build_src = torch.empty(n * plen + 64, dtype=torch.uint8, device=dev)
+            self.build_src.random_(0, 256)
+            self.build_out = torch.empty(n * (plen + 14) + 64, dtype=torch.uint8, device=dev)
+            self.build_off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        if mode == "streams":
+            import numpy as np
+            conns = args.conns or (4096 if frag else n)
+            per = n // conns
+            st = np.zeros(conns, dtype=U.STREAM_DT)
+            st["begin"] = np.arange(conns, dtype=np.uint64) * per * stride
+            st["len"] = per * stride
+            st["recv_buffer_size"] = max(65536, per * stride)
+            st["max_frame_size"], st["max_message_size"], st["is_server"] = 16 << 20, mm, 1
+            if frag:  # connection k continues the message: all its frames are continuations
+                st["pending_bytes"][1:] = 1
+                st["pending_opcode"] = 2
+            self.conns = conns
+            self.streams_dev = torch.from_numpy(st.view(np.uint8).copy()).to(dev)
+            self.s_desc = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+            self.s_res = torch.empty(conns * U.STREAM_RESULT_BYTES, dtype=torch.uint8, device=dev)
+
+    def one_pass(self):
+        eng, stream = self.eng, self.stream
+        if self.build_dev is not None:
+            eng.build_frames(self.build_src, self.build_dev, self.n, self.build_out,
+                             out_off=self.build_off, stream=stream)
+        elif self.streams_dev is not None:
+            eng.decode_streams(self.wire, self.streams_dev, self.conns, self.n, desc=self.s_desc,
+                               results=self.s_res, wire_len=self.wire_len, stream=stream)
+        elif self.arena is None:
+            eng.decode_inplace(self.wire, self.n, stride=self.stride, max_message_size=self.mm,
+                               wire_len=self.wire_len, desc=self.desc, summary=self.summ,
+                               stream=stream)
+        else:
+            eng.decode_compact(self.wire, self.n, self.arena, stride=self.stride,
+                               max_message_size=self.mm, wire_len=self.wire_len, desc=self.desc,
+                               msgs=self.msgs, summary=self.summ, stream=stream)
+
+    def step(self):
+        for _ in range(self.passes):
+            self.one_pass()
+
+    def sync(self):
+        self.torch.cuda.synchronize()
+
+    def set_timing(self, on):
+        self.eng.set_timing(on)
+
+    def kernel_time(self):
+        return self.eng.kernel_time()
+
+    def check(self):
+        """Every frame of the shard must have been delivered (the decode really ran)."""
+        n = self.n
+        if self.build_dev is not None:
+            want = n * (self.stride - (0 if self.mode == "build_masked" else 4))
+            if int(self.build_off[n].item()) != want:
+                raise SystemExit("build failed")
+        elif self.streams_dev is not None:
+            rs = self.eng.read_stream_results(self.s_res, self.conns)
+            if sum(r.n_delivered for r in rs) != n or any(r.status for r in rs):
+                raise SystemExit(f"stream decode failed: {rs[0].as_dict()}")
+        else:
+            s = self.eng.read_summary(self.summ)
+            if s["n_delivered"] != n or s["status"] != 0:
+                raise SystemExit(f"decode failed: {s}")
+
+    def close(self):
+        self.eng.close()
+        for k in ("wire", "desc", "summ", "arena", "msgs", "build_src", "build_out",
+                  "streams_dev", "s_desc"):
+            setattr(self, k, None)
+        self.torch.cuda.empty_cache()
+
+
+def timed_run(wl, steps, warmup, world):
+    """W untimed steps, then exactly K timed steps bracketed by barrier + device sync on both
+    sides; returns (max elapsed over ranks, kernel ms, kernel launches)."""
+    import torch.distributed as dist
+    for _ in range(warmup):
+        wl.step()
+    wl.sync()
+    wl.check()
+    wl.kernel_time()  # discard warmup events
+    wl.set_timing(True)
+    if world > 1:
+        dist.barrier()
+    wl.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        wl.step()
+    wl.sync()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    wl.set_timing(False)
+    k_ms, k_n = wl.kernel_time()
+    wl.check()
+    return max_over_ranks(elapsed, world), k_ms, k_n
+
+
+def c5_one_gpu(args, local, steps=2, warmup=1):
+    """BASELINE C5 on this one GPU (8 resident passes of 1 048 576 frames per step): the N=1
+    point of the C5 curve the multi-GPU runs report."""
+    a = argparse.Namespace(**vars(args))
+    a.mode = "inplace"
+    wl = GpuWorkload(a, "c5", 0, 1, local)
+    el, k_ms, k_n = timed_run(wl, steps, warmup, 1)
+    n_total = CONFIGS["c5"][0]
+    out = {"value": round(n_total * wl.plen * steps / el / GIB, 2), "unit": "GiB/s",
+           "steps": steps, "ms_per_step": round(el / steps * 1e3, 3),
+           "avg_kernel_us": round(k_ms * 1e3 / k_n, 2) if k_n else None,
+           "note": "C5 8388608 x 64 KiB frames on 1 GPU: 8 resident passes of 1048576 frames"}
+    wl.close()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
+                    help="default: c3 on one GPU, c5 (strong scaling) on more")
     ap.add_argument("--mode", default="inplace",
                     choices=["inplace", "compact", "streams", "build", "build_masked"])
     ap.add_argument("--conns", type=int, default=0,
                     help="streams mode: connections the frames are split over "
                          "(default: one frame per connection, 4096 for c4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-c5-base", action="store_true",
+                    help="N=1: skip the extra C5-on-one-GPU measurement")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--e2e", action="store_true", help="also time host->device->host")
+    ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)  # launcher tests
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        if not args.stub:
+            import torch  # device_count does not initialise the GPU on this image
+            have = torch.cuda.device_count()
+            if have < args.gpus:
+                raise SystemExit(f"--gpus {args.gpus} but only {have} GPU(s) visible")
+        raise SystemExit(spawn_ranks(args.gpus))
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
+    cfg = args.config or ("c5" if world > 1 else "c3")
 
-    import torch
     import torch.distributed as dist
-    import uvhttp_amd as U
-
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    torch.cuda.set_device(local)
-    dev = f"cuda:{local}"
 
-    _, plen, frag, mm = CONFIGS[args.config]
-    first, n, passes = shard_plan(args.config, rank, world)
-    stride = U.gen_frame_stride(plen)
-    wire_len = stride * n
-    eng = U.GpuEngine(local)
-    stream = torch.cuda.current_stream(local)
-    wire = torch.empty(wire_len + 64, dtype=torch.uint8, device=dev)
-    eng.gen_frames(wire, n, plen, SEED + first, opcode0=2, fragmented=frag, stream=stream)
-    desc, summ = eng.alloc_outputs(n)
-    arena = msgs = None
-    if args.mode == "compact":
-        arena = torch.empty(n * plen + 64, dtype=torch.uint8, device=dev)
-        msgs = torch.empty(n * 32, dtype=torch.uint8, device=dev)
-    eng.reserve(n, wire_len, n * plen if arena is not None else 0)
-    streams_dev = build_dev = None
-    if args.mode.startswith("build"):
-        # send side: frame n payloads of the config (server echo: unmasked; client: masked)
-        import numpy as np
-        fr = np.zeros(n, dtype=[("po", "<u8"), ("pl", "<u8"), ("key", "<u4"), ("op", "u1"),
-                                ("fin", "u1"), ("mask", "u1"), ("r0", "u1"), ("r1", "<u8")])
-        fr["po"] = np.arange(n, dtype=np.uint64) * plen
-        fr["pl"] = plen
-        fr["key"] = np.arange(n, dtype=np.uint32) * 2654435761
-        fr["op"], fr["fin"] = 2, 1
-        fr["mask"] = 1 if args.mode == "build_masked" else 0
-        build_dev = torch.from_numpy(fr.view(np.uint8).copy()).to(dev)
-        build_src = torch.empty(n * plen + 64, dtype=torch.uint8, device=dev)
-        build_src.random_(0, 256)
-        build_out = torch.empty(n * (plen + 14) + 64, dtype=torch.uint8, device=dev)
-        build_off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-    if args.mode == "streams":
-        import numpy as np
-        conns = args.conns or (4096 if frag else n)
-        per = n // conns
-        st = np.zeros(conns, dtype=[("begin", "<u8"), ("len", "<u8"), ("rbs", "<u8"),
-                                    ("pend", "<u8"), ("pop", "<i4"), ("mf", "<i4"),
-                                    ("mm", "<i4"), ("srv", "<i4")])
-        st["begin"] = np.arange(conns, dtype=np.uint64) * per * stride
-        st["len"] = per * stride
-        st["rbs"] = max(65536, per * stride)
-        st["mf"], st["mm"], st["srv"] = 16 * 1024 * 1024, mm, 1
-        if frag:  # connection k continues the message: all its frames are continuations
-            st["pend"][1:] = 1
-            st["pop"] = 2
-        streams_dev = torch.from_numpy(st.view(np.uint8).copy()).to(dev)
-        s_desc = torch.empty(n * 32, dtype=torch.uint8, device=dev)
-        s_res = torch.empty(conns * 48, dtype=torch.uint8, device=dev)
-
-    def step():
-        for _ in range(passes):
-            one_pass()
-
-    def one_pass():
-        if build_dev is not None:
-            eng.build_frames(build_src, build_dev, n, build_out, out_off=build_off, stream=stream)
-        elif streams_dev is not None:
-            eng.decode_streams(wire, streams_dev, streams_dev.numel() // 48, n, desc=s_desc,
-                               results=s_res, wire_len=wire_len, stream=stream)
-        elif arena is None:
-            eng.decode_inplace(wire, n, stride=stride, max_message_size=mm, wire_len=wire_len,
-                               desc=desc, summary=summ, stream=stream)
-        else:
-            eng.decode_compact(wire, n, arena, stride=stride, max_message_size=mm,
-                               wire_len=wire_len, desc=desc, msgs=msgs, summary=summ,
-                               stream=stream)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if build_dev is not None:
-        if int(build_off[n].item()) != n * (stride - (0 if args.mode == "build_masked" else 4)):
-            raise SystemExit("build failed")
-    elif streams_dev is not None:
-        rs = eng.read_stream_results(s_res, streams_dev.numel() // 48)
-        if sum(r.n_delivered for r in rs) != n or any(r.status for r in rs):
-            raise SystemExit(f"stream decode failed: {rs[0].as_dict()}")
-    else:
-        s = eng.read_summary(summ)
-        if s["n_delivered"] != n or s["status"] != 0:
-            raise SystemExit(f"decode failed: {s}")
-    eng.kernel_time()  # discard warmup events
-
-    eng.set_timing(True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    eng.set_timing(False)
-    k_ms, k_n = eng.kernel_time()
-    if streams_dev is None and build_dev is None:
-        s = eng.read_summary(summ)
-        assert s["n_delivered"] == n and s["status"] == 0, s
-
-    el_max = max_over_ranks(elapsed, world)
+    wl = (StubWorkload if args.stub else GpuWorkload)(args, cfg, rank, world, local)
+    el_max, k_ms, k_n = timed_run(wl, args.steps, args.warmup, world)
+    n, plen, passes, stride = wl.n, wl.plen, wl.passes, wl.stride
     payload_per_rank = n * plen * passes
     total_payload = payload_per_rank * world * args.steps
     value = total_payload / el_max / GIB
@@ -333,15 +471,19 @@ def main():
     # frame's header+key+payload is read and its payload written; compact reads the same
     # and writes the payload into the arena.
     alg_bytes = n * ((header_size(plen) + 4 + plen) + plen)
-    if build_dev is not None:  # payload read + frame written
+    if args.mode.startswith("build"):  # payload read + frame written
         alg_bytes = n * (plen + header_size(plen) + (4 if args.mode == "build_masked" else 0) + plen)
     avg_kernel_s = (k_ms / 1e3 / k_n) if k_n else float("nan")
     achieved = alg_bytes / avg_kernel_s / 1e9 if k_n else None
-    traffic = pmc_traffic(args.config, args.mode)
+    traffic = pmc_traffic(cfg, args.mode)
+    wl.close()
 
-    e2e = None
-    if args.e2e and rank == 0:
-        e2e = e2e_rate(n, plen, stride, mm, local)
+    extra = {}
+    if rank == 0 and world == 1 and not args.stub:
+        if cfg == "c3" and args.mode == "inplace" and not args.no_c5_base:
+            extra["c5_1gpu"] = c5_one_gpu(args, local)
+        if args.e2e:
+            extra["e2e_pcie"] = e2e_rate(n, plen, stride, CONFIGS[cfg][3], local)
 
     if rank == 0:
         out = {
@@ -353,12 +495,12 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(el_max / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "strong" if args.config == "c5" else "weak",
+            "scaling": "strong" if cfg == "c5" else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (splitmix64 payload + per-frame keys, generated on device)",
             "config": {
-                "workload": WORKLOAD[args.config],
+                "workload": WORKLOAD[cfg],
                 "mode": args.mode,
                 "frames_per_gpu": n * passes,
                 "decode_passes_per_step": passes,
@@ -368,8 +510,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": {"compact": "k_gather_compact", "build": "kb_emit",
-                           "build_masked": "kb_emit"}.get(args.mode, "k_unmask_inplace"),
+                "kernel": wl.kernel,
                 "achieved": round(achieved, 1) if achieved else None,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -380,14 +521,14 @@ def main():
                 "launches_timed": k_n,
             },
         }
-        if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_seconds)
-        if e2e:
-            out["e2e_pcie"] = e2e
+        if args.stub:
+            out["stub"] = True
+        if world == 1 and not args.no_cpu_baseline and not args.stub:
+            out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
+        out.update(extra)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
-    eng.close()
 
 
 def e2e_rate(n, plen, stride, mm, local, depth=3, slot_frames=1024):

@@ -47,8 +47,15 @@
  * in record order.  out_off is the connection's base in a layout where every counted record
  * reserves its largest possible content (length - overhead, - 1 more for TLS 1.3, never
  * below 0), connections in index order from 0; out_cap >= the total wire bytes of the
- * connections always suffices.  Bytes of out outside the delivered ranges are unspecified.
+ * connections always suffices.  Bytes of out outside the delivered ranges are unspecified
+ * and MAY HOLD UNAUTHENTICATED PLAINTEXT: records are decrypted in parallel, so a record whose
+ * tag fails, and records after a connection's first undelivered record, may have had their
+ * plaintext written to their reservation before the verdict.  Read only
+ * [out_off, out_off + plain_len) of a connection (and the records' [out_off, + content_len)).
  * The ciphertext in wire is not modified.
+ *
+ * A connection's reservation is ws_prefix bytes followed by its records' reservations; its
+ * plaintext starts at out_off = reservation start + ws_prefix.
  */
 #ifndef UVHTTP_TLS_AMD_H
 #define UVHTTP_TLS_AMD_H
@@ -103,11 +110,14 @@ typedef struct {
 
 /* One connection's buffered ciphertext (32 bytes). */
 typedef struct {
-    uint64_t begin;  /* offset in wire */
-    uint64_t len;    /* bytes */
-    uint64_t seq;    /* read sequence number of the first record */
-    uint32_t key;    /* key slot */
-    uint32_t reserved;
+    uint64_t begin;     /* offset in wire */
+    uint64_t len;       /* bytes */
+    uint64_t seq;       /* read sequence number of the first record */
+    uint32_t key;       /* key slot */
+    uint32_t ws_prefix; /* bytes reserved in out directly before the plaintext (out_off -
+                           ws_prefix ...): room for what the connection's WebSocket decoder
+                           already buffers (recv_buffer[0, recv_buffer_pos)), so the decoded
+                           stream is contiguous; 0 = none */
 } uvhttp_tls_stream_t;
 
 /* One counted record (device-written, 32 bytes). */
@@ -175,6 +185,23 @@ int uvhttp_tls_gpu_open_records(uvhttp_tls_gpu_engine_t* eng, const uint8_t* wir
  * for TLS 1.3, `type` for TLS 1.2), TLS 1.2 AES-GCM explicit nonce = be64(seq), ciphertext, tag; the
  * TLS 1.3 inner plaintext is content || type with no padding.  Device pointers throughout;
  * records must not overlap src. */
+/* The TLS -> WebSocket hand-off on the device.  For every connection s: the ws_prefix bytes
+ * at prefix_src[prefix_off[s]] (its recv_buffer[0, recv_buffer_pos), staged by the caller;
+ * prefix_src may be NULL when every ws_prefix is 0) are copied to out[out_off - ws_prefix,
+ * out_off), and ws_streams[s] (the caller filled the connection state with
+ * uvhttp_ws_stream_init) gets begin = out_off - ws_prefix, len = ws_prefix + plain_len and
+ * one process_data call per delivered record:
+ * first_read = first_record, n_reads = n_delivered, read_end[first_record + k] = ws_prefix +
+ * the content of records 0..k — exactly the chunks on_websocket_read hands to process_data,
+ * one per mbedtls_ssl_read (src/uvhttp_connection.c:1128-1159; a read returns one record's
+ * content when read_buffer_size >= 16384, the reference default).  read_end has max_records
+ * entries.  Connections whose result is ERR_CAPACITY or ERR_KEY must not be decoded. */
+int uvhttp_tls_gpu_ws_streams(uvhttp_tls_gpu_engine_t* eng, const uvhttp_tls_result_t* results,
+                              const uvhttp_tls_record_t* records, uint32_t n_streams,
+                              const uvhttp_tls_stream_t* streams, const uint8_t* prefix_src,
+                              const uint64_t* prefix_off, uint8_t* out, void* ws_streams,
+                              uint64_t* read_end, void* stream);
+
 int uvhttp_tls_gpu_seal_records(uvhttp_tls_gpu_engine_t* eng, const uint8_t* src,
                                 uint64_t src_len, const uvhttp_tls_seal_t* recs,
                                 uint32_t n_records, const uvhttp_tls_key_t* keys,

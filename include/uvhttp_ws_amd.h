@@ -244,6 +244,9 @@ void uvhttp_ws_amd_set_control_hooks(uvhttp_ws_amd_context_resolver resolver,
 #define UVHTTP_WS_FRAME_ERR_MESSAGE (-8)    /* fragments exceed max_message_size (:786-791) */
 #define UVHTTP_WS_FRAME_ERR_LAYOUT (-9)     /* offset table disagrees with the frame lengths */
 #define UVHTTP_WS_FRAME_ERR_CAPACITY (-10)  /* stream decode: more frames than the desc array holds */
+#define UVHTTP_WS_FRAME_ERR_DEVICE (-11)    /* the device could not complete the call (a bounded
+                                               wait in the single-pass scan gave up): nothing was
+                                               decoded; uvhttp_ws_gpu_engine_sync reports ELAUNCH */
 
 /* Frame flags (uvhttp_ws_frame_desc_t.flags). */
 #define UVHTTP_WS_FLAG_FIN 0x01u
@@ -324,6 +327,22 @@ int uvhttp_ws_gpu_engine_set_timing(uvhttp_ws_gpu_engine_t* eng, int enable);
 int uvhttp_ws_gpu_engine_kernel_time(uvhttp_ws_gpu_engine_t* eng, double* ms,
                                      uint64_t* launches);
 const char* uvhttp_ws_gpu_engine_last_error(const uvhttp_ws_gpu_engine_t* eng);
+/* Wait for `stream` and report device-side failures of the calls made since the previous
+ * sync: UVHTTP_WS_GPU_ELAUNCH if any of them flagged UVHTTP_WS_FRAME_ERR_DEVICE (their
+ * summaries / results say so too, and nothing of them was unmasked), else OK. */
+int uvhttp_ws_gpu_engine_sync(uvhttp_ws_gpu_engine_t* eng, void* stream);
+
+/* Streams and graphs.  An engine owns one workspace, so its calls must execute one after
+ * another: when a call names a different stream than the previous call, the engine makes the
+ * new stream wait for the work already queued on the old one (an event), so calls from
+ * several streams serialise on the device instead of corrupting each other.  For concurrency
+ * use one engine per stream (the pipelines do).
+ * A call made while its stream is being captured (hipStreamBeginCapture) is graph-safe: its
+ * kernels take their epoch tag from device memory, bumped by a small kernel at the start of
+ * every replay, so replays of the same graph over changing frame bytes never accept tags a
+ * previous replay left behind.  Reserve the workspace before capturing (engine_reserve;
+ * stream decode: one uncaptured call of the same or larger shape) — a captured call that
+ * would allocate fails with EINVAL.  Kernel timing is not recorded inside a capture. */
 
 /* In-place decode: parse + validate every frame, run the fragment state machine, then
  * unmask the payload of every delivered frame in place in batch->wire (the reference
@@ -363,34 +382,51 @@ int uvhttp_ws_gpu_gen_frames(uvhttp_ws_gpu_engine_t* eng, uint8_t* d_wire, uint3
 
 /* ---- batched stateful stream decode (many connections per launch) --------------------- */
 /* One entry per connection: the bytes uvhttp_ws_process_data would hold after appending the
- * new read (recv_buffer[0, recv_buffer_pos) followed by the read), placed at wire[begin,
+ * new reads (recv_buffer[0, recv_buffer_pos) followed by the reads), placed at wire[begin,
  * begin + len), plus the connection state the decoder reads.  Streams must be ordered by
- * `begin` and must not overlap.  Frame boundaries are found on the device (one lane walks
- * each connection's headers), so no offset table is needed. */
+ * `begin` and must not overlap.  Frame boundaries are found on the device (one lane or wave
+ * walks each connection's headers), so no offset table is needed.
+ *
+ * Reads.  n_reads == 0: the bytes are ONE process_data call.  n_reads > 0: they are n_reads
+ * consecutive calls, read k ending at stream offset read_end[first_read + k] (relative to
+ * begin; non-decreasing; the last equals len; the buffered prefix belongs to call 0).  The
+ * device applies process_data's per-call rules exactly as the reference meets them when
+ * on_websocket_read feeds one libuv read or one mbedtls_ssl_read chunk per call
+ * (src/uvhttp_connection.c:1128-1164): the recv-buffer growth and its max_frame_size cap at
+ * the start of every call (src/uvhttp_websocket.c:832-857), a frame is delivered by the call
+ * that completes it, a frame whose header fails a check fails the call in which its header
+ * bytes arrive, and the calls after a failing call never run (the caller closes). */
 typedef struct {
     uint64_t begin;             /* offset of the connection's bytes in the batch wire */
     uint64_t len;               /* recv_buffer_pos + new bytes */
-    uint64_t recv_buffer_size;  /* conn->recv_buffer_size before the call */
+    uint64_t recv_buffer_size;  /* conn->recv_buffer_size before the first call */
     uint64_t pending_bytes;     /* conn->fragmented_size if conn->fragmented_message, else 0 */
     int32_t pending_opcode;     /* conn->fragmented_opcode */
     int32_t max_frame_size;     /* conn->config.max_frame_size */
     int32_t max_message_size;   /* conn->config.max_message_size */
     int32_t is_server;          /* conn->is_server */
-} uvhttp_ws_stream_t;
+    uint32_t first_read;        /* this connection's reads: read_end[first_read, +n_reads) */
+    uint32_t n_reads;           /* 0 = one call with all len bytes */
+    uint64_t reserved;
+} uvhttp_ws_stream_t;           /* 64 bytes */
 
-/* Per-connection outcome: exactly what uvhttp_ws_process_data(conn, bytes, len) returns and
- * leaves behind (src/uvhttp_websocket.c:825-1097). */
+/* Per-connection outcome: exactly what the process_data calls return and leave behind
+ * (src/uvhttp_websocket.c:825-1097). */
 typedef struct {
     uint32_t first_frame;        /* this connection's frames start at desc[first_frame] */
     uint32_t n_frames;           /* frames found: delivered + (if it failed) the failing one */
     uint32_t n_delivered;
-    int32_t status;              /* process_data's return: UVHTTP_OK or ..._INVALID_PARAM */
-    int32_t first_status;        /* UVHTTP_WS_FRAME_* of the failing frame (0 if none) */
-    uint32_t reserved;
-    uint64_t consumed_bytes;     /* complete frames drained from the front of the buffer */
-    uint64_t recv_buffer_size;   /* after the call (the buffer may have grown) */
-    uint64_t pending_bytes;      /* open fragmented message after the call (0 = none) */
-} uvhttp_ws_stream_result_t;
+    int32_t status;              /* the last call's return: UVHTTP_OK or ..._INVALID_PARAM */
+    int32_t first_status;        /* UVHTTP_WS_FRAME_* of the failure (0 if none) */
+    uint32_t calls;              /* process_data calls that ran (a failing call included) */
+    uint64_t consumed_bytes;     /* complete frames drained from the front of the stream */
+    uint64_t recv_buffer_size;   /* after the last call that ran (the buffer may have grown) */
+    uint64_t pending_bytes;      /* open fragmented message after the calls (0 = none) */
+    uint64_t buffered_end;       /* stream bytes [consumed_bytes, buffered_end) are what
+                                    recv_buffer holds afterwards (0 when the first call failed
+                                    its growth check: recv_buffer is then untouched) */
+    uint64_t reserved;
+} uvhttp_ws_stream_result_t;     /* 64 bytes */
 
 /* Decode every connection's frames in one set of launches, in place (delivered payloads
  * unmasked inside wire).  d_desc has room for max_frames; if the streams hold more frames
@@ -399,13 +435,26 @@ int uvhttp_ws_gpu_decode_streams(uvhttp_ws_gpu_engine_t* eng, uint8_t* d_wire, u
                                  const uvhttp_ws_stream_t* d_streams, uint32_t n_streams,
                                  uint32_t max_frames, uvhttp_ws_frame_desc_t* d_desc,
                                  uvhttp_ws_stream_result_t* d_results, void* stream);
+/* As decode_streams, with several process_data calls per connection: d_read_end (device,
+ * n_reads_total entries) holds the read boundaries the streams' first_read / n_reads index.
+ * A connection whose read table is malformed (out of range, decreasing, last != len) reports
+ * UVHTTP_WS_FRAME_ERR_LAYOUT and is not decoded.  decode_streams == decode_reads with no
+ * read table (every stream must then have n_reads == 0). */
+int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* eng, uint8_t* d_wire, uint64_t wire_len,
+                               const uvhttp_ws_stream_t* d_streams, uint32_t n_streams,
+                               const uint64_t* d_read_end, uint32_t n_reads_total,
+                               uint32_t max_frames, uvhttp_ws_frame_desc_t* d_desc,
+                               uvhttp_ws_stream_result_t* d_results, void* stream);
 
 /* Host side of the stream decode.  stream_init fills a descriptor from a live connection
- * (the caller copies recv_buffer[0, recv_buffer_pos) and the new read to wire[begin, ...));
- * deliver_stream then applies a decoded result to the connection exactly as process_data
- * would have: recv buffer growth, on_message / on_close / control hooks for the delivered
- * frames (fragments reassembled in conn->fragmented_message), and the undelivered tail kept
- * in recv_buffer.  `wire` and `desc` are host copies of the decoded batch. */
+ * (the caller copies recv_buffer[0, recv_buffer_pos) and the new reads to wire[begin, ...);
+ * n_reads = 0, set first_read / n_reads for several calls); deliver_stream then applies a
+ * decoded result to the connection exactly as the process_data calls would have: recv buffer
+ * growth, on_message / on_close / control hooks for the delivered frames (fragments
+ * reassembled in conn->fragmented_message), the bytes left in recv_buffer — including a
+ * failing data frame the reference had already unmasked before its fragment check rejected
+ * it (src/uvhttp_websocket.c:944 before :964-1000) — and the fragment state that check left.
+ * `wire` and `desc` are host copies of the decoded batch. */
 void uvhttp_ws_stream_init(const struct uvhttp_ws_connection* conn, uint64_t begin,
                            uint64_t len, uvhttp_ws_stream_t* out);
 uvhttp_error_t uvhttp_ws_deliver_stream(struct uvhttp_ws_connection* conn, const uint8_t* wire,

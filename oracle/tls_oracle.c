@@ -379,7 +379,7 @@ typedef struct {
 } orc_tls_key_t;
 typedef struct {
     uint64_t begin, len, seq;
-    uint32_t key, reserved;
+    uint32_t key, ws_prefix;
 } orc_tls_stream_t;
 typedef struct {
     uint64_t rec_off, out_off;
@@ -519,11 +519,11 @@ static void walk_stream(const uint8_t* wire, uint64_t wire_len, const orc_tls_st
                         const orc_tls_key_t* keys, uint32_t n_keys, uint32_t* n_rec,
                         uint64_t* cap, int* key_bad) {
     *n_rec = 0;
-    *cap = 0;
+    *cap = st->ws_prefix; /* the connection's reservation starts with the WebSocket prefix */
     *key_bad = st->key >= n_keys || !key_ok(&keys[st->key]);
     if (*key_bad) return;
     const orc_tls_key_t* k = &keys[st->key];
-    const uint64_t L = st->begin + st->len <= wire_len ? st->len : 0;
+    const uint64_t L = st->len <= wire_len && st->begin <= wire_len - st->len ? st->len : 0;
     const uint8_t* p = wire + st->begin;
     uint64_t pos = 0;
     while (L - pos >= 5) {
@@ -574,7 +574,7 @@ uint64_t oracle_tls_open_batch(const uint8_t* wire, uint64_t wire_len, const orc
         memset(r, 0, sizeof(*r));
         r->first_record = (uint32_t)rec_base;
         r->n_records = n;
-        r->out_off = out_base;
+        r->out_off = out_base + st->ws_prefix;
         r->next_seq = st->seq;
         if (kb) {
             r->status = -1;
@@ -600,14 +600,14 @@ uint64_t oracle_tls_open_batch(const uint8_t* wire, uint64_t wire_len, const orc
                 if (!status) {
                     uint8_t type;
                     uint32_t clen;
-                    status = open_record(&a, st->seq + j, p + pos, out + out_base + plain, &type,
-                                         &clen);
+                    status = open_record(&a, st->seq + j, p + pos, out + r->out_off + plain,
+                                         &type, &clen);
                     rec->type = type;
                     rec->content_len = clen;
                 }
                 rec->status = (int8_t)status;
                 if (status == T_OK) {
-                    rec->out_off = out_base + plain;
+                    rec->out_off = r->out_off + plain;
                     plain += rec->content_len;
                     r->n_delivered++;
                     r->consumed_bytes = pos + 5 + len;

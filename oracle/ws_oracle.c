@@ -179,6 +179,13 @@ size_t oracle_conn_recv_pos(const orc_conn_t* c) { return c->rbuf_pos; }
 size_t oracle_conn_recv_size(const orc_conn_t* c) { return c->rbuf_size; }
 size_t oracle_conn_frag_size(const orc_conn_t* c) { return c->frag ? c->frag_size : 0; }
 int oracle_conn_frag_pending(const orc_conn_t* c) { return c->frag != NULL; }
+int oracle_conn_frag_opcode(const orc_conn_t* c) { return c->frag_opcode; }
+/* harness: copy of recv_buffer[0, rbuf_pos) (tests compare the bytes left buffered) */
+size_t oracle_conn_recv_bytes(const orc_conn_t* c, uint8_t* out, size_t cap) {
+    const size_t n = c->rbuf_pos < cap ? c->rbuf_pos : cap;
+    if (n && out) memcpy(out, c->rbuf, n);
+    return c->rbuf_pos;
+}
 
 /* transcript record: u8 type | i32 a | u64 len | len bytes (only when record) */
 static void ev_push(orc_conn_t* c, uint8_t type, int32_t a, const uint8_t* p, uint64_t len) {

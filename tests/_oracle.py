@@ -58,6 +58,9 @@ def load():
         "oracle_conn_recv_pos": (sz, [vp]),
         "oracle_conn_recv_size": (sz, [vp]),
         "oracle_conn_frag_size": (sz, [vp]),
+        "oracle_conn_frag_opcode": (C.c_int, [vp]),
+        "oracle_conn_frag_pending": (C.c_int, [vp]),
+        "oracle_conn_recv_bytes": (sz, [vp, vp, sz]),
         "oracle_conn_events": (sz, [vp, vp, sz]),
         "oracle_process_data": (C.c_int, [vp, vp, sz]),
         "oracle_decode_batch": (C.c_int, [vp, u64, vp, u64, u32, C.c_int, C.c_int, C.c_int, vp,
@@ -130,6 +133,39 @@ class OracleConn:
     @property
     def recv_size(self):
         return self.L.oracle_conn_recv_size(self.c)
+
+    @property
+    def recv_pos(self):
+        return self.L.oracle_conn_recv_pos(self.c)
+
+    def recv_bytes(self) -> bytes:
+        n = self.L.oracle_conn_recv_pos(self.c)
+        buf = (C.c_uint8 * max(1, n))()
+        self.L.oracle_conn_recv_bytes(self.c, buf, n)
+        return bytes(buf)[:n]
+
+    @property
+    def frag_size(self):
+        return self.L.oracle_conn_frag_size(self.c)
+
+    @property
+    def frag_opcode(self):
+        return self.L.oracle_conn_frag_opcode(self.c)
+
+    @property
+    def frag_pending(self):
+        return bool(self.L.oracle_conn_frag_pending(self.c))
+
+    def process_reads(self, reads):
+        """The reference's on_websocket_read loop: process_data per read until a call fails
+        (src/uvhttp_connection.c:1128-1164).  -> (rc of the last call, calls that ran)."""
+        rc, calls = 0, 0
+        for r in reads:
+            calls += 1
+            rc = self.process_data(r)
+            if rc != 0:
+                break
+        return rc, calls
 
     @property
     def last_reason(self):
@@ -223,7 +259,7 @@ def build_frame(payload: bytes, opcode, mask, fin, key=b"\x00\x00\x00\x00", cap=
 TLS_KEY_DT = np.dtype([("key", "u1", 32), ("iv", "u1", 12), ("key_len", "<u4"),
                        ("version", "<u4"), ("cipher", "<u4"), ("reserved", "<u4", 2)])
 TLS_STREAM_DT = np.dtype([("begin", "<u8"), ("len", "<u8"), ("seq", "<u8"), ("key", "<u4"),
-                          ("reserved", "<u4")])
+                          ("ws_prefix", "<u4")])
 TLS_RECORD_DT = np.dtype([("rec_off", "<u8"), ("out_off", "<u8"), ("content_len", "<u4"),
                           ("stream", "<u4"), ("type", "u1"), ("status", "i1"),
                           ("reserved", "<u2"), ("reserved2", "<u4")])

@@ -58,3 +58,45 @@ def test_shards_and_max_reduce(world):
     assert all(a[1] == b[0] for a, b in zip(covered, covered[1:]))
     # c3: every rank decodes its own full batch (weak scaling)
     assert all(plans["c3"][1] == 65536 and plans["c3"][2] == 1 for _, plans, _ in res)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_self_spawns_ranks(world):
+    """`python bench.py --gpus N` with no launcher: the parent spawns N rank processes (before
+    any GPU call), every rank bootstraps gloo, runs the timed region between barriers, and rank
+    0's line reports N GPUs and the C5 strong-scaling workload.  --stub swaps the device step
+    for a host sleep; everything else is the real main()."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", str(world),
+                        "--stub", "--steps", "3", "--warmup", "1"], capture_output=True,
+                       text=True, timeout=300, env=env, cwd=repo)
+    assert p.returncode == 0, p.stderr
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == world and out["stub"] is True
+    assert out["scaling"] == "strong" and out["config"]["workload"].startswith("C5")
+    # the shard each rank timed: 8 388 608 / world frames in resident passes
+    assert out["config"]["frames_per_gpu"] == 8388608 // world
+    assert out["steps"] == 3 and out["ms_per_step"] > 0
+
+
+def test_bench_torchrun_form_single_process():
+    """WORLD_SIZE=1 set by a launcher: no spawning, one rank, C3 default."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--stub", "--steps", "2",
+                        "--warmup", "0"], capture_output=True, text=True, timeout=300, env=env,
+                       cwd=repo)
+    assert p.returncode == 0, p.stderr
+    out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    assert out["n_gpus"] == 1 and out["scaling"] == "weak"
+    assert out["config"]["workload"].startswith("C3")

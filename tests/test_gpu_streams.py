@@ -117,54 +117,96 @@ def _conn_case(rng, U, bad):
     assert r1 == r2
     if r1 != 0:
         return None
-    return prod, orc, new
+    return prod, orc, _cut(rng, new)
 
 
-def _run_cases(torch, eng, U, cases, rng, max_frames):
-    """One decode_streams call over every (product conn, oracle conn, new bytes) case, then the
-    reference semantics: deliver_stream on the product side vs process_data on the oracle."""
-    # batch wire: each connection's buffered bytes + new read, 16-B aligned starts, gaps allowed
-    chunks, streams, pos = [], [], 0
-    for prod, orc, new in cases:
+def _cut(rng, data, sizes=(0, 1, 2, 3, 7, 100, 1000, 4096, 16384)):
+    """Split `data` into the reads a libuv loop would deliver (zero-length reads included)."""
+    reads, pos = [], 0
+    while pos < len(data):
+        n = rng.choice(sizes) if rng.random() < 0.8 else rng.randint(1, 20000)
+        reads.append(data[pos:pos + n])
+        pos += n
+    if not reads or rng.random() < 0.1:
+        reads.append(b"")
+    return reads
+
+
+def _run_cases(torch, eng, U, cases, rng, max_frames, use_reads=False):
+    """One device call over every (product conn, oracle conn, reads) case, then the reference
+    semantics: deliver_stream on the product side vs the oracle's process_data called once per
+    read until a call fails (on_websocket_read, src/uvhttp_connection.c:1128-1164).  With
+    use_reads=False each case's reads are joined into ONE call (n_reads = 0)."""
+    # batch wire: each connection's buffered bytes + new reads, 16-B aligned starts, gaps
+    chunks, streams, read_end, pos = [], [], [], 0
+    for prod, orc, reads in cases:
+        if not use_reads:
+            reads[:] = [b"".join(reads)]
         st = prod.struct
         buffered = C.string_at(st.recv_buffer, st.recv_buffer_pos) if st.recv_buffer_pos else b""
-        data = buffered + new
+        data = buffered + b"".join(reads)
         pos = (pos + 15) & ~15
         pos += rng.choice([0, 0, 16, 48])
         s = U.Stream()
         U.lib().uvhttp_ws_stream_init(prod.ptr, pos, len(data), C.byref(s))
+        if use_reads:
+            s.first_read, s.n_reads = len(read_end), len(reads)
+            e = len(buffered)
+            for r in reads:
+                e += len(r)
+                read_end.append(e)
         streams.append(s)
         chunks.append((pos, data))
         pos += len(data)
     wire = np.zeros(pos + 64, np.uint8)
+    guard = np.frombuffer(bytes(rng.getrandbits(8) for _ in range(64)), np.uint8)
+    wire[pos:] = guard  # bytes past wire_len: never written
     for p, d in chunks:
         wire[p:p + len(d)] = np.frombuffer(d, np.uint8)
     n = len(streams)
     sbytes = b"".join(bytes(s) for s in streams)
     dev_streams = torch.from_numpy(np.frombuffer(sbytes, np.uint8).copy()).to("cuda")
     dw = torch.from_numpy(wire.copy()).to("cuda")
-    desc, res = eng.decode_streams(dw, dev_streams, n, max_frames, wire_len=pos)
+    re_dev = None
+    if use_reads:
+        re_dev = torch.from_numpy(np.array(read_end or [0], np.uint64).view(np.int64)).to("cuda")
+    desc_t = torch.full(((max_frames + 2) * 32,), 0xA5, dtype=torch.uint8, device="cuda")
+    res_t = torch.full(((n + 1) * U.STREAM_RESULT_BYTES,), 0x5A, dtype=torch.uint8, device="cuda")
+    desc, res = eng.decode_streams(dw, dev_streams, n, max_frames, wire_len=pos, desc=desc_t,
+                                   results=res_t, read_end=re_dev, n_reads=len(read_end))
     torch.cuda.synchronize()
+    eng.sync()
     results = eng.read_stream_results(res, n)
     host_wire = dw.cpu().numpy()
     host_desc = desc.cpu().numpy()
+    # guard bytes: nothing past the wire, the desc array or the results array was written
+    assert np.array_equal(host_wire[pos:], guard)
+    assert (host_desc[max_frames * 32:] == 0xA5).all()
+    assert (res.cpu().numpy()[n * U.STREAM_RESULT_BYTES:] == 0x5A).all()
     hw = (C.c_uint8 * host_wire.size).from_buffer(host_wire)
     hd = (C.c_uint8 * host_desc.size).from_buffer(host_desc)
-    for k, (prod, orc, new) in enumerate(cases):
+    L = _oracle.load()
+    for k, (prod, orc, reads) in enumerate(cases):
         SINK.pop(C.addressof(prod.ptr.contents), None)
         rc = U.lib().uvhttp_ws_deliver_stream(prod.ptr, hw, hd, C.byref(streams[k]),
                                               C.byref(results[k]))
-        orc_rc = orc.process_data(new)
-        assert rc == orc_rc, (k, results[k].as_dict())
+        orc_rc, calls = orc.process_reads(reads)
+        info = (k, results[k].as_dict(), [len(r) for r in reads])
+        assert rc == orc_rc, info
+        assert results[k].calls == calls, info
         pev = [(t, a, p) for t, a, p in prod.events if t in ("message", "close")]
         oev = [(t, a, p if t == "message" else None) for t, a, p in orc.events()
                if t in ("message", "close")]
-        assert pev == oev, k
+        assert pev == oev, info
         st = prod.struct
-        assert st.recv_buffer_pos == _oracle.load().oracle_conn_recv_pos(orc.c), k
-        assert st.recv_buffer_size == orc.recv_size, k
+        assert st.recv_buffer_pos == L.oracle_conn_recv_pos(orc.c), info
+        assert C.string_at(st.recv_buffer, st.recv_buffer_pos) == orc.recv_bytes(), info
+        assert st.recv_buffer_size == orc.recv_size, info
         frag = st.fragmented_size if st.fragmented_message else 0
-        assert frag == _oracle.load().oracle_conn_frag_size(orc.c), k
+        assert frag == L.oracle_conn_frag_size(orc.c), info
+        assert bool(st.fragmented_message) == orc.frag_pending, info
+        assert st.fragmented_opcode == orc.frag_opcode, info
+        assert (st.state == 3) == (orc.state == 3), info  # CLOSED after a CLOSE frame
         if rc == 0:
             assert results[k].pending_bytes == frag
         sink = SINK.get(C.addressof(prod.ptr.contents), [])
@@ -172,6 +214,7 @@ def _run_cases(torch, eng, U, cases, rng, max_frames):
         # the prefix's control frames went through process_data before this test's sink
         # snapshot; compare the tail the stream delivery produced
         assert sink == exp[len(exp) - len(sink):], k
+    return results
 
 
 @pytest.mark.parametrize("seed", range(10))
@@ -217,5 +260,114 @@ def test_streams_many_small_frames(torch, eng, hooks, seed):
         new = b"".join(frames)
         if rng.random() < 0.5:
             new = new[: rng.randint(1, len(new))]
-        cases.append((prod, orc, new))
+        cases.append((prod, orc, [new]))
     _run_cases(torch, eng, U, cases, rng, 16384)
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_streams_per_read_calls(torch, eng, hooks, seed):
+    """Several process_data calls per connection in one launch: every connection's new bytes
+    are cut into libuv-sized reads (zero-length reads too) and decoded with a read table;
+    the oracle runs process_data once per read.  Growth, buffered bytes, fragment state and
+    the call that failed must all agree."""
+    import uvhttp_amd as U
+    rng = random.Random(5100 + seed)
+    bad = seed % 2 == 1
+    cases = [c for c in (_conn_case(rng, U, bad) for _ in range(rng.choice([1, 7, 60, 250]))) if c]
+    _run_cases(torch, eng, U, cases, rng, 8192, use_reads=True)
+
+
+def _small_frames(rng, total, plen=256):
+    out = []
+    while sum(len(f) for f in out) < total:
+        out.append(_frame(2, 1, rng.randbytes(plen), rng.randbytes(4), True, 0))
+    return b"".join(out)
+
+
+def test_reads_exceed_cap_only_when_joined(torch, eng, hooks):
+    """max_frame_size 4000 with the default 64 KiB buffer: 80 KB of 262-byte frames fed as
+    16 KiB reads is fine (every call holds < 64 KiB), the same bytes as one call fail the
+    growth cap (:851-857).  Per-read decode must succeed exactly as the per-read oracle."""
+    import uvhttp_amd as U
+    rng = random.Random(77)
+    data = _small_frames(rng, 80000)
+    for use_reads in (True, False):
+        prod = U.WsConnection(1, 4000, 64 * 1024 * 1024, user_data=True)
+        orc = _oracle.OracleConn(1, 4000, 64 * 1024 * 1024, record=1, wrapper=True)
+        reads = [data[i:i + 16384] for i in range(0, len(data), 16384)]
+        res = _run_cases(torch, eng, U, [(prod, orc, reads)], rng, 4096, use_reads=use_reads)[0]
+        if use_reads:
+            assert res.status == 0 and res.n_delivered == len(data) // 264
+            assert res.calls == len(reads)
+        else:
+            assert res.status == -1 and res.first_status == -6 and res.n_delivered == 0
+
+
+def test_reads_growth_fails_midway(torch, eng, hooks):
+    """A frame whose payload passes max_frame_size (100 000) but whose wire bytes (100 009)
+    do not fit the capped buffer: the call in which the buffered bytes pass the cap fails
+    with ERR_BUFFER, after the earlier calls delivered their frames."""
+    import uvhttp_amd as U
+    rng = random.Random(78)
+    head = _small_frames(rng, 3000, 100)
+    big = _frame(2, 1, rng.randbytes(99995), rng.randbytes(4), True, 0)
+    data = head + big + _small_frames(rng, 40000, 100)  # reads after the failing call never run
+    prod = U.WsConnection(1, 100000, 64 * 1024 * 1024, user_data=True)
+    orc = _oracle.OracleConn(1, 100000, 64 * 1024 * 1024, record=1, wrapper=True)
+    reads = [data[i:i + 16384] for i in range(0, len(data), 16384)]
+    res = _run_cases(torch, eng, U, [(prod, orc, reads)], rng, 4096, use_reads=True)[0]
+    assert res.status == -1 and res.first_status == -6
+    assert 1 < res.calls < len(reads) and res.n_delivered > 0
+
+
+def test_fragment_error_leaves_reference_bytes(torch, eng, hooks):
+    """ERR_FRAGMENT / ERR_MESSAGE: the reference unmasks the failing frame in recv_buffer
+    (:944) before the fragment checks reject it (:964-1000), and a rejected start still
+    records its opcode.  recv_buffer bytes and fragment state must match byte for byte."""
+    import uvhttp_amd as U
+    rng = random.Random(79)
+    key = b"\x11\x22\x33\x44"
+    scenarios = [
+        # data frame inside a fragmented message (ERR_FRAGMENT)
+        [_frame(1, 0, b"abc", key), _frame(2, 1, b"interrupt!", key), _frame(2, 1, b"x", key)],
+        # continuation with nothing open (ERR_FRAGMENT)
+        [_frame(0, 1, b"orphan-cont", key), _frame(2, 1, b"tail", key)],
+        # fragments over max_message_size (ERR_MESSAGE), start fits, continuation does not
+        [_frame(2, 0, bytes(600), key), _frame(0, 1, rng.randbytes(700), key)],
+        # a start alone over max_message_size: its opcode is recorded before the check fails
+        [_frame(1, 0, rng.randbytes(1200), key), _frame(2, 1, b"after", key)],
+    ]
+    for use_reads in (False, True):
+        cases = []
+        for frames in scenarios:
+            prod = U.WsConnection(1, 16 * 1024 * 1024, 1000, user_data=True)
+            orc = _oracle.OracleConn(1, 16 * 1024 * 1024, 1000, record=1, wrapper=True)
+            cases.append((prod, orc, [f for f in frames]))
+        res = _run_cases(torch, eng, U, cases, rng, 64, use_reads=use_reads)
+        assert [r.first_status for r in res] == [-7, -7, -8, -8]
+
+
+def test_reads_layout_errors(torch, eng):
+    """Malformed descriptors are API errors (ERR_LAYOUT): a decreasing read table, a last
+    read that does not end at len, a read table out of range, a stream past the wire (also
+    with begin near 2^64, which must not wrap the bounds test).  Nothing is decoded."""
+    import uvhttp_amd as U
+    frame = _frame(2, 1, b"hello", b"\x01\x02\x03\x04")
+    L = len(frame)
+    wire = torch.zeros(4 * 64 + 64, dtype=torch.uint8, device="cuda")
+    for k in range(4):
+        wire[k * 64:k * 64 + L] = torch.tensor(list(frame), dtype=torch.uint8)
+    before = wire.clone()
+    specs = [(0, L, 0, 2), (64, L, 2, 2), (128, L, 4, 5), (2**64 - 16, L, 0, 0)]
+    read_end = [L, 3, 3, L - 1]
+    st = np.zeros(4, U.STREAM_DT)
+    for k, (b, ln, fr, nr) in enumerate(specs):
+        st[k] = (b, ln, 65536, 0, 0, 1 << 24, 1 << 26, 1, fr, nr, 0)
+    dev_st = torch.from_numpy(st.view(np.uint8).copy()).to("cuda")
+    re_dev = torch.tensor(read_end, dtype=torch.int64, device="cuda")
+    desc, res = eng.decode_streams(wire, dev_st, 4, 16, wire_len=4 * 64, read_end=re_dev,
+                                   n_reads=len(read_end))
+    torch.cuda.synchronize()
+    rs = eng.read_stream_results(res, 4)
+    assert [(r.status, r.first_status, r.n_delivered) for r in rs] == [(-1, -9, 0)] * 4
+    assert torch.equal(wire, before)

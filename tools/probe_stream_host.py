@@ -13,7 +13,7 @@ st = np.zeros(conns, dtype=[("begin", "<u8"), ("len", "<u8"), ("rbs", "<u8"), ("
 st["begin"] = np.arange(conns, dtype=np.uint64) * stride
 st["len"] = stride; st["rbs"] = 65536; st["mf"], st["mm"], st["srv"] = 1 << 24, 1 << 26, 1
 sd = torch.from_numpy(st.view(np.uint8).copy()).cuda()
-desc = torch.empty(n * 32, dtype=torch.uint8, device="cuda"); res = torch.empty(conns * 48, dtype=torch.uint8, device="cuda")
+desc = torch.empty(n * 32, dtype=torch.uint8, device="cuda"); res = torch.empty(conns * 64, dtype=torch.uint8, device="cuda")
 for timing in (False, True):
     eng.set_timing(timing)
     for k in range(3):

@@ -20,7 +20,7 @@ __all__ = [
     "lib", "LIB_PATH", "FrameHeader", "FrameDesc", "MessageDesc", "BatchSummary", "Batch",
     "WsConnectionStruct", "parse_frame_header", "apply_mask", "WsConnection", "GpuEngine",
     "GpuError", "OPCODES", "FRAME_STATUS", "gen_frame_stride", "GpuPipeline", "Stream",
-    "StreamResult",
+    "StreamResult", "STREAM_DT", "STREAM_RESULT_DT", "STREAM_RESULT_BYTES",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -30,7 +30,7 @@ OPCODES = dict(CONTINUATION=0x0, TEXT=0x1, BINARY=0x2, CLOSE=0x8, PING=0x9, PONG
 FRAME_STATUS = {
     0: "OK", 1: "INCOMPLETE", 2: "SKIPPED", -1: "ERR_PARSE", -2: "ERR_RSV", -3: "ERR_CONTROL",
     -4: "ERR_UNMASKED", -5: "ERR_TOO_BIG", -6: "ERR_BUFFER", -7: "ERR_FRAGMENT",
-    -8: "ERR_MESSAGE", -9: "ERR_LAYOUT", -10: "ERR_CAPACITY",
+    -8: "ERR_MESSAGE", -9: "ERR_LAYOUT", -10: "ERR_CAPACITY", -11: "ERR_DEVICE",
 }
 FLAG_FIN, FLAG_MASK, FLAG_MSG_END = 0x01, 0x02, 0x20
 
@@ -72,22 +72,37 @@ class BatchSummary(C.Structure):
 
 
 class Stream(C.Structure):
-    """uvhttp_ws_stream_t (48 B)."""
+    """uvhttp_ws_stream_t (64 B)."""
     _fields_ = [("begin", C.c_uint64), ("len", C.c_uint64), ("recv_buffer_size", C.c_uint64),
                 ("pending_bytes", C.c_uint64), ("pending_opcode", C.c_int32),
                 ("max_frame_size", C.c_int32), ("max_message_size", C.c_int32),
-                ("is_server", C.c_int32)]
+                ("is_server", C.c_int32), ("first_read", C.c_uint32), ("n_reads", C.c_uint32),
+                ("reserved", C.c_uint64)]
 
 
 class StreamResult(C.Structure):
-    """uvhttp_ws_stream_result_t (48 B)."""
+    """uvhttp_ws_stream_result_t (64 B)."""
     _fields_ = [("first_frame", C.c_uint32), ("n_frames", C.c_uint32),
                 ("n_delivered", C.c_uint32), ("status", C.c_int32), ("first_status", C.c_int32),
-                ("reserved", C.c_uint32), ("consumed_bytes", C.c_uint64),
-                ("recv_buffer_size", C.c_uint64), ("pending_bytes", C.c_uint64)]
+                ("calls", C.c_uint32), ("consumed_bytes", C.c_uint64),
+                ("recv_buffer_size", C.c_uint64), ("pending_bytes", C.c_uint64),
+                ("buffered_end", C.c_uint64), ("reserved", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+def _np_dtype(struct):
+    import numpy as np
+    codes = {C.c_uint64: "<u8", C.c_int64: "<i8", C.c_uint32: "<u4", C.c_int32: "<i4"}
+    dt = np.dtype([(name, codes[t]) for name, t in struct._fields_])
+    assert dt.itemsize == C.sizeof(struct)
+    return dt
+
+
+STREAM_DT = _np_dtype(Stream)
+STREAM_RESULT_DT = _np_dtype(StreamResult)
+STREAM_RESULT_BYTES = C.sizeof(StreamResult)
 
 
 class Batch(C.Structure):
@@ -186,6 +201,7 @@ def load_library(path: str) -> C.CDLL:
         "uvhttp_ws_gpu_engine_kernel_time": (C.c_int, [vp, C.POINTER(C.c_double),
                                                        C.POINTER(u64)]),
         "uvhttp_ws_gpu_engine_last_error": (C.c_char_p, [vp]),
+        "uvhttp_ws_gpu_engine_sync": (C.c_int, [vp, vp]),
         "uvhttp_ws_gpu_decode_inplace": (C.c_int, [vp, C.POINTER(Batch), vp, vp, vp]),
         "uvhttp_ws_gpu_decode_compact": (C.c_int, [vp, C.POINTER(Batch), vp, u64, vp, vp, vp,
                                                    vp]),
@@ -200,6 +216,7 @@ def load_library(path: str) -> C.CDLL:
         "uvhttp_ws_gpu_pipeline_wait": (C.c_int, [vp, C.c_int, C.POINTER(vp), C.POINTER(vp)]),
         "uvhttp_ws_deliver_batch": (C.c_int, [C.POINTER(WsConnectionStruct), vp, vp, vp]),
         "uvhttp_ws_gpu_decode_streams": (C.c_int, [vp, vp, u64, vp, u32, u32, vp, vp, vp]),
+        "uvhttp_ws_gpu_decode_reads": (C.c_int, [vp, vp, u64, vp, u32, vp, u32, u32, vp, vp, vp]),
         "uvhttp_ws_gpu_build_frames": (C.c_int, [vp, vp, u64, vp, u32, vp, u64, vp, vp]),
         "uvhttp_ws_stream_init": (None, [C.POINTER(WsConnectionStruct), u64, u64,
                                          C.POINTER(Stream)]),
@@ -217,6 +234,7 @@ def load_library(path: str) -> C.CDLL:
         "uvhttp_tls_gpu_open_records": (C.c_int, [vp, vp, u64, vp, u32, vp, u32, vp, u32, vp, vp,
                                                   u64, vp]),
         "uvhttp_tls_gpu_seal_records": (C.c_int, [vp, vp, u64, vp, u32, vp, u32, vp, u64, vp]),
+        "uvhttp_tls_gpu_ws_streams": (C.c_int, [vp, vp, vp, u32, vp, vp, vp, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -425,8 +443,9 @@ class GpuEngine:
         return desc, msgs, summary
 
     def decode_streams(self, wire, streams_dev, n_streams, max_frames, desc=None, results=None,
-                       wire_len=None, stream=None):
-        """uvhttp_ws_gpu_decode_streams; streams_dev = device uint8 tensor of n_streams
+                       wire_len=None, stream=None, read_end=None, n_reads=0):
+        """uvhttp_ws_gpu_decode_streams (or _decode_reads when `read_end`, a device uint64
+        tensor of read boundaries, is given); streams_dev = device uint8 tensor of n_streams
         uvhttp_ws_stream_t records.  Returns (desc, results) device tensors."""
         t = self.torch
         dev = f"cuda:{self.device}"
@@ -435,12 +454,25 @@ class GpuEngine:
         if results is None:
             results = t.zeros(max(1, n_streams) * C.sizeof(StreamResult), dtype=t.uint8,
                               device=dev)
-        self._check(self._L.uvhttp_ws_gpu_decode_streams(
-            self.h, C.c_void_p(wire.data_ptr()), wire.numel() if wire_len is None else wire_len,
-            C.c_void_p(streams_dev.data_ptr()), n_streams, max_frames,
-            C.c_void_p(desc.data_ptr()), C.c_void_p(results.data_ptr()), self._stream(stream)),
-            "decode_streams")
+        wl = wire.numel() if wire_len is None else wire_len
+        if read_end is None:
+            rc = self._L.uvhttp_ws_gpu_decode_streams(
+                self.h, C.c_void_p(wire.data_ptr()), wl, C.c_void_p(streams_dev.data_ptr()),
+                n_streams, max_frames, C.c_void_p(desc.data_ptr()),
+                C.c_void_p(results.data_ptr()), self._stream(stream))
+        else:
+            rc = self._L.uvhttp_ws_gpu_decode_reads(
+                self.h, C.c_void_p(wire.data_ptr()), wl, C.c_void_p(streams_dev.data_ptr()),
+                n_streams, C.c_void_p(read_end.data_ptr()), n_reads or read_end.numel(),
+                max_frames, C.c_void_p(desc.data_ptr()), C.c_void_p(results.data_ptr()),
+                self._stream(stream))
+        self._check(rc, "decode_streams")
         return desc, results
+
+    def sync(self, stream=None):
+        """uvhttp_ws_gpu_engine_sync: raises GpuError if a call since the last sync gave up
+        on the device (its outputs say ERR_DEVICE)."""
+        self._check(self._L.uvhttp_ws_gpu_engine_sync(self.h, self._stream(stream)), "sync")
 
     def build_frames(self, src, frames_dev, n_frames, out, out_off=None, stream=None):
         """uvhttp_ws_gpu_build_frames; frames_dev = device uint8 tensor of n_frames
@@ -629,6 +661,15 @@ class TlsEngine:
             C.c_void_p(records.data_ptr()), max_records, C.c_void_p(results.data_ptr()),
             C.c_void_p(out.data_ptr()), out.numel(), self._stream(stream)), "open_records")
         return records, results
+
+    def ws_streams(self, results, records, n_streams, streams, out, ws_streams, read_end,
+                   prefix_src=None, prefix_off=None, stream=None):
+        """uvhttp_tls_gpu_ws_streams: per-record WebSocket stream descriptors (+ prefixes)"""
+        ptr = lambda t: C.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+        self._check(self._L.uvhttp_tls_gpu_ws_streams(
+            self.h, ptr(results), ptr(records), n_streams, ptr(streams), ptr(prefix_src),
+            ptr(prefix_off), ptr(out), ptr(ws_streams), ptr(read_end), self._stream(stream)),
+            "ws_streams")
 
     def seal_records(self, src, recs, n_records, keys, n_keys, out, stream=None):
         """uvhttp_tls_gpu_seal_records (recs: device tensor of uvhttp_tls_seal_t)"""

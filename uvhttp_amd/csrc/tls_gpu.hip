@@ -36,6 +36,7 @@
 #include <string.h>
 
 #include "uvhttp_tls_amd.h"
+#include "uvhttp_ws_amd.h"
 
 namespace {
 
@@ -102,7 +103,9 @@ struct RecWork {
     uint32_t key;
     int32_t status;       // header status from the walk, then the open result
     uint32_t content_len;
-    uint32_t type;
+    uint16_t type;
+    int16_t walk_status;  // header status from the walk, never rewritten: kernels that split
+                          // the records between them decide from it (and from len / cipher)
 };
 static_assert(sizeof(RecWork) == 48, "record work layout");
 
@@ -405,14 +408,15 @@ template <bool WRITE>
 __device__ inline uint32_t walk(const TlsArgs& a, uint32_t s, uint64_t* cap_out, uint32_t first,
                                 uint64_t base, uint32_t* size_bits = nullptr) {
     const uvhttp_tls_stream_t st = a.streams[s];
-    *cap_out = 0;
+    *cap_out = st.ws_prefix;  // the connection's reservation starts with its WebSocket prefix
     if (st.key >= a.n_keys) return 0;
     const uvhttp_tls_key_t k = a.keys[st.key];
     if (!key_valid(k)) return 0;
-    const uint64_t L = st.begin + st.len <= a.wire_len ? st.len : 0;
+    // bounds test that cannot wrap (a begin near 2^64 fails it)
+    const uint64_t L = st.len <= a.wire_len && st.begin <= a.wire_len - st.len ? st.len : 0;
     const uint8_t* p = a.wire + st.begin;
     uint32_t n = 0;
-    uint64_t pos = 0, cap = 0;
+    uint64_t pos = 0, cap = st.ws_prefix;
     while (L - pos >= 5) {
         const uint32_t type = p[pos], ver = be16(p + pos + 1), len = be16(p + pos + 3);
         const int32_t hs = header_status(k.version, k.cipher, type, ver, len);
@@ -428,6 +432,7 @@ __device__ inline uint32_t walk(const TlsArgs& a, uint32_t s, uint64_t* cap_out,
             w.stream = s;
             w.key = st.key;
             w.status = hs;
+            w.walk_status = (int16_t)hs;
             w.content_len = 0;
             w.type = 0;
             a.work[first + n] = w;
@@ -1113,8 +1118,10 @@ __device__ inline void open_status_at(const TlsArgs& a, uint32_t r, const CryptO
     a.work[r].content_len = cl;
 }
 
-// does group g (work items [g kPack, g kPack + kPack)) hold a ChaCha record too long to pack?
-// (wave-uniform; both ChaCha kernels decide the same way)
+// does group g (work items [g kPack, g kPack + kPack)) hold a record of `cipher` too long to
+// pack?  (wave-uniform; the per-record and the packed kernel of a cipher decide the same way:
+// only fields no kernel rewrites are read — the walk's header status, the length, the key —
+// so a record the first kernel already opened, whatever its outcome, cannot move its group)
 __device__ inline bool group_has_long(const TlsArgs& a, uint32_t g, uint32_t n,
                                       uint32_t cipher = UVHTTP_TLS_CIPHER_CHACHA20_POLY1305) {
     const uint32_t lane = threadIdx.x & 63;
@@ -1122,7 +1129,7 @@ __device__ inline bool group_has_long(const TlsArgs& a, uint32_t g, uint32_t n,
     bool big = false;
     if (lane < kPack && g * kPack + lane < n) {
         const RecWork w = a.work[g * kPack + lane];
-        big = w.status == 0 && w.len > lim && a.sched[w.key].cipher == cipher;
+        big = w.walk_status == 0 && w.len > lim && a.sched[w.key].cipher == cipher;
     }
     return __builtin_amdgcn_readfirstlane(__ballot(big) != 0 ? 1u : 0u) != 0;
 }
@@ -1748,7 +1755,7 @@ __global__ __launch_bounds__(kBlock) void k_tls_finalize(TlsArgs a) {
     const StreamWork sw = a.sw[s];
     r.first_record = sw.key_bad;
     r.n_records = sw.n_rec;
-    r.out_off = sw.cap;
+    r.out_off = sw.cap + st.ws_prefix;
     const bool kbad = st.key >= a.n_keys || !key_valid(a.keys[st.key]);
     if (kbad) {
         r.status = -1;
@@ -1816,6 +1823,45 @@ __global__ __launch_bounds__(kBlock) void k_tls_fixup(TlsArgs a) {
     }
 }
 
+// k_tls_ws_streams: one lane per connection — the WebSocket stream descriptor over its
+// plaintext, one process_data call per delivered record (uvhttp_tls_gpu_ws_streams)
+__global__ __launch_bounds__(kBlock) void k_tls_ws_streams(const uvhttp_tls_result_t* results,
+                                                           const uvhttp_tls_record_t* records,
+                                                           uint32_t n_streams,
+                                                           const uvhttp_tls_stream_t* streams,
+                                                           uvhttp_ws_stream_t* ws,
+                                                           uint64_t* read_end) {
+    const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
+    if (s >= n_streams) return;
+    const uvhttp_tls_result_t r = results[s];
+    const uint64_t prefix = streams[s].ws_prefix;
+    uvhttp_ws_stream_t w = ws[s];
+    w.begin = r.out_off - prefix;
+    w.len = prefix + r.plain_len;
+    w.first_read = r.first_record;
+    w.n_reads = r.n_delivered;
+    uint64_t end = prefix;
+    for (uint32_t k = 0; k < r.n_delivered; ++k) {
+        end += records[r.first_record + k].content_len;
+        read_end[r.first_record + k] = end;
+    }
+    ws[s] = w;
+}
+
+// k_tls_ws_prefix: one workgroup per connection copies its buffered WebSocket bytes in front
+// of its plaintext
+__global__ __launch_bounds__(kBlock) void k_tls_ws_prefix(const uvhttp_tls_result_t* results,
+                                                          const uvhttp_tls_stream_t* streams,
+                                                          const uint8_t* src,
+                                                          const uint64_t* src_off, uint8_t* out) {
+    const uint32_t s = blockIdx.x;
+    const uint64_t n = streams[s].ws_prefix;
+    if (!n || results[s].first_status == UVHTTP_TLS_REC_ERR_CAPACITY) return;
+    const uint8_t* p = src + src_off[s];
+    uint8_t* q = out + results[s].out_off - n;
+    for (uint64_t o = threadIdx.x; o < n; o += kBlock) q[o] = p[o];
+}
+
 }  // namespace
 
 // ---- engine ---------------------------------------------------------------------------------
@@ -1838,8 +1884,21 @@ struct uvhttp_tls_gpu_engine {
     double time_ms;
     uint64_t launches;
     int crypt_grid;
+    hipStream_t last_stream;  // calls share one workspace: a call on a new stream waits for
+    int have_last;            // the previous stream's queued work (order_ev)
+    hipEvent_t order_ev;
     char err[256];
 };
+
+static void tls_call_begin(uvhttp_tls_gpu_engine_t* e, hipStream_t s) {
+    if (e->have_last && e->last_stream != s) {
+        if (!e->order_ev) (void)hipEventCreateWithFlags(&e->order_ev, hipEventDisableTiming);
+        if (e->order_ev && hipEventRecord(e->order_ev, e->last_stream) == hipSuccess)
+            (void)hipStreamWaitEvent(s, e->order_ev, 0);
+    }
+    e->last_stream = s;
+    e->have_last = 1;
+}
 
 static int tls_err(uvhttp_tls_gpu_engine_t* e, int code, const char* what, hipError_t h) {
     if (e) snprintf(e->err, sizeof(e->err), "%s: %s", what, h == hipSuccess ? "" : hipGetErrorString(h));
@@ -1955,6 +2014,7 @@ void uvhttp_tls_gpu_engine_free(uvhttp_tls_gpu_engine_t* e) {
     (void)hipSetDevice(e->device);
     if (e->ws) (void)hipFree(e->ws);
     if (e->te0) (void)hipFree(e->te0);
+    if (e->order_ev) (void)hipEventDestroy(e->order_ev);
     for (int k = 0; k < e->ev_created; ++k) (void)hipEventDestroy(e->ev[k]);
     (void)hipSetDevice(prev);
     free(e);
@@ -2001,6 +2061,7 @@ int uvhttp_tls_gpu_open_records(uvhttp_tls_gpu_engine_t* e, const uint8_t* wire,
         return rc;
     }
     hipStream_t s = (hipStream_t)stream;
+    tls_call_begin(e, s);
     TlsArgs a;
     a.wire = wire;
     a.wire_len = wire_len;
@@ -2059,6 +2120,7 @@ int uvhttp_tls_gpu_seal_records(uvhttp_tls_gpu_engine_t* e, const uint8_t* src, 
         return rc;
     }
     hipStream_t s = (hipStream_t)stream;
+    tls_call_begin(e, s);
     if (n_keys)
         hipLaunchKernelGGL(k_tls_keys, dim3((n_keys + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
                            keys, n_keys, (const uint32_t*)e->te0, e->sched);
@@ -2069,6 +2131,32 @@ int uvhttp_tls_gpu_seal_records(uvhttp_tls_gpu_engine_t* e, const uint8_t* src, 
     hipLaunchKernelGGL(k_tls_seal, dim3(grid), dim3(kCryptWG), 0, s, a);
     hipLaunchKernelGGL(k_tls_seal_chacha, dim3(grid), dim3(kCryptWG), 0, s, a);
     tls_timing_end(e, tk, s);
+    const hipError_t h = hipGetLastError();
+    if (prev != e->device) (void)hipSetDevice(prev);
+    if (h != hipSuccess) return tls_err(e, UVHTTP_TLS_GPU_ELAUNCH, "launch", h);
+    return UVHTTP_TLS_GPU_OK;
+}
+
+int uvhttp_tls_gpu_ws_streams(uvhttp_tls_gpu_engine_t* e, const uvhttp_tls_result_t* results,
+                              const uvhttp_tls_record_t* records, uint32_t n_streams,
+                              const uvhttp_tls_stream_t* streams, const uint8_t* prefix_src,
+                              const uint64_t* prefix_off, uint8_t* out, void* ws_streams,
+                              uint64_t* read_end, void* stream) {
+    if (!e || (n_streams && (!results || !streams || !ws_streams || !out)) ||
+        (prefix_src && !prefix_off))
+        return UVHTTP_TLS_GPU_EINVAL;
+    if (!n_streams) return UVHTTP_TLS_GPU_OK;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    if (prev != e->device) (void)hipSetDevice(e->device);
+    hipStream_t s = (hipStream_t)stream;
+    tls_call_begin(e, s);
+    if (prefix_src)
+        hipLaunchKernelGGL(k_tls_ws_prefix, dim3(n_streams), dim3(kBlock), 0, s, results, streams,
+                           prefix_src, prefix_off, out);
+    hipLaunchKernelGGL(k_tls_ws_streams, dim3((n_streams + kBlock - 1) / kBlock), dim3(kBlock), 0,
+                       s, results, records, n_streams, streams, (uvhttp_ws_stream_t*)ws_streams,
+                       read_end);
     const hipError_t h = hipGetLastError();
     if (prev != e->device) (void)hipSetDevice(prev);
     if (h != hipSuccess) return tls_err(e, UVHTTP_TLS_GPU_ELAUNCH, "launch", h);

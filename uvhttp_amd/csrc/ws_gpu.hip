@@ -197,7 +197,18 @@ struct Workspace {
     uint64_t* tile_first;  // [n_tiles]: tagged first frame whose slot contains the tile start
     uint64_t* first_bad;   // [1]: tagged first failing frame of the batch
     uint64_t* arena_first; // [n_arena_tiles]: tagged first data frame of the arena tile
+    uint32_t* ctl;         // control words outside the clearable workspace (see kCtl*)
 };
+
+// ctl words (their own allocation, never cleared with the workspace)
+constexpr int kCtlEpoch = 0;     // device epoch of graph-captured calls
+constexpr int kCtlDone = 1;      // k_epoch's last-block counter
+constexpr int kCtlFaultEp = 2;   // epoch of the latest call whose look-back gave up
+constexpr int kCtlFaults = 3;    // running count of such calls (engine_sync compares it)
+constexpr int kCtlWords = 4;
+// epochs: host-issued tags run 1 .. kMaxHostEpoch, device-issued ones (captured calls)
+// kMaxHostEpoch + 1 .. kMaxEpoch, so a replayed graph never meets a tag a host call left
+constexpr uint32_t kMaxHostEpoch = kMaxEpoch / 2;
 
 // Epoch tags.  Every decode call gets a fresh 32-bit epoch; map entries and first_bad are
 // stored as (epoch << 32) | ~frame and claimed with atomicMax, so within a call the smallest
@@ -227,6 +238,9 @@ struct StreamScratch {
     uint64_t* walk_base;   // [n_streams] slice start within its 256-connection block
     uint64_t* bound_blk;   // [stream blocks + 1] slice totals, then prefixes; [nb] = total
     uint32_t* walk_single; // [1] 1 when every slice fits walk_tmp
+    uint64_t* walk_stop;   // [n_streams] (kind << 32) | call where the walk stopped
+    uint64_t* stop_size;   // [n_streams] recv-buffer size after that call
+    uint64_t* read_size;   // [n_reads_total] recv-buffer size after each call
 };
 
 struct BatchArgs {
@@ -250,9 +264,21 @@ struct BatchArgs {
     uint64_t* open_after;
     uint32_t* seg_bad;
     uint32_t epoch;          // tag of this call's map / first_bad entries
+    uint32_t dev_epoch;      // 1: a captured call, the epoch is ws.ctl[kCtlEpoch]
+    uint32_t max_polls;      // look-back wait bound (0: give up at the first wait; tests)
     uvhttp_ws_batch_summary_t* summary;  // batch mode: written by k_finalize
     uint32_t plan_frames;    // frames per k_plan block (kBlock * FPT)
 };
+
+// every kernel of a call starts here: a captured call reads the epoch the replay's k_epoch set
+__device__ inline void resolve_epoch(BatchArgs& a, const Workspace& ws) {
+    if (a.dev_epoch) a.epoch = *reinterpret_cast<volatile const uint32_t*>(ws.ctl + kCtlEpoch);
+}
+
+// the call's look-back gave up (k_plan recorded this epoch): nothing of it may be delivered
+__device__ inline bool device_fault(const BatchArgs& a, const Workspace& ws) {
+    return *reinterpret_cast<volatile const uint32_t*>(ws.ctl + kCtlFaultEp) == a.epoch;
+}
 
 __device__ inline uint32_t first_bad_of(const BatchArgs& a, const Workspace& ws, uint32_t n) {
     return tag_get(*ws.first_bad, a.epoch, n);
@@ -316,7 +342,7 @@ __device__ inline uint32_t rotr32(uint32_t x, uint32_t s) {
 // bytes past the frame's slot are loaded but never used (only the last 16 bytes of the wire
 // go bytewise)
 __device__ inline u32x4 load_header(const BatchArgs& a, uint64_t o) {
-    if (o + 16 <= a.wire_len) {
+    if (a.wire_len >= 16 && o <= a.wire_len - 16) {  // (cannot wrap for o near 2^64)
         u32x4 v;
         __builtin_memcpy(&v, a.wire + o, 16);
         return v;
@@ -447,7 +473,10 @@ __device__ inline void resolve_one(const BatchArgs& a, uvhttp_ws_message_desc_t*
         uint64_t end = (i + 1 < n) ? frame_start(a, i + 1) : a.wire_len;
         if (end > a.wire_len) end = a.wire_len;
         const uint64_t lo = (i == 0) ? 0 : o;
-        for (uint64_t t = (lo + kMapTile - 1) / kMapTile; t * kMapTile < end && t < a.n_tiles; ++t)
+        // (a start past the end claims nothing; the guard also keeps lo + kMapTile from
+        // wrapping for an offset-table entry near 2^64)
+        for (uint64_t t = lo < end ? lo / kMapTile + (lo % kMapTile != 0) : a.n_tiles;
+             t * kMapTile < end && t < a.n_tiles; ++t)
             tag_claim(&ws.tile_first[t], a.epoch, i);
     }
 
@@ -516,7 +545,9 @@ __device__ inline void resolve_one(const BatchArgs& a, uvhttp_ws_message_desc_t*
 // (sc1) 16-byte accesses.  A reader accepts a record only when all four tags carry this
 // call's epoch and kind, so one round trip both polls and fetches — no flags, no L2
 // writeback or invalidate.  Polls are bounded so a defect cannot hang the device: on
-// exhaustion the block proceeds and its result is wrong (the parity tests catch that).
+// exhaustion the block still publishes (so its successors finish) but records the call's
+// epoch in ws.ctl[kCtlFaultEp] and bumps ws.ctl[kCtlFaults]; the call then delivers nothing
+// (first_bad = frame 0 / every stream ERR_DEVICE) and engine_sync reports ELAUNCH.
 // ------------------------------------------------------------------------------------
 constexpr uint32_t kRecAgg = 1, kRecPrefix = 2;
 constexpr uint32_t kMaxPolls = 1u << 20;
@@ -570,7 +601,7 @@ __device__ inline ScanElem rec_value(const u32x4v x[4]) {
 
 // exclusive prefix of block b (all threads call; the value is broadcast through LDS)
 __device__ ScanElem lookback_prefix(const Workspace& ws, uint32_t b, const ScanElem& agg,
-                                    uint32_t epoch) {
+                                    uint32_t epoch, uint32_t max_polls) {
     __shared__ ScanElem s_wave[kBlock / 64];
     __shared__ ScanElem s_pre;
     __shared__ int s_kstar;
@@ -593,7 +624,8 @@ __device__ ScanElem lookback_prefix(const Workspace& ws, uint32_t b, const ScanE
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     ScanElem run = scan_identity();  // thread 0: combination of the predecessors seen so far
     int64_t end = b;                 // window: blocks [end - 256, end)
-    uint32_t polls = 0;
+    uint32_t polls = 0;              // uniform: every thread counts the same rounds
+    bool gave_up = false;
     for (;;) {
         const int64_t j = end - 1 - t;  // larger t = older block
         ScanElem v = scan_identity();
@@ -609,7 +641,11 @@ __device__ ScanElem lookback_prefix(const Workspace& ws, uint32_t b, const ScanE
                     v = rec_value(xa), ready = true;
                 }
             }
-            if (__syncthreads_and(ready) || ++polls > kMaxPolls) break;
+            if (__syncthreads_and(ready) && max_polls) break;
+            if (++polls > max_polls) {
+                gave_up = true;
+                break;
+            }
             // back off so waiting blocks do not flood memory while predecessors still parse
             __builtin_amdgcn_s_sleep(8);
         }
@@ -629,7 +665,7 @@ __device__ ScanElem lookback_prefix(const Workspace& ws, uint32_t b, const ScanE
 #pragma unroll
             for (int k = kBlock / 64 - 1; k >= 0; --k) w = scan_combine(w, s_wave[k]);
             run = scan_combine(w, run);
-            s_go = (kstar < kBlock || polls > kMaxPolls) ? 0 : 1;
+            s_go = (kstar < kBlock || gave_up) ? 0 : 1;
         }
         __syncthreads();
         if (!s_go) break;
@@ -641,6 +677,11 @@ __device__ ScanElem lookback_prefix(const Workspace& ws, uint32_t b, const ScanE
         ws.block_excl[b] = run;
         ws.block_incl[b] = incl;
         rec_store(ws.rec_p, b, incl, tag_p);
+        if (gave_up) {
+            __hip_atomic_store(&ws.ctl[kCtlFaultEp], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&ws.ctl[kCtlFaults], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            tag_claim(ws.first_bad, epoch, 0);  // batch mode: the payload pass unmasks nothing
+        }
     }
     __syncthreads();
     return s_pre;
@@ -655,6 +696,7 @@ __device__ ScanElem lookback_prefix(const Workspace& ws, uint32_t b, const ScanE
 template <int FPT>
 __global__ __launch_bounds__(kBlock) void k_plan(BatchArgs a, uvhttp_ws_frame_desc_t* desc,
                                                  uvhttp_ws_message_desc_t* msgs, Workspace ws) {
+    resolve_epoch(a, ws);
     __shared__ uint32_t s_ticket;
     if (threadIdx.x == 0) {
         const uint32_t t =
@@ -677,7 +719,7 @@ __global__ __launch_bounds__(kBlock) void k_plan(BatchArgs a, uvhttp_ws_frame_de
         }
         ScanElem agg;
         const ScanElem local = block_exclusive_scan(elem, &agg);
-        const ScanElem pre = lookback_prefix(ws, b, agg, a.epoch);
+        const ScanElem pre = lookback_prefix(ws, b, agg, a.epoch, a.max_polls);
         if (i0 < n) {
             resolve_one(a, msgs, ws, i0, n, g, scan_combine(pre, local), d);
             desc[i0] = d;
@@ -705,14 +747,14 @@ __global__ __launch_bounds__(kBlock) void k_plan(BatchArgs a, uvhttp_ws_frame_de
         if (a.wire_len >= 16) {
 #pragma unroll
             for (int k = 0; k < FPT; ++k) {
-                const uint64_t oc = o[k] + 16 <= a.wire_len ? o[k] : a.wire_len - 16;
+                const uint64_t oc = o[k] <= a.wire_len - 16 ? o[k] : a.wire_len - 16;
                 __builtin_memcpy(&hv[k], a.wire + oc, 16);
             }
             // a header within 16 bytes of the wire's end: its bytes sit d = o - oc bytes into
             // the clamped window; shift them down, zeros past the end (as load_header)
 #pragma unroll
             for (int k = 0; k < FPT; ++k) {
-                const uint64_t oc = o[k] + 16 <= a.wire_len ? o[k] : a.wire_len - 16;
+                const uint64_t oc = o[k] <= a.wire_len - 16 ? o[k] : a.wire_len - 16;
                 const uint64_t d = o[k] - oc;
                 unsigned __int128 v = ((unsigned __int128)(((uint64_t)hv[k].w << 32) | hv[k].z) << 64) |
                                       (((uint64_t)hv[k].y << 32) | hv[k].x);
@@ -731,7 +773,7 @@ __global__ __launch_bounds__(kBlock) void k_plan(BatchArgs a, uvhttp_ws_frame_de
     }
     ScanElem agg;
     const ScanElem local = block_exclusive_scan(tagg, &agg);
-    ScanElem run = scan_combine(lookback_prefix(ws, b, agg, a.epoch), local);
+    ScanElem run = scan_combine(lookback_prefix(ws, b, agg, a.epoch, a.max_polls), local);
     // pass 2: the state machine in frame order
 #pragma unroll
     for (int k = 0; k < FPT; ++k) {
@@ -795,8 +837,21 @@ __device__ void write_summary(const BatchArgs& a, const uvhttp_ws_frame_desc_t* 
 // place; wave 0 of block 0 writes the batch summary
 __global__ __launch_bounds__(kBlock) void k_finalize(BatchArgs a, uvhttp_ws_frame_desc_t* desc,
                                                      Workspace ws) {
-    const uint32_t nb = first_bad_of(a, ws, a.n);
+    resolve_epoch(a, ws);
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (device_fault(a, ws)) {  // nothing was delivered (the payload pass saw first_bad = 0)
+        if (i < a.n) desc[i].status = UVHTTP_WS_FRAME_SKIPPED;
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            uvhttp_ws_batch_summary_t s;
+            memset(&s, 0, sizeof(s));
+            s.n_frames = a.n;
+            s.status = -1;
+            s.first_status = UVHTTP_WS_FRAME_ERR_DEVICE;
+            *a.summary = s;
+        }
+        return;
+    }
+    const uint32_t nb = first_bad_of(a, ws, a.n);
     if (i < a.n) {
         if (i > nb) desc[i].status = UVHTTP_WS_FRAME_SKIPPED;
         if (a.arena && i < nb) {
@@ -997,6 +1052,7 @@ template <int BLOCK, int VPT, int STORE_AUX = 0>
 __global__ __launch_bounds__(BLOCK) void k_unmask_inplace(
     BatchArgs a, const uvhttp_ws_frame_desc_t* __restrict__ desc, Workspace ws,
     uint64_t tile_base) {
+    resolve_epoch(a, ws);
     uint32_t n, nb;
     unmask_tile<BLOCK, VPT, STORE_AUX>(a, desc, ws, tile_base, n, nb);
 }
@@ -1181,6 +1237,7 @@ template <int BLOCK, int VPT>
 __global__ __launch_bounds__(BLOCK) void k_gather_compact(
     BatchArgs a, const uvhttp_ws_frame_desc_t* __restrict__ desc, Workspace ws,
     uint64_t arena_bytes_cap, uint64_t tile_base) {
+    resolve_epoch(a, ws);
     const uint32_t n = nframes(a);
     gather_tile<BLOCK, VPT>(a, desc, ws, arena_bytes_cap, tile_base, n, first_bad_of(a, ws, n));
 }
@@ -1226,6 +1283,7 @@ template <int BLOCK, int VPT>
 __global__ __launch_bounds__(BLOCK) void k_scatter_compact(
     BatchArgs a, const uvhttp_ws_frame_desc_t* __restrict__ desc, Workspace ws,
     uint64_t arena_bytes_cap, uint64_t tile_base) {
+    resolve_epoch(a, ws);
     constexpr uint64_t kT = (uint64_t)BLOCK * VPT * 16;
     __shared__ uint64_t s_ps[BLOCK];  // wire offset of the payload
     __shared__ uint64_t s_pe[BLOCK];  // its end (== start: not a delivered data frame)
@@ -1317,12 +1375,16 @@ __global__ __launch_bounds__(BLOCK) void k_scatter_compact(
 }
 
 // ------------------------------------------------------------------------------------
-// stream decode: frame discovery.  One lane per connection walks its buffered bytes header
-// by header exactly as process_data's loop does (:872-932) and stops where process_data
-// stops: fewer bytes than a header needs, a frame process_data rejects before unmasking
-// (counted: it is the failing frame), or an incomplete frame (not counted: it stays in the
-// buffer).  Pass 1 counts frames; pass 2 (after a scan of the counts) writes the offsets.
-// The recv-buffer growth check (:832-866) runs once per connection on all its bytes.
+// stream decode: frame discovery.  One lane (or one wave) per connection walks its buffered
+// bytes header by header exactly as the reference's process_data calls do
+// (src/uvhttp_websocket.c:832-932), one call per read: at the start of every call the
+// recv-buffer growth check runs on the bytes the call holds (:832-857); within a call frames
+// are taken while complete; the walk stops where the calls stop: at a frame process_data
+// rejects before unmasking (counted: it is the failing frame; it fails the call in which its
+// header bytes arrived), at a call whose growth check fails, or after the last call (an
+// incomplete frame is not counted: it stays in the buffer).  Pass 1 counts frames; after a
+// scan of the counts the frame offsets are written.  The walk also records, per connection,
+// the call it stopped in and why, and the recv-buffer size after every call.
 // ------------------------------------------------------------------------------------
 struct WalkArgs {
     const uint8_t* wire;
@@ -1330,11 +1392,20 @@ struct WalkArgs {
     const uvhttp_ws_stream_t* streams;
     uint32_t n_streams;
     uint32_t max_frames;
+    const uint64_t* read_end;  // [n_reads_total] read boundaries (relative), or null
+    uint32_t n_reads_total;
     uvhttp_ws_stream_result_t* results;
     StreamScratch sc;
 };
 
-// process_data's buffer growth: returns false on failure, else the size after the call
+// how a connection's walk ended (walk_stop = kind << 32 | call)
+constexpr uint32_t kStopEnd = 0;     // every call ran; what is left waits in recv_buffer
+constexpr uint32_t kStopBad = 1;     // the last counted frame failed its header checks
+constexpr uint32_t kStopGrow = 2;    // the call's recv-buffer growth check failed
+constexpr uint32_t kStopLayout = 3;  // malformed descriptor / read table: nothing decoded
+
+// process_data's buffer growth: returns false on failure (*out = size then), else the size
+// after the call
 __device__ inline bool grow_recv(uint64_t have, uint64_t size, int32_t max_frame, uint64_t* out) {
     *out = size;
     if (have <= size) return true;
@@ -1354,40 +1425,130 @@ __device__ inline bool grow_recv(uint64_t have, uint64_t size, int32_t max_frame
     return true;
 }
 
+// the connection's bytes, or 0 with *ok = false when the descriptor is out of range (the
+// bounds test cannot wrap: begin near 2^64 fails it)
+__device__ inline uint64_t stream_bytes(const WalkArgs& w, const uvhttp_ws_stream_t& st, bool* ok) {
+    *ok = st.len <= w.wire_len && st.begin <= w.wire_len - st.len;
+    return *ok ? st.len : 0;
+}
+
+// the read table of a connection: in range, non-decreasing, ending at len.  Lanes
+// [lane, lane + step, ...) check their entries; the caller combines the lanes' answers.
+__device__ inline bool reads_ok_part(const WalkArgs& w, const uvhttp_ws_stream_t& st, uint64_t L,
+                                     uint32_t lane, uint32_t step) {
+    if (st.n_reads == 0) return true;
+    if (!w.read_end || st.first_read > w.n_reads_total ||
+        st.n_reads > w.n_reads_total - st.first_read)
+        return false;
+    const uint64_t* re = w.read_end + st.first_read;
+    bool ok = lane != 0 || re[st.n_reads - 1] == L;
+    for (uint32_t k = lane; k < st.n_reads && ok; k += step) {
+        const uint64_t prev = k ? re[k - 1] : 0;
+        ok = re[k] >= prev && re[k] <= L;
+    }
+    return ok;
+}
+
+// The walk over the calls.  fetch(pos, hb) yields the ten header bytes at stream offset pos;
+// emit(pos, idx) records counted frame idx; `writer` lanes store the stop record and the
+// per-call buffer sizes.  Returns the number of frames counted.
+template <typename Fetch, typename Emit>
+__device__ inline uint32_t walk_calls(const WalkArgs& w, uint32_t s, const uvhttp_ws_stream_t& st,
+                                      uint64_t L, bool writer, Fetch&& fetch, Emit&& emit) {
+    const uint64_t mf = (uint64_t)(int64_t)st.max_frame_size;
+    const uint32_t K = st.n_reads ? st.n_reads : 1;
+    const uint64_t* re = st.n_reads ? w.read_end + st.first_read : nullptr;
+    uint32_t count = 0, k = 0, kind = kStopEnd;
+    uint64_t pos = 0, size = st.recv_buffer_size;
+    uint64_t end = re ? re[0] : L;
+    bool grown = grow_recv(end, size, st.max_frame_size, &size);  // call 0
+    if (writer && re) w.sc.read_size[st.first_read] = size;
+    if (!grown) kind = kStopGrow;
+    while (grown) {
+        uint64_t need_end;  // the stream offset the next decision needs
+        if (end - pos >= 2) {
+            uint32_t hb[10];
+            fetch(pos, hb);
+            const uint32_t b0 = hb[0], b1 = hb[1];
+            const uint32_t code = b1 & 0x7F;
+            const uint32_t need = code == 126 ? 4 : code == 127 ? 10 : 2;
+            if (end - pos >= need) {
+                uint64_t plen = code;
+                if (need == 4) {
+                    plen = (hb[2] << 8) | hb[3];
+                } else if (need == 10) {
+                    plen = 0;
+#pragma unroll
+                    for (int q = 2; q < 10; ++q) plen = (plen << 8) | hb[q];
+                }
+                const bool bad = (need == 10 && (plen >> 63)) || (b0 & 0x70) ||
+                                 ((b0 & 0x0F) >= 8 && (plen > 125 || !(b0 & 0x80))) ||
+                                 (st.is_server && !(b1 & 0x80)) || plen > mf;
+                if (bad) {  // process_data returns at this frame, in this call
+                    emit(pos, count);
+                    ++count;
+                    kind = kStopBad;
+                    break;
+                }
+                const uint64_t wl = need + ((b1 & 0x80) ? 4u : 0u) + plen;
+                if (end - pos >= wl) {  // complete: delivered by this call
+                    emit(pos, count);
+                    ++count;
+                    pos += wl;
+                    continue;
+                }
+                need_end = pos + wl;
+            } else {
+                need_end = pos + need;
+            }
+        } else {
+            need_end = pos + 2;
+        }
+        // the bytes of the next decision come with a later call: run the calls up to it
+        // (each one's growth check sees the partial frame plus everything it appended)
+        while (end < need_end && k + 1 < K) {
+            ++k;
+            end = re[k];
+            grown = grow_recv(end - pos, size, st.max_frame_size, &size);
+            if (writer) w.sc.read_size[st.first_read + k] = size;
+            if (!grown) break;
+        }
+        if (!grown) {
+            kind = kStopGrow;
+            break;
+        }
+        if (end < need_end) break;  // every call ran: the rest waits in recv_buffer
+    }
+    if (writer) {
+        w.sc.walk_stop[s] = ((uint64_t)kind << 32) | k;
+        w.sc.stop_size[s] = size;
+    }
+    return count;
+}
+
+// lane walk: one lane per connection, header bytes straight from global memory
 template <bool WRITE>
 __device__ inline uint32_t walk_stream(const WalkArgs& w, uint32_t s, uint32_t first) {
     const uvhttp_ws_stream_t st = w.streams[s];
-    const uint8_t* p = w.wire + st.begin;
-    const uint64_t L = st.begin + st.len <= w.wire_len ? st.len : 0;
-    uint64_t grown;
-    if (!grow_recv(L, st.recv_buffer_size, st.max_frame_size, &grown)) return 0;
-    const uint64_t mf = (uint64_t)(int64_t)st.max_frame_size;
-    uint32_t count = 0;
-    uint64_t pos = 0;
-    while (L - pos >= 2) {
-        const uint32_t b0 = p[pos], b1 = p[pos + 1];
-        const uint32_t code = b1 & 0x7F;
-        const uint32_t need = code == 126 ? 4 : code == 127 ? 10 : 2;
-        if (L - pos < need) break;
-        uint64_t plen = code;
-        if (need > 2) {
-            plen = 0;
-            for (uint32_t k = 2; k < need; ++k) plen = (plen << 8) | p[pos + k];
-        }
-        const bool bad = (need == 10 && (plen >> 63)) || (b0 & 0x70) ||
-                         ((b0 & 0x0F) >= 8 && (plen > 125 || !(b0 & 0x80))) ||
-                         (st.is_server && !(b1 & 0x80)) || plen > mf;
-        const uint64_t wl = need + ((b1 & 0x80) ? 4u : 0u) + plen;
-        if (!bad && L - pos < wl) break;  // incomplete: waits for more bytes
-        if (WRITE && first + count < w.max_frames) {
-            w.sc.frame_off[first + count] = st.begin + pos;
-            w.sc.frame_seg[first + count] = s;
-        }
-        ++count;
-        if (bad) break;  // process_data returns at this frame
-        pos += wl;
+    bool in_range;
+    const uint64_t L = stream_bytes(w, st, &in_range);
+    if (!in_range || !reads_ok_part(w, st, L, 0, 1)) {
+        if (!WRITE) w.sc.walk_stop[s] = (uint64_t)kStopLayout << 32;
+        return 0;
     }
-    return count;
+    const uint8_t* p = w.wire + st.begin;
+    return walk_calls(
+        w, s, st, L, !WRITE,
+        [&](uint64_t pos, uint32_t hb[10]) {
+#pragma unroll
+            for (int q = 0; q < 10; ++q) hb[q] = pos + q < L ? p[pos + q] : 0u;
+        },
+        [&](uint64_t pos, uint32_t idx) {
+            if (WRITE && first + idx < w.max_frames) {
+                w.sc.frame_off[first + idx] = st.begin + pos;
+                w.sc.frame_seg[first + idx] = s;
+            }
+        });
 }
 
 __device__ inline uint64_t block_exclusive_sum_u64(uint64_t v, uint64_t* total) {
@@ -1449,7 +1610,7 @@ __device__ inline void walk_load_block(const WalkArgs& w, uint64_t blk, u32x4 v[
 #pragma unroll
     for (int k = 0; k < kWalkVec; ++k) {
         const uint64_t src = blk * kWalkBlk + (uint64_t)(k * 64 + lane) * 16u;
-        if (src + 16 <= w.wire_len) {
+        if (w.wire_len >= 16 && src <= w.wire_len - 16) {
             v[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(w.wire + src));
         } else {
             uint32_t t[4] = {0, 0, 0, 0};
@@ -1481,75 +1642,61 @@ __device__ inline uint32_t walk_stream_wave(const WalkArgs& w, uint32_t s, uint6
                                             uint8_t* ring) {
     const int lane = threadIdx.x & 63;
     const uvhttp_ws_stream_t st = w.streams[s];
-    const uint64_t L = st.begin + st.len <= w.wire_len ? st.len : 0;
-    uint64_t grown;
-    if (!grow_recv(L, st.recv_buffer_size, st.max_frame_size, &grown)) return 0;
-    const uint64_t mf = (uint64_t)(int64_t)st.max_frame_size;
-    uint32_t count = 0;
-    uint64_t pos = 0;
+    bool in_range;
+    const uint64_t L = stream_bytes(w, st, &in_range);
+    const bool reads_ok = in_range && __all(reads_ok_part(w, st, L, lane, 64));
+    const bool writer = MODE != 1 && lane == 0;  // the count pass records stop / sizes
+    if (!reads_ok) {
+        if (writer) w.sc.walk_stop[s] = (uint64_t)kStopLayout << 32;
+        return 0;
+    }
     uint64_t cur = ~0ull;  // block of the current header; LDS holds cur and cur + 1
     u32x4 pf[kWalkVec];    // block cur + 2, in flight
     auto byte_at = [&](uint64_t x) { return (uint32_t)ring[((x / kWalkBlk) & 1) * kWalkBlk + x % kWalkBlk]; };
-    while (L - pos >= 2) {
-        const uint64_t at = st.begin + pos;
-        const uint64_t blk = at / kWalkBlk;
-        if (blk != cur) {
-            if (cur != ~0ull && blk == cur + 1) {
-                walk_store_block(ring, blk + 1, pf);  // the prefetched block joins the ring
-            } else {
-                u32x4 t[kWalkVec];
-                walk_load_block(w, blk, t);
-                walk_load_block(w, blk + 1, pf);
-                walk_store_block(ring, blk, t);
-                walk_store_block(ring, blk + 1, pf);
+    return walk_calls(
+        w, s, st, L, writer,
+        [&](uint64_t pos, uint32_t hb[10]) {
+            const uint64_t at = st.begin + pos;
+            const uint64_t blk = at / kWalkBlk;
+            if (blk != cur) {
+                if (cur != ~0ull && blk == cur + 1) {
+                    walk_store_block(ring, blk + 1, pf);  // the prefetched block joins the ring
+                } else {
+                    u32x4 t[kWalkVec];
+                    walk_load_block(w, blk, t);
+                    walk_load_block(w, blk + 1, pf);
+                    walk_store_block(ring, blk, t);
+                    walk_store_block(ring, blk + 1, pf);
+                }
+                walk_load_block(w, blk + 2, pf);
+                cur = blk;
+                wave_sync_lds();
             }
-            walk_load_block(w, blk + 2, pf);
-            cur = blk;
-            wave_sync_lds();
-        }
-        // the ten bytes a header can use, all independent LDS reads
-        uint32_t hb[10];
+            // the ten bytes a header can use, all independent LDS reads
 #pragma unroll
-        for (int k = 0; k < 10; ++k) hb[k] = byte_at(at + k);
-        const uint32_t b0 = hb[0], b1 = hb[1];
-        const uint32_t code = b1 & 0x7F;
-        const uint32_t need = code == 126 ? 4 : code == 127 ? 10 : 2;
-        if (L - pos < need) break;
-        uint64_t plen = code;
-        if (need == 4) {
-            plen = (hb[2] << 8) | hb[3];
-        } else if (need == 10) {
-            plen = 0;
-#pragma unroll
-            for (int k = 2; k < 10; ++k) plen = (plen << 8) | hb[k];
-        }
-        const bool bad = (need == 10 && (plen >> 63)) || (b0 & 0x70) ||
-                         ((b0 & 0x0F) >= 8 && (plen > 125 || !(b0 & 0x80))) ||
-                         (st.is_server && !(b1 & 0x80)) || plen > mf;
-        const uint64_t wl = need + ((b1 & 0x80) ? 4u : 0u) + plen;
-        if (!bad && L - pos < wl) break;  // incomplete: waits for more bytes
-        if (MODE == 1 && lane == 0 && first + count < w.max_frames) {
-            w.sc.frame_off[first + count] = at;
-            w.sc.frame_seg[first + count] = s;
-        }
-        if (MODE == 2 && lane == 0) w.sc.walk_tmp[first + count] = (uint32_t)pos;
-        ++count;
-        if (bad) break;  // process_data returns at this frame
-        pos += wl;
-    }
-    return count;
+            for (int q = 0; q < 10; ++q) hb[q] = byte_at(at + q);
+        },
+        [&](uint64_t pos, uint32_t idx) {
+            if (MODE == 1 && lane == 0 && first + idx < w.max_frames) {
+                w.sc.frame_off[first + idx] = st.begin + pos;
+                w.sc.frame_seg[first + idx] = s;
+            }
+            if (MODE == 2 && lane == 0) w.sc.walk_tmp[first + idx] = (uint32_t)pos;
+        });
 }
 
 // single-pass wave walk, step 1: each connection's slice of walk_tmp, an upper bound on the
 // frames the walk can count: every counted frame but the last (failing) one is >= 2 bytes,
-// and >= 6 on a server connection (unmasked frames fail there, :910-912)
+// and >= 6 on a server connection (unmasked frames fail there, :910-912).  Slices hold
+// 32-bit positions, so a connection of 4 GiB or more forces the two-walk path.
 __global__ __launch_bounds__(kBlock) void k_walk_bound(WalkArgs w) {
     const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
     uint64_t b = 0;
     if (s < w.n_streams) {
         const uvhttp_ws_stream_t st = w.streams[s];
-        const uint64_t L = st.begin + st.len <= w.wire_len ? st.len : 0;
-        b = L / (st.is_server ? 6 : 2) + 1;
+        bool in_range;
+        const uint64_t L = stream_bytes(w, st, &in_range);
+        b = L >> 32 ? (1ull << 60) : L / (st.is_server ? 6 : 2) + 1;
     }
     uint64_t total;
     const uint64_t local = block_exclusive_sum_u64(b, &total);
@@ -1659,6 +1806,8 @@ __global__ __launch_bounds__(kBlock) void k_walk_scan(WalkArgs w, uint32_t n_blo
     if (threadIdx.x == 0) *w.sc.n_total = total <= w.max_frames ? total : 0;
 }
 
+// each connection's first frame (scan of the counts) and its provisional result; the lane
+// walk also writes its frame offsets here (second walk)
 template <bool WALK>
 __global__ __launch_bounds__(kBlock) void k_walk_write(WalkArgs w) {
     const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
@@ -1667,21 +1816,24 @@ __global__ __launch_bounds__(kBlock) void k_walk_write(WalkArgs w) {
     const uint32_t first = w.sc.walk_agg[blockIdx.x] + block_exclusive_sum_u32(c, &total);
     if (s >= w.n_streams) return;
     const bool fits = *w.sc.n_total != 0 || c == 0;  // n_total 0 with frames = overflow
-    uvhttp_ws_stream_result_t r;
     const uvhttp_ws_stream_t st = w.streams[s];
-    uint64_t grown;
-    const uint64_t L = st.begin + st.len <= w.wire_len ? st.len : 0;
-    const bool grow_ok = grow_recv(L, st.recv_buffer_size, st.max_frame_size, &grown);
+    const bool layout = (uint32_t)(w.sc.walk_stop[s] >> 32) == kStopLayout;
+    uvhttp_ws_stream_result_t r;
     r.first_frame = first;
     r.n_frames = c;
     r.n_delivered = 0;
-    r.status = grow_ok ? 0 : -1;
-    r.first_status = grow_ok ? 0 : UVHTTP_WS_FRAME_ERR_BUFFER;
-    r.reserved = 0;
+    r.status = 0;
+    r.first_status = 0;
+    r.calls = 0;
     r.consumed_bytes = 0;
-    r.recv_buffer_size = grow_ok ? grown : st.recv_buffer_size;
+    r.recv_buffer_size = st.recv_buffer_size;
     r.pending_bytes = st.pending_bytes;
-    if (!fits) {
+    r.buffered_end = 0;
+    r.reserved = 0;
+    if (layout) {
+        r.status = -1;
+        r.first_status = UVHTTP_WS_FRAME_ERR_LAYOUT;
+    } else if (!fits) {
         r.status = -1;
         r.first_status = UVHTTP_WS_FRAME_ERR_CAPACITY;
         r.n_frames = 0;
@@ -1692,27 +1844,72 @@ __global__ __launch_bounds__(kBlock) void k_walk_write(WalkArgs w) {
     w.results[s] = r;
 }
 
+// the call (0-based) of connection st that completes a frame ending at stream offset fe
+__device__ inline uint32_t call_of_end(const uint64_t* read_end, const uvhttp_ws_stream_t& st,
+                                       uint64_t fe) {
+    if (!st.n_reads) return 0;
+    const uint64_t* re = read_end + st.first_read;
+    uint32_t lo = 0, hi = st.n_reads - 1;  // first k with re[k] >= fe (the last one does)
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (re[mid] >= fe) hi = mid;
+        else lo = mid + 1;
+    }
+    return lo;
+}
+
 // k_stream_mark: after the state machine.  Frames past their connection's first failure
-// become SKIPPED (so the payload pass leaves them masked); per-connection results.
+// become SKIPPED (so the payload pass leaves them masked); per-connection results: which call
+// failed (or how many ran), the buffer size it left, the bytes left buffered.
 __global__ __launch_bounds__(kBlock) void k_stream_mark(BatchArgs a, uvhttp_ws_frame_desc_t* desc,
                                                         uvhttp_ws_stream_result_t* results,
-                                                        uint32_t n_streams) {
+                                                        uint32_t n_streams, Workspace ws,
+                                                        StreamScratch sc, const uint64_t* read_end) {
+    resolve_epoch(a, ws);
+    const bool dev_fault = device_fault(a, ws);
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t n = nframes(a);
-    if (i < n && i > a.seg_bad[a.frame_seg[i]]) desc[i].status = UVHTTP_WS_FRAME_SKIPPED;
+    if (i < n && (dev_fault || i > a.seg_bad[a.frame_seg[i]])) desc[i].status = UVHTTP_WS_FRAME_SKIPPED;
     if (i >= n_streams) return;
     uvhttp_ws_stream_result_t r = results[i];
-    if (r.first_status != 0) return;  // buffer growth or capacity failure: nothing decoded
+    if (dev_fault) {
+        r.status = -1;
+        r.first_status = UVHTTP_WS_FRAME_ERR_DEVICE;
+        r.n_delivered = 0;
+        results[i] = r;
+        return;
+    }
+    if (r.first_status != 0) return;  // layout or capacity failure: nothing decoded
+    const uvhttp_ws_stream_t st = a.streams[i];
+    const uint64_t stop = sc.walk_stop[i];
+    const uint32_t kind = (uint32_t)(stop >> 32), scall = (uint32_t)stop;
+    auto size_after = [&](uint32_t call) {
+        return st.n_reads ? sc.read_size[st.first_read + call] : sc.stop_size[i];
+    };
+    auto end_of = [&](uint32_t call) { return st.n_reads ? read_end[st.first_read + call] : st.len; };
     const uint32_t bad = a.seg_bad[i];
     const uint32_t delivered = bad - r.first_frame;
     r.n_delivered = delivered;
-    if (delivered < r.n_frames) {
+    uint32_t call = scall;
+    if (delivered < r.n_frames) {  // a frame failed: header checks or the state machine
         r.first_status = desc[bad].status;
         r.status = r.first_status < 0 ? -1 : 0;
+        const bool walk_bad = kind == kStopBad && bad + 1 == r.first_frame + r.n_frames;
+        if (!walk_bad)  // a complete frame the state machine rejected: the call completing it
+            call = call_of_end(read_end, st, frame_start(a, bad) + desc[bad].wire_len - st.begin);
+        r.buffered_end = end_of(call);
+    } else if (kind == kStopGrow) {
+        r.status = -1;
+        r.first_status = UVHTTP_WS_FRAME_ERR_BUFFER;
+        r.buffered_end = call ? end_of(call - 1) : 0;  // the failing call appended nothing
+    } else {
+        r.buffered_end = end_of(call);
     }
+    r.calls = call + 1;
+    r.recv_buffer_size = size_after(call);
     if (delivered) {
         const uint32_t lastf = r.first_frame + delivered - 1;
-        r.consumed_bytes = frame_start(a, lastf) + desc[lastf].wire_len - a.streams[i].begin;
+        r.consumed_bytes = frame_start(a, lastf) + desc[lastf].wire_len - st.begin;
         r.pending_bytes = a.open_after[lastf];
     }
     results[i] = r;
@@ -1757,7 +1954,13 @@ struct BuildArgs {
     uint32_t map_shift;  // log2 of the map tile (>= the emit tile; ~ the average frame size)
     uint32_t epoch;      // tag of this call's map records (stale records never match)
     uint32_t group;      // kb_emit_frames: frames per workgroup (<= kEmitF)
+    const uint32_t* ctl; // captured calls (dev_epoch): the epoch is ctl[kCtlEpoch]
+    uint32_t dev_epoch;
 };
+
+__device__ inline void resolve_epoch(BuildArgs& b) {
+    if (b.dev_epoch) b.epoch = *reinterpret_cast<volatile const uint32_t*>(b.ctl + kCtlEpoch);
+}
 
 __device__ inline uint64_t build_size(const uvhttp_ws_build_desc_t& f) {
     const uint64_t p = f.payload_len;
@@ -1830,6 +2033,7 @@ __device__ inline u32x4 build_header(const uvhttp_ws_build_desc_t& d, uint32_t* 
 }
 
 __global__ __launch_bounds__(kBlock) void kb_offsets(BuildArgs b, uint32_t n_groups) {
+    resolve_epoch(b);
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     const uint64_t sz = i < b.n ? build_size(b.frames[i]) : 0;
     uint64_t total;
@@ -1889,6 +2093,7 @@ __device__ inline void build_vector(const BuildArgs& b, uint64_t oa, uint64_t fs
 
 template <int BLOCK, int VPT>
 __global__ __launch_bounds__(BLOCK) void kb_emit(BuildArgs b, uint64_t tile_base) {
+    resolve_epoch(b);
     constexpr uint64_t kT = (uint64_t)BLOCK * VPT * 16;
     __shared__ uint64_t s_start[BLOCK];  // frame start in out
     __shared__ uint64_t s_pstart[BLOCK]; // payload start in out
@@ -2252,6 +2457,36 @@ __global__ __launch_bounds__(kBlock) void k_gen_frames(uint8_t* wire, uint32_t n
     }
 }
 
+// k_epoch: first kernel of a captured call.  Every block reads the current device epoch,
+// then the last block to finish stores the next one (all reads happen before the store,
+// which waits for every block's done-increment).  When the device half of the epoch space is
+// used up the workspace and the send-side map are cleared first (grid-stride), so no stale
+// tag can match after the wrap.
+__global__ __launch_bounds__(kBlock) void k_epoch(uint32_t* ctl, uint64_t* ws_words,
+                                                  uint64_t n_ws, uint64_t* bs_words,
+                                                  uint64_t n_bs) {
+    const uint32_t e = *reinterpret_cast<volatile uint32_t*>(ctl + kCtlEpoch);
+    const bool wrap = e >= kMaxEpoch || e <= kMaxHostEpoch;  // also the first captured call
+    if (wrap) {
+        const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+        for (uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x; k < n_ws; k += stride)
+            ws_words[k] = 0;
+        for (uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x; k < n_bs; k += stride)
+            bs_words[k] = 0;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        const uint32_t t =
+            __hip_atomic_fetch_add(&ctl[kCtlDone], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (t + 1 == gridDim.x) {
+            __hip_atomic_store(&ctl[kCtlDone], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&ctl[kCtlEpoch], wrap ? kMaxHostEpoch + 1 : e + 1, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 }  // namespace
 
 // ======================================================================================
@@ -2271,7 +2506,7 @@ struct uvhttp_ws_gpu_engine {
     int plan_fpt;              // k_plan frames per lane, 0 = automatic
     int walk_mode;             // stream frame discovery: 0 automatic, 1 lane, 2 wave
     void* ss_mem;              // stream-decode scratch
-    uint32_t ss_frames, ss_streams;
+    uint32_t ss_frames, ss_streams, ss_reads;
     StreamScratch ss;
     void* wt_mem;              // single-pass walk scratch (frame starts per connection slice)
     uint64_t wt_cap;
@@ -2281,6 +2516,13 @@ struct uvhttp_ws_gpu_engine {
     int build_small;           // emit shape for frames < 4 KiB (UVHTTP_WS_BUILD_SMALL, tuning)
     uint64_t build_frames_max; // frame-grouped LDS emit below this average frame (UVHTTP_WS_BUILD_FRAMES; 0 = off)
     int compact_mode;          // 0 automatic, 1 arena-driven gather, 2 wire-driven scatter
+    uint32_t* ctl;             // device control words (kCtl*), own allocation
+    uint32_t faults_seen;      // ctl[kCtlFaults] at the last engine_sync
+    uint32_t max_polls;        // look-back wait bound (UVHTTP_WS_MAX_POLLS: tests)
+    int capturing;             // the current call is being captured into a graph
+    hipStream_t last_stream;   // stream of the previous call (calls are serialised on it)
+    int have_last;
+    hipEvent_t order_ev;       // orders a call on a new stream after the previous stream's work
     hipEvent_t ev[2 * 1024];
     int ev_created;
     int ev_used;       // event pairs recorded and not yet harvested
@@ -2326,12 +2568,28 @@ int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out) {
     if (!e) return UVHTTP_WS_GPU_ENOMEM;
     e->device = device;
     e->store_aux = 18;
+    e->max_polls = kMaxPolls;
+    if (const char* mp = getenv("UVHTTP_WS_MAX_POLLS")) e->max_polls = (uint32_t)strtoul(mp, nullptr, 0);
+    {
+        int prev = 0;
+        (void)hipGetDevice(&prev);
+        (void)hipSetDevice(device);
+        hipError_t h = hipMalloc(&e->ctl, kCtlWords * sizeof(uint32_t));
+        if (h == hipSuccess) h = hipMemset(e->ctl, 0, kCtlWords * sizeof(uint32_t));
+        if (h == hipSuccess) h = hipDeviceSynchronize();
+        (void)hipSetDevice(prev);
+        if (h != hipSuccess) {
+            if (e->ctl) (void)hipFree(e->ctl);
+            free(e);
+            return UVHTTP_WS_GPU_ENOMEM;
+        }
+    }
     if (const char* sp = getenv("UVHTTP_WS_STORE_POLICY")) e->store_aux = atoi(sp) == 18 ? 18 : 0;
     if (const char* fp = getenv("UVHTTP_WS_PLAN_FPT")) e->plan_fpt = atoi(fp);
     // test hook: start near the end of the epoch space to exercise the wrap-around clear
     if (const char* ep = getenv("UVHTTP_WS_EPOCH_START")) {
         const unsigned long v = strtoul(ep, nullptr, 0);
-        e->epoch = v < kMaxEpoch ? (uint32_t)v : 0;
+        e->epoch = v < kMaxHostEpoch ? (uint32_t)v : 0;
     }
     if (const char* bs = getenv("UVHTTP_WS_BUILD_SMALL")) e->build_small = atoi(bs);
     e->build_frames_max = 4096;
@@ -2354,6 +2612,8 @@ void uvhttp_ws_gpu_engine_free(uvhttp_ws_gpu_engine_t* e) {
     if (e->ss_mem) (void)hipFree(e->ss_mem);
     if (e->bs_mem) (void)hipFree(e->bs_mem);
     if (e->wt_mem) (void)hipFree(e->wt_mem);
+    if (e->ctl) (void)hipFree(e->ctl);
+    if (e->order_ev) (void)hipEventDestroy(e->order_ev);
     for (int k = 0; k < e->ev_created; ++k) (void)hipEventDestroy(e->ev[k]);
     (void)hipSetDevice(prev);
     free(e);
@@ -2361,6 +2621,27 @@ void uvhttp_ws_gpu_engine_free(uvhttp_ws_gpu_engine_t* e) {
 
 const char* uvhttp_ws_gpu_engine_last_error(const uvhttp_ws_gpu_engine_t* e) {
     return e ? e->err : "no engine";
+}
+
+int uvhttp_ws_gpu_engine_sync(uvhttp_ws_gpu_engine_t* e, void* stream) {
+    if (!e) return UVHTTP_WS_GPU_EINVAL;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    if (prev != e->device) (void)hipSetDevice(e->device);
+    hipError_t h = hipStreamSynchronize((hipStream_t)stream);
+    uint32_t faults = e->faults_seen;
+    if (h == hipSuccess)
+        h = hipMemcpy(&faults, e->ctl + kCtlFaults, sizeof(faults), hipMemcpyDeviceToHost);
+    if (prev != e->device) (void)hipSetDevice(prev);
+    if (h != hipSuccess) return set_err(e, UVHTTP_WS_GPU_ELAUNCH, "sync", h);
+    if (faults != e->faults_seen) {
+        const uint32_t n = faults - e->faults_seen;
+        e->faults_seen = faults;
+        snprintf(e->err, sizeof(e->err),
+                 "%u call(s) gave up waiting in the single-pass scan: nothing of them was decoded", n);
+        return UVHTTP_WS_GPU_ELAUNCH;
+    }
+    return UVHTTP_WS_GPU_OK;
 }
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -2374,6 +2655,9 @@ int uvhttp_ws_gpu_engine_reserve(uvhttp_ws_gpu_engine_t* e, uint32_t max_frames,
     if (e->ws_mem && max_frames <= e->cap_frames && tiles <= e->cap_tiles &&
         atiles <= e->cap_arena_tiles)
         return UVHTTP_WS_GPU_OK;
+    if (e->capturing)
+        return set_err(e, UVHTTP_WS_GPU_EINVAL, "workspace too small for a captured call: reserve first",
+                       hipSuccess);
     const uint32_t fr = max_frames > e->cap_frames ? max_frames : e->cap_frames;
     const uint64_t tl = tiles > e->cap_tiles ? tiles : e->cap_tiles;
     const uint64_t at = atiles > e->cap_arena_tiles ? atiles : e->cap_arena_tiles;
@@ -2418,6 +2702,7 @@ int uvhttp_ws_gpu_engine_reserve(uvhttp_ws_gpu_engine_t* e, uint32_t max_frames,
     e->ws.tile_first = (uint64_t*)(b + off_tiles);
     e->ws.first_bad = (uint64_t*)(b + off_bad);
     e->ws.arena_first = (uint64_t*)(b + off_arena);
+    e->ws.ctl = e->ctl;
     e->ws_bytes = bytes;
     e->cap_frames = fr;
     e->cap_tiles = tl;
@@ -2473,7 +2758,7 @@ int uvhttp_ws_gpu_engine_kernel_time(uvhttp_ws_gpu_engine_t* e, double* ms, uint
 }
 
 static int timing_begin(uvhttp_ws_gpu_engine_t* e, hipStream_t s) {
-    if (!e->timing) return -1;
+    if (!e->timing || e->capturing) return -1;
     if (e->ev_used * 2 + 2 > (int)(sizeof(e->ev) / sizeof(e->ev[0]))) harvest(e);
     const int k = e->ev_used;
     while (e->ev_created < 2 * k + 2) {
@@ -2495,12 +2780,40 @@ static void timing_end(uvhttp_ws_gpu_engine_t* e, int k, hipStream_t s) {
 // can carry a live tag.
 
 static uint32_t next_epoch(uvhttp_ws_gpu_engine_t* e, hipStream_t s) {
-    if (e->epoch >= kMaxEpoch) {
+    if (e->capturing) {  // the replay's k_epoch issues it; kernels read ctl[kCtlEpoch]
+        hipLaunchKernelGGL(k_epoch, dim3(64), dim3(kBlock), 0, s, e->ctl, (uint64_t*)e->ws_mem,
+                           (uint64_t)(e->ws_mem ? e->ws_bytes / 8 : 0), (uint64_t*)e->bs_mem,
+                           (uint64_t)(e->bs_mem ? e->bs_tiles * sizeof(BuildRec) / 8 : 0));
+        return 0;
+    }
+    if (e->epoch >= kMaxHostEpoch) {
         (void)hipMemsetAsync(e->ws_mem, 0, e->ws_bytes, s);
         if (e->bs_mem) (void)hipMemsetAsync(e->bs_mem, 0, e->bs_tiles * sizeof(BuildRec), s);
         e->epoch = 0;
     }
     return ++e->epoch;
+}
+
+// scope of one API call: call_begin decides capture mode; leaving the call clears it
+struct CallScope {
+    uvhttp_ws_gpu_engine_t* e;
+    ~CallScope() { e->capturing = 0; }
+};
+
+// Start of every call: is the stream being captured, and does the call switch streams?  The
+// engine's workspace serves one call at a time, so a call on a new stream first waits for
+// what the previous call's stream has queued.
+static void call_begin(uvhttp_ws_gpu_engine_t* e, hipStream_t s) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) != hipSuccess) cs = hipStreamCaptureStatusNone;
+    e->capturing = cs == hipStreamCaptureStatusActive;
+    if (!e->capturing && e->have_last && e->last_stream != s) {
+        if (!e->order_ev) (void)hipEventCreateWithFlags(&e->order_ev, hipEventDisableTiming);
+        if (e->order_ev && hipEventRecord(e->order_ev, e->last_stream) == hipSuccess)
+            (void)hipStreamWaitEvent(s, e->order_ev, 0);
+    }
+    e->last_stream = s;
+    e->have_last = 1;
 }
 
 // k_plan launch: frames per lane chosen so the grid stays within ~512 blocks — every block
@@ -2545,6 +2858,8 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
                       void* stream) {
     int rc = check_batch(e, b, d_desc, d_summary);
     if (rc) return rc;
+    CallScope scope{e};
+    call_begin(e, (hipStream_t)stream);
     const uint64_t n_tiles = (b->wire_len + kMapTile - 1) / kMapTile;
     // arena tiles: bounded by both the capacity and the data payload that can exist
     uint64_t arena_need = arena ? (arena_cap < b->wire_len ? arena_cap : b->wire_len) : 0;
@@ -2571,7 +2886,8 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
     a.arena_cap = arena_cap;
     a.n_arena_tiles = n_atiles;
     a.summary = d_summary;
-
+    a.max_polls = e->max_polls;
+    a.dev_epoch = e->capturing ? 1u : 0u;
     a.epoch = next_epoch(e, s);
 
     launch_plan(e, a, a.n, d_desc, d_msgs, s);
@@ -2645,10 +2961,17 @@ int uvhttp_ws_gpu_decode_compact(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batc
     return run_decode(e, b, d_arena, arena_cap, d_desc, d_msgs, d_summary, stream);
 }
 
-static int reserve_streams(uvhttp_ws_gpu_engine_t* e, uint32_t frames, uint32_t streams) {
-    if (e->ss_mem && frames <= e->ss_frames && streams <= e->ss_streams) return UVHTTP_WS_GPU_OK;
+static int reserve_streams(uvhttp_ws_gpu_engine_t* e, uint32_t frames, uint32_t streams,
+                           uint32_t reads) {
+    if (reads == 0) reads = 1;
+    if (e->ss_mem && frames <= e->ss_frames && streams <= e->ss_streams && reads <= e->ss_reads)
+        return UVHTTP_WS_GPU_OK;
+    if (e->capturing)
+        return set_err(e, UVHTTP_WS_GPU_EINVAL, "stream scratch too small for a captured call",
+                       hipSuccess);
     const uint32_t fr = frames > e->ss_frames ? frames : e->ss_frames;
     const uint32_t sn = streams > e->ss_streams ? streams : e->ss_streams;
+    const uint32_t rd = reads > e->ss_reads ? reads : e->ss_reads;
     const uint64_t sblk = (sn + kBlock - 1) / kBlock + 2;
     size_t o_off = 0;
     size_t o_seg = align_up(o_off + (size_t)fr * 8, 256);
@@ -2659,7 +2982,10 @@ static int reserve_streams(uvhttp_ws_gpu_engine_t* e, uint32_t frames, uint32_t 
     size_t o_wbase = align_up(o_tot + 16, 256);
     size_t o_bblk = align_up(o_wbase + (size_t)sn * 8, 256);
     size_t o_single = align_up(o_bblk + sblk * 8, 256);
-    size_t bytes = align_up(o_single + 16, 256);
+    size_t o_stop = align_up(o_single + 16, 256);
+    size_t o_ssize = align_up(o_stop + (size_t)sn * 8, 256);
+    size_t o_rsize = align_up(o_ssize + (size_t)sn * 8, 256);
+    size_t bytes = align_up(o_rsize + (size_t)rd * 8, 256);
     int prev = 0;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(e->device);
@@ -2668,7 +2994,7 @@ static int reserve_streams(uvhttp_ws_gpu_engine_t* e, uint32_t frames, uint32_t 
     const hipError_t h = hipMalloc(&e->ss_mem, bytes);
     (void)hipSetDevice(prev);
     if (h != hipSuccess) {
-        e->ss_frames = e->ss_streams = 0;
+        e->ss_frames = e->ss_streams = e->ss_reads = 0;
         return set_err(e, UVHTTP_WS_GPU_ENOMEM, "hipMalloc stream scratch", h);
     }
     char* b = (char*)e->ss_mem;
@@ -2681,8 +3007,12 @@ static int reserve_streams(uvhttp_ws_gpu_engine_t* e, uint32_t frames, uint32_t 
     e->ss.walk_base = (uint64_t*)(b + o_wbase);
     e->ss.bound_blk = (uint64_t*)(b + o_bblk);
     e->ss.walk_single = (uint32_t*)(b + o_single);
+    e->ss.walk_stop = (uint64_t*)(b + o_stop);
+    e->ss.stop_size = (uint64_t*)(b + o_ssize);
+    e->ss.read_size = (uint64_t*)(b + o_rsize);
     e->ss_frames = fr;
     e->ss_streams = sn;
+    e->ss_reads = rd;
     return UVHTTP_WS_GPU_OK;
 }
 
@@ -2690,17 +3020,28 @@ int uvhttp_ws_gpu_decode_streams(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uin
                                  const uvhttp_ws_stream_t* d_streams, uint32_t n_streams,
                                  uint32_t max_frames, uvhttp_ws_frame_desc_t* d_desc,
                                  uvhttp_ws_stream_result_t* d_results, void* stream) {
+    return uvhttp_ws_gpu_decode_reads(e, d_wire, wire_len, d_streams, n_streams, nullptr, 0,
+                                      max_frames, d_desc, d_results, stream);
+}
+
+int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint64_t wire_len,
+                               const uvhttp_ws_stream_t* d_streams, uint32_t n_streams,
+                               const uint64_t* d_read_end, uint32_t n_reads_total,
+                               uint32_t max_frames, uvhttp_ws_frame_desc_t* d_desc,
+                               uvhttp_ws_stream_result_t* d_results, void* stream) {
     if (!e || (!d_wire && wire_len) || (!d_streams && n_streams) || !d_results ||
-        (!d_desc && max_frames))
+        (!d_desc && max_frames) || (!d_read_end && n_reads_total))
         return UVHTTP_WS_GPU_EINVAL;
     if (((uintptr_t)d_wire) & 15u)
         return set_err(e, UVHTTP_WS_GPU_EINVAL, "wire must be 16-byte aligned", hipSuccess);
     if (max_frames > kMaxFrames || n_streams > kMaxFrames)
         return set_err(e, UVHTTP_WS_GPU_EINVAL, "too many frames/streams", hipSuccess);
     if (!n_streams) return UVHTTP_WS_GPU_OK;
+    CallScope scope{e};
+    call_begin(e, (hipStream_t)stream);
     const uint32_t cap = max_frames ? max_frames : 1;
     int rc = uvhttp_ws_gpu_engine_reserve(e, cap, wire_len, 0);
-    if (!rc) rc = reserve_streams(e, cap, n_streams);
+    if (!rc) rc = reserve_streams(e, cap, n_streams, n_reads_total);
     if (rc) return rc;
     int prev = 0;
     (void)hipGetDevice(&prev);
@@ -2713,6 +3054,8 @@ int uvhttp_ws_gpu_decode_streams(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uin
     w.streams = d_streams;
     w.n_streams = n_streams;
     w.max_frames = max_frames;
+    w.read_end = d_read_end;
+    w.n_reads_total = n_reads_total;
     w.results = d_results;
     w.sc = e->ss;
     const uint32_t nsb = (n_streams + kBlock - 1) / kBlock;
@@ -2724,7 +3067,7 @@ int uvhttp_ws_gpu_decode_streams(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uin
         // single pass when the offset scratch fits: bound <= wire/2 + one per connection
         // (4-byte entries, so at most 2 bytes per wire byte; capped at 8 GiB)
         const uint64_t want = wire_len / 2 + n_streams + 1;
-        if (e->walk_single_off == 0 && want * 4 <= (8ull << 30) && want > e->wt_cap) {
+        if (e->walk_single_off == 0 && !e->capturing && want * 4 <= (8ull << 30) && want > e->wt_cap) {
             if (e->wt_mem) (void)hipFree(e->wt_mem);
             e->wt_mem = nullptr;
             e->wt_cap = 0;
@@ -2762,12 +3105,14 @@ int uvhttp_ws_gpu_decode_streams(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uin
     a.n_dev = e->ss.n_total;
     a.open_after = e->ss.open_after;
     a.seg_bad = e->ss.seg_bad;
+    a.max_polls = e->max_polls;
+    a.dev_epoch = e->capturing ? 1u : 0u;
     a.epoch = next_epoch(e, s);
     launch_plan(e, a, cap, d_desc, nullptr, s);
     const uint32_t grid_f = (cap + kBlock - 1) / kBlock;
     const uint32_t grid_m = grid_f > nsb ? grid_f : nsb;
     hipLaunchKernelGGL(k_stream_mark, dim3(grid_m), dim3(kBlock), 0, s, a, d_desc, d_results,
-                       n_streams);
+                       n_streams, e->ws, e->ss, d_read_end);
     int blk = e->tile_block ? e->tile_block : 256, vpt = e->tile_block ? e->tile_vpt : 2;
     const uint64_t tile_bytes = (uint64_t)blk * vpt * 16;
     const uint64_t n_ptiles = (wire_len + tile_bytes - 1) / tile_bytes;
@@ -2801,6 +3146,8 @@ int uvhttp_ws_gpu_build_frames(uvhttp_ws_gpu_engine_t* e, const uint8_t* d_src, 
     if (((uintptr_t)d_out) & 15u)
         return set_err(e, UVHTTP_WS_GPU_EINVAL, "out must be 16-byte aligned", hipSuccess);
     if (n_frames > kMaxFrames) return set_err(e, UVHTTP_WS_GPU_EINVAL, "too many frames", hipSuccess);
+    CallScope scope{e};
+    call_begin(e, (hipStream_t)stream);
     // scratch: reuse the engine workspace (block/group aggregates as u64, arena map)
     int rc = uvhttp_ws_gpu_engine_reserve(e, n_frames ? n_frames : 1, 0, 0);
     if (rc) return rc;
@@ -2837,6 +3184,11 @@ int uvhttp_ws_gpu_build_frames(uvhttp_ws_gpu_engine_t* e, const uint8_t* d_src, 
     b.map_shift = shift;
     b.n_map = grouped ? 0 : (out_cap + (1ull << shift) - 1) >> shift;  // grouped: no map records
     if (!grouped && b.n_map + 1 > e->bs_tiles) {
+        if (e->capturing) {
+            if (prev != e->device) (void)hipSetDevice(prev);
+            return set_err(e, UVHTTP_WS_GPU_EINVAL, "build map too small for a captured call",
+                           hipSuccess);
+        }
         if (e->bs_mem) (void)hipFree(e->bs_mem);
         e->bs_mem = nullptr;
         e->bs_tiles = 0;
@@ -2854,6 +3206,8 @@ int uvhttp_ws_gpu_build_frames(uvhttp_ws_gpu_engine_t* e, const uint8_t* d_src, 
         e->bs_tiles = b.n_map + 1;
     }
     b.mrec = reinterpret_cast<BuildRec*>(e->bs_mem);
+    b.ctl = e->ctl;
+    b.dev_epoch = e->capturing ? 1u : 0u;
     b.epoch = next_epoch(e, s);
     const uint32_t grid_f = n_frames ? (n_frames + kBlock - 1) / kBlock : 1;
     const uint32_t n_groups = (grid_f + kBlock - 1) / kBlock;
@@ -2909,6 +3263,8 @@ int uvhttp_ws_gpu_apply_mask(uvhttp_ws_gpu_engine_t* e, uint8_t* d_data, uint64_
     (void)hipGetDevice(&prev);
     if (prev != e->device) (void)hipSetDevice(e->device);
     hipStream_t s = (hipStream_t)stream;
+    CallScope scope{e};
+    call_begin(e, s);
     const int tk = timing_begin(e, s);
     hipLaunchKernelGGL(k_apply_mask, dim3((uint32_t)grid), dim3(kBlock), 0, s, d_data, len, k, head);
     timing_end(e, tk, s);

@@ -366,9 +366,16 @@ uvhttp_error_t uvhttp_ws_deliver_stream(struct uvhttp_ws_connection* c, const ui
                                         const uvhttp_ws_stream_result_t* r) {
     if (c == NULL || s == NULL || r == NULL || (s->len && wire == NULL))
         return UVHTTP_ERROR_INVALID_PARAM;
-    /* growth failed: process_data returns before touching the buffer (:836-857) */
-    if (r->first_status == UVHTTP_WS_FRAME_ERR_BUFFER ||
-        r->first_status == UVHTTP_WS_FRAME_ERR_CAPACITY)
+    /* nothing ran on the connection: a malformed descriptor, too many frames for the batch,
+     * a device fault, or the first call failed its growth check and returned before touching
+     * the buffer (src/uvhttp_websocket.c:836-857) */
+    if (r->first_status == UVHTTP_WS_FRAME_ERR_CAPACITY ||
+        r->first_status == UVHTTP_WS_FRAME_ERR_LAYOUT ||
+        r->first_status == UVHTTP_WS_FRAME_ERR_DEVICE ||
+        (r->first_status == UVHTTP_WS_FRAME_ERR_BUFFER && r->calls <= 1))
+        return UVHTTP_ERROR_INVALID_PARAM;
+    if (r->consumed_bytes > r->buffered_end || r->buffered_end > s->len ||
+        (r->n_delivered && desc == NULL))
         return UVHTTP_ERROR_INVALID_PARAM;
     if (r->recv_buffer_size != c->recv_buffer_size) {
         uint8_t* nb = (uint8_t*)realloc(c->recv_buffer, (size_t)r->recv_buffer_size);
@@ -388,9 +395,40 @@ uvhttp_error_t uvhttp_ws_deliver_stream(struct uvhttp_ws_connection* c, const ui
         const uint8_t* payload = d->payload_len ? wire + d->payload_off : NULL;
         if (dispatch_frame(c, &h, payload) != 0) break; /* cannot happen after a clean decode */
     }
-    /* what process_data leaves buffered: everything after the delivered frames */
-    const size_t rest = (size_t)(s->len - r->consumed_bytes);
+    /* what the calls leave buffered: the stream bytes after the delivered frames, up to the
+     * end of the last call that ran */
+    const size_t rest = (size_t)(r->buffered_end - r->consumed_bytes);
     if (rest) memmove(c->recv_buffer, base + r->consumed_bytes, rest);
     c->recv_buffer_pos = rest;
+    /* a complete data frame rejected by the fragment state machine: the reference unmasked it
+     * in recv_buffer (:944) before its fragment checks failed (:964-1000), and those checks
+     * may already have changed the fragment state (a start records its opcode before the
+     * size check) — replay that frame's unmask and dispatch, which fails the same way */
+    if ((r->first_status == UVHTTP_WS_FRAME_ERR_FRAGMENT ||
+         r->first_status == UVHTTP_WS_FRAME_ERR_MESSAGE) && desc != NULL) {
+        const uvhttp_ws_frame_desc_t* d = &desc[r->first_frame + r->n_delivered];
+        const size_t at = (size_t)(d->payload_off - s->begin - r->consumed_bytes);
+        if (d->payload_len && at + d->payload_len <= rest) {
+            uint8_t* payload = c->recv_buffer + at;
+            if (d->flags & UVHTTP_WS_FLAG_MASK) {
+                uint8_t key[4];
+                memcpy(key, &d->masking_key, 4); /* k0 = low byte */
+                uvhttp_ws_apply_mask(payload, (size_t)d->payload_len, key);
+            }
+            uvhttp_ws_frame_header_t h;
+            memset(&h, 0, sizeof(h));
+            h.fin = (d->flags & UVHTTP_WS_FLAG_FIN) ? 1 : 0;
+            h.mask = (d->flags & UVHTTP_WS_FLAG_MASK) ? 1 : 0;
+            h.opcode = d->opcode & 0x0F;
+            h.payload_length = d->payload_len;
+            (void)dispatch_frame(c, &h, payload);
+        } else if (!d->payload_len) {
+            uvhttp_ws_frame_header_t h;
+            memset(&h, 0, sizeof(h));
+            h.fin = (d->flags & UVHTTP_WS_FLAG_FIN) ? 1 : 0;
+            h.opcode = d->opcode & 0x0F;
+            (void)dispatch_frame(c, &h, NULL);
+        }
+    }
     return r->status == 0 ? UVHTTP_OK : UVHTTP_ERROR_INVALID_PARAM;
 }
