@@ -11,7 +11,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Iinclude -Wall -Werror 
             -mcode-object-version=5
 CFLAGS := -O2 -DNDEBUG -fPIC -std=gnu11 -Iinclude -Wall -Wextra -Werror
 
-all: $(LIB) oracle
+all: $(LIB) oracle ctests
 
 $(BUILD)/ws_gpu.o: uvhttp_amd/csrc/ws_gpu.hip include/uvhttp_ws_amd.h
 	@mkdir -p $(BUILD)
@@ -21,16 +21,25 @@ $(BUILD)/tls_gpu.o: uvhttp_amd/csrc/tls_gpu.hip include/uvhttp_tls_amd.h
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
+$(BUILD)/ws_batcher.o: uvhttp_amd/csrc/ws_batcher.hip include/uvhttp_ws_amd.h
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
 $(BUILD)/ws_host.o: uvhttp_amd/csrc/ws_host.c include/uvhttp_ws_amd.h
 	@mkdir -p $(BUILD)
 	$(CC) $(CFLAGS) -c -o $@ $<
 
-$(LIB): $(BUILD)/ws_gpu.o $(BUILD)/tls_gpu.o $(BUILD)/ws_host.o
+$(LIB): $(BUILD)/ws_gpu.o $(BUILD)/tls_gpu.o $(BUILD)/ws_batcher.o $(BUILD)/ws_host.o
 	@mkdir -p $(dir $@)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
 oracle:
 	$(MAKE) -C oracle
+
+# test programs: the C1 libuv echo harness (against the product library) and the
+# ASan/UBSan builds of the host decoder + oracle (tests/c/Makefile)
+ctests: $(LIB) oracle
+	$(MAKE) -C tests/c
 
 asm: uvhttp_amd/csrc/ws_gpu.hip uvhttp_amd/csrc/tls_gpu.hip
 	@mkdir -p $(BUILD)
@@ -40,5 +49,6 @@ asm: uvhttp_amd/csrc/ws_gpu.hip uvhttp_amd/csrc/tls_gpu.hip
 clean:
 	rm -rf $(BUILD) uvhttp_amd/lib
 	$(MAKE) -C oracle clean
+	$(MAKE) -C tests/c clean
 
-.PHONY: all oracle clean asm
+.PHONY: all oracle ctests clean asm

@@ -522,6 +522,61 @@ uvhttp_error_t uvhttp_ws_deliver_batch(struct uvhttp_ws_connection* conn, const 
                                        const uvhttp_ws_frame_desc_t* desc,
                                        const uvhttp_ws_batch_summary_t* summary);
 
+/* ---- batcher: live libuv reads -> one device decode per flush -------------------------- */
+/* The caller side of the reference, on_websocket_read (src/uvhttp_connection.c:1098-1175),
+ * calls uvhttp_ws_process_data once per libuv read.  The batcher takes those reads instead
+ * (submit_read copies them, as process_data copies into recv_buffer) and decodes everything
+ * queued at flush(): per connection, exactly the sequence of process_data calls the reads
+ * would have made — same return codes, callbacks, recv-buffer and fragment state (tests/
+ * test_c1_echo.py, tests/test_gpu_batcher.py check it against the oracle).  Callbacks fire
+ * from flush(), connection by connection in first-read order; within a connection in read
+ * order.  A flush whose queued bytes are below min_device_bytes runs the host decoder (one
+ * libuv-sized read does not pay for a device round trip); a larger one goes
+ * through the device: stage buffered bytes + reads in pinned memory -> H2D ->
+ * uvhttp_ws_gpu_decode_reads -> D2H -> uvhttp_ws_deliver_stream per connection.
+ * Not thread-safe (the loop thread owns it, like the reference). */
+typedef struct uvhttp_ws_amd_batcher uvhttp_ws_amd_batcher_t;
+/* a connection's queued reads failed: process_data returned rc (the reference then sends
+ * close 1002 and closes, :1166-1174); the batcher drops the connection's later reads until
+ * uvhttp_ws_amd_batcher_forget */
+typedef void (*uvhttp_ws_amd_failure_cb)(void* ctx, struct uvhttp_ws_connection* conn, int rc);
+typedef struct {
+    int device;                /* HIP device for large flushes; -1 = host decoder only */
+    uint64_t min_device_bytes; /* flushes with fewer queued bytes run on the host */
+    uint64_t max_bytes;        /* staging capacity (buffered bytes + reads) per flush */
+    uint32_t max_connections;  /* connections per flush */
+    uint32_t max_reads;        /* reads per flush */
+    uvhttp_ws_amd_failure_cb on_failure;
+    void* ctx;
+} uvhttp_ws_amd_batcher_config_t;
+typedef struct {
+    uint64_t flushes, device_flushes, host_flushes;
+    uint64_t host_reads, device_reads;    /* reads decoded by each path */
+    uint64_t device_frames, device_bytes; /* frames / staged bytes decoded on the device */
+    uint64_t failures;                    /* connections reported through on_failure */
+    uint64_t capacity_flushes;            /* device flushes re-run on the host (frame capacity) */
+    double device_ms;                     /* wall time of device flushes (stage -> deliver) */
+} uvhttp_ws_amd_batcher_stats_t;
+void uvhttp_ws_amd_batcher_config_init(uvhttp_ws_amd_batcher_config_t* cfg);
+/* UVHTTP_WS_GPU_ENODEV if cfg->device >= 0 names no usable MI355X (no silent host mode) */
+int uvhttp_ws_amd_batcher_create(const uvhttp_ws_amd_batcher_config_t* cfg,
+                                 uvhttp_ws_amd_batcher_t** out);
+void uvhttp_ws_amd_batcher_free(uvhttp_ws_amd_batcher_t* b);
+/* Queue one read of `conn` (the bytes are copied).  Flushes first when the read would not
+ * fit the staging capacity.  Returns UVHTTP_OK, or UVHTTP_ERROR_INVALID_PARAM for a NULL
+ * argument or a connection whose earlier reads already failed. */
+uvhttp_error_t uvhttp_ws_amd_batcher_submit_read(uvhttp_ws_amd_batcher_t* b,
+                                                 struct uvhttp_ws_connection* conn,
+                                                 const uint8_t* data, size_t len);
+/* Decode everything queued (callbacks fire here).  0, or a UVHTTP_WS_GPU_* error of the
+ * device path (then nothing of the flush was delivered and the reads stay queued). */
+int uvhttp_ws_amd_batcher_flush(uvhttp_ws_amd_batcher_t* b);
+/* Drop a connection's queued reads and failure mark (call before freeing the connection;
+ * safe from inside callbacks of a flush). */
+void uvhttp_ws_amd_batcher_forget(uvhttp_ws_amd_batcher_t* b, struct uvhttp_ws_connection* conn);
+int uvhttp_ws_amd_batcher_stats(const uvhttp_ws_amd_batcher_t* b,
+                                uvhttp_ws_amd_batcher_stats_t* out);
+
 /* Library identity, for the loader checks in tests/. */
 const char* uvhttp_ws_amd_version(void);
 

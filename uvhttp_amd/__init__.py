@@ -20,7 +20,7 @@ __all__ = [
     "lib", "LIB_PATH", "FrameHeader", "FrameDesc", "MessageDesc", "BatchSummary", "Batch",
     "WsConnectionStruct", "parse_frame_header", "apply_mask", "WsConnection", "GpuEngine",
     "GpuError", "OPCODES", "FRAME_STATUS", "gen_frame_stride", "GpuPipeline", "Stream",
-    "StreamResult", "STREAM_DT", "STREAM_RESULT_DT", "STREAM_RESULT_BYTES",
+    "StreamResult", "STREAM_DT", "STREAM_RESULT_DT", "STREAM_RESULT_BYTES", "Batcher",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -116,6 +116,7 @@ ON_MESSAGE = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_char), C.c_size_t, C
 ON_CLOSE = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_char_p)
 ON_ERROR = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_char_p)
 CONTEXT_RESOLVER = C.CFUNCTYPE(C.c_void_p, C.c_void_p)
+FAILURE_CB = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p, C.c_int)
 CONTROL_SINK = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_uint8),
                            C.c_size_t)
 
@@ -155,6 +156,23 @@ class UvhttpConfig(C.Structure):
                 ("cache_default_ttl", C.c_int), ("lru_cache_batch_eviction_size", C.c_int),
                 ("rate_limit_max_requests", C.c_int), ("rate_limit_max_window_seconds", C.c_int),
                 ("rate_limit_min_timeout_seconds", C.c_int)]
+
+
+class BatcherConfig(C.Structure):
+    """uvhttp_ws_amd_batcher_config_t"""
+    _fields_ = [("device", C.c_int), ("min_device_bytes", C.c_uint64), ("max_bytes", C.c_uint64),
+                ("max_connections", C.c_uint32), ("max_reads", C.c_uint32),
+                ("on_failure", FAILURE_CB), ("ctx", C.c_void_p)]
+
+
+class BatcherStats(C.Structure):
+    """uvhttp_ws_amd_batcher_stats_t"""
+    _fields_ = [(k, C.c_uint64) for k in ("flushes", "device_flushes", "host_flushes", "host_reads",
+                                          "device_reads", "device_frames", "device_bytes",
+                                          "failures", "capacity_flushes")] + [("device_ms", C.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 # ---- library ----------------------------------------------------------------------------
@@ -224,6 +242,15 @@ def load_library(path: str) -> C.CDLL:
                                                C.POINTER(Stream), C.POINTER(StreamResult)]),
         "uvhttp_ws_gpu_gen_frames": (C.c_int, [vp, vp, u32, u64, u64, C.c_int, C.c_int, C.c_int,
                                                vp]),
+        # batcher (include/uvhttp_ws_amd.h)
+        "uvhttp_ws_amd_batcher_config_init": (None, [C.POINTER(BatcherConfig)]),
+        "uvhttp_ws_amd_batcher_create": (C.c_int, [C.POINTER(BatcherConfig), C.POINTER(vp)]),
+        "uvhttp_ws_amd_batcher_free": (None, [vp]),
+        "uvhttp_ws_amd_batcher_submit_read": (C.c_int, [vp, C.POINTER(WsConnectionStruct), vp,
+                                                        C.c_size_t]),
+        "uvhttp_ws_amd_batcher_flush": (C.c_int, [vp]),
+        "uvhttp_ws_amd_batcher_forget": (None, [vp, C.POINTER(WsConnectionStruct)]),
+        "uvhttp_ws_amd_batcher_stats": (C.c_int, [vp, C.POINTER(BatcherStats)]),
         # TLS record layer (include/uvhttp_tls_amd.h)
         "uvhttp_tls_gpu_engine_create": (C.c_int, [C.c_int, C.POINTER(vp)]),
         "uvhttp_tls_gpu_engine_free": (None, [vp]),
@@ -677,3 +704,54 @@ class TlsEngine:
             self.h, C.c_void_p(src.data_ptr()), src.numel(), C.c_void_p(recs.data_ptr()),
             n_records, C.c_void_p(keys.data_ptr()), n_keys, C.c_void_p(out.data_ptr()),
             out.numel(), self._stream(stream)), "seal_records")
+
+
+class Batcher:
+    """uvhttp_ws_amd_batcher_t: queue live reads of WsConnection objects, decode at flush().
+    device=-1 runs the host decoder only; failures arrive in self.failures {conn ptr: rc}."""
+
+    def __init__(self, device=-1, min_device_bytes=0, max_bytes=32 << 20,
+                 max_connections=16384, max_reads=1 << 18):
+        L = lib()
+        self._L = L
+        cfg = BatcherConfig()
+        L.uvhttp_ws_amd_batcher_config_init(C.byref(cfg))
+        cfg.device, cfg.min_device_bytes, cfg.max_bytes = device, min_device_bytes, max_bytes
+        cfg.max_connections, cfg.max_reads = max_connections, max_reads
+        self.failures = {}
+        self._cb = FAILURE_CB(self._on_failure)
+        cfg.on_failure = self._cb
+        h = C.c_void_p()
+        rc = L.uvhttp_ws_amd_batcher_create(C.byref(cfg), C.byref(h))
+        if rc != 0:
+            raise GpuError(f"uvhttp_ws_amd_batcher_create rc={rc}")
+        self.h = h
+
+    def _on_failure(self, ctx, conn, rc):
+        self.failures[conn] = rc
+
+    def submit(self, conn: "WsConnection", data: bytes) -> int:
+        buf = (C.c_uint8 * max(1, len(data))).from_buffer_copy(bytes(data) or b"\0")
+        return self._L.uvhttp_ws_amd_batcher_submit_read(self.h, conn.ptr, buf, len(data))
+
+    def flush(self) -> int:
+        return self._L.uvhttp_ws_amd_batcher_flush(self.h)
+
+    def forget(self, conn: "WsConnection"):
+        self._L.uvhttp_ws_amd_batcher_forget(self.h, conn.ptr)
+
+    def stats(self) -> dict:
+        s = BatcherStats()
+        self._L.uvhttp_ws_amd_batcher_stats(self.h, C.byref(s))
+        return s.as_dict()
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._L.uvhttp_ws_amd_batcher_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

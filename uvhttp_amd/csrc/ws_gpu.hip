@@ -270,9 +270,12 @@ struct BatchArgs {
     uint32_t plan_frames;    // frames per k_plan block (kBlock * FPT)
 };
 
-// every kernel of a call starts here: a captured call reads the epoch the replay's k_epoch set
+// every kernel of a call resolves its epoch: a captured call reads the one the replay's
+// k_epoch set (a plain load: written by an earlier kernel of the stream, so visible, and
+// uniform, so it stays a scalar load — a volatile load here turned every tag test of the
+// payload kernel into vector code, +6 us on C2)
 __device__ inline void resolve_epoch(BatchArgs& a, const Workspace& ws) {
-    if (a.dev_epoch) a.epoch = *reinterpret_cast<volatile const uint32_t*>(ws.ctl + kCtlEpoch);
+    if (a.dev_epoch) a.epoch = ws.ctl[kCtlEpoch];
 }
 
 // the call's look-back gave up (k_plan recorded this epoch): nothing of it may be delivered
@@ -914,7 +917,7 @@ __device__ inline bool any_bits(const u32x4& m) { return (m.x | m.y | m.z | m.w)
 // sc1|nt (write-through, not kept in L2), measured 1.7 % faster for the 64x1 shape
 // (tools/stream_probe.hip, profiles/r01_stream_probe_policy.txt)
 template <int BLOCK, int VPT, int STORE_AUX>
-__device__ __forceinline__ void unmask_tile(const BatchArgs& a,
+__device__ __forceinline__ void unmask_tile(BatchArgs a,
                                             const uvhttp_ws_frame_desc_t* __restrict__ desc,
                                             const Workspace& ws, uint64_t tile_base,
                                             uint32_t& n_out, uint32_t& nb_out) {
@@ -939,7 +942,9 @@ __device__ __forceinline__ void unmask_tile(const BatchArgs& a,
         data[v] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.wire + la));
     }
 
-    // batch mode: frames >= nb are not delivered (read after the loads are issued)
+    // batch mode: frames >= nb are not delivered (read after the loads are issued, like the
+    // epoch of a captured call)
+    resolve_epoch(a, ws);
     const uint32_t n = nframes(a);
     const uint32_t nb = first_bad_of(a, ws, n);
     n_out = n;
@@ -1052,9 +1057,8 @@ template <int BLOCK, int VPT, int STORE_AUX = 0>
 __global__ __launch_bounds__(BLOCK) void k_unmask_inplace(
     BatchArgs a, const uvhttp_ws_frame_desc_t* __restrict__ desc, Workspace ws,
     uint64_t tile_base) {
-    resolve_epoch(a, ws);
     uint32_t n, nb;
-    unmask_tile<BLOCK, VPT, STORE_AUX>(a, desc, ws, tile_base, n, nb);
+    unmask_tile<BLOCK, VPT, STORE_AUX>(a, desc, ws, tile_base, n, nb);  // resolves the epoch
 }
 
 // ------------------------------------------------------------------------------------
@@ -1283,7 +1287,6 @@ template <int BLOCK, int VPT>
 __global__ __launch_bounds__(BLOCK) void k_scatter_compact(
     BatchArgs a, const uvhttp_ws_frame_desc_t* __restrict__ desc, Workspace ws,
     uint64_t arena_bytes_cap, uint64_t tile_base) {
-    resolve_epoch(a, ws);
     constexpr uint64_t kT = (uint64_t)BLOCK * VPT * 16;
     __shared__ uint64_t s_ps[BLOCK];  // wire offset of the payload
     __shared__ uint64_t s_pe[BLOCK];  // its end (== start: not a delivered data frame)
@@ -1313,6 +1316,7 @@ __global__ __launch_bounds__(BLOCK) void k_scatter_compact(
             data[v] = u32x4{t[0], t[1], t[2], t[3]};
         }
     }
+    resolve_epoch(a, ws);  // after the loads are issued
     const uint32_t n = nframes(a);
     const uint32_t nb = first_bad_of(a, ws, n);
     if (nb == 0 || n == 0 || t0 >= vend) return;
@@ -1959,7 +1963,7 @@ struct BuildArgs {
 };
 
 __device__ inline void resolve_epoch(BuildArgs& b) {
-    if (b.dev_epoch) b.epoch = *reinterpret_cast<volatile const uint32_t*>(b.ctl + kCtlEpoch);
+    if (b.dev_epoch) b.epoch = b.ctl[kCtlEpoch];
 }
 
 __device__ inline uint64_t build_size(const uvhttp_ws_build_desc_t& f) {
