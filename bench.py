@@ -484,6 +484,7 @@ def main():
             extra["c5_1gpu"] = c5_one_gpu(args, local)
         if args.e2e:
             extra["e2e_pcie"] = e2e_rate(n, plen, stride, CONFIGS[cfg][3], local)
+            extra["e2e_live"] = e2e_live(local)
 
     if rank == 0:
         out = {
@@ -529,6 +530,23 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def e2e_live(local, conns=1024, frames=4, size=65536, flushes=20):
+    """The live shape end to end (tests/c/batcher_e2e.c): 16 KiB libuv reads of `conns`
+    connections queued in the batcher, one device flush per round (stage, H2D,
+    decode_reads, D2H, on_message per connection); the same reads through the host decoder
+    on one core beside it.  PCIe- and host-memcpy-bound; recorded in DESIGN.md, never the
+    metric."""
+    exe = os.path.join(REPO, "tests", "c", "_build", "batcher_e2e")
+    out = {}
+    for name, dev in (("device", local), ("host_1core", -1)):
+        p = subprocess.run([exe, "--conns", str(conns), "--frames", str(frames), "--size",
+                            str(size), "--flushes", str(flushes if dev >= 0 else 3),
+                            "--device", str(dev)], capture_output=True, text=True, timeout=600)
+        out[name] = json.loads(p.stdout.strip().splitlines()[-1]) if p.returncode == 0 else \
+            {"error": p.returncode, "stderr": p.stderr[-300:]}
+    return out
 
 
 def e2e_rate(n, plen, stride, mm, local, depth=3, slot_frames=1024):

@@ -1,0 +1,109 @@
+/*
+ * batcher_e2e.c — end-to-end rate of the live shape (measurement only): libuv-
+ * sized reads of many connections start and end in host memory; each flush stages them,
+ * copies them to the MI355X, decodes them there (uvhttp_ws_gpu_decode_reads), copies the
+ * result back and delivers on_message per connection (uvhttp_ws_amd_batcher_*).  The same
+ * reads through the host decoder (--device -1: process_data per read on this core) give the
+ * reference-shaped CPU rate.  Prints one JSON line.
+ *
+ *   batcher_e2e --conns N --frames M --size S --read R --flushes F --device D
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "uvhttp_ws_amd.h"
+
+static uint64_t g_msgs, g_bytes;
+static int on_message(uvhttp_ws_connection_t* c, const char* d, size_t n, int op) {
+    (void)c;
+    (void)d;
+    (void)op;
+    g_msgs++;
+    g_bytes += n;
+    return 0;
+}
+
+static double now_s(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+
+int main(int argc, char** argv) {
+    int conns = 1024, frames = 4, flushes = 20, device = 0;
+    size_t size = 65536, rd = 16384;
+    for (int i = 1; i + 1 < argc; i += 2) {
+        if (!strcmp(argv[i], "--conns")) conns = atoi(argv[i + 1]);
+        else if (!strcmp(argv[i], "--frames")) frames = atoi(argv[i + 1]);
+        else if (!strcmp(argv[i], "--size")) size = (size_t)strtoull(argv[i + 1], NULL, 10);
+        else if (!strcmp(argv[i], "--read")) rd = (size_t)strtoull(argv[i + 1], NULL, 10);
+        else if (!strcmp(argv[i], "--flushes")) flushes = atoi(argv[i + 1]);
+        else if (!strcmp(argv[i], "--device")) device = atoi(argv[i + 1]);
+    }
+    /* one connection's stream: M masked BINARY frames of S bytes (every connection sends
+     * the same bytes; keys differ per frame) */
+    const size_t hs = size < 126 ? 2 : size < 65536 ? 4 : 10;
+    const size_t flen = hs + 4 + size, slen = flen * (size_t)frames;
+    uint8_t* stream = (uint8_t*)malloc(slen);
+    uint64_t s = 12345;
+    for (int f = 0; f < frames; ++f) {
+        uint8_t* p = stream + (size_t)f * flen;
+        p[0] = 0x82;
+        if (hs == 2) p[1] = 0x80 | (uint8_t)size;
+        else if (hs == 4) { p[1] = 0x80 | 126; p[2] = (uint8_t)(size >> 8); p[3] = (uint8_t)size; }
+        else { p[1] = 0x80 | 127; for (int k = 0; k < 8; ++k) p[2 + k] = (uint8_t)(size >> (56 - 8 * k)); }
+        for (size_t b = 0; b < 4 + size; ++b) {
+            s = s * 6364136223846793005ull + 1442695040888963407ull;
+            p[hs + b] = (uint8_t)(s >> 33);
+        }
+    }
+    uvhttp_ws_connection_t** cs = (uvhttp_ws_connection_t**)calloc((size_t)conns, sizeof(*cs));
+    for (int c = 0; c < conns; ++c) {
+        cs[c] = uvhttp_ws_connection_create(-1, NULL, 1, NULL);
+        uvhttp_ws_set_callbacks(cs[c], on_message, NULL, NULL);
+    }
+    uvhttp_ws_amd_batcher_config_t cfg;
+    uvhttp_ws_amd_batcher_config_init(&cfg);
+    cfg.device = device;
+    cfg.min_device_bytes = 0;
+    cfg.max_bytes = (uint64_t)conns * (slen + 64) + (1u << 20);
+    cfg.max_connections = (uint32_t)conns;
+    cfg.max_reads = (uint32_t)((size_t)conns * (slen / rd + 2));
+    uvhttp_ws_amd_batcher_t* b = NULL;
+    if (uvhttp_ws_amd_batcher_create(&cfg, &b) != 0) {
+        fprintf(stderr, "batcher_create failed\n");
+        return 1;
+    }
+    double t0 = 0;
+    for (int it = -2; it < flushes; ++it) {  /* two warm-up flushes */
+        if (it == 0) {
+            g_msgs = g_bytes = 0;
+            t0 = now_s();
+        }
+        for (int c = 0; c < conns; ++c)
+            for (size_t o = 0; o < slen; o += rd)
+                if (uvhttp_ws_amd_batcher_submit_read(b, cs[c], stream + o, o + rd <= slen ? rd : slen - o)) return 2;
+        if (uvhttp_ws_amd_batcher_flush(b) != 0) return 3;
+    }
+    const double el = now_s() - t0;
+    uvhttp_ws_amd_batcher_stats_t st;
+    uvhttp_ws_amd_batcher_stats(b, &st);
+    const double payload = (double)size * frames * conns * flushes;
+    printf("{\"path\": \"%s\", \"value\": %.3f, \"unit\": \"GiB/s\", \"conns\": %d, "
+           "\"frames_per_conn\": %d, \"payload\": %zu, \"read\": %zu, \"flushes\": %d, "
+           "\"ms_per_flush\": %.3f, \"messages_ok\": %d, \"device_flushes\": %llu, "
+           "\"device_ms_total\": %.1f}\n",
+           device >= 0 ? "device batcher (stage, H2D, decode_reads, D2H, deliver)"
+                       : "host decoder (process_data per read, 1 core)",
+           payload / el / (1024.0 * 1024 * 1024), conns, frames, size, rd, flushes,
+           el * 1e3 / flushes, g_msgs == (uint64_t)conns * frames * flushes,
+           (unsigned long long)st.device_flushes, st.device_ms);
+    uvhttp_ws_amd_batcher_free(b);
+    for (int c = 0; c < conns; ++c) uvhttp_ws_connection_free(cs[c]);
+    free(cs);
+    free(stream);
+    return 0;
+}

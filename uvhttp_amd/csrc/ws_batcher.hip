@@ -149,6 +149,26 @@ static int flush_device(uvhttp_ws_amd_batcher_t* b) {
     int prev = 0;
     (void)hipGetDevice(&prev);
     if (prev != b->cfg.device) (void)hipSetDevice(b->cfg.device);
+    // frames this flush can hold: a server connection's frames are >= 6 bytes except a
+    // failing last one, so bytes / 6 + connections never overflows for servers; the
+    // descriptor buffers grow to that bound on demand
+    const uint64_t bound = pos / 6 + nk + 1;
+    if (bound > b->max_frames) {
+        const uint64_t nf = bound > 2ull * b->max_frames ? bound : 2ull * b->max_frames;
+        (void)hipHostFree(b->h_desc);
+        (void)hipFree(b->d_desc);
+        b->h_desc = nullptr;
+        b->d_desc = nullptr;
+        b->max_frames = 0;
+        if (nf > 0xFFFFFFFFull ||
+            hipHostMalloc((void**)&b->h_desc, nf * sizeof(uvhttp_ws_frame_desc_t), hipHostMallocDefault) != hipSuccess ||
+            hipMalloc((void**)&b->d_desc, nf * sizeof(uvhttp_ws_frame_desc_t)) != hipSuccess ||
+            uvhttp_ws_gpu_engine_reserve(b->eng, (uint32_t)nf, b->wire_cap, 0) != 0) {
+            if (prev != b->cfg.device) (void)hipSetDevice(prev);
+            return UVHTTP_WS_GPU_ENOMEM;
+        }
+        b->max_frames = (uint32_t)nf;
+    }
     hipStream_t s = b->stream;
     int rc = UVHTTP_WS_GPU_OK;
     hipError_t h = hipMemcpyAsync(b->d_wire, b->h_wire, pos, hipMemcpyHostToDevice, s);
@@ -228,6 +248,7 @@ int uvhttp_ws_amd_batcher_create(const uvhttp_ws_amd_batcher_config_t* cfg,
     if (!b) return UVHTTP_WS_GPU_ENOMEM;
     b->cfg = *cfg;
     memset(&b->st, 0, sizeof(b->st));
+    b->arena.reserve(cfg->max_bytes < (64ull << 20) ? cfg->max_bytes : (64ull << 20));
     if (cfg->device >= 0) {
         int rc = uvhttp_ws_gpu_engine_create(cfg->device, &b->eng);
         if (rc) {
@@ -235,10 +256,9 @@ int uvhttp_ws_amd_batcher_create(const uvhttp_ws_amd_batcher_config_t* cfg,
             delete b;
             return rc;
         }
-        // frames per flush: a server connection's frames are >= 6 bytes except a failing
-        // last one, so bytes / 6 + connections never overflows for servers
+        // descriptor capacity starts small and grows with the flushes (flush_device)
         b->wire_cap = cfg->max_bytes + 16ull * cfg->max_connections + 64;
-        b->max_frames = (uint32_t)(cfg->max_bytes / 6 + cfg->max_connections);
+        b->max_frames = 65536;
         int prev = 0;
         (void)hipGetDevice(&prev);
         (void)hipSetDevice(cfg->device);
