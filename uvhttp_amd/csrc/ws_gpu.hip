@@ -225,22 +225,11 @@ __device__ inline uint32_t tag_get(uint64_t v, uint32_t epoch, uint32_t none) {
 
 // extra scratch of the stream decode (one allocation per engine, grown on demand)
 struct StreamScratch {
-    uint64_t* frame_off;   // [max_frames] frame starts found by the walk
-    uint32_t* frame_seg;   // [max_frames] connection of each frame
-    uint64_t* open_after;  // [max_frames] open fragmented bytes after the frame
-    uint32_t* seg_bad;     // [n_streams] first undelivered frame of each connection
-    uint32_t* walk_agg;    // [stream blocks + 1] frame counts per block, then prefixes
-    uint32_t* n_total;     // [1] frames found (device-side frame count)
-    // single-pass wave walk: each connection's frame starts (relative u32) go to its slice of
-    // walk_tmp during the counting walk, then are copied into place (no second walk)
-    uint32_t* walk_tmp;    // [tmp_cap]
-    uint64_t tmp_cap;      // 0 = single pass unavailable
-    uint64_t* walk_base;   // [n_streams] slice start within its 256-connection block
-    uint64_t* bound_blk;   // [stream blocks + 1] slice totals, then prefixes; [nb] = total
-    uint32_t* walk_single; // [1] 1 when every slice fits walk_tmp
-    uint64_t* walk_stop;   // [n_streams] (kind << 32) | call where the walk stopped
-    uint64_t* stop_size;   // [n_streams] recv-buffer size after that call
+    uint64_t* frame_off;   // [max_frames] two-pass walk: frame starts; then every frame's end
+    uint32_t* n_total;     // [1] frames found (0 on capacity overflow)
     uint64_t* read_size;   // [n_reads_total] recv-buffer size after each call
+    uint32_t* walk_tmp;    // single pass: per-connection slices of 32-bit frame starts
+    uint32_t* agg;         // [n_streams / 256 + 1] lane walk block counts -> prefixes
 };
 
 struct BatchArgs {
@@ -256,13 +245,11 @@ struct BatchArgs {
     uint8_t* arena;          // compact mode (nullptr: in-place)
     uint64_t arena_cap;
     uint64_t n_arena_tiles;
-    // stream mode (streams != nullptr): frames come from the walk, n is the capacity and the
-    // real count is *n_dev; limits and initial fragment state are per connection
+    // stream mode (streams != nullptr; only the claims and payload kernels run): frames come
+    // from the walk, n is the capacity and the real count is *n_dev; a frame is delivered iff
+    // its descriptor says OK
     const uvhttp_ws_stream_t* streams;
-    const uint32_t* frame_seg;
     const uint32_t* n_dev;
-    uint64_t* open_after;
-    uint32_t* seg_bad;
     uint32_t epoch;          // tag of this call's map / first_bad entries
     uint32_t dev_epoch;      // 1: a captured call, the epoch is ws.ctl[kCtlEpoch]
     uint32_t max_polls;      // look-back wait bound (0: give up at the first wait; tests)
@@ -305,28 +292,15 @@ struct SegInfo {
 
 __device__ inline SegInfo seg_info(const BatchArgs& a, uint32_t i, uint32_t n) {
     SegInfo g;
-    if (a.streams) {
-        g.seg = a.frame_seg[i];
-        g.head = (i == 0) || a.frame_seg[i - 1] != g.seg;
-        g.last = (i + 1 == n) || a.frame_seg[i + 1] != g.seg;
-        const uvhttp_ws_stream_t st = a.streams[g.seg];
-        g.end = g.last ? st.begin + st.len : frame_start(a, i + 1);
-        g.max_frame_size = st.max_frame_size;
-        g.max_message_size = st.max_message_size;
-        g.is_server = st.is_server;
-        g.init_pending = st.pending_bytes;
-        g.init_opcode = st.pending_opcode;
-    } else {
-        g.seg = 0;
-        g.head = (i == 0);
-        g.last = (i + 1 == n);
-        g.end = g.last ? a.wire_len : frame_start(a, i + 1);
-        g.max_frame_size = a.max_frame_size;
-        g.max_message_size = a.max_message_size;
-        g.is_server = a.is_server;
-        g.init_pending = 0;
-        g.init_opcode = 0;
-    }
+    g.seg = 0;
+    g.head = (i == 0);
+    g.last = (i + 1 == n);
+    g.end = g.last ? a.wire_len : frame_start(a, i + 1);
+    g.max_frame_size = a.max_frame_size;
+    g.max_message_size = a.max_message_size;
+    g.is_server = a.is_server;
+    g.init_pending = 0;
+    g.init_opcode = 0;
     if (g.end > a.wire_len) g.end = a.wire_len;
     return g;
 }
@@ -344,16 +318,37 @@ __device__ inline uint32_t rotr32(uint32_t x, uint32_t s) {
 // the at most 14 header bytes (2 + 8 length + 4 key) of the frame at o in one 16-byte load;
 // bytes past the frame's slot are loaded but never used (only the last 16 bytes of the wire
 // go bytewise)
-__device__ inline u32x4 load_header(const BatchArgs& a, uint64_t o) {
-    if (a.wire_len >= 16 && o <= a.wire_len - 16) {  // (cannot wrap for o near 2^64)
-        u32x4 v;
-        __builtin_memcpy(&v, a.wire + o, 16);
-        return v;
+// The 16 bytes at wire[o, o + 16) (zeros past `len`).  Away from the end of the buffer they
+// come from the two ALIGNED 16-byte vectors around them and a byte funnel shift: an unaligned
+// 16-byte copy compiles to sixteen byte loads on gfx950 (k_plan spent most of its time there).
+// The last 32 bytes of the buffer go bytewise so nothing past `len` is read.
+__device__ inline u32x4 load16_at(const uint8_t* base, uint64_t len, uint64_t o) {
+    const uint64_t lo = o & ~(uint64_t)15;
+    if (len >= 32 && lo <= len - 32) {  // (cannot wrap for o near 2^64)
+        const u32x4 v0 = *reinterpret_cast<const u32x4*>(base + lo);
+        const u32x4 v1 = *reinterpret_cast<const u32x4*>(base + lo + 16);
+        uint64_t x0 = v0.x | ((uint64_t)v0.y << 32), x1 = v0.z | ((uint64_t)v0.w << 32);
+        uint64_t x2 = v1.x | ((uint64_t)v1.y << 32);
+        const uint64_t x3 = v1.z | ((uint64_t)v1.w << 32);
+        const uint32_t d = (uint32_t)(o & 15);
+        if (d & 8) {
+            x0 = x1;
+            x1 = x2;
+            x2 = x3;
+        }
+        const uint32_t s = (d & 7) * 8;
+        const uint64_t r0 = s ? (x0 >> s) | (x1 << (64 - s)) : x0;
+        const uint64_t r1 = s ? (x1 >> s) | (x2 << (64 - s)) : x1;
+        return u32x4{(uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)r1, (uint32_t)(r1 >> 32)};
     }
-    const uint64_t avail = a.wire_len > o ? a.wire_len - o : 0;
+    const uint64_t avail = len > o ? len - o : 0;
     uint32_t t[4] = {0, 0, 0, 0};
-    for (uint32_t k = 0; k < 16 && k < avail; ++k) t[k >> 2] |= (uint32_t)a.wire[o + k] << (8 * (k & 3));
+    for (uint32_t k = 0; k < 16 && k < avail; ++k) t[k >> 2] |= (uint32_t)base[o + k] << (8 * (k & 3));
     return u32x4{t[0], t[1], t[2], t[3]};
+}
+
+__device__ inline u32x4 load_header(const BatchArgs& a, uint64_t o) {
+    return load16_at(a.wire, a.wire_len, o);
 }
 
 __device__ inline ScanElem parse_hdr(const BatchArgs& a, uint32_t i, const SegInfo& g, uint64_t o,
@@ -488,7 +483,6 @@ __device__ inline void resolve_one(const BatchArgs& a, uvhttp_ws_message_desc_t*
     const bool pending = ex.last_data >= 0 ? (ex.bits & kLastOpen) != 0 : g.init_pending > 0;
     // bytes of the open message so far (the connection's carried part when no start yet)
     const uint64_t acc = (ex.bits & kSegFlag) ? ex.seg_pay : g.init_pending + ex.seg_pay;
-    uint64_t open_after = pending ? acc : 0;
 
     int st = d.status;
     if (st == UVHTTP_WS_FRAME_OK && is_data_op(d.opcode)) {
@@ -504,7 +498,6 @@ __device__ inline void resolve_one(const BatchArgs& a, uvhttp_ws_message_desc_t*
                 st = UVHTTP_WS_FRAME_ERR_MESSAGE;
         }
         if (st == UVHTTP_WS_FRAME_OK) {
-            open_after = fin ? 0 : (pending ? acc + d.payload_len : d.payload_len);
             d.message = ex.n_fin;
             if (a.arena) d.payload_off = ex.data_pay;
             if (fin) {
@@ -531,11 +524,7 @@ __device__ inline void resolve_one(const BatchArgs& a, uvhttp_ws_message_desc_t*
         }
         d.status = (int8_t)st;
     }
-    if (a.open_after) a.open_after[i] = open_after;
-    if (st != UVHTTP_WS_FRAME_OK) {
-        if (a.seg_bad) atomicMin(&a.seg_bad[g.seg], i);
-        else tag_claim(ws.first_bad, a.epoch, i);
-    }
+    if (st != UVHTTP_WS_FRAME_OK) tag_claim(ws.first_bad, a.epoch, i);
 }
 
 // ------------------------------------------------------------------------------------
@@ -747,27 +736,9 @@ __global__ __launch_bounds__(kBlock) void k_plan(BatchArgs a, uvhttp_ws_frame_de
 #pragma unroll
             for (int k = 0; k < FPT; ++k) o[k] = (uint64_t)(i0 + k < n ? i0 + k : ilast) * a.frame_stride;
         }
-        if (a.wire_len >= 16) {
+        // two aligned 16-byte loads per frame, all issued before any is used
 #pragma unroll
-            for (int k = 0; k < FPT; ++k) {
-                const uint64_t oc = o[k] <= a.wire_len - 16 ? o[k] : a.wire_len - 16;
-                __builtin_memcpy(&hv[k], a.wire + oc, 16);
-            }
-            // a header within 16 bytes of the wire's end: its bytes sit d = o - oc bytes into
-            // the clamped window; shift them down, zeros past the end (as load_header)
-#pragma unroll
-            for (int k = 0; k < FPT; ++k) {
-                const uint64_t oc = o[k] <= a.wire_len - 16 ? o[k] : a.wire_len - 16;
-                const uint64_t d = o[k] - oc;
-                unsigned __int128 v = ((unsigned __int128)(((uint64_t)hv[k].w << 32) | hv[k].z) << 64) |
-                                      (((uint64_t)hv[k].y << 32) | hv[k].x);
-                v = d >= 16 ? 0 : v >> (8 * d);
-                hv[k] = u32x4{(uint32_t)v, (uint32_t)(v >> 32), (uint32_t)(v >> 64), (uint32_t)(v >> 96)};
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < FPT; ++k) hv[k] = load_header(a, o[k]);
-        }
+        for (int k = 0; k < FPT; ++k) hv[k] = load_header(a, o[k]);
 #pragma unroll
         for (int k = 0; k < FPT; ++k) {
             const uint32_t i = i0 + k;
@@ -1378,17 +1349,46 @@ __global__ __launch_bounds__(BLOCK) void k_scatter_compact(
     }
 }
 
+__device__ inline uint64_t block_exclusive_sum_u64(uint64_t v, uint64_t* total) {
+    __shared__ uint64_t wsum[kBlock / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint64_t inc = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t o = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += o;
+    }
+    if (lane == 63) wsum[wave] = inc;
+    __syncthreads();
+    uint64_t pre = 0, all = 0;
+    for (int k = 0; k < kBlock / 64; ++k) {
+        if (k < wave) pre += wsum[k];
+        all += wsum[k];
+    }
+    __syncthreads();
+    *total = all;
+    return pre + inc - v;
+}
+
 // ------------------------------------------------------------------------------------
-// stream decode: frame discovery.  One lane (or one wave) per connection walks its buffered
-// bytes header by header exactly as the reference's process_data calls do
-// (src/uvhttp_websocket.c:832-932), one call per read: at the start of every call the
-// recv-buffer growth check runs on the bytes the call holds (:832-857); within a call frames
-// are taken while complete; the walk stops where the calls stop: at a frame process_data
-// rejects before unmasking (counted: it is the failing frame; it fails the call in which its
-// header bytes arrived), at a call whose growth check fails, or after the last call (an
-// incomplete frame is not counted: it stays in the buffer).  Pass 1 counts frames; after a
-// scan of the counts the frame offsets are written.  The walk also records, per connection,
-// the call it stopped in and why, and the recv-buffer size after every call.
+// Stream decode (uvhttp_ws_gpu_decode_streams / _decode_reads): many connections, each with
+// its own state, limits and one process_data call per read.  Frames of one connection depend
+// on each other only through the sequential header chain and the fragment state machine, and
+// connections are the parallelism: one wave (few, long connections) or one lane (many short
+// ones) runs a connection's whole process_data sequence (src/uvhttp_websocket.c:825-1097):
+//   per call: the recv-buffer growth check (:832-857) on what the call holds;
+//   per frame: header parse + the checks before unmasking (:876-932) — a rejected frame fails
+//     the call in which its header bytes arrive — and, once the call holds the whole frame,
+//     the fragment state machine and max_message_size (:950-1015, :781-822);
+//   the calls after a failing call never run (the caller closes).
+// The walk records each counted frame's start (the failing frame is the last one counted)
+// and writes the connection's whole result except its first descriptor index.  Then:
+//   k_swalk_scan    first frame of every connection, total, capacity
+//   k_stream_desc   a wave per connection re-reads its headers (two aligned 16-byte loads
+//                   each) and writes the descriptors, message ids and frame ends
+//   k_stream_claims a lane per frame claims the 16 KiB map tiles the frame's end passes
+//   payload kernel  (k_unmask_inplace) unmasks every delivered frame in place
+// No look-back, no bounded waits: nothing here can give up.
 // ------------------------------------------------------------------------------------
 struct WalkArgs {
     const uint8_t* wire;
@@ -1398,15 +1398,12 @@ struct WalkArgs {
     uint32_t max_frames;
     const uint64_t* read_end;  // [n_reads_total] read boundaries (relative), or null
     uint32_t n_reads_total;
+    uint32_t single;           // 1: frame starts go to per-connection slices of walk_tmp
+    uint32_t* agg;             // lane walk: frame counts per 256-connection block -> prefixes
     uvhttp_ws_stream_result_t* results;
+    uvhttp_ws_frame_desc_t* desc;
     StreamScratch sc;
 };
-
-// how a connection's walk ended (walk_stop = kind << 32 | call)
-constexpr uint32_t kStopEnd = 0;     // every call ran; what is left waits in recv_buffer
-constexpr uint32_t kStopBad = 1;     // the last counted frame failed its header checks
-constexpr uint32_t kStopGrow = 2;    // the call's recv-buffer growth check failed
-constexpr uint32_t kStopLayout = 3;  // malformed descriptor / read table: nothing decoded
 
 // process_data's buffer growth: returns false on failure (*out = size then), else the size
 // after the call
@@ -1429,154 +1426,203 @@ __device__ inline bool grow_recv(uint64_t have, uint64_t size, int32_t max_frame
     return true;
 }
 
-// the connection's bytes, or 0 with *ok = false when the descriptor is out of range (the
-// bounds test cannot wrap: begin near 2^64 fails it)
-__device__ inline uint64_t stream_bytes(const WalkArgs& w, const uvhttp_ws_stream_t& st, bool* ok) {
-    *ok = st.len <= w.wire_len && st.begin <= w.wire_len - st.len;
-    return *ok ? st.len : 0;
-}
-
-// the read table of a connection: in range, non-decreasing, ending at len.  Lanes
-// [lane, lane + step, ...) check their entries; the caller combines the lanes' answers.
-__device__ inline bool reads_ok_part(const WalkArgs& w, const uvhttp_ws_stream_t& st, uint64_t L,
-                                     uint32_t lane, uint32_t step) {
+// Is connection s's descriptor usable?  In range of the wire (a test that cannot wrap for a
+// begin near 2^64), after the previous connection (streams are ordered and disjoint), under
+// 4 GiB (frame starts are kept as 32-bit offsets), and its read table — when it has one — in
+// range, non-decreasing and ending at len.  Lanes [lane, lane + step, ...) check the read
+// entries; the caller combines the lanes' answers.
+__device__ inline bool stream_ok_part(const WalkArgs& w, uint32_t s, const uvhttp_ws_stream_t& st,
+                                      uint32_t lane, uint32_t step) {
+    if (!(st.len <= w.wire_len && st.begin <= w.wire_len - st.len) || (st.len >> 32)) return false;
+    if (s > 0 && lane == 0) {
+        const uvhttp_ws_stream_t pv = w.streams[s - 1];
+        if (st.begin < pv.begin || st.begin - pv.begin < pv.len) return false;
+    }
     if (st.n_reads == 0) return true;
     if (!w.read_end || st.first_read > w.n_reads_total ||
         st.n_reads > w.n_reads_total - st.first_read)
         return false;
     const uint64_t* re = w.read_end + st.first_read;
-    bool ok = lane != 0 || re[st.n_reads - 1] == L;
+    bool ok = lane != 0 || re[st.n_reads - 1] == st.len;
     for (uint32_t k = lane; k < st.n_reads && ok; k += step) {
         const uint64_t prev = k ? re[k - 1] : 0;
-        ok = re[k] >= prev && re[k] <= L;
+        ok = re[k] >= prev && re[k] <= st.len;
     }
     return ok;
 }
 
-// The walk over the calls.  fetch(pos, hb) yields the ten header bytes at stream offset pos;
-// emit(pos, idx) records counted frame idx; `writer` lanes store the stop record and the
-// per-call buffer sizes.  Returns the number of frames counted.
-template <typename Fetch, typename Emit>
-__device__ inline uint32_t walk_calls(const WalkArgs& w, uint32_t s, const uvhttp_ws_stream_t& st,
-                                      uint64_t L, bool writer, Fetch&& fetch, Emit&& emit) {
+// per-connection decoder state carried by the walk (wave-uniform in the wave walk)
+struct ConnState {
+    uint64_t pos;        // stream offset of the next undecided frame
+    uint64_t end;        // stream bytes the current call holds
+    uint64_t size;       // recv_buffer_size after the current call's growth
+    uint64_t acc;        // bytes of the open fragmented message (pending)
+    uint32_t k;          // current call
+    uint32_t count;      // frames counted
+    uint32_t pending;    // a fragmented message is open (fragmented_message != NULL)
+    int32_t fail;        // UVHTTP_WS_FRAME_* of the failure (0: none)
+    uint32_t grow_fail;  // the current call failed its growth check
+};
+
+// One connection's process_data calls, frame by frame.  hdr(pos, hb) yields the ten header
+// bytes at stream offset pos; emit(pos, idx) records counted frame idx.  Returns the state at
+// the stop; the caller turns it into the result.
+// fast(c) may first take any run of frames it can decide alone (complete, valid, accepted by
+// the state machine) and advance c; everything else goes through the general code below.
+struct NoFast {
+    __device__ void operator()(struct ConnState&) const {}
+};
+
+template <typename Hdr, typename Emit, typename Fast = NoFast>
+__device__ inline ConnState walk_calls(const WalkArgs& w, const uvhttp_ws_stream_t& st, Hdr&& hdr,
+                                       Emit&& emit, Fast&& fast = NoFast()) {
     const uint64_t mf = (uint64_t)(int64_t)st.max_frame_size;
+    const uint64_t lim = (uint64_t)(int64_t)st.max_message_size;
     const uint32_t K = st.n_reads ? st.n_reads : 1;
     const uint64_t* re = st.n_reads ? w.read_end + st.first_read : nullptr;
-    uint32_t count = 0, k = 0, kind = kStopEnd;
-    uint64_t pos = 0, size = st.recv_buffer_size;
-    uint64_t end = re ? re[0] : L;
-    bool grown = grow_recv(end, size, st.max_frame_size, &size);  // call 0
-    if (writer && re) w.sc.read_size[st.first_read] = size;
-    if (!grown) kind = kStopGrow;
-    while (grown) {
+    ConnState c;
+    c.pos = 0;
+    c.k = 0;
+    c.count = 0;
+    c.fail = 0;
+    c.pending = st.pending_bytes ? 1u : 0u;
+    c.acc = st.pending_bytes;
+    c.end = re ? re[0] : st.len;
+    c.grow_fail = grow_recv(c.end, st.recv_buffer_size, st.max_frame_size, &c.size) ? 0u : 1u;
+    if (re) w.sc.read_size[st.first_read] = c.size;
+    while (!c.grow_fail) {
+        fast(c);
         uint64_t need_end;  // the stream offset the next decision needs
-        if (end - pos >= 2) {
+        if (c.end - c.pos >= 2) {
             uint32_t hb[10];
-            fetch(pos, hb);
+            hdr(c.pos, hb);
             const uint32_t b0 = hb[0], b1 = hb[1];
             const uint32_t code = b1 & 0x7F;
             const uint32_t need = code == 126 ? 4 : code == 127 ? 10 : 2;
-            if (end - pos >= need) {
+            if (c.end - c.pos >= need) {
                 uint64_t plen = code;
                 if (need == 4) {
                     plen = (hb[2] << 8) | hb[3];
                 } else if (need == 10) {
-                    plen = 0;
-#pragma unroll
-                    for (int q = 2; q < 10; ++q) plen = (plen << 8) | hb[q];
+                    plen = ((uint64_t)((hb[2] << 24) | (hb[3] << 16) | (hb[4] << 8) | hb[5]) << 32) |
+                           (uint32_t)((hb[6] << 24) | (hb[7] << 16) | (hb[8] << 8) | hb[9]);
                 }
-                const bool bad = (need == 10 && (plen >> 63)) || (b0 & 0x70) ||
-                                 ((b0 & 0x0F) >= 8 && (plen > 125 || !(b0 & 0x80))) ||
-                                 (st.is_server && !(b1 & 0x80)) || plen > mf;
-                if (bad) {  // process_data returns at this frame, in this call
-                    emit(pos, count);
-                    ++count;
-                    kind = kStopBad;
+                const uint32_t op = b0 & 0x0F;
+                const bool fin = b0 & 0x80;
+                int32_t st_h = UVHTTP_WS_FRAME_OK;  // :876-921, in the reference's order
+                if (need == 10 && (plen >> 63)) st_h = UVHTTP_WS_FRAME_ERR_PARSE;
+                else if (b0 & 0x70) st_h = UVHTTP_WS_FRAME_ERR_RSV;
+                else if (op >= 8 && (plen > 125 || !fin)) st_h = UVHTTP_WS_FRAME_ERR_CONTROL;
+                else if (st.is_server && !(b1 & 0x80)) st_h = UVHTTP_WS_FRAME_ERR_UNMASKED;
+                else if (plen > mf) st_h = UVHTTP_WS_FRAME_ERR_TOO_BIG;
+                if (st_h != UVHTTP_WS_FRAME_OK) {  // fails this call, before any unmasking
+                    emit(c.pos, c.count);
+                    ++c.count;
+                    c.fail = st_h;
                     break;
                 }
                 const uint64_t wl = need + ((b1 & 0x80) ? 4u : 0u) + plen;
-                if (end - pos >= wl) {  // complete: delivered by this call
-                    emit(pos, count);
-                    ++count;
-                    pos += wl;
+                if (c.end - c.pos >= wl) {  // complete: this call unmasks and dispatches it
+                    if (op <= 2) {  // the fragment state machine (:950-1015)
+                        const bool cont = op == 0;
+                        int32_t sm = UVHTTP_WS_FRAME_OK;
+                        if (!c.pending) {
+                            if (cont) sm = UVHTTP_WS_FRAME_ERR_FRAGMENT;
+                            else if (!fin && lim != 0 && plen > lim) sm = UVHTTP_WS_FRAME_ERR_MESSAGE;
+                            else if (!fin && plen) {  // an empty first fragment opens nothing
+                                c.pending = 1;
+                                c.acc = plen;
+                            }
+                        } else if (!cont) {
+                            sm = UVHTTP_WS_FRAME_ERR_FRAGMENT;
+                        } else if (lim != 0 && (c.acc > lim || plen > lim - c.acc)) {
+                            sm = UVHTTP_WS_FRAME_ERR_MESSAGE;
+                        } else if (fin) {
+                            c.pending = 0;
+                            c.acc = 0;
+                        } else {
+                            c.acc += plen;
+                        }
+                        if (sm != UVHTTP_WS_FRAME_OK) {
+                            emit(c.pos, c.count);
+                            ++c.count;
+                            c.fail = sm;
+                            break;
+                        }
+                    }
+                    emit(c.pos, c.count);
+                    ++c.count;
+                    c.pos += wl;
                     continue;
                 }
-                need_end = pos + wl;
+                need_end = c.pos + wl;
             } else {
-                need_end = pos + need;
+                need_end = c.pos + need;
             }
         } else {
-            need_end = pos + 2;
+            need_end = c.pos + 2;
         }
         // the bytes of the next decision come with a later call: run the calls up to it
         // (each one's growth check sees the partial frame plus everything it appended)
-        while (end < need_end && k + 1 < K) {
-            ++k;
-            end = re[k];
-            grown = grow_recv(end - pos, size, st.max_frame_size, &size);
-            if (writer) w.sc.read_size[st.first_read + k] = size;
-            if (!grown) break;
+        while (c.end < need_end && c.k + 1 < K) {
+            ++c.k;
+            c.end = re[c.k];
+            uint64_t grown;
+            c.grow_fail = grow_recv(c.end - c.pos, c.size, st.max_frame_size, &grown) ? 0u : 1u;
+            c.size = grown;
+            w.sc.read_size[st.first_read + c.k] = grown;
+            if (c.grow_fail) break;
         }
-        if (!grown) {
-            kind = kStopGrow;
-            break;
-        }
-        if (end < need_end) break;  // every call ran: the rest waits in recv_buffer
+        if (c.grow_fail || c.end < need_end) break;  // else every call ran: the rest waits
     }
-    if (writer) {
-        w.sc.walk_stop[s] = ((uint64_t)kind << 32) | k;
-        w.sc.stop_size[s] = size;
-    }
-    return count;
+    return c;
 }
 
-// lane walk: one lane per connection, header bytes straight from global memory
-template <bool WRITE>
-__device__ inline uint32_t walk_stream(const WalkArgs& w, uint32_t s, uint32_t first) {
-    const uvhttp_ws_stream_t st = w.streams[s];
-    bool in_range;
-    const uint64_t L = stream_bytes(w, st, &in_range);
-    if (!in_range || !reads_ok_part(w, st, L, 0, 1)) {
-        if (!WRITE) w.sc.walk_stop[s] = (uint64_t)kStopLayout << 32;
-        return 0;
-    }
-    const uint8_t* p = w.wire + st.begin;
-    return walk_calls(
-        w, s, st, L, !WRITE,
-        [&](uint64_t pos, uint32_t hb[10]) {
-#pragma unroll
-            for (int q = 0; q < 10; ++q) hb[q] = pos + q < L ? p[pos + q] : 0u;
-        },
-        [&](uint64_t pos, uint32_t idx) {
-            if (WRITE && first + idx < w.max_frames) {
-                w.sc.frame_off[first + idx] = st.begin + pos;
-                w.sc.frame_seg[first + idx] = s;
-            }
-        });
+// the connection's result from its walk (first_frame is placed by k_swalk_scan)
+__device__ inline uvhttp_ws_stream_result_t walk_result(const WalkArgs& w, const uvhttp_ws_stream_t& st,
+                                                        const ConnState& c) {
+    const uint64_t* re = st.n_reads ? w.read_end + st.first_read : nullptr;
+    auto end_of = [&](uint32_t call) { return re ? re[call] : st.len; };
+    uvhttp_ws_stream_result_t r;
+    r.first_frame = 0;
+    r.n_frames = c.count;
+    r.n_delivered = c.count - (c.fail ? 1u : 0u);
+    r.status = (c.fail || c.grow_fail) ? -1 : 0;
+    r.first_status = c.fail ? c.fail : c.grow_fail ? UVHTTP_WS_FRAME_ERR_BUFFER : 0;
+    r.calls = c.k + 1;
+    r.consumed_bytes = c.pos;  // the end of the last delivered frame
+    r.recv_buffer_size = c.size;
+    // the fragment state after the last delivered frame (a failing frame changes nothing the
+    // device reports; deliver_stream replays its partial effect on the host)
+    r.pending_bytes = c.pending ? c.acc : 0;
+    // a failing growth check returns before appending: the buffer holds what the calls
+    // before it left (the first call: untouched, marked by 0)
+    r.buffered_end = c.grow_fail ? (c.k ? end_of(c.k - 1) : 0) : end_of(c.k);
+    r.reserved = 0;
+    return r;
 }
 
-__device__ inline uint64_t block_exclusive_sum_u64(uint64_t v, uint64_t* total) {
-    __shared__ uint64_t wsum[kBlock / 64];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint64_t inc = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint64_t o = __shfl_up(inc, d, 64);
-        if (lane >= d) inc += o;
-    }
-    if (lane == 63) wsum[wave] = inc;
-    __syncthreads();
-    uint64_t pre = 0, all = 0;
-    for (int k = 0; k < kBlock / 64; ++k) {
-        if (k < wave) pre += wsum[k];
-        all += wsum[k];
-    }
-    __syncthreads();
-    *total = all;
-    return pre + inc - v;
+__device__ inline uvhttp_ws_stream_result_t layout_result(const uvhttp_ws_stream_t& st) {
+    uvhttp_ws_stream_result_t r;
+    memset(&r, 0, sizeof(r));
+    r.status = -1;
+    r.first_status = UVHTTP_WS_FRAME_ERR_LAYOUT;
+    r.recv_buffer_size = st.recv_buffer_size;
+    r.pending_bytes = st.pending_bytes;
+    return r;
 }
 
-__device__ inline uint32_t block_exclusive_sum_u32(uint32_t v, uint32_t* total) {
+// slice of connection s in walk_tmp (single pass): its frames are >= 2 bytes apart and
+// connections are disjoint and ordered, so begin / 2 + s leaves room for every start
+__device__ inline uint64_t slice_base(const uvhttp_ws_stream_t& st, uint32_t s) {
+    return st.begin / 2 + s;
+}
+
+// ---- lane walk: one lane per connection, headers straight from global memory -------------
+// MODE 0: count; 1: write starts to frame_off from the connection's first frame (two-pass);
+// 2: count and write starts into the connection's slice (single pass)
+// block-wide sum (256 threads) and exclusive prefix of one u32 per thread
+__device__ inline uint32_t block_scan_u32(uint32_t v, uint32_t* total) {
     __shared__ uint32_t wsum[kBlock / 64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t inc = v;
@@ -1597,40 +1643,86 @@ __device__ inline uint32_t block_exclusive_sum_u32(uint32_t v, uint32_t* total) 
     return pre + inc - v;
 }
 
-// Wave-per-connection walk (connections with many small frames).  The connection's bytes are
-// read in aligned 4 KiB blocks: LDS holds the block of the current header and the next one (a
-// two-slot ring, so a header straddling a block end is readable), and the block after those is
-// already in flight in registers (one 16-byte load per lane x 4), issued when the walk entered
-// the current block.  (A second block in flight measured the same: the compiler's waitcnt at
-// the loop head drains both.)  Every lane parses the same header from LDS (broadcast reads): the ten
-// bytes a header can need are independent ds_read_u8, one LDS round trip per hop.  A frame
-// longer than a block (the walk jumps) reloads the ring at the new position.  Same decisions
-// as walk_stream, byte for byte.
+// lane mode: connection s's first frame = its block's prefix (k_swalk_scan) + the counts of
+// the block's earlier connections (every thread of the block calls this)
+__device__ inline uint32_t lane_first(const WalkArgs& w, uint32_t s) {
+    const uint32_t c = s < w.n_streams ? w.results[s].n_frames : 0;
+    uint32_t total;
+    const uint32_t local = block_scan_u32(c, &total);
+    return w.agg[blockIdx.x] + local;
+}
+
+template <int MODE>
+__device__ inline uint32_t walk_lane(const WalkArgs& w, uint32_t s, uint32_t lf) {
+    const uvhttp_ws_stream_t st = w.streams[s];
+    if (!stream_ok_part(w, s, st, 0, 1)) {
+        if (MODE != 1) w.results[s] = layout_result(st);
+        return 0;
+    }
+    const uint64_t first = MODE == 1 ? lf : slice_base(st, s);
+    const ConnState c = walk_calls(
+        w, st,
+        [&](uint64_t pos, uint32_t hb[10]) {  // (bytes past the stream are never used)
+            const u32x4 v = load16_at(w.wire, w.wire_len, st.begin + pos);
+            const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int q = 0; q < 10; ++q) hb[q] = (x[q >> 2] >> (8 * (q & 3))) & 0xFF;
+        },
+        [&](uint64_t pos, uint32_t idx) {
+            if (MODE == 1 && first + idx < w.max_frames) w.sc.frame_off[first + idx] = st.begin + pos;
+            if (MODE == 2) w.sc.walk_tmp[first + idx] = (uint32_t)pos;
+        });
+    if (MODE != 1) w.results[s] = walk_result(w, st, c);
+    return c.count;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_swalk_lane(WalkArgs w) {
+    const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t lf = MODE == 1 ? lane_first(w, s) : 0;  // (before any thread leaves)
+    uint32_t count = 0;
+    if (s < w.n_streams) count = walk_lane<MODE>(w, s, lf);
+    if (MODE == 1) return;
+    uint32_t total;
+    (void)block_scan_u32(count, &total);
+    if (threadIdx.x == 0) w.agg[blockIdx.x] = total;
+}
+
+// ---- wave walk: one wave per connection (connections with many frames) -------------------
+// The connection's bytes pass through LDS in aligned 4 KiB blocks: a two-slot ring (the block
+// of the current header and the next) plus a 16-byte mirror of slot 0 after slot 1, so the
+// ten bytes of any header are one run of LDS bytes; the block after those is in flight in
+// registers, issued when the walk entered the current block.  Block loads are buffer loads
+// bounded by the wire's end (bytes past it read as 0): no per-lane branches.  Every lane
+// reads the same header bytes (broadcast) and readfirstlane makes them scalar, so the header
+// decode, the checks and the state machine run on the scalar unit with uniform branches.
+// Frame starts are collected one per lane and stored 64 at a time.
 constexpr uint32_t kWalkBlk = 4096;
 constexpr int kWalkVec = (int)(kWalkBlk / (64u * 16u));  // 16-byte loads per lane per block
+constexpr uint32_t kRingBytes = 2 * kWalkBlk + 16;
 
 __device__ inline void walk_load_block(const WalkArgs& w, uint64_t blk, u32x4 v[kWalkVec]) {
     const int lane = threadIdx.x & 63;
+    const uint64_t base = blk * kWalkBlk;
+    const uint64_t room = w.wire_len > base ? w.wire_len - base : 0;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(w.wire + (room ? base : 0)), 0, (int)(room < kWalkBlk ? room : kWalkBlk),
+        0x00020000);
 #pragma unroll
-    for (int k = 0; k < kWalkVec; ++k) {
-        const uint64_t src = blk * kWalkBlk + (uint64_t)(k * 64 + lane) * 16u;
-        if (w.wire_len >= 16 && src <= w.wire_len - 16) {
-            v[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(w.wire + src));
-        } else {
-            uint32_t t[4] = {0, 0, 0, 0};
-            for (uint32_t q = 0; q < 16 && src + q < w.wire_len; ++q)
-                t[q >> 2] |= (uint32_t)w.wire[src + q] << (8 * (q & 3));
-            v[k] = u32x4{t[0], t[1], t[2], t[3]};
-        }
-    }
+    for (int k = 0; k < kWalkVec; ++k)
+        v[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                             rs, (uint32_t)(k * 64 + lane) * 16u, 0, 0));
 }
 
 __device__ inline void walk_store_block(uint8_t* ring, uint64_t blk, const u32x4 v[kWalkVec]) {
     const int lane = threadIdx.x & 63;
-    uint8_t* slot = ring + (blk & 1) * kWalkBlk;
+    const uint32_t slot = (uint32_t)(blk & 1);
+    uint8_t* dst = ring + slot * kWalkBlk;
 #pragma unroll
     for (int k = 0; k < kWalkVec; ++k)
-        *reinterpret_cast<u32x4*>(slot + (uint32_t)(k * 64 + lane) * 16u) = v[k];
+        *reinterpret_cast<u32x4*>(dst + (uint32_t)(k * 64 + lane) * 16u) = v[k];
+    if (slot == 0 && lane == 0)  // the mirror after slot 1: slot 0's first 16 bytes
+        *reinterpret_cast<u32x4*>(ring + 2 * kWalkBlk) = v[0];
 }
 
 __device__ inline void wave_sync_lds() {
@@ -1639,26 +1731,30 @@ __device__ inline void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// MODE 0: count; 1: write frame_off / frame_seg from `first`; 2: write starts relative to
-// the connection into walk_tmp from `first` (a slice index)
 template <int MODE>
-__device__ inline uint32_t walk_stream_wave(const WalkArgs& w, uint32_t s, uint64_t first,
-                                            uint8_t* ring) {
-    const int lane = threadIdx.x & 63;
+__device__ inline void walk_wave(const WalkArgs& w, uint32_t s, uint8_t* ring) {
+    const uint32_t lane = threadIdx.x & 63;
     const uvhttp_ws_stream_t st = w.streams[s];
-    bool in_range;
-    const uint64_t L = stream_bytes(w, st, &in_range);
-    const bool reads_ok = in_range && __all(reads_ok_part(w, st, L, lane, 64));
-    const bool writer = MODE != 1 && lane == 0;  // the count pass records stop / sizes
-    if (!reads_ok) {
-        if (writer) w.sc.walk_stop[s] = (uint64_t)kStopLayout << 32;
-        return 0;
+    const bool ok = __all(stream_ok_part(w, s, st, lane, 64));
+    if (!ok) {
+        if (MODE != 1 && lane == 0) w.results[s] = layout_result(st);
+        return;
     }
+    const uint64_t first = MODE == 1 ? w.results[s].first_frame : slice_base(st, s);
     uint64_t cur = ~0ull;  // block of the current header; LDS holds cur and cur + 1
     u32x4 pf[kWalkVec];    // block cur + 2, in flight
-    auto byte_at = [&](uint64_t x) { return (uint32_t)ring[((x / kWalkBlk) & 1) * kWalkBlk + x % kWalkBlk]; };
-    return walk_calls(
-        w, s, st, L, writer,
+    uint32_t batch = 0;    // lane j holds start (first + 64 m + j) of the current batch m
+    auto emit = [&](uint64_t pos, uint32_t idx) {
+        if (MODE == 0) return;
+        if (lane == (idx & 63)) batch = (uint32_t)pos;
+        if ((idx & 63) == 63) {  // a full batch: one coalesced store
+            const uint64_t f = first + (idx & ~63u) + lane;
+            if (MODE == 2) w.sc.walk_tmp[f] = batch;
+            else if (f < w.max_frames) w.sc.frame_off[f] = st.begin + batch;
+        }
+    };
+    const ConnState c = walk_calls(
+        w, st,
         [&](uint64_t pos, uint32_t hb[10]) {
             const uint64_t at = st.begin + pos;
             const uint64_t blk = at / kWalkBlk;
@@ -1676,248 +1772,259 @@ __device__ inline uint32_t walk_stream_wave(const WalkArgs& w, uint32_t s, uint6
                 cur = blk;
                 wave_sync_lds();
             }
-            // the ten bytes a header can use, all independent LDS reads
+            const uint32_t r = (uint32_t)((blk & 1) * kWalkBlk + at % kWalkBlk);
 #pragma unroll
-            for (int q = 0; q < 10; ++q) hb[q] = byte_at(at + q);
+            for (int q = 0; q < 10; ++q) hb[q] = __builtin_amdgcn_readfirstlane(ring[r + q]);
         },
-        [&](uint64_t pos, uint32_t idx) {
-            if (MODE == 1 && lane == 0 && first + idx < w.max_frames) {
-                w.sc.frame_off[first + idx] = st.begin + pos;
-                w.sc.frame_seg[first + idx] = s;
+        [&](uint64_t pos, uint32_t idx) { emit(pos, idx); },
+        [&](ConnState& c) {
+            // The hot loop: frames decided from the ring alone — header in the current ring
+            // block, at least ten bytes of the current call left, complete in this call,
+            // valid, accepted by the fragment state machine.  Vector arithmetic on every lane
+            // (identical values) keeps the shared scalar unit free; only the exit tests are
+            // made uniform (readfirstlane).  Anything else leaves for the general code.
+            if (cur == ~0ull || c.grow_fail) return;
+            const uint64_t cur_rel = cur - st.begin / kWalkBlk;  // ring block, stream-relative
+            const uint32_t off0 = (uint32_t)(st.begin % kWalkBlk), par0 = (uint32_t)((st.begin / kWalkBlk) & 1);
+            const uint32_t end32 = (uint32_t)c.end;
+            const uint64_t mf = (uint64_t)(int64_t)st.max_frame_size;
+            const uint64_t lim = (uint64_t)(int64_t)st.max_message_size;
+            uint32_t pos = (uint32_t)c.pos, pend = c.pending;
+            uint64_t acc = c.acc;
+            uint32_t cnt = c.count;
+            for (;;) {
+                const uint32_t off = off0 + pos;
+                if (__builtin_amdgcn_readfirstlane((uint32_t)((off / kWalkBlk) != cur_rel) | (uint32_t)(end32 - pos < 10)))
+                    break;
+                const uint32_t r = (((par0 + off / kWalkBlk) & 1) * kWalkBlk) + off % kWalkBlk;
+                uint32_t hb[10];
+#pragma unroll
+                for (int q = 0; q < 10; ++q) hb[q] = ring[r + q];
+                const uint32_t b0 = hb[0], b1 = hb[1], code = b1 & 0x7F;
+                const uint32_t need = code < 126 ? 2u : code == 126 ? 4u : 10u;
+                uint64_t plen = code;
+                if (code == 126) plen = (hb[2] << 8) | hb[3];
+                if (code == 127)
+                    plen = ((uint64_t)((hb[2] << 24) | (hb[3] << 16) | (hb[4] << 8) | hb[5]) << 32) |
+                           (uint32_t)((hb[6] << 24) | (hb[7] << 16) | (hb[8] << 8) | hb[9]);
+                const uint32_t op = b0 & 0x0F, fin = b0 >> 7, m = b1 >> 7;
+                const bool bad = (b0 & 0x70) || (op >= 8 && (plen > 125 || !fin)) ||
+                                 (st.is_server && !m) || plen > mf;  // (plen <= mf < 2^31)
+                const uint64_t wl = need + 4u * m + plen;
+                const bool data = op <= 2;
+                const bool smf = data && (pend ? (op != 0 || (lim != 0 && (acc > lim || plen > lim - acc)))
+                                               : (op == 0 || (!fin && lim != 0 && plen > lim)));
+                if (__builtin_amdgcn_readfirstlane((uint32_t)(bad || wl > end32 - pos || smf))) break;
+                emit(pos, cnt);
+                if (data) {
+                    if (pend) {
+                        acc = fin ? 0 : acc + plen;
+                        pend = fin ? 0u : 1u;
+                    } else if (!fin && plen) {
+                        pend = 1;
+                        acc = plen;
+                    }
+                }
+                pos += (uint32_t)wl;
+                ++cnt;
             }
-            if (MODE == 2 && lane == 0) w.sc.walk_tmp[first + idx] = (uint32_t)pos;
+            c.pos = __builtin_amdgcn_readfirstlane(pos);
+            c.pending = __builtin_amdgcn_readfirstlane(pend);
+            c.acc = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(acc >> 32)) << 32) |
+                    __builtin_amdgcn_readfirstlane((uint32_t)acc);
+            c.count = cnt;
         });
-}
-
-// single-pass wave walk, step 1: each connection's slice of walk_tmp, an upper bound on the
-// frames the walk can count: every counted frame but the last (failing) one is >= 2 bytes,
-// and >= 6 on a server connection (unmasked frames fail there, :910-912).  Slices hold
-// 32-bit positions, so a connection of 4 GiB or more forces the two-walk path.
-__global__ __launch_bounds__(kBlock) void k_walk_bound(WalkArgs w) {
-    const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
-    uint64_t b = 0;
-    if (s < w.n_streams) {
-        const uvhttp_ws_stream_t st = w.streams[s];
-        bool in_range;
-        const uint64_t L = stream_bytes(w, st, &in_range);
-        b = L >> 32 ? (1ull << 60) : L / (st.is_server ? 6 : 2) + 1;
+    if (MODE != 0 && (c.count & 63)) {  // the last, partial batch
+        const uint64_t f = first + (c.count & ~63u) + lane;
+        if (lane < (c.count & 63)) {
+            if (MODE == 2) w.sc.walk_tmp[f] = batch;
+            else if (f < w.max_frames) w.sc.frame_off[f] = st.begin + batch;
+        }
     }
-    uint64_t total;
-    const uint64_t local = block_exclusive_sum_u64(b, &total);
-    if (s < w.n_streams) w.sc.walk_base[s] = local;
-    if (threadIdx.x == 0) w.sc.bound_blk[blockIdx.x] = total;
+    if (MODE == 1 || lane != 0) return;
+    w.results[s] = walk_result(w, st, c);
 }
 
-// step 2: slice prefixes over the blocks; single pass only if every slice fits
-__global__ __launch_bounds__(kBlock) void k_walk_bound_scan(WalkArgs w, uint32_t n_blocks) {
-    const uint32_t per = (n_blocks + kBlock - 1) / kBlock;
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_swalk_wave(WalkArgs w) {
+    __shared__ __attribute__((aligned(16))) uint8_t ring[kBlock / 64][kRingBytes];
+    // readfirstlane: the connection (and all walk state derived from it) is wave-uniform, so
+    // it lives in scalar registers and the walk's branches are scalar branches
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t s = blockIdx.x * (kBlock / 64) + wave;
+    if (s >= w.n_streams) return;
+    if (MODE == 1 && !w.results[s].n_frames) return;
+    walk_wave<MODE>(w, s, ring[wave]);
+}
+
+// first frames, total, capacity (one workgroup).  Lane mode scans the walk's per-block
+// counts (agg, in place; k_stream_desc_lane adds the block-local part); wave mode (at most
+// 16384 connections) writes every connection's first frame itself.  Each thread takes a
+// contiguous chunk: sum it, scan the sums across the block, then write the chunk's prefixes.
+__global__ __launch_bounds__(kBlock) void k_swalk_scan(WalkArgs w, uint32_t lane_mode) {
+    const uint32_t m = lane_mode ? (w.n_streams + kBlock - 1) / kBlock : w.n_streams;
+    const uint32_t per = (m + kBlock - 1) / kBlock;
     const uint32_t beg = threadIdx.x * per;
-    const uint32_t fin = beg + per < n_blocks ? beg + per : n_blocks;
+    const uint32_t fin = beg + per < m ? beg + per : m;
+    auto count_of = [&](uint32_t j) { return lane_mode ? w.agg[j] : w.results[j].n_frames; };
     uint64_t run = 0;
-    for (uint32_t b = beg; b < fin; ++b) run += w.sc.bound_blk[b];
+    for (uint32_t j = beg; j < fin; ++j) run += count_of(j);
     uint64_t total;
     uint64_t pre = block_exclusive_sum_u64(run, &total);
-    for (uint32_t b = beg; b < fin; ++b) {
-        const uint64_t v = w.sc.bound_blk[b];
-        w.sc.bound_blk[b] = pre;
+    for (uint32_t j = beg; j < fin; ++j) {
+        const uint32_t v = count_of(j);
+        if (lane_mode) w.agg[j] = (uint32_t)pre;
+        else w.results[j].first_frame = (uint32_t)pre;
         pre += v;
     }
-    if (threadIdx.x == 0) *w.sc.walk_single = total <= w.sc.tmp_cap ? 1u : 0u;
+    if (threadIdx.x == 0) *w.sc.n_total = total <= w.max_frames ? (uint32_t)total : 0u;
 }
 
-// step 3: the one walk — counts, and records the starts in the connection's slice
-__global__ __launch_bounds__(kBlock) void k_walk_once_wave(WalkArgs w) {
-    __shared__ __attribute__((aligned(16))) uint8_t win[kBlock / 64][2 * kWalkBlk];
-    const uint32_t wave = threadIdx.x >> 6;
-    const uint32_t s = blockIdx.x * (kBlock / 64) + wave;
-    if (s >= w.n_streams) return;
-    const uint32_t c = *w.sc.walk_single
-        ? walk_stream_wave<2>(w, s, w.sc.walk_base[s] + w.sc.bound_blk[s / kBlock], win[wave])
-        : walk_stream_wave<0>(w, s, 0, win[wave]);
-    if ((threadIdx.x & 63) == 0) w.results[s].n_frames = c;
-}
-
-// step 5 (after the count scan placed each connection's first frame): copy the slice into
-// frame_off / frame_seg, coalesced
-__global__ __launch_bounds__(kBlock) void k_walk_compact(WalkArgs w) {
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t s = blockIdx.x * (kBlock / 64) + wave;
-    if (s >= w.n_streams || !*w.sc.walk_single) return;
-    const uvhttp_ws_stream_result_t r = w.results[s];
-    const uint64_t base = w.sc.walk_base[s] + w.sc.bound_blk[s / kBlock];
-    const uint64_t begin = w.streams[s].begin;
-    for (uint32_t k = lane; k < r.n_frames; k += 64) {
-        const uint64_t f = (uint64_t)r.first_frame + k;
-        if (f >= w.max_frames) break;
-        w.sc.frame_off[f] = begin + w.sc.walk_tmp[base + k];
-        w.sc.frame_seg[f] = s;
+// frame k of connection s (frame start `pos`, stream-relative): its descriptor and end
+__device__ inline void stream_frame_desc(const WalkArgs& w, const uvhttp_ws_stream_t& st,
+                                         const uvhttp_ws_stream_result_t& r, uint32_t k,
+                                         uint64_t pos, uvhttp_ws_frame_desc_t& d, bool& fin_data,
+                                         uint64_t& fe) {
+    const u32x4 hv = load16_at(w.wire, w.wire_len, st.begin + pos);
+    const uint64_t hlo = hv.x | ((uint64_t)hv.y << 32), hhi = hv.z | ((uint64_t)hv.w << 32);
+    auto hb = [&](int q) -> uint32_t {
+        return (uint32_t)((q < 8 ? hlo >> (8 * q) : hhi >> (8 * (q - 8))) & 0xFF);
+    };
+    const uint32_t b0 = hb(0), b1 = hb(1), code = b1 & 0x7F;
+    const uint32_t hsz = code == 126 ? 4 : code == 127 ? 10 : 2;
+    uint64_t plen = code;
+    if (hsz == 4) {
+        plen = (hb(2) << 8) | hb(3);
+    } else if (hsz == 10) {
+        plen = 0;
+#pragma unroll
+        for (int q = 2; q < 10; ++q) plen = (plen << 8) | hb(q);
     }
+    const bool msb = hsz == 10 && (plen >> 63);
+    const uint32_t m = (b1 >> 7) ? 4u : 0u;
+    const uint64_t slot = st.len - pos;
+    const bool failing = k + 1 == r.n_frames && r.n_delivered < r.n_frames;
+    d.payload_off = st.begin + pos + (msb ? 0 : hsz + m);
+    d.payload_len = plen;
+    d.masking_key = (m && slot >= hsz + 4)
+                        ? (hsz == 2 ? (uint32_t)(hlo >> 16) : hsz == 4 ? (uint32_t)(hlo >> 32)
+                                                                      : (uint32_t)(hhi >> 16))
+                        : 0u;
+    d.message = 0;
+    d.opcode = (uint8_t)(b0 & 0x0F);
+    d.flags = (uint8_t)(((b0 >> 7) & 1) | ((b1 >> 7) << 1) | (((b0 >> 6) & 1) << 2) |
+                        (((b0 >> 5) & 1) << 3) | (((b0 >> 4) & 1) << 4));
+    d.header_size = (uint8_t)hsz;
+    d.status = (int8_t)(failing ? r.first_status : UVHTTP_WS_FRAME_OK);
+    const uint64_t wl = msb ? 0 : hsz + m + plen;
+    d.wire_len = wl > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)wl;
+    fin_data = !failing && d.opcode <= 2 && (b0 & 0x80);
+    if (fin_data) d.flags |= UVHTTP_WS_FLAG_MSG_END;
+    // the frame's end for the tile claims, clamped to the connection for a failing frame's
+    // declared length
+    fe = st.begin + (msb || wl > slot ? st.len : pos + wl);
 }
 
-// wave mode pass 1: frames per connection (one wave each)
-__global__ __launch_bounds__(kBlock) void k_walk_count_wave(WalkArgs w) {
-    __shared__ __attribute__((aligned(16))) uint8_t win[kBlock / 64][2 * kWalkBlk];
-    const uint32_t wave = threadIdx.x >> 6;
-    const uint32_t s = blockIdx.x * (kBlock / 64) + wave;
-    if (s >= w.n_streams) return;
-    const uint32_t c = walk_stream_wave<0>(w, s, 0, win[wave]);
-    if ((threadIdx.x & 63) == 0) w.results[s].n_frames = c;
-}
-
-// wave mode: per-256-connection sums of the counts (the lane-mode count pass's aggregate)
-__global__ __launch_bounds__(kBlock) void k_walk_agg(WalkArgs w) {
-    const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t c = s < w.n_streams ? w.results[s].n_frames : 0;
-    uint32_t total;
-    (void)block_exclusive_sum_u32(c, &total);
-    if (threadIdx.x == 0) w.sc.walk_agg[blockIdx.x] = total;
-}
-
-// wave mode pass 2: offsets, after k_walk_write<false> placed each connection's first frame
-__global__ __launch_bounds__(kBlock) void k_walk_write_wave(WalkArgs w) {
-    __shared__ __attribute__((aligned(16))) uint8_t win[kBlock / 64][2 * kWalkBlk];
-    const uint32_t wave = threadIdx.x >> 6;
-    const uint32_t s = blockIdx.x * (kBlock / 64) + wave;
-    if (s >= w.n_streams) return;
-    if (w.sc.tmp_cap && *w.sc.walk_single) return;  // the single pass already has the starts
-    const uvhttp_ws_stream_result_t r = w.results[s];
-    if (r.n_frames) (void)walk_stream_wave<1>(w, s, r.first_frame, win[wave]);
-}
-
-
-__global__ __launch_bounds__(kBlock) void k_walk_count(WalkArgs w) {
-    const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t c = s < w.n_streams ? walk_stream<false>(w, s, 0) : 0;
-    if (s < w.n_streams) w.results[s].n_frames = c;
-    uint32_t total;
-    (void)block_exclusive_sum_u32(c, &total);
-    if (threadIdx.x == 0) w.sc.walk_agg[blockIdx.x] = total;
-}
-
-__global__ __launch_bounds__(kBlock) void k_walk_scan(WalkArgs w, uint32_t n_blocks) {
-    const uint32_t per = (n_blocks + kBlock - 1) / kBlock;
-    const uint32_t beg = threadIdx.x * per;
-    const uint32_t fin = beg + per < n_blocks ? beg + per : n_blocks;
-    uint32_t run = 0;
-    for (uint32_t b = beg; b < fin; ++b) run += w.sc.walk_agg[b];
-    uint32_t total;
-    uint32_t pre = block_exclusive_sum_u32(run, &total);
-    for (uint32_t b = beg; b < fin; ++b) {
-        const uint32_t v = w.sc.walk_agg[b];
-        w.sc.walk_agg[b] = pre;
-        pre += v;
-    }
-    if (threadIdx.x == 0) *w.sc.n_total = total <= w.max_frames ? total : 0;
-}
-
-// each connection's first frame (scan of the counts) and its provisional result; the lane
-// walk also writes its frame offsets here (second walk)
-template <bool WALK>
-__global__ __launch_bounds__(kBlock) void k_walk_write(WalkArgs w) {
-    const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t c = s < w.n_streams ? w.results[s].n_frames : 0;
-    uint32_t total;
-    const uint32_t first = w.sc.walk_agg[blockIdx.x] + block_exclusive_sum_u32(c, &total);
-    if (s >= w.n_streams) return;
-    const bool fits = *w.sc.n_total != 0 || c == 0;  // n_total 0 with frames = overflow
-    const uvhttp_ws_stream_t st = w.streams[s];
-    const bool layout = (uint32_t)(w.sc.walk_stop[s] >> 32) == kStopLayout;
-    uvhttp_ws_stream_result_t r;
-    r.first_frame = first;
-    r.n_frames = c;
-    r.n_delivered = 0;
-    r.status = 0;
-    r.first_status = 0;
+__device__ inline void capacity_result(uvhttp_ws_stream_result_t& r) {
+    r.status = -1;
+    r.first_status = UVHTTP_WS_FRAME_ERR_CAPACITY;
+    r.n_frames = r.n_delivered = 0;
     r.calls = 0;
     r.consumed_bytes = 0;
-    r.recv_buffer_size = st.recv_buffer_size;
-    r.pending_bytes = st.pending_bytes;
     r.buffered_end = 0;
-    r.reserved = 0;
-    if (layout) {
-        r.status = -1;
-        r.first_status = UVHTTP_WS_FRAME_ERR_LAYOUT;
-    } else if (!fits) {
-        r.status = -1;
-        r.first_status = UVHTTP_WS_FRAME_ERR_CAPACITY;
-        r.n_frames = 0;
-    } else if (c && WALK) {
-        (void)walk_stream<true>(w, s, first);
-    }
-    w.sc.seg_bad[s] = first + (fits ? c : 0);
-    w.results[s] = r;
 }
 
-// the call (0-based) of connection st that completes a frame ending at stream offset fe
-__device__ inline uint32_t call_of_end(const uint64_t* read_end, const uvhttp_ws_stream_t& st,
-                                       uint64_t fe) {
-    if (!st.n_reads) return 0;
-    const uint64_t* re = read_end + st.first_read;
-    uint32_t lo = 0, hi = st.n_reads - 1;  // first k with re[k] >= fe (the last one does)
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (re[mid] >= fe) hi = mid;
-        else lo = mid + 1;
-    }
-    return lo;
-}
-
-// k_stream_mark: after the state machine.  Frames past their connection's first failure
-// become SKIPPED (so the payload pass leaves them masked); per-connection results: which call
-// failed (or how many ran), the buffer size it left, the bytes left buffered.
-__global__ __launch_bounds__(kBlock) void k_stream_mark(BatchArgs a, uvhttp_ws_frame_desc_t* desc,
-                                                        uvhttp_ws_stream_result_t* results,
-                                                        uint32_t n_streams, Workspace ws,
-                                                        StreamScratch sc, const uint64_t* read_end) {
-    resolve_epoch(a, ws);
-    const bool dev_fault = device_fault(a, ws);
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t n = nframes(a);
-    if (i < n && (dev_fault || i > a.seg_bad[a.frame_seg[i]])) desc[i].status = UVHTTP_WS_FRAME_SKIPPED;
-    if (i >= n_streams) return;
-    uvhttp_ws_stream_result_t r = results[i];
-    if (dev_fault) {
-        r.status = -1;
-        r.first_status = UVHTTP_WS_FRAME_ERR_DEVICE;
-        r.n_delivered = 0;
-        results[i] = r;
+// lane mode: one lane per connection (few frames each) writes its descriptors in order
+__global__ __launch_bounds__(kBlock) void k_stream_desc_lane(WalkArgs w) {
+    const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t first = lane_first(w, s);
+    if (s >= w.n_streams) return;
+    uvhttp_ws_stream_result_t r = w.results[s];
+    if (*w.sc.n_total == 0 && r.n_frames) {
+        capacity_result(r);
+        w.results[s] = r;
         return;
     }
-    if (r.first_status != 0) return;  // layout or capacity failure: nothing decoded
-    const uvhttp_ws_stream_t st = a.streams[i];
-    const uint64_t stop = sc.walk_stop[i];
-    const uint32_t kind = (uint32_t)(stop >> 32), scall = (uint32_t)stop;
-    auto size_after = [&](uint32_t call) {
-        return st.n_reads ? sc.read_size[st.first_read + call] : sc.stop_size[i];
-    };
-    auto end_of = [&](uint32_t call) { return st.n_reads ? read_end[st.first_read + call] : st.len; };
-    const uint32_t bad = a.seg_bad[i];
-    const uint32_t delivered = bad - r.first_frame;
-    r.n_delivered = delivered;
-    uint32_t call = scall;
-    if (delivered < r.n_frames) {  // a frame failed: header checks or the state machine
-        r.first_status = desc[bad].status;
-        r.status = r.first_status < 0 ? -1 : 0;
-        const bool walk_bad = kind == kStopBad && bad + 1 == r.first_frame + r.n_frames;
-        if (!walk_bad)  // a complete frame the state machine rejected: the call completing it
-            call = call_of_end(read_end, st, frame_start(a, bad) + desc[bad].wire_len - st.begin);
-        r.buffered_end = end_of(call);
-    } else if (kind == kStopGrow) {
-        r.status = -1;
-        r.first_status = UVHTTP_WS_FRAME_ERR_BUFFER;
-        r.buffered_end = call ? end_of(call - 1) : 0;  // the failing call appended nothing
-    } else {
-        r.buffered_end = end_of(call);
+    w.results[s].first_frame = first;
+    if (!r.n_frames) return;
+    r.first_frame = first;
+    const uvhttp_ws_stream_t st = w.streams[s];
+    const uint64_t sb = slice_base(st, s);
+    uint32_t msg = 0;
+    for (uint32_t k = 0; k < r.n_frames; ++k) {
+        const uint64_t pos = w.single ? w.sc.walk_tmp[sb + k] : w.sc.frame_off[first + k] - st.begin;
+        uvhttp_ws_frame_desc_t d;
+        bool fin_data;
+        uint64_t fe;
+        stream_frame_desc(w, st, r, k, pos, d, fin_data, fe);
+        if (d.status == UVHTTP_WS_FRAME_OK && d.opcode <= 2) d.message = msg;
+        msg += fin_data ? 1u : 0u;
+        w.desc[first + k] = d;
+        w.sc.frame_off[first + k] = fe;
     }
-    r.calls = call + 1;
-    r.recv_buffer_size = size_after(call);
-    if (delivered) {
-        const uint32_t lastf = r.first_frame + delivered - 1;
-        r.consumed_bytes = frame_start(a, lastf) + desc[lastf].wire_len - st.begin;
-        r.pending_bytes = a.open_after[lastf];
-    }
-    results[i] = r;
 }
+
+// k_stream_desc: one wave per connection writes its descriptors (the frames' headers re-read
+// with two aligned 16-byte loads each), the running message id (FIN data frames delivered
+// before the frame in its connection), MSG_END, the failing frame's status, and each
+// frame's end for the tile claims.  Capacity overflow: every result says so, nothing else.
+__global__ __launch_bounds__(kBlock) void k_stream_desc(WalkArgs w) {
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const uint32_t s = blockIdx.x * (kBlock / 64) + wave;
+    if (s >= w.n_streams) return;
+    uvhttp_ws_stream_result_t r = w.results[s];
+    const bool fits = *w.sc.n_total != 0 || r.n_frames == 0;
+    if (!fits) {
+        if (lane == 0) {
+            capacity_result(r);
+            w.results[s] = r;
+        }
+        return;
+    }
+    if (!r.n_frames) return;
+    const uvhttp_ws_stream_t st = w.streams[s];
+    const uint64_t sb = slice_base(st, s);
+    uint32_t msg = 0;  // FIN data frames delivered before this chunk
+    for (uint32_t k0 = 0; k0 < r.n_frames; k0 += 64) {
+        const uint32_t k = k0 + lane;
+        const bool act = k < r.n_frames;
+        uvhttp_ws_frame_desc_t d;
+        bool fin_data = false;
+        if (act) {
+            const uint64_t pos = w.single ? w.sc.walk_tmp[sb + k] : w.sc.frame_off[r.first_frame + k] - st.begin;
+            uint64_t fe;
+            stream_frame_desc(w, st, r, k, pos, d, fin_data, fe);
+            w.sc.frame_off[r.first_frame + k] = fe;  // (this lane read its own entry above)
+        }
+        // message id: FIN data frames delivered before this one in the connection
+        const uint64_t fm = __ballot(fin_data);
+        const uint32_t before = msg + (uint32_t)__builtin_popcountll(fm & ((1ull << lane) - 1));
+        if (act) {
+            if (d.status == UVHTTP_WS_FRAME_OK && d.opcode <= 2) d.message = before;
+            w.desc[r.first_frame + k] = d;
+        }
+        msg += (uint32_t)__builtin_popcountll(fm);
+    }
+}
+
+// k_stream_claims: frame i claims the 16 KiB map tiles whose first byte lies in
+// [end of frame i - 1, end of frame i): the first frame ending after a tile's start, which is
+// where the payload kernel's frame range for that tile must begin (gaps between connections
+// and undecoded tails are covered by the next frame, tiles after the last frame stay
+// unclaimed and are skipped)
+__global__ __launch_bounds__(kBlock) void k_stream_claims(BatchArgs a, Workspace ws,
+                                                          const uint64_t* frame_end) {
+    resolve_epoch(a, ws);
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t n = nframes(a);
+    if (i >= n) return;
+    const uint64_t lo = i ? frame_end[i - 1] : 0;
+    uint64_t hi = frame_end[i];
+    if (hi > a.wire_len) hi = a.wire_len;
+    for (uint64_t t = lo / kMapTile + (lo % kMapTile != 0); t * kMapTile < hi && t < a.n_tiles; ++t)
+        tag_claim(&ws.tile_first[t], a.epoch, i);
+}
+
 
 // ------------------------------------------------------------------------------------
 // send side: batched uvhttp_ws_build_frame (:204-285).  kb_size -> two-level u64 scan ->
@@ -2510,7 +2617,7 @@ struct uvhttp_ws_gpu_engine {
     int plan_fpt;              // k_plan frames per lane, 0 = automatic
     int walk_mode;             // stream frame discovery: 0 automatic, 1 lane, 2 wave
     void* ss_mem;              // stream-decode scratch
-    uint32_t ss_frames, ss_streams, ss_reads;
+    uint32_t ss_frames, ss_reads;
     StreamScratch ss;
     void* wt_mem;              // single-pass walk scratch (frame starts per connection slice)
     uint64_t wt_cap;
@@ -2967,29 +3074,19 @@ int uvhttp_ws_gpu_decode_compact(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batc
 
 static int reserve_streams(uvhttp_ws_gpu_engine_t* e, uint32_t frames, uint32_t streams,
                            uint32_t reads) {
+    (void)streams;
     if (reads == 0) reads = 1;
-    if (e->ss_mem && frames <= e->ss_frames && streams <= e->ss_streams && reads <= e->ss_reads)
-        return UVHTTP_WS_GPU_OK;
+    if (e->ss_mem && frames <= e->ss_frames && reads <= e->ss_reads) return UVHTTP_WS_GPU_OK;
     if (e->capturing)
         return set_err(e, UVHTTP_WS_GPU_EINVAL, "stream scratch too small for a captured call",
                        hipSuccess);
     const uint32_t fr = frames > e->ss_frames ? frames : e->ss_frames;
-    const uint32_t sn = streams > e->ss_streams ? streams : e->ss_streams;
     const uint32_t rd = reads > e->ss_reads ? reads : e->ss_reads;
-    const uint64_t sblk = (sn + kBlock - 1) / kBlock + 2;
     size_t o_off = 0;
-    size_t o_seg = align_up(o_off + (size_t)fr * 8, 256);
-    size_t o_open = align_up(o_seg + (size_t)fr * 4, 256);
-    size_t o_bad = align_up(o_open + (size_t)fr * 8, 256);
-    size_t o_agg = align_up(o_bad + (size_t)sn * 4, 256);
-    size_t o_tot = align_up(o_agg + sblk * 4, 256);
-    size_t o_wbase = align_up(o_tot + 16, 256);
-    size_t o_bblk = align_up(o_wbase + (size_t)sn * 8, 256);
-    size_t o_single = align_up(o_bblk + sblk * 8, 256);
-    size_t o_stop = align_up(o_single + 16, 256);
-    size_t o_ssize = align_up(o_stop + (size_t)sn * 8, 256);
-    size_t o_rsize = align_up(o_ssize + (size_t)sn * 8, 256);
-    size_t bytes = align_up(o_rsize + (size_t)rd * 8, 256);
+    size_t o_tot = align_up(o_off + (size_t)fr * 8, 256);
+    size_t o_rsize = align_up(o_tot + 16, 256);
+    size_t o_agg = align_up(o_rsize + (size_t)rd * 8, 256);
+    size_t bytes = align_up(o_agg + ((size_t)kMaxFrames / kBlock + 2) * 4, 256);
     int prev = 0;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(e->device);
@@ -2998,24 +3095,15 @@ static int reserve_streams(uvhttp_ws_gpu_engine_t* e, uint32_t frames, uint32_t 
     const hipError_t h = hipMalloc(&e->ss_mem, bytes);
     (void)hipSetDevice(prev);
     if (h != hipSuccess) {
-        e->ss_frames = e->ss_streams = e->ss_reads = 0;
+        e->ss_frames = e->ss_reads = 0;
         return set_err(e, UVHTTP_WS_GPU_ENOMEM, "hipMalloc stream scratch", h);
     }
     char* b = (char*)e->ss_mem;
     e->ss.frame_off = (uint64_t*)(b + o_off);
-    e->ss.frame_seg = (uint32_t*)(b + o_seg);
-    e->ss.open_after = (uint64_t*)(b + o_open);
-    e->ss.seg_bad = (uint32_t*)(b + o_bad);
-    e->ss.walk_agg = (uint32_t*)(b + o_agg);
     e->ss.n_total = (uint32_t*)(b + o_tot);
-    e->ss.walk_base = (uint64_t*)(b + o_wbase);
-    e->ss.bound_blk = (uint64_t*)(b + o_bblk);
-    e->ss.walk_single = (uint32_t*)(b + o_single);
-    e->ss.walk_stop = (uint64_t*)(b + o_stop);
-    e->ss.stop_size = (uint64_t*)(b + o_ssize);
     e->ss.read_size = (uint64_t*)(b + o_rsize);
+    e->ss.agg = (uint32_t*)(b + o_agg);
     e->ss_frames = fr;
-    e->ss_streams = sn;
     e->ss_reads = rd;
     return UVHTTP_WS_GPU_OK;
 }
@@ -3028,6 +3116,10 @@ int uvhttp_ws_gpu_decode_streams(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uin
                                       max_frames, d_desc, d_results, stream);
 }
 
+// The stream decode: walk (per connection: calls, frames, state machine, result) -> first
+// frames -> descriptors -> tile claims -> the in-place payload kernel.  Frame starts go to
+// per-connection slices (single pass) when the slice scratch fits; otherwise the walk runs
+// twice (count, then write the starts).
 int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint64_t wire_len,
                                const uvhttp_ws_stream_t* d_streams, uint32_t n_streams,
                                const uint64_t* d_read_end, uint32_t n_reads_total,
@@ -3052,6 +3144,14 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     if (prev != e->device) (void)hipSetDevice(e->device);
     hipStream_t s = (hipStream_t)stream;
 
+    // slices: connection s's starts at walk_tmp[begin / 2 + s ...] (4-byte entries)
+    const uint64_t want = wire_len / 2 + n_streams + 1;
+    if (e->walk_single_off == 0 && !e->capturing && want * 4 <= (8ull << 30) && want > e->wt_cap) {
+        if (e->wt_mem) (void)hipFree(e->wt_mem);
+        e->wt_mem = nullptr;
+        e->wt_cap = 0;
+        if (hipMalloc(&e->wt_mem, want * 4) == hipSuccess) e->wt_cap = want;
+    }
     WalkArgs w;
     w.wire = d_wire;
     w.wire_len = wire_len;
@@ -3060,63 +3160,45 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     w.max_frames = max_frames;
     w.read_end = d_read_end;
     w.n_reads_total = n_reads_total;
+    w.single = (e->walk_single_off == 0 && e->wt_cap >= want) ? 1u : 0u;
     w.results = d_results;
+    w.desc = d_desc;
     w.sc = e->ss;
+    w.sc.walk_tmp = (uint32_t*)e->wt_mem;
+    w.agg = e->ss.agg;
     const uint32_t nsb = (n_streams + kBlock - 1) / kBlock;
-    // frame discovery: a lane per connection, or a wave per connection when the waves fit
-    // the chip in about one round (UVHTTP_WS_WALK=lane|wave pins it)
+    const uint32_t nwb = (n_streams + kBlock / 64 - 1) / (kBlock / 64);
+    // a wave per connection when the waves fill the chip in about one round, else a lane
+    // (UVHTTP_WS_WALK=lane|wave pins it)
     const bool wave_walk = e->walk_mode ? e->walk_mode == 2 : n_streams <= 16384;
     if (wave_walk) {
-        const uint32_t nwb = (n_streams + kBlock / 64 - 1) / (kBlock / 64);
-        // single pass when the offset scratch fits: bound <= wire/2 + one per connection
-        // (4-byte entries, so at most 2 bytes per wire byte; capped at 8 GiB)
-        const uint64_t want = wire_len / 2 + n_streams + 1;
-        if (e->walk_single_off == 0 && !e->capturing && want * 4 <= (8ull << 30) && want > e->wt_cap) {
-            if (e->wt_mem) (void)hipFree(e->wt_mem);
-            e->wt_mem = nullptr;
-            e->wt_cap = 0;
-            if (hipMalloc(&e->wt_mem, want * 4) == hipSuccess) e->wt_cap = want;
-        }
-        w.sc.walk_tmp = (uint32_t*)e->wt_mem;
-        w.sc.tmp_cap = e->walk_single_off ? 0 : e->wt_cap;
-        if (w.sc.tmp_cap) {
-            hipLaunchKernelGGL(k_walk_bound, dim3(nsb), dim3(kBlock), 0, s, w);
-            hipLaunchKernelGGL(k_walk_bound_scan, dim3(1), dim3(kBlock), 0, s, w, nsb);
-            hipLaunchKernelGGL(k_walk_once_wave, dim3(nwb), dim3(kBlock), 0, s, w);
-        } else {
-            hipLaunchKernelGGL(k_walk_count_wave, dim3(nwb), dim3(kBlock), 0, s, w);
-        }
-        hipLaunchKernelGGL(k_walk_agg, dim3(nsb), dim3(kBlock), 0, s, w);
-        hipLaunchKernelGGL(k_walk_scan, dim3(1), dim3(kBlock), 0, s, w, nsb);
-        hipLaunchKernelGGL(k_walk_write<false>, dim3(nsb), dim3(kBlock), 0, s, w);
-        if (w.sc.tmp_cap) hipLaunchKernelGGL(k_walk_compact, dim3(nwb), dim3(kBlock), 0, s, w);
-        hipLaunchKernelGGL(k_walk_write_wave, dim3(nwb), dim3(kBlock), 0, s, w);  // fallback
+        if (w.single) hipLaunchKernelGGL(k_swalk_wave<2>, dim3(nwb), dim3(kBlock), 0, s, w);
+        else hipLaunchKernelGGL(k_swalk_wave<0>, dim3(nwb), dim3(kBlock), 0, s, w);
     } else {
-        hipLaunchKernelGGL(k_walk_count, dim3(nsb), dim3(kBlock), 0, s, w);
-        hipLaunchKernelGGL(k_walk_scan, dim3(1), dim3(kBlock), 0, s, w, nsb);
-        hipLaunchKernelGGL(k_walk_write<true>, dim3(nsb), dim3(kBlock), 0, s, w);
+        if (w.single) hipLaunchKernelGGL(k_swalk_lane<2>, dim3(nsb), dim3(kBlock), 0, s, w);
+        else hipLaunchKernelGGL(k_swalk_lane<0>, dim3(nsb), dim3(kBlock), 0, s, w);
     }
+    hipLaunchKernelGGL(k_swalk_scan, dim3(1), dim3(kBlock), 0, s, w, wave_walk ? 0u : 1u);
+    if (!w.single) {
+        if (wave_walk) hipLaunchKernelGGL(k_swalk_wave<1>, dim3(nwb), dim3(kBlock), 0, s, w);
+        else hipLaunchKernelGGL(k_swalk_lane<1>, dim3(nsb), dim3(kBlock), 0, s, w);
+    }
+    if (wave_walk) hipLaunchKernelGGL(k_stream_desc, dim3(nwb), dim3(kBlock), 0, s, w);
+    else hipLaunchKernelGGL(k_stream_desc_lane, dim3(nsb), dim3(kBlock), 0, s, w);
 
     BatchArgs a;
     memset(&a, 0, sizeof(a));
     a.wire = d_wire;
     a.wire_len = wire_len;
-    a.frame_off = e->ss.frame_off;
     a.n = cap;
     a.n_tiles = (wire_len + kMapTile - 1) / kMapTile;
     a.streams = d_streams;
-    a.frame_seg = e->ss.frame_seg;
     a.n_dev = e->ss.n_total;
-    a.open_after = e->ss.open_after;
-    a.seg_bad = e->ss.seg_bad;
     a.max_polls = e->max_polls;
     a.dev_epoch = e->capturing ? 1u : 0u;
     a.epoch = next_epoch(e, s);
-    launch_plan(e, a, cap, d_desc, nullptr, s);
-    const uint32_t grid_f = (cap + kBlock - 1) / kBlock;
-    const uint32_t grid_m = grid_f > nsb ? grid_f : nsb;
-    hipLaunchKernelGGL(k_stream_mark, dim3(grid_m), dim3(kBlock), 0, s, a, d_desc, d_results,
-                       n_streams, e->ws, e->ss, d_read_end);
+    hipLaunchKernelGGL(k_stream_claims, dim3((cap + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a,
+                       e->ws, (const uint64_t*)e->ss.frame_off);
     int blk = e->tile_block ? e->tile_block : 256, vpt = e->tile_block ? e->tile_vpt : 2;
     const uint64_t tile_bytes = (uint64_t)blk * vpt * 16;
     const uint64_t n_ptiles = (wire_len + tile_bytes - 1) / tile_bytes;
