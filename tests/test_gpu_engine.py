@@ -74,7 +74,19 @@ def test_lookback_give_up_is_reported(torch):
     with pytest.raises(U.GpuError):
         eng.sync()
     eng.sync()  # reported once
-    # stream decode on the same engine: every connection ERR_DEVICE, nothing unmasked
+    # a stride batch of small frames (k_unmask_stride parses headers itself): nothing unmasked
+    sw = b"".join(_frame(2, 1, rng.randbytes(40), rng.randbytes(4), True, 0) for _ in range(30000))
+    sd = torch.from_numpy(np.frombuffer(sw + bytes(64), np.uint8).copy()).to("cuda")
+    sbefore = sd.clone()
+    desc, summ = eng.decode_inplace(sd, 30000, stride=len(sw) // 30000, wire_len=len(sw))
+    torch.cuda.synchronize()
+    s = eng.read_summary(summ)
+    assert s["status"] == -1 and s["first_status"] == -11 and s["n_delivered"] == 0, s
+    assert torch.equal(sd, sbefore)
+    with pytest.raises(U.GpuError):
+        eng.sync()
+    # the stream decode has no look-back (per-connection walk + one-block scan): the same
+    # engine still decodes streams normally
     st = np.zeros(64, U.STREAM_DT)
     per = w.size // 64
     idx = np.minimum(np.searchsorted(offs, np.arange(64) * per), len(offs) - 1)
@@ -82,13 +94,13 @@ def test_lookback_give_up_is_reported(torch):
     for k in range(64):
         st[k] = (cut[k], cut[k + 1] - cut[k], 1 << 30, 0, 0, 1 << 24, 1 << 26, 1, 0, 0, 0)
     sdev = torch.from_numpy(st.view(np.uint8).copy()).to("cuda")
-    _, res = eng.decode_streams(d, sdev, 64, 8192, wire_len=w.size)
+    d2 = before.clone()
+    _, res = eng.decode_streams(d2, sdev, 64, 8192, wire_len=w.size)
     torch.cuda.synchronize()
     rs = eng.read_stream_results(res, 64)
-    assert all(r.first_status == -11 and r.n_delivered == 0 for r in rs)
-    assert torch.equal(d, before)
-    with pytest.raises(U.GpuError):
-        eng.sync()
+    assert all(r.status == 0 for r in rs)
+    assert sum(r.n_delivered for r in rs) == len(offs)
+    eng.sync()
     eng.close()
     good = _engine()
     desc, summ = good.decode_inplace(d, len(offs), offsets=o, wire_len=w.size)

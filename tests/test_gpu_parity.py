@@ -365,6 +365,13 @@ def test_config_c4_default_limit_rejects(torch, eng):
     s = eng.read_summary(summ)
     assert s["n_delivered"] == 262144 and s["first_status"] == -8 and s["status"] == -1
     assert s["pending_bytes"] == 262144 * 256
+    # frames before the rejected one unmasked, it and every later frame left masked
+    for i in (0, 262143, 262144, 262145, n - 1):
+        got = d[i * stride:(i + 1) * stride].cpu().numpy()
+        ow, _ = _oracle.gen_frames(n, plen, SEED, fragmented=True, first=i, count=1, total=n)
+        if i < 262144:
+            _oracle.load().oracle_unmask_frames(_oracle._ptr(ow), 1, stride)
+        assert np.array_equal(got, ow), i
 
 
 @pytest.mark.parametrize("shape", [(64, 1), (64, 2), (64, 4), (128, 1), (128, 2), (256, 1),
@@ -531,3 +538,42 @@ def test_stride_layouts(torch, eng, plen, compact):
             ref, got = _run_both(torch, eng, wire, len(frames), stride=stride, wire_len=wl,
                                  compact=compact)
             _compare(ref, got, compact)
+
+
+def test_stride_state_machine_failures(torch):
+    """Stride batches with failures only the state machine sees — a CONTINUATION with nothing
+    open, a new data frame inside a fragmented message, a message over max_message_size — at
+    the first, a middle and the last frame, and deep in a batch of 60 000 frames: bytes,
+    statuses and summaries equal the oracle's (frames from the failing one on stay masked)."""
+    import uvhttp_amd as U
+    e = U.GpuEngine(0)
+    try:
+        rng = random.Random(55)
+        k = lambda: rng.randbytes(4)  # noqa: E731
+        for plen, n in ((60, 600), (200, 600), (3000, 200), (1, 60000)):
+            for where in (0, 1, n // 2, n - 1):
+                for kind in ("cont", "new_in_frag", "too_big", "ok"):
+                    frames = [_frame(2, 1, rng.randbytes(plen), k()) for _ in range(n)]
+                    mm = MM
+                    if kind == "cont":
+                        frames[where] = _frame(0, 1, rng.randbytes(plen), k())
+                    elif kind == "new_in_frag":
+                        if where == 0:
+                            continue
+                        frames[where - 1] = _frame(1, 0, rng.randbytes(plen), k())
+                        frames[where] = _frame(2, 1, rng.randbytes(plen), k())
+                    elif kind == "too_big":
+                        # a fragmented message from frame 0 that passes the limit at `where`
+                        frames = [_frame(2 if i == 0 else 0, 0, rng.randbytes(plen), k())
+                                  for i in range(n)]
+                        mm = plen * (where + 1) - 1
+                        if mm == 0:  # (0 means no limit)
+                            continue
+                    wire = np.frombuffer(b"".join(frames), np.uint8).copy()
+                    stride = len(frames[0])
+                    ref, got = _run_both(torch, e, wire, n, stride=stride, mm=mm)
+                    if kind != "ok":
+                        assert ref["summary"]["status"] == -1
+                    _compare(ref, got)
+    finally:
+        e.close()
