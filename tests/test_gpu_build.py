@@ -49,6 +49,9 @@ def eng(torch, request):
     e.close()
 
 
+GUARD = 256
+
+
 def _build(torch, eng, src, frames, cap_extra=64, cap=None):
     total = 0
     exp = []
@@ -64,10 +67,16 @@ def _build(torch, eng, src, frames, cap_extra=64, cap=None):
         torch.zeros(16, dtype=torch.uint8, device="cuda")
     dfr = torch.from_numpy(frames.view(np.uint8).copy()).to("cuda") if len(frames) else \
         torch.zeros(32, dtype=torch.uint8, device="cuda")
-    out = torch.zeros(max(16, cap), dtype=torch.uint8, device="cuda")
+    size = max(16, cap)
+    out = torch.zeros(size + GUARD, dtype=torch.uint8, device="cuda")
+    out[size:] = 0xA5  # guard: nothing may be written past the caller's buffer
+    src_before, fr_before = dsrc.clone(), dfr.clone()
     off = eng.build_frames(dsrc, dfr, len(frames), out[:cap] if cap else out[:0])
     torch.cuda.synchronize()
-    return exp, total, out.cpu().numpy(), off.cpu().numpy()
+    host = out.cpu().numpy()
+    assert (host[size:] == 0xA5).all(), "write past the output buffer"
+    assert torch.equal(dsrc, src_before) and torch.equal(dfr, fr_before), "inputs modified"
+    return exp, total, host[:size], off.cpu().numpy()
 
 
 def _rand_frames(rng, src_len, n, sizes):

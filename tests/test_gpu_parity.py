@@ -109,34 +109,65 @@ def _rand_batch(rng, n, sizes, p_ctrl=0.1, p_frag=0.3, p_bad=0.0):
     return wire, offs
 
 
+GUARD = 0xA5  # fill of the bytes around every buffer a decode may not write
+
+
 def _to_dev(torch, arr, pad=64):
-    t = torch.zeros(arr.size + pad, dtype=torch.uint8, device="cuda")
+    t = torch.full((arr.size + pad,), GUARD, dtype=torch.uint8, device="cuda")
     if arr.size:
         t[: arr.size] = torch.from_numpy(arr).to("cuda")
     return t
 
 
+def _guarded(torch, nbytes, pad=256):
+    """(whole, view): an output buffer of nbytes followed by `pad` guard bytes"""
+    t = torch.full((nbytes + pad,), GUARD, dtype=torch.uint8, device="cuda")
+    return t, t[:nbytes]
+
+
+def _guard_ok(t, start):
+    return bool((t[start:] == GUARD).all())
+
+
 def _run_both(torch, eng, wire, n, offs=None, stride=None, mf=MF, mm=MM, compact=False,
               wire_len=None):
+    import ctypes as C
+    import uvhttp_amd as U
     wl = wire.size if wire_len is None else wire_len
     ref = _oracle.decode_batch(wire, n, stride=stride, offsets=offs, wire_len=wl,
                                max_frame_size=mf, max_message_size=mm, compact=compact,
                                arena_cap=wire.size + 64)
     dw = _to_dev(torch, wire)
     doff = torch.from_numpy(offs.astype(np.int64)).to("cuda") if offs is not None else None
+    doff_before = doff.clone() if doff is not None else None
+    # every output in a guarded buffer: descriptors / messages for n frames, the summary
+    nd = max(1, n) * eng.DESC_BYTES
+    desc_all, desc = _guarded(torch, nd)
+    summ_all, summ = _guarded(torch, 64)
     if compact:
-        arena = torch.zeros(wire.size + 64, dtype=torch.uint8, device="cuda")
-        desc, msgs, summ = eng.decode_compact(dw, n, arena, stride=stride, offsets=doff,
-                                              max_frame_size=mf, max_message_size=mm,
-                                              wire_len=wl)
+        arena_all, arena = _guarded(torch, wire.size + 64)
+        msgs_all, msgs = _guarded(torch, max(1, n) * eng.MSG_BYTES)
+        eng.decode_compact(dw, n, arena, stride=stride, offsets=doff, max_frame_size=mf,
+                           max_message_size=mm, wire_len=wl, desc=desc, msgs=msgs, summary=summ)
     else:
-        desc, summ = eng.decode_inplace(dw, n, stride=stride, offsets=doff, max_frame_size=mf,
-                                        max_message_size=mm, wire_len=wl)
+        eng.decode_inplace(dw, n, stride=stride, offsets=doff, max_frame_size=mf,
+                           max_message_size=mm, wire_len=wl, desc=desc, summary=summ)
     torch.cuda.synchronize()
     got = dict(summary=eng.read_summary(summ), desc=eng.read_desc(desc, n),
                wire=dw[: wire.size].cpu().numpy())
+    # nothing written past the wire, the descriptors, the summary (or the arena / messages)
+    assert _guard_ok(dw, wire.size), "write past the wire buffer"
+    assert _guard_ok(desc_all, nd), "write past the descriptors"
+    assert _guard_ok(summ_all, C.sizeof(U.BatchSummary)), "write past the summary"
+    if doff is not None:
+        assert torch.equal(doff, doff_before), "offset table modified"
     if compact:
-        got["arena"] = arena.cpu().numpy()
+        assert _guard_ok(msgs_all, max(1, n) * eng.MSG_BYTES), "write past the messages"
+        a = arena.cpu().numpy()
+        ab = got["summary"]["arena_bytes"]
+        assert (a[ab:] == GUARD).all(), "arena written past the delivered payload"
+        assert _guard_ok(arena_all, wire.size + 64)
+        got["arena"] = a
         got["msgs"] = eng.read_msgs(msgs, got["summary"]["n_messages"])
     return ref, got
 
