@@ -74,7 +74,7 @@ def test_lookback_give_up_is_reported(torch):
     with pytest.raises(U.GpuError):
         eng.sync()
     eng.sync()  # reported once
-    # a stride batch of small frames (k_unmask_stride parses headers itself): nothing unmasked
+    # a stride batch of small frames: nothing unmasked either
     sw = b"".join(_frame(2, 1, rng.randbytes(40), rng.randbytes(4), True, 0) for _ in range(30000))
     sd = torch.from_numpy(np.frombuffer(sw + bytes(64), np.uint8).copy()).to("cuda")
     sbefore = sd.clone()
@@ -184,4 +184,46 @@ def test_calls_on_two_streams_serialise(torch):
         ref = _oracle.decode_batch(w, len(o), offsets=o)
         assert eng.read_summary(summ) == ref["summary"]
         assert np.array_equal(d[:w.size].cpu().numpy(), ref["wire"])
+    eng.close()
+
+
+def test_graph_capture_replay_stride_batches(torch):
+    """A stride-layout decode captured and replayed over changing frame bytes of one stride: no
+    failure, a state-machine failure early, none again, a failure late."""
+    t = torch
+    rng = random.Random(14)
+    n, plen = 20000, 200
+
+    def batch(fail_at):
+        frames = []
+        for i in range(n):
+            op = 0 if i == fail_at else 2  # CONTINUATION with nothing open
+            frames.append(_frame(op, 1, rng.randbytes(plen), rng.randbytes(4), True, 0))
+        return b"".join(frames)
+    batches = [batch(None), batch(37), batch(None), batch(19000)]
+    stride = len(batches[0]) // n
+    wl = len(batches[0])
+    eng = _engine()
+    wire = t.zeros(wl + 64, dtype=t.uint8, device="cuda")
+    desc, summ = eng.alloc_outputs(n)
+    eng.reserve(n, wl, 0)
+    s = t.cuda.Stream()
+    wire[:wl].copy_(t.from_numpy(np.frombuffer(batches[0], np.uint8).copy()))
+    with t.cuda.stream(s):
+        eng.decode_inplace(wire, n, stride=stride, wire_len=wl, desc=desc, summary=summ, stream=s)
+    s.synchronize()
+    g = t.cuda.CUDAGraph()
+    with t.cuda.graph(g, stream=s):
+        eng.decode_inplace(wire, n, stride=stride, wire_len=wl, desc=desc, summary=summ, stream=s)
+    for k in [0, 1, 2, 3, 1]:
+        host = np.frombuffer(batches[k], np.uint8).copy()
+        wire[:wl].copy_(t.from_numpy(host))
+        t.cuda.synchronize()
+        g.replay()
+        t.cuda.synchronize()
+        ref = _oracle.decode_batch(host, n, stride=stride, wire_len=wl)
+        assert eng.read_summary(summ) == ref["summary"], k
+        assert np.array_equal(wire[:wl].cpu().numpy(), ref["wire"]), k
+        assert np.array_equal(eng.read_desc(desc, n)["status"], ref["status"]), k
+    eng.sync()
     eng.close()

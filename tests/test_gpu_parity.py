@@ -608,3 +608,41 @@ def test_stride_state_machine_failures(torch):
                     _compare(ref, got)
     finally:
         e.close()
+
+
+def test_stride_random_batches(torch):
+    """Random stride batches (every frame the same wire size: PING/PONG/CLOSE/TEXT/BINARY/CONT
+    mixed, header violations, cut last frames, frames past the end of the wire), in place,
+    against the oracle."""
+    import uvhttp_amd as U
+    e = U.GpuEngine(0)
+    try:
+        rng = random.Random(808)
+        for it in range(24):
+            plen = rng.choice([0, 1, 5, 60, 125, 200, 1000, 3000, 9000])
+            n = rng.choice([2, 3, 64, 500, 3000])
+            frames, open_msg = [], False
+            for i in range(n):
+                r = rng.random()
+                if r < 0.1 and plen <= 125:
+                    op, fin = rng.choice([8, 9, 10]), 1
+                elif open_msg:
+                    op, fin = 0, rng.random() < 0.3
+                else:
+                    op, fin = rng.choice([1, 2]), rng.random() < 0.7
+                if op <= 2:
+                    open_msg = not fin
+                rsv = 4 if rng.random() < 0.002 else 0
+                frames.append(_frame(op, fin, rng.randbytes(plen), rng.randbytes(4), True, rsv))
+            wire = np.frombuffer(b"".join(frames), np.uint8).copy()
+            stride = len(frames[0])
+            wl = wire.size
+            if it % 4 == 1:
+                wl -= rng.randint(1, min(stride, 40))            # last frame cut short
+            elif it % 4 == 2 and n > 2:
+                wl -= stride + rng.randint(0, stride - 1)         # last frame(s) past the end
+            mm = rng.choice([MM, 0, plen * 3 + 1])
+            ref, got = _run_both(torch, e, wire, n, stride=stride, wire_len=wl, mm=mm)
+            _compare(ref, got)
+    finally:
+        e.close()
