@@ -1278,36 +1278,56 @@ __device__ void chacha_open_packed(const TlsArgs& a, uint32_t r0, uint8_t* win) 
     }
 }
 
-// Packed AES-GCM open for records up to kPackMaxLenAes: a group of kPack consecutive work items
-// on one wave, kSeg lanes per record — the same segment layout as the packed ChaCha kernel.
-// Segment k stages its key's round keys and the 4-bit GHASH tables of H, H^2 ... H^16 in LDS
-// (the record's key differs per segment); lane u of round j takes GHASH position kSeg j + u of
-// the record's left-padded sequence (AAD, ciphertext blocks, length block), runs AES-CTR for it
-// from the shared T-table and Horner with multiplier H^16; the segment's lanes combine in four
-// shuffle levels (H, H^2, H^4, H^8) and a final x H.
-__device__ inline U128 shfl_down128_seg(U128 v, int d) {
-    const uint32_t a = __shfl_down((uint32_t)v.hi, d, kSeg), b = __shfl_down((uint32_t)(v.hi >> 32), d, kSeg);
-    const uint32_t c = __shfl_down((uint32_t)v.lo, d, kSeg), e = __shfl_down((uint32_t)(v.lo >> 32), d, kSeg);
+// Packed AES-GCM: the records of a group of short records share one wave, SEG lanes per
+// record (segment k = lanes [k SEG, (k+1) SEG)).  Segment k stages its key's round keys and the
+// 4-bit GHASH tables of H, H^2 ... H^SEG in LDS (the record's key differs per segment); lane u of
+// round j takes GHASH position SEG j + u of the record's left-padded sequence (AAD, ciphertext
+// blocks, length block), runs AES-CTR for it from the shared T-table and Horner with multiplier
+// H^SEG; the segment's lanes combine in log2(SEG) shuffle levels (H, H^2, ...) and a final x H.
+// SEG = 4 (sixteen records per wave): per record the 4-bit-table multiplies of the lane tree
+// and the idle AES lanes of the last round cost less than with 16 lanes, so every packed size
+// gets cheaper (modelled per 256-byte record: ~25 k lane operations at SEG 4 vs ~69 k at 16).
+template <int SEG>
+__device__ inline U128 shfl_down128_w(U128 v, int d) {
+    const uint32_t a = __shfl_down((uint32_t)v.hi, d, SEG), b = __shfl_down((uint32_t)(v.hi >> 32), d, SEG);
+    const uint32_t c = __shfl_down((uint32_t)v.lo, d, SEG), e = __shfl_down((uint32_t)(v.lo >> 32), d, SEG);
     return U128{((uint64_t)b << 32) | a, ((uint64_t)e << 32) | c};
 }
 
+constexpr int kAesSeg = 4;                   // lanes per record in k_tls_open_aes_packed
+constexpr int kAesSegLog = 2;
+constexpr int kAesPackW = 64 / kAesSeg;      // records per wave
+static_assert((1 << kAesSegLog) == kAesSeg && kAesPackW % kPack == 0, "AES segment size");
+
+// records r0 .. r0 + 64/SEG - 1, each skipped when its group of kPack holds a long AES record
+// (that group goes to k_tls_open)
+template <int SEG, int LOG>
 __device__ void aes_open_packed(const TlsArgs& a, uint32_t r0, const uint32_t* te, uint32_t (*s_rk)[64],
-                                U128 (*s_tab)[kSegLog + 1][16]) {
-    const uint32_t lane = threadIdx.x & 63, k = lane / kSeg, u = lane % kSeg;
+                                U128 (*s_tab)[LOG + 1][16]) {
+    const uint32_t lane = threadIdx.x & 63, k = lane / SEG, u = lane % SEG;
     const uint32_t r = r0 + k;
-    bool act = r < a.n_total[0];
+    const uint32_t n = a.n_total[0];
+    // long-record groups among the wave's records: lane l < 64/SEG looks at record r0 + l
+    bool big = false;
+    if (lane < 64u / SEG && r0 + lane < n) {
+        const RecWork wb = a.work[r0 + lane];
+        big = wb.walk_status == 0 && wb.len > kPackMaxLenAes && a.sched[wb.key].cipher == UVHTTP_TLS_CIPHER_AES_GCM;
+    }
+    const uint64_t bigm = __ballot(big);
+    const uint32_t gfirst = (r0 / kPack) * kPack;  // (r0 is a multiple of kPack)
+    const bool grp_long = ((bigm >> ((r - gfirst) / kPack * kPack)) & ((1ull << kPack) - 1)) != 0;
+    bool act = r < n && !grp_long;
     RecWork w;
     if (act) {
         w = a.work[r];
         act = w.status == 0 && a.sched[w.key].cipher == UVHTTP_TLS_CIPHER_AES_GCM;
     }
     const KeySched* ks = a.sched + (act ? w.key : 0);
-    if (act) {  // the segment's round keys and H^(2^t) tables, t = 0..4
+    if (act) {  // the segment's round keys and H^(2^t) tables, t = 0..LOG
+        for (uint32_t i = u; i < 60; i += SEG) s_rk[k][i] = ks->rk[i];
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-            if (u + 16 * i < 60) s_rk[k][u + 16 * i] = ks->rk[u + 16 * i];
-#pragma unroll
-        for (int i = 0; i <= kSegLog; ++i) s_tab[k][i][u] = ks->tab[i][u];
+        for (int i = 0; i <= LOG; ++i)
+            for (uint32_t e = u; e < 16; e += SEG) s_tab[k][i][e] = ks->tab[i][e];
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1349,8 +1369,8 @@ __device__ void aes_open_packed(const TlsArgs& a, uint32_t r0, const uint32_t* t
     }
     const uint32_t nblk = (clen + 15) / 16;
     const uint32_t m = act ? nblk + 2 : 0;             // AAD, ciphertext blocks, length block
-    const uint32_t Jr = (m + kSeg - 1) / kSeg;          // this segment's rounds
-    const uint32_t pad = kSeg * Jr - m;                 // left padding (< kSeg)
+    const uint32_t Jr = (m + SEG - 1) / SEG;            // this segment's rounds
+    const uint32_t pad = SEG * Jr - m;                  // left padding (< SEG)
     uint32_t J = Jr;
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {
@@ -1364,9 +1384,9 @@ __device__ void aes_open_packed(const TlsArgs& a, uint32_t r0, const uint32_t* t
     uint32_t ej0[4] = {0, 0, 0, 0};
     LastNz nz{0, {0, 0, 0, 0}};
     for (uint32_t j = 0; j < J; ++j) {
-        const int32_t q = (int32_t)(kSeg * j + u) - (int32_t)pad;
+        const int32_t q = (int32_t)(SEG * j + u) - (int32_t)pad;
         uint32_t cb[4] = {nonce[0], nonce[1], nonce[2], q <= 0 ? 1u : (uint32_t)q + 1u};
-        aes_encrypt(s_rk[k], nr, cb, te_lds);
+        if (j < Jr) aes_encrypt(s_rk[k], nr, cb, te_lds);  // (segments with fewer rounds idle)
         if (j >= Jr) continue;
         U128 x{0, 0};
         if (q == 0) {
@@ -1390,19 +1410,19 @@ __device__ void aes_open_packed(const TlsArgs& a, uint32_t r0, const uint32_t* t
         } else if ((uint32_t)q == m - 1) {
             x = U128{(uint64_t)alen * 8, (uint64_t)clen * 8};
         }
-        acc = j == 0 ? x : gf_xor(gf_mul_tab(acc, s_tab[k][kSegLog]), x);  // Horner, H^16
+        acc = j == 0 ? x : gf_xor(gf_mul_tab(acc, s_tab[k][LOG]), x);  // Horner, H^SEG
     }
 #pragma unroll
-    for (int t = 0; t < kSegLog; ++t) acc = gf_xor(gf_mul_tab(acc, s_tab[k][t]), shfl_down128_seg(acc, 1 << t));
+    for (int t = 0; t < LOG; ++t) acc = gf_xor(gf_mul_tab(acc, s_tab[k][t]), shfl_down128_w<SEG>(acc, 1 << t));
     acc = gf_mul_tab(acc, s_tab[k][0]);
     uint32_t e[4];
 #pragma unroll
-    for (int b = 0; b < 4; ++b) e[b] = __shfl(ej0[b], (int)pad, kSeg);  // E(K, J0): round 0, lane pad
+    for (int b = 0; b < 4; ++b) e[b] = __shfl(ej0[b], (int)pad, SEG);  // E(K, J0): round 0, lane pad
     const U128 tag{acc.hi ^ (((uint64_t)e[0] << 32) | e[1]), acc.lo ^ (((uint64_t)e[2] << 32) | e[3])};
     uint32_t last_nz = nz.resolve();
 #pragma unroll
-    for (int d = kSeg / 2; d >= 1; d >>= 1) {
-        const uint32_t o = __shfl_xor(last_nz, d, kSeg);
+    for (int d = SEG / 2; d >= 1; d >>= 1) {
+        const uint32_t o = __shfl_xor(last_nz, d, SEG);
         if (o > last_nz) last_nz = o;
     }
     if (act && u == 0) {
@@ -1542,15 +1562,14 @@ __global__ CRYPT_ATTR void k_tls_open(TlsArgs a) {
 
 __global__ CRYPT_ATTR void k_tls_open_aes_packed(TlsArgs a) {
     __shared__ uint32_t te[256 * TLS_TE_COPIES];
-    __shared__ uint32_t s_rk[kCryptWaves][kPack][64];
-    __shared__ U128 s_tab[kCryptWaves][kPack][kSegLog + 1][16];
+    __shared__ uint32_t s_rk[kCryptWaves][kAesPackW][64];
+    __shared__ U128 s_tab[kCryptWaves][kAesPackW][kAesSegLog + 1][16];
     if (!(a.n_total[2] & 16u)) return;  // no short AES-GCM record
     fill_te(a.te0, te);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t n = a.n_total[0];
-    for (uint32_t g = blockIdx.x * kCryptWaves + wave; g * kPack < n; g += gridDim.x * kCryptWaves)
-        if (!group_has_long(a, g, n, UVHTTP_TLS_CIPHER_AES_GCM))
-            aes_open_packed(a, g * kPack, te, s_rk[wave], s_tab[wave]);
+    for (uint32_t g = blockIdx.x * kCryptWaves + wave; g * kAesPackW < n; g += gridDim.x * kCryptWaves)
+        aes_open_packed<kAesSeg, kAesSegLog>(a, g * kAesPackW, te, s_rk[wave], s_tab[wave]);
 }
 
 // ChaCha20-Poly1305 records (the AES-GCM kernel skips them): one wave per record, no shared
