@@ -48,7 +48,14 @@ constexpr int kCryptWaves = kCryptWG / 64;
 // plaintext: 4-bit Horner + 32 copies 310, 8-bit Horner + 32 copies 355, 8-bit + 16 copies 394,
 // 8-bit + 8 copies 379; forcing 4 waves/SIMD spills and loses)
 #ifndef TLS_TE_COPIES
-#define TLS_TE_COPIES 16   // copies of Te0 in LDS (32: conflict-free; 16: 3 workgroups per CU)
+#define TLS_TE_COPIES 16   // copies of Te0 in LDS for the packed kernel (16: more workgroups per CU)
+#endif
+#ifndef TLS_RED8
+#define TLS_RED8 1         // GHASH 8-bit Horner: reduction byte from a 256-word LDS table
+#endif
+#ifndef TLS_TE_COPIES_REC
+#define TLS_TE_COPIES_REC 16  // copies for the one-record-per-wave kernels (32 would make every
+                              // ds_read_b32 conflict-free, but measured 397 vs 465 GB/s: occupancy)
 #endif
 #ifndef TLS_GHASH8
 #define TLS_GHASH8 1       // 1: Horner multiplier H^64 through an 8-bit table (4 KiB per wave)
@@ -76,6 +83,7 @@ constexpr int kCryptWaves = kCryptWG / 64;
 #define CHACHA_ATTR __launch_bounds__(kCryptWG)
 #endif
 constexpr uint32_t kTeShift = TLS_TE_COPIES == 32 ? 5 : TLS_TE_COPIES == 16 ? 4 : 3;
+constexpr uint32_t kTeShiftRec = TLS_TE_COPIES_REC == 32 ? 5 : TLS_TE_COPIES_REC == 16 ? 4 : 3;
 
 struct U128 {  // a GCM block as a big-endian 128-bit value (bit 0 of the spec = MSB of hi)
     uint64_t hi, lo;
@@ -201,8 +209,11 @@ __device__ inline U128 gf_mul_tab(U128 x, const U128* __restrict__ t) {
     return z;
 }
 
-// X . P with P's 8-bit table T8 (256 entries of P * (byte polynomials)): Horner in x^8
-[[maybe_unused]] __device__ inline U128 gf_mul_tab8(U128 x, const U128* __restrict__ t) {
+// X . P with P's 8-bit table T8 (256 entries of P * (byte polynomials)): Horner in x^8.  The
+// reduction of the byte shifted out each step comes from red8 (gf_last8 >> 32, 256 words in
+// LDS: one lookup instead of four shifts and three XORs)
+[[maybe_unused]] __device__ inline U128 gf_mul_tab8(U128 x, const U128* __restrict__ t,
+                                                    const uint32_t* __restrict__ red8) {
     U128 z = t[x.lo & 0xFF];
 #pragma unroll
     for (int k = 14; k >= 0; --k) {
@@ -210,12 +221,22 @@ __device__ inline U128 gf_mul_tab(U128 x, const U128* __restrict__ t) {
                                   : (uint32_t)(x.hi >> ((7 - k) * 8)) & 0xFF;
         const uint32_t r = (uint32_t)z.lo & 0xFF;
         z.lo = (z.lo >> 8) | (z.hi << 56);
+#if TLS_RED8
+        z.hi = (z.hi >> 8) ^ ((uint64_t)red8[r] << 32);
+#else
+        (void)red8;
         z.hi = (z.hi >> 8) ^ gf_last8(r);
+#endif
         const U128 e = t[n];
         z.hi ^= e.hi;
         z.lo ^= e.lo;
     }
     return z;
+}
+
+// red8[r] = gf_last8(r) >> 32
+__device__ inline void fill_red8(uint32_t* red8) {
+    for (uint32_t r = threadIdx.x; r < 256; r += blockDim.x) red8[r] = (uint32_t)(gf_last8(r) >> 32);
 }
 
 // 8-bit table from the 4-bit one: byte v = (high nibble: x^0..x^3)(low nibble: x^4..x^7), so
@@ -239,32 +260,52 @@ __device__ inline U128 gf_mul_tab(U128 x, const U128* __restrict__ t) {
 __device__ inline uint32_t ror32(uint32_t x, int s) { return (x >> s) | (x << (32 - s)); }
 __device__ inline uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
-// one AES encryption with the T-table accessor te(x) (Te0[x]); rk = big-endian round keys.
-// NR is a template argument so every round-key index is a constant (the keys stay in scalar
-// registers when rk is wave-uniform).
-template <int NR, typename TE>
-__device__ inline void aes_enc(const uint32_t* __restrict__ rk, uint32_t in[4], TE te) {
+// AES rounds R0 .. NR of one block with the T-table accessor te(x) (Te0[x]); rk = big-endian
+// round keys; s0..s3 = the state entering round R0; the ciphertext goes to out.  NR is a
+// template argument so every round-key index is a constant (the keys stay in scalar registers
+// when rk is wave-uniform).
+// a ^ b ^ c in one instruction (v_bitop3_b32, truth table 0x96): the compiler splits a three-way
+// XOR into two v_xor_b32 on gfx950; and (a | b) ^ c (0x56) for the last round's byte merge
+__device__ inline uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ inline uint32_t or_xor(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x56);
+}
+
+template <int NR, int R0, typename TE>
+__device__ inline void aes_rounds(const uint32_t* __restrict__ rk, uint32_t s0, uint32_t s1, uint32_t s2,
+                                  uint32_t s3, uint32_t out[4], TE te) {
     constexpr uint32_t nr = NR;
-    uint32_t s0 = in[0] ^ rk[0], s1 = in[1] ^ rk[1], s2 = in[2] ^ rk[2], s3 = in[3] ^ rk[3];
 #pragma unroll
-    for (uint32_t r = 1; r < nr; ++r) {
-        const uint32_t t0 = te(s0 >> 24) ^ ror32(te((s1 >> 16) & 0xFF), 8) ^
-                            ror32(te((s2 >> 8) & 0xFF), 16) ^ ror32(te(s3 & 0xFF), 24) ^ rk[4 * r];
-        const uint32_t t1 = te(s1 >> 24) ^ ror32(te((s2 >> 16) & 0xFF), 8) ^
-                            ror32(te((s3 >> 8) & 0xFF), 16) ^ ror32(te(s0 & 0xFF), 24) ^ rk[4 * r + 1];
-        const uint32_t t2 = te(s2 >> 24) ^ ror32(te((s3 >> 16) & 0xFF), 8) ^
-                            ror32(te((s0 >> 8) & 0xFF), 16) ^ ror32(te(s1 & 0xFF), 24) ^ rk[4 * r + 2];
-        const uint32_t t3 = te(s3 >> 24) ^ ror32(te((s0 >> 16) & 0xFF), 8) ^
-                            ror32(te((s1 >> 8) & 0xFF), 16) ^ ror32(te(s2 & 0xFF), 24) ^ rk[4 * r + 3];
+    for (uint32_t r = R0; r < nr; ++r) {
+        const uint32_t t0 = xor3(xor3(te(s0 >> 24), ror32(te((s1 >> 16) & 0xFF), 8), ror32(te((s2 >> 8) & 0xFF), 16)),
+                                 ror32(te(s3 & 0xFF), 24), rk[4 * r]);
+        const uint32_t t1 = xor3(xor3(te(s1 >> 24), ror32(te((s2 >> 16) & 0xFF), 8), ror32(te((s3 >> 8) & 0xFF), 16)),
+                                 ror32(te(s0 & 0xFF), 24), rk[4 * r + 1]);
+        const uint32_t t2 = xor3(xor3(te(s2 >> 24), ror32(te((s3 >> 16) & 0xFF), 8), ror32(te((s0 >> 8) & 0xFF), 16)),
+                                 ror32(te(s1 & 0xFF), 24), rk[4 * r + 2]);
+        const uint32_t t3 = xor3(xor3(te(s3 >> 24), ror32(te((s0 >> 16) & 0xFF), 8), ror32(te((s1 >> 8) & 0xFF), 16)),
+                                 ror32(te(s2 & 0xFF), 24), rk[4 * r + 3]);
         s0 = t0, s1 = t1, s2 = t2, s3 = t3;
     }
-    // last round: S-box byte = bits 16..23 of Te0
-    auto sb = [&](uint32_t x) { return (te(x) >> 16) & 0xFF; };
+    // last round: the S-box byte is byte 2 of Te0[x]; v_perm_b32 moves two of them into place
+    // (selector bytes 4-7 pick from the first operand, 0-3 from the second, 0x0C gives zero)
     const uint32_t* k = rk + 4 * nr;
-    in[0] = ((sb(s0 >> 24) << 24) | (sb((s1 >> 16) & 0xFF) << 16) | (sb((s2 >> 8) & 0xFF) << 8) | sb(s3 & 0xFF)) ^ k[0];
-    in[1] = ((sb(s1 >> 24) << 24) | (sb((s2 >> 16) & 0xFF) << 16) | (sb((s3 >> 8) & 0xFF) << 8) | sb(s0 & 0xFF)) ^ k[1];
-    in[2] = ((sb(s2 >> 24) << 24) | (sb((s3 >> 16) & 0xFF) << 16) | (sb((s0 >> 8) & 0xFF) << 8) | sb(s1 & 0xFF)) ^ k[2];
-    in[3] = ((sb(s3 >> 24) << 24) | (sb((s0 >> 16) & 0xFF) << 16) | (sb((s1 >> 8) & 0xFF) << 8) | sb(s2 & 0xFF)) ^ k[3];
+    auto word = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t key) {
+        const uint32_t hi = __builtin_amdgcn_perm(te(a), te(b), 0x06020C0Cu);
+        const uint32_t lo = __builtin_amdgcn_perm(te(c), te(d), 0x0C0C0602u);
+        return or_xor(hi, lo, key);
+    };
+    out[0] = word(s0 >> 24, (s1 >> 16) & 0xFF, (s2 >> 8) & 0xFF, s3 & 0xFF, k[0]);
+    out[1] = word(s1 >> 24, (s2 >> 16) & 0xFF, (s3 >> 8) & 0xFF, s0 & 0xFF, k[1]);
+    out[2] = word(s2 >> 24, (s3 >> 16) & 0xFF, (s0 >> 8) & 0xFF, s1 & 0xFF, k[2]);
+    out[3] = word(s3 >> 24, (s0 >> 16) & 0xFF, (s1 >> 8) & 0xFF, s2 & 0xFF, k[3]);
+}
+
+template <int NR, typename TE>
+__device__ inline void aes_enc(const uint32_t* __restrict__ rk, uint32_t in[4], TE te) {
+    aes_rounds<NR, 1>(rk, in[0] ^ rk[0], in[1] ^ rk[1], in[2] ^ rk[2], in[3] ^ rk[3], in, te);
 }
 
 template <typename TE>
@@ -273,6 +314,48 @@ __device__ inline void aes_encrypt(const uint32_t* __restrict__ rk, uint32_t nr,
         aes_enc<10>(rk, in, te);
     else
         aes_enc<14>(rk, in, te);
+}
+
+// AES-CTR with a counter below 2^16 (every GCM counter of a TLS record: J0 + 1 + block index,
+// at most 1043): of the counter block only bytes 14 and 15 change, so round 1 depends on two
+// varying bytes (columns 0 and 1 of its output) and round 2 reads eight varying bytes; the
+// other 22 of those rounds' 32 table lookups are the same for every block of the record and
+// are folded into six words once per record (the counter-mode caching of Bernstein-Schwabe).
+struct CtrCache {
+    uint32_t c0, c1;          // round-1 output columns 0 / 1 without their varying lookup
+    uint32_t d0, d1, d2, d3;  // round-2 output without the lookups of round-1 columns 0 / 1
+};
+
+template <typename TE>
+__device__ inline CtrCache ctr_cache(const uint32_t* __restrict__ rk, const uint32_t nonce[3], TE te) {
+    const uint32_t s0 = nonce[0] ^ rk[0], s1 = nonce[1] ^ rk[1], s2 = nonce[2] ^ rk[2];
+    const uint32_t s3 = rk[3];  // bytes 12, 13 of the counter are zero; 14, 15 vary
+    CtrCache c;
+    c.c0 = te(s0 >> 24) ^ ror32(te((s1 >> 16) & 0xFF), 8) ^ ror32(te((s2 >> 8) & 0xFF), 16) ^ rk[4];
+    c.c1 = te(s1 >> 24) ^ ror32(te((s2 >> 16) & 0xFF), 8) ^ ror32(te(s0 & 0xFF), 24) ^ rk[5];
+    const uint32_t t2 = te(s2 >> 24) ^ ror32(te((s3 >> 16) & 0xFF), 8) ^ ror32(te((s0 >> 8) & 0xFF), 16) ^
+                        ror32(te(s1 & 0xFF), 24) ^ rk[6];
+    const uint32_t t3 = te(s3 >> 24) ^ ror32(te((s0 >> 16) & 0xFF), 8) ^ ror32(te((s1 >> 8) & 0xFF), 16) ^
+                        ror32(te(s2 & 0xFF), 24) ^ rk[7];
+    c.d0 = ror32(te((t2 >> 8) & 0xFF), 16) ^ ror32(te(t3 & 0xFF), 24) ^ rk[8];
+    c.d1 = ror32(te((t2 >> 16) & 0xFF), 8) ^ ror32(te((t3 >> 8) & 0xFF), 16) ^ rk[9];
+    c.d2 = te(t2 >> 24) ^ ror32(te((t3 >> 16) & 0xFF), 8) ^ rk[10];
+    c.d3 = te(t3 >> 24) ^ ror32(te(t2 & 0xFF), 24) ^ rk[11];
+    return c;
+}
+
+// E(K, nonce || ctr) for ctr < 2^16 from the record's cache (out = the 4 big-endian words)
+template <int NR, typename TE>
+__device__ inline void aes_ctr_cached(const uint32_t* __restrict__ rk, const CtrCache& c, uint32_t ctr,
+                                      uint32_t out[4], TE te) {
+    const uint32_t s3 = rk[3] ^ ctr;
+    const uint32_t t0 = c.c0 ^ ror32(te(s3 & 0xFF), 24);
+    const uint32_t t1 = c.c1 ^ ror32(te((s3 >> 8) & 0xFF), 16);
+    const uint32_t u0 = xor3(te(t0 >> 24), ror32(te((t1 >> 16) & 0xFF), 8), c.d0);
+    const uint32_t u1 = xor3(te(t1 >> 24), ror32(te(t0 & 0xFF), 24), c.d1);
+    const uint32_t u2 = xor3(ror32(te((t0 >> 8) & 0xFF), 16), ror32(te(t1 & 0xFF), 24), c.d2);
+    const uint32_t u3 = xor3(ror32(te((t0 >> 16) & 0xFF), 8), ror32(te((t1 >> 8) & 0xFF), 16), c.d3);
+    aes_rounds<NR, 3>(rk, u0, u1, u2, u3, out, te);
 }
 
 // S-box (FIPS-197 §5.1.1: inverse in GF(2^8), then the affine map) and Te0, one thread
@@ -628,7 +711,8 @@ struct Lanes {          // per-lane state after the Horner pass
 
 template <bool SEAL>
 __device__ Lanes gcm_lanes(const KeySched* __restrict__ ks, const uint32_t* te, uint32_t lane32,
-                           const U128 (*tabs)[16], const U128* t8, const uint32_t nonce[3], U128 aad,
+                           const U128 (*tabs)[16], const U128* t8, const uint32_t* red8,
+                           const uint32_t nonce[3], U128 aad,
                            uint32_t alen, const uint8_t* ct_in, uint8_t* ct_out, uint32_t clen,
                            uint8_t* dst, uint32_t wlen, const uint8_t* src, uint32_t src_n,
                            uint32_t inner_type, bool is13) {
@@ -638,11 +722,15 @@ __device__ Lanes gcm_lanes(const KeySched* __restrict__ ks, const uint32_t* te, 
     const uint32_t m = nblk + 2;             // AAD, ciphertext blocks, length block
     const uint32_t J = (m + 63) / 64;
     const uint32_t pad = 64 * J - m;
-    auto te_lds = [&](uint32_t x) { return te[(x << kTeShift) | lane32]; };
+    auto te_lds = [&](uint32_t x) { return te[(x << kTeShiftRec) | lane32]; };
     const uint32_t* __restrict__ rk = ks->rk;
     U128 acc{0, 0};
     uint32_t ej0[4] = {0, 0, 0, 0};
     LastNz nz{0, {0, 0, 0, 0}};
+    // every counter of the record below 2^16 (always, for TLS record sizes): rounds 1-2 cached
+    const bool cached = m + 1 < 65536u;
+    CtrCache cc{0, 0, 0, 0, 0, 0};
+    if (cached) cc = ctr_cache(rk, nonce, te_lds);
     for (uint32_t j = 0; j < J; ++j) {
         const int32_t q = (int32_t)(64 * j + lane) - (int32_t)pad;  // position in the sequence
         U128 x{0, 0};
@@ -650,7 +738,12 @@ __device__ Lanes gcm_lanes(const KeySched* __restrict__ ks, const uint32_t* te, 
         uint32_t cb[4] = {nonce[0], nonce[1], nonce[2], q <= 0 ? 1u : (uint32_t)q + 1u};
         // (loading the ciphertext block ahead of the rounds, pinned by a sched_barrier, measured
         // neutral here — 410 GB/s either way — unlike ChaCha20-Poly1305, where it gained 20%)
-        aes_encrypt(rk, nr, cb, te_lds);
+        if (!cached)
+            aes_encrypt(rk, nr, cb, te_lds);
+        else if (nr == 10)
+            aes_ctr_cached<10>(rk, cc, cb[3], cb, te_lds);
+        else
+            aes_ctr_cached<14>(rk, cc, cb[3], cb, te_lds);
         if (q == 0) {
             x = aad;
             ej0[0] = cb[0], ej0[1] = cb[1], ej0[2] = cb[2], ej0[3] = cb[3];
@@ -697,7 +790,7 @@ __device__ Lanes gcm_lanes(const KeySched* __restrict__ ks, const uint32_t* te, 
             x = U128{(uint64_t)alen * 8, (uint64_t)clen * 8};
         }
 #if TLS_GHASH8
-        acc = j == 0 ? x : gf_xor(gf_mul_tab8(acc, t8), x);  // Horner, multiplier H^64
+        acc = j == 0 ? x : gf_xor(gf_mul_tab8(acc, t8, red8), x);  // Horner, multiplier H^64
 #else
         acc = j == 0 ? x : gf_xor(gf_mul_tab(acc, tabs[6]), x);  // Horner, multiplier H^64
 #endif
@@ -1063,8 +1156,10 @@ __device__ inline void load_tables(const KeySched* ks, U128 (*tabs)[16]) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+template <uint32_t COPIES = TLS_TE_COPIES>
 __device__ inline void fill_te(const uint32_t* te0, uint32_t* te) {
-    for (uint32_t i = threadIdx.x; i < 256 * TLS_TE_COPIES; i += blockDim.x) te[i] = te0[i >> kTeShift];
+    constexpr uint32_t sh = COPIES == 32 ? 5 : COPIES == 16 ? 4 : 3;
+    for (uint32_t i = threadIdx.x; i < 256 * COPIES; i += blockDim.x) te[i] = te0[i >> sh];
     __syncthreads();
 }
 
@@ -1383,10 +1478,17 @@ __device__ void aes_open_packed(const TlsArgs& a, uint32_t r0, const uint32_t* t
     U128 acc{0, 0};
     uint32_t ej0[4] = {0, 0, 0, 0};
     LastNz nz{0, {0, 0, 0, 0}};
+    // rounds 1-2 of the record's counter blocks cached (packed records are far below 2^16 blocks)
+    const CtrCache cc = ctr_cache(s_rk[k], nonce, te_lds);
     for (uint32_t j = 0; j < J; ++j) {
         const int32_t q = (int32_t)(SEG * j + u) - (int32_t)pad;
         uint32_t cb[4] = {nonce[0], nonce[1], nonce[2], q <= 0 ? 1u : (uint32_t)q + 1u};
-        if (j < Jr) aes_encrypt(s_rk[k], nr, cb, te_lds);  // (segments with fewer rounds idle)
+        if (j < Jr) {  // (segments with fewer rounds idle)
+            if (nr == 10)
+                aes_ctr_cached<10>(s_rk[k], cc, cb[3], cb, te_lds);
+            else
+                aes_ctr_cached<14>(s_rk[k], cc, cb[3], cb, te_lds);
+        }
         if (j >= Jr) continue;
         U128 x{0, 0};
         if (q == 0) {
@@ -1461,7 +1563,7 @@ __device__ inline void open_status(const TlsArgs& a, uint32_t r, const CryptOut&
 }
 
 __global__ CRYPT_ATTR void k_tls_open(TlsArgs a) {
-    __shared__ uint32_t te[256 * TLS_TE_COPIES];
+    __shared__ uint32_t te[256 * TLS_TE_COPIES_REC];
     __shared__ U128 tabs[kCryptWaves][7][16];
 #if TLS_GHASH8
     __shared__ U128 t8s[kCryptWaves][256];
@@ -1472,8 +1574,10 @@ __global__ CRYPT_ATTR void k_tls_open(TlsArgs a) {
 #if TLS_WG_TREE
     __shared__ U128 s_acc[kCryptWaves][64];
 #endif
+    __shared__ uint32_t red8[256];
     if (!(a.n_total[2] & 32u)) return;  // no AES-GCM record too long to pack
-    fill_te(a.te0, te);
+    fill_red8(red8);
+    fill_te<TLS_TE_COPIES_REC>(a.te0, te);
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t n = a.n_total[0];
     uint32_t cur = 0xFFFFFFFFu, cur8 = 0xFFFFFFFFu;  // key slots of the wave's 4-bit / 8-bit tables
@@ -1537,7 +1641,7 @@ __global__ CRYPT_ATTR void k_tls_open(TlsArgs a) {
                 ct = rec + 13;
             }
             const uint32_t wlen = is13 ? (clen > 0 ? clen - 1 : 0) : clen;
-            L = gcm_lanes<false>(ks, te, lane & (TLS_TE_COPIES - 1), tabs[wave], t8, nonce, aad,
+            L = gcm_lanes<false>(ks, te, lane & (TLS_TE_COPIES_REC - 1), tabs[wave], t8, red8, nonce, aad,
                                  alen, ct, nullptr, clen, a.out + w.spec_off, wlen, nullptr, 0, 0,
                                  is13);
         }
@@ -1641,7 +1745,7 @@ __device__ inline bool seal_prep(const SealArgs& a, uint32_t r, uint32_t cipher,
 }
 
 __global__ CRYPT_ATTR void k_tls_seal(SealArgs a) {
-    __shared__ uint32_t te[256 * TLS_TE_COPIES];
+    __shared__ uint32_t te[256 * TLS_TE_COPIES_REC];
     __shared__ U128 tabs[kCryptWaves][7][16];
 #if TLS_GHASH8
     __shared__ U128 t8s[kCryptWaves][256];
@@ -1652,7 +1756,9 @@ __global__ CRYPT_ATTR void k_tls_seal(SealArgs a) {
 #if TLS_WG_TREE
     __shared__ U128 s_acc[kCryptWaves][64];
 #endif
-    fill_te(a.te0, te);
+    __shared__ uint32_t red8[256];
+    fill_red8(red8);
+    fill_te<TLS_TE_COPIES_REC>(a.te0, te);
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t cur = 0xFFFFFFFFu, cur8 = 0xFFFFFFFFu;  // key slots of the wave's 4-bit / 8-bit tables
     for (uint32_t rb = blockIdx.x * kCryptWaves; rb < a.n; rb += gridDim.x * kCryptWaves) {
@@ -1699,7 +1805,7 @@ __global__ CRYPT_ATTR void k_tls_seal(SealArgs a) {
             } else if (!is13 && lane < 13) {
                 rec[lane] = (uint8_t)(sr.seq >> (8 * (12 - lane)));
             }
-            L = gcm_lanes<true>(ks, te, lane & (TLS_TE_COPIES - 1), tabs[wave], t8, nonce, aad,
+            L = gcm_lanes<true>(ks, te, lane & (TLS_TE_COPIES_REC - 1), tabs[wave], t8, red8, nonce, aad,
                                 alen, nullptr, ct, clen, nullptr, 0, a.src + sr.src_off,
                                 sr.plain_len, sr.type, is13);
         }
