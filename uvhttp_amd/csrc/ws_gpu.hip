@@ -1743,16 +1743,15 @@ __device__ inline void walk_wave(const WalkArgs& w, uint32_t s, uint8_t* ring) {
     const uint64_t first = MODE == 1 ? w.results[s].first_frame : slice_base(st, s);
     uint64_t cur = ~0ull;  // block of the current header; LDS holds cur and cur + 1
     u32x4 pf[kWalkVec];    // block cur + 2, in flight
-    uint32_t batch = 0;    // lane j holds start (first + 64 m + j) of the current batch m
-    auto emit = [&](uint64_t pos, uint32_t idx) {
-        if (MODE == 0) return;
-        if (lane == (idx & 63)) batch = (uint32_t)pos;
-        if ((idx & 63) == 63) {  // a full batch: one coalesced store
-            const uint64_t f = first + (idx & ~63u) + lane;
-            if (MODE == 2) w.sc.walk_tmp[f] = batch;
-            else if (f < w.max_frames) w.sc.frame_off[f] = st.begin + batch;
-        }
+    // frame start records: one lane per frame (the fast path below stores a run of frames, one
+    // per lane, in one instruction)
+    auto emit_lane = [&](uint64_t pos, uint32_t idx, bool on) {
+        if (MODE == 0 || !on) return;
+        const uint64_t f = first + idx;
+        if (MODE == 2) w.sc.walk_tmp[f] = (uint32_t)pos;
+        else if (f < w.max_frames) w.sc.frame_off[f] = st.begin + pos;
     };
+    auto emit = [&](uint64_t pos, uint32_t idx) { emit_lane(pos, idx, lane == 0); };
     const ConnState c = walk_calls(
         w, st,
         [&](uint64_t pos, uint32_t hb[10]) {
@@ -1778,55 +1777,103 @@ __device__ inline void walk_wave(const WalkArgs& w, uint32_t s, uint8_t* ring) {
         },
         [&](uint64_t pos, uint32_t idx) { emit(pos, idx); },
         [&](ConnState& c) {
-            // The hot loop: frames decided from the ring alone — header in the current ring
-            // block, at least ten bytes of the current call left, complete in this call,
-            // valid, accepted by the fragment state machine.  Vector arithmetic on every lane
-            // (identical values) keeps the shared scalar unit free; only the exit tests are
-            // made uniform (readfirstlane).  Anything else leaves for the general code.
+            // The hot loop, on runs of equal frames.  Frame 0 of a step is the one at pos;
+            // lane l speculates that frames 0 .. l-1 have frame 0's wire length, parses the
+            // header at pos + l * wl0 from the ring and checks it: same first byte (opcode and
+            // flags) and the same length as frame 0, in the ring window, complete in the
+            // current call, valid, and accepted by the fragment state machine given the run
+            // before it.  The leading accepted lanes (a ballot) are all decided at once: a run
+            // of 264-byte frames advances up to ~30 frames per step instead of one.  Runs that
+            // the state machine cannot take whole — a message start without FIN, a final
+            // fragment — stop after their first frame; anything else leaves for the general
+            // code.  All lanes compute with vector registers; the step's outcome is made
+            // uniform by readfirstlane.
             if (cur == ~0ull || c.grow_fail) return;
             const uint64_t cur_rel = cur - st.begin / kWalkBlk;  // ring block, stream-relative
             const uint32_t off0 = (uint32_t)(st.begin % kWalkBlk), par0 = (uint32_t)((st.begin / kWalkBlk) & 1);
             const uint32_t end32 = (uint32_t)c.end;
+            // stream offset where the ring's second block ends
+            const uint64_t win_end64 = (cur_rel + 2) * kWalkBlk - off0;
+            const uint32_t win_end = win_end64 < end32 ? (uint32_t)win_end64 : end32;
             const uint64_t mf = (uint64_t)(int64_t)st.max_frame_size;
             const uint64_t lim = (uint64_t)(int64_t)st.max_message_size;
             uint32_t pos = (uint32_t)c.pos, pend = c.pending;
             uint64_t acc = c.acc;
             uint32_t cnt = c.count;
-            for (;;) {
-                const uint32_t off = off0 + pos;
-                if (__builtin_amdgcn_readfirstlane((uint32_t)((off / kWalkBlk) != cur_rel) | (uint32_t)(end32 - pos < 10)))
-                    break;
+            auto parse = [&](uint32_t p, uint32_t& b0, uint32_t& wl, uint64_t& plen, bool& bad) {
+                const uint32_t off = off0 + p;
                 const uint32_t r = (((par0 + off / kWalkBlk) & 1) * kWalkBlk) + off % kWalkBlk;
                 uint32_t hb[10];
 #pragma unroll
                 for (int q = 0; q < 10; ++q) hb[q] = ring[r + q];
-                const uint32_t b0 = hb[0], b1 = hb[1], code = b1 & 0x7F;
+                b0 = hb[0];
+                const uint32_t b1 = hb[1], code = b1 & 0x7F;
                 const uint32_t need = code < 126 ? 2u : code == 126 ? 4u : 10u;
-                uint64_t plen = code;
+                plen = code;
                 if (code == 126) plen = (hb[2] << 8) | hb[3];
                 if (code == 127)
                     plen = ((uint64_t)((hb[2] << 24) | (hb[3] << 16) | (hb[4] << 8) | hb[5]) << 32) |
                            (uint32_t)((hb[6] << 24) | (hb[7] << 16) | (hb[8] << 8) | hb[9]);
                 const uint32_t op = b0 & 0x0F, fin = b0 >> 7, m = b1 >> 7;
-                const bool bad = (b0 & 0x70) || (op >= 8 && (plen > 125 || !fin)) ||
-                                 (st.is_server && !m) || plen > mf;  // (plen <= mf < 2^31)
-                const uint64_t wl = need + 4u * m + plen;
-                const bool data = op <= 2;
-                const bool smf = data && (pend ? (op != 0 || (lim != 0 && (acc > lim || plen > lim - acc)))
-                                               : (op == 0 || (!fin && lim != 0 && plen > lim)));
-                if (__builtin_amdgcn_readfirstlane((uint32_t)(bad || wl > end32 - pos || smf))) break;
-                emit(pos, cnt);
-                if (data) {
+                bad = (b0 & 0x70) || (op >= 8 && (plen > 125 || !fin)) || (st.is_server && !m) ||
+                      plen > mf || (plen >> 31);  // (a length of 2^31 or more: general code)
+                wl = need + 4u * m + (uint32_t)plen;
+            };
+            uint32_t wlp = 0;  // wire length of the previous step's frames: lane l parses the
+                               // header at pos + l * wlp (lane 0: the frame at pos)
+            for (;;) {
+                const uint32_t off = off0 + pos;
+                if (__builtin_amdgcn_readfirstlane((uint32_t)((off / kWalkBlk) != cur_rel) | (uint32_t)(end32 - pos < 10)))
+                    break;
+                const uint64_t pl = (uint64_t)pos + (uint64_t)lane * wlp;
+                uint32_t b0l, wll;
+                uint64_t plenl;
+                bool badl;
+                parse((uint32_t)pl, b0l, wll, plenl, badl);  // (any position reads inside the ring)
+                // frame 0 = lane 0's header
+                const uint32_t b00 = __builtin_amdgcn_readfirstlane(b0l), wl0 = __builtin_amdgcn_readfirstlane(wll);
+                const uint64_t plen0 = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(plenl >> 32)) << 32) |
+                                       __builtin_amdgcn_readfirstlane((uint32_t)plenl);
+                const bool bad0 = __builtin_amdgcn_readfirstlane((uint32_t)badl) != 0;
+                const uint32_t op0 = b00 & 0x0F, fin0 = b00 >> 7;
+                const bool data0 = op0 <= 2;
+                const bool smf0 = data0 && (pend ? (op0 != 0 || (lim != 0 && (acc > lim || plen0 > lim - acc)))
+                                                 : (op0 == 0 || (!fin0 && lim != 0 && plen0 > lim)));
+                if (bad0 || wl0 > end32 - pos || smf0) break;
+                // runs: control frames, complete messages (op 1/2 + FIN, nothing open), and
+                // middle fragments (CONTINUATION without FIN, a message open)
+                const uint32_t kind = !data0 ? 0u : (op0 != 0 && fin0) ? 1u : (op0 == 0 && !fin0) ? 2u : 3u;
+                uint32_t n = 1;
+                if (kind != 3 && wl0 == wlp) {
+                    // lane l's header: inside the ring window (one starting in the second ring
+                    // block must not leave it), complete in the call, the same first byte and
+                    // length as frame 0, valid, and (middle fragments) within max_message_size
+                    const uint32_t offl = off0 + (uint32_t)pl;
+                    const bool in_ring = pl + 10 <= win_end &&
+                                         ((offl / kWalkBlk) == cur_rel ||
+                                          ((offl / kWalkBlk) == cur_rel + 1 && offl % kWalkBlk + 10 <= kWalkBlk));
+                    bool okl = lane == 0 ||
+                               (in_ring && pl + wl0 <= end32 && !badl && b0l == b00 && wll == wl0 && plenl == plen0 &&
+                                (kind != 2 || lim == 0 || acc + (uint64_t)(lane + 1) * plen0 <= lim));
+                    const uint64_t good = __ballot(okl);
+                    n = ~good == 0 ? 64u : (uint32_t)__builtin_ctzll(~good);  // leading accepted frames
+                    n = __builtin_amdgcn_readfirstlane(n);
+                }
+                emit_lane((uint64_t)pos + (uint64_t)lane * wl0, cnt + lane, lane < n);
+                if (kind == 2) {
+                    acc += (uint64_t)n * plen0;
+                } else if (kind == 3) {  // one frame: a start without FIN or a final fragment
                     if (pend) {
-                        acc = fin ? 0 : acc + plen;
-                        pend = fin ? 0u : 1u;
-                    } else if (!fin && plen) {
+                        acc = 0;
+                        pend = 0;
+                    } else if (plen0) {
                         pend = 1;
-                        acc = plen;
+                        acc = plen0;
                     }
                 }
-                pos += (uint32_t)wl;
-                ++cnt;
+                pos += n * wl0;
+                cnt += n;
+                wlp = wl0;
             }
             c.pos = __builtin_amdgcn_readfirstlane(pos);
             c.pending = __builtin_amdgcn_readfirstlane(pend);
@@ -1834,13 +1881,6 @@ __device__ inline void walk_wave(const WalkArgs& w, uint32_t s, uint8_t* ring) {
                     __builtin_amdgcn_readfirstlane((uint32_t)acc);
             c.count = cnt;
         });
-    if (MODE != 0 && (c.count & 63)) {  // the last, partial batch
-        const uint64_t f = first + (c.count & ~63u) + lane;
-        if (lane < (c.count & 63)) {
-            if (MODE == 2) w.sc.walk_tmp[f] = batch;
-            else if (f < w.max_frames) w.sc.frame_off[f] = st.begin + batch;
-        }
-    }
     if (MODE == 1 || lane != 0) return;
     w.results[s] = walk_result(w, st, c);
 }
@@ -3207,10 +3247,14 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     for (uint64_t tb = 0; tb < n_ptiles; tb += max_tiles) {
         const uint32_t grid_p = (uint32_t)((n_ptiles - tb) < max_tiles ? (n_ptiles - tb) : max_tiles);
 #define UVWS_LAUNCH(B, V)                                                                        \
-    if (blk == B && vpt == V)                                                                    \
-        hipLaunchKernelGGL((k_unmask_inplace<B, V>), dim3(grid_p), dim3(B), 0, s, a, d_desc,     \
-                           e->ws, tb);                                                           \
-    else
+    if (blk == B && vpt == V) {                                                                  \
+        if (e->store_aux == 18)                                                                  \
+            hipLaunchKernelGGL((k_unmask_inplace<B, V, 18>), dim3(grid_p), dim3(B), 0, s, a,     \
+                               d_desc, e->ws, tb);                                               \
+        else                                                                                     \
+            hipLaunchKernelGGL((k_unmask_inplace<B, V>), dim3(grid_p), dim3(B), 0, s, a, d_desc, \
+                               e->ws, tb);                                                       \
+    } else
         UVWS_LAUNCH(64, 1) UVWS_LAUNCH(64, 2) UVWS_LAUNCH(64, 4) UVWS_LAUNCH(128, 1)
         UVWS_LAUNCH(128, 2) UVWS_LAUNCH(256, 1) UVWS_LAUNCH(256, 2) UVWS_LAUNCH(256, 4) {}
 #undef UVWS_LAUNCH
