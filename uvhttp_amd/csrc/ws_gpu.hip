@@ -1789,12 +1789,15 @@ __device__ inline void walk_wave(const WalkArgs& w, uint32_t s, uint8_t* ring) {
             // code.  All lanes compute with vector registers; the step's outcome is made
             // uniform by readfirstlane.
             if (cur == ~0ull || c.grow_fail) return;
-            const uint64_t cur_rel = cur - st.begin / kWalkBlk;  // ring block, stream-relative
+            uint64_t cur_rel = cur - st.begin / kWalkBlk;  // ring block, stream-relative
             const uint32_t off0 = (uint32_t)(st.begin % kWalkBlk), par0 = (uint32_t)((st.begin / kWalkBlk) & 1);
             const uint32_t end32 = (uint32_t)c.end;
             // stream offset where the ring's second block ends
-            const uint64_t win_end64 = (cur_rel + 2) * kWalkBlk - off0;
-            const uint32_t win_end = win_end64 < end32 ? (uint32_t)win_end64 : end32;
+            auto window_end = [&]() {
+                const uint64_t e = (cur_rel + 2) * kWalkBlk - off0;
+                return e < end32 ? (uint32_t)e : end32;
+            };
+            uint32_t win_end = window_end();
             const uint64_t mf = (uint64_t)(int64_t)st.max_frame_size;
             const uint64_t lim = (uint64_t)(int64_t)st.max_message_size;
             uint32_t pos = (uint32_t)c.pos, pend = c.pending;
@@ -1823,6 +1826,17 @@ __device__ inline void walk_wave(const WalkArgs& w, uint32_t s, uint8_t* ring) {
                                // header at pos + l * wlp (lane 0: the frame at pos)
             for (;;) {
                 const uint32_t off = off0 + pos;
+                if (off / kWalkBlk == cur_rel + 1 && end32 - pos >= 10) {
+                    // the header moved into the ring's second block: advance the ring here (the
+                    // prefetched block joins it, the one after is requested) instead of leaving
+                    // for the general code
+                    walk_store_block(ring, cur + 2, pf);
+                    walk_load_block(w, cur + 3, pf);
+                    ++cur;
+                    ++cur_rel;
+                    win_end = window_end();
+                    wave_sync_lds();
+                }
                 if (__builtin_amdgcn_readfirstlane((uint32_t)((off / kWalkBlk) != cur_rel) | (uint32_t)(end32 - pos < 10)))
                     break;
                 const uint64_t pl = (uint64_t)pos + (uint64_t)lane * wlp;
@@ -1907,10 +1921,14 @@ __global__ __launch_bounds__(kBlock) void k_swalk_scan(WalkArgs w, uint32_t lane
     const uint32_t beg = threadIdx.x * per;
     const uint32_t fin = beg + per < m ? beg + per : m;
     auto count_of = [&](uint32_t j) { return lane_mode ? w.agg[j] : w.results[j].n_frames; };
+    // (unrolled by 8 so each thread's loads are in flight together: a chunk of 16 results read
+    // one after another cost ~12 us at 4096 connections)
     uint64_t run = 0;
+#pragma unroll 8
     for (uint32_t j = beg; j < fin; ++j) run += count_of(j);
     uint64_t total;
     uint64_t pre = block_exclusive_sum_u64(run, &total);
+#pragma unroll 8
     for (uint32_t j = beg; j < fin; ++j) {
         const uint32_t v = count_of(j);
         if (lane_mode) w.agg[j] = (uint32_t)pre;
@@ -1923,9 +1941,8 @@ __global__ __launch_bounds__(kBlock) void k_swalk_scan(WalkArgs w, uint32_t lane
 // frame k of connection s (frame start `pos`, stream-relative): its descriptor and end
 __device__ inline void stream_frame_desc(const WalkArgs& w, const uvhttp_ws_stream_t& st,
                                          const uvhttp_ws_stream_result_t& r, uint32_t k,
-                                         uint64_t pos, uvhttp_ws_frame_desc_t& d, bool& fin_data,
-                                         uint64_t& fe) {
-    const u32x4 hv = load16_at(w.wire, w.wire_len, st.begin + pos);
+                                         uint64_t pos, const u32x4& hv, uvhttp_ws_frame_desc_t& d,
+                                         bool& fin_data, uint64_t& fe) {
     const uint64_t hlo = hv.x | ((uint64_t)hv.y << 32), hhi = hv.z | ((uint64_t)hv.w << 32);
     auto hb = [&](int q) -> uint32_t {
         return (uint32_t)((q < 8 ? hlo >> (8 * q) : hhi >> (8 * (q - 8))) & 0xFF);
@@ -1996,7 +2013,7 @@ __global__ __launch_bounds__(kBlock) void k_stream_desc_lane(WalkArgs w) {
         uvhttp_ws_frame_desc_t d;
         bool fin_data;
         uint64_t fe;
-        stream_frame_desc(w, st, r, k, pos, d, fin_data, fe);
+        stream_frame_desc(w, st, r, k, pos, load16_at(w.wire, w.wire_len, st.begin + pos), d, fin_data, fe);
         if (d.status == UVHTTP_WS_FRAME_OK && d.opcode <= 2) d.message = msg;
         msg += fin_data ? 1u : 0u;
         w.desc[first + k] = d;
@@ -2025,25 +2042,41 @@ __global__ __launch_bounds__(kBlock) void k_stream_desc(WalkArgs w) {
     const uvhttp_ws_stream_t st = w.streams[s];
     const uint64_t sb = slice_base(st, s);
     uint32_t msg = 0;  // FIN data frames delivered before this chunk
-    for (uint32_t k0 = 0; k0 < r.n_frames; k0 += 64) {
-        const uint32_t k = k0 + lane;
-        const bool act = k < r.n_frames;
-        uvhttp_ws_frame_desc_t d;
-        bool fin_data = false;
-        if (act) {
-            const uint64_t pos = w.single ? w.sc.walk_tmp[sb + k] : w.sc.frame_off[r.first_frame + k] - st.begin;
-            uint64_t fe;
-            stream_frame_desc(w, st, r, k, pos, d, fin_data, fe);
-            w.sc.frame_off[r.first_frame + k] = fe;  // (this lane read its own entry above)
+    // groups of four 64-frame chunks: every start and header load of a group is issued before
+    // any is used (one chunk at a time cost two dependent round trips per 64 frames)
+    constexpr int kG = 4;
+    for (uint32_t g0 = 0; g0 < r.n_frames; g0 += 64 * kG) {
+        uint64_t pos[kG];
+        u32x4 hv[kG];
+#pragma unroll
+        for (int c = 0; c < kG; ++c) {
+            const uint32_t k = g0 + 64 * c + lane;
+            const bool act = k < r.n_frames;
+            pos[c] = !act ? 0 : w.single ? w.sc.walk_tmp[sb + k] : w.sc.frame_off[r.first_frame + k] - st.begin;
         }
-        // message id: FIN data frames delivered before this one in the connection
-        const uint64_t fm = __ballot(fin_data);
-        const uint32_t before = msg + (uint32_t)__builtin_popcountll(fm & ((1ull << lane) - 1));
-        if (act) {
-            if (d.status == UVHTTP_WS_FRAME_OK && d.opcode <= 2) d.message = before;
-            w.desc[r.first_frame + k] = d;
+#pragma unroll
+        for (int c = 0; c < kG; ++c) hv[c] = load16_at(w.wire, w.wire_len, st.begin + pos[c]);
+#pragma unroll
+        for (int c = 0; c < kG; ++c) {
+            if (g0 + 64 * c >= r.n_frames) break;  // (uniform)
+            const uint32_t k = g0 + 64 * c + lane;
+            const bool act = k < r.n_frames;
+            uvhttp_ws_frame_desc_t d;
+            bool fin_data = false;
+            if (act) {
+                uint64_t fe;
+                stream_frame_desc(w, st, r, k, pos[c], hv[c], d, fin_data, fe);
+                w.sc.frame_off[r.first_frame + k] = fe;  // (this lane read its own entry above)
+            }
+            // message id: FIN data frames delivered before this one in the connection
+            const uint64_t fm = __ballot(fin_data);
+            const uint32_t before = msg + (uint32_t)__builtin_popcountll(fm & ((1ull << lane) - 1));
+            if (act) {
+                if (d.status == UVHTTP_WS_FRAME_OK && d.opcode <= 2) d.message = before;
+                w.desc[r.first_frame + k] = d;
+            }
+            msg += (uint32_t)__builtin_popcountll(fm);
         }
-        msg += (uint32_t)__builtin_popcountll(fm);
     }
 }
 
