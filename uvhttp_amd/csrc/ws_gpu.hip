@@ -1737,10 +1737,14 @@ __device__ inline void walk_wave(const WalkArgs& w, uint32_t s, uint8_t* ring) {
     const uvhttp_ws_stream_t st = w.streams[s];
     const bool ok = __all(stream_ok_part(w, s, st, lane, 64));
     if (!ok) {
-        if (MODE != 1 && lane == 0) w.results[s] = layout_result(st);
+        if (MODE != 1 && lane == 0) {
+            w.results[s] = layout_result(st);
+            w.agg[s] = 0;
+        }
         return;
     }
-    const uint64_t first = MODE == 1 ? w.results[s].first_frame : slice_base(st, s);
+    // (wave mode: agg[s] holds the connection's frame count for k_swalk_scan, then its first)
+    const uint64_t first = MODE == 1 ? w.agg[s] : slice_base(st, s);
     uint64_t cur = ~0ull;  // block of the current header; LDS holds cur and cur + 1
     u32x4 pf[kWalkVec];    // block cur + 2, in flight
     // frame start records: one lane per frame (the fast path below stores a run of frames, one
@@ -1777,38 +1781,30 @@ __device__ inline void walk_wave(const WalkArgs& w, uint32_t s, uint8_t* ring) {
         },
         [&](uint64_t pos, uint32_t idx) { emit(pos, idx); },
         [&](ConnState& c) {
-            // The hot loop, on runs of equal frames.  Frame 0 of a step is the one at pos;
-            // lane l speculates that frames 0 .. l-1 have frame 0's wire length, parses the
-            // header at pos + l * wl0 from the ring and checks it: same first byte (opcode and
-            // flags) and the same length as frame 0, in the ring window, complete in the
+            // The hot loop, on runs of equal frames.  Frame 0 of a step is the one at pos (its
+            // header from the LDS ring, or carried from the step before).  When frame 0 has the
+            // previous frame's wire length wl0, lane l speculates that frames 0 .. l-1 all have
+            // it and loads the header at pos + l * wl0 straight from global memory (one 32-byte
+            // window per lane — the payload bytes between headers are never fetched), then
+            // checks it: same first byte (opcode and flags), same length, complete in the
             // current call, valid, and accepted by the fragment state machine given the run
-            // before it.  The leading accepted lanes (a ballot) are all decided at once: a run
-            // of 264-byte frames advances up to ~30 frames per step instead of one.  Runs that
-            // the state machine cannot take whole — a message start without FIN, a final
-            // fragment — stop after their first frame; anything else leaves for the general
-            // code.  All lanes compute with vector registers; the step's outcome is made
-            // uniform by readfirstlane.
+            // before it.  The leading accepted lanes (a ballot) are decided at once — up to 64
+            // frames per step — and the first rejected lane's header becomes the next step's
+            // frame 0.  Runs the state machine cannot take whole (a message start without FIN,
+            // a final fragment) stop after their first frame; anything else leaves for the
+            // general code.  All lanes compute with vector registers; each step's outcome is
+            // made uniform by readfirstlane.
             if (cur == ~0ull || c.grow_fail) return;
             uint64_t cur_rel = cur - st.begin / kWalkBlk;  // ring block, stream-relative
             const uint32_t off0 = (uint32_t)(st.begin % kWalkBlk), par0 = (uint32_t)((st.begin / kWalkBlk) & 1);
             const uint32_t end32 = (uint32_t)c.end;
-            // stream offset where the ring's second block ends
-            auto window_end = [&]() {
-                const uint64_t e = (cur_rel + 2) * kWalkBlk - off0;
-                return e < end32 ? (uint32_t)e : end32;
-            };
-            uint32_t win_end = window_end();
             const uint64_t mf = (uint64_t)(int64_t)st.max_frame_size;
             const uint64_t lim = (uint64_t)(int64_t)st.max_message_size;
             uint32_t pos = (uint32_t)c.pos, pend = c.pending;
             uint64_t acc = c.acc;
             uint32_t cnt = c.count;
-            auto parse = [&](uint32_t p, uint32_t& b0, uint32_t& wl, uint64_t& plen, bool& bad) {
-                const uint32_t off = off0 + p;
-                const uint32_t r = (((par0 + off / kWalkBlk) & 1) * kWalkBlk) + off % kWalkBlk;
-                uint32_t hb[10];
-#pragma unroll
-                for (int q = 0; q < 10; ++q) hb[q] = ring[r + q];
+            // header fields from ten bytes hb[0..9]
+            auto decode = [&](const uint32_t* hb, uint32_t& b0, uint32_t& wl, uint64_t& plen, bool& bad) {
                 b0 = hb[0];
                 const uint32_t b1 = hb[1], code = b1 & 0x7F;
                 const uint32_t need = code < 126 ? 2u : code == 126 ? 4u : 10u;
@@ -1822,33 +1818,53 @@ __device__ inline void walk_wave(const WalkArgs& w, uint32_t s, uint8_t* ring) {
                       plen > mf || (plen >> 31);  // (a length of 2^31 or more: general code)
                 wl = need + 4u * m + (uint32_t)plen;
             };
-            uint32_t wlp = 0;  // wire length of the previous step's frames: lane l parses the
-                               // header at pos + l * wlp (lane 0: the frame at pos)
+            auto parse_ring = [&](uint32_t p, uint32_t& b0, uint32_t& wl, uint64_t& plen, bool& bad) {
+                const uint32_t off = off0 + p;
+                const uint32_t r = (((par0 + off / kWalkBlk) & 1) * kWalkBlk) + off % kWalkBlk;
+                uint32_t hb[10];
+#pragma unroll
+                for (int q = 0; q < 10; ++q) hb[q] = ring[r + q];
+                decode(hb, b0, wl, plen, bad);
+            };
+            auto parse_global = [&](uint64_t p, uint32_t& b0, uint32_t& wl, uint64_t& plen, bool& bad) {
+                const u32x4 v = load16_at(w.wire, w.wire_len, st.begin + p);
+                const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+                uint32_t hb[10];
+#pragma unroll
+                for (int q = 0; q < 10; ++q) hb[q] = (x[q >> 2] >> (8 * (q & 3))) & 0xFF;
+                decode(hb, b0, wl, plen, bad);
+            };
+            uint32_t wlp = 0;          // the previous step's frame length
+            bool have0 = false;        // frame 0's header carried from the previous step
+            uint32_t cb0 = 0, cwl = 0;  // (its fields)
+            uint64_t cplen = 0;
+            bool cbad = false;
             for (;;) {
-                const uint32_t off = off0 + pos;
-                if (off / kWalkBlk == cur_rel + 1 && end32 - pos >= 10) {
-                    // the header moved into the ring's second block: advance the ring here (the
-                    // prefetched block joins it, the one after is requested) instead of leaving
-                    // for the general code
-                    walk_store_block(ring, cur + 2, pf);
-                    walk_load_block(w, cur + 3, pf);
-                    ++cur;
-                    ++cur_rel;
-                    win_end = window_end();
-                    wave_sync_lds();
+                if (end32 - pos < 10) break;  // (uniform)
+                uint32_t b00, wl0;
+                uint64_t plen0;
+                bool bad0;
+                if (have0) {
+                    b00 = cb0, wl0 = cwl, plen0 = cplen, bad0 = cbad;
+                } else {
+                    // frame 0 from the ring: header in the ring's current block (or, after a
+                    // run, in the next one: the ring advances here), else the general code
+                    const uint32_t off = off0 + pos;
+                    if (off / kWalkBlk == cur_rel + 1) {
+                        walk_store_block(ring, cur + 2, pf);
+                        walk_load_block(w, cur + 3, pf);
+                        ++cur;
+                        ++cur_rel;
+                        wave_sync_lds();
+                    }
+                    if (off / kWalkBlk != cur_rel) break;  // (uniform)
+                    parse_ring(pos, b00, wl0, plen0, bad0);
+                    b00 = __builtin_amdgcn_readfirstlane(b00);
+                    wl0 = __builtin_amdgcn_readfirstlane(wl0);
+                    plen0 = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(plen0 >> 32)) << 32) |
+                            __builtin_amdgcn_readfirstlane((uint32_t)plen0);
+                    bad0 = __builtin_amdgcn_readfirstlane((uint32_t)bad0) != 0;
                 }
-                if (__builtin_amdgcn_readfirstlane((uint32_t)((off / kWalkBlk) != cur_rel) | (uint32_t)(end32 - pos < 10)))
-                    break;
-                const uint64_t pl = (uint64_t)pos + (uint64_t)lane * wlp;
-                uint32_t b0l, wll;
-                uint64_t plenl;
-                bool badl;
-                parse((uint32_t)pl, b0l, wll, plenl, badl);  // (any position reads inside the ring)
-                // frame 0 = lane 0's header
-                const uint32_t b00 = __builtin_amdgcn_readfirstlane(b0l), wl0 = __builtin_amdgcn_readfirstlane(wll);
-                const uint64_t plen0 = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(plenl >> 32)) << 32) |
-                                       __builtin_amdgcn_readfirstlane((uint32_t)plenl);
-                const bool bad0 = __builtin_amdgcn_readfirstlane((uint32_t)badl) != 0;
                 const uint32_t op0 = b00 & 0x0F, fin0 = b00 >> 7;
                 const bool data0 = op0 <= 2;
                 const bool smf0 = data0 && (pend ? (op0 != 0 || (lim != 0 && (acc > lim || plen0 > lim - acc)))
@@ -1858,20 +1874,34 @@ __device__ inline void walk_wave(const WalkArgs& w, uint32_t s, uint8_t* ring) {
                 // middle fragments (CONTINUATION without FIN, a message open)
                 const uint32_t kind = !data0 ? 0u : (op0 != 0 && fin0) ? 1u : (op0 == 0 && !fin0) ? 2u : 3u;
                 uint32_t n = 1;
+                have0 = false;
                 if (kind != 3 && wl0 == wlp) {
-                    // lane l's header: inside the ring window (one starting in the second ring
-                    // block must not leave it), complete in the call, the same first byte and
-                    // length as frame 0, valid, and (middle fragments) within max_message_size
-                    const uint32_t offl = off0 + (uint32_t)pl;
-                    const bool in_ring = pl + 10 <= win_end &&
-                                         ((offl / kWalkBlk) == cur_rel ||
-                                          ((offl / kWalkBlk) == cur_rel + 1 && offl % kWalkBlk + 10 <= kWalkBlk));
-                    bool okl = lane == 0 ||
-                               (in_ring && pl + wl0 <= end32 && !badl && b0l == b00 && wll == wl0 && plenl == plen0 &&
-                                (kind != 2 || lim == 0 || acc + (uint64_t)(lane + 1) * plen0 <= lim));
+                    const uint64_t pl = (uint64_t)pos + (uint64_t)lane * wl0;  // frame `lane`
+                    uint32_t b0l = 0, wll = 0;
+                    uint64_t plenl = 0;
+                    bool badl = true;
+                    const bool hdr_in = lane > 0 && pl + 10 <= end32;
+                    if (hdr_in) parse_global(pl, b0l, wll, plenl, badl);
+                    const bool okl = lane == 0 ||
+                                     (hdr_in && pl + wl0 <= end32 && !badl && b0l == b00 && wll == wl0 &&
+                                      plenl == plen0 &&
+                                      (kind != 2 || lim == 0 || acc + (uint64_t)(lane + 1) * plen0 <= lim));
                     const uint64_t good = __ballot(okl);
                     n = ~good == 0 ? 64u : (uint32_t)__builtin_ctzll(~good);  // leading accepted frames
                     n = __builtin_amdgcn_readfirstlane(n);
+                    // frame n (the first not taken) is the next step's frame 0 when its header
+                    // was read
+                    if (n < 64) {
+                        const uint32_t hin = __builtin_amdgcn_readlane((uint32_t)hdr_in, n);
+                        if (hin) {
+                            have0 = true;
+                            cb0 = __builtin_amdgcn_readlane(b0l, n);
+                            cwl = __builtin_amdgcn_readlane(wll, n);
+                            cplen = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(plenl >> 32), n) << 32) |
+                                    __builtin_amdgcn_readlane((uint32_t)plenl, n);
+                            cbad = __builtin_amdgcn_readlane((uint32_t)badl, n) != 0;
+                        }
+                    }
                 }
                 emit_lane((uint64_t)pos + (uint64_t)lane * wl0, cnt + lane, lane < n);
                 if (kind == 2) {
@@ -1897,6 +1927,7 @@ __device__ inline void walk_wave(const WalkArgs& w, uint32_t s, uint8_t* ring) {
         });
     if (MODE == 1 || lane != 0) return;
     w.results[s] = walk_result(w, st, c);
+    w.agg[s] = c.count;
 }
 
 template <int MODE>
@@ -1920,7 +1951,7 @@ __global__ __launch_bounds__(kBlock) void k_swalk_scan(WalkArgs w, uint32_t lane
     const uint32_t per = (m + kBlock - 1) / kBlock;
     const uint32_t beg = threadIdx.x * per;
     const uint32_t fin = beg + per < m ? beg + per : m;
-    auto count_of = [&](uint32_t j) { return lane_mode ? w.agg[j] : w.results[j].n_frames; };
+    auto count_of = [&](uint32_t j) { return w.agg[j]; };  // (block counts / connection counts)
     // (unrolled by 8 so each thread's loads are in flight together: a chunk of 16 results read
     // one after another cost ~12 us at 4096 connections)
     uint64_t run = 0;
@@ -1931,8 +1962,7 @@ __global__ __launch_bounds__(kBlock) void k_swalk_scan(WalkArgs w, uint32_t lane
 #pragma unroll 8
     for (uint32_t j = beg; j < fin; ++j) {
         const uint32_t v = count_of(j);
-        if (lane_mode) w.agg[j] = (uint32_t)pre;
-        else w.results[j].first_frame = (uint32_t)pre;
+        w.agg[j] = (uint32_t)pre;
         pre += v;
     }
     if (threadIdx.x == 0) *w.sc.n_total = total <= w.max_frames ? (uint32_t)total : 0u;
@@ -2030,6 +2060,7 @@ __global__ __launch_bounds__(kBlock) void k_stream_desc(WalkArgs w) {
     const uint32_t s = blockIdx.x * (kBlock / 64) + wave;
     if (s >= w.n_streams) return;
     uvhttp_ws_stream_result_t r = w.results[s];
+    r.first_frame = w.agg[s];  // (k_swalk_scan's prefix)
     const bool fits = *w.sc.n_total != 0 || r.n_frames == 0;
     if (!fits) {
         if (lane == 0) {
@@ -2038,6 +2069,7 @@ __global__ __launch_bounds__(kBlock) void k_stream_desc(WalkArgs w) {
         }
         return;
     }
+    if (lane == 0) w.results[s].first_frame = r.first_frame;
     if (!r.n_frames) return;
     const uvhttp_ws_stream_t st = w.streams[s];
     const uint64_t sb = slice_base(st, s);
