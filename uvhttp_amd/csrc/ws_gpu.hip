@@ -3304,7 +3304,14 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     a.epoch = next_epoch(e, s);
     hipLaunchKernelGGL(k_stream_claims, dim3((cap + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a,
                        e->ws, (const uint64_t*)e->ss.frame_off);
-    int blk = e->tile_block ? e->tile_block : 256, vpt = e->tile_block ? e->tile_vpt : 2;
+    // payload tile shape: the frame count is only known on the device, so the caller's frame
+    // capacity stands in for it (wire bytes per frame slot; the same rule as the batch decode)
+    int blk = e->tile_block, vpt = e->tile_vpt;
+    if (!blk) {
+        const uint64_t avg = max_frames ? wire_len / max_frames : wire_len;
+        blk = avg >= 32768 ? 64 : 256;
+        vpt = avg >= 32768 ? 1 : avg >= 2048 ? 2 : 4;
+    }
     const uint64_t tile_bytes = (uint64_t)blk * vpt * 16;
     const uint64_t n_ptiles = (wire_len + tile_bytes - 1) / tile_bytes;
     const uint64_t max_tiles = (1ull << 24);
