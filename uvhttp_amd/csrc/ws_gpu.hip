@@ -809,13 +809,16 @@ __device__ void write_summary(const BatchArgs& a, const uvhttp_ws_frame_desc_t* 
 // k_finalize (batch mode, after the payload pass, one lane per frame): statuses after the
 // first failure become SKIPPED; a compact decode unmasks control payloads (<= 125 B) in
 // place; wave 0 of block 0 writes the batch summary
-__global__ __launch_bounds__(kBlock) void k_finalize(BatchArgs a, uvhttp_ws_frame_desc_t* desc,
-                                                     Workspace ws) {
-    resolve_epoch(a, ws);
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+// (block `blk` of a grid of `nthr`-thread blocks, one frame per thread, `a` with its epoch
+// resolved and nb = first_bad_of(a, ws, a.n); no workgroup barrier, so the in-place payload
+// kernel runs it at the end of its first blocks and the decode needs no third launch)
+__device__ inline void finalize_frames(const BatchArgs& a, uvhttp_ws_frame_desc_t* desc,
+                                       const Workspace& ws, uint32_t blk, uint32_t nthr,
+                                       uint32_t nb) {
+    const uint32_t i = blk * nthr + threadIdx.x;
     if (device_fault(a, ws)) {  // nothing was delivered (the payload pass saw first_bad = 0)
         if (i < a.n) desc[i].status = UVHTTP_WS_FRAME_SKIPPED;
-        if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (blk == 0 && threadIdx.x == 0) {
             uvhttp_ws_batch_summary_t s;
             memset(&s, 0, sizeof(s));
             s.n_frames = a.n;
@@ -825,7 +828,6 @@ __global__ __launch_bounds__(kBlock) void k_finalize(BatchArgs a, uvhttp_ws_fram
         }
         return;
     }
-    const uint32_t nb = first_bad_of(a, ws, a.n);
     if (i < a.n) {
         if (i > nb) desc[i].status = UVHTTP_WS_FRAME_SKIPPED;
         if (a.arena && i < nb) {
@@ -837,7 +839,13 @@ __global__ __launch_bounds__(kBlock) void k_finalize(BatchArgs a, uvhttp_ws_fram
             }
         }
     }
-    if (blockIdx.x == 0 && threadIdx.x < 64) write_summary(a, desc, ws, nb);
+    if (blk == 0 && threadIdx.x < 64) write_summary(a, desc, ws, nb);
+}
+
+__global__ __launch_bounds__(kBlock) void k_finalize(BatchArgs a, uvhttp_ws_frame_desc_t* desc,
+                                                     Workspace ws) {
+    resolve_epoch(a, ws);
+    finalize_frames(a, desc, ws, blockIdx.x, kBlock, first_bad_of(a, ws, a.n));
 }
 
 // ------------------------------------------------------------------------------------
@@ -1030,6 +1038,15 @@ __global__ __launch_bounds__(BLOCK) void k_unmask_inplace(
     uint64_t tile_base) {
     uint32_t n, nb;
     unmask_tile<BLOCK, VPT, STORE_AUX>(a, desc, ws, tile_base, n, nb);  // resolves the epoch
+    // batch in-place decode: the first ceil(n / BLOCK) workgroups then do k_finalize's work
+    // (statuses after the first failure become SKIPPED — frames no tile reads — and the
+    // summary); the launch covers max(tiles, those blocks).  After the tile, so the tile's
+    // workspace and descriptor reads stay scalar loads no store of this kernel precedes.
+    if (!a.streams && tile_base + blockIdx.x < (a.n + BLOCK - 1) / BLOCK) {
+        resolve_epoch(a, ws);
+        finalize_frames(a, const_cast<uvhttp_ws_frame_desc_t*>(desc), ws,
+                        (uint32_t)(tile_base + blockIdx.x), BLOCK, nb);
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -3125,7 +3142,12 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
     }
     const uint64_t span = arena && !scatter ? n_atiles * kMapTile : b->wire_len;
     const uint64_t tile_bytes = (uint64_t)blk * vpt * 16;
-    const uint64_t n_ptiles = (span + tile_bytes - 1) / tile_bytes;
+    uint64_t n_ptiles = (span + tile_bytes - 1) / tile_bytes;
+    // in place: the payload kernel's first ceil(n / blk) blocks also finalize (no k_finalize)
+    // (not over an empty wire: its tile loads would have no buffer to read)
+    const bool fold_fin = !arena && b->wire_len;
+    const uint64_t n_fin = (a.n + blk - 1) / blk;
+    if (fold_fin && n_ptiles < n_fin) n_ptiles = n_fin;
     // the dispatch packet counts work-items in 32 bits: split very large passes
     const uint64_t max_tiles = (1ull << 24);
     const int tk = timing_begin(e, s);
@@ -3151,7 +3173,7 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
 #undef UVWS_LAUNCH
     }
     timing_end(e, tk, s);
-    {
+    if (!fold_fin || !a.n) {
         const uint32_t grid_fin = a.n ? (a.n + kBlock - 1) / kBlock : 1;
         hipLaunchKernelGGL(k_finalize, dim3(grid_fin), dim3(kBlock), 0, s, a, d_desc, e->ws);
     }
