@@ -591,27 +591,32 @@ __device__ inline ScanElem rec_value(const u32x4v x[4]) {
     return e;
 }
 
-// exclusive prefix of block b (all threads call; the value is broadcast through LDS)
-__device__ ScanElem lookback_prefix(const Workspace& ws, uint32_t b, const ScanElem& agg,
-                                    uint32_t epoch, uint32_t max_polls) {
+// first half of the look-back: block b publishes its aggregate (block 0 its inclusive prefix)
+__device__ inline void lookback_publish(const Workspace& ws, uint32_t b, const ScanElem& agg,
+                                        uint32_t epoch) {
+    if (threadIdx.x == 0) {
+        if (b == 0) {
+            rec_store(ws.rec_p, 0, agg, (epoch << 2) | kRecPrefix);
+            ws.block_excl[0] = scan_identity();
+            ws.block_incl[0] = agg;
+        } else {
+            rec_store(ws.rec_a, b, agg, (epoch << 2) | kRecAgg);
+        }
+    }
+}
+
+// second half: the exclusive prefix of block b (all threads call; the value is broadcast
+// through LDS).  k_decode_stride publishes long before it waits, with its payload pass between.
+__device__ ScanElem lookback_wait(const Workspace& ws, uint32_t b, const ScanElem& agg,
+                                  uint32_t epoch, uint32_t max_polls) {
     __shared__ ScanElem s_wave[kBlock / 64];
     __shared__ ScanElem s_pre;
     __shared__ int s_kstar;
     __shared__ int s_go;
     const uint32_t tag_a = (epoch << 2) | kRecAgg, tag_p = (epoch << 2) | kRecPrefix;
-    if (threadIdx.x == 0) {
-        if (b == 0) {
-            rec_store(ws.rec_p, 0, agg, tag_p);
-            s_pre = scan_identity();
-            ws.block_excl[0] = scan_identity();
-            ws.block_incl[0] = agg;
-        } else {
-            rec_store(ws.rec_a, b, agg, tag_a);
-        }
-    }
     if (b == 0) {
         __syncthreads();
-        return s_pre;
+        return scan_identity();
     }
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     ScanElem run = scan_identity();  // thread 0: combination of the predecessors seen so far
@@ -677,6 +682,12 @@ __device__ ScanElem lookback_prefix(const Workspace& ws, uint32_t b, const ScanE
     }
     __syncthreads();
     return s_pre;
+}
+
+__device__ inline ScanElem lookback_prefix(const Workspace& ws, uint32_t b, const ScanElem& agg,
+                                           uint32_t epoch, uint32_t max_polls) {
+    lookback_publish(ws, b, agg, epoch);
+    return lookback_wait(ws, b, agg, epoch, max_polls);
 }
 
 // k_plan: one launch per decode: parse -> block scan -> look-back -> state machine.  Each
@@ -1046,6 +1057,244 @@ __global__ __launch_bounds__(BLOCK) void k_unmask_inplace(
         resolve_epoch(a, ws);
         finalize_frames(a, const_cast<uvhttp_ws_frame_desc_t*>(desc), ws,
                         (uint32_t)(tile_base + blockIdx.x), BLOCK, nb);
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// k_decode_stride: the whole in-place decode of a fixed-stride batch of small frames in one
+// launch (C4: 1 048 576 x 264-byte frames).  The two-launch form spends ~60 us in k_plan
+// before the payload pass may start; here each ticket-ordered workgroup owns FPB consecutive
+// frames and, in order:
+//   1. parses their headers (every check before the state machine, parse_hdr), reduces their
+//      scan values and PUBLISHES its aggregate for the look-back at once;
+//   2. unmasks the payload bytes of its own frames that passed the parse — speculatively:
+//      whether a frame is delivered also depends on the state machine and on every earlier
+//      frame, which are not known yet.  The workgroup's byte range [S, E) is exactly its
+//      frames' slots (i * stride ...), so ranges of different workgroups are disjoint;
+//      16-byte vectors inside [S, E) are stored whole, the (at most two) vectors a workgroup
+//      shares with a neighbour are written byte by byte, only where its mask is non-zero;
+//   3. waits for its exclusive prefix (by now the predecessors have long published), runs the
+//      state machine (resolve_one) and stores each descriptor once.
+// k_stride_tail then finishes the call: with no failure it only writes the summary; after a
+// failure at frame nb it XORs the payload of every frame >= nb that step 2 unmasked back to
+// the wire bytes (XOR is an involution) and marks frames > nb SKIPPED — exactly the bytes and
+// statuses of the two-launch decode.  Stride layouts only: an offset table may place frames
+// out of order, and then two workgroups' ranges could overlap.
+// Frame lookup is arithmetic: byte p of the block (relative to the aligned start V0) lies in
+// the slot of local frame (p - d0) / stride; LDS holds per frame its key and
+// (payload offset in slot << 24 | payload length), 0 for a frame that failed its parse.
+// ------------------------------------------------------------------------------------
+constexpr uint32_t kStrideSpanMax = 1u << 24;  // block spans (and the last frame) below 16 MiB
+constexpr uint32_t kStrideMinFpb = 64;         // frames per block: 64 .. 2048
+constexpr uint32_t kStrideMaxFpb = 2048;
+constexpr uint64_t kStrideAutoMax = 8192;      // automatic choice: strides up to this
+
+// mask contribution of payload [ps, pe) (offsets relative to the block's aligned start) to
+// the 16-byte vector at x; payload byte j uses key byte j & 3
+__device__ inline void add_mask32(u32x4& m, uint32_t x, uint32_t ps, uint32_t pe, uint32_t key) {
+    if (pe <= x || ps >= x + 16u) return;
+    const uint32_t rk = rotr32(key, 8u * ((x - ps) & 3u));
+    if (ps <= x && x + 16u <= pe) {
+        m = u32x4{rk, rk, rk, rk};
+        return;
+    }
+    const int lo = ps > x ? (int)(ps - x) : 0;
+    const int hi = pe < x + 16u ? (int)(pe - x) : 16;
+    m.x |= rk & lane_bytes(lo, hi, 0);
+    m.y |= rk & lane_bytes(lo, hi, 1);
+    m.z |= rk & lane_bytes(lo, hi, 2);
+    m.w |= rk & lane_bytes(lo, hi, 3);
+}
+
+// y / s for y < 2^24 + 16 (float reciprocal, then exact correction)
+__device__ inline uint32_t div_stride(uint32_t y, uint32_t s, float inv_s) {
+    uint32_t q = (uint32_t)((float)y * inv_s);
+    if (q * s > y) --q;
+    if (q * s > y) --q;
+    if ((q + 1u) * s <= y) ++q;
+    if ((q + 1u) * s <= y) ++q;
+    return q;
+}
+
+template <int FPT, int U>
+__global__ __launch_bounds__(kBlock) void k_decode_stride(BatchArgs a, uvhttp_ws_frame_desc_t* desc,
+                                                          Workspace ws, uint32_t fpb, float inv_s) {
+    constexpr uint32_t kMaxF = (uint32_t)kBlock * FPT;
+    __shared__ uint32_t s_key[kMaxF];
+    __shared__ uint32_t s_meta[kMaxF];
+    __shared__ uint32_t s_ticket;
+    resolve_epoch(a, ws);
+    if (threadIdx.x == 0) {
+        const uint32_t t =
+            __hip_atomic_fetch_add(&ws.counters[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t + 1 == gridDim.x)
+            __hip_atomic_store(&ws.counters[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_ticket = t;
+    }
+    __syncthreads();
+    const uint32_t b = s_ticket;
+    const uint32_t n = a.n;
+    const uint64_t s = a.frame_stride;
+    const uint32_t i0 = b * fpb;
+    const uint32_t cnt = n - i0 < fpb ? n - i0 : fpb;
+    const uint32_t l0 = threadIdx.x * FPT;  // this lane's first local frame
+
+    // 1. parse (all header loads in flight together, as k_plan's pass 1)
+    ScanElem tagg = scan_identity();
+    uvhttp_ws_frame_desc_t dv[FPT];
+    {
+        uint64_t o[FPT];
+        u32x4 hv[FPT];
+        const uint32_t ilast = n - 1;
+#pragma unroll
+        for (int k = 0; k < FPT; ++k) {
+            const uint32_t i = i0 + l0 + k;
+            o[k] = (uint64_t)(l0 + k < cnt ? i : ilast) * s;
+        }
+#pragma unroll
+        for (int k = 0; k < FPT; ++k) hv[k] = load_header(a, o[k]);
+#pragma unroll
+        for (int k = 0; k < FPT; ++k) {
+            const uint32_t l = l0 + k;
+            if (l < cnt) {
+                const uint32_t i = i0 + l;
+                tagg = scan_combine(tagg, parse_hdr(a, i, seg_info(a, i, n), o[k], hv[k], dv[k]));
+                const bool ok = dv[k].status == UVHTTP_WS_FRAME_OK;
+                s_key[l] = dv[k].masking_key;
+                s_meta[l] = ok ? ((uint32_t)(dv[k].payload_off - o[k]) << 24) | (uint32_t)dv[k].payload_len
+                               : 0u;
+            }
+        }
+    }
+    ScanElem agg;
+    const ScanElem local = block_exclusive_scan(tagg, &agg);  // (its barriers publish s_key/s_meta)
+    lookback_publish(ws, b, agg, a.epoch);
+
+    // 2. speculative unmask of the block's byte range
+    {
+        const uint64_t wl = a.wire_len;
+        uint64_t S = (uint64_t)i0 * s, E = i0 + cnt == n ? wl : (uint64_t)(i0 + cnt) * s;
+        if (S > wl) S = wl;
+        if (E > wl) E = wl;
+        const uint64_t V0 = S & ~(uint64_t)15;
+        const uint32_t d0 = (uint32_t)(S - V0);
+        const uint32_t hi_in = (uint32_t)(E - V0);            // bytes [d0, hi_in) are ours
+        const uint64_t full_end = wl & ~(uint64_t)15;
+        const uint32_t full_rel = full_end > V0 ? (uint32_t)(full_end - V0) : 0u;
+        const uint32_t in_end = hi_in < full_rel ? hi_in : full_rel;  // whole-vector limit
+        const uint32_t nvec = (hi_in + 15u) >> 4;
+        const uint32_t s32 = (uint32_t)s;
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(a.wire + V0, 0, (int)(in_end ? in_end : 16u), 0x00020000);
+        for (uint32_t r = 0; r < nvec; r += kBlock * U) {
+            u32x4 data[U];
+            uint32_t xs[U];
+            bool inner[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t vi = r + (uint32_t)u * kBlock + threadIdx.x;
+                xs[u] = vi << 4;
+                inner[u] = vi < nvec && xs[u] >= d0 && xs[u] + 16u <= in_end;
+                if (inner[u]) data[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.wire + V0 + xs[u]));
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t x = xs[u];
+                if ((x >> 4) >= nvec) continue;
+                u32x4 m = u32x4{0, 0, 0, 0};
+                uint32_t fl = x > d0 ? div_stride(x - d0, s32, inv_s) : 0u;
+                if (fl >= cnt) fl = cnt - 1;  // inside the last frame's longer slot
+                for (; fl < cnt; ++fl) {
+                    const uint32_t fs = d0 + fl * s32;
+                    if (fs >= x + 16u) break;
+                    const uint32_t meta = s_meta[fl];
+                    const uint32_t plen = meta & 0xFFFFFFu;
+                    if (plen) {
+                        const uint32_t ps = fs + (meta >> 24);
+                        add_mask32(m, x, ps, ps + plen, s_key[fl]);
+                    }
+                }
+                if (!any_bits(m)) continue;
+                if (inner[u]) {
+                    const u32x4 v = data[u] ^ m;
+                    __builtin_amdgcn_raw_buffer_store_b128(
+                        __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v), rs, x, 0, 18);
+                } else {
+                    // a vector shared with a neighbouring block or straddling the end of the
+                    // wire: only this block's payload bytes (mask bytes != 0) are written
+                    const uint32_t mw[4] = {m.x, m.y, m.z, m.w};
+                    for (uint32_t c = 0; c < 16; ++c) {
+                        const uint8_t mb = (uint8_t)(mw[c >> 2] >> (8 * (c & 3)));
+                        if (mb) a.wire[V0 + x + c] ^= mb;
+                    }
+                }
+            }
+        }
+    }
+
+    // 3. prefix, state machine, descriptors
+    ScanElem run = scan_combine(lookback_wait(ws, b, agg, a.epoch, a.max_polls), local);
+#pragma unroll
+    for (int k = 0; k < FPT; ++k) {
+        const uint32_t l = l0 + k;
+        if (l < cnt) {
+            const uint32_t i = i0 + l;
+            const SegInfo g = seg_info(a, i, n);
+            ScanElem e = scan_identity();
+            if (dv[k].status == UVHTTP_WS_FRAME_OK) e = scan_elem_of(dv[k], (int32_t)i, g.head);
+            else if (g.head) e.bits = kHead;
+            resolve_one(a, nullptr, ws, i, n, g, run, dv[k]);
+            desc[i] = dv[k];
+            run = scan_combine(run, e);
+        }
+    }
+}
+
+// XOR frame d's payload with its key again (k_stride_tail: a speculatively unmasked frame that
+// is not delivered).  Aligned interior vectors lie in this frame alone; the edges go bytewise.
+__device__ inline void remask_payload(uint8_t* wire, const uvhttp_ws_frame_desc_t& d) {
+    const uint64_t ps = d.payload_off, pe = ps + d.payload_len;
+    const uint32_t key = d.masking_key;
+    if (!key || ps >= pe) return;
+    uint64_t a0 = (ps + 15) & ~(uint64_t)15, a1 = pe & ~(uint64_t)15;
+    if (a0 > a1) a0 = a1 = pe;
+    for (uint64_t q = ps; q < a0; ++q) wire[q] ^= (uint8_t)(key >> (8 * ((q - ps) & 3)));
+    const uint32_t rk = rotr32(key, 8u * (uint32_t)((a0 - ps) & 3u));
+    for (uint64_t q = a0; q < a1; q += 16) {
+        u32x4* p = reinterpret_cast<u32x4*>(wire + q);
+        *p = *p ^ u32x4{rk, rk, rk, rk};
+    }
+    for (uint64_t q = a1 > a0 ? a1 : a0; q < pe; ++q) wire[q] ^= (uint8_t)(key >> (8 * ((q - ps) & 3)));
+}
+
+__global__ __launch_bounds__(kBlock) void k_stride_tail(BatchArgs a, uvhttp_ws_frame_desc_t* desc,
+                                                        Workspace ws) {
+    resolve_epoch(a, ws);
+    const uint32_t n = a.n;
+    const bool fault = device_fault(a, ws);
+    const uint32_t nb = fault ? 0u : first_bad_of(a, ws, n);
+    if (blockIdx.x == 0 && threadIdx.x < 64) {
+        if (fault) {
+            if (threadIdx.x == 0) {
+                uvhttp_ws_batch_summary_t sm;
+                memset(&sm, 0, sizeof(sm));
+                sm.n_frames = n;
+                sm.status = -1;
+                sm.first_status = UVHTTP_WS_FRAME_ERR_DEVICE;
+                *a.summary = sm;
+            }
+        } else {
+            write_summary(a, desc, ws, nb);  // reads desc[0 .. nb] only: nothing below changes them
+        }
+    }
+    for (uint32_t i = nb + blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        const uvhttp_ws_frame_desc_t d = desc[i];
+        // the frames step 2 unmasked: every frame whose parse passed (the state machine only
+        // turns OK into ERR_FRAGMENT / ERR_MESSAGE)
+        if (d.status == UVHTTP_WS_FRAME_OK || d.status == UVHTTP_WS_FRAME_ERR_FRAGMENT ||
+            d.status == UVHTTP_WS_FRAME_ERR_MESSAGE)
+            remask_payload(a.wire, d);
+        if (fault || i > nb) desc[i].status = UVHTTP_WS_FRAME_SKIPPED;
     }
 }
 
@@ -2749,6 +2998,9 @@ struct uvhttp_ws_gpu_engine {
     int build_small;           // emit shape for frames < 4 KiB (UVHTTP_WS_BUILD_SMALL, tuning)
     uint64_t build_frames_max; // frame-grouped LDS emit below this average frame (UVHTTP_WS_BUILD_FRAMES; 0 = off)
     int compact_mode;          // 0 automatic, 1 arena-driven gather, 2 wire-driven scatter
+    int stride_mode;           // one-launch stride decode: 0 off, 1 whenever legal, 2 automatic
+    uint32_t stride_blocks;    // its target grid (UVHTTP_WS_STRIDE_BLOCKS)
+    int stride_u;              // its vectors per lane per round (UVHTTP_WS_STRIDE_U: 2, 4, 8)
     uint32_t* ctl;             // device control words (kCtl*), own allocation
     uint32_t faults_seen;      // ctl[kCtlFaults] at the last engine_sync
     uint32_t max_polls;        // look-back wait bound (UVHTTP_WS_MAX_POLLS: tests)
@@ -2830,6 +3082,14 @@ int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out) {
     if (const char* cm = getenv("UVHTTP_WS_COMPACT"))
         e->compact_mode = strcmp(cm, "gather") == 0 ? 1 : strcmp(cm, "scatter") == 0 ? 2 : 0;
     if (const char* ws = getenv("UVHTTP_WS_WALK_SINGLE")) e->walk_single_off = atoi(ws) == 0;
+    e->stride_mode = 2;
+    if (const char* sm = getenv("UVHTTP_WS_STRIDE")) e->stride_mode = atoi(sm) == 0 ? 0 : atoi(sm) == 1 ? 1 : 2;
+    e->stride_blocks = 1024;
+    if (const char* sb = getenv("UVHTTP_WS_STRIDE_BLOCKS")) e->stride_blocks = (uint32_t)strtoul(sb, nullptr, 0);
+    if (e->stride_blocks < 1) e->stride_blocks = 1;
+    e->stride_u = 4;
+    if (const char* su = getenv("UVHTTP_WS_STRIDE_U")) e->stride_u = atoi(su);
+    if (e->stride_u != 2 && e->stride_u != 8) e->stride_u = 4;
     if (const char* wm = getenv("UVHTTP_WS_WALK"))
         e->walk_mode = strcmp(wm, "lane") == 0 ? 1 : strcmp(wm, "wave") == 0 ? 2 : 0;
     *out = e;
@@ -2894,7 +3154,8 @@ int uvhttp_ws_gpu_engine_reserve(uvhttp_ws_gpu_engine_t* e, uint32_t max_frames,
     const uint32_t fr = max_frames > e->cap_frames ? max_frames : e->cap_frames;
     const uint64_t tl = tiles > e->cap_tiles ? tiles : e->cap_tiles;
     const uint64_t at = atiles > e->cap_arena_tiles ? atiles : e->cap_arena_tiles;
-    const uint64_t nblk = (fr + kBlock - 1) / kBlock + 2;
+    // look-back records for k_plan (>= 256 frames per block) and k_decode_stride (>= 64)
+    const uint64_t nblk = (fr + kStrideMinFpb - 1) / kStrideMinFpb + 2;
     const uint64_t ngrp = nblk / kBlock + 2;
     size_t off_agg = 0;
     size_t off_grp = align_up(off_agg + nblk * sizeof(ScanElem), 256);
@@ -3073,6 +3334,44 @@ static void launch_plan(uvhttp_ws_gpu_engine_t* e, BatchArgs& a, uint32_t n_cap,
     }
 }
 
+// k_decode_stride + k_stride_tail for an in-place fixed-stride batch, when it fits: frames
+// per block the smallest power of two from 64 whose grid stays within stride_blocks (each
+// block costs a ticket and a look-back round; ~1024 blocks keep the payload pass streaming),
+// every block's byte span and the last frame below 16 MiB (32-bit offsets, float division).
+static bool launch_stride_decode(uvhttp_ws_gpu_engine_t* e, BatchArgs& a,
+                                 uvhttp_ws_frame_desc_t* d_desc, hipStream_t s) {
+    if (e->stride_mode == 0 || a.arena || a.frame_off || a.n == 0 || a.wire_len == 0) return false;
+    const uint64_t st = a.frame_stride;
+    if (st == 0 || st >= kStrideSpanMax) return false;
+    if (e->stride_mode == 2 && st > kStrideAutoMax) return false;
+    uint32_t fpb = kStrideMinFpb;
+    while (fpb < kStrideMaxFpb && (a.n + fpb - 1) / fpb > e->stride_blocks) fpb *= 2;
+    while (fpb > kStrideMinFpb && (uint64_t)fpb * st > kStrideSpanMax) fpb /= 2;
+    if ((uint64_t)fpb * st > kStrideSpanMax) return false;
+    uint64_t last0 = (uint64_t)((a.n - 1) / fpb) * fpb * st;
+    if (last0 > a.wire_len) last0 = a.wire_len;
+    if (a.wire_len - last0 > kStrideSpanMax) return false;
+    a.plan_frames = fpb;
+    a.n_tiles = 0;  // no tile maps: resolve_one claims none
+    const uint32_t grid = (a.n + fpb - 1) / fpb;
+    const float inv_s = 1.0f / (float)st;
+    const int fpt = fpb >= 256 ? (int)(fpb / 256) : 1;
+    const int tk = timing_begin(e, s);
+#define UVWS_STRIDE(F, V)                                                                        \
+    if (fpt == F && e->stride_u == V) {                                                          \
+        hipLaunchKernelGGL((k_decode_stride<F, V>), dim3(grid), dim3(kBlock), 0, s, a, d_desc,   \
+                           e->ws, fpb, inv_s);                                                   \
+    } else
+    UVWS_STRIDE(1, 2) UVWS_STRIDE(1, 4) UVWS_STRIDE(1, 8) UVWS_STRIDE(2, 2) UVWS_STRIDE(2, 4)
+    UVWS_STRIDE(2, 8) UVWS_STRIDE(4, 2) UVWS_STRIDE(4, 4) UVWS_STRIDE(4, 8) UVWS_STRIDE(8, 2)
+    UVWS_STRIDE(8, 4) UVWS_STRIDE(8, 8) {}
+#undef UVWS_STRIDE
+    timing_end(e, tk, s);
+    const uint32_t tgrid = (a.n + kBlock - 1) / kBlock < 1024 ? (a.n + kBlock - 1) / kBlock : 1024;
+    hipLaunchKernelGGL(k_stride_tail, dim3(tgrid), dim3(kBlock), 0, s, a, d_desc, e->ws);
+    return true;
+}
+
 static int check_batch(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b,
                        const void* d_desc, const void* d_summary) {
     if (!e || !b || !d_desc || !d_summary) return UVHTTP_WS_GPU_EINVAL;
@@ -3123,6 +3422,12 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
     a.dev_epoch = e->capturing ? 1u : 0u;
     a.epoch = next_epoch(e, s);
 
+    if (launch_stride_decode(e, a, d_desc, s)) {
+        const hipError_t h = hipGetLastError();
+        if (prev != e->device) (void)hipSetDevice(prev);
+        if (h != hipSuccess) return set_err(e, UVHTTP_WS_GPU_ELAUNCH, "launch", h);
+        return UVHTTP_WS_GPU_OK;
+    }
     launch_plan(e, a, a.n, d_desc, d_msgs, s);
     // payload kernel tile shape: explicit (set_tile) or by average wire bytes per frame
     // (auto shapes from tools/tile_sweep.py on MI355X, profiles/r01_tile_sweep.txt)
