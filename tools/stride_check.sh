@@ -14,12 +14,12 @@ if [[ ${SKIP_TESTS:-0} != 1 ]]; then
   tail -2 $OUT/${TAG}_pytest.log
 fi
 : > $OUT/${TAG}_bench.jsonl
-for cfg in C4 C2; do
-  for v in "0 1024 4" "1 1024 4" "1 512 4" "1 2048 4" "1 1024 8" "1 1024 2"; do
+for cfg in c4 c2; do
+  for v in "0 4" "1 4" "1 2" "1 8"; do
     set -- $v
-    UVHTTP_WS_STRIDE=$1 UVHTTP_WS_STRIDE_BLOCKS=$2 UVHTTP_WS_STRIDE_U=$3 timeout -k 10 120 \
+    UVHTTP_WS_STRIDE=$1 UVHTTP_WS_STRIDE_U=$2 timeout -k 10 120 \
       python bench.py --config $cfg --steps 50 --warmup 5 --no-cpu-baseline --no-c5-base \
-      2> $OUT/${TAG}_bench.err | python -c "import json,sys; d=json.loads(sys.stdin.readline()); print(json.dumps({'cfg': '$cfg', 'stride': '$1', 'blocks': $2, 'u': $3, 'value': d['value'], 'ms': d['ms_per_step'], 'kernel_us': d['roofline']['avg_kernel_us'], 'frac': d['roofline']['frac']}))" \
+      2> $OUT/${TAG}_bench.err | python -c "import json,sys; d=json.loads(sys.stdin.readline()); print(json.dumps({'cfg': '$cfg', 'stride': '$1', 'u': $2, 'value': d['value'], 'ms': d['ms_per_step'], 'kernel_us': d['roofline']['avg_kernel_us'], 'frac': d['roofline']['frac']}))" \
       | tee -a $OUT/${TAG}_bench.jsonl
   done
 done
