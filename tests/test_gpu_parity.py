@@ -45,30 +45,6 @@ def eng(torch, request):
     e.close()
 
 
-def _engine_env(env):
-    import os
-    import uvhttp_amd as U
-    old = {k: os.environ.get(k) for k in env}
-    os.environ.update(env)
-    try:
-        return U.GpuEngine(0)
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
-
-
-@pytest.fixture(scope="module", params=["0", "1"])
-def stride_eng(torch, request):
-    """In-place stride batches through the two-launch decode (k_plan + k_unmask_inplace,
-    UVHTTP_WS_STRIDE=0) and the one-launch k_decode_stride + k_stride_tail (=1, every size)."""
-    e = _engine_env({"UVHTTP_WS_STRIDE": request.param})
-    yield e
-    e.close()
-
-
 def _frame(op, fin, payload, key=None, masked=True, rsv=0, len_form=None):
     n = len(payload)
     b0 = (0x80 if fin else 0) | (rsv << 4) | (op & 0xF)
@@ -406,41 +382,6 @@ def test_config_c4_full(torch, eng, compact):
     _full_config(torch, eng, 1048576, 256, True, compact, chunk=131072)
 
 
-@pytest.mark.parametrize("cfg", [(65536, 4096, False), (1048576, 256, True)])
-def test_config_two_launch_path(torch, cfg):
-    """C2 and C4 in place through the two-launch decode (the automatic choice for these
-    stride batches is the one-launch k_decode_stride, which test_config_c2/c4_full cover)."""
-    e = _engine_env({"UVHTTP_WS_STRIDE": "0"})
-    try:
-        _full_config(torch, e, cfg[0], cfg[1], cfg[2], False, chunk=131072)
-    finally:
-        e.close()
-
-
-def test_stride_tail_remask_wide(torch):
-    """k_decode_stride unmasks every parsed frame before it knows the first failure;
-    k_stride_tail must restore the wire bytes of every later frame: failures at frame 0, in
-    the first block, mid-batch and at the last frame of a 200 000-frame batch whose last frame
-    is longer than the stride, for several frame sizes (including frames under 16 bytes, where
-    one vector spans several frames)."""
-    rng = random.Random(99)
-    e = _engine_env({"UVHTTP_WS_STRIDE": "1"})
-    try:
-        for plen, n in ((0, 5000), (1, 200000), (7, 50000), (200, 20000), (2000, 3000)):
-            base = [_frame(2, 1, rng.randbytes(plen), rng.randbytes(4)) for _ in range(n)]
-            stride = len(base[0])
-            for where in (0, 1, 70, n // 2, n - 1, None):
-                frames = list(base)
-                frames[-1] = _frame(1, 1, rng.randbytes(plen + 3000), rng.randbytes(4))
-                if where is not None:
-                    frames[where] = _frame(0, 1, rng.randbytes(plen), rng.randbytes(4))
-                wire = np.frombuffer(b"".join(frames), np.uint8).copy()
-                ref, got = _run_both(torch, e, wire, n, stride=stride)
-                _compare(ref, got)
-    finally:
-        e.close()
-
-
 def test_config_c4_default_limit_rejects(torch, eng):
     """With the default 64 MiB max_message_size the reference rejects C4 at frame 262 144
     (SURVEY §0); the device path reports the same frame and reason."""
@@ -602,7 +543,7 @@ def test_epoch_wraparound(torch, monkeypatch):
 
 @pytest.mark.parametrize("compact", [False, True])
 @pytest.mark.parametrize("plen", [0, 3, 60, 200, 1000])
-def test_stride_layouts(torch, eng, stride_eng, plen, compact):
+def test_stride_layouts(torch, eng, plen, compact):
     """Fixed-stride batches of small frames (the payload kernels find a vector's frame by
     arithmetic there): uniform frames, a longer last frame, a wrong-sized frame (LAYOUT), a cut
     last frame, a failing frame in the middle, mixed opcodes of the same wire size."""
@@ -625,18 +566,18 @@ def test_stride_layouts(torch, eng, stride_eng, plen, compact):
     for name, frames in variants.items():
         wire = np.frombuffer(b"".join(frames), np.uint8).copy()
         for wl in (wire.size, wire.size - 1 - rng.randrange(min(stride, 30))):
-            ref, got = _run_both(torch, eng if compact else stride_eng, wire, len(frames),
-                                 stride=stride, wire_len=wl, compact=compact)
+            ref, got = _run_both(torch, eng, wire, len(frames), stride=stride, wire_len=wl,
+                                 compact=compact)
             _compare(ref, got, compact)
 
 
-@pytest.mark.parametrize("smode", ["0", "1"])
-def test_stride_state_machine_failures(torch, smode):
+def test_stride_state_machine_failures(torch):
     """Stride batches with failures only the state machine sees — a CONTINUATION with nothing
     open, a new data frame inside a fragmented message, a message over max_message_size — at
     the first, a middle and the last frame, and deep in a batch of 60 000 frames: bytes,
     statuses and summaries equal the oracle's (frames from the failing one on stay masked)."""
-    e = _engine_env({"UVHTTP_WS_STRIDE": smode})
+    import uvhttp_amd as U
+    e = U.GpuEngine(0)
     try:
         rng = random.Random(55)
         k = lambda: rng.randbytes(4)  # noqa: E731
@@ -669,12 +610,12 @@ def test_stride_state_machine_failures(torch, smode):
         e.close()
 
 
-@pytest.mark.parametrize("smode", ["0", "1"])
-def test_stride_random_batches(torch, smode):
+def test_stride_random_batches(torch):
     """Random stride batches (every frame the same wire size: PING/PONG/CLOSE/TEXT/BINARY/CONT
     mixed, header violations, cut last frames, frames past the end of the wire), in place,
     against the oracle."""
-    e = _engine_env({"UVHTTP_WS_STRIDE": smode})
+    import uvhttp_amd as U
+    e = U.GpuEngine(0)
     try:
         rng = random.Random(808)
         for it in range(24):

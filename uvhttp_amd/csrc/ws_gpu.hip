@@ -591,32 +591,27 @@ __device__ inline ScanElem rec_value(const u32x4v x[4]) {
     return e;
 }
 
-// first half of the look-back: block b publishes its aggregate (block 0 its inclusive prefix)
-__device__ inline void lookback_publish(const Workspace& ws, uint32_t b, const ScanElem& agg,
-                                        uint32_t epoch) {
-    if (threadIdx.x == 0) {
-        if (b == 0) {
-            rec_store(ws.rec_p, 0, agg, (epoch << 2) | kRecPrefix);
-            ws.block_excl[0] = scan_identity();
-            ws.block_incl[0] = agg;
-        } else {
-            rec_store(ws.rec_a, b, agg, (epoch << 2) | kRecAgg);
-        }
-    }
-}
-
-// second half: the exclusive prefix of block b (all threads call; the value is broadcast
-// through LDS).  k_decode_stride publishes long before it waits, with its payload pass between.
-__device__ ScanElem lookback_wait(const Workspace& ws, uint32_t b, const ScanElem& agg,
-                                  uint32_t epoch, uint32_t max_polls) {
+// exclusive prefix of block b (all threads call; the value is broadcast through LDS)
+__device__ ScanElem lookback_prefix(const Workspace& ws, uint32_t b, const ScanElem& agg,
+                                    uint32_t epoch, uint32_t max_polls) {
     __shared__ ScanElem s_wave[kBlock / 64];
     __shared__ ScanElem s_pre;
     __shared__ int s_kstar;
     __shared__ int s_go;
     const uint32_t tag_a = (epoch << 2) | kRecAgg, tag_p = (epoch << 2) | kRecPrefix;
+    if (threadIdx.x == 0) {
+        if (b == 0) {
+            rec_store(ws.rec_p, 0, agg, tag_p);
+            s_pre = scan_identity();
+            ws.block_excl[0] = scan_identity();
+            ws.block_incl[0] = agg;
+        } else {
+            rec_store(ws.rec_a, b, agg, tag_a);
+        }
+    }
     if (b == 0) {
         __syncthreads();
-        return scan_identity();
+        return s_pre;
     }
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     ScanElem run = scan_identity();  // thread 0: combination of the predecessors seen so far
@@ -682,12 +677,6 @@ __device__ ScanElem lookback_wait(const Workspace& ws, uint32_t b, const ScanEle
     }
     __syncthreads();
     return s_pre;
-}
-
-__device__ inline ScanElem lookback_prefix(const Workspace& ws, uint32_t b, const ScanElem& agg,
-                                           uint32_t epoch, uint32_t max_polls) {
-    lookback_publish(ws, b, agg, epoch);
-    return lookback_wait(ws, b, agg, epoch, max_polls);
 }
 
 // k_plan: one launch per decode: parse -> block scan -> look-back -> state machine.  Each
@@ -1057,284 +1046,6 @@ __global__ __launch_bounds__(BLOCK) void k_unmask_inplace(
         resolve_epoch(a, ws);
         finalize_frames(a, const_cast<uvhttp_ws_frame_desc_t*>(desc), ws,
                         (uint32_t)(tile_base + blockIdx.x), BLOCK, nb);
-    }
-}
-
-// ------------------------------------------------------------------------------------
-// k_decode_stride: the whole in-place decode of a fixed-stride batch of small frames in one
-// launch (C4: 1 048 576 x 264-byte frames).  The two-launch form spends ~60 us in k_plan
-// before the payload pass may start.  Here workgroup b owns FPB consecutive frames, whose
-// slots (i * stride ...) span at most 256 x VPL x 16 bytes, and in order:
-//   1. issues the loads of its whole byte range (like the tile kernel: nothing to wait for);
-//   2. parses its frames' headers (one per lane, every check before the state machine,
-//      parse_hdr), reduces their scan values and PUBLISHES its aggregate for the look-back;
-//   3. unmasks the payload bytes of its frames that passed the parse — speculatively: whether
-//      a frame is delivered also depends on the state machine and on every earlier frame,
-//      which are not known yet.  The byte ranges of different workgroups are disjoint (stride
-//      slots); 16-byte vectors inside the range are stored whole, the (at most two) vectors a
-//      workgroup shares with a neighbour are written byte by byte, only where its mask is set;
-//   4. waits for its exclusive prefix — a 16-lane look-back (records of 64 B; by now the
-//      predecessors have usually published their inclusive prefix) — runs the state machine
-//      (resolve_one) and stores each descriptor once.
-// No ticket: workgroups wait only on lower indices, and every XCD dispatches its workgroups in
-// index order, so the lowest unfinished workgroup is always resident and never waits (the
-// bounded polls still report ERR_DEVICE rather than hang).  k_stride_tail finishes the call:
-// with no failure it only writes the summary; after a failure at frame nb it XORs every frame
-// >= nb that step 3 unmasked back to its wire bytes (XOR is an involution) and marks frames
-// > nb SKIPPED — exactly the bytes and statuses of the two-launch decode.  Stride layouts
-// only: an offset table may place frames out of order, and then ranges could overlap.
-// Frame lookup is arithmetic: byte p of the range (relative to its aligned start V0) lies in
-// the slot of local frame (p - d0) / stride; LDS holds per frame its key and
-// (payload offset in slot << 24 | payload length), 0 for a frame that failed its parse.
-// ------------------------------------------------------------------------------------
-constexpr uint32_t kStrideSpanMax = 1u << 24;  // the last frame's slot below 16 MiB
-constexpr uint64_t kStrideAutoMax = 8192;      // automatic choice: strides up to this
-constexpr int kStrideLb = 16;                  // look-back window (lanes of wave 0)
-
-// mask contribution of payload [ps, pe) (offsets relative to the range's aligned start) to
-// the 16-byte vector at x; payload byte j uses key byte j & 3
-__device__ inline void add_mask32(u32x4& m, uint32_t x, uint32_t ps, uint32_t pe, uint32_t key) {
-    if (pe <= x || ps >= x + 16u) return;
-    const uint32_t rk = rotr32(key, 8u * ((x - ps) & 3u));
-    if (ps <= x && x + 16u <= pe) {
-        m = u32x4{rk, rk, rk, rk};
-        return;
-    }
-    const int lo = ps > x ? (int)(ps - x) : 0;
-    const int hi = pe < x + 16u ? (int)(pe - x) : 16;
-    m.x |= rk & lane_bytes(lo, hi, 0);
-    m.y |= rk & lane_bytes(lo, hi, 1);
-    m.z |= rk & lane_bytes(lo, hi, 2);
-    m.w |= rk & lane_bytes(lo, hi, 3);
-}
-
-// y / s for y < 2^24 + 16 (float reciprocal, then exact correction)
-__device__ inline uint32_t div_stride(uint32_t y, uint32_t s, float inv_s) {
-    uint32_t q = (uint32_t)((float)y * inv_s);
-    if (q * s > y) --q;
-    if (q * s > y) --q;
-    if ((q + 1u) * s <= y) ++q;
-    if ((q + 1u) * s <= y) ++q;
-    return q;
-}
-
-// exclusive prefix of block b from a kStrideLb-lane look-back run by wave 0 (the other waves
-// wait at the closing barrier); writes block_excl / block_incl and publishes the inclusive
-// prefix.  Same records, tags and give-up rule as lookback_wait.
-__device__ ScanElem lookback_narrow(const Workspace& ws, uint32_t b, const ScanElem& agg,
-                                    uint32_t epoch, uint32_t max_polls) {
-    __shared__ ScanElem s_pre;
-    if (threadIdx.x < 64) {
-        const int lane = threadIdx.x;
-        const uint32_t tag_a = (epoch << 2) | kRecAgg, tag_p = (epoch << 2) | kRecPrefix;
-        ScanElem run = scan_identity();
-        bool gave_up = false;
-        if (b != 0) {
-            int64_t end = b;
-            uint32_t polls = 0;
-            for (;;) {
-                const int64_t j = end - 1 - lane;
-                const bool mine = lane < kStrideLb;
-                ScanElem v = scan_identity();
-                bool is_p = mine && j < 0, ready = !mine || j < 0;
-                for (;;) {
-                    if (!ready) {
-                        u32x4v xp[4], xa[4];
-                        rec_fetch(ws.rec_p, (uint32_t)j, xp);
-                        rec_fetch(ws.rec_a, (uint32_t)j, xa);
-                        if (rec_valid(xp, tag_p)) {
-                            v = rec_value(xp), is_p = true, ready = true;
-                        } else if (rec_valid(xa, tag_a)) {
-                            v = rec_value(xa), ready = true;
-                        }
-                    }
-                    if (__ballot(!ready) == 0 && max_polls) break;
-                    if (++polls > max_polls) {
-                        gave_up = true;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(4);
-                }
-                const uint64_t pm = __ballot(is_p);
-                const int kstar = pm ? __builtin_ctzll(pm) : 64;
-                if (lane > kstar || !mine || j < 0) v = scan_identity();
-                v = wave_reduce_newest_first(v);  // lane 0: oldest (+) ... (+) newest
-                run = scan_combine(v, run);
-                if (kstar < 64 || gave_up) break;
-                end -= kStrideLb;
-            }
-        }
-        if (lane == 0) {
-            s_pre = run;
-            const ScanElem incl = scan_combine(run, agg);
-            ws.block_excl[b] = run;
-            ws.block_incl[b] = incl;
-            if (b != 0) rec_store(ws.rec_p, b, incl, (epoch << 2) | kRecPrefix);
-            if (gave_up) {
-                __hip_atomic_store(&ws.ctl[kCtlFaultEp], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_fetch_add(&ws.ctl[kCtlFaults], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                tag_claim(ws.first_bad, epoch, 0);
-            }
-        }
-    }
-    __syncthreads();
-    return s_pre;
-}
-
-template <int VPL>
-__global__ __launch_bounds__(kBlock) void k_decode_stride(BatchArgs a, uvhttp_ws_frame_desc_t* desc,
-                                                          Workspace ws, uint32_t fpb, float inv_s) {
-    __shared__ uint32_t s_key[kBlock];
-    __shared__ uint32_t s_meta[kBlock];
-    resolve_epoch(a, ws);
-    const uint32_t b = blockIdx.x;
-    const uint32_t n = a.n;
-    const uint64_t s = a.frame_stride;
-    const uint32_t i0 = b * fpb;
-    const uint32_t cnt = n - i0 < fpb ? n - i0 : fpb;
-    const uint32_t t = threadIdx.x;
-
-    // the block's byte range
-    const uint64_t wl = a.wire_len;
-    uint64_t S = (uint64_t)i0 * s, E = i0 + cnt == n ? wl : (uint64_t)(i0 + cnt) * s;
-    if (S > wl) S = wl;
-    if (E > wl) E = wl;
-    const uint64_t V0 = S & ~(uint64_t)15;
-    const uint32_t d0 = (uint32_t)(S - V0);
-    const uint32_t hi_in = (uint32_t)(E - V0);            // bytes [d0, hi_in) are this block's
-    const uint64_t full_end = wl & ~(uint64_t)15;
-    const uint32_t full_rel = full_end > V0 ? (uint32_t)(full_end - V0) : 0u;
-    const uint32_t in_end = hi_in < full_rel ? hi_in : full_rel;  // whole-vector limit
-    const uint32_t nvec = (hi_in + 15u) >> 4;
-
-    // 1. the first round's loads, before anything else
-    u32x4 data[VPL];
-    bool inner[VPL];
-#pragma unroll
-    for (int u = 0; u < VPL; ++u) {
-        const uint32_t x = ((uint32_t)u * kBlock + t) << 4;
-        inner[u] = x >= d0 && x + 16u <= in_end;
-        if (inner[u]) data[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.wire + V0 + x));
-    }
-
-    // 2. parse: frame i0 + t on lane t
-    uvhttp_ws_frame_desc_t d;
-    SegInfo g;
-    ScanElem elem = scan_identity();
-    if (t < cnt) {
-        const uint32_t i = i0 + t;
-        const uint64_t o = (uint64_t)i * s;
-        g = seg_info(a, i, n);
-        elem = parse_hdr(a, i, g, o, load_header(a, o), d);
-        const bool ok = d.status == UVHTTP_WS_FRAME_OK;
-        s_key[t] = d.masking_key;
-        s_meta[t] = ok ? ((uint32_t)(d.payload_off - o) << 24) | (uint32_t)d.payload_len : 0u;
-    }
-    ScanElem agg;
-    const ScanElem local = block_exclusive_scan(elem, &agg);  // (its barriers publish s_key/s_meta)
-    lookback_publish(ws, b, agg, a.epoch);
-
-    // 3. speculative unmask of the block's range
-    const uint32_t s32 = (uint32_t)s;
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(a.wire + V0, 0, (int)(in_end ? in_end : 16u), 0x00020000);
-    for (uint32_t r = 0; r < nvec; r += kBlock * VPL) {
-        if (r) {  // ranges longer than one round (a long last frame)
-#pragma unroll
-            for (int u = 0; u < VPL; ++u) {
-                const uint32_t x = (r + (uint32_t)u * kBlock + t) << 4;
-                inner[u] = x >= d0 && x + 16u <= in_end;
-                if (inner[u]) data[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.wire + V0 + x));
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < VPL; ++u) {
-            const uint32_t x = (r + (uint32_t)u * kBlock + t) << 4;
-            if ((x >> 4) >= nvec) continue;
-            u32x4 m = u32x4{0, 0, 0, 0};
-            uint32_t fl = x > d0 ? div_stride(x - d0, s32, inv_s) : 0u;
-            if (fl >= cnt) fl = cnt - 1;  // inside the last frame's longer slot
-            for (; fl < cnt; ++fl) {
-                const uint32_t fs = d0 + fl * s32;
-                if (fs >= x + 16u) break;
-                const uint32_t meta = s_meta[fl];
-                const uint32_t plen = meta & 0xFFFFFFu;
-                if (plen) {
-                    const uint32_t ps = fs + (meta >> 24);
-                    add_mask32(m, x, ps, ps + plen, s_key[fl]);
-                }
-            }
-            if (!any_bits(m)) continue;
-            if (inner[u]) {
-                const u32x4 v = data[u] ^ m;
-                __builtin_amdgcn_raw_buffer_store_b128(
-                    __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v), rs, x, 0, 18);
-            } else {
-                // a vector shared with a neighbouring block or straddling the end of the wire:
-                // only this block's payload bytes (mask bytes != 0) are written
-                const uint32_t mw[4] = {m.x, m.y, m.z, m.w};
-                for (uint32_t c = 0; c < 16; ++c) {
-                    const uint8_t mb = (uint8_t)(mw[c >> 2] >> (8 * (c & 3)));
-                    if (mb) a.wire[V0 + x + c] ^= mb;
-                }
-            }
-        }
-    }
-
-    // 4. prefix, state machine, descriptor
-    const ScanElem pre = lookback_narrow(ws, b, agg, a.epoch, a.max_polls);
-    if (t < cnt) {
-        const uint32_t i = i0 + t;
-        resolve_one(a, nullptr, ws, i, n, g, scan_combine(pre, local), d);
-        desc[i] = d;
-    }
-}
-
-// XOR frame d's payload with its key again (k_stride_tail: a speculatively unmasked frame that
-// is not delivered).  Aligned interior vectors lie in this frame alone; the edges go bytewise.
-__device__ inline void remask_payload(uint8_t* wire, const uvhttp_ws_frame_desc_t& d) {
-    const uint64_t ps = d.payload_off, pe = ps + d.payload_len;
-    const uint32_t key = d.masking_key;
-    if (!key || ps >= pe) return;
-    uint64_t a0 = (ps + 15) & ~(uint64_t)15, a1 = pe & ~(uint64_t)15;
-    if (a0 > a1) a0 = a1 = pe;
-    for (uint64_t q = ps; q < a0; ++q) wire[q] ^= (uint8_t)(key >> (8 * ((q - ps) & 3)));
-    const uint32_t rk = rotr32(key, 8u * (uint32_t)((a0 - ps) & 3u));
-    for (uint64_t q = a0; q < a1; q += 16) {
-        u32x4* p = reinterpret_cast<u32x4*>(wire + q);
-        *p = *p ^ u32x4{rk, rk, rk, rk};
-    }
-    for (uint64_t q = a1 > a0 ? a1 : a0; q < pe; ++q) wire[q] ^= (uint8_t)(key >> (8 * ((q - ps) & 3)));
-}
-
-__global__ __launch_bounds__(kBlock) void k_stride_tail(BatchArgs a, uvhttp_ws_frame_desc_t* desc,
-                                                        Workspace ws) {
-    resolve_epoch(a, ws);
-    const uint32_t n = a.n;
-    const bool fault = device_fault(a, ws);
-    const uint32_t nb = fault ? 0u : first_bad_of(a, ws, n);
-    if (blockIdx.x == 0 && threadIdx.x < 64) {
-        if (fault) {
-            if (threadIdx.x == 0) {
-                uvhttp_ws_batch_summary_t sm;
-                memset(&sm, 0, sizeof(sm));
-                sm.n_frames = n;
-                sm.status = -1;
-                sm.first_status = UVHTTP_WS_FRAME_ERR_DEVICE;
-                *a.summary = sm;
-            }
-        } else {
-            write_summary(a, desc, ws, nb);  // reads desc[0 .. nb] only: nothing below changes them
-        }
-    }
-    for (uint32_t i = nb + blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-        const uvhttp_ws_frame_desc_t d = desc[i];
-        // the frames step 2 unmasked: every frame whose parse passed (the state machine only
-        // turns OK into ERR_FRAGMENT / ERR_MESSAGE)
-        if (d.status == UVHTTP_WS_FRAME_OK || d.status == UVHTTP_WS_FRAME_ERR_FRAGMENT ||
-            d.status == UVHTTP_WS_FRAME_ERR_MESSAGE)
-            remask_payload(a.wire, d);
-        if (fault || i > nb) desc[i].status = UVHTTP_WS_FRAME_SKIPPED;
     }
 }
 
@@ -3019,7 +2730,7 @@ struct uvhttp_ws_gpu_engine {
     void* ws_mem;
     size_t ws_bytes;
     uint32_t cap_frames;
-    uint64_t cap_tiles, cap_arena_tiles, cap_blocks;
+    uint64_t cap_tiles, cap_arena_tiles;
     Workspace ws;
     int timing;
     int tile_block, tile_vpt;  // payload kernel shape, 0 = automatic
@@ -3038,8 +2749,6 @@ struct uvhttp_ws_gpu_engine {
     int build_small;           // emit shape for frames < 4 KiB (UVHTTP_WS_BUILD_SMALL, tuning)
     uint64_t build_frames_max; // frame-grouped LDS emit below this average frame (UVHTTP_WS_BUILD_FRAMES; 0 = off)
     int compact_mode;          // 0 automatic, 1 arena-driven gather, 2 wire-driven scatter
-    int stride_mode;           // one-launch stride decode: 0 off, 1 whenever legal, 2 automatic
-    int stride_u;              // its vectors per lane (UVHTTP_WS_STRIDE_U: 2, 4, 8)
     uint32_t* ctl;             // device control words (kCtl*), own allocation
     uint32_t faults_seen;      // ctl[kCtlFaults] at the last engine_sync
     uint32_t max_polls;        // look-back wait bound (UVHTTP_WS_MAX_POLLS: tests)
@@ -3121,11 +2830,6 @@ int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out) {
     if (const char* cm = getenv("UVHTTP_WS_COMPACT"))
         e->compact_mode = strcmp(cm, "gather") == 0 ? 1 : strcmp(cm, "scatter") == 0 ? 2 : 0;
     if (const char* ws = getenv("UVHTTP_WS_WALK_SINGLE")) e->walk_single_off = atoi(ws) == 0;
-    e->stride_mode = 2;
-    if (const char* sm = getenv("UVHTTP_WS_STRIDE")) e->stride_mode = atoi(sm) == 0 ? 0 : atoi(sm) == 1 ? 1 : 2;
-    e->stride_u = 4;
-    if (const char* su = getenv("UVHTTP_WS_STRIDE_U")) e->stride_u = atoi(su);
-    if (e->stride_u != 2 && e->stride_u != 8) e->stride_u = 4;
     if (const char* wm = getenv("UVHTTP_WS_WALK"))
         e->walk_mode = strcmp(wm, "lane") == 0 ? 1 : strcmp(wm, "wave") == 0 ? 2 : 0;
     *out = e;
@@ -3175,15 +2879,14 @@ int uvhttp_ws_gpu_engine_sync(uvhttp_ws_gpu_engine_t* e, void* stream) {
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-// workspace for max_frames frames (k_plan: one look-back record set per 256 frames) and at
-// least min_blocks look-back blocks (k_decode_stride: one per FPB frames)
-static int reserve_ws(uvhttp_ws_gpu_engine_t* e, uint32_t max_frames, uint64_t max_wire_bytes,
-                      uint64_t max_arena_bytes, uint64_t min_blocks) {
+int uvhttp_ws_gpu_engine_reserve(uvhttp_ws_gpu_engine_t* e, uint32_t max_frames,
+                                 uint64_t max_wire_bytes, uint64_t max_arena_bytes) {
+    if (!e) return UVHTTP_WS_GPU_EINVAL;
     if (max_frames > kMaxFrames) return set_err(e, UVHTTP_WS_GPU_EINVAL, "too many frames", hipSuccess);
     const uint64_t tiles = (max_wire_bytes + kMapTile - 1) / kMapTile + 1;
     const uint64_t atiles = (max_arena_bytes + kMapTile - 1) / kMapTile + 1;
     if (e->ws_mem && max_frames <= e->cap_frames && tiles <= e->cap_tiles &&
-        atiles <= e->cap_arena_tiles && min_blocks <= e->cap_blocks)
+        atiles <= e->cap_arena_tiles)
         return UVHTTP_WS_GPU_OK;
     if (e->capturing)
         return set_err(e, UVHTTP_WS_GPU_EINVAL, "workspace too small for a captured call: reserve first",
@@ -3191,9 +2894,7 @@ static int reserve_ws(uvhttp_ws_gpu_engine_t* e, uint32_t max_frames, uint64_t m
     const uint32_t fr = max_frames > e->cap_frames ? max_frames : e->cap_frames;
     const uint64_t tl = tiles > e->cap_tiles ? tiles : e->cap_tiles;
     const uint64_t at = atiles > e->cap_arena_tiles ? atiles : e->cap_arena_tiles;
-    uint64_t nblk = (fr + kBlock - 1) / kBlock + 2;
-    if (nblk < min_blocks + 2) nblk = min_blocks + 2;
-    if (nblk < e->cap_blocks + 2) nblk = e->cap_blocks + 2;
+    const uint64_t nblk = (fr + kBlock - 1) / kBlock + 2;
     const uint64_t ngrp = nblk / kBlock + 2;
     size_t off_agg = 0;
     size_t off_grp = align_up(off_agg + nblk * sizeof(ScanElem), 256);
@@ -3220,7 +2921,7 @@ static int reserve_ws(uvhttp_ws_gpu_engine_t* e, uint32_t max_frames, uint64_t m
         if (e->ws_mem) (void)hipFree(e->ws_mem);
         e->ws_mem = nullptr;
         e->cap_frames = 0;
-        e->cap_tiles = e->cap_arena_tiles = e->cap_blocks = 0;
+        e->cap_tiles = e->cap_arena_tiles = 0;
         return set_err(e, UVHTTP_WS_GPU_ENOMEM, "hipMalloc workspace", h);
     }
     char* b = (char*)e->ws_mem;
@@ -3239,14 +2940,7 @@ static int reserve_ws(uvhttp_ws_gpu_engine_t* e, uint32_t max_frames, uint64_t m
     e->cap_frames = fr;
     e->cap_tiles = tl;
     e->cap_arena_tiles = at;
-    e->cap_blocks = nblk - 2;
     return UVHTTP_WS_GPU_OK;
-}
-
-int uvhttp_ws_gpu_engine_reserve(uvhttp_ws_gpu_engine_t* e, uint32_t max_frames,
-                                 uint64_t max_wire_bytes, uint64_t max_arena_bytes) {
-    if (!e) return UVHTTP_WS_GPU_EINVAL;
-    return reserve_ws(e, max_frames, max_wire_bytes, max_arena_bytes, 0);
 }
 
 int uvhttp_ws_gpu_engine_set_tile(uvhttp_ws_gpu_engine_t* e, int block, int vectors_per_lane) {
@@ -3379,39 +3073,6 @@ static void launch_plan(uvhttp_ws_gpu_engine_t* e, BatchArgs& a, uint32_t n_cap,
     }
 }
 
-// k_decode_stride + k_stride_tail for an in-place fixed-stride batch of small frames: frames
-// per block as many as fit in 256 x VPL 16-byte vectors (at most 256), every offset of a
-// block (and the last frame's slot) below 16 MiB
-static bool launch_stride_decode(uvhttp_ws_gpu_engine_t* e, BatchArgs& a,
-                                 uvhttp_ws_frame_desc_t* d_desc, hipStream_t s) {
-    if (e->stride_mode == 0 || a.arena || a.frame_off || a.n == 0 || a.wire_len == 0) return false;
-    const uint64_t st = a.frame_stride;
-    const uint64_t span = (uint64_t)kBlock * e->stride_u * 16 - 16;  // one round of loads
-    if (st == 0 || st > span) return false;
-    if (e->stride_mode == 2 && st > kStrideAutoMax) return false;
-    uint32_t fpb = (uint32_t)(span / st);
-    if (fpb > (uint32_t)kBlock) fpb = kBlock;
-    uint64_t last0 = (uint64_t)((a.n - 1) / fpb) * fpb * st;
-    if (last0 > a.wire_len) last0 = a.wire_len;
-    if (a.wire_len - last0 > kStrideSpanMax) return false;
-    const uint32_t grid = (a.n + fpb - 1) / fpb;
-    if (reserve_ws(e, a.n, a.wire_len, 0, grid) != UVHTTP_WS_GPU_OK) return false;
-    a.plan_frames = fpb;
-    a.n_tiles = 0;  // no tile maps: resolve_one claims none
-    const float inv_s = 1.0f / (float)st;
-    const int tk = timing_begin(e, s);
-    if (e->stride_u == 2)
-        hipLaunchKernelGGL(k_decode_stride<2>, dim3(grid), dim3(kBlock), 0, s, a, d_desc, e->ws, fpb, inv_s);
-    else if (e->stride_u == 8)
-        hipLaunchKernelGGL(k_decode_stride<8>, dim3(grid), dim3(kBlock), 0, s, a, d_desc, e->ws, fpb, inv_s);
-    else
-        hipLaunchKernelGGL(k_decode_stride<4>, dim3(grid), dim3(kBlock), 0, s, a, d_desc, e->ws, fpb, inv_s);
-    timing_end(e, tk, s);
-    const uint32_t tgrid = (a.n + kBlock - 1) / kBlock < 1024 ? (a.n + kBlock - 1) / kBlock : 1024;
-    hipLaunchKernelGGL(k_stride_tail, dim3(tgrid), dim3(kBlock), 0, s, a, d_desc, e->ws);
-    return true;
-}
-
 static int check_batch(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b,
                        const void* d_desc, const void* d_summary) {
     if (!e || !b || !d_desc || !d_summary) return UVHTTP_WS_GPU_EINVAL;
@@ -3462,12 +3123,6 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
     a.dev_epoch = e->capturing ? 1u : 0u;
     a.epoch = next_epoch(e, s);
 
-    if (launch_stride_decode(e, a, d_desc, s)) {
-        const hipError_t h = hipGetLastError();
-        if (prev != e->device) (void)hipSetDevice(prev);
-        if (h != hipSuccess) return set_err(e, UVHTTP_WS_GPU_ELAUNCH, "launch", h);
-        return UVHTTP_WS_GPU_OK;
-    }
     launch_plan(e, a, a.n, d_desc, d_msgs, s);
     // payload kernel tile shape: explicit (set_tile) or by average wire bytes per frame
     // (auto shapes from tools/tile_sweep.py on MI355X, profiles/r01_tile_sweep.txt)
