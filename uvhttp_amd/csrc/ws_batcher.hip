@@ -7,8 +7,11 @@
 // as those calls would: the device path stages recv_buffer[0, recv_buffer_pos) + the reads
 // per connection with a read table (one entry per call) and runs uvhttp_ws_gpu_decode_reads;
 // uvhttp_ws_deliver_stream replays the callbacks and the buffer / fragment state.  Small
-// flushes run the host decoder (the product's ws_host.c) read by read.  Host code only: no
-// kernels live here.
+// flushes run the host decoder (the product's ws_host.c) read by read.
+// With a device, reads are queued straight into a pinned arena in arrival order; a flush
+// uploads the arena once and k_batcher_gather lays every connection's bytes out contiguously
+// in device memory (the host never re-copies the reads into the decode layout: that staging
+// memcpy, 256 MiB per flush on the loop thread, was most of a flush's time).
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -38,12 +41,27 @@ struct ConnSlot {
 
 inline uint64_t align16(uint64_t x) { return (x + 15) & ~(uint64_t)15; }
 
+struct GatherSeg {  // arena[src, src + len) -> wire[dst, dst + len)
+    uint64_t src, dst, len;
+};
+
+// one workgroup per segment (a read, or a connection's recv-buffer prefix); byte copies with
+// consecutive lanes on consecutive bytes (source and destination alignments differ per read)
+__global__ __launch_bounds__(256) void k_batcher_gather(const uint8_t* __restrict__ arena,
+                                                        uint8_t* __restrict__ wire,
+                                                        const GatherSeg* __restrict__ seg) {
+    const GatherSeg g = seg[blockIdx.x];
+    for (uint64_t i = threadIdx.x; i < g.len; i += 256) wire[g.dst + i] = arena[g.src + i];
+}
+
 }  // namespace
 
 struct uvhttp_ws_amd_batcher {
     uvhttp_ws_amd_batcher_config_t cfg;
     // queue of the current flush
-    std::vector<uint8_t> arena;
+    std::vector<uint8_t> arena;  // host-only batcher: the queued reads
+    uint8_t* h_arena;            // device batcher: the queued reads, pinned (wire_cap bytes)
+    uint64_t arena_len;
     std::vector<QueuedRead> reads;
     std::vector<ConnSlot> slots;
     std::unordered_map<uvhttp_ws_connection_t*, uint32_t> slot_of;
@@ -60,8 +78,27 @@ struct uvhttp_ws_amd_batcher {
     uvhttp_ws_stream_result_t *h_results, *d_results;
     uint64_t *h_read_end, *d_read_end;
     uvhttp_ws_frame_desc_t *h_desc, *d_desc;
+    uint8_t* d_arena;
+    GatherSeg *h_seg, *d_seg;
     uvhttp_ws_amd_batcher_stats_t st;
 };
+
+static uint8_t* arena_data(uvhttp_ws_amd_batcher_t* b) {
+    return b->h_arena ? b->h_arena : b->arena.data();
+}
+
+// append len bytes to the queue's arena; returns their offset
+static uint64_t arena_append(uvhttp_ws_amd_batcher_t* b, const uint8_t* data, size_t len) {
+    if (!b->h_arena) {
+        const uint64_t off = b->arena.size();
+        b->arena.insert(b->arena.end(), data, data + len);
+        return off;
+    }
+    const uint64_t off = b->arena_len;
+    if (len) memcpy(b->h_arena + off, data, len);
+    b->arena_len += len;
+    return off;
+}
 
 static void release(uvhttp_ws_amd_batcher_t* b) {
     if (b->eng) {
@@ -74,6 +111,10 @@ static void release(uvhttp_ws_amd_batcher_t* b) {
         (void)hipHostFree(b->h_results);
         (void)hipHostFree(b->h_read_end);
         (void)hipHostFree(b->h_desc);
+        (void)hipHostFree(b->h_arena);
+        (void)hipHostFree(b->h_seg);
+        (void)hipFree(b->d_arena);
+        (void)hipFree(b->d_seg);
         (void)hipFree(b->d_wire);
         (void)hipFree(b->d_streams);
         (void)hipFree(b->d_results);
@@ -88,6 +129,7 @@ static void release(uvhttp_ws_amd_batcher_t* b) {
 
 static void clear_queue(uvhttp_ws_amd_batcher_t* b) {
     b->arena.clear();
+    b->arena_len = 0;
     b->reads.clear();
     b->slots.clear();
     b->slot_of.clear();
@@ -110,7 +152,7 @@ static void flush_host(uvhttp_ws_amd_batcher_t* b) {
             if (s.dropped) break;
             const QueuedRead& q = b->reads[r];
             const uvhttp_error_t rc =
-                uvhttp_ws_process_data(s.conn, b->arena.data() + q.off, (size_t)q.len);
+                uvhttp_ws_process_data(s.conn, arena_data(b) + q.off, (size_t)q.len);
             b->st.host_reads++;
             if (rc != UVHTTP_OK) report_failure(b, s, rc);
         }
@@ -123,7 +165,7 @@ static void flush_host(uvhttp_ws_amd_batcher_t* b) {
 static int flush_device(uvhttp_ws_amd_batcher_t* b) {
     const auto t0 = std::chrono::steady_clock::now();
     uint64_t pos = 0;
-    uint32_t nr = 0, nk = 0;
+    uint32_t nr = 0, nk = 0, nseg = 0;
     std::vector<uint32_t> slot_k(b->slots.size(), UINT32_MAX);
     for (size_t k = 0; k < b->slots.size(); ++k) {
         ConnSlot& s = b->slots[k];
@@ -131,12 +173,15 @@ static int flush_device(uvhttp_ws_amd_batcher_t* b) {
         uvhttp_ws_connection_t* c = s.conn;
         pos = align16(pos);
         const uint64_t begin = pos;
-        if (c->recv_buffer_pos) memcpy(b->h_wire + pos, c->recv_buffer, c->recv_buffer_pos);
+        if (c->recv_buffer_pos) {  // the bytes recv_buffer already holds come first
+            const uint64_t off = arena_append(b, c->recv_buffer, c->recv_buffer_pos);
+            b->h_seg[nseg++] = GatherSeg{off, pos, c->recv_buffer_pos};
+        }
         pos += c->recv_buffer_pos;
         const uint32_t r0 = nr;
         for (uint32_t r : s.reads) {
             const QueuedRead& q = b->reads[r];
-            if (q.len) memcpy(b->h_wire + pos, b->arena.data() + q.off, q.len);
+            if (q.len) b->h_seg[nseg++] = GatherSeg{q.off, pos, q.len};
             pos += q.len;
             b->h_read_end[nr++] = pos - begin;
         }
@@ -171,7 +216,14 @@ static int flush_device(uvhttp_ws_amd_batcher_t* b) {
     }
     hipStream_t s = b->stream;
     int rc = UVHTTP_WS_GPU_OK;
-    hipError_t h = hipMemcpyAsync(b->d_wire, b->h_wire, pos, hipMemcpyHostToDevice, s);
+    hipError_t h = hipMemcpyAsync(b->d_arena, b->h_arena, b->arena_len, hipMemcpyHostToDevice, s);
+    if (h == hipSuccess && nseg)
+        h = hipMemcpyAsync(b->d_seg, b->h_seg, nseg * sizeof(GatherSeg), hipMemcpyHostToDevice, s);
+    if (h == hipSuccess && nseg) {
+        hipLaunchKernelGGL(k_batcher_gather, dim3(nseg), dim3(256), 0, s, b->d_arena, b->d_wire,
+                           b->d_seg);
+        h = hipGetLastError();
+    }
     if (h == hipSuccess)
         h = hipMemcpyAsync(b->d_streams, b->h_streams, nk * sizeof(uvhttp_ws_stream_t),
                            hipMemcpyHostToDevice, s);
@@ -248,7 +300,7 @@ int uvhttp_ws_amd_batcher_create(const uvhttp_ws_amd_batcher_config_t* cfg,
     if (!b) return UVHTTP_WS_GPU_ENOMEM;
     b->cfg = *cfg;
     memset(&b->st, 0, sizeof(b->st));
-    b->arena.reserve(cfg->max_bytes < (64ull << 20) ? cfg->max_bytes : (64ull << 20));
+    if (cfg->device < 0) b->arena.reserve(cfg->max_bytes < (64ull << 20) ? cfg->max_bytes : (64ull << 20));
     if (cfg->device >= 0) {
         int rc = uvhttp_ws_gpu_engine_create(cfg->device, &b->eng);
         if (rc) {
@@ -273,7 +325,11 @@ int uvhttp_ws_amd_batcher_create(const uvhttp_ws_amd_batcher_config_t* cfg,
                   hipMalloc((void**)&b->d_streams, ns * sizeof(uvhttp_ws_stream_t)) == hipSuccess &&
                   hipMalloc((void**)&b->d_results, ns * sizeof(uvhttp_ws_stream_result_t)) == hipSuccess &&
                   hipMalloc((void**)&b->d_read_end, cfg->max_reads * sizeof(uint64_t)) == hipSuccess &&
-                  hipMalloc((void**)&b->d_desc, (size_t)b->max_frames * sizeof(uvhttp_ws_frame_desc_t)) == hipSuccess;
+                  hipMalloc((void**)&b->d_desc, (size_t)b->max_frames * sizeof(uvhttp_ws_frame_desc_t)) == hipSuccess &&
+                  hipHostMalloc((void**)&b->h_arena, b->wire_cap, hipHostMallocDefault) == hipSuccess &&
+                  hipMalloc((void**)&b->d_arena, b->wire_cap) == hipSuccess &&
+                  hipHostMalloc((void**)&b->h_seg, ((size_t)cfg->max_reads + ns) * sizeof(GatherSeg), hipHostMallocDefault) == hipSuccess &&
+                  hipMalloc((void**)&b->d_seg, ((size_t)cfg->max_reads + ns) * sizeof(GatherSeg)) == hipSuccess;
         if (ok) ok = uvhttp_ws_gpu_engine_reserve(b->eng, b->max_frames, b->wire_cap, 0) == 0;
         (void)hipSetDevice(prev);
         if (!ok) {
@@ -343,8 +399,7 @@ uvhttp_error_t uvhttp_ws_amd_batcher_submit_read(uvhttp_ws_amd_batcher_t* b,
     } else {
         k = it->second;
     }
-    const uint64_t off = b->arena.size();
-    b->arena.insert(b->arena.end(), data, data + len);
+    const uint64_t off = arena_append(b, data, len);
     b->reads.push_back(QueuedRead{off, len});
     b->slots[k].reads.push_back((uint32_t)(b->reads.size() - 1));
     b->slots[k].bytes += len;
