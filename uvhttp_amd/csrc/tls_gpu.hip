@@ -1224,24 +1224,33 @@ __device__ inline void fill_te(const uint32_t* te0, uint32_t* te) {
 #define TLS_WG_TREE 1      // 1: the lane combine of the workgroup's 4 records shared through LDS
 #endif
 
-// Packed ChaCha20-Poly1305 open for records up to 8 KiB: a group of kPack consecutive work
-// items shares one wave, kSeg lanes per record (segment k = lanes [k kSeg, (k+1) kSeg)), so a
+// Packed ChaCha20-Poly1305 open for records up to 8 KiB: 64 / SEG consecutive work items
+// share one wave, SEG lanes per record (segment k = lanes [k SEG, (k+1) SEG)), so a
 // small record no longer costs a whole wave round of the block function plus its own one-time
 // key, key powers and lane combine.  Same structure as chacha_record within each segment: lane
-// u of round j takes chunk kSeg j + u, the round's ciphertext goes through the wave's LDS window,
-// Poly1305 block b of the record is Horner-accumulated by lane b % kSeg (multiplier r^kSeg),
-// and the segment's lanes combine after the rotation by R = nct mod kSeg in log2(kSeg) shuffle
+// u of round j takes chunk SEG j + u, the round's ciphertext goes through the wave's LDS window,
+// Poly1305 block b of the record is Horner-accumulated by lane b % SEG (multiplier r^SEG),
+// and the segment's lanes combine after the rotation by R = nct mod SEG in log2(SEG) shuffle
 // levels confined to the segment.  Record parameters live in vector registers (they differ
 // between segments).
-constexpr int kSeg = 16;
-constexpr int kPack = 64 / kSeg;
-constexpr int kSegLog = 4;
-static_assert((1 << kSegLog) == kSeg, "segment size");
+// kPack: the record groups both AEADs route by (a group holding a long record goes to the
+// one-record-per-wave kernel); TLS_CC_SEG: lanes per record in the packed ChaCha20-Poly1305
+// kernel (16 records per wave at 4: a 256-byte record has four 64-byte chunks, so 16-lane
+// segments left 12 lanes idle in the block function)
+constexpr int kPack = 4;
+#ifndef TLS_CC_SEG
+#define TLS_CC_SEG 4
+#endif
+constexpr int kCcSeg = TLS_CC_SEG;
+constexpr int kCcSegLog = kCcSeg == 16 ? 4 : kCcSeg == 8 ? 3 : 2;
+constexpr int kCcPackW = 64 / kCcSeg;  // records per wave
+static_assert((1 << kCcSegLog) == kCcSeg && kCcPackW % kPack == 0, "ChaCha segment size");
 
+template <int SEG>
 __device__ inline P130 shfl_seg(const P130& v, int src) {
     P130 r;
 #pragma unroll
-    for (int i = 0; i < 5; ++i) r.h[i] = __shfl(v.h[i], src, kSeg);
+    for (int i = 0; i < 5; ++i) r.h[i] = __shfl(v.h[i], src, SEG);
     return r;
 }
 
@@ -1286,10 +1295,23 @@ __device__ inline bool group_has_long(const TlsArgs& a, uint32_t g, uint32_t n,
     return __builtin_amdgcn_readfirstlane(__ballot(big) != 0 ? 1u : 0u) != 0;
 }
 
+// records r0 .. r0 + 64/SEG - 1, each skipped when its group of kPack holds a long ChaCha
+// record (that group goes to k_tls_open_chacha)
+template <int SEG, int LOG>
 __device__ void chacha_open_packed(const TlsArgs& a, uint32_t r0, uint8_t* win) {
-    const uint32_t lane = threadIdx.x & 63, k = lane / kSeg, u = lane % kSeg;
+    const uint32_t lane = threadIdx.x & 63, k = lane / SEG, u = lane % SEG;
     const uint32_t r = r0 + k;
-    bool act = r < a.n_total[0];
+    const uint32_t n = a.n_total[0];
+    bool big = false;
+    if (lane < 64u / SEG && r0 + lane < n) {
+        const RecWork wb = a.work[r0 + lane];
+        big = wb.walk_status == 0 && wb.len > kPackMaxLen &&
+              a.sched[wb.key].cipher == UVHTTP_TLS_CIPHER_CHACHA20_POLY1305;
+    }
+    const uint64_t bigm = __ballot(big);
+    const uint32_t gfirst = (r0 / kPack) * kPack;  // (r0 is a multiple of kPack)
+    const bool grp_long = ((bigm >> ((r - gfirst) / kPack * kPack)) & ((1ull << kPack) - 1)) != 0;
+    bool act = r < n && !grp_long;
     RecWork w;
     if (act) {
         w = a.work[r];
@@ -1330,13 +1352,13 @@ __device__ void chacha_open_packed(const TlsArgs& a, uint32_t r0, uint8_t* win) 
     chacha_block(key, 0, nonce, x);  // the segment's one-time key
     const uint32_t rw[4] = {x[0] & 0x0fffffffu, x[1] & 0x0ffffffcu, x[2] & 0x0ffffffcu, x[3] & 0x0ffffffcu};
     const uint32_t sw[4] = {x[4], x[5], x[6], x[7]};
-    P130 pr[kSegLog + 1];  // r^(2^t), t = 0..log2(kSeg)
+    P130 pr[LOG + 1];  // r^(2^t), t = 0..log2(SEG)
     pr[0] = p_from_le16(rw, 0);
 #pragma unroll
-    for (int t = 1; t <= kSegLog; ++t) pr[t] = p_mul(pr[t - 1], pr[t - 1]);
+    for (int t = 1; t <= LOG; ++t) pr[t] = p_mul(pr[t - 1], pr[t - 1]);
     const uint32_t nct = (clen + 15) / 16;
     const uint32_t nchunk = (clen + 63) / 64;
-    uint32_t J = (nchunk + kSeg - 1) / kSeg;  // rounds this segment needs; the wave runs the max
+    uint32_t J = (nchunk + SEG - 1) / SEG;  // rounds this segment needs; the wave runs the max
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {
         const uint32_t o = __shfl_xor(J, d, 64);
@@ -1346,7 +1368,7 @@ __device__ void chacha_open_packed(const TlsArgs& a, uint32_t r0, uint8_t* win) 
     P130 acc{{0, 0, 0, 0, 0}};
     LastNz nz{0, {0, 0, 0, 0}};
     for (uint32_t j = 0; j < J; ++j) {
-        const uint32_t chunk = kSeg * j + u;
+        const uint32_t chunk = SEG * j + u;
         const uint32_t off = 64 * chunk;
         uint32_t d[16];
         if (chunk < nchunk) {
@@ -1391,24 +1413,24 @@ __device__ void chacha_open_packed(const TlsArgs& a, uint32_t r0, uint8_t* win) 
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const uint32_t blk = 4 * kSeg * j + kSeg * q + u;  // the record's Poly1305 block
+            const uint32_t blk = 4 * SEG * j + SEG * q + u;  // the record's Poly1305 block
             if (blk < nct) {
-                const uint4 c4 = *reinterpret_cast<const uint4*>(win + 64 * kSeg * k + 16 * (kSeg * q + u));
+                const uint4 c4 = *reinterpret_cast<const uint4*>(win + 64 * SEG * k + 16 * (SEG * q + u));
                 const uint32_t cw[4] = {c4.x, c4.y, c4.z, c4.w};
                 P130 c = p_from_le16(cw, 1u << 24);
                 if (blk == 0) c = p_add(p_mul(p_from_le16(aad16, 1u << 24), pr[0]), c);
-                acc = blk < kSeg ? c : p_add(p_mul(acc, pr[kSegLog]), c);
+                acc = blk < SEG ? c : p_add(p_mul(acc, pr[LOG]), c);
             }
         }
     }
-    // T = sum over the segment's lanes of A_u r^((R - 1 - u) mod kSeg); rank i = lane (i + R)
-    const uint32_t R = nct ? nct - kSeg * ((nct - 1) / kSeg) : 0;
-    P130 b = shfl_seg(acc, (int)((u + R) & (kSeg - 1)));
+    // T = sum over the segment's lanes of A_u r^((R - 1 - u) mod SEG); rank i = lane (i + R)
+    const uint32_t R = nct ? nct - SEG * ((nct - 1) / SEG) : 0;
+    P130 b = shfl_seg<SEG>(acc, (int)((u + R) & (SEG - 1)));
 #pragma unroll
-    for (int t = 0; t < kSegLog; ++t) {
+    for (int t = 0; t < LOG; ++t) {
         P130 right;
 #pragma unroll
-        for (int i = 0; i < 5; ++i) right.h[i] = __shfl_down(b.h[i], 1 << t, kSeg);
+        for (int i = 0; i < 5; ++i) right.h[i] = __shfl_down(b.h[i], 1 << t, SEG);
         b = p_add(p_mul(b, pr[t]), right);
     }
     P130 total = nct ? p_mul(b, pr[0]) : p_mul(p_from_le16(aad16, 1u << 24), pr[0]);
@@ -1418,8 +1440,8 @@ __device__ void chacha_open_packed(const TlsArgs& a, uint32_t r0, uint8_t* win) 
     p_tag(total, sw, tag);
     uint32_t last_nz = nz.resolve();
 #pragma unroll
-    for (int d = kSeg / 2; d >= 1; d >>= 1) {
-        const uint32_t o = __shfl_xor(last_nz, d, kSeg);
+    for (int d = SEG / 2; d >= 1; d >>= 1) {
+        const uint32_t o = __shfl_xor(last_nz, d, SEG);
         if (o > last_nz) last_nz = o;
     }
     if (act && u == 0) {
@@ -1783,8 +1805,8 @@ k_tls_open_chacha_packed(TlsArgs a) {
     if (!(a.n_total[2] & 4u)) return;  // no short ChaCha20-Poly1305 record
     const uint32_t n = a.n_total[0];
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    for (uint32_t g = blockIdx.x * kCryptWaves + wave; g * kPack < n; g += gridDim.x * kCryptWaves)
-        if (!group_has_long(a, g, n)) chacha_open_packed(a, g * kPack, win);
+    for (uint32_t g = blockIdx.x * kCryptWaves + wave; g * kCcPackW < n; g += gridDim.x * kCryptWaves)
+        chacha_open_packed<kCcSeg, kCcSegLog>(a, g * kCcPackW, win);
 }
 
 // seal descriptor r checked against the contract (key slot, key, content size, buffers) and
