@@ -1468,8 +1468,11 @@ __device__ inline U128 shfl_down128_w(U128 v, int d) {
     return U128{((uint64_t)b << 32) | a, ((uint64_t)e << 32) | c};
 }
 
-constexpr int kAesSeg = 4;                   // lanes per record in k_tls_open_aes_packed
-constexpr int kAesSegLog = 2;
+#ifndef TLS_AES_SEG
+#define TLS_AES_SEG 4
+#endif
+constexpr int kAesSeg = TLS_AES_SEG;         // lanes per record in k_tls_open_aes_packed
+constexpr int kAesSegLog = kAesSeg == 16 ? 4 : kAesSeg == 8 ? 3 : kAesSeg == 4 ? 2 : 1;
 constexpr int kAesPackW = 64 / kAesSeg;      // records per wave
 static_assert((1 << kAesSegLog) == kAesSeg && kAesPackW % kPack == 0, "AES segment size");
 
