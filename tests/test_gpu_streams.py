@@ -27,14 +27,16 @@ def torch():
     return t
 
 
-@pytest.fixture(scope="module", params=["lane", "wave", "wave-twopass"])
+@pytest.fixture(scope="module", params=["lane", "wave", "wave-norec", "wave-twopass"])
 def eng(torch, request):
     """Every frame-discovery walk (a lane per connection; a wave per connection, single pass
-    through the offset scratch or the two-walk fallback) must decode alike."""
+    through the offset scratch — with the fast path's frame records or re-reading every header
+    in k_stream_desc — or the two-walk fallback) must decode alike."""
     import os
     import uvhttp_amd as U
     env = {"UVHTTP_WS_WALK": request.param.split("-")[0],
-           "UVHTTP_WS_WALK_SINGLE": "0" if request.param.endswith("twopass") else "1"}
+           "UVHTTP_WS_WALK_SINGLE": "0" if request.param.endswith("twopass") else "1",
+           "UVHTTP_WS_WALK_REC": "0" if request.param.endswith("norec") else "1"}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:

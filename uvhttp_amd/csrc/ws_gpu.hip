@@ -229,6 +229,8 @@ struct StreamScratch {
     uint32_t* n_total;     // [1] frames found (0 on capacity overflow)
     uint64_t* read_size;   // [n_reads_total] recv-buffer size after each call
     uint32_t* walk_tmp;    // single pass: per-connection slices of 32-bit frame starts
+    uint2* walk_rec;       // single pass, wave walk (or null): per start, the frame's key and
+                           // header bytes when the walk's fast path parsed them (kNoRec: not)
     uint32_t* agg;         // [n_streams / 256 + 1] lane walk block counts -> prefixes
 };
 
@@ -1635,6 +1637,22 @@ __device__ inline uint64_t slice_base(const uvhttp_ws_stream_t& st, uint32_t s) 
     return st.begin / 2 + s;
 }
 
+// Frame records of the wave walk's fast path (walk_rec, parallel to walk_tmp): the masking key
+// and b0 | b1 << 8 | payload length << 16 for a frame with a 7- or 16-bit length, so
+// k_stream_desc builds that frame's descriptor without gathering its header from HBM again
+// (C4 streams: the gather was most of k_stream_desc).  kNoRec: the header must be re-read.
+constexpr uint32_t kNoRec = 0xFFFFFFFFu;
+
+// the 16-byte header image of a recorded frame (what load16_at would return for its header)
+__device__ inline u32x4 rec_header(uint2 r) {
+    const uint32_t b0 = r.y & 0xFF, b1 = (r.y >> 8) & 0xFF, plen = r.y >> 16;
+    const uint32_t key = r.x;
+    if ((b1 & 0x7F) == 126) {  // b0 b1 len_hi len_lo key0..3
+        return u32x4{b0 | (b1 << 8) | ((plen >> 8) << 16) | ((plen & 0xFF) << 24), key, 0u, 0u};
+    }
+    return u32x4{b0 | (b1 << 8) | (key << 16), key >> 16, 0u, 0u};  // b0 b1 key0..3
+}
+
 // ---- lane walk: one lane per connection, headers straight from global memory -------------
 // MODE 0: count; 1: write starts to frame_off from the connection's first frame (two-pass);
 // 2: count and write starts into the connection's slice (single pass)
@@ -1766,13 +1784,17 @@ __device__ inline void walk_wave(const WalkArgs& w, uint32_t s, uint8_t* ring) {
     u32x4 pf[kWalkVec];    // block cur + 2, in flight
     // frame start records: one lane per frame (the fast path below stores a run of frames, one
     // per lane, in one instruction)
-    auto emit_lane = [&](uint64_t pos, uint32_t idx, bool on) {
+    auto emit_lane = [&](uint64_t pos, uint32_t idx, bool on, uint2 rec) {
         if (MODE == 0 || !on) return;
         const uint64_t f = first + idx;
-        if (MODE == 2) w.sc.walk_tmp[f] = (uint32_t)pos;
-        else if (f < w.max_frames) w.sc.frame_off[f] = st.begin + pos;
+        if (MODE == 2) {
+            w.sc.walk_tmp[f] = (uint32_t)pos;
+            if (w.sc.walk_rec) w.sc.walk_rec[f] = rec;
+        } else if (f < w.max_frames) {
+            w.sc.frame_off[f] = st.begin + pos;
+        }
     };
-    auto emit = [&](uint64_t pos, uint32_t idx) { emit_lane(pos, idx, lane == 0); };
+    auto emit = [&](uint64_t pos, uint32_t idx) { emit_lane(pos, idx, lane == 0, uint2{0u, kNoRec}); };
     const ConnState c = walk_calls(
         w, st,
         [&](uint64_t pos, uint32_t hb[10]) {
@@ -1843,13 +1865,20 @@ __device__ inline void walk_wave(const WalkArgs& w, uint32_t s, uint8_t* ring) {
                 for (int q = 0; q < 10; ++q) hb[q] = ring[r + q];
                 decode(hb, b0, wl, plen, bad);
             };
-            auto parse_global = [&](uint64_t p, uint32_t& b0, uint32_t& wl, uint64_t& plen, bool& bad) {
+            // (also the frame's record for k_stream_desc: key and header bytes, kNoRec for a
+            // 64-bit length)
+            auto parse_global = [&](uint64_t p, uint32_t& b0, uint32_t& wl, uint64_t& plen, bool& bad,
+                                    uint2& rec) {
                 const u32x4 v = load16_at(w.wire, w.wire_len, st.begin + p);
                 const uint32_t x[4] = {v.x, v.y, v.z, v.w};
                 uint32_t hb[10];
 #pragma unroll
                 for (int q = 0; q < 10; ++q) hb[q] = (x[q >> 2] >> (8 * (q & 3))) & 0xFF;
                 decode(hb, b0, wl, plen, bad);
+                const uint32_t code = hb[1] & 0x7F;
+                const uint32_t key = code < 126 ? (v.x >> 16) | (v.y << 16) : v.y;  // bytes 2-5 / 4-7
+                rec = code < 127 ? uint2{(hb[1] & 0x80) ? key : 0u, hb[0] | (hb[1] << 8) | ((uint32_t)plen << 16)}
+                                 : uint2{0u, kNoRec};
             };
             uint32_t wlp = 0;          // the previous step's frame length
             bool have0 = false;        // frame 0's header carried from the previous step
@@ -1892,13 +1921,14 @@ __device__ inline void walk_wave(const WalkArgs& w, uint32_t s, uint8_t* ring) {
                 const uint32_t kind = !data0 ? 0u : (op0 != 0 && fin0) ? 1u : (op0 == 0 && !fin0) ? 2u : 3u;
                 uint32_t n = 1;
                 have0 = false;
+                uint2 recl{0u, kNoRec};  // lane l's frame record (frame 0's header is not re-read here)
                 if (kind != 3 && wl0 == wlp) {
                     const uint64_t pl = (uint64_t)pos + (uint64_t)lane * wl0;  // frame `lane`
                     uint32_t b0l = 0, wll = 0;
                     uint64_t plenl = 0;
                     bool badl = true;
                     const bool hdr_in = lane > 0 && pl + 10 <= end32;
-                    if (hdr_in) parse_global(pl, b0l, wll, plenl, badl);
+                    if (hdr_in) parse_global(pl, b0l, wll, plenl, badl, recl);
                     const bool okl = lane == 0 ||
                                      (hdr_in && pl + wl0 <= end32 && !badl && b0l == b00 && wll == wl0 &&
                                       plenl == plen0 &&
@@ -1920,7 +1950,7 @@ __device__ inline void walk_wave(const WalkArgs& w, uint32_t s, uint8_t* ring) {
                         }
                     }
                 }
-                emit_lane((uint64_t)pos + (uint64_t)lane * wl0, cnt + lane, lane < n);
+                emit_lane((uint64_t)pos + (uint64_t)lane * wl0, cnt + lane, lane < n, recl);
                 if (kind == 2) {
                     acc += (uint64_t)n * plen0;
                 } else if (kind == 3) {  // one frame: a start without FIN or a final fragment
@@ -2097,14 +2127,18 @@ __global__ __launch_bounds__(kBlock) void k_stream_desc(WalkArgs w) {
     for (uint32_t g0 = 0; g0 < r.n_frames; g0 += 64 * kG) {
         uint64_t pos[kG];
         u32x4 hv[kG];
+        uint2 rec[kG];
 #pragma unroll
         for (int c = 0; c < kG; ++c) {
             const uint32_t k = g0 + 64 * c + lane;
             const bool act = k < r.n_frames;
             pos[c] = !act ? 0 : w.single ? w.sc.walk_tmp[sb + k] : w.sc.frame_off[r.first_frame + k] - st.begin;
+            rec[c] = act && w.single && w.sc.walk_rec ? w.sc.walk_rec[sb + k] : uint2{0u, kNoRec};
         }
+        // headers the walk recorded are rebuilt from their records; the others are gathered
 #pragma unroll
-        for (int c = 0; c < kG; ++c) hv[c] = load16_at(w.wire, w.wire_len, st.begin + pos[c]);
+        for (int c = 0; c < kG; ++c)
+            hv[c] = rec[c].y != kNoRec ? rec_header(rec[c]) : load16_at(w.wire, w.wire_len, st.begin + pos[c]);
 #pragma unroll
         for (int c = 0; c < kG; ++c) {
             if (g0 + 64 * c >= r.n_frames) break;  // (uniform)
@@ -2743,6 +2777,9 @@ struct uvhttp_ws_gpu_engine {
     StreamScratch ss;
     void* wt_mem;              // single-pass walk scratch (frame starts per connection slice)
     uint64_t wt_cap;
+    void* wr_mem;              // the wave walk's frame records (parallel to wt_mem)
+    uint64_t wr_cap;
+    int wr_rec_on;             // UVHTTP_WS_WALK_REC=0: k_stream_desc gathers every header (A/B)
     int walk_single_off;       // UVHTTP_WS_WALK_SINGLE=0: always walk twice (tests, A/B)
     void* bs_mem;              // send-side output-map records (BuildRec per map tile)
     uint64_t bs_tiles;
@@ -2830,6 +2867,8 @@ int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out) {
     if (const char* cm = getenv("UVHTTP_WS_COMPACT"))
         e->compact_mode = strcmp(cm, "gather") == 0 ? 1 : strcmp(cm, "scatter") == 0 ? 2 : 0;
     if (const char* ws = getenv("UVHTTP_WS_WALK_SINGLE")) e->walk_single_off = atoi(ws) == 0;
+    e->wr_rec_on = 1;
+    if (const char* wr = getenv("UVHTTP_WS_WALK_REC")) e->wr_rec_on = atoi(wr) != 0;
     if (const char* wm = getenv("UVHTTP_WS_WALK"))
         e->walk_mode = strcmp(wm, "lane") == 0 ? 1 : strcmp(wm, "wave") == 0 ? 2 : 0;
     *out = e;
@@ -2845,6 +2884,7 @@ void uvhttp_ws_gpu_engine_free(uvhttp_ws_gpu_engine_t* e) {
     if (e->ss_mem) (void)hipFree(e->ss_mem);
     if (e->bs_mem) (void)hipFree(e->bs_mem);
     if (e->wt_mem) (void)hipFree(e->wt_mem);
+    if (e->wr_mem) (void)hipFree(e->wr_mem);
     if (e->ctl) (void)hipFree(e->ctl);
     if (e->order_ev) (void)hipEventDestroy(e->order_ev);
     for (int k = 0; k < e->ev_created; ++k) (void)hipEventDestroy(e->ev[k]);
@@ -3279,6 +3319,14 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
         e->wt_cap = 0;
         if (hipMalloc(&e->wt_mem, want * 4) == hipSuccess) e->wt_cap = want;
     }
+    // the wave walk's frame records (8 bytes per slice entry) while slices and records stay
+    // within 8 GiB together; larger calls gather every header again in k_stream_desc
+    if (e->walk_single_off == 0 && !e->capturing && want * 12 <= (8ull << 30) && want > e->wr_cap) {
+        if (e->wr_mem) (void)hipFree(e->wr_mem);
+        e->wr_mem = nullptr;
+        e->wr_cap = 0;
+        if (hipMalloc(&e->wr_mem, want * 8) == hipSuccess) e->wr_cap = want;
+    }
     WalkArgs w;
     w.wire = d_wire;
     w.wire_len = wire_len;
@@ -3292,6 +3340,7 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     w.desc = d_desc;
     w.sc = e->ss;
     w.sc.walk_tmp = (uint32_t*)e->wt_mem;
+    w.sc.walk_rec = (w.single && e->wr_cap >= want && e->wr_rec_on) ? (uint2*)e->wr_mem : nullptr;
     w.agg = e->ss.agg;
     const uint32_t nsb = (n_streams + kBlock - 1) / kBlock;
     const uint32_t nwb = (n_streams + kBlock / 64 - 1) / (kBlock / 64);
