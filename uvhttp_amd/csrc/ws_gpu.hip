@@ -257,6 +257,7 @@ struct BatchArgs {
     uint32_t max_polls;      // look-back wait bound (0: give up at the first wait; tests)
     uvhttp_ws_batch_summary_t* summary;  // batch mode: written by k_finalize
     uint32_t plan_frames;    // frames per k_plan block (kBlock * FPT)
+    uint32_t no_ticket;      // k_plan orders blocks by blockIdx (experiment: UVHTTP_WS_PLAN_TICKET=0)
 };
 
 // every kernel of a call resolves its epoch: a captured call reads the one the replay's
@@ -693,10 +694,12 @@ __global__ __launch_bounds__(kBlock) void k_plan(BatchArgs a, uvhttp_ws_frame_de
     resolve_epoch(a, ws);
     __shared__ uint32_t s_ticket;
     if (threadIdx.x == 0) {
-        const uint32_t t =
-            __hip_atomic_fetch_add(&ws.counters[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (t + 1 == gridDim.x)
-            __hip_atomic_store(&ws.counters[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t t = blockIdx.x;
+        if (!a.no_ticket) {
+            t = __hip_atomic_fetch_add(&ws.counters[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (t + 1 == gridDim.x)
+                __hip_atomic_store(&ws.counters[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         s_ticket = t;
     }
     __syncthreads();
@@ -2771,6 +2774,7 @@ struct uvhttp_ws_gpu_engine {
     int store_aux;             // payload store cache policy (0 = nt global store, 18 = sc1|nt)
     uint32_t epoch;            // tag of the latest decode call, 1 .. kMaxEpoch
     int plan_fpt;              // k_plan frames per lane, 0 = automatic
+    uint32_t plan_no_ticket;   // UVHTTP_WS_PLAN_TICKET=0: blockIdx order instead of tickets
     int walk_mode;             // stream frame discovery: 0 automatic, 1 lane, 2 wave
     void* ss_mem;              // stream-decode scratch
     uint32_t ss_frames, ss_reads;
@@ -2856,6 +2860,7 @@ int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out) {
     }
     if (const char* sp = getenv("UVHTTP_WS_STORE_POLICY")) e->store_aux = atoi(sp) == 18 ? 18 : 0;
     if (const char* fp = getenv("UVHTTP_WS_PLAN_FPT")) e->plan_fpt = atoi(fp);
+    if (const char* pt = getenv("UVHTTP_WS_PLAN_TICKET")) e->plan_no_ticket = atoi(pt) == 0;
     // test hook: start near the end of the epoch space to exercise the wrap-around clear
     if (const char* ep = getenv("UVHTTP_WS_EPOCH_START")) {
         const unsigned long v = strtoul(ep, nullptr, 0);
@@ -3103,6 +3108,7 @@ static void launch_plan(uvhttp_ws_gpu_engine_t* e, BatchArgs& a, uint32_t n_cap,
     }
     const uint32_t per = kBlock * fpt;
     a.plan_frames = per;
+    a.no_ticket = e->plan_no_ticket;
     const uint32_t grid = n_cap ? (n_cap + per - 1) / per : 1;
     switch (fpt) {
         case 1: hipLaunchKernelGGL(k_plan<1>, dim3(grid), dim3(kBlock), 0, s, a, d_desc, d_msgs, e->ws); break;
