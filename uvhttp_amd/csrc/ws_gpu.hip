@@ -1888,13 +1888,15 @@ __device__ inline void walk_wave(const WalkArgs& w, uint32_t s, uint8_t* ring) {
             uint32_t cb0 = 0, cwl = 0;  // (its fields)
             uint64_t cplen = 0;
             bool cbad = false;
+            uint2 crec{0u, kNoRec};    // (and its record)
             for (;;) {
                 if (end32 - pos < 10) break;  // (uniform)
                 uint32_t b00, wl0;
                 uint64_t plen0;
                 bool bad0;
+                uint2 rec0{0u, kNoRec};
                 if (have0) {
-                    b00 = cb0, wl0 = cwl, plen0 = cplen, bad0 = cbad;
+                    b00 = cb0, wl0 = cwl, plen0 = cplen, bad0 = cbad, rec0 = crec;
                 } else {
                     // frame 0 from the ring: header in the ring's current block (or, after a
                     // run, in the next one: the ring advances here), else the general code
@@ -1924,36 +1926,40 @@ __device__ inline void walk_wave(const WalkArgs& w, uint32_t s, uint8_t* ring) {
                 const uint32_t kind = !data0 ? 0u : (op0 != 0 && fin0) ? 1u : (op0 == 0 && !fin0) ? 2u : 3u;
                 uint32_t n = 1;
                 have0 = false;
-                uint2 recl{0u, kNoRec};  // lane l's frame record (frame 0's header is not re-read here)
+                uint2 recl{0u, kNoRec};  // lane l: the record of frame l + 1 (its header, parsed)
                 if (kind != 3 && wl0 == wlp) {
-                    const uint64_t pl = (uint64_t)pos + (uint64_t)lane * wl0;  // frame `lane`
+                    // lane l speculates on frame l + 1 (frames 1 .. 64), so the frame after the
+                    // run — the next step's frame 0 — was always read, even after a full run
+                    const uint32_t f = lane + 1;
+                    const uint64_t pl = (uint64_t)pos + (uint64_t)f * wl0;
                     uint32_t b0l = 0, wll = 0;
                     uint64_t plenl = 0;
                     bool badl = true;
-                    const bool hdr_in = lane > 0 && pl + 10 <= end32;
+                    const bool hdr_in = pl + 10 <= end32;
                     if (hdr_in) parse_global(pl, b0l, wll, plenl, badl, recl);
-                    const bool okl = lane == 0 ||
-                                     (hdr_in && pl + wl0 <= end32 && !badl && b0l == b00 && wll == wl0 &&
-                                      plenl == plen0 &&
-                                      (kind != 2 || lim == 0 || acc + (uint64_t)(lane + 1) * plen0 <= lim));
+                    const bool okl = hdr_in && pl + wl0 <= end32 && !badl && b0l == b00 && wll == wl0 &&
+                                     plenl == plen0 &&
+                                     (kind != 2 || lim == 0 || acc + (uint64_t)(f + 1) * plen0 <= lim);
                     const uint64_t good = __ballot(okl);
-                    n = ~good == 0 ? 64u : (uint32_t)__builtin_ctzll(~good);  // leading accepted frames
-                    n = __builtin_amdgcn_readfirstlane(n);
-                    // frame n (the first not taken) is the next step's frame 0 when its header
-                    // was read
-                    if (n < 64) {
-                        const uint32_t hin = __builtin_amdgcn_readlane((uint32_t)hdr_in, n);
-                        if (hin) {
-                            have0 = true;
-                            cb0 = __builtin_amdgcn_readlane(b0l, n);
-                            cwl = __builtin_amdgcn_readlane(wll, n);
-                            cplen = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(plenl >> 32), n) << 32) |
-                                    __builtin_amdgcn_readlane((uint32_t)plenl, n);
-                            cbad = __builtin_amdgcn_readlane((uint32_t)badl, n) != 0;
-                        }
+                    // frame 0 plus the leading accepted frames, at most 64 per step
+                    const uint32_t m = ~good == 0 ? 64u : (uint32_t)__builtin_ctzll(~good);
+                    n = __builtin_amdgcn_readfirstlane(m + 1 < 64u ? m + 1 : 64u);
+                    // frame n (the first not taken) is the next step's frame 0; lane n - 1 read it
+                    const uint32_t hin = __builtin_amdgcn_readlane((uint32_t)hdr_in, n - 1);
+                    if (hin) {
+                        have0 = true;
+                        cb0 = __builtin_amdgcn_readlane(b0l, n - 1);
+                        cwl = __builtin_amdgcn_readlane(wll, n - 1);
+                        cplen = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(plenl >> 32), n - 1) << 32) |
+                                __builtin_amdgcn_readlane((uint32_t)plenl, n - 1);
+                        cbad = __builtin_amdgcn_readlane((uint32_t)badl, n - 1) != 0;
+                        crec = uint2{__builtin_amdgcn_readlane(recl.x, n - 1), __builtin_amdgcn_readlane(recl.y, n - 1)};
                     }
                 }
-                emit_lane((uint64_t)pos + (uint64_t)lane * wl0, cnt + lane, lane < n, recl);
+                // lane l emits frame l: its record is lane l - 1's (frame 0's is the carried one)
+                uint2 rece{__shfl_up(recl.x, 1, 64), __shfl_up(recl.y, 1, 64)};
+                if (lane == 0) rece = rec0;
+                emit_lane((uint64_t)pos + (uint64_t)lane * wl0, cnt + lane, lane < n, rece);
                 if (kind == 2) {
                     acc += (uint64_t)n * plen0;
                 } else if (kind == 3) {  // one frame: a start without FIN or a final fragment
