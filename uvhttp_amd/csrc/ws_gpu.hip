@@ -1408,7 +1408,8 @@ __device__ inline uint64_t block_exclusive_sum_u64(uint64_t v, uint64_t* total) 
 //   k_swalk_scan    first frame of every connection, total, capacity
 //   k_stream_desc   a wave per connection re-reads its headers (two aligned 16-byte loads
 //                   each) and writes the descriptors, message ids and frame ends
-//   k_stream_claims a lane per frame claims the 16 KiB map tiles the frame's end passes
+//   k_stream_claims (lane path; the wave path's k_stream_desc claims them itself) a lane per
+//   frame claims the 16 KiB map tiles the frame's end passes
 //   payload kernel  (k_unmask_inplace) unmasks every delivered frame in place
 // No look-back, no bounded waits: nothing here can give up.
 // ------------------------------------------------------------------------------------
@@ -1425,6 +1426,12 @@ struct WalkArgs {
     uvhttp_ws_stream_result_t* results;
     uvhttp_ws_frame_desc_t* desc;
     StreamScratch sc;
+    // k_stream_desc (wave mode) claims the payload kernel's tile map itself
+    uint64_t* tile_first;      // Workspace::tile_first
+    uint64_t n_tiles;
+    uint32_t epoch;            // this call's tag (dev_epoch: ctl[kCtlEpoch])
+    uint32_t dev_epoch;
+    const uint32_t* ctl;
 };
 
 // process_data's buffer growth: returns false on failure (*out = size then), else the size
@@ -2130,6 +2137,22 @@ __global__ __launch_bounds__(kBlock) void k_stream_desc(WalkArgs w) {
     const uvhttp_ws_stream_t st = w.streams[s];
     const uint64_t sb = slice_base(st, s);
     uint32_t msg = 0;  // FIN data frames delivered before this chunk
+    const uint32_t epoch = w.dev_epoch ? w.ctl[kCtlEpoch] : w.epoch;
+    // k_stream_claims' rule (frame i claims the map tiles whose first byte lies in [end of
+    // frame i - 1, end of frame i)), here: frame 0 of the connection starts its range at the
+    // begin of the nearest earlier connection with frames (at or before that connection's last
+    // frame end; the max-of-tag claim keeps the smallest frame, so claiming more is harmless)
+    uint64_t prev_end = 0;
+    if (lane == 0) {
+        for (int64_t j = (int64_t)s - 1; j >= 0; --j) {
+            if (w.results[j].n_frames) {
+                prev_end = w.streams[j].begin;
+                break;
+            }
+        }
+    }
+    prev_end = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(prev_end >> 32)) << 32) |
+               __builtin_amdgcn_readfirstlane((uint32_t)prev_end);
     // groups of four 64-frame chunks: every start and header load of a group is issued before
     // any is used (one chunk at a time cost two dependent round trips per 64 frames)
     constexpr int kG = 4;
@@ -2155,10 +2178,18 @@ __global__ __launch_bounds__(kBlock) void k_stream_desc(WalkArgs w) {
             const bool act = k < r.n_frames;
             uvhttp_ws_frame_desc_t d;
             bool fin_data = false;
+            uint64_t fe = 0;
+            if (act) stream_frame_desc(w, st, r, k, pos[c], hv[c], d, fin_data, fe);
+            // the previous frame's end: lane - 1, or the last frame of the chunk before
+            uint64_t lo = ((uint64_t)__shfl_up((uint32_t)(fe >> 32), 1, 64) << 32) | __shfl_up((uint32_t)fe, 1, 64);
+            if (lane == 0) lo = prev_end;
+            prev_end = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(fe >> 32), 63) << 32) |
+                       __builtin_amdgcn_readlane((uint32_t)fe, 63);
             if (act) {
-                uint64_t fe;
-                stream_frame_desc(w, st, r, k, pos[c], hv[c], d, fin_data, fe);
-                w.sc.frame_off[r.first_frame + k] = fe;  // (this lane read its own entry above)
+                uint64_t hi = fe < w.wire_len ? fe : w.wire_len;
+                const uint32_t fi = r.first_frame + k;
+                for (uint64_t t = lo / kMapTile + (lo % kMapTile != 0); t * kMapTile < hi && t < w.n_tiles; ++t)
+                    tag_claim(&w.tile_first[t], epoch, fi);
             }
             // message id: FIN data frames delivered before this one in the connection
             const uint64_t fm = __ballot(fin_data);
@@ -3350,6 +3381,11 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     w.single = (e->walk_single_off == 0 && e->wt_cap >= want) ? 1u : 0u;
     w.results = d_results;
     w.desc = d_desc;
+    w.tile_first = e->ws.tile_first;
+    w.n_tiles = (wire_len + kMapTile - 1) / kMapTile;
+    w.ctl = e->ctl;
+    w.dev_epoch = e->capturing ? 1u : 0u;
+    w.epoch = next_epoch(e, s);
     w.sc = e->ss;
     w.sc.walk_tmp = (uint32_t*)e->wt_mem;
     w.sc.walk_rec = (w.single && e->wr_cap >= want && e->wr_rec_on) ? (uint2*)e->wr_mem : nullptr;
@@ -3383,10 +3419,12 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     a.streams = d_streams;
     a.n_dev = e->ss.n_total;
     a.max_polls = e->max_polls;
-    a.dev_epoch = e->capturing ? 1u : 0u;
-    a.epoch = next_epoch(e, s);
-    hipLaunchKernelGGL(k_stream_claims, dim3((cap + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a,
-                       e->ws, (const uint64_t*)e->ss.frame_off);
+    a.dev_epoch = w.dev_epoch;
+    a.epoch = w.epoch;
+    // (the wave path's k_stream_desc claimed the tile map already)
+    if (!wave_walk)
+        hipLaunchKernelGGL(k_stream_claims, dim3((cap + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a,
+                           e->ws, (const uint64_t*)e->ss.frame_off);
     // payload tile shape: the frame count is only known on the device, so the caller's frame
     // capacity stands in for it (wire bytes per frame slot; the same rule as the batch decode)
     int blk = e->tile_block, vpt = e->tile_vpt;
