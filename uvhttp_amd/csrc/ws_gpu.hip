@@ -1406,8 +1406,9 @@ __device__ inline uint64_t block_exclusive_sum_u64(uint64_t v, uint64_t* total) 
 // The walk records each counted frame's start (the failing frame is the last one counted)
 // and writes the connection's whole result except its first descriptor index.  Then:
 //   k_swalk_scan    first frame of every connection, total, capacity
-//   k_stream_desc   a wave per connection re-reads its headers (two aligned 16-byte loads
-//                   each) and writes the descriptors, message ids and frame ends
+//   k_stream_desc   a wave per connection rebuilds its headers from the walk's frame records
+//                   (or re-reads them: two aligned 16-byte loads each), writes the descriptors
+//                   and message ids, and claims the tile map (lane path: writes frame ends)
 //   k_stream_claims (lane path; the wave path's k_stream_desc claims them itself) a lane per
 //   frame claims the 16 KiB map tiles the frame's end passes
 //   payload kernel  (k_unmask_inplace) unmasks every delivered frame in place
