@@ -60,8 +60,9 @@ struct uvhttp_ws_amd_batcher {
     uvhttp_ws_amd_batcher_config_t cfg;
     // queue of the current flush
     std::vector<uint8_t> arena;  // host-only batcher: the queued reads
-    uint8_t* h_arena;            // device batcher: the queued reads, pinned (wire_cap bytes)
-    uint64_t arena_len;
+    uint8_t* h_arena;            // device batcher: the queued reads, pinned (wire_cap bytes),
+    uint64_t arena_len;          // then (scratch of each device flush) the recv-buffer prefixes
+    uint64_t reads_end;          // end of the queued reads in h_arena
     std::vector<QueuedRead> reads;
     std::vector<ConnSlot> slots;
     std::unordered_map<uvhttp_ws_connection_t*, uint32_t> slot_of;
@@ -129,7 +130,7 @@ static void release(uvhttp_ws_amd_batcher_t* b) {
 
 static void clear_queue(uvhttp_ws_amd_batcher_t* b) {
     b->arena.clear();
-    b->arena_len = 0;
+    b->arena_len = b->reads_end = 0;
     b->reads.clear();
     b->slots.clear();
     b->slot_of.clear();
@@ -167,6 +168,8 @@ static int flush_device(uvhttp_ws_amd_batcher_t* b) {
     uint64_t pos = 0;
     uint32_t nr = 0, nk = 0, nseg = 0;
     std::vector<uint32_t> slot_k(b->slots.size(), UINT32_MAX);
+    // prefixes go after the reads; a flush that failed (queue kept) and is retried starts over
+    b->arena_len = b->reads_end;
     for (size_t k = 0; k < b->slots.size(); ++k) {
         ConnSlot& s = b->slots[k];
         if (s.dropped) continue;
@@ -400,6 +403,7 @@ uvhttp_error_t uvhttp_ws_amd_batcher_submit_read(uvhttp_ws_amd_batcher_t* b,
         k = it->second;
     }
     const uint64_t off = arena_append(b, data, len);
+    b->reads_end = b->arena_len;
     b->reads.push_back(QueuedRead{off, len});
     b->slots[k].reads.push_back((uint32_t)(b->reads.size() - 1));
     b->slots[k].bytes += len;
