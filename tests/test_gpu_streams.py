@@ -266,6 +266,28 @@ def test_streams_many_small_frames(torch, eng, hooks, seed):
     _run_cases(torch, eng, U, cases, rng, 16384)
 
 
+def test_streams_runs_without_frames(torch, eng, hooks):
+    """Long runs of connections holding no complete frame (a partial frame each, up to 40 KB:
+    16 KiB map tiles start inside them) between connections with frames: the payload kernel's
+    tile map must still lead to the next connection's frames (the wave path's k_stream_desc
+    searches back past the run, 64 connections per step)."""
+    import uvhttp_amd as U
+    rng = random.Random(4040)
+    cases = []
+    for run in (70, 1, 200, 0, 65, 3):
+        for _ in range(run):
+            prod = U.WsConnection(1, 16 * 1024 * 1024, 64 * 1024 * 1024, user_data=True)
+            orc = _oracle.OracleConn(1, 16 * 1024 * 1024, 64 * 1024 * 1024, record=1, wrapper=True)
+            f = _frame(2, 1, rng.randbytes(rng.choice([300, 9000, 40000])), rng.randbytes(4))
+            cases.append((prod, orc, [f[: rng.randint(1, len(f) - 1)]]))
+        prod = U.WsConnection(1, 16 * 1024 * 1024, 64 * 1024 * 1024, user_data=True)
+        orc = _oracle.OracleConn(1, 16 * 1024 * 1024, 64 * 1024 * 1024, record=1, wrapper=True)
+        frames = [_frame(2, 1, rng.randbytes(rng.choice([1, 200, 5000, 20000])), rng.randbytes(4))
+                  for _ in range(rng.randint(1, 40))]
+        cases.append((prod, orc, [b"".join(frames)]))
+    _run_cases(torch, eng, U, cases, rng, 8192)
+
+
 @pytest.mark.parametrize("seed", range(10))
 def test_streams_per_read_calls(torch, eng, hooks, seed):
     """Several process_data calls per connection in one launch: every connection's new bytes

@@ -2161,17 +2161,21 @@ __global__ __launch_bounds__(kBlock) void k_stream_desc(WalkArgs w) {
     // frame i - 1, end of frame i)), here: frame 0 of the connection starts its range at the
     // begin of the nearest earlier connection with frames (at or before that connection's last
     // frame end; the max-of-tag claim keeps the smallest frame, so claiming more is harmless)
+    // (the direct predecessor first; past it, 64 connections per step by a ballot, so a long
+    // run of connections without frames costs one round trip per 64)
     uint64_t prev_end = 0;
-    if (lane == 0) {
-        for (int64_t j = (int64_t)s - 1; j >= 0; --j) {
-            if (w.results[j].n_frames) {
-                prev_end = w.streams[j].begin;
+    if (s > 0 && w.results[s - 1].n_frames) {
+        prev_end = w.streams[s - 1].begin;
+    } else {
+        for (int64_t base = (int64_t)s - 2; base >= 0; base -= 64) {
+            const int64_t j = base - (int64_t)lane;
+            const uint64_t m = __ballot(j >= 0 && w.results[j].n_frames != 0);
+            if (m) {
+                prev_end = w.streams[base - __builtin_ctzll(m)].begin;
                 break;
             }
         }
     }
-    prev_end = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(prev_end >> 32)) << 32) |
-               __builtin_amdgcn_readfirstlane((uint32_t)prev_end);
     // groups of four 64-frame chunks: every start and header load of a group is issued before
     // any is used (one chunk at a time cost two dependent round trips per 64 frames)
     constexpr int kG = 4;
