@@ -392,8 +392,11 @@ def timed_run(wl, steps, warmup, world):
         dist.barrier()
     wl.sync()
     t0 = time.perf_counter()
+    host = 0.0  # time the host spends issuing the steps (device idle if it exceeds the GPU's)
     for _ in range(steps):
+        h0 = time.perf_counter()
         wl.step()
+        host += time.perf_counter() - h0
     wl.sync()
     if world > 1:
         dist.barrier()
@@ -401,6 +404,7 @@ def timed_run(wl, steps, warmup, world):
     wl.set_timing(False)
     k_ms, k_n = wl.kernel_time()
     wl.check()
+    wl.host_issue_s = host
     return max_over_ranks(elapsed, world), k_ms, k_n
 
 
@@ -521,6 +525,7 @@ def main():
                 "avg_kernel_us": round(avg_kernel_s * 1e6, 2) if k_n else None,
                 "launches_timed": k_n,
             },
+            "host_issue_us_per_step": round(getattr(wl, "host_issue_s", 0.0) / args.steps * 1e6, 2),
         }
         if args.stub:
             out["stub"] = True

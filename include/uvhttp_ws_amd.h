@@ -532,22 +532,39 @@ uvhttp_error_t uvhttp_ws_deliver_batch(struct uvhttp_ws_connection* conn, const 
  * from flush(), connection by connection in first-read order; within a connection in read
  * order.  A flush whose queued bytes are below min_device_bytes runs the host decoder (one
  * libuv-sized read does not pay for a device round trip); a larger one goes
- * through the device: stage buffered bytes + reads in pinned memory -> H2D ->
+ * through the device: buffered bytes + reads in a pinned arena -> H2D -> gather ->
  * uvhttp_ws_gpu_decode_reads -> D2H -> uvhttp_ws_deliver_stream per connection.
- * Not thread-safe (the loop thread owns it, like the reference). */
+ *
+ * Asynchronous flushes.  The batcher holds two queues.  flush_async() hands the queue being
+ * filled to the device and returns at once; submit_read() keeps queueing into the other one
+ * (whose arena already streams to HBM while it fills, once it holds min_device_bytes).  The
+ * decoded queue is delivered — callbacks fire — by poll() once its results are back in host
+ * memory (or by flush()); a queue is staged for the device only after the queue before it
+ * was delivered (a connection's later reads see the state its earlier ones left, so every
+ * connection still sees exactly the process_data sequence).  With the host decoder (device -1, or a small queue) every
+ * flush delivers before it returns.  Integration: flush_async() in the loop's uv_check
+ * callback, poll() from a uv_async_t that on_ready signals.
+ * Not thread-safe (the loop thread owns it, like the reference); only on_ready runs on
+ * another thread. */
 typedef struct uvhttp_ws_amd_batcher uvhttp_ws_amd_batcher_t;
 /* a connection's queued reads failed: process_data returned rc (the reference then sends
  * close 1002 and closes, :1166-1174); the batcher drops the connection's later reads until
  * uvhttp_ws_amd_batcher_forget */
 typedef void (*uvhttp_ws_amd_failure_cb)(void* ctx, struct uvhttp_ws_connection* conn, int rc);
+/* an asynchronous flush's results are in host memory (called from a HIP runtime thread:
+ * only signal the loop, e.g. uv_async_send; then call poll() on the loop thread) */
+typedef void (*uvhttp_ws_amd_ready_cb)(void* ctx);
 typedef struct {
     int device;                /* HIP device for large flushes; -1 = host decoder only */
     uint64_t min_device_bytes; /* flushes with fewer queued bytes run on the host */
-    uint64_t max_bytes;        /* staging capacity (buffered bytes + reads) per flush */
+    uint64_t max_bytes;        /* staging capacity (buffered bytes + reads) per flush; with a
+                                  device, max_bytes / 6 + max_connections must stay < 2^26 */
     uint32_t max_connections;  /* connections per flush */
     uint32_t max_reads;        /* reads per flush */
     uvhttp_ws_amd_failure_cb on_failure;
     void* ctx;
+    uvhttp_ws_amd_ready_cb on_ready; /* optional */
+    void* ready_ctx;
 } uvhttp_ws_amd_batcher_config_t;
 typedef struct {
     uint64_t flushes, device_flushes, host_flushes;
@@ -556,23 +573,47 @@ typedef struct {
     uint64_t failures;                    /* connections reported through on_failure */
     uint64_t capacity_flushes;            /* device flushes re-run on the host (frame capacity) */
     double device_ms;                     /* wall time of device flushes (stage -> deliver) */
+    uint64_t async_flushes;               /* queues handed to the device */
+    uint64_t fallback_flushes;            /* queues that did not fit the device layout: host */
+    uint64_t device_errors;               /* device failures; those queues ran on the host */
+    uint64_t direct_reads;                /* reads larger than a flush, decoded in submit_read */
+    double blocked_ms;                    /* loop-thread time inside batcher calls that flush,
+                                             poll or wait: staging, delivering, waiting */
+    double max_blocked_ms;                /* the longest single such call */
+    double wait_ms;                       /* of blocked_ms: waiting for a device decode */
 } uvhttp_ws_amd_batcher_stats_t;
 void uvhttp_ws_amd_batcher_config_init(uvhttp_ws_amd_batcher_config_t* cfg);
 /* UVHTTP_WS_GPU_ENODEV if cfg->device >= 0 names no usable MI355X (no silent host mode) */
 int uvhttp_ws_amd_batcher_create(const uvhttp_ws_amd_batcher_config_t* cfg,
                                  uvhttp_ws_amd_batcher_t** out);
 void uvhttp_ws_amd_batcher_free(uvhttp_ws_amd_batcher_t* b);
-/* Queue one read of `conn` (the bytes are copied).  Flushes first when the read would not
- * fit the staging capacity.  Returns UVHTTP_OK, or UVHTTP_ERROR_INVALID_PARAM for a NULL
- * argument or a connection whose earlier reads already failed. */
+/* Queue one read of `conn` (the bytes are copied).  When the read would not fit the staging
+ * capacity the queue is handed over first (flush_async); a read larger than a whole flush is
+ * decoded right here, after the connection's earlier reads were delivered.  Returns
+ * UVHTTP_OK, or UVHTTP_ERROR_INVALID_PARAM for a NULL argument, a connection whose earlier
+ * reads already failed, or — only from inside a batcher callback, where no flush can start —
+ * a read that does not fit the queue. */
 uvhttp_error_t uvhttp_ws_amd_batcher_submit_read(uvhttp_ws_amd_batcher_t* b,
                                                  struct uvhttp_ws_connection* conn,
                                                  const uint8_t* data, size_t len);
-/* Decode everything queued (callbacks fire here).  0, or a UVHTTP_WS_GPU_* error of the
- * device path (then nothing of the flush was delivered and the reads stay queued). */
+/* Hand everything queued to the decoder and return (see "Asynchronous flushes").  Never waits
+ * for the device: when a queue is still in flight the request is remembered and poll() starts
+ * this queue right after delivering that one (until then reads keep joining it; a read that
+ * no longer fits makes submit_read wait).  0, or the UVHTTP_WS_GPU_* error of a device decode
+ * that failed (its queue was decoded by the host decoder instead, so nothing is lost; stats
+ * count it).  From inside a batcher callback: does nothing. */
+int uvhttp_ws_amd_batcher_flush_async(uvhttp_ws_amd_batcher_t* b);
+/* Deliver the queue in flight if its results are back (never waits), then start the queue a
+ * flush_async asked for meanwhile: 1 delivered, 0 nothing to deliver yet, or a
+ * UVHTTP_WS_GPU_* error as flush_async. */
+int uvhttp_ws_amd_batcher_poll(uvhttp_ws_amd_batcher_t* b);
+/* 1 while a queue is in flight (the loop must poll or flush before it can idle) */
+int uvhttp_ws_amd_batcher_in_flight(const uvhttp_ws_amd_batcher_t* b);
+/* Decode everything queued — the queue in flight, then the one being filled — and deliver it
+ * before returning (callbacks fire here); returns as flush_async. */
 int uvhttp_ws_amd_batcher_flush(uvhttp_ws_amd_batcher_t* b);
-/* Drop a connection's queued reads and failure mark (call before freeing the connection;
- * safe from inside callbacks of a flush). */
+/* Drop a connection's queued reads (in both queues) and failure mark (call before freeing
+ * the connection; safe from inside callbacks of a flush). */
 void uvhttp_ws_amd_batcher_forget(uvhttp_ws_amd_batcher_t* b, struct uvhttp_ws_connection* conn);
 int uvhttp_ws_amd_batcher_stats(const uvhttp_ws_amd_batcher_t* b,
                                 uvhttp_ws_amd_batcher_stats_t* out);

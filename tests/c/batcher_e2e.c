@@ -6,7 +6,10 @@
  * reads through the host decoder (--device -1: process_data per read on this core) give the
  * reference-shaped CPU rate.  Prints one JSON line.
  *
- *   batcher_e2e --conns N --frames M --size S --read R --flushes F --device D
+ * --async 1: one flush_async per round (the loop's uv_check), so the device decodes round k
+ * while the loop takes the reads of round k+1; the last round is flushed synchronously.
+ *
+ *   batcher_e2e --conns N --frames M --size S --read R --flushes F --device D [--async 1]
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -33,7 +36,7 @@ static double now_s(void) {
 }
 
 int main(int argc, char** argv) {
-    int conns = 1024, frames = 4, flushes = 20, device = 0;
+    int conns = 1024, frames = 4, flushes = 20, device = 0, async = 0;
     size_t size = 65536, rd = 16384;
     for (int i = 1; i + 1 < argc; i += 2) {
         if (!strcmp(argv[i], "--conns")) conns = atoi(argv[i + 1]);
@@ -42,6 +45,7 @@ int main(int argc, char** argv) {
         else if (!strcmp(argv[i], "--read")) rd = (size_t)strtoull(argv[i + 1], NULL, 10);
         else if (!strcmp(argv[i], "--flushes")) flushes = atoi(argv[i + 1]);
         else if (!strcmp(argv[i], "--device")) device = atoi(argv[i + 1]);
+        else if (!strcmp(argv[i], "--async")) async = atoi(argv[i + 1]);
     }
     /* one connection's stream: M masked BINARY frames of S bytes (every connection sends
      * the same bytes; keys differ per frame) */
@@ -77,17 +81,32 @@ int main(int argc, char** argv) {
         fprintf(stderr, "batcher_create failed\n");
         return 1;
     }
-    double t0 = 0;
+    double t0 = 0, t_submit = 0, t_flush = 0;
+    uvhttp_ws_amd_batcher_stats_t st0;
+    memset(&st0, 0, sizeof(st0));
     for (int it = -2; it < flushes; ++it) {  /* two warm-up flushes */
         if (it == 0) {
+            if (async && uvhttp_ws_amd_batcher_flush(b) != 0) return 3;  /* drain the warm-up */
             g_msgs = g_bytes = 0;
+            uvhttp_ws_amd_batcher_stats(b, &st0);
             t0 = now_s();
         }
+        const double ts = now_s();
         for (int c = 0; c < conns; ++c)
             for (size_t o = 0; o < slen; o += rd)
                 if (uvhttp_ws_amd_batcher_submit_read(b, cs[c], stream + o, o + rd <= slen ? rd : slen - o)) return 2;
-        if (uvhttp_ws_amd_batcher_flush(b) != 0) return 3;
+        const double tf = now_s();
+        /* async: the loop's uv_async wake-up (poll) and uv_check (flush_async) */
+        if (async && uvhttp_ws_amd_batcher_poll(b) < 0) return 3;
+        if ((async ? uvhttp_ws_amd_batcher_flush_async(b) : uvhttp_ws_amd_batcher_flush(b)) != 0) return 3;
+        if (it >= 0) {
+            t_submit += tf - ts;
+            t_flush += now_s() - tf;
+        }
     }
+    const double tl = now_s();
+    if (async && uvhttp_ws_amd_batcher_flush(b) != 0) return 3;
+    t_flush += now_s() - tl;
     const double el = now_s() - t0;
     uvhttp_ws_amd_batcher_stats_t st;
     uvhttp_ws_amd_batcher_stats(b, &st);
@@ -95,12 +114,16 @@ int main(int argc, char** argv) {
     printf("{\"path\": \"%s\", \"value\": %.3f, \"unit\": \"GiB/s\", \"conns\": %d, "
            "\"frames_per_conn\": %d, \"payload\": %zu, \"read\": %zu, \"flushes\": %d, "
            "\"ms_per_flush\": %.3f, \"messages_ok\": %d, \"device_flushes\": %llu, "
-           "\"device_ms_total\": %.1f}\n",
+           "\"device_ms_total\": %.1f, \"async\": %d, \"submit_ms_per_flush\": %.3f, "
+           "\"flush_call_ms_per_flush\": %.3f, \"blocked_ms_per_flush\": %.3f, "
+           "\"max_blocked_ms\": %.3f}\n",
            device >= 0 ? "device batcher (stage, H2D, decode_reads, D2H, deliver)"
                        : "host decoder (process_data per read, 1 core)",
            payload / el / (1024.0 * 1024 * 1024), conns, frames, size, rd, flushes,
            el * 1e3 / flushes, g_msgs == (uint64_t)conns * frames * flushes,
-           (unsigned long long)st.device_flushes, st.device_ms);
+           (unsigned long long)(st.device_flushes - st0.device_flushes), st.device_ms - st0.device_ms,
+           async, t_submit * 1e3 / flushes, t_flush * 1e3 / flushes,
+           (st.blocked_ms - st0.blocked_ms) / flushes, st.max_blocked_ms);
     uvhttp_ws_amd_batcher_free(b);
     for (int c = 0; c < conns; ++c) uvhttp_ws_connection_free(cs[c]);
     free(cs);

@@ -64,7 +64,8 @@ static int g_n_conns;
 static client_t g_clients[MAX_CLIENTS];
 static int g_n_clients, g_done_clients;
 static uint64_t g_reads, g_read_bytes, g_max_read, g_messages, g_errors;
-static int g_batch;
+static int g_batch, g_async;
+static uv_async_t g_ready;
 #ifndef C1_HOST_ONLY
 static uvhttp_ws_amd_batcher_t* g_batcher;
 #endif
@@ -193,7 +194,21 @@ static void on_batch_failure(void* ctx, uvhttp_ws_connection_t* ws, int rc) {
 
 static void on_flush_check(uv_check_t* h) {
     (void)h;
-    if (g_batcher && uvhttp_ws_amd_batcher_flush(g_batcher) != 0) g_errors++;
+    if (!g_batcher) return;
+    if ((g_async ? uvhttp_ws_amd_batcher_flush_async(g_batcher)
+                 : uvhttp_ws_amd_batcher_flush(g_batcher)) != 0)
+        g_errors++;
+}
+
+/* --async 1: a device queue's results are back (HIP runtime thread): wake the loop */
+static void on_batch_ready(void* ctx) {
+    (void)ctx;
+    uv_async_send(&g_ready);
+}
+/* ... and deliver them on the loop thread */
+static void on_ready_async(uv_async_t* h) {
+    (void)h;
+    if (g_batcher && uvhttp_ws_amd_batcher_poll(g_batcher) < 0) g_errors++;
 }
 #endif
 
@@ -226,6 +241,7 @@ static void on_client_closed(uv_handle_t* h) {
     if (++g_done_clients == g_n_clients) {
         uv_close((uv_handle_t*)&g_server, NULL);
         if (g_batch) uv_close((uv_handle_t*)&g_flush_check, NULL);
+        if (g_async) uv_close((uv_handle_t*)&g_ready, NULL);
         for (int i = 0; i < g_n_conns; ++i)
             if (g_conns[i]) server_close(g_conns[i]);
     }
@@ -320,6 +336,7 @@ int main(int argc, char** argv) {
         else if (!strcmp(argv[i], "--chunk")) g_chunk = (size_t)strtoull(argv[i + 1], NULL, 10);
         else if (!strcmp(argv[i], "--seed")) seed = strtoull(argv[i + 1], NULL, 10);
         else if (!strcmp(argv[i], "--batch")) g_batch = atoi(argv[i + 1]);
+        else if (!strcmp(argv[i], "--async")) g_async = atoi(argv[i + 1]);
         else if (!strcmp(argv[i], "--device")) device = atoi(argv[i + 1]);
         else if (!strcmp(argv[i], "--threshold")) threshold = strtoull(argv[i + 1], NULL, 10);
         else if (!strcmp(argv[i], "--dump")) dump = argv[i + 1];
@@ -329,14 +346,19 @@ int main(int argc, char** argv) {
 #ifdef C1_HOST_ONLY
     (void)device;
     (void)threshold;
-    if (g_batch) return 2;
+    if (g_batch || g_async) return 2;
 #else
+    if (g_async && !g_batch) return 2;
     if (g_batch) {
         uvhttp_ws_amd_batcher_config_t bc;
         uvhttp_ws_amd_batcher_config_init(&bc);
         bc.device = device;
         bc.min_device_bytes = threshold;
         bc.on_failure = on_batch_failure;
+        if (g_async) {
+            uv_async_init(g_loop, &g_ready, on_ready_async);
+            bc.on_ready = on_batch_ready;
+        }
         if (uvhttp_ws_amd_batcher_create(&bc, &g_batcher) != 0) {
             fprintf(stderr, "batcher_create failed\n");
             return 3;

@@ -1,0 +1,245 @@
+"""The batcher's state transitions (include/uvhttp_ws_amd.h, uvhttp_ws_amd_batcher_*), each
+checked against the oracle fed the same reads per connection (the reference's
+on_websocket_read loop: process_data per read until one fails, src/uvhttp_connection.c:
+1098-1175):
+
+* a queue that overflows max_bytes / max_reads / max_connections inside submit_read (the
+  queue is handed over there), reads larger than a whole flush (decoded in submit_read after
+  the connection's earlier reads), flush / flush_async / poll interleaved at random;
+* reads submitted and connections forgotten (and re-created) from inside on_message while a
+  flush delivers — on the host path and, with a device, while the other queue fills;
+* (device) client-side connections whose tiny unmasked frames overflow the frame capacity
+  (ERR_CAPACITY -> the queue re-runs on the host) and injected device failures
+  (UVHTTP_WS_BATCHER_FAIL_EVERY -> the queue decodes on the host, the error is returned).
+
+device = -1 runs here on the CPU (host decoder); device = 0 is marked gpu.
+"""
+import ctypes as C
+import os
+import random
+
+import pytest
+
+import _oracle
+from test_gpu_streams import _frame, _frames
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DEVICES = [-1, pytest.param(0, marks=pytest.mark.gpu)]
+
+
+def _need_device(device):
+    if device >= 0:
+        import torch
+        if not torch.cuda.is_available():
+            pytest.skip("no GPU")
+
+
+def _conn_reads(rng, big=0):
+    frames, _ = _frames(rng, rng.randint(0, 10), False, bad=rng.random() < 0.3)
+    data = b"".join(frames)
+    reads, pos = [], 0
+    while pos < len(data):
+        n = rng.choice([1, 7, 300, 4096, 16384, rng.randint(1, 20000)] + ([big] if big else []))
+        reads.append(data[pos:pos + n])
+        pos += n
+    return reads
+
+
+class Pair:
+    """A product connection and its oracle twin fed the same reads."""
+
+    def __init__(self, U, rng, mf=None, mm=None, reads=None):
+        mf = mf or rng.choice([16 * 1024 * 1024, 65536, 4000])
+        mm = mm if mm is not None else rng.choice([64 * 1024 * 1024, 9000, 0])
+        self.prod = U.WsConnection(1, mf, mm, user_data=False)
+        self.orc = _oracle.OracleConn(1, mf, mm, record=1)
+        self.reads = reads if reads is not None else []
+        self.next = 0
+        self.orc_failed = False
+        self.submit_failed = False
+        self.dead = False  # forgotten and freed
+
+    @property
+    def key(self):
+        return C.addressof(self.prod.ptr.contents)
+
+    def feed(self, b, data):
+        """one read: to the batcher and (until it fails) to the oracle"""
+        if self.orc_failed or self.submit_failed or self.dead:
+            return
+        rc = b.submit(self.prod, data)
+        # (a read larger than a flush is decoded inside submit_read: its rc is process_data's)
+        if self.orc.process_data(data) != 0:
+            self.orc_failed = True
+        if rc != 0:
+            self.submit_failed = True
+
+    def events(self):
+        pev = [(t, a, p) for t, a, p in self.prod.events if t in ("message", "close")]
+        oev = [(t, a, p if t == "message" else None) for t, a, p in self.orc.events()
+               if t in ("message", "close")]
+        return pev, oev
+
+    def check(self, b, L):
+        if self.dead:  # delivered up to the forget: a prefix of the oracle's transcript
+            pev, oev = self.events()
+            assert pev == oev[:len(pev)]
+            return
+        failed = self.key in b.failures or self.submit_failed
+        assert failed == self.orc_failed
+        pev, oev = self.events()
+        assert pev == oev
+        s = self.prod.struct
+        assert s.recv_buffer_pos == self.orc.recv_pos
+        assert C.string_at(s.recv_buffer, s.recv_buffer_pos) == self.orc.recv_bytes()
+        assert s.recv_buffer_size == self.orc.recv_size
+        assert (s.fragmented_size if s.fragmented_message else 0) == L.oracle_conn_frag_size(self.orc.c)
+        assert s.fragmented_opcode == self.orc.frag_opcode
+
+
+def _drive(U, b, rng, pairs):
+    """random loop iterations: some connections get a read each, then flush / flush_async /
+    poll / nothing; finally flush"""
+    while any(p.next < len(p.reads) for p in pairs):
+        for p in rng.sample(pairs, len(pairs)):
+            if p.next >= len(p.reads) or rng.random() < 0.3:
+                continue
+            p.feed(b, p.reads[p.next])
+            p.next += 1
+        act = rng.random()
+        if act < 0.3:
+            assert b.flush() == 0
+        elif act < 0.6:
+            assert b.flush_async() == 0
+        elif act < 0.8:
+            assert b.poll() in (0, 1)
+    assert b.flush() == 0
+    assert not b.in_flight()
+
+
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("seed", [1, 2])
+def test_overflow_and_oversize_reads(device, seed):
+    """tiny queue limits: flushes start inside submit_read; 70 000-byte reads exceed a whole
+    flush (max_bytes 48 KiB) and are decoded directly, after the connection's queued reads"""
+    _need_device(device)
+    import uvhttp_amd as U
+    rng = random.Random(seed)
+    b = U.Batcher(device=device, min_device_bytes=0, max_bytes=48 * 1024,
+                  max_connections=6, max_reads=40)
+    pairs = [Pair(U, rng, reads=_conn_reads(rng, big=70000)) for _ in range(24)]
+    _drive(U, b, rng, pairs)
+    st = b.stats()
+    assert st["direct_reads"] > 0 and st["flushes"] > 10
+    if device >= 0:
+        assert st["device_flushes"] > 0 and st["async_flushes"] > 0
+    L = _oracle.load()
+    for p in pairs:
+        p.check(b, L)
+    b.close()
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_submit_and_forget_from_callbacks(device):
+    """on_message of the 'driver' connections submits a read for a 'chained' connection (it
+    lands in the queue being filled, never the one being delivered) and forgets a 'victim'
+    connection mid-stream, re-creating a fresh connection that then gets reads of its own"""
+    _need_device(device)
+    import uvhttp_amd as U
+    rng = random.Random(7)
+    b = U.Batcher(device=device, min_device_bytes=0)
+    key = b"\x11\x22\x33\x44"
+    # chained connections: their whole stream is submitted from callbacks, one read per event
+    chained = [Pair(U, rng, mf=16 << 20, mm=64 << 20,
+                    reads=_conn_reads(rng)) for _ in range(6)]
+    victims = [Pair(U, rng, mf=16 << 20, mm=64 << 20,
+                    reads=[_frame(2, 1, rng.randbytes(100), key, True, 0)] * 40) for _ in range(4)]
+    fresh = []
+    drivers = [Pair(U, rng, mf=16 << 20, mm=64 << 20,
+                    reads=[_frame(1, 1, b"tick %d" % i, key, True, 0) for i in range(60)])
+               for _ in range(3)]
+
+    def hook(conn, ev):
+        for c in chained:
+            if c.next < len(c.reads) and rng.random() < 0.5:
+                c.feed(b, c.reads[c.next])
+                c.next += 1
+        if victims and rng.random() < 0.1:
+            v = victims.pop()
+            b.forget(v.prod)
+            v.dead = True
+            v.prod.close()  # a new connection may now get the same address
+            n = Pair(U, rng, mf=16 << 20, mm=64 << 20, reads=_conn_reads(rng))
+            fresh.append(n)
+            n.feed(b, n.reads[0])
+            n.next = 1
+            forgotten_pairs.append(v)
+
+    forgotten_pairs = []
+    all_victims = list(victims)
+    for d in drivers:
+        d.prod.hook = hook
+    _drive(U, b, rng, drivers + victims + fresh)
+    # whatever the callbacks queued last
+    while any(c.next < len(c.reads) for c in chained + fresh):
+        for c in chained + fresh:
+            if c.next < len(c.reads):
+                c.feed(b, c.reads[c.next])
+                c.next += 1
+        assert b.flush() == 0
+    assert b.flush() == 0
+    L = _oracle.load()
+    for p in drivers + chained + fresh + all_victims:
+        p.check(b, L)
+    assert forgotten_pairs, "no connection was forgotten from a callback"
+    b.close()
+
+
+@pytest.mark.gpu
+def test_capacity_and_device_failure_fall_back_to_host():
+    """client-side connections of 2-byte unmasked frames overflow the frame capacity
+    (bytes / 6 + connections): the device reports ERR_CAPACITY and the queue re-runs on the
+    host.  Then every device launch fails (test hook): each queue is decoded on the host,
+    flush returns ELAUNCH and nothing is lost."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import uvhttp_amd as U
+    rng = random.Random(5)
+    L = _oracle.load()
+    b = U.Batcher(device=0, min_device_bytes=0)
+    prods, orcs = [], []
+    for k in range(8):
+        prod = U.WsConnection(0, 16 << 20, 64 << 20)
+        orc = _oracle.OracleConn(0, 16 << 20, 64 << 20, record=1)
+        data = b"".join(_frame(2, 1, b"", b"", False, 0) for _ in range(3000))
+        assert b.submit(prod, data) == 0
+        assert orc.process_data(data) == 0
+        prods.append(prod)
+        orcs.append(orc)
+    assert b.flush() == 0
+    st = b.stats()
+    assert st["capacity_flushes"] == 1 and st["host_reads"] == 8
+    for prod, orc in zip(prods, orcs):
+        assert len(prod.events) == len(orc.events()) == 3000
+    b.close()
+
+    os.environ["UVHTTP_WS_BATCHER_FAIL_EVERY"] = "1"
+    try:
+        b = U.Batcher(device=0, min_device_bytes=0)
+    finally:
+        del os.environ["UVHTTP_WS_BATCHER_FAIL_EVERY"]
+    pairs = [Pair(U, rng, reads=_conn_reads(rng)) for _ in range(10)]
+    rcs = []
+    while any(p.next < len(p.reads) for p in pairs):
+        for p in pairs:
+            if p.next < len(p.reads):
+                p.feed(b, p.reads[p.next])
+                p.next += 1
+        rcs.append(b.flush())
+    assert set(rcs) <= {0, -4} and -4 in rcs
+    st = b.stats()
+    assert st["device_errors"] > 0 and st["device_flushes"] == 0
+    for p in pairs:
+        p.check(b, L)
+    b.close()

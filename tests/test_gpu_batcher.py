@@ -40,20 +40,24 @@ def _c1(*args):
     return json.loads(p.stdout.strip().splitlines()[-1])
 
 
+@pytest.mark.parametrize("async_", [0, 1])
 @pytest.mark.parametrize("clients,frames,size,chunk", [(16, 40, 3000, 777), (4, 6, 70000, 5000),
                                                        (1, 1, 1024, 1032)])
-def test_c1_echo_through_device_batcher(torch, clients, frames, size, chunk):
+def test_c1_echo_through_device_batcher(torch, clients, frames, size, chunk, async_):
+    """async_ = 1: flush_async from uv_check, delivery from a uv_async_t that the batcher's
+    on_ready (a HIP host callback) signals — the loop never waits for the device"""
     args = ("--clients", clients, "--frames", frames, "--size", size, "--chunk", chunk,
             "--seed", 11)
     direct = _c1(*args)
-    dev = _c1(*args, "--batch", 1, "--device", 0, "--threshold", 0)
+    dev = _c1(*args, "--batch", 1, "--device", 0, "--threshold", 0, "--async", async_)
     assert all(c["match"] for c in dev["clients"]) and dev["errors"] == 0
     assert [c["echo_fnv"] for c in dev["clients"]] == [c["echo_fnv"] for c in direct["clients"]]
     assert dev["device_flushes"] > 0 and dev["device_reads"] == dev["reads"]
     assert dev["host_reads"] == 0 and dev["device_frames"] >= clients * frames
 
 
-def test_batcher_random_connections_vs_oracle(torch):
+@pytest.mark.parametrize("async_", [0, 1])
+def test_batcher_random_connections_vs_oracle(torch, async_):
     import uvhttp_amd as U
     rng = random.Random(2024)
     b = U.Batcher(device=0, min_device_bytes=0)
@@ -88,10 +92,15 @@ def test_batcher_random_connections_vs_oracle(torch):
             orc_rc = orc.process_data(reads[nxt])
             if orc_rc != 0:
                 c[4] = ("oracle", orc_rc)
-        assert b.flush() == 0
+        if async_:
+            assert b.poll() in (0, 1)
+            assert b.flush_async() == 0
+        else:
+            assert b.flush() == 0
         flushes += 1
+    assert b.flush() == 0
     st = b.stats()
-    assert 0 < st["device_flushes"] == st["flushes"] <= flushes  # (empty flushes do nothing)
+    assert 0 < st["device_flushes"] == st["flushes"] <= flushes + 1  # (empty flushes do nothing)
     assert st["host_reads"] == 0 and st["device_reads"] > 0
     L = _oracle.load()
     for prod, orc, reads, _, end in conns:

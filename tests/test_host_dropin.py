@@ -67,6 +67,9 @@ def test_struct_abi():
     assert U.WsConnectionStruct.frames_received.offset == 240
     assert U.UvhttpConfig.websocket_max_frame_size.offset == 64
     assert C.sizeof(U.FrameDesc) == 32 and C.sizeof(U.MessageDesc) == 32
+    # batcher structs (include/uvhttp_ws_amd.h, checked against gcc's layout)
+    assert C.sizeof(U.BatcherConfig) == 64 and U.BatcherConfig.on_ready.offset == 48
+    assert C.sizeof(U.BatcherStats) == 136 and U.BatcherStats.blocked_ms.offset == 112
 
 
 def test_null_and_empty():

@@ -117,6 +117,7 @@ ON_CLOSE = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_char_p)
 ON_ERROR = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_char_p)
 CONTEXT_RESOLVER = C.CFUNCTYPE(C.c_void_p, C.c_void_p)
 FAILURE_CB = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p, C.c_int)
+READY_CB = C.CFUNCTYPE(None, C.c_void_p)
 CONTROL_SINK = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_uint8),
                            C.c_size_t)
 
@@ -162,14 +163,18 @@ class BatcherConfig(C.Structure):
     """uvhttp_ws_amd_batcher_config_t"""
     _fields_ = [("device", C.c_int), ("min_device_bytes", C.c_uint64), ("max_bytes", C.c_uint64),
                 ("max_connections", C.c_uint32), ("max_reads", C.c_uint32),
-                ("on_failure", FAILURE_CB), ("ctx", C.c_void_p)]
+                ("on_failure", FAILURE_CB), ("ctx", C.c_void_p),
+                ("on_ready", READY_CB), ("ready_ctx", C.c_void_p)]
 
 
 class BatcherStats(C.Structure):
     """uvhttp_ws_amd_batcher_stats_t"""
     _fields_ = [(k, C.c_uint64) for k in ("flushes", "device_flushes", "host_flushes", "host_reads",
                                           "device_reads", "device_frames", "device_bytes",
-                                          "failures", "capacity_flushes")] + [("device_ms", C.c_double)]
+                                          "failures", "capacity_flushes")] + [("device_ms", C.c_double)] + \
+        [(k, C.c_uint64) for k in ("async_flushes", "fallback_flushes", "device_errors",
+                                   "direct_reads")] + \
+        [("blocked_ms", C.c_double), ("max_blocked_ms", C.c_double), ("wait_ms", C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -249,6 +254,9 @@ def load_library(path: str) -> C.CDLL:
         "uvhttp_ws_amd_batcher_submit_read": (C.c_int, [vp, C.POINTER(WsConnectionStruct), vp,
                                                         C.c_size_t]),
         "uvhttp_ws_amd_batcher_flush": (C.c_int, [vp]),
+        "uvhttp_ws_amd_batcher_flush_async": (C.c_int, [vp]),
+        "uvhttp_ws_amd_batcher_poll": (C.c_int, [vp]),
+        "uvhttp_ws_amd_batcher_in_flight": (C.c_int, [vp]),
         "uvhttp_ws_amd_batcher_forget": (None, [vp, C.POINTER(WsConnectionStruct)]),
         "uvhttp_ws_amd_batcher_stats": (C.c_int, [vp, C.POINTER(BatcherStats)]),
         # TLS record layer (include/uvhttp_tls_amd.h)
@@ -319,6 +327,7 @@ class WsConnection:
         if not self.ptr:
             raise MemoryError("uvhttp_ws_connection_create failed")
         self.events = []
+        self.hook = None  # optional f(conn, event), run inside on_message (tests)
         if callbacks:
             self._cbs = (ON_MESSAGE(self._on_message), ON_CLOSE(self._on_close),
                          ON_ERROR(self._on_error))
@@ -327,7 +336,10 @@ class WsConnection:
             self.ptr.contents.user_data = 1
 
     def _on_message(self, conn, data, n, opcode):
-        self.events.append(("message", opcode, C.string_at(data, n) if n else b""))
+        ev = ("message", opcode, C.string_at(data, n) if n else b"")
+        self.events.append(ev)
+        if self.hook is not None:
+            self.hook(self, ev)
         return 0
 
     def _on_close(self, conn, code, reason):
@@ -736,6 +748,15 @@ class Batcher:
 
     def flush(self) -> int:
         return self._L.uvhttp_ws_amd_batcher_flush(self.h)
+
+    def flush_async(self) -> int:
+        return self._L.uvhttp_ws_amd_batcher_flush_async(self.h)
+
+    def poll(self) -> int:
+        return self._L.uvhttp_ws_amd_batcher_poll(self.h)
+
+    def in_flight(self) -> bool:
+        return bool(self._L.uvhttp_ws_amd_batcher_in_flight(self.h))
 
     def forget(self, conn: "WsConnection"):
         self._L.uvhttp_ws_amd_batcher_forget(self.h, conn.ptr)

@@ -1,5 +1,5 @@
 // ws_batcher.hip — the batcher (include/uvhttp_ws_amd.h): live libuv reads of many
-// connections, queued by the loop thread and decoded together at flush().
+// connections, queued by the loop thread and decoded together.
 //
 // It sits where the reference's on_websocket_read calls uvhttp_ws_process_data once per read
 // (src/uvhttp_connection.c:1098-1175).  Per connection the queued reads are exactly the
@@ -8,10 +8,19 @@
 // per connection with a read table (one entry per call) and runs uvhttp_ws_gpu_decode_reads;
 // uvhttp_ws_deliver_stream replays the callbacks and the buffer / fragment state.  Small
 // flushes run the host decoder (the product's ws_host.c) read by read.
-// With a device, reads are queued straight into a pinned arena in arrival order; a flush
-// uploads the arena once and k_batcher_gather lays every connection's bytes out contiguously
-// in device memory (the host never re-copies the reads into the decode layout: that staging
-// memcpy, 256 MiB per flush on the loop thread, was most of a flush's time).
+//
+// Two queues, so the loop thread never waits for PCIe or the GPU while it has reads to take:
+//   * the accumulating queue takes submit_read's bytes into its pinned arena; once the queue
+//     is large enough for the device, the arena streams to HBM in 8 MiB pieces on the upload
+//     stream while reads keep arriving (the H2D overlaps the loop's own work);
+//   * flush_async hands the accumulating queue to the device (the recv-buffer prefixes and
+//     read tables are staged then, from the connections' state at that moment, so they see
+//     every earlier flush) and switches submit_read to the other queue: gather, decode and
+//     D2H run on the compute stream while the loop returns to libuv;
+//   * poll (or the next flush) delivers the finished queue: callbacks, recv-buffer and
+//     fragment state per connection, exactly what process_data per read would have left.
+// A connection's reads in the accumulating queue are staged only after the in-flight queue
+// has been delivered (flush_async completes it first), so its state is always current.
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -24,19 +33,24 @@
 
 #include "uvhttp_ws_amd.h"
 
+extern "C" void uvhttp_ws_amd_copy_stream(void* dst, const void* src, size_t len);  // ws_host.c
+
 namespace {
 
+constexpr uint32_t kMaxFramesPerFlush = 1u << 26;  // decode_reads' frame limit (ws_gpu.hip)
+constexpr uint64_t kUploadPiece = 8ull << 20;        // arena bytes per early H2D
+constexpr uint32_t kMinFrames = 65536;              // initial descriptor capacity per queue
+
 struct QueuedRead {
-    uint64_t off;  // in the arena
+    uint64_t off;  // in the queue's arena
     uint64_t len;
 };
 
 struct ConnSlot {
     uvhttp_ws_connection_t* conn;
-    std::vector<uint32_t> reads;  // indices into reads_, arrival order
+    std::vector<uint32_t> reads;  // indices into Queue::reads, arrival order
     uint64_t bytes;               // queued read bytes
-    uint64_t prefix;              // recv_buffer_pos when the slot opened
-    bool dropped;                 // forgotten (or failed) during this flush
+    bool dropped;                 // forgotten, or failed in an earlier queue
 };
 
 inline uint64_t align16(uint64_t x) { return (x + 15) & ~(uint64_t)15; }
@@ -54,233 +68,393 @@ __global__ __launch_bounds__(256) void k_batcher_gather(const uint8_t* __restric
     for (uint64_t i = threadIdx.x; i < g.len; i += 256) wire[g.dst + i] = arena[g.src + i];
 }
 
+double ms_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
 }  // namespace
 
-struct uvhttp_ws_amd_batcher {
-    uvhttp_ws_amd_batcher_config_t cfg;
-    // queue of the current flush
+// One queue: the reads of one flush, and (device batcher) the buffers its decode uses.
+struct BatchQueue {
     std::vector<uint8_t> arena;  // host-only batcher: the queued reads
-    uint8_t* h_arena;            // device batcher: the queued reads, pinned (wire_cap bytes),
-    uint64_t arena_len;          // then (scratch of each device flush) the recv-buffer prefixes
-    uint64_t reads_end;          // end of the queued reads in h_arena
+    uint8_t* h_arena = nullptr;  // device batcher: the reads, pinned (wire_cap bytes), then
+    uint64_t arena_len = 0;      // the recv-buffer prefixes staged at flush time
+    uint64_t uploaded = 0;       // h_arena[0, uploaded) is already on its way to d_arena
     std::vector<QueuedRead> reads;
     std::vector<ConnSlot> slots;
     std::unordered_map<uvhttp_ws_connection_t*, uint32_t> slot_of;
-    uint64_t staged;  // bytes the device layout needs (prefixes + reads + alignment)
+    uint64_t staged = 0;  // estimate of the device layout (reads + prefixes + alignment)
+    uint64_t bytes = 0;   // queued read bytes
+    // device buffers
+    uint8_t *d_arena = nullptr, *h_wire = nullptr, *d_wire = nullptr;
+    uvhttp_ws_stream_t *h_streams = nullptr, *d_streams = nullptr;
+    uvhttp_ws_stream_result_t *h_results = nullptr, *d_results = nullptr;
+    uint64_t *h_read_end = nullptr, *d_read_end = nullptr;
+    uvhttp_ws_frame_desc_t *h_desc = nullptr, *d_desc = nullptr;
+    GatherSeg *h_seg = nullptr, *d_seg = nullptr;
+    uint32_t max_frames = 0;
+    hipEvent_t up_ev = nullptr, done_ev = nullptr;
+    // the flush in flight
+    bool in_flight = false;
+    int launch_rc = 0;
+    uint32_t nk = 0;               // connections staged
+    uint64_t pos = 0;              // wire bytes staged
+    std::vector<uint32_t> slot_k;  // slot -> stream index (UINT32_MAX: not staged)
+    std::chrono::steady_clock::time_point t_submit;
+};
+
+struct uvhttp_ws_amd_batcher {
+    uvhttp_ws_amd_batcher_config_t cfg;
+    BatchQueue q[2];
+    int cur = 0;  // the accumulating queue; q[cur ^ 1] is idle or in flight
     std::unordered_set<uvhttp_ws_connection_t*> failed;
-    bool in_flush;
+    int delivering = 0;  // callbacks of a delivery are running (no nested flushes)
+    bool want_flush = false;  // flush_async asked while a queue was in flight: poll starts it
     // device path
-    uvhttp_ws_gpu_engine_t* eng;
-    hipStream_t stream;
-    uint32_t max_frames;
-    uint64_t wire_cap;
-    uint8_t *h_wire, *d_wire;
-    uvhttp_ws_stream_t *h_streams, *d_streams;
-    uvhttp_ws_stream_result_t *h_results, *d_results;
-    uint64_t *h_read_end, *d_read_end;
-    uvhttp_ws_frame_desc_t *h_desc, *d_desc;
-    uint8_t* d_arena;
-    GatherSeg *h_seg, *d_seg;
+    uvhttp_ws_gpu_engine_t* eng = nullptr;
+    hipStream_t up = nullptr;  // H2D of the arenas
+    hipStream_t cs = nullptr;  // gather, decode, D2H
+    uint64_t wire_cap = 0;
+    uint32_t fail_every = 0;  // test hook (UVHTTP_WS_BATCHER_FAIL_EVERY=k): every k-th device
+    uint32_t launches = 0;    // launch reports ELAUNCH before enqueueing anything
     uvhttp_ws_amd_batcher_stats_t st;
 };
 
-static uint8_t* arena_data(uvhttp_ws_amd_batcher_t* b) {
-    return b->h_arena ? b->h_arena : b->arena.data();
+namespace {
+
+uint8_t* arena_data(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
+    return b->eng ? q.h_arena : q.arena.data();
 }
 
-// append len bytes to the queue's arena; returns their offset
-static uint64_t arena_append(uvhttp_ws_amd_batcher_t* b, const uint8_t* data, size_t len) {
-    if (!b->h_arena) {
-        const uint64_t off = b->arena.size();
-        b->arena.insert(b->arena.end(), data, data + len);
-        return off;
-    }
-    const uint64_t off = b->arena_len;
-    if (len) memcpy(b->h_arena + off, data, len);
-    b->arena_len += len;
-    return off;
+void free_queue(BatchQueue& q) {
+    (void)hipHostFree(q.h_arena);
+    (void)hipHostFree(q.h_wire);
+    (void)hipHostFree(q.h_streams);
+    (void)hipHostFree(q.h_results);
+    (void)hipHostFree(q.h_read_end);
+    (void)hipHostFree(q.h_desc);
+    (void)hipHostFree(q.h_seg);
+    (void)hipFree(q.d_arena);
+    (void)hipFree(q.d_wire);
+    (void)hipFree(q.d_streams);
+    (void)hipFree(q.d_results);
+    (void)hipFree(q.d_read_end);
+    (void)hipFree(q.d_desc);
+    (void)hipFree(q.d_seg);
+    if (q.up_ev) (void)hipEventDestroy(q.up_ev);
+    if (q.done_ev) (void)hipEventDestroy(q.done_ev);
 }
 
-static void release(uvhttp_ws_amd_batcher_t* b) {
+bool alloc_queue(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
+    const size_t ns = b->cfg.max_connections, nr = b->cfg.max_reads;
+    q.max_frames = kMinFrames;
+    return hipHostMalloc((void**)&q.h_arena, b->wire_cap, hipHostMallocDefault) == hipSuccess &&
+           hipHostMalloc((void**)&q.h_wire, b->wire_cap, hipHostMallocDefault) == hipSuccess &&
+           hipHostMalloc((void**)&q.h_streams, ns * sizeof(uvhttp_ws_stream_t), hipHostMallocDefault) == hipSuccess &&
+           hipHostMalloc((void**)&q.h_results, ns * sizeof(uvhttp_ws_stream_result_t), hipHostMallocDefault) == hipSuccess &&
+           hipHostMalloc((void**)&q.h_read_end, nr * sizeof(uint64_t), hipHostMallocDefault) == hipSuccess &&
+           hipHostMalloc((void**)&q.h_desc, (size_t)q.max_frames * sizeof(uvhttp_ws_frame_desc_t), hipHostMallocDefault) == hipSuccess &&
+           hipHostMalloc((void**)&q.h_seg, (nr + ns) * sizeof(GatherSeg), hipHostMallocDefault) == hipSuccess &&
+           hipMalloc((void**)&q.d_arena, b->wire_cap) == hipSuccess &&
+           hipMalloc((void**)&q.d_wire, b->wire_cap) == hipSuccess &&
+           hipMalloc((void**)&q.d_streams, ns * sizeof(uvhttp_ws_stream_t)) == hipSuccess &&
+           hipMalloc((void**)&q.d_results, ns * sizeof(uvhttp_ws_stream_result_t)) == hipSuccess &&
+           hipMalloc((void**)&q.d_read_end, nr * sizeof(uint64_t)) == hipSuccess &&
+           hipMalloc((void**)&q.d_desc, (size_t)q.max_frames * sizeof(uvhttp_ws_frame_desc_t)) == hipSuccess &&
+           hipMalloc((void**)&q.d_seg, (nr + ns) * sizeof(GatherSeg)) == hipSuccess &&
+           hipEventCreateWithFlags(&q.up_ev, hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&q.done_ev, hipEventDisableTiming) == hipSuccess;
+}
+
+void release(uvhttp_ws_amd_batcher_t* b) {
     if (b->eng) {
         int prev = 0;
         (void)hipGetDevice(&prev);
         (void)hipSetDevice(b->cfg.device);
-        if (b->stream) (void)hipStreamSynchronize(b->stream);
-        (void)hipHostFree(b->h_wire);
-        (void)hipHostFree(b->h_streams);
-        (void)hipHostFree(b->h_results);
-        (void)hipHostFree(b->h_read_end);
-        (void)hipHostFree(b->h_desc);
-        (void)hipHostFree(b->h_arena);
-        (void)hipHostFree(b->h_seg);
-        (void)hipFree(b->d_arena);
-        (void)hipFree(b->d_seg);
-        (void)hipFree(b->d_wire);
-        (void)hipFree(b->d_streams);
-        (void)hipFree(b->d_results);
-        (void)hipFree(b->d_read_end);
-        (void)hipFree(b->d_desc);
-        if (b->stream) (void)hipStreamDestroy(b->stream);
+        if (b->up) (void)hipStreamSynchronize(b->up);
+        if (b->cs) (void)hipStreamSynchronize(b->cs);
+        free_queue(b->q[0]);
+        free_queue(b->q[1]);
+        if (b->up) (void)hipStreamDestroy(b->up);
+        if (b->cs) (void)hipStreamDestroy(b->cs);
         uvhttp_ws_gpu_engine_free(b->eng);
         (void)hipSetDevice(prev);
     }
     delete b;
 }
 
-static void clear_queue(uvhttp_ws_amd_batcher_t* b) {
-    b->arena.clear();
-    b->arena_len = b->reads_end = 0;
-    b->reads.clear();
-    b->slots.clear();
-    b->slot_of.clear();
-    b->staged = 0;
+void clear_queue(BatchQueue& q) {
+    q.arena.clear();
+    q.arena_len = q.uploaded = 0;
+    q.reads.clear();
+    q.slots.clear();
+    q.slot_of.clear();
+    q.staged = q.bytes = 0;
+    q.in_flight = false;
+    q.launch_rc = 0;
+    q.nk = 0;
+    q.pos = 0;
+    q.slot_k.clear();
 }
 
-static void report_failure(uvhttp_ws_amd_batcher_t* b, ConnSlot& s, int rc) {
-    b->failed.insert(s.conn);
-    b->st.failures++;
-    s.dropped = true;
-    if (b->cfg.on_failure) b->cfg.on_failure(b->cfg.ctx, s.conn, rc);
-}
-
-// the reference's path: process_data per read, until one fails
-static void flush_host(uvhttp_ws_amd_batcher_t* b) {
-    b->st.host_flushes++;
-    for (size_t k = 0; k < b->slots.size(); ++k) {
-        ConnSlot& s = b->slots[k];
-        for (uint32_t r : s.reads) {
-            if (s.dropped) break;
-            const QueuedRead& q = b->reads[r];
-            const uvhttp_error_t rc =
-                uvhttp_ws_process_data(s.conn, arena_data(b) + q.off, (size_t)q.len);
-            b->st.host_reads++;
-            if (rc != UVHTTP_OK) report_failure(b, s, rc);
-        }
+// device batcher: the arena bytes not yet sent go to HBM on the upload stream
+void upload_tail(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
+    if (q.arena_len > q.uploaded) {
+        (void)hipMemcpyAsync(q.d_arena + q.uploaded, q.h_arena + q.uploaded,
+                             q.arena_len - q.uploaded, hipMemcpyHostToDevice, b->up);
+        q.uploaded = q.arena_len;
     }
 }
 
-// stage -> H2D -> decode_reads -> D2H -> deliver.  Returns 1 when the flush must run on
-// the host instead (frame capacity), 0 when delivered, < 0 on a device error (nothing
-// delivered).
-static int flush_device(uvhttp_ws_amd_batcher_t* b) {
-    const auto t0 = std::chrono::steady_clock::now();
+void report_failure(uvhttp_ws_amd_batcher_t* b, uvhttp_ws_connection_t* conn, int rc) {
+    b->failed.insert(conn);
+    b->st.failures++;
+    if (b->cfg.on_failure) b->cfg.on_failure(b->cfg.ctx, conn, rc);
+}
+
+// the reference's path: process_data per read, until one fails.  Slots are addressed by
+// index and re-read after every callback (forget() may mark one dropped meanwhile); reads
+// submitted from callbacks go to the other queue, so this queue does not change under us.
+void flush_host(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
+    b->st.host_flushes++;
+    b->delivering++;
+    for (size_t k = 0; k < q.slots.size(); ++k) {
+        for (size_t j = 0; j < q.slots[k].reads.size(); ++j) {
+            if (q.slots[k].dropped || b->failed.count(q.slots[k].conn)) break;
+            const QueuedRead r = q.reads[q.slots[k].reads[j]];
+            uvhttp_ws_connection_t* conn = q.slots[k].conn;
+            const uvhttp_error_t rc =
+                uvhttp_ws_process_data(conn, arena_data(b, q) + r.off, (size_t)r.len);
+            b->st.host_reads++;
+            if (rc != UVHTTP_OK) {
+                q.slots[k].dropped = true;
+                report_failure(b, conn, rc);
+            }
+        }
+    }
+    b->delivering--;
+}
+
+// grow a queue's descriptor capacity to nf frames (device + pinned host copy)
+int grow_desc(uvhttp_ws_amd_batcher_t* b, BatchQueue& q, uint64_t nf) {
+    if (nf <= q.max_frames) return 0;
+    uint64_t want = 2ull * q.max_frames;
+    if (want < nf) want = nf;
+    if (want > kMaxFramesPerFlush) want = kMaxFramesPerFlush;
+    if (want < nf) return 1;  // more frames than one decode takes: the host decodes it
+    (void)hipHostFree(q.h_desc);
+    (void)hipFree(q.d_desc);
+    q.h_desc = nullptr;
+    q.d_desc = nullptr;
+    q.max_frames = 0;
+    if (hipHostMalloc((void**)&q.h_desc, want * sizeof(uvhttp_ws_frame_desc_t), hipHostMallocDefault) != hipSuccess ||
+        hipMalloc((void**)&q.d_desc, want * sizeof(uvhttp_ws_frame_desc_t)) != hipSuccess ||
+        uvhttp_ws_gpu_engine_reserve(b->eng, (uint32_t)want, b->wire_cap, 0) != 0)
+        return UVHTTP_WS_GPU_ENOMEM;
+    q.max_frames = (uint32_t)want;
+    return 0;
+}
+
+// Stage q's connections (recv-buffer prefixes from their current state, read tables) and
+// enqueue H2D -> gather -> decode_reads -> D2H.  Returns 0 when launched, 1 when the queue
+// must be decoded on the host instead (it does not fit the device layout), < 0 on an error.
+int launch_device(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
     uint64_t pos = 0;
     uint32_t nr = 0, nk = 0, nseg = 0;
-    std::vector<uint32_t> slot_k(b->slots.size(), UINT32_MAX);
-    // prefixes go after the reads; a flush that failed (queue kept) and is retried starts over
-    b->arena_len = b->reads_end;
-    for (size_t k = 0; k < b->slots.size(); ++k) {
-        ConnSlot& s = b->slots[k];
-        if (s.dropped) continue;
+    q.slot_k.assign(q.slots.size(), UINT32_MAX);
+    // room check first: prefixes go after the reads in the arena, and the device layout
+    // (16-byte aligned connections) must fit the device wire
+    uint64_t prefix = 0, layout = 0;
+    for (const ConnSlot& s : q.slots) {
+        if (s.dropped || b->failed.count(s.conn)) continue;
+        prefix += s.conn->recv_buffer_pos;
+        layout = align16(layout) + s.conn->recv_buffer_pos + s.bytes;
+    }
+    if (q.arena_len + prefix > b->wire_cap || layout > b->wire_cap) return 1;
+    for (size_t k = 0; k < q.slots.size(); ++k) {
+        ConnSlot& s = q.slots[k];
+        if (s.dropped || b->failed.count(s.conn)) continue;
         uvhttp_ws_connection_t* c = s.conn;
         pos = align16(pos);
         const uint64_t begin = pos;
         if (c->recv_buffer_pos) {  // the bytes recv_buffer already holds come first
-            const uint64_t off = arena_append(b, c->recv_buffer, c->recv_buffer_pos);
-            b->h_seg[nseg++] = GatherSeg{off, pos, c->recv_buffer_pos};
+            const uint64_t off = q.arena_len;
+            memcpy(q.h_arena + off, c->recv_buffer, c->recv_buffer_pos);
+            q.arena_len += c->recv_buffer_pos;
+            q.h_seg[nseg++] = GatherSeg{off, pos, c->recv_buffer_pos};
         }
         pos += c->recv_buffer_pos;
         const uint32_t r0 = nr;
         for (uint32_t r : s.reads) {
-            const QueuedRead& q = b->reads[r];
-            if (q.len) b->h_seg[nseg++] = GatherSeg{q.off, pos, q.len};
-            pos += q.len;
-            b->h_read_end[nr++] = pos - begin;
+            const QueuedRead& qr = q.reads[r];
+            if (qr.len) q.h_seg[nseg++] = GatherSeg{qr.off, pos, qr.len};
+            pos += qr.len;
+            q.h_read_end[nr++] = pos - begin;
         }
-        uvhttp_ws_stream_init(c, begin, pos - begin, &b->h_streams[nk]);
-        b->h_streams[nk].first_read = r0;
-        b->h_streams[nk].n_reads = nr - r0;
-        slot_k[k] = nk++;
+        uvhttp_ws_stream_init(c, begin, pos - begin, &q.h_streams[nk]);
+        q.h_streams[nk].first_read = r0;
+        q.h_streams[nk].n_reads = nr - r0;
+        q.slot_k[k] = nk++;
     }
-    if (!nk) return 0;
-    int prev = 0;
-    (void)hipGetDevice(&prev);
-    if (prev != b->cfg.device) (void)hipSetDevice(b->cfg.device);
+    q.nk = nk;
+    q.pos = pos;
+    if (!nk) return 1;  // nothing left to decode (all dropped): the host path is a no-op
     // frames this flush can hold: a server connection's frames are >= 6 bytes except a
-    // failing last one, so bytes / 6 + connections never overflows for servers; the
-    // descriptor buffers grow to that bound on demand
-    const uint64_t bound = pos / 6 + nk + 1;
-    if (bound > b->max_frames) {
-        const uint64_t nf = bound > 2ull * b->max_frames ? bound : 2ull * b->max_frames;
-        (void)hipHostFree(b->h_desc);
-        (void)hipFree(b->d_desc);
-        b->h_desc = nullptr;
-        b->d_desc = nullptr;
-        b->max_frames = 0;
-        if (nf > 0xFFFFFFFFull ||
-            hipHostMalloc((void**)&b->h_desc, nf * sizeof(uvhttp_ws_frame_desc_t), hipHostMallocDefault) != hipSuccess ||
-            hipMalloc((void**)&b->d_desc, nf * sizeof(uvhttp_ws_frame_desc_t)) != hipSuccess ||
-            uvhttp_ws_gpu_engine_reserve(b->eng, (uint32_t)nf, b->wire_cap, 0) != 0) {
-            if (prev != b->cfg.device) (void)hipSetDevice(prev);
-            return UVHTTP_WS_GPU_ENOMEM;
-        }
-        b->max_frames = (uint32_t)nf;
-    }
-    hipStream_t s = b->stream;
-    int rc = UVHTTP_WS_GPU_OK;
-    hipError_t h = hipMemcpyAsync(b->d_arena, b->h_arena, b->arena_len, hipMemcpyHostToDevice, s);
+    // failing last one, so bytes / 6 + connections bounds them for servers (a client-side
+    // connection that exceeds it reports ERR_CAPACITY and is re-run on the host)
+    const int g = grow_desc(b, q, pos / 6 + nk + 1);
+    if (g) return g;
+    if (b->fail_every && ++b->launches % b->fail_every == 0) return UVHTTP_WS_GPU_ELAUNCH;
+    hipStream_t s = b->cs;
+    upload_tail(b, q);
+    hipError_t h = hipEventRecord(q.up_ev, b->up);
+    if (h == hipSuccess) h = hipStreamWaitEvent(s, q.up_ev, 0);
     if (h == hipSuccess && nseg)
-        h = hipMemcpyAsync(b->d_seg, b->h_seg, nseg * sizeof(GatherSeg), hipMemcpyHostToDevice, s);
+        h = hipMemcpyAsync(q.d_seg, q.h_seg, nseg * sizeof(GatherSeg), hipMemcpyHostToDevice, s);
     if (h == hipSuccess && nseg) {
-        hipLaunchKernelGGL(k_batcher_gather, dim3(nseg), dim3(256), 0, s, b->d_arena, b->d_wire,
-                           b->d_seg);
+        hipLaunchKernelGGL(k_batcher_gather, dim3(nseg), dim3(256), 0, s, q.d_arena, q.d_wire, q.d_seg);
         h = hipGetLastError();
     }
     if (h == hipSuccess)
-        h = hipMemcpyAsync(b->d_streams, b->h_streams, nk * sizeof(uvhttp_ws_stream_t),
+        h = hipMemcpyAsync(q.d_streams, q.h_streams, nk * sizeof(uvhttp_ws_stream_t),
                            hipMemcpyHostToDevice, s);
     if (h == hipSuccess && nr)
-        h = hipMemcpyAsync(b->d_read_end, b->h_read_end, nr * sizeof(uint64_t),
-                           hipMemcpyHostToDevice, s);
+        h = hipMemcpyAsync(q.d_read_end, q.h_read_end, nr * sizeof(uint64_t), hipMemcpyHostToDevice, s);
+    int rc = UVHTTP_WS_GPU_OK;
     if (h == hipSuccess)
-        rc = uvhttp_ws_gpu_decode_reads(b->eng, b->d_wire, pos, b->d_streams, nk, b->d_read_end,
-                                        nr, b->max_frames, b->d_desc, b->d_results, s);
+        rc = uvhttp_ws_gpu_decode_reads(b->eng, q.d_wire, pos, q.d_streams, nk, q.d_read_end, nr,
+                                        q.max_frames, q.d_desc, q.d_results, s);
     if (h == hipSuccess && rc == UVHTTP_WS_GPU_OK)
-        h = hipMemcpyAsync(b->h_results, b->d_results, nk * sizeof(uvhttp_ws_stream_result_t),
+        h = hipMemcpyAsync(q.h_results, q.d_results, nk * sizeof(uvhttp_ws_stream_result_t),
                            hipMemcpyDeviceToHost, s);
     if (h == hipSuccess && rc == UVHTTP_WS_GPU_OK)
-        h = hipMemcpyAsync(b->h_wire, b->d_wire, pos, hipMemcpyDeviceToHost, s);
-    if (h == hipSuccess && rc == UVHTTP_WS_GPU_OK) rc = uvhttp_ws_gpu_engine_sync(b->eng, s);
+        h = hipMemcpyAsync(q.h_wire, q.d_wire, pos, hipMemcpyDeviceToHost, s);
+    if (h == hipSuccess && rc == UVHTTP_WS_GPU_OK) h = hipEventRecord(q.done_ev, s);
+    if (h == hipSuccess && rc == UVHTTP_WS_GPU_OK && b->cfg.on_ready)
+        h = hipLaunchHostFunc(s, b->cfg.on_ready, b->cfg.ready_ctx);
+    if (h != hipSuccess) return UVHTTP_WS_GPU_ELAUNCH;
+    return rc;
+}
+
+// q's decode has finished (or failed): deliver it, or decode it on the host when the
+// device could not (nothing of q has been delivered before this point).
+int complete_device(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
+    int rc = q.launch_rc;
+    if (!rc) {
+        const auto tw = std::chrono::steady_clock::now();
+        if (hipEventSynchronize(q.done_ev) != hipSuccess) rc = UVHTTP_WS_GPU_ELAUNCH;
+        else rc = uvhttp_ws_gpu_engine_sync(b->eng, b->cs);  // device-side give-ups
+        b->st.wait_ms += ms_since(tw);
+    }
     uint64_t frames = 0;
     bool capacity = false;
-    if (h == hipSuccess && rc == UVHTTP_WS_GPU_OK) {
-        for (uint32_t k = 0; k < nk; ++k) {
-            const uvhttp_ws_stream_result_t& r = b->h_results[k];
+    if (!rc) {
+        for (uint32_t k = 0; k < q.nk; ++k) {
+            const uvhttp_ws_stream_result_t& r = q.h_results[k];
             if (r.first_status == UVHTTP_WS_FRAME_ERR_CAPACITY) capacity = true;
             const uint64_t e = (uint64_t)r.first_frame + r.n_frames;
             if (r.n_frames && e > frames) frames = e;
         }
-        if (!capacity && frames) {
-            h = hipMemcpyAsync(b->h_desc, b->d_desc, frames * sizeof(uvhttp_ws_frame_desc_t),
-                               hipMemcpyDeviceToHost, s);
-            if (h == hipSuccess) h = hipStreamSynchronize(s);
-        }
+        if (!capacity && frames &&
+            hipMemcpy(q.h_desc, q.d_desc, frames * sizeof(uvhttp_ws_frame_desc_t),
+                      hipMemcpyDeviceToHost) != hipSuccess)
+            rc = UVHTTP_WS_GPU_ELAUNCH;
     }
-    if (prev != b->cfg.device) (void)hipSetDevice(prev);
-    if (h != hipSuccess) return UVHTTP_WS_GPU_ELAUNCH;
-    if (rc != UVHTTP_WS_GPU_OK) return rc;
-    if (capacity) {
-        b->st.capacity_flushes++;
-        return 1;
+    if (rc || capacity) {
+        // the host decodes the queue instead (the reads are still in the pinned arena and
+        // no connection has seen any of them); a device error is counted and returned
+        if (capacity) b->st.capacity_flushes++;
+        if (rc) b->st.device_errors++;
+        flush_host(b, q);
+        return rc;
     }
     b->st.device_flushes++;
-    b->st.device_bytes += pos;
+    b->st.device_bytes += q.pos;
     b->st.device_frames += frames;
     // deliver, connection by connection (callbacks may forget connections as we go)
-    for (size_t k = 0; k < b->slots.size(); ++k) {
-        ConnSlot& sl = b->slots[k];
-        if (slot_k[k] == UINT32_MAX || sl.dropped) continue;
-        const uint32_t j = slot_k[k];
-        const uvhttp_error_t dr = uvhttp_ws_deliver_stream(sl.conn, b->h_wire, b->h_desc,
-                                                           &b->h_streams[j], &b->h_results[j]);
-        b->st.device_reads += b->h_results[j].calls;
-        if (dr != UVHTTP_OK) report_failure(b, sl, dr);
+    b->delivering++;
+    for (size_t k = 0; k < q.slots.size(); ++k) {
+        if (q.slot_k[k] == UINT32_MAX || q.slots[k].dropped) continue;
+        const uint32_t j = q.slot_k[k];
+        uvhttp_ws_connection_t* conn = q.slots[k].conn;
+        const uvhttp_error_t dr =
+            uvhttp_ws_deliver_stream(conn, q.h_wire, q.h_desc, &q.h_streams[j], &q.h_results[j]);
+        b->st.device_reads += q.h_results[j].calls;
+        if (dr != UVHTTP_OK) {
+            q.slots[k].dropped = true;
+            report_failure(b, conn, dr);
+        }
     }
-    b->st.device_ms +=
-        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    b->delivering--;
+    b->st.device_ms += ms_since(q.t_submit);
     return 0;
 }
+
+// Finish the queue in flight, if any.  wait = false: only when its results are already back.
+// Returns 1 when a queue was delivered, 0 when none (or not ready), < 0 a device error (the
+// queue was then decoded on the host).
+int finish_inflight(uvhttp_ws_amd_batcher_t* b, bool wait) {
+    BatchQueue& q = b->q[b->cur ^ 1];
+    if (!q.in_flight) return 0;
+    if (!wait && !q.launch_rc && hipEventQuery(q.done_ev) == hipErrorNotReady) return 0;
+    const int rc = complete_device(b, q);
+    clear_queue(q);
+    return rc < 0 ? rc : 1;
+}
+
+// Hand the accumulating queue over: finish the one in flight (its connections' state must be
+// final before this queue is staged), switch submit_read to the other queue, then decode this
+// one on the host (small) or start its device decode.  wait = false: when the queue in flight
+// is not finished yet, only note the request (poll starts the queue once it has delivered).
+int start_flush(uvhttp_ws_amd_batcher_t* b, bool wait) {
+    const BatchQueue& other = b->q[b->cur ^ 1];
+    if (other.in_flight && !wait && !other.launch_rc && hipEventQuery(other.done_ev) == hipErrorNotReady) {
+        b->want_flush = true;
+        return 0;
+    }
+    int rc = finish_inflight(b, true);
+    rc = rc < 0 ? rc : 0;
+    b->want_flush = false;
+    BatchQueue& q = b->q[b->cur];
+    if (q.reads.empty()) return rc;
+    b->st.flushes++;
+    b->cur ^= 1;  // reads submitted from now on (callbacks included) queue in the other one
+    if (b->eng && q.bytes >= b->cfg.min_device_bytes) {
+        int prev = 0;
+        (void)hipGetDevice(&prev);
+        if (prev != b->cfg.device) (void)hipSetDevice(b->cfg.device);
+        q.t_submit = std::chrono::steady_clock::now();
+        const int lr = launch_device(b, q);
+        if (prev != b->cfg.device) (void)hipSetDevice(prev);
+        if (lr == 1) {
+            b->st.fallback_flushes++;
+            flush_host(b, q);
+            clear_queue(q);
+        } else {
+            // launched, or a launch error that complete_device turns into a host decode
+            q.in_flight = true;
+            q.launch_rc = lr;
+            b->st.async_flushes++;
+        }
+    } else {
+        flush_host(b, q);
+        clear_queue(q);
+    }
+    return rc;
+}
+
+// loop-thread time spent inside one batcher call (waiting, staging, delivering)
+struct Blocked {
+    uvhttp_ws_amd_batcher_t* b;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    ~Blocked() {
+        const double ms = ms_since(t0);
+        b->st.blocked_ms += ms;
+        if (ms > b->st.max_blocked_ms) b->st.max_blocked_ms = ms;
+    }
+};
+
+}  // namespace
 
 extern "C" {
 
@@ -299,41 +473,34 @@ int uvhttp_ws_amd_batcher_create(const uvhttp_ws_amd_batcher_config_t* cfg,
     if (!cfg || !out || !cfg->max_bytes || !cfg->max_connections || !cfg->max_reads)
         return UVHTTP_WS_GPU_EINVAL;
     *out = nullptr;
+    // one flush's device layout must stay addressable by decode_reads (its frame bound is
+    // bytes / 6 + connections <= 2^26; larger flushes would always fall back to the host)
+    if (cfg->device >= 0 && cfg->max_bytes / 6 + cfg->max_connections + 1 > kMaxFramesPerFlush)
+        return UVHTTP_WS_GPU_EINVAL;
     uvhttp_ws_amd_batcher_t* b = new (std::nothrow) uvhttp_ws_amd_batcher_t();
     if (!b) return UVHTTP_WS_GPU_ENOMEM;
     b->cfg = *cfg;
     memset(&b->st, 0, sizeof(b->st));
-    if (cfg->device < 0) b->arena.reserve(cfg->max_bytes < (64ull << 20) ? cfg->max_bytes : (64ull << 20));
-    if (cfg->device >= 0) {
+    if (cfg->device < 0) {
+        const size_t r = cfg->max_bytes < (64ull << 20) ? cfg->max_bytes : (64ull << 20);
+        b->q[0].arena.reserve(r);
+        b->q[1].arena.reserve(r);
+    } else {
         int rc = uvhttp_ws_gpu_engine_create(cfg->device, &b->eng);
         if (rc) {
             b->eng = nullptr;
             delete b;
             return rc;
         }
-        // descriptor capacity starts small and grows with the flushes (flush_device)
         b->wire_cap = cfg->max_bytes + 16ull * cfg->max_connections + 64;
-        b->max_frames = 65536;
+        if (const char* fe = getenv("UVHTTP_WS_BATCHER_FAIL_EVERY")) b->fail_every = (uint32_t)atoi(fe);
         int prev = 0;
         (void)hipGetDevice(&prev);
         (void)hipSetDevice(cfg->device);
-        const size_t ns = cfg->max_connections;
-        bool ok = hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) == hipSuccess &&
-                  hipHostMalloc((void**)&b->h_wire, b->wire_cap, hipHostMallocDefault) == hipSuccess &&
-                  hipHostMalloc((void**)&b->h_streams, ns * sizeof(uvhttp_ws_stream_t), hipHostMallocDefault) == hipSuccess &&
-                  hipHostMalloc((void**)&b->h_results, ns * sizeof(uvhttp_ws_stream_result_t), hipHostMallocDefault) == hipSuccess &&
-                  hipHostMalloc((void**)&b->h_read_end, cfg->max_reads * sizeof(uint64_t), hipHostMallocDefault) == hipSuccess &&
-                  hipHostMalloc((void**)&b->h_desc, (size_t)b->max_frames * sizeof(uvhttp_ws_frame_desc_t), hipHostMallocDefault) == hipSuccess &&
-                  hipMalloc((void**)&b->d_wire, b->wire_cap) == hipSuccess &&
-                  hipMalloc((void**)&b->d_streams, ns * sizeof(uvhttp_ws_stream_t)) == hipSuccess &&
-                  hipMalloc((void**)&b->d_results, ns * sizeof(uvhttp_ws_stream_result_t)) == hipSuccess &&
-                  hipMalloc((void**)&b->d_read_end, cfg->max_reads * sizeof(uint64_t)) == hipSuccess &&
-                  hipMalloc((void**)&b->d_desc, (size_t)b->max_frames * sizeof(uvhttp_ws_frame_desc_t)) == hipSuccess &&
-                  hipHostMalloc((void**)&b->h_arena, b->wire_cap, hipHostMallocDefault) == hipSuccess &&
-                  hipMalloc((void**)&b->d_arena, b->wire_cap) == hipSuccess &&
-                  hipHostMalloc((void**)&b->h_seg, ((size_t)cfg->max_reads + ns) * sizeof(GatherSeg), hipHostMallocDefault) == hipSuccess &&
-                  hipMalloc((void**)&b->d_seg, ((size_t)cfg->max_reads + ns) * sizeof(GatherSeg)) == hipSuccess;
-        if (ok) ok = uvhttp_ws_gpu_engine_reserve(b->eng, b->max_frames, b->wire_cap, 0) == 0;
+        bool ok = hipStreamCreateWithFlags(&b->up, hipStreamNonBlocking) == hipSuccess &&
+                  hipStreamCreateWithFlags(&b->cs, hipStreamNonBlocking) == hipSuccess &&
+                  alloc_queue(b, b->q[0]) && alloc_queue(b, b->q[1]);
+        if (ok) ok = uvhttp_ws_gpu_engine_reserve(b->eng, kMinFrames, b->wire_cap, 0) == 0;
         (void)hipSetDevice(prev);
         if (!ok) {
             release(b);
@@ -348,25 +515,37 @@ void uvhttp_ws_amd_batcher_free(uvhttp_ws_amd_batcher_t* b) {
     if (b) release(b);
 }
 
+int uvhttp_ws_amd_batcher_flush_async(uvhttp_ws_amd_batcher_t* b) {
+    if (!b) return UVHTTP_WS_GPU_EINVAL;
+    if (b->delivering) return UVHTTP_WS_GPU_OK;  // (from a callback: the caller flushes later)
+    Blocked bl{b};
+    return start_flush(b, false);
+}
+
+int uvhttp_ws_amd_batcher_poll(uvhttp_ws_amd_batcher_t* b) {
+    if (!b) return UVHTTP_WS_GPU_EINVAL;
+    if (b->delivering) return 0;
+    if (!b->q[b->cur ^ 1].in_flight) return 0;
+    Blocked bl{b};
+    const int rc = finish_inflight(b, false);
+    if (rc != 0 && b->want_flush) {  // delivered: start what flush_async asked for meanwhile
+        const int r2 = start_flush(b, false);
+        if (r2 < 0 && rc > 0) return r2;
+    }
+    return rc;
+}
+
+int uvhttp_ws_amd_batcher_in_flight(const uvhttp_ws_amd_batcher_t* b) {
+    return b && b->q[b->cur ^ 1].in_flight ? 1 : 0;
+}
+
 int uvhttp_ws_amd_batcher_flush(uvhttp_ws_amd_batcher_t* b) {
     if (!b) return UVHTTP_WS_GPU_EINVAL;
-    if (b->in_flush || b->reads.empty()) return UVHTTP_WS_GPU_OK;
-    b->in_flush = true;
-    b->st.flushes++;
-    int rc = UVHTTP_WS_GPU_OK;
-    uint64_t queued = 0;
-    for (const ConnSlot& s : b->slots) queued += s.bytes;
-    if (b->eng && queued >= b->cfg.min_device_bytes) {
-        rc = flush_device(b);
-        if (rc == 1) {  // frame capacity (client-side connections only): the host decodes it
-            flush_host(b);
-            rc = UVHTTP_WS_GPU_OK;
-        }
-    } else {
-        flush_host(b);
-    }
-    b->in_flush = false;
-    if (rc == UVHTTP_WS_GPU_OK) clear_queue(b);
+    if (b->delivering) return UVHTTP_WS_GPU_OK;
+    Blocked bl{b};
+    int rc = start_flush(b, true);            // finishes the queue in flight, starts this one
+    const int r2 = finish_inflight(b, true);  // and waits for it
+    if (!rc && r2 < 0) rc = r2;
     return rc;
 }
 
@@ -375,51 +554,80 @@ uvhttp_error_t uvhttp_ws_amd_batcher_submit_read(uvhttp_ws_amd_batcher_t* b,
                                                  const uint8_t* data, size_t len) {
     if (!b || !conn || (!data && len)) return UVHTTP_ERROR_INVALID_PARAM;
     if (b->failed.count(conn)) return UVHTTP_ERROR_INVALID_PARAM;
-    auto it = b->slot_of.find(conn);
-    const bool fresh = it == b->slot_of.end();
-    const uint64_t need = (uint64_t)len + (fresh ? align16(conn->recv_buffer_pos) + 16 : 0);
-    if (b->staged + need > b->cfg.max_bytes || b->reads.size() + 1 > b->cfg.max_reads ||
-        (fresh && b->slots.size() + 1 > b->cfg.max_connections)) {
-        if (b->in_flush) return UVHTTP_ERROR_INVALID_PARAM;  // (not from a flush callback)
-        if (uvhttp_ws_amd_batcher_flush(b) != UVHTTP_WS_GPU_OK) return UVHTTP_ERROR_INVALID_PARAM;
+    BatchQueue* q = &b->q[b->cur];
+    auto it = q->slot_of.find(conn);
+    bool fresh = it == q->slot_of.end();
+    const uint64_t pre = align16(conn->recv_buffer_pos) + 16;
+    const uint64_t need = (uint64_t)len + (fresh ? pre : 0);
+    if (q->staged + need > b->cfg.max_bytes || q->reads.size() + 1 > b->cfg.max_reads ||
+        (fresh && q->slots.size() + 1 > b->cfg.max_connections)) {
+        // the queue is full: hand it to the decoder first (not from inside a callback, where
+        // the flush being delivered cannot be finished: the read is refused there)
+        if (b->delivering) return UVHTTP_ERROR_INVALID_PARAM;
+        Blocked bl{b};
+        (void)start_flush(b, true);  // (a device error there was decoded on the host and counted)
         if (b->failed.count(conn)) return UVHTTP_ERROR_INVALID_PARAM;
-        it = b->slot_of.end();
-        if (align16(conn->recv_buffer_pos) + 16 + len > b->cfg.max_bytes) {
-            // larger than a whole flush: decode it here, in order (nothing of it is queued)
+        if (pre + len > b->cfg.max_bytes) {
+            // larger than a whole flush: every earlier read of the connection must be
+            // delivered first, then the read is decoded here (nothing of it is queued)
+            (void)finish_inflight(b, true);
+            if (b->failed.count(conn)) return UVHTTP_ERROR_INVALID_PARAM;
             const uvhttp_error_t rc = uvhttp_ws_process_data(conn, data, len);
             b->st.host_reads++;
+            b->st.direct_reads++;
             if (rc != UVHTTP_OK) b->failed.insert(conn);
             return rc;
         }
-        return uvhttp_ws_amd_batcher_submit_read(b, conn, data, len);
+        q = &b->q[b->cur];
+        it = q->slot_of.find(conn);
+        fresh = it == q->slot_of.end();
     }
     uint32_t k;
     if (fresh) {
-        k = (uint32_t)b->slots.size();
-        b->slots.push_back(ConnSlot{conn, {}, 0, conn->recv_buffer_pos, false});
-        b->slot_of[conn] = k;
-        b->staged += align16(conn->recv_buffer_pos) + 16;
+        k = (uint32_t)q->slots.size();
+        q->slots.push_back(ConnSlot{conn, {}, 0, false});
+        q->slot_of[conn] = k;
+        q->staged += pre;
     } else {
         k = it->second;
     }
-    const uint64_t off = arena_append(b, data, len);
-    b->reads_end = b->arena_len;
-    b->reads.push_back(QueuedRead{off, len});
-    b->slots[k].reads.push_back((uint32_t)(b->reads.size() - 1));
-    b->slots[k].bytes += len;
-    b->staged += len;
+    uint64_t off;
+    if (!b->eng) {
+        off = q->arena.size();
+        q->arena.insert(q->arena.end(), data, data + len);
+    } else {
+        off = q->arena_len;
+        if (off + len > b->wire_cap) return UVHTTP_ERROR_INVALID_PARAM;  // (cannot happen)
+        if (len) uvhttp_ws_amd_copy_stream(q->h_arena + off, data, len);
+        q->arena_len += len;
+        // a queue large enough for the device streams to HBM while it fills
+        if (q->bytes + len >= b->cfg.min_device_bytes && q->arena_len - q->uploaded >= kUploadPiece) {
+            int prev = 0;
+            (void)hipGetDevice(&prev);
+            if (prev != b->cfg.device) (void)hipSetDevice(b->cfg.device);
+            upload_tail(b, *q);
+            if (prev != b->cfg.device) (void)hipSetDevice(prev);
+        }
+    }
+    q->reads.push_back(QueuedRead{off, len});
+    q->slots[k].reads.push_back((uint32_t)(q->reads.size() - 1));
+    q->slots[k].bytes += len;
+    q->staged += len;
+    q->bytes += len;
     return UVHTTP_OK;
 }
 
 void uvhttp_ws_amd_batcher_forget(uvhttp_ws_amd_batcher_t* b, struct uvhttp_ws_connection* conn) {
     if (!b || !conn) return;
     b->failed.erase(conn);
-    auto it = b->slot_of.find(conn);
-    if (it == b->slot_of.end()) return;
-    b->slots[it->second].dropped = true;  // the flush in progress (if any) skips it
-    if (!b->in_flush) {                   // (a new connection at this address gets a new slot)
-        b->slots[it->second].reads.clear();
-        b->slot_of.erase(it);
+    for (int i = 0; i < 2; ++i) {
+        BatchQueue& q = b->q[i];
+        auto it = q.slot_of.find(conn);
+        if (it == q.slot_of.end()) continue;
+        q.slots[it->second].dropped = true;  // a delivery in progress skips it
+        // (a new connection at this address gets a new slot; the old slot's reads stay in
+        // the arena, unreferenced)
+        if (i == b->cur) q.slot_of.erase(it);
     }
 }
 

@@ -432,3 +432,38 @@ uvhttp_error_t uvhttp_ws_deliver_stream(struct uvhttp_ws_connection* c, const ui
     }
     return r->status == 0 ? UVHTTP_OK : UVHTTP_ERROR_INVALID_PARAM;
 }
+
+/* Copy of a read into the batcher's pinned arena (ws_batcher.hip; internal).  The arena is
+ * only read again by the DMA engine, so whole 16-byte vectors go out with non-temporal stores:
+ * no read-for-ownership of the destination lines, no cache pollution (glibc memcpy switches
+ * to streaming stores only far above libuv's 16 KiB reads). */
+#include <emmintrin.h>
+__attribute__((visibility("hidden"))) void uvhttp_ws_amd_copy_stream(void* dst, const void* src,
+                                                                     size_t len) {
+    uint8_t* d = (uint8_t*)dst;
+    const uint8_t* s = (const uint8_t*)src;
+    if (len < 1024) {
+        memcpy(d, s, len);
+        return;
+    }
+    const size_t head = (16u - ((uintptr_t)d & 15u)) & 15u;
+    memcpy(d, s, head);
+    d += head;
+    s += head;
+    len -= head;
+    size_t i = 0;
+    for (; i + 64 <= len; i += 64) {
+        const __m128i a = _mm_loadu_si128((const __m128i*)(s + i));
+        const __m128i b = _mm_loadu_si128((const __m128i*)(s + i + 16));
+        const __m128i c = _mm_loadu_si128((const __m128i*)(s + i + 32));
+        const __m128i e = _mm_loadu_si128((const __m128i*)(s + i + 48));
+        _mm_stream_si128((__m128i*)(d + i), a);
+        _mm_stream_si128((__m128i*)(d + i + 16), b);
+        _mm_stream_si128((__m128i*)(d + i + 32), c);
+        _mm_stream_si128((__m128i*)(d + i + 48), e);
+    }
+    for (; i + 16 <= len; i += 16)
+        _mm_stream_si128((__m128i*)(d + i), _mm_loadu_si128((const __m128i*)(s + i)));
+    _mm_sfence();
+    memcpy(d + i, s + i, len - i);
+}
