@@ -5,17 +5,23 @@ Metric (BASELINE.json): "WebSocket payload unmask GiB/s (device-resident), 64 Ki
 1/2/4/8 GPU".  One *step* = one pass of the hot path — frame-header parse + validation +
 fragment state machine + payload unmask (include/uvhttp_ws_amd.h, decode_inplace) — over one
 batch of synthetic masked frames already resident in HBM.  Default workload = BASELINE
-config C3: 65 536 x 64 KiB masked BINARY frames per GPU.  Multi-GPU: one process per GPU
-(torch.distributed.run), each rank decodes its own shard (frames are independent: weak
-scaling, no data-path collective); a gloo barrier brackets the timed region and the max
-elapsed time over ranks is used.
+config C3: 65 536 x 64 KiB masked BINARY frames on one GPU.  Multi-GPU (default C5): one
+process per GPU, each rank decodes its own contiguous shard of the 8 388 608 frames (frames
+are independent: strong scaling, no data-path collective); a gloo barrier brackets the timed
+region and the max elapsed time over ranks is used.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4] [--mode inplace|compact]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4|c5] [--mode inplace|compact]
+                  [--rotate R]
 
 --config c5 runs BASELINE config C5 instead: 8 388 608 x 64 KiB frames in total, split into
 contiguous per-rank shards (strong scaling), each decoded in resident 1 048 576-frame passes.
 It is the default whenever more than one GPU runs (BASELINE config 5, "reported at 1/2/4/8
-GPUs"); the N=1 default (C3) also times C5 on its one GPU ("c5_1gpu") so the curve has a base.
+GPUs"); the N=1 default (C3) also times C5 on its one GPU ("c5_1gpu", and "c5_base": that
+value in the N>1 lines' unit) so the curve has a base.
+
+--rotate R decodes R independent copies of the batch round-robin (one per step), so a step's
+wire was last touched R-1 steps earlier: with R copies larger than the 256 MB Infinity Cache
+the rate is the cold-HBM one (C2 / C4 fit the cache once).
 
 Launch: under torch.distributed.run (RANK/WORLD_SIZE set) every process is one rank.  Started
 directly with --gpus N > 1, this process spawns the N rank processes itself (before anything
@@ -154,15 +160,38 @@ def _cpu_share():
         return os.cpu_count() or 1
 
 
+def cpu_quota():
+    """CPUs the cgroup grants this process (cgroup v2 cpu.max "quota period"), or None."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            return max(1, -(-int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def cpu_threads():
+    """(threads, source) for the all-cores baseline: UVHTTP_WS_CPU_THREADS, else the cgroup CPU
+    quota when one is set (the box grants a share of a larger machine), else every CPU in this
+    process's affinity mask."""
+    if os.environ.get("UVHTTP_WS_CPU_THREADS"):
+        return int(os.environ["UVHTTP_WS_CPU_THREADS"]), "UVHTTP_WS_CPU_THREADS"
+    aff, quota = _cpu_share(), cpu_quota()
+    if quota is not None and quota < aff:
+        return quota, f"cgroup cpu.max quota ({quota} CPUs; affinity mask {aff})"
+    return aff, f"sched_getaffinity ({aff} CPUs; cgroup cpu.max {'max' if quota is None else quota})"
+
+
 def cpu_baseline_threads(L, orc, cfg_name, seconds):
     """SURVEY §8(d)'s all-cores variant: T threads, one independent connection stream each
     (its own ~32 MiB sample of the workload), header parse + apply_mask, timed together.
-    T = the CPUs this process may run on, at most 16 (the GPU box grants each job a 16-CPU
-    share of a larger machine, so "all cores" here means that share; machine_cpus in the
-    record is the whole host).  UVHTTP_WS_CPU_THREADS overrides."""
+    T = cpu_threads(): the CPUs this process may really use (cgroup quota, else affinity),
+    named in the record."""
     import threading
     n, plen, frag, _ = CONFIGS[cfg_name]
-    T = int(os.environ.get("UVHTTP_WS_CPU_THREADS", min(16, _cpu_share())))
+    T, source = cpu_threads()
     sample = max(1, min(n, (32 << 20) // max(plen, 1)))
     bufs = [orc.gen_frames(sample, plen, SEED + 1 + t, fragmented=frag, total=sample)
             for t in range(T)]
@@ -188,8 +217,9 @@ def cpu_baseline_threads(L, orc, cfg_name, seconds):
         x.join()
     el = time.perf_counter() - t0
     return {"value": round(sum(done) / el / GIB, 3), "unit": "GiB/s", "cores": T,
+            "cores_source": source,
             "sample": f"{T} threads x {sample} frames x {plen} B, {el:.1f} s",
-            "note": "all CPUs granted to this process (<= 16), one connection stream each"}
+            "note": "every CPU this process may use, one connection stream each"}
 
 
 def pmc_traffic(cfg_name, mode):
@@ -214,6 +244,36 @@ def free_port():
     return port
 
 
+def visible_gpus():
+    """GPUs this process could use, without initialising HIP: HIP_VISIBLE_DEVICES /
+    ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES when set, else the KFD topology nodes that
+    have SIMDs (/sys/class/kfd/kfd/topology/nodes/*/properties: simd_count > 0)."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            return len([x for x in v.split(",") if x.strip() != ""])
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    n = 0
+    try:
+        for node in os.listdir(base):
+            try:
+                with open(os.path.join(base, node, "properties")) as f:
+                    props = dict(line.split() for line in f if len(line.split()) == 2)
+                if int(props.get("simd_count", "0")) > 0:
+                    n += 1
+            except (OSError, ValueError):
+                continue
+    except OSError:
+        pass
+    return n
+
+
+def parent_touched_gpu():
+    """True if this process imported torch and initialised its GPU state (never before a spawn)"""
+    t = sys.modules.get("torch")
+    return bool(t is not None and t.cuda.is_initialized())
+
+
 def spawn_ranks(n):
     """`python bench.py --gpus N` without a launcher: start N rank processes of this script
     (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, one GPU each), wait for all of them and
@@ -223,7 +283,8 @@ def spawn_ranks(n):
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
-                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   UVHTTP_WS_SPAWNED_FROM_GPU_PROCESS="1" if parent_touched_gpu() else "0")
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
                                       env=env, stdout=subprocess.PIPE if r == 0 else None,
                                       text=True))
@@ -258,7 +319,9 @@ class StubWorkload:
         return 0.0, 0
 
     def check(self):
-        pass
+        # tests: a rank whose decode "fails" must make the whole run exit non-zero
+        if os.environ.get("UVHTTP_WS_STUB_FAIL_RANK") == os.environ.get("RANK", "0"):
+            raise SystemExit("stub decode failed")
 
     def close(self):
         pass
@@ -283,6 +346,10 @@ class GpuWorkload:
         self.stream = stream = torch.cuda.current_stream(local)
         self.wire = torch.empty(wire_len + 64, dtype=torch.uint8, device=dev)
         eng.gen_frames(self.wire, n, plen, SEED + first, opcode0=2, fragmented=frag, stream=stream)
+        # --rotate R: R copies decoded round-robin, so a step's bytes are not the ones the
+        # previous step just wrote (cold HBM once R copies exceed the Infinity Cache)
+        self.wires = [self.wire] + [self.wire.clone() for _ in range(max(1, args.rotate) - 1)]
+        self.turn = 0
         self.desc, self.summ = eng.alloc_outputs(n)
         self.arena = self.msgs = None
         if mode == "compact":
@@ -326,6 +393,8 @@ class GpuWorkload:
 
     def one_pass(self):
         eng, stream = self.eng, self.stream
+        self.wire = self.wires[self.turn % len(self.wires)]
+        self.turn += 1
         if self.build_dev is not None:
             eng.build_frames(self.build_src, self.build_dev, self.n, self.build_out,
                              out_off=self.build_off, stream=stream)
@@ -354,6 +423,22 @@ class GpuWorkload:
     def kernel_time(self):
         return self.eng.kernel_time()
 
+    def copy_ceiling(self, reps=10):
+        """Same-run streaming ceiling: uvhttp_ws_gpu_apply_mask — one key XOR-ed
+        over the whole wire in place, the payload kernel's access pattern with no framing —
+        timed with HIP events on the same stream; an even count leaves the wire as it was.
+        -> (GB/s of read + write, average µs)"""
+        eng, w = self.eng, self.wires[0]
+        eng.kernel_time()
+        eng.set_timing(True)
+        for _ in range(reps + reps % 2):
+            eng.apply_mask(w, b"\x5a\xa5\x3c\xc3", length=self.wire_len, stream=self.stream)
+        self.torch.cuda.synchronize()
+        eng.set_timing(False)
+        ms, k = eng.kernel_time()
+        avg = ms / 1e3 / k
+        return 2 * self.wire_len / avg / 1e9, avg * 1e6
+
     def check(self):
         """Every frame of the shard must have been delivered (the decode really ran)."""
         n = self.n
@@ -372,7 +457,7 @@ class GpuWorkload:
 
     def close(self):
         self.eng.close()
-        for k in ("wire", "desc", "summ", "arena", "msgs", "build_src", "build_out",
+        for k in ("wire", "wires", "desc", "summ", "arena", "msgs", "build_src", "build_out",
                   "streams_dev", "s_desc"):
             setattr(self, k, None)
         self.torch.cuda.empty_cache()
@@ -441,13 +526,17 @@ def main():
                     help="N=1: skip the extra C5-on-one-GPU measurement")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--e2e", action="store_true", help="also time host->device->host")
+    ap.add_argument("--rotate", type=int, default=1,
+                    help="decode R copies of the batch round-robin (cold-cache rates)")
+    ap.add_argument("--no-ceiling", action="store_true", help="skip the copy-ceiling timing")
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)  # launcher tests
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # the parent never touches HIP (nor imports torch): it only counts devices from the
+        # environment / KFD topology and starts fresh rank processes
         if not args.stub:
-            import torch  # device_count does not initialise the GPU on this image
-            have = torch.cuda.device_count()
+            have = visible_gpus()
             if have < args.gpus:
                 raise SystemExit(f"--gpus {args.gpus} but only {have} GPU(s) visible")
         raise SystemExit(spawn_ranks(args.gpus))
@@ -480,12 +569,17 @@ def main():
     avg_kernel_s = (k_ms / 1e3 / k_n) if k_n else float("nan")
     achieved = alg_bytes / avg_kernel_s / 1e9 if k_n else None
     traffic = pmc_traffic(cfg, args.mode)
+    ceiling = None
+    if rank == 0 and not args.stub and not args.no_ceiling:
+        ceiling = wl.copy_ceiling()
     wl.close()
 
     extra = {}
     if rank == 0 and world == 1 and not args.stub:
         if cfg == "c3" and args.mode == "inplace" and not args.no_c5_base:
             extra["c5_1gpu"] = c5_one_gpu(args, local)
+            # the N>1 lines (default config C5) divide by this: same metric, same unit
+            extra["c5_base"] = extra["c5_1gpu"]["value"]
         if args.e2e:
             extra["e2e_pcie"] = e2e_rate(n, plen, stride, CONFIGS[cfg][3], local)
             extra["e2e_live"] = e2e_live(local)
@@ -524,11 +618,21 @@ def main():
                 "alg_bytes_per_launch": alg_bytes,
                 "avg_kernel_us": round(avg_kernel_s * 1e6, 2) if k_n else None,
                 "launches_timed": k_n,
+                "copy_ceiling": None if ceiling is None else {
+                    "kernel": "k_apply_mask (uvhttp_ws_gpu_apply_mask over the whole wire)",
+                    "achieved": round(ceiling[0], 1), "unit": "GB/s",
+                    "avg_us": round(ceiling[1], 2),
+                    "frac_of_peak": round(ceiling[0] / HBM_PEAK_GBS, 4),
+                    "kernel_frac_of_ceiling": round(achieved / ceiling[0], 4) if achieved else None},
             },
             "host_issue_us_per_step": round(getattr(wl, "host_issue_s", 0.0) / args.steps * 1e6, 2),
         }
         if args.stub:
             out["stub"] = True
+        if "UVHTTP_WS_SPAWNED_FROM_GPU_PROCESS" in os.environ:
+            out["spawned_from_gpu_process"] = os.environ["UVHTTP_WS_SPAWNED_FROM_GPU_PROCESS"] == "1"
+        if args.rotate > 1:
+            out["config"]["rotate"] = args.rotate
         if world == 1 and not args.no_cpu_baseline and not args.stub:
             out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
         out.update(extra)

@@ -198,8 +198,8 @@ def test_submit_and_forget_from_callbacks(device):
 @pytest.mark.gpu
 def test_capacity_and_device_failure_fall_back_to_host():
     """client-side connections of 2-byte unmasked frames overflow the frame capacity
-    (bytes / 6 + connections): the device reports ERR_CAPACITY and the queue re-runs on the
-    host.  Then every device launch fails (test hook): each queue is decoded on the host,
+    (a queue's descriptors: max(65 536, bytes / 6 + connections)): the device reports
+    ERR_CAPACITY and the queue re-runs on the host.  Then every device launch fails (test hook): each queue is decoded on the host,
     flush returns ELAUNCH and nothing is lost."""
     import torch
     if not torch.cuda.is_available():
@@ -212,7 +212,7 @@ def test_capacity_and_device_failure_fall_back_to_host():
     for k in range(8):
         prod = U.WsConnection(0, 16 << 20, 64 << 20)
         orc = _oracle.OracleConn(0, 16 << 20, 64 << 20, record=1)
-        data = b"".join(_frame(2, 1, b"", b"", False, 0) for _ in range(3000))
+        data = b"".join(_frame(2, 1, b"", b"", False, 0) for _ in range(12000))
         assert b.submit(prod, data) == 0
         assert orc.process_data(data) == 0
         prods.append(prod)
@@ -221,7 +221,7 @@ def test_capacity_and_device_failure_fall_back_to_host():
     st = b.stats()
     assert st["capacity_flushes"] == 1 and st["host_reads"] == 8
     for prod, orc in zip(prods, orcs):
-        assert len(prod.events) == len(orc.events()) == 3000
+        assert len(prod.events) == len(orc.events()) == 12000
     b.close()
 
     os.environ["UVHTTP_WS_BATCHER_FAIL_EVERY"] = "1"

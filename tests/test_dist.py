@@ -84,6 +84,36 @@ def test_bench_self_spawns_ranks(world):
     # the shard each rank timed: 8 388 608 / world frames in resident passes
     assert out["config"]["frames_per_gpu"] == 8388608 // world
     assert out["steps"] == 3 and out["ms_per_step"] > 0
+    # the parent spawned its ranks without importing torch / touching HIP
+    assert out["spawned_from_gpu_process"] is False
+
+
+def test_bench_rank_failure_fails_the_run():
+    """every rank checks its decode; one failing rank makes `bench.py --gpus 2` exit non-zero"""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["UVHTTP_WS_STUB_FAIL_RANK"] = "1"
+    p = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2",
+                        "--stub", "--steps", "2", "--warmup", "0"], capture_output=True,
+                       text=True, timeout=300, env=env, cwd=repo)
+    assert p.returncode != 0
+
+
+def test_visible_gpus_without_hip(monkeypatch):
+    """device counting for the spawn never calls into HIP"""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,3,5")
+    assert bench.visible_gpus() == 3
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES")
+    for v in ("ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+    assert bench.visible_gpus() >= 0  # KFD topology (0 in a container without a GPU)
+    assert "torch" not in sys.modules or not sys.modules["torch"].cuda.is_initialized()
 
 
 def test_bench_torchrun_form_single_process():

@@ -2168,7 +2168,12 @@ static int tls_timing_begin(uvhttp_tls_gpu_engine_t* e, hipStream_t s) {
     if (e->ev_used * 2 + 2 > (int)(sizeof(e->ev) / sizeof(e->ev[0]))) tls_harvest(e);
     const int k = e->ev_used;
     while (e->ev_created < 2 * k + 2) {
-        if (hipEventCreate(&e->ev[e->ev_created]) != hipSuccess) return -1;
+        // timing-only events: no system-scope fence (a fenced marker between two kernels
+        // idled the device ~5.8 us per event, profiles/r03p1 kernel trace); the caller's own
+        // synchronisation still orders the results.  UVHTTP_WS_TIMING_FENCE=1: fenced (A/B)
+        static const unsigned flags = getenv("UVHTTP_WS_TIMING_FENCE") && atoi(getenv("UVHTTP_WS_TIMING_FENCE"))
+                                          ? hipEventDefault : hipEventDisableSystemFence;
+        if (hipEventCreateWithFlags(&e->ev[e->ev_created], flags) != hipSuccess) return -1;
         e->ev_created++;
     }
     (void)hipEventRecord(e->ev[2 * k], s);

@@ -198,6 +198,7 @@ struct Workspace {
     uint64_t* first_bad;   // [1]: tagged first failing frame of the batch
     uint64_t* arena_first; // [n_arena_tiles]: tagged first data frame of the arena tile
     uint32_t* ctl;         // control words outside the clearable workspace (see kCtl*)
+    void* recs;            // [n_frames] FrameRec: the fused stride path's parsed headers
 };
 
 // ctl words (their own allocation, never cleared with the workspace)
@@ -234,11 +235,25 @@ struct StreamScratch {
     uint32_t* agg;         // [n_streams / 256 + 1] lane walk block counts -> prefixes
 };
 
+// parse_hdr's result for one frame, 16 bytes (stride batches: written by the payload pass,
+// read by k_plan and k_fixup instead of the headers).  flags bit 7 (kRecHasLen): the header
+// parsed to a wire length (then payload_off / wire_len follow from header_size and the mask).
+struct alignas(16) FrameRec {
+    uint64_t payload_len;
+    uint32_t masking_key;
+    uint8_t opcode, flags, header_size;
+    int8_t status;  // before the state machine
+};
+static_assert(sizeof(FrameRec) == 16, "one 16-byte load per record");
+constexpr uint8_t kRecHasLen = 0x80;
+
 struct BatchArgs {
     uint8_t* wire;
     uint64_t wire_len;
     const uint64_t* frame_off;
     uint64_t frame_stride;
+    double stride_inv;        // 1 / frame_stride (stride batches: frame index by multiply)
+    FrameRec* recs;           // stride batches decoded by the fused path (else null)
     uint32_t n;
     int32_t max_frame_size;
     int32_t max_message_size;
@@ -454,6 +469,49 @@ __device__ inline ScanElem parse_one(const BatchArgs& a, uint32_t i, const SegIn
     return parse_hdr(a, i, g, o, load_header(a, o), d);
 }
 
+__device__ inline FrameRec rec_of(const uvhttp_ws_frame_desc_t& d) {
+    FrameRec r;
+    r.payload_len = d.payload_len;
+    r.masking_key = d.masking_key;
+    r.opcode = d.opcode;
+    r.flags = (uint8_t)(d.flags | (d.wire_len ? kRecHasLen : 0));  // wire_len >= 2 iff parsed
+    r.header_size = d.header_size;
+    r.status = d.status;
+    return r;
+}
+
+// the descriptor parse_hdr wrote for the frame at o, rebuilt from its record
+__device__ inline void desc_of_rec(const FrameRec& r, uint64_t o, uvhttp_ws_frame_desc_t& d) {
+    const bool has_len = r.flags & kRecHasLen;
+    const uint64_t m = (r.flags & UVHTTP_WS_FLAG_MASK) ? 4u : 0u;
+    d.payload_len = r.payload_len;
+    d.masking_key = r.masking_key;
+    d.message = 0;
+    d.opcode = r.opcode;
+    d.flags = (uint8_t)(r.flags & ~kRecHasLen);
+    d.header_size = r.header_size;
+    d.status = r.status;
+    d.payload_off = has_len ? o + r.header_size + m : o;
+    const uint64_t wlen = has_len ? r.header_size + m + r.payload_len : 0;
+    d.wire_len = wlen > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)wlen;
+}
+
+// the frame's scan element from its parsed descriptor (what parse_hdr returns)
+__device__ inline ScanElem elem_of_parsed(const uvhttp_ws_frame_desc_t& d, uint32_t i, bool head) {
+    ScanElem e = scan_identity();
+    if (d.status == UVHTTP_WS_FRAME_OK) e = scan_elem_of(d, (int32_t)i, head);
+    else if (head) e.bits = kHead;
+    return e;
+}
+
+// x / frame_stride for a stride batch (x < 2^53): a double multiply, then one correction
+__device__ inline uint64_t div_stride(const BatchArgs& a, uint64_t x) {
+    uint64_t q = (uint64_t)((double)x * a.stride_inv);
+    if (q * a.frame_stride > x) --q;
+    else if ((q + 1) * a.frame_stride <= x) ++q;
+    return q;
+}
+
 // resolve_one: frame i's state-machine step.  With E = scan over the frames of the same
 // connection before i, the state before frame i follows from the latest data frame p alone
 // (all frames before a delivered frame are valid): PENDING iff p exists, p has FIN=0, and p
@@ -468,8 +526,9 @@ __device__ inline void resolve_one(const BatchArgs& a, uvhttp_ws_message_desc_t*
 
     // in-place tiles whose start byte lies in this frame's span up to the next frame (frame
     // 0 also owns the bytes before its start); the max-of-tag claim keeps the smallest frame
-    // when a bad offset table makes slots overlap
-    {
+    // when a bad offset table makes slots overlap.  (The fused stride path's payload pass
+    // finds frames by arithmetic: no tile map.)
+    if (!a.recs) {
         const uint64_t o = frame_start(a, i);
         uint64_t end = (i + 1 < n) ? frame_start(a, i + 1) : a.wire_len;
         if (end > a.wire_len) end = a.wire_len;
@@ -712,7 +771,12 @@ __global__ __launch_bounds__(kBlock) void k_plan(BatchArgs a, uvhttp_ws_frame_de
         ScanElem elem = scan_identity();
         if (i0 < n) {
             g = seg_info(a, i0, n);
-            elem = parse_one(a, i0, g, d);
+            if (a.recs) {  // fused stride path: the payload pass parsed the header already
+                desc_of_rec(a.recs[i0], frame_start(a, i0), d);
+                elem = elem_of_parsed(d, i0, g.head);
+            } else {
+                elem = parse_one(a, i0, g, d);
+            }
         }
         ScanElem agg;
         const ScanElem local = block_exclusive_scan(elem, &agg);
@@ -727,7 +791,21 @@ __global__ __launch_bounds__(kBlock) void k_plan(BatchArgs a, uvhttp_ws_frame_de
     // registers (descriptors are stored once, after the state machine)
     ScanElem tagg = scan_identity();
     uvhttp_ws_frame_desc_t dv[FPT];
-    {
+    if (a.recs) {
+        // fused stride path: the lane's FPT records are one contiguous 16 * FPT-byte run
+        FrameRec r[FPT];
+        const uint32_t ilast = n ? n - 1 : 0;
+#pragma unroll
+        for (int k = 0; k < FPT; ++k) r[k] = a.recs[i0 + k < n ? i0 + k : ilast];
+#pragma unroll
+        for (int k = 0; k < FPT; ++k) {
+            const uint32_t i = i0 + k;
+            if (i < n) {
+                desc_of_rec(r[k], (uint64_t)i * a.frame_stride, dv[k]);
+                tagg = scan_combine(tagg, elem_of_parsed(dv[k], i, i == 0));
+            }
+        }
+    } else {
         // every load unconditional (indices clamped to the last frame, header windows to the
         // last 16 wire bytes) so all of them are in flight together: under per-frame branches
         // the compiler waited for each load before issuing the next (32 round trips per lane)
@@ -1051,6 +1129,205 @@ __global__ __launch_bounds__(BLOCK) void k_unmask_inplace(
         resolve_epoch(a, ws);
         finalize_frames(a, const_cast<uvhttp_ws_frame_desc_t*>(desc), ws,
                         (uint32_t)(tile_base + blockIdx.x), BLOCK, nb);
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// Stride batches (frame i at i * stride, stride >= kFusedMinStride), in place: the fused
+// path.  k_plan's header gather reads one scattered 16-byte window per frame; from cold HBM
+// that costs as much as streaming the whole wire (tools/hdr_probe.hip: 1 048 576 headers of
+// 264-byte frames 52-60 us, the 277 MB wire read linearly 43 us).  The payload pass reads
+// every byte anyway, so here it parses the headers itself:
+//   k_unmask_stride  each workgroup stages its tile in LDS, parses the frames whose header
+//                    starts in it (parse_hdr: every pre-state-machine check), writes their
+//                    16-byte records, and unmasks every locally valid frame (speculatively:
+//                    the state machine has not run yet);
+//   k_plan (recs)    the scan + state machine from the records (contiguous, just written);
+//   k_fixup          statuses after the first failure, the summary, and — only when a frame
+//                    failed — the re-mask of the frames from the first failure on, which
+//                    restores their bytes (XOR is its own inverse): the batch contract's
+//                    "failing frame and everything after it are left untouched".
+// ------------------------------------------------------------------------------------
+constexpr uint64_t kFusedMinStride = 64;
+
+template <int BLOCK, int VPT>
+__global__ __launch_bounds__(BLOCK) void k_unmask_stride(BatchArgs a, uint64_t tile_base) {
+    constexpr uint64_t kT = (uint64_t)BLOCK * VPT * 16;
+    constexpr int kMaxF = (int)(kT / kFusedMinStride) + 2;  // frames touching one tile
+    __shared__ u32x4 s_tile[BLOCK * VPT + 1];               // the tile + the 16 bytes after
+    __shared__ uint64_t s_ps[kMaxF];
+    __shared__ uint64_t s_pe[kMaxF];
+    __shared__ uint32_t s_key[kMaxF];
+    __shared__ u32x4 s_h0;                                  // header of the frame covering t0
+
+    const uint64_t t0 = (tile_base + blockIdx.x) * kT;
+    const uint64_t vend = a.wire_len;
+    const uint64_t full_end = vend & ~(uint64_t)15;
+    const uint64_t clamp_va = full_end ? full_end - 16 : 0;
+    const uint64_t S = a.frame_stride;
+    const uint32_t n = a.n;
+
+    u32x4 data[VPT];
+    uint64_t va[VPT];
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {
+        va[v] = t0 + ((uint64_t)v * BLOCK + threadIdx.x) * 16u;
+        const uint64_t la = va[v] < full_end ? va[v] : clamp_va;
+        data[v] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.wire + la));
+    }
+    // frames of this tile: fbase covers t0 (or is the last frame), fb starts last in it
+    const uint64_t q0 = div_stride(a, t0);
+    const uint32_t fbase = (uint32_t)(q0 < n ? q0 : n - 1);
+    const uint64_t qb = div_stride(a, t0 + kT - 1);
+    const uint32_t fb = (uint32_t)(qb < n ? qb : n - 1);
+    const uint64_t obase = (uint64_t)fbase * S;
+    // the two windows outside the tile, issued with the tile's loads: the header of the frame
+    // that started before t0, and the 16 bytes after the tile (a header near the tile's end)
+    u32x4 extra = u32x4{0, 0, 0, 0};
+    if (threadIdx.x == 0 && obase < t0) extra = load16_at(a.wire, vend, obase);
+    if (threadIdx.x == 1) extra = load16_at(a.wire, vend, t0 + kT);
+
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {
+        u32x4 x = data[v];
+        // the vector straddling the end of the wire: its real bytes (zeros past the end)
+        if (va[v] == full_end && full_end < vend) x = load16_at(a.wire, vend, full_end);
+        s_tile[v * BLOCK + threadIdx.x] = x;
+    }
+    if (threadIdx.x == 0) s_h0 = extra;
+    if (threadIdx.x == 1) s_tile[BLOCK * VPT] = extra;
+    __syncthreads();
+
+    // parse: thread j takes frame fbase + j (loops for frames smaller than kT / BLOCK)
+    const uint32_t nf = fb - fbase + 1;
+    for (uint32_t j = threadIdx.x; j < nf; j += BLOCK) {
+        const uint32_t f = fbase + j;
+        const uint64_t o = (uint64_t)f * S;
+        u32x4 hv;
+        if (o < t0) {
+            hv = s_h0;
+        } else {
+            // 16 bytes at tile offset r from the two aligned LDS vectors around it
+            const uint64_t r = o - t0;
+            const u32x4 v0 = s_tile[r >> 4], v1 = s_tile[(r >> 4) + 1];
+            uint64_t x0 = v0.x | ((uint64_t)v0.y << 32), x1 = v0.z | ((uint64_t)v0.w << 32);
+            uint64_t x2 = v1.x | ((uint64_t)v1.y << 32);
+            const uint64_t x3 = v1.z | ((uint64_t)v1.w << 32);
+            const uint32_t dd = (uint32_t)(r & 15);
+            if (dd & 8) {
+                x0 = x1;
+                x1 = x2;
+                x2 = x3;
+            }
+            const uint32_t s = (dd & 7) * 8;
+            const uint64_t r0 = s ? (x0 >> s) | (x1 << (64 - s)) : x0;
+            const uint64_t r1 = s ? (x1 >> s) | (x2 << (64 - s)) : x1;
+            hv = u32x4{(uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)r1, (uint32_t)(r1 >> 32)};
+        }
+        uvhttp_ws_frame_desc_t d;
+        (void)parse_hdr(a, f, seg_info(a, f, n), o, hv, d);
+        if (o >= t0) a.recs[f] = rec_of(d);  // (a frame that started earlier: its own tile)
+        const bool ok = d.status == UVHTTP_WS_FRAME_OK;
+        s_ps[j] = d.payload_off;
+        s_pe[j] = d.payload_off + (ok ? d.payload_len : 0);
+        s_key[j] = d.masking_key;
+    }
+    __syncthreads();
+
+    u32x4 m[VPT];
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {
+        m[v] = u32x4{0, 0, 0, 0};
+        if (va[v] >= vend) continue;
+        // a payload lies inside its frame's slot: only frames lo..hi can touch this vector
+        const uint64_t ql = div_stride(a, va[v]);
+        const uint32_t lo = (uint32_t)(ql < n ? ql : n - 1);
+        const uint64_t qh = div_stride(a, va[v] + 15);
+        const uint32_t hi = (uint32_t)(qh < fb ? qh : fb);
+        for (uint32_t f = lo; f <= hi; ++f) {
+            const uint32_t j = f - fbase;
+            add_mask(m[v], va[v], s_ps[j], s_pe[j], s_key[j]);
+        }
+    }
+    const uint64_t room = vend > t0 ? vend - t0 : 0;
+    const uint32_t nrec = (uint32_t)(room < kT ? room : kT);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.wire + t0, 0, (int)nrec, 0x00020000);
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {
+        if (any_bits(m[v]) && va[v] + 16 <= vend) {
+            const u32x4 x = data[v] ^ m[v];
+            __builtin_amdgcn_raw_buffer_store_b128(
+                __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, x), rs,
+                (uint32_t)(va[v] - t0), 0, 18);
+        }
+    }
+    if (full_end != vend && full_end >= t0 && full_end < t0 + kT) {
+#pragma unroll
+        for (int v = 0; v < VPT; ++v) {
+            if (va[v] == full_end && any_bits(m[v])) {
+                const uint32_t mw[4] = {m[v].x, m[v].y, m[v].z, m[v].w};
+                for (uint64_t bq = 0; full_end + bq < vend; ++bq) {
+                    const uint8_t mb = (uint8_t)(mw[bq >> 2] >> (8 * (bq & 3)));
+                    if (mb) a.wire[full_end + bq] ^= mb;
+                }
+            }
+        }
+    }
+}
+
+// XOR frame payload bytes [ps, pe) with the key again (one wave; 16-byte vectors inside,
+// single bytes at the two ends, so no byte outside the payload is rewritten)
+__device__ inline void remask_range(uint8_t* wire, uint64_t ps, uint64_t pe, uint32_t key) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t a0 = (ps + 15) & ~(uint64_t)15, a1 = pe & ~(uint64_t)15;
+    if (a0 >= a1) {
+        for (uint64_t b = ps + lane; b < pe; b += 64) wire[b] ^= (uint8_t)(key >> (8 * ((b - ps) & 3)));
+        return;
+    }
+    for (uint64_t b = ps + lane; b < a0; b += 64) wire[b] ^= (uint8_t)(key >> (8 * ((b - ps) & 3)));
+    for (uint64_t b = a1 + lane; b < pe; b += 64) wire[b] ^= (uint8_t)(key >> (8 * ((b - ps) & 3)));
+    const uint32_t rk = rotr32(key, 8u * (uint32_t)((a0 - ps) & 3u));
+    for (uint64_t v = a0 + 16ull * lane; v < a1; v += 16ull * 64) {
+        u32x4* p = reinterpret_cast<u32x4*>(wire + v);
+        *p = *p ^ u32x4{rk, rk, rk, rk};
+    }
+}
+
+// After the fused path's k_plan: statuses after the first failure become SKIPPED, block 0
+// writes the summary, and every frame the payload pass unmasked from the first failure on is
+// masked again.  A look-back give-up (device fault) claimed first_bad = 0: all is restored.
+__global__ __launch_bounds__(kBlock) void k_fixup(BatchArgs a, uvhttp_ws_frame_desc_t* desc,
+                                                  Workspace ws) {
+    resolve_epoch(a, ws);
+    const uint32_t n = a.n;
+    const uint32_t nb = first_bad_of(a, ws, n);
+    const bool fault = device_fault(a, ws);
+    const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t nthreads = (uint64_t)gridDim.x * kBlock;
+    if (blockIdx.x == 0 && threadIdx.x < 64) {
+        if (fault) {
+            if (threadIdx.x == 0) {
+                uvhttp_ws_batch_summary_t s;
+                memset(&s, 0, sizeof(s));
+                s.n_frames = n;
+                s.status = -1;
+                s.first_status = UVHTTP_WS_FRAME_ERR_DEVICE;
+                *a.summary = s;
+            }
+        } else {
+            write_summary(a, desc, ws, nb);
+        }
+    }
+    if (nb >= n) return;  // every frame delivered: nothing to undo
+    for (uint64_t i = tid; i < n; i += nthreads)
+        if (i > nb || fault) desc[i].status = UVHTTP_WS_FRAME_SKIPPED;
+    const uint64_t wave = tid >> 6, nwaves = nthreads >> 6;
+    for (uint64_t i = nb + wave; i < n; i += nwaves) {
+        const FrameRec r = a.recs[i];
+        if (r.status != UVHTTP_WS_FRAME_OK || r.payload_len == 0) continue;  // not unmasked
+        uvhttp_ws_frame_desc_t d;
+        desc_of_rec(r, i * a.frame_stride, d);
+        remask_range(a.wire, d.payload_off, d.payload_off + d.payload_len, d.masking_key);
     }
 }
 
@@ -2713,22 +2990,35 @@ __global__ __launch_bounds__(BLOCK) void kb_emit_frames(BuildArgs b) {
     }
 }
 
-// plain unmask of one buffer with one key (uvhttp_ws_apply_mask over device memory)
-__global__ __launch_bounds__(kBlock) void k_apply_mask(uint8_t* data, uint64_t len, uint32_t key,
-                                                       uint64_t head) {
+// plain unmask of one buffer with one key (uvhttp_ws_apply_mask over device memory).  The
+// payload kernel's streaming shape: a 64-lane workgroup per 1 KiB tile of 16-byte vectors,
+// one non-temporal load per lane, one sc1|nt buffer store (DESIGN.md §4 "Why 1 KiB
+// workgroups"); bench.py also times it over the whole wire as the same-run copy ceiling.
+constexpr int kMaskBlock = 64;
+__global__ __launch_bounds__(kMaskBlock) void k_apply_mask(uint8_t* data, uint64_t len, uint32_t key,
+                                                           uint64_t head, uint64_t tile_base) {
     // bytes [0, head) are the unaligned head; vectors start at data + head
-    const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-    if (tid < head && tid < len) data[tid] ^= (uint8_t)(key >> (8 * (tid & 3)));
+    const uint64_t tile = tile_base + blockIdx.x;
     const uint64_t body = len > head ? len - head : 0;
     const uint64_t nvec = body / 16;
-    const uint32_t rk = rotr32(key, 8u * (uint32_t)(head & 3u));
-    const u32x4 km{rk, rk, rk, rk};
-    u32x4* vp = reinterpret_cast<u32x4*>(data + head);
-    for (uint64_t v = tid; v < nvec; v += stride) vp[v] ^= km;
+    const uint64_t v = tile * kMaskBlock + threadIdx.x;
+    if (v < nvec) {
+        const uint32_t rk = rotr32(key, 8u * (uint32_t)(head & 3u));
+        uint8_t* base = data + head + tile * kMaskBlock * 16;
+        const uint64_t room = (nvec - tile * kMaskBlock) * 16;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            base, 0, (int)(room < kMaskBlock * 16 ? room : kMaskBlock * 16), 0x00020000);
+        const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(base) + threadIdx.x) ^
+                        u32x4{rk, rk, rk, rk};
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, x), rs,
+            threadIdx.x * 16u, 0, 18);
+    }
+    if (tile == 0 && threadIdx.x < head && threadIdx.x < len)
+        data[threadIdx.x] ^= (uint8_t)(key >> (8 * (threadIdx.x & 3)));
     const uint64_t tail0 = head + nvec * 16;
-    if (tid < len - tail0 && tail0 < len) {
-        const uint64_t b = tail0 + tid;
+    if (tile == 0 && tail0 < len && threadIdx.x < len - tail0) {
+        const uint64_t b = tail0 + threadIdx.x;
         data[b] ^= (uint8_t)(key >> (8 * (b & 3)));
     }
 }
@@ -2834,6 +3124,7 @@ struct uvhttp_ws_gpu_engine {
     int store_aux;             // payload store cache policy (0 = nt global store, 18 = sc1|nt)
     uint32_t epoch;            // tag of the latest decode call, 1 .. kMaxEpoch
     int plan_fpt;              // k_plan frames per lane, 0 = automatic
+    int fused_off;             // UVHTTP_WS_FUSED=0: stride batches take the k_plan-first path
     uint32_t plan_no_ticket;   // UVHTTP_WS_PLAN_TICKET=0: blockIdx order instead of tickets
     int walk_mode;             // stream frame discovery: 0 automatic, 1 lane, 2 wave
     void* ss_mem;              // stream-decode scratch
@@ -2927,6 +3218,7 @@ int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out) {
         e->epoch = v < kMaxHostEpoch ? (uint32_t)v : 0;
     }
     if (const char* bs = getenv("UVHTTP_WS_BUILD_SMALL")) e->build_small = atoi(bs);
+    if (const char* fu = getenv("UVHTTP_WS_FUSED")) e->fused_off = atoi(fu) == 0;
     e->build_frames_max = 4096;
     if (const char* bf = getenv("UVHTTP_WS_BUILD_FRAMES")) e->build_frames_max = strtoull(bf, nullptr, 10);
     if (const char* cm = getenv("UVHTTP_WS_COMPACT"))
@@ -3011,7 +3303,8 @@ int uvhttp_ws_gpu_engine_reserve(uvhttp_ws_gpu_engine_t* e, uint32_t max_frames,
     size_t off_tiles = align_up(off_cnt + 16, 256);
     size_t off_bad = align_up(off_tiles + tl * sizeof(uint64_t), 256);
     size_t off_arena = align_up(off_bad + 16, 256);
-    size_t bytes = align_up(off_arena + at * sizeof(uint64_t), 256);
+    size_t off_recs = align_up(off_arena + at * sizeof(uint64_t), 256);
+    size_t bytes = align_up(off_recs + (size_t)fr * 16, 256);
     int prev = 0;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(e->device);
@@ -3040,6 +3333,7 @@ int uvhttp_ws_gpu_engine_reserve(uvhttp_ws_gpu_engine_t* e, uint32_t max_frames,
     e->ws.tile_first = (uint64_t*)(b + off_tiles);
     e->ws.first_bad = (uint64_t*)(b + off_bad);
     e->ws.arena_first = (uint64_t*)(b + off_arena);
+    e->ws.recs = b + off_recs;
     e->ws.ctl = e->ctl;
     e->ws_bytes = bytes;
     e->cap_frames = fr;
@@ -3100,7 +3394,12 @@ static int timing_begin(uvhttp_ws_gpu_engine_t* e, hipStream_t s) {
     if (e->ev_used * 2 + 2 > (int)(sizeof(e->ev) / sizeof(e->ev[0]))) harvest(e);
     const int k = e->ev_used;
     while (e->ev_created < 2 * k + 2) {
-        if (hipEventCreate(&e->ev[e->ev_created]) != hipSuccess) return -1;
+        // timing-only events: no system-scope fence (a fenced marker between two kernels
+        // idled the device ~5.8 us per event, profiles/r03p1 kernel trace); the caller's own
+        // synchronisation still orders the results.  UVHTTP_WS_TIMING_FENCE=1: fenced (A/B)
+        static const unsigned flags = getenv("UVHTTP_WS_TIMING_FENCE") && atoi(getenv("UVHTTP_WS_TIMING_FENCE"))
+                                          ? hipEventDefault : hipEventDisableSystemFence;
+        if (hipEventCreateWithFlags(&e->ev[e->ev_created], flags) != hipSuccess) return -1;
         e->ev_created++;
     }
     (void)hipEventRecord(e->ev[2 * k], s);
@@ -3229,6 +3528,42 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
     a.dev_epoch = e->capturing ? 1u : 0u;
     a.epoch = next_epoch(e, s);
 
+    // stride batches in place: the fused path (payload pass parses the headers, k_plan runs
+    // on its records, k_fixup undoes what a failure must leave untouched)
+    const bool fused = !arena && !b->frame_off && !e->fused_off && a.n > 0 &&
+                       b->frame_stride >= kFusedMinStride && b->wire_len > 0 &&
+                       b->wire_len < (1ull << 52) &&
+                       (uint64_t)(a.n - 1) <= (b->wire_len - 1) / b->frame_stride;
+    if (fused) {
+        a.recs = reinterpret_cast<FrameRec*>(e->ws.recs);
+        a.stride_inv = 1.0 / (double)b->frame_stride;
+        int fb = e->tile_block, fv = e->tile_vpt;
+        const uint64_t favg = b->wire_len / a.n;
+        if (!fb) {
+            fb = favg >= 32768 ? 64 : 256;
+            fv = favg >= 32768 ? 1 : favg >= 2048 ? 2 : 4;
+        }
+        const uint64_t ft = (uint64_t)fb * fv * 16;
+        const uint64_t f_tiles = (b->wire_len + ft - 1) / ft;
+        const uint64_t f_max = (1ull << 24);
+        const int ftk = timing_begin(e, s);
+        for (uint64_t tb = 0; tb < f_tiles; tb += f_max) {
+            const uint32_t grid_p = (uint32_t)((f_tiles - tb) < f_max ? (f_tiles - tb) : f_max);
+#define UVWS_FUSED(B, V) \
+    if (fb == B && fv == V) hipLaunchKernelGGL((k_unmask_stride<B, V>), dim3(grid_p), dim3(B), 0, s, a, tb); else
+            UVWS_FUSED(64, 1) UVWS_FUSED(64, 2) UVWS_FUSED(64, 4) UVWS_FUSED(128, 1)
+            UVWS_FUSED(128, 2) UVWS_FUSED(256, 1) UVWS_FUSED(256, 2) UVWS_FUSED(256, 4) {}
+#undef UVWS_FUSED
+        }
+        timing_end(e, ftk, s);
+        launch_plan(e, a, a.n, d_desc, d_msgs, s);
+        const uint32_t fx = (a.n + kBlock - 1) / kBlock;
+        hipLaunchKernelGGL(k_fixup, dim3(fx < 1024 ? fx : 1024), dim3(kBlock), 0, s, a, d_desc, e->ws);
+        hipError_t hf = hipGetLastError();
+        if (prev != e->device) (void)hipSetDevice(prev);
+        if (hf != hipSuccess) return set_err(e, UVHTTP_WS_GPU_ELAUNCH, "launch", hf);
+        return UVHTTP_WS_GPU_OK;
+    }
     launch_plan(e, a, a.n, d_desc, d_msgs, s);
     // payload kernel tile shape: explicit (set_tile) or by average wire bytes per frame
     // (auto shapes from tools/tile_sweep.py on MI355X, profiles/r01_tile_sweep.txt)
@@ -3603,9 +3938,8 @@ int uvhttp_ws_gpu_apply_mask(uvhttp_ws_gpu_engine_t* e, uint8_t* d_data, uint64_
     uint64_t head = (16u - ((uintptr_t)d_data & 15u)) & 15u;
     if (head > len) head = len;
     const uint64_t nvec = (len - head) / 16;
-    uint64_t grid = (nvec + kBlock - 1) / kBlock;
-    if (grid < 1) grid = 1;
-    if (grid > 8192) grid = 8192;
+    uint64_t tiles = (nvec + kMaskBlock - 1) / kMaskBlock;
+    if (tiles < 1) tiles = 1;  // tile 0 also does the head and tail bytes
     int prev = 0;
     (void)hipGetDevice(&prev);
     if (prev != e->device) (void)hipSetDevice(e->device);
@@ -3613,7 +3947,11 @@ int uvhttp_ws_gpu_apply_mask(uvhttp_ws_gpu_engine_t* e, uint8_t* d_data, uint64_
     CallScope scope{e};
     call_begin(e, s);
     const int tk = timing_begin(e, s);
-    hipLaunchKernelGGL(k_apply_mask, dim3((uint32_t)grid), dim3(kBlock), 0, s, d_data, len, k, head);
+    const uint64_t max_tiles = (1ull << 24);
+    for (uint64_t tb = 0; tb < tiles; tb += max_tiles) {
+        const uint32_t grid = (uint32_t)((tiles - tb) < max_tiles ? (tiles - tb) : max_tiles);
+        hipLaunchKernelGGL(k_apply_mask, dim3(grid), dim3(kMaskBlock), 0, s, d_data, len, k, head, tb);
+    }
     timing_end(e, tk, s);
     hipError_t h = hipGetLastError();
     if (prev != e->device) (void)hipSetDevice(prev);
