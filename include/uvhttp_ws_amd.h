@@ -581,6 +581,10 @@ typedef struct {
                                              poll or wait: staging, delivering, waiting */
     double max_blocked_ms;                /* the longest single such call */
     double wait_ms;                       /* of blocked_ms: waiting for a device decode */
+    double copy_ms;                       /* submit_read: copying reads into the pinned arena */
+    double upload_ms;                     /* submit_read: enqueueing early H2D pieces */
+    double stage_ms;                      /* staging a queue (prefixes, tables) + enqueueing */
+    double deliver_ms;                    /* delivering device results (callbacks included) */
 } uvhttp_ws_amd_batcher_stats_t;
 void uvhttp_ws_amd_batcher_config_init(uvhttp_ws_amd_batcher_config_t* cfg);
 /* UVHTTP_WS_GPU_ENODEV if cfg->device >= 0 names no usable MI355X (no silent host mode) */

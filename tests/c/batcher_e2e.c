@@ -116,14 +116,18 @@ int main(int argc, char** argv) {
            "\"ms_per_flush\": %.3f, \"messages_ok\": %d, \"device_flushes\": %llu, "
            "\"device_ms_total\": %.1f, \"async\": %d, \"submit_ms_per_flush\": %.3f, "
            "\"flush_call_ms_per_flush\": %.3f, \"blocked_ms_per_flush\": %.3f, "
-           "\"max_blocked_ms\": %.3f}\n",
+           "\"max_blocked_ms\": %.3f, \"per_flush_ms\": {\"copy\": %.3f, \"upload\": %.3f, "
+           "\"stage\": %.3f, \"wait\": %.3f, \"deliver\": %.3f}}\n",
            device >= 0 ? "device batcher (stage, H2D, decode_reads, D2H, deliver)"
                        : "host decoder (process_data per read, 1 core)",
            payload / el / (1024.0 * 1024 * 1024), conns, frames, size, rd, flushes,
            el * 1e3 / flushes, g_msgs == (uint64_t)conns * frames * flushes,
            (unsigned long long)(st.device_flushes - st0.device_flushes), st.device_ms - st0.device_ms,
            async, t_submit * 1e3 / flushes, t_flush * 1e3 / flushes,
-           (st.blocked_ms - st0.blocked_ms) / flushes, st.max_blocked_ms);
+           (st.blocked_ms - st0.blocked_ms) / flushes, st.max_blocked_ms,
+           (st.copy_ms - st0.copy_ms) / flushes, (st.upload_ms - st0.upload_ms) / flushes,
+           (st.stage_ms - st0.stage_ms) / flushes, (st.wait_ms - st0.wait_ms) / flushes,
+           (st.deliver_ms - st0.deliver_ms) / flushes);
     uvhttp_ws_amd_batcher_free(b);
     for (int c = 0; c < conns; ++c) uvhttp_ws_connection_free(cs[c]);
     free(cs);

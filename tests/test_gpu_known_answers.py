@@ -168,6 +168,7 @@ def test_parse_known_answers_device(torch, eng, known_answers):
         parsed = int(r["status"]) != -1 and int(r["wire_len"]) > 0
         exp = case["expect"]
         assert (0 if parsed else -1) == exp["rc"], case["id"]
+        ran += 1
         if not parsed:
             continue
         hsz = int(r["header_size"])
@@ -178,8 +179,7 @@ def test_parse_known_answers_device(torch, eng, known_answers):
         for k, v in exp.items():
             if k != "rc":
                 assert got[k] == v, (case["id"], k)
-        ran += 1
-    assert ran >= 15
+    assert ran == 16, ran  # every case but the three NULL-argument ones
 
 
 @pytest.mark.parametrize("offset", [0, 1, 7])

@@ -69,7 +69,7 @@ def test_struct_abi():
     assert C.sizeof(U.FrameDesc) == 32 and C.sizeof(U.MessageDesc) == 32
     # batcher structs (include/uvhttp_ws_amd.h, checked against gcc's layout)
     assert C.sizeof(U.BatcherConfig) == 64 and U.BatcherConfig.on_ready.offset == 48
-    assert C.sizeof(U.BatcherStats) == 136 and U.BatcherStats.blocked_ms.offset == 112
+    assert C.sizeof(U.BatcherStats) == 168 and U.BatcherStats.blocked_ms.offset == 112
 
 
 def test_null_and_empty():

@@ -174,7 +174,8 @@ class BatcherStats(C.Structure):
                                           "failures", "capacity_flushes")] + [("device_ms", C.c_double)] + \
         [(k, C.c_uint64) for k in ("async_flushes", "fallback_flushes", "device_errors",
                                    "direct_reads")] + \
-        [("blocked_ms", C.c_double), ("max_blocked_ms", C.c_double), ("wait_ms", C.c_double)]
+        [(k, C.c_double) for k in ("blocked_ms", "max_blocked_ms", "wait_ms", "copy_ms",
+                                   "upload_ms", "stage_ms", "deliver_ms")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

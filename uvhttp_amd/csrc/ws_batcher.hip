@@ -372,6 +372,7 @@ int complete_device(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
     b->st.device_bytes += q.pos;
     b->st.device_frames += frames;
     // deliver, connection by connection (callbacks may forget connections as we go)
+    const auto td = std::chrono::steady_clock::now();
     b->delivering++;
     for (size_t k = 0; k < q.slots.size(); ++k) {
         if (q.slot_k[k] == UINT32_MAX || q.slots[k].dropped) continue;
@@ -386,6 +387,7 @@ int complete_device(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
         }
     }
     b->delivering--;
+    b->st.deliver_ms += ms_since(td);
     b->st.device_ms += ms_since(q.t_submit);
     return 0;
 }
@@ -424,7 +426,9 @@ int start_flush(uvhttp_ws_amd_batcher_t* b, bool wait) {
         (void)hipGetDevice(&prev);
         if (prev != b->cfg.device) (void)hipSetDevice(b->cfg.device);
         q.t_submit = std::chrono::steady_clock::now();
+        const auto tl = std::chrono::steady_clock::now();
         const int lr = launch_device(b, q);
+        b->st.stage_ms += ms_since(tl);
         if (prev != b->cfg.device) (void)hipSetDevice(prev);
         if (lr == 1) {
             b->st.fallback_flushes++;
@@ -598,14 +602,18 @@ uvhttp_error_t uvhttp_ws_amd_batcher_submit_read(uvhttp_ws_amd_batcher_t* b,
     } else {
         off = q->arena_len;
         if (off + len > b->wire_cap) return UVHTTP_ERROR_INVALID_PARAM;  // (cannot happen)
+        const auto tc = std::chrono::steady_clock::now();
         if (len) uvhttp_ws_amd_copy_stream(q->h_arena + off, data, len);
+        b->st.copy_ms += ms_since(tc);
         q->arena_len += len;
         // a queue large enough for the device streams to HBM while it fills
         if (q->bytes + len >= b->cfg.min_device_bytes && q->arena_len - q->uploaded >= kUploadPiece) {
             int prev = 0;
             (void)hipGetDevice(&prev);
             if (prev != b->cfg.device) (void)hipSetDevice(b->cfg.device);
+            const auto tu = std::chrono::steady_clock::now();
             upload_tail(b, *q);
+            b->st.upload_ms += ms_since(tu);
             if (prev != b->cfg.device) (void)hipSetDevice(prev);
         }
     }
