@@ -84,6 +84,7 @@ def max_over_ranks(value, world):
     return float(t.item())
 
 
+TIMING_EVERY = int(os.environ.get("UVHTTP_WS_TIMING_EVERY", "10"))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
 SEED = 0x5EED0001
 GIB = float(1 << 30)
@@ -418,7 +419,10 @@ class GpuWorkload:
         self.torch.cuda.synchronize()
 
     def set_timing(self, on):
-        self.eng.set_timing(on)
+        # events around every TIMING_EVERY-th payload kernel: a timed marker idles the device
+        # ~4.6 us per event (rocprofv3 trace, profiles/r03p4_*), so timing every launch would
+        # inflate the step it measures
+        self.eng.set_timing(on, every=TIMING_EVERY)
 
     def kernel_time(self):
         return self.eng.kernel_time()

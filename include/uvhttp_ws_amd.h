@@ -320,9 +320,11 @@ int uvhttp_ws_gpu_engine_reserve(uvhttp_ws_gpu_engine_t* eng, uint32_t max_frame
  * workgroup tile; (0, 0) = automatic (by average frame size).  Supported: 64x1, 64x2, 64x4,
  * 128x1, 128x2, 256x1, 256x2, 256x4.  A tuning knob only: results are identical. */
 int uvhttp_ws_gpu_engine_set_tile(uvhttp_ws_gpu_engine_t* eng, int block, int vectors_per_lane);
-/* Kernel timing: when enabled, HIP events bracket the dominant (payload) kernel of every
- * decode call on its stream; kernel_time returns the summed milliseconds and the number
- * of bracketed launches completed so far (synchronises on the last event). */
+/* Kernel timing: with enable = k >= 1, HIP events bracket the dominant (payload) kernel of
+ * every k-th call (k = 1: every call) on its stream — each timed marker idles the device a few
+ * microseconds, so sampling keeps that cost off most calls; 0 disables.  kernel_time returns
+ * the summed milliseconds and the number of bracketed launches completed so far
+ * (synchronises on the last event). */
 int uvhttp_ws_gpu_engine_set_timing(uvhttp_ws_gpu_engine_t* eng, int enable);
 int uvhttp_ws_gpu_engine_kernel_time(uvhttp_ws_gpu_engine_t* eng, double* ms,
                                      uint64_t* launches);

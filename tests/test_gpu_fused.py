@@ -45,9 +45,12 @@ def _engine(env=None):
                 os.environ[k] = v
 
 
-@pytest.fixture(scope="module")
-def engines(torch):
-    fused, plain = _engine(), _engine({"UVHTTP_WS_FUSED": "0"})
+@pytest.fixture(scope="module", params=["3pass", "lookback"])
+def engines(torch, request):
+    """the fused path (records scanned by reduce-then-scan, or by k_plan's look-back) and the
+    k_plan-first path; the fused path is forced for every frame size"""
+    fused = _engine({"UVHTTP_WS_REC_SCAN": request.param, "UVHTTP_WS_FUSED_MAX": str(1 << 40)})
+    plain = _engine({"UVHTTP_WS_FUSED": "0"})
     yield fused, plain
     fused.close()
     plain.close()
@@ -158,14 +161,16 @@ def test_layout_and_client_frames(torch, engines):
 
 
 def test_lookback_give_up_restores_everything(torch):
-    """UVHTTP_WS_MAX_POLLS=0: the scan gives up, first_bad = 0, and k_fixup re-masks every
-    frame the payload pass had unmasked: the wire is byte-identical to the input"""
+    """UVHTTP_WS_MAX_POLLS=0 with the look-back scan over the records (UVHTTP_WS_REC_SCAN=
+    lookback; the default reduce-then-scan never waits): the scan gives up, first_bad = 0, and
+    k_fixup re-masks every frame the payload pass had unmasked — the wire is byte-identical to
+    the input"""
     import uvhttp_amd as U
     rng = random.Random(9)
     n, plen = 300000, 250  # k_plan runs many blocks
     wire, _ = _batch(rng, n, plen)
     stride = wire.size // n
-    eng = _engine({"UVHTTP_WS_MAX_POLLS": "0"})
+    eng = _engine({"UVHTTP_WS_MAX_POLLS": "0", "UVHTTP_WS_REC_SCAN": "lookback"})
     try:
         got = _decode(torch, eng, wire, n, stride, wire.size)
         s = got["summary"]

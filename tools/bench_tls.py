@@ -14,7 +14,14 @@ EVP AES-GCM / ChaCha20-Poly1305 from the system libcrypto (AES-NI + PCLMUL / AVX
 production CPU stack does).
 
     python tools/bench_tls.py [--conns N] [--records R] [--plen P] [--version 13|12] [--klen 16|32]
-                              [--cipher aes|chacha]
+                              [--cipher aes|chacha] [--chain]
+
+--chain: the TLS -> WebSocket chain the reference runs per read (src/uvhttp_connection.c:
+1128-1158: mbedtls_ssl_read, then process_data on each decrypted chunk).  Each connection's
+plaintext is one masked BINARY WebSocket frame filling its records (65 528-byte payload at the
+default 4 x 16 KiB), and a step is open_records -> ws_streams (one process_data call per
+record) -> decode_reads: ciphertext in HBM -> unmasked messages in HBM.  The rate is WebSocket
+payload bytes per second.
 """
 import argparse
 import ctypes as C
@@ -99,6 +106,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=4.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--lib", default=None, help="another build of the library (A/B runs)")
+    ap.add_argument("--chain", action="store_true", help="open_records -> ws_streams -> decode_reads")
     args = ap.parse_args()
 
     import torch
@@ -136,6 +144,14 @@ def main():
     dev = "cuda:0"
     t = torch
     src = t.randint(0, 256, (n * per * plen,), dtype=t.uint8, device=dev)
+    weng = None
+    if args.chain:
+        # one masked BINARY frame per connection filling its per * plen plaintext bytes
+        weng = U.GpuEngine(0)
+        conn_bytes = per * plen
+        fp = conn_bytes - 8 if conn_bytes - 8 < 65536 else conn_bytes - 14
+        assert U.gen_frame_stride(fp) == conn_bytes, "pick --records * --plen >= 134"
+        weng.gen_frames(src, n, fp, 11, opcode0=2)
     wire = t.empty(n * per * stride, dtype=t.uint8, device=dev)
     out = t.empty(wire.numel(), dtype=t.uint8, device=dev)
     dk = t.from_numpy(keys.view(np.uint8).reshape(-1).copy()).to(dev)
@@ -146,16 +162,37 @@ def main():
     recs = t.empty(n * per * 32, dtype=t.uint8, device=dev)
     res = t.empty(n * 64, dtype=t.uint8, device=dev)
 
+    if args.chain:
+        ws0 = np.zeros(n, U.STREAM_DT)  # fresh server connections (uvhttp_ws_stream_init)
+        ws0["recv_buffer_size"] = 65536
+        ws0["max_frame_size"], ws0["max_message_size"], ws0["is_server"] = 16 << 20, 64 << 20, 1
+        ws_dev = t.from_numpy(ws0.view(np.uint8).reshape(-1).copy()).to(dev)
+        read_end = t.zeros(n * per, dtype=t.int64, device=dev)
+        wdesc = t.empty(n * 32, dtype=t.uint8, device=dev)
+        wres = t.empty(n * U.STREAM_RESULT_BYTES, dtype=t.uint8, device=dev)
+        weng.reserve(n, out.numel(), 0)
+
     def step():
         eng.open_records(wire, dk, nk, dst, n, n * per, out, records=recs, results=res)
+        if args.chain:
+            eng.ws_streams(res, recs, n, dst, out, ws_dev, read_end)
+            weng.decode_streams(out, ws_dev, n, n, desc=wdesc, results=wres, read_end=read_end,
+                                n_reads=n * per)
 
     for _ in range(args.warmup):
         step()
     t.cuda.synchronize()
     R = res.cpu().numpy().view(O.TLS_RESULT_DT)
     assert (R["n_delivered"] == per).all() and (R["plain_len"] == per * plen).all(), "open failed"
-    got = out.view(-1)[: per * plen]
-    assert t.equal(got, src[: per * plen]), "plaintext mismatch"
+    if args.chain:
+        # every connection: one message of fp bytes, unmasked in place inside `out`
+        wr = weng.read_stream_results(wres, n)
+        assert all(r.status == 0 and r.n_delivered == 1 and r.calls == per for r in wr[:64]), wr[0].as_dict()
+        assert sum(r.n_delivered for r in wr) == n
+        weng.sync()
+    else:
+        got = out.view(-1)[: per * plen]
+        assert t.equal(got, src[: per * plen]), "plaintext mismatch"
     eng.set_timing(True)
     eng.kernel_time()
     t.cuda.synchronize()
@@ -169,8 +206,12 @@ def main():
     plain = n * per * plen
     kus = kms * 1e3 / max(1, launches)
     moved = n * per * (stride + plen)  # ciphertext records read + plaintext written
+    if args.chain:
+        plain = n * fp  # WebSocket payload delivered per step
     line = {
-        "metric": "TLS record open GiB/s (device-resident)", "value": round(plain * args.steps / el / GIB, 2),
+        "metric": ("TLS -> WebSocket chain GiB/s (ciphertext in HBM -> unmasked messages)"
+                   if args.chain else "TLS record open GiB/s (device-resident)"),
+        "value": round(plain * args.steps / el / GIB, 2),
         "unit": "GiB/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(el / args.steps * 1e3, 4), "higher_is_better": True,
         "dtype": "u8/u32 (ChaCha20-Poly1305)" if chacha else "u8/u32 (AES-GCM)", "data": "synthetic (random plaintext sealed on the device)",
@@ -183,7 +224,10 @@ def main():
     }
     if args.lib:
         line["lib"] = os.path.basename(args.lib)
-    if not args.no_cpu_baseline:
+    if args.chain:
+        line["config"]["chain"] = ("open_records -> ws_streams (one process_data call per record) "
+                                   f"-> decode_reads; one {fp}-byte masked BINARY frame per connection")
+    if not args.no_cpu_baseline and not args.chain:
         m = per  # connection 0's records (one key, sequence numbers 0 .. per-1)
         sample = wire[: m * stride].cpu().numpy()
         ob = np.zeros(m * stride, np.uint8)

@@ -423,8 +423,9 @@ class GpuEngine:
         self._check(self._L.uvhttp_ws_gpu_engine_set_tile(self.h, block, vectors_per_lane),
                     "set_tile")
 
-    def set_timing(self, on: bool):
-        self._check(self._L.uvhttp_ws_gpu_engine_set_timing(self.h, 1 if on else 0), "timing")
+    def set_timing(self, on, every=1):
+        """HIP events around the payload kernel of every `every`-th call while on"""
+        self._check(self._L.uvhttp_ws_gpu_engine_set_timing(self.h, every if on else 0), "timing")
 
     def kernel_time(self):
         ms, n = C.c_double(0), C.c_uint64(0)

@@ -150,11 +150,12 @@ __device__ inline ScanElem wave_reduce_newest_first(ScanElem v) {
     return v;
 }
 
-// Block-wide exclusive scan (256 threads = 4 waves): wave-level Hillis-Steele over the 64
-// lanes with __shfl_up, then the 4 wave totals through LDS.  Returns the exclusive prefix
+// Block-wide exclusive scan (NT threads = NT / 64 waves): wave-level Hillis-Steele over the
+// 64 lanes with __shfl_up, then the wave totals through LDS.  Returns the exclusive prefix
 // for this thread; *total receives the block aggregate.
+template <int NT = kBlock>
 __device__ ScanElem block_exclusive_scan(ScanElem v, ScanElem* total) {
-    __shared__ ScanElem wave_tot[kBlock / 64];
+    __shared__ ScanElem wave_tot[NT / 64];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     ScanElem inc = v;
@@ -168,7 +169,7 @@ __device__ ScanElem block_exclusive_scan(ScanElem v, ScanElem* total) {
     ScanElem wave_pre = scan_identity();
     ScanElem all = scan_identity();
 #pragma unroll
-    for (int w = 0; w < kBlock / 64; ++w) {
+    for (int w = 0; w < NT / 64; ++w) {
         if (w < wave) wave_pre = scan_combine(wave_pre, wave_tot[w]);
         all = scan_combine(all, wave_tot[w]);
     }
@@ -741,6 +742,48 @@ __device__ ScanElem lookback_prefix(const Workspace& ws, uint32_t b, const ScanE
     return s_pre;
 }
 
+// fused stride path: the lane's FPT records (one contiguous 16 * FPT-byte run) -> the
+// frames' descriptors in registers and the lane's scan aggregate
+template <int FPT>
+__device__ inline ScanElem rec_pass1(const BatchArgs& a, uint32_t i0, uint32_t n,
+                                     uvhttp_ws_frame_desc_t (&dv)[FPT]) {
+    ScanElem tagg = scan_identity();
+    FrameRec r[FPT];
+    const uint32_t ilast = n ? n - 1 : 0;
+#pragma unroll
+    for (int k = 0; k < FPT; ++k) r[k] = a.recs[i0 + k < n ? i0 + k : ilast];
+#pragma unroll
+    for (int k = 0; k < FPT; ++k) {
+        const uint32_t i = i0 + k;
+        if (i < n) {
+            desc_of_rec(r[k], (uint64_t)i * a.frame_stride, dv[k]);
+            tagg = scan_combine(tagg, elem_of_parsed(dv[k], i, i == 0));
+        }
+    }
+    return tagg;
+}
+
+// pass 2: the state machine in frame order from the lane's exclusive prefix `run`; each
+// descriptor is stored once
+template <int FPT>
+__device__ inline void plan_pass2(const BatchArgs& a, uvhttp_ws_frame_desc_t* desc,
+                                  uvhttp_ws_message_desc_t* msgs, const Workspace& ws, uint32_t i0,
+                                  uint32_t n, ScanElem run, uvhttp_ws_frame_desc_t (&dv)[FPT]) {
+#pragma unroll
+    for (int k = 0; k < FPT; ++k) {
+        const uint32_t i = i0 + k;
+        if (i < n) {
+            const SegInfo g = seg_info(a, i, n);
+            ScanElem e = scan_identity();
+            if (dv[k].status == UVHTTP_WS_FRAME_OK) e = scan_elem_of(dv[k], (int32_t)i, g.head);
+            else if (g.head) e.bits = kHead;
+            resolve_one(a, msgs, ws, i, n, g, run, dv[k]);
+            desc[i] = dv[k];
+            run = scan_combine(run, e);
+        }
+    }
+}
+
 // k_plan: one launch per decode: parse -> block scan -> look-back -> state machine.  Each
 // lane owns FPT consecutive frames (FPT > 1 keeps the block count, and with it the look-back
 // chain, short for large batches): pass 1 parses them and reduces their scan elements,
@@ -792,19 +835,7 @@ __global__ __launch_bounds__(kBlock) void k_plan(BatchArgs a, uvhttp_ws_frame_de
     ScanElem tagg = scan_identity();
     uvhttp_ws_frame_desc_t dv[FPT];
     if (a.recs) {
-        // fused stride path: the lane's FPT records are one contiguous 16 * FPT-byte run
-        FrameRec r[FPT];
-        const uint32_t ilast = n ? n - 1 : 0;
-#pragma unroll
-        for (int k = 0; k < FPT; ++k) r[k] = a.recs[i0 + k < n ? i0 + k : ilast];
-#pragma unroll
-        for (int k = 0; k < FPT; ++k) {
-            const uint32_t i = i0 + k;
-            if (i < n) {
-                desc_of_rec(r[k], (uint64_t)i * a.frame_stride, dv[k]);
-                tagg = scan_combine(tagg, elem_of_parsed(dv[k], i, i == 0));
-            }
-        }
+        tagg = rec_pass1<FPT>(a, i0, n, dv);
     } else {
         // every load unconditional (indices clamped to the last frame, header windows to the
         // last 16 wire bytes) so all of them are in flight together: under per-frame branches
@@ -831,20 +862,55 @@ __global__ __launch_bounds__(kBlock) void k_plan(BatchArgs a, uvhttp_ws_frame_de
     ScanElem agg;
     const ScanElem local = block_exclusive_scan(tagg, &agg);
     ScanElem run = scan_combine(lookback_prefix(ws, b, agg, a.epoch, a.max_polls), local);
-    // pass 2: the state machine in frame order
-#pragma unroll
-    for (int k = 0; k < FPT; ++k) {
-        const uint32_t i = i0 + k;
-        if (i < n) {
-            const SegInfo g = seg_info(a, i, n);
-            ScanElem e = scan_identity();
-            if (dv[k].status == UVHTTP_WS_FRAME_OK) e = scan_elem_of(dv[k], (int32_t)i, g.head);
-            else if (g.head) e.bits = kHead;
-            resolve_one(a, msgs, ws, i, n, g, run, dv[k]);
-            desc[i] = dv[k];
-            run = scan_combine(run, e);
-        }
+    plan_pass2<FPT>(a, desc, msgs, ws, i0, n, run, dv);
+}
+
+// ------------------------------------------------------------------------------------
+// Reduce-then-scan over the fused path's records (no tickets, no look-back waits): the
+// records are 16 contiguous bytes per frame, so reading them twice is cheaper than making
+// 256 blocks wait on each other (tools/ab_lib.py).
+//   k_rec_reduce   block b: the scan aggregate of its kBlock * FPT frames -> block_agg[b]
+//   k_rec_scan     one 1024-thread block: exclusive / inclusive prefixes of the aggregates
+//   k_rec_resolve  block b: its frames' descriptors, the block scan from block_excl[b], the
+//                  state machine and the descriptor stores (k_plan's pass 2)
+// ------------------------------------------------------------------------------------
+template <int FPT>
+__global__ __launch_bounds__(kBlock) void k_rec_reduce(BatchArgs a, Workspace ws) {
+    const uint32_t n = a.n;
+    const uint32_t i0 = (blockIdx.x * kBlock + threadIdx.x) * FPT;
+    uvhttp_ws_frame_desc_t dv[FPT];
+    const ScanElem tagg = rec_pass1<FPT>(a, i0, n, dv);
+    ScanElem agg;
+    (void)block_exclusive_scan(tagg, &agg);
+    if (threadIdx.x == 0) ws.block_agg[blockIdx.x] = agg;
+}
+
+constexpr int kScanBlock = 1024;
+__global__ __launch_bounds__(kScanBlock) void k_rec_scan(Workspace ws, uint32_t nblocks) {
+    const uint32_t per = (nblocks + kScanBlock - 1) / kScanBlock;
+    const uint32_t j0 = threadIdx.x * per;
+    ScanElem mine = scan_identity();
+    for (uint32_t j = j0; j < j0 + per && j < nblocks; ++j) mine = scan_combine(mine, ws.block_agg[j]);
+    ScanElem tot;
+    ScanElem run = block_exclusive_scan<kScanBlock>(mine, &tot);
+    for (uint32_t j = j0; j < j0 + per && j < nblocks; ++j) {
+        ws.block_excl[j] = run;
+        run = scan_combine(run, ws.block_agg[j]);
+        ws.block_incl[j] = run;
     }
+}
+
+template <int FPT>
+__global__ __launch_bounds__(kBlock) void k_rec_resolve(BatchArgs a, uvhttp_ws_frame_desc_t* desc,
+                                                        uvhttp_ws_message_desc_t* msgs, Workspace ws) {
+    resolve_epoch(a, ws);
+    const uint32_t n = a.n;
+    const uint32_t i0 = (blockIdx.x * kBlock + threadIdx.x) * FPT;
+    uvhttp_ws_frame_desc_t dv[FPT];
+    const ScanElem tagg = rec_pass1<FPT>(a, i0, n, dv);
+    ScanElem agg;
+    const ScanElem local = block_exclusive_scan(tagg, &agg);
+    plan_pass2<FPT>(a, desc, msgs, ws, i0, n, scan_combine(ws.block_excl[blockIdx.x], local), dv);
 }
 
 // summary of a batch decode, after k_plan (one wave of k_finalize): E(nb) is
@@ -1149,6 +1215,10 @@ __global__ __launch_bounds__(BLOCK) void k_unmask_inplace(
 //                    "failing frame and everything after it are left untouched".
 // ------------------------------------------------------------------------------------
 constexpr uint64_t kFusedMinStride = 64;
+// above this many wire bytes per frame the headers are few and the k_plan-first path is
+// faster (its payload pass overlaps the descriptor lookup with the loads; tools/fused_sweep.py,
+// profiles/r03p5_fused_sweep.txt: fused wins by 6 us at 2 KiB frames, loses by 7 at 4 KiB)
+constexpr uint64_t kFusedMaxAvg = 3072;
 
 template <int BLOCK, int VPT>
 __global__ __launch_bounds__(BLOCK) void k_unmask_stride(BatchArgs a, uint64_t tile_base) {
@@ -1198,9 +1268,13 @@ __global__ __launch_bounds__(BLOCK) void k_unmask_stride(BatchArgs a, uint64_t t
     if (threadIdx.x == 1) s_tile[BLOCK * VPT] = extra;
     __syncthreads();
 
-    // parse: thread j takes frame fbase + j (loops for frames smaller than kT / BLOCK)
+    // parse: frame fbase + j on thread (j % W) * 64 + j / W of the W waves, so every wave
+    // takes a share (a tile of 256-byte frames has ~62: one wave alone left three idle at the
+    // barrier); loops for frames smaller than kT / BLOCK
     const uint32_t nf = fb - fbase + 1;
-    for (uint32_t j = threadIdx.x; j < nf; j += BLOCK) {
+    constexpr uint32_t W = BLOCK / 64;
+    const uint32_t jt = (threadIdx.x & 63) * W + (threadIdx.x >> 6);
+    for (uint32_t j = jt; j < nf; j += BLOCK) {
         const uint32_t f = fbase + j;
         const uint64_t o = (uint64_t)f * S;
         u32x4 hv;
@@ -3119,12 +3193,15 @@ struct uvhttp_ws_gpu_engine {
     uint32_t cap_frames;
     uint64_t cap_tiles, cap_arena_tiles;
     Workspace ws;
-    int timing;
+    int timing;                // 0: off; k >= 1: HIP events around every k-th call's payload kernel
+    uint64_t timing_calls;     // calls seen while timing (the sampling counter)
     int tile_block, tile_vpt;  // payload kernel shape, 0 = automatic
     int store_aux;             // payload store cache policy (0 = nt global store, 18 = sc1|nt)
     uint32_t epoch;            // tag of the latest decode call, 1 .. kMaxEpoch
     int plan_fpt;              // k_plan frames per lane, 0 = automatic
     int fused_off;             // UVHTTP_WS_FUSED=0: stride batches take the k_plan-first path
+    uint64_t fused_max_avg;    // fused only up to this many wire bytes per frame (UVHTTP_WS_FUSED_MAX)
+    int rec_lookback;          // fused path: records scanned by k_plan (1) or reduce-then-scan (0)
     uint32_t plan_no_ticket;   // UVHTTP_WS_PLAN_TICKET=0: blockIdx order instead of tickets
     int walk_mode;             // stream frame discovery: 0 automatic, 1 lane, 2 wave
     void* ss_mem;              // stream-decode scratch
@@ -3219,6 +3296,12 @@ int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out) {
     }
     if (const char* bs = getenv("UVHTTP_WS_BUILD_SMALL")) e->build_small = atoi(bs);
     if (const char* fu = getenv("UVHTTP_WS_FUSED")) e->fused_off = atoi(fu) == 0;
+    e->fused_max_avg = kFusedMaxAvg;
+    if (const char* fm = getenv("UVHTTP_WS_FUSED_MAX")) e->fused_max_avg = strtoull(fm, nullptr, 10);
+    // the fused path scans its records with k_plan's look-back by default (C4: 133-136 us per
+    // step against 144-145 for reduce-then-scan, profiles/r03p6_*); UVHTTP_WS_REC_SCAN=3pass
+    e->rec_lookback = 1;
+    if (const char* rs = getenv("UVHTTP_WS_REC_SCAN")) e->rec_lookback = strcmp(rs, "3pass") != 0;
     e->build_frames_max = 4096;
     if (const char* bf = getenv("UVHTTP_WS_BUILD_FRAMES")) e->build_frames_max = strtoull(bf, nullptr, 10);
     if (const char* cm = getenv("UVHTTP_WS_COMPACT"))
@@ -3358,7 +3441,8 @@ int uvhttp_ws_gpu_engine_set_tile(uvhttp_ws_gpu_engine_t* e, int block, int vect
 
 int uvhttp_ws_gpu_engine_set_timing(uvhttp_ws_gpu_engine_t* e, int enable) {
     if (!e) return UVHTTP_WS_GPU_EINVAL;
-    e->timing = enable ? 1 : 0;
+    e->timing = enable > 0 ? enable : 0;
+    e->timing_calls = 0;
     return UVHTTP_WS_GPU_OK;
 }
 
@@ -3391,6 +3475,9 @@ int uvhttp_ws_gpu_engine_kernel_time(uvhttp_ws_gpu_engine_t* e, double* ms, uint
 
 static int timing_begin(uvhttp_ws_gpu_engine_t* e, hipStream_t s) {
     if (!e->timing || e->capturing) return -1;
+    // a timed marker between two kernels idles the device for a few us (the CP drains the
+    // first kernel and writes the timestamp): sampled timing keeps that off most calls
+    if (e->timing_calls++ % (uint64_t)e->timing != 0) return -1;
     if (e->ev_used * 2 + 2 > (int)(sizeof(e->ev) / sizeof(e->ev[0]))) harvest(e);
     const int k = e->ev_used;
     while (e->ev_created < 2 * k + 2) {
@@ -3462,8 +3549,11 @@ static void launch_plan(uvhttp_ws_gpu_engine_t* e, BatchArgs& a, uint32_t n_cap,
                         hipStream_t s) {
     int fpt = e->plan_fpt;
     if (fpt != 1 && fpt != 2 && fpt != 4 && fpt != 8 && fpt != 16) {
+        // records (fused stride path): contiguous 16-byte loads, no header gather to hide, so
+        // fewer blocks (C4 fused: 512 blocks 143.8 us per step, 256 blocks 136.4, r03p4)
+        const uint64_t max_blocks = a.recs ? 256 : 512;
         fpt = 1;
-        while (fpt < 16 && ((uint64_t)n_cap + kBlock * fpt - 1) / (kBlock * fpt) > 512) fpt *= 2;
+        while (fpt < 16 && ((uint64_t)n_cap + kBlock * fpt - 1) / (kBlock * fpt) > max_blocks) fpt *= 2;
     }
     const uint32_t per = kBlock * fpt;
     a.plan_frames = per;
@@ -3531,6 +3621,7 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
     // stride batches in place: the fused path (payload pass parses the headers, k_plan runs
     // on its records, k_fixup undoes what a failure must leave untouched)
     const bool fused = !arena && !b->frame_off && !e->fused_off && a.n > 0 &&
+                       b->wire_len / a.n <= e->fused_max_avg &&
                        b->frame_stride >= kFusedMinStride && b->wire_len > 0 &&
                        b->wire_len < (1ull << 52) &&
                        (uint64_t)(a.n - 1) <= (b->wire_len - 1) / b->frame_stride;
@@ -3556,7 +3647,17 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
 #undef UVWS_FUSED
         }
         timing_end(e, ftk, s);
-        launch_plan(e, a, a.n, d_desc, d_msgs, s);
+        if (e->rec_lookback) {
+            launch_plan(e, a, a.n, d_desc, d_msgs, s);
+        } else {
+            constexpr int kRecFpt = 4;
+            a.plan_frames = kBlock * kRecFpt;
+            const uint32_t nblk = (a.n + a.plan_frames - 1) / a.plan_frames;
+            hipLaunchKernelGGL(k_rec_reduce<kRecFpt>, dim3(nblk), dim3(kBlock), 0, s, a, e->ws);
+            hipLaunchKernelGGL(k_rec_scan, dim3(1), dim3(kScanBlock), 0, s, e->ws, nblk);
+            hipLaunchKernelGGL(k_rec_resolve<kRecFpt>, dim3(nblk), dim3(kBlock), 0, s, a, d_desc,
+                               d_msgs, e->ws);
+        }
         const uint32_t fx = (a.n + kBlock - 1) / kBlock;
         hipLaunchKernelGGL(k_fixup, dim3(fx < 1024 ? fx : 1024), dim3(kBlock), 0, s, a, d_desc, e->ws);
         hipError_t hf = hipGetLastError();
