@@ -556,6 +556,17 @@ typedef void (*uvhttp_ws_amd_failure_cb)(void* ctx, struct uvhttp_ws_connection*
 /* an asynchronous flush's results are in host memory (called from a HIP runtime thread:
  * only signal the loop, e.g. uv_async_send; then call poll() on the loop thread) */
 typedef void (*uvhttp_ws_amd_ready_cb)(void* ctx);
+/* A TLS connection's record stream reached something that is not authenticated application
+ * data the device may open: an alert or handshake record (first_status
+ * UVHTTP_TLS_REC_CONTROL: close_notify, KeyUpdate, NewSessionTicket ...).  The records before it
+ * were decrypted and decoded; `ciphertext` (len bytes, valid during the call) is everything
+ * from that record on, including reads queued since, and next_seq is the read sequence number
+ * of its first record.  The batcher forgets the connection's TLS state: the caller hands the
+ * bytes to mbedtls (mbedtls_ssl_read, as src/uvhttp_connection.c:1128-1144 does) and may
+ * register the connection again with uvhttp_ws_amd_batcher_set_tls (e.g. after a KeyUpdate). */
+typedef void (*uvhttp_ws_amd_tls_handback_cb)(void* ctx, struct uvhttp_ws_connection* conn,
+                                              const uint8_t* ciphertext, size_t len,
+                                              uint64_t next_seq, int first_status);
 typedef struct {
     int device;                /* HIP device for large flushes; -1 = host decoder only */
     uint64_t min_device_bytes; /* flushes with fewer queued bytes run on the host */
@@ -567,6 +578,7 @@ typedef struct {
     void* ctx;
     uvhttp_ws_amd_ready_cb on_ready; /* optional */
     void* ready_ctx;
+    uvhttp_ws_amd_tls_handback_cb on_tls_handback; /* TLS connections (called with ctx) */
 } uvhttp_ws_amd_batcher_config_t;
 typedef struct {
     uint64_t flushes, device_flushes, host_flushes;
@@ -587,6 +599,9 @@ typedef struct {
     double upload_ms;                     /* submit_read: enqueueing early H2D pieces */
     double stage_ms;                      /* staging a queue (prefixes, tables) + enqueueing */
     double deliver_ms;                    /* delivering device results (callbacks included) */
+    uint64_t tls_records;                 /* TLS records opened and delivered on the device */
+    uint64_t tls_bytes;                   /* their ciphertext bytes */
+    uint64_t tls_handbacks;               /* connections handed back (on_tls_handback) */
 } uvhttp_ws_amd_batcher_stats_t;
 void uvhttp_ws_amd_batcher_config_init(uvhttp_ws_amd_batcher_config_t* cfg);
 /* UVHTTP_WS_GPU_ENODEV if cfg->device >= 0 names no usable MI355X (no silent host mode) */
@@ -618,9 +633,31 @@ int uvhttp_ws_amd_batcher_in_flight(const uvhttp_ws_amd_batcher_t* b);
 /* Decode everything queued — the queue in flight, then the one being filled — and deliver it
  * before returning (callbacks fire here); returns as flush_async. */
 int uvhttp_ws_amd_batcher_flush(uvhttp_ws_amd_batcher_t* b);
-/* Drop a connection's queued reads (in both queues) and failure mark (call before freeing
- * the connection; safe from inside callbacks of a flush). */
+/* Drop a connection's queued reads (in both queues), failure mark and TLS state (call before
+ * freeing the connection; safe from inside callbacks of a flush). */
 void uvhttp_ws_amd_batcher_forget(uvhttp_ws_amd_batcher_t* b, struct uvhttp_ws_connection* conn);
+
+/* TLS connections (the on_websocket_read TLS branch, src/uvhttp_connection.c:1122-1159:
+ * mbedtls_ssl_read until WANT_READ, process_data on every decrypted chunk).  set_tls registers
+ * the connection's read key (include/uvhttp_tls_amd.h: AES-128/256-GCM or ChaCha20-Poly1305,
+ * TLS 1.3 or 1.2, from mbedtls's key export) and the sequence number of its next record;
+ * submit_tls_read then queues ciphertext as libuv delivers it.  A flush opens the records of
+ * every TLS connection on the device (uvhttp_tls_gpu_open_records), hands each delivered
+ * record's content to the WebSocket decoder as one process_data call
+ * (uvhttp_tls_gpu_ws_streams -> uvhttp_ws_gpu_decode_reads) and delivers as for plain
+ * connections; an incomplete trailing record is kept for the next flush.  A record that is
+ * not application data ends the batcher's TLS handling of the connection
+ * (on_tls_handback); a record that fails (bad MAC, overflow, bad type or version) reports the
+ * connection through on_failure with UVHTTP_ERROR_INVALID_PARAM, as the reference closes it
+ * (:1139-1144).  TLS queues always decode on the device (the host decoder has no AEAD):
+ * set_tls returns UVHTTP_WS_GPU_ENODEV for a host-only batcher.  A connection is either
+ * plain or TLS: submit_read on a TLS connection (and submit_tls_read on a plain one) is
+ * UVHTTP_ERROR_INVALID_PARAM. */
+int uvhttp_ws_amd_batcher_set_tls(uvhttp_ws_amd_batcher_t* b, struct uvhttp_ws_connection* conn,
+                                  const void* tls_key /* uvhttp_tls_key_t */, uint64_t read_seq);
+uvhttp_error_t uvhttp_ws_amd_batcher_submit_tls_read(uvhttp_ws_amd_batcher_t* b,
+                                                     struct uvhttp_ws_connection* conn,
+                                                     const uint8_t* ciphertext, size_t len);
 int uvhttp_ws_amd_batcher_stats(const uvhttp_ws_amd_batcher_t* b,
                                 uvhttp_ws_amd_batcher_stats_t* out);
 

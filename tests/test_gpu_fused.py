@@ -45,11 +45,13 @@ def _engine(env=None):
                 os.environ[k] = v
 
 
-@pytest.fixture(scope="module", params=["3pass", "lookback"])
+@pytest.fixture(scope="module", params=["3pass", "lookback", "lookback256"])
 def engines(torch, request):
-    """the fused path (records scanned by reduce-then-scan, or by k_plan's look-back) and the
-    k_plan-first path; the fused path is forced for every frame size"""
-    fused = _engine({"UVHTTP_WS_REC_SCAN": request.param, "UVHTTP_WS_FUSED_MAX": str(1 << 40)})
+    """the fused path (records scanned by reduce-then-scan, or by k_plan's look-back in
+    1024- or 256-thread blocks) and the k_plan-first path; the fused path is forced for every
+    frame size"""
+    fused = _engine({"UVHTTP_WS_REC_SCAN": request.param[:8], "UVHTTP_WS_FUSED_MAX": str(1 << 40),
+                     "UVHTTP_WS_PLAN_WIDE": "0" if request.param.endswith("256") else "1"})
     plain = _engine({"UVHTTP_WS_FUSED": "0"})
     yield fused, plain
     fused.close()

@@ -118,6 +118,8 @@ ON_ERROR = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_char_p)
 CONTEXT_RESOLVER = C.CFUNCTYPE(C.c_void_p, C.c_void_p)
 FAILURE_CB = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p, C.c_int)
 READY_CB = C.CFUNCTYPE(None, C.c_void_p)
+TLS_HANDBACK_CB = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p, C.POINTER(C.c_uint8), C.c_size_t,
+                              C.c_uint64, C.c_int)
 CONTROL_SINK = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_uint8),
                            C.c_size_t)
 
@@ -164,7 +166,8 @@ class BatcherConfig(C.Structure):
     _fields_ = [("device", C.c_int), ("min_device_bytes", C.c_uint64), ("max_bytes", C.c_uint64),
                 ("max_connections", C.c_uint32), ("max_reads", C.c_uint32),
                 ("on_failure", FAILURE_CB), ("ctx", C.c_void_p),
-                ("on_ready", READY_CB), ("ready_ctx", C.c_void_p)]
+                ("on_ready", READY_CB), ("ready_ctx", C.c_void_p),
+                ("on_tls_handback", TLS_HANDBACK_CB)]
 
 
 class BatcherStats(C.Structure):
@@ -175,7 +178,8 @@ class BatcherStats(C.Structure):
         [(k, C.c_uint64) for k in ("async_flushes", "fallback_flushes", "device_errors",
                                    "direct_reads")] + \
         [(k, C.c_double) for k in ("blocked_ms", "max_blocked_ms", "wait_ms", "copy_ms",
-                                   "upload_ms", "stage_ms", "deliver_ms")]
+                                   "upload_ms", "stage_ms", "deliver_ms")] + \
+        [(k, C.c_uint64) for k in ("tls_records", "tls_bytes", "tls_handbacks")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -258,6 +262,10 @@ def load_library(path: str) -> C.CDLL:
         "uvhttp_ws_amd_batcher_flush_async": (C.c_int, [vp]),
         "uvhttp_ws_amd_batcher_poll": (C.c_int, [vp]),
         "uvhttp_ws_amd_batcher_in_flight": (C.c_int, [vp]),
+        "uvhttp_ws_amd_batcher_set_tls": (C.c_int, [vp, C.POINTER(WsConnectionStruct), vp,
+                                                   C.c_uint64]),
+        "uvhttp_ws_amd_batcher_submit_tls_read": (C.c_int, [vp, C.POINTER(WsConnectionStruct),
+                                                           vp, C.c_size_t]),
         "uvhttp_ws_amd_batcher_forget": (None, [vp, C.POINTER(WsConnectionStruct)]),
         "uvhttp_ws_amd_batcher_stats": (C.c_int, [vp, C.POINTER(BatcherStats)]),
         # TLS record layer (include/uvhttp_tls_amd.h)
@@ -733,8 +741,11 @@ class Batcher:
         cfg.device, cfg.min_device_bytes, cfg.max_bytes = device, min_device_bytes, max_bytes
         cfg.max_connections, cfg.max_reads = max_connections, max_reads
         self.failures = {}
+        self.handbacks = {}  # conn ptr -> (ciphertext bytes, next_seq, first_status)
         self._cb = FAILURE_CB(self._on_failure)
         cfg.on_failure = self._cb
+        self._hb = TLS_HANDBACK_CB(self._on_handback)
+        cfg.on_tls_handback = self._hb
         h = C.c_void_p()
         rc = L.uvhttp_ws_amd_batcher_create(C.byref(cfg), C.byref(h))
         if rc != 0:
@@ -743,6 +754,18 @@ class Batcher:
 
     def _on_failure(self, ctx, conn, rc):
         self.failures[conn] = rc
+
+    def _on_handback(self, ctx, conn, data, n, next_seq, status):
+        self.handbacks[conn] = (C.string_at(data, n) if n else b"", next_seq, status)
+
+    def set_tls(self, conn: "WsConnection", key_bytes: bytes, read_seq: int) -> int:
+        """key_bytes: one uvhttp_tls_key_t (64 bytes)"""
+        kb = (C.c_uint8 * 64).from_buffer_copy(bytes(key_bytes))
+        return self._L.uvhttp_ws_amd_batcher_set_tls(self.h, conn.ptr, kb, read_seq)
+
+    def submit_tls(self, conn: "WsConnection", data: bytes) -> int:
+        buf = (C.c_uint8 * max(1, len(data))).from_buffer_copy(bytes(data) or b"\0")
+        return self._L.uvhttp_ws_amd_batcher_submit_tls_read(self.h, conn.ptr, buf, len(data))
 
     def submit(self, conn: "WsConnection", data: bytes) -> int:
         buf = (C.c_uint8 * max(1, len(data))).from_buffer_copy(bytes(data) or b"\0")

@@ -655,9 +655,10 @@ __device__ inline ScanElem rec_value(const u32x4v x[4]) {
 }
 
 // exclusive prefix of block b (all threads call; the value is broadcast through LDS)
+template <int NT = kBlock>
 __device__ ScanElem lookback_prefix(const Workspace& ws, uint32_t b, const ScanElem& agg,
                                     uint32_t epoch, uint32_t max_polls) {
-    __shared__ ScanElem s_wave[kBlock / 64];
+    __shared__ ScanElem s_wave[NT / 64];
     __shared__ ScanElem s_pre;
     __shared__ int s_kstar;
     __shared__ int s_go;
@@ -678,7 +679,7 @@ __device__ ScanElem lookback_prefix(const Workspace& ws, uint32_t b, const ScanE
     }
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     ScanElem run = scan_identity();  // thread 0: combination of the predecessors seen so far
-    int64_t end = b;                 // window: blocks [end - 256, end)
+    int64_t end = b;                 // window: blocks [end - NT, end)
     uint32_t polls = 0;              // uniform: every thread counts the same rounds
     bool gave_up = false;
     for (;;) {
@@ -705,7 +706,7 @@ __device__ ScanElem lookback_prefix(const Workspace& ws, uint32_t b, const ScanE
             __builtin_amdgcn_s_sleep(8);
         }
         // nearest published prefix (smallest t with P)
-        if (t == 0) s_kstar = kBlock;
+        if (t == 0) s_kstar = NT;
         __syncthreads();
         const uint64_t pm = __ballot(is_p);
         if (lane == 0 && pm) atomicMin(&s_kstar, wave * 64 + __builtin_ctzll(pm));
@@ -718,13 +719,13 @@ __device__ ScanElem lookback_prefix(const Workspace& ws, uint32_t b, const ScanE
         if (t == 0) {
             ScanElem w = scan_identity();
 #pragma unroll
-            for (int k = kBlock / 64 - 1; k >= 0; --k) w = scan_combine(w, s_wave[k]);
+            for (int k = NT / 64 - 1; k >= 0; --k) w = scan_combine(w, s_wave[k]);
             run = scan_combine(w, run);
-            s_go = (kstar < kBlock || gave_up) ? 0 : 1;
+            s_go = (kstar < NT || gave_up) ? 0 : 1;
         }
         __syncthreads();
         if (!s_go) break;
-        end -= kBlock;
+        end -= NT;
     }
     if (t == 0) {
         s_pre = run;
@@ -790,8 +791,8 @@ __device__ inline void plan_pass2(const BatchArgs& a, uvhttp_ws_frame_desc_t* de
 // pass 2 (after the block's prefix is known) re-reads their descriptors and runs the state
 // machine in frame order.  The block holding the last ticket resets the counter for the
 // next call.
-template <int FPT>
-__global__ __launch_bounds__(kBlock) void k_plan(BatchArgs a, uvhttp_ws_frame_desc_t* desc,
+template <int FPT, int NT = kBlock>
+__global__ __launch_bounds__(NT) void k_plan(BatchArgs a, uvhttp_ws_frame_desc_t* desc,
                                                  uvhttp_ws_message_desc_t* msgs, Workspace ws) {
     resolve_epoch(a, ws);
     __shared__ uint32_t s_ticket;
@@ -807,7 +808,7 @@ __global__ __launch_bounds__(kBlock) void k_plan(BatchArgs a, uvhttp_ws_frame_de
     __syncthreads();
     const uint32_t b = s_ticket;
     const uint32_t n = nframes(a);
-    const uint32_t i0 = (b * kBlock + threadIdx.x) * FPT;
+    const uint32_t i0 = (b * NT + threadIdx.x) * FPT;
     if (FPT == 1) {
         SegInfo g;
         uvhttp_ws_frame_desc_t d;
@@ -822,8 +823,8 @@ __global__ __launch_bounds__(kBlock) void k_plan(BatchArgs a, uvhttp_ws_frame_de
             }
         }
         ScanElem agg;
-        const ScanElem local = block_exclusive_scan(elem, &agg);
-        const ScanElem pre = lookback_prefix(ws, b, agg, a.epoch, a.max_polls);
+        const ScanElem local = block_exclusive_scan<NT>(elem, &agg);
+        const ScanElem pre = lookback_prefix<NT>(ws, b, agg, a.epoch, a.max_polls);
         if (i0 < n) {
             resolve_one(a, msgs, ws, i0, n, g, scan_combine(pre, local), d);
             desc[i0] = d;
@@ -860,8 +861,8 @@ __global__ __launch_bounds__(kBlock) void k_plan(BatchArgs a, uvhttp_ws_frame_de
         }
     }
     ScanElem agg;
-    const ScanElem local = block_exclusive_scan(tagg, &agg);
-    ScanElem run = scan_combine(lookback_prefix(ws, b, agg, a.epoch, a.max_polls), local);
+    const ScanElem local = block_exclusive_scan<NT>(tagg, &agg);
+    ScanElem run = scan_combine(lookback_prefix<NT>(ws, b, agg, a.epoch, a.max_polls), local);
     plan_pass2<FPT>(a, desc, msgs, ws, i0, n, run, dv);
 }
 
@@ -1217,8 +1218,8 @@ __global__ __launch_bounds__(BLOCK) void k_unmask_inplace(
 constexpr uint64_t kFusedMinStride = 64;
 // above this many wire bytes per frame the headers are few and the k_plan-first path is
 // faster (its payload pass overlaps the descriptor lookup with the loads; tools/fused_sweep.py,
-// profiles/r03p5_fused_sweep.txt: fused wins by 6 us at 2 KiB frames, loses by 7 at 4 KiB)
-constexpr uint64_t kFusedMaxAvg = 3072;
+// profiles/r03p8_fused_sweep.txt: fused wins by 7 us at 2 KiB frames, loses by 4 at 3 KiB)
+constexpr uint64_t kFusedMaxAvg = 2560;
 
 template <int BLOCK, int VPT>
 __global__ __launch_bounds__(BLOCK) void k_unmask_stride(BatchArgs a, uint64_t tile_base) {
@@ -1268,13 +1269,11 @@ __global__ __launch_bounds__(BLOCK) void k_unmask_stride(BatchArgs a, uint64_t t
     if (threadIdx.x == 1) s_tile[BLOCK * VPT] = extra;
     __syncthreads();
 
-    // parse: frame fbase + j on thread (j % W) * 64 + j / W of the W waves, so every wave
-    // takes a share (a tile of 256-byte frames has ~62: one wave alone left three idle at the
-    // barrier); loops for frames smaller than kT / BLOCK
+    // parse: thread j takes frame fbase + j (loops for frames smaller than kT / BLOCK);
+    // consecutive lanes on consecutive frames keep the LDS header reads and the record stores
+    // dense (spreading the frames over all four waves measured 5 us slower on C4, r03p7)
     const uint32_t nf = fb - fbase + 1;
-    constexpr uint32_t W = BLOCK / 64;
-    const uint32_t jt = (threadIdx.x & 63) * W + (threadIdx.x >> 6);
-    for (uint32_t j = jt; j < nf; j += BLOCK) {
+    for (uint32_t j = threadIdx.x; j < nf; j += BLOCK) {
         const uint32_t f = fbase + j;
         const uint64_t o = (uint64_t)f * S;
         u32x4 hv;
@@ -3202,6 +3201,7 @@ struct uvhttp_ws_gpu_engine {
     int fused_off;             // UVHTTP_WS_FUSED=0: stride batches take the k_plan-first path
     uint64_t fused_max_avg;    // fused only up to this many wire bytes per frame (UVHTTP_WS_FUSED_MAX)
     int rec_lookback;          // fused path: records scanned by k_plan (1) or reduce-then-scan (0)
+    int plan_wide;             // records: k_plan with 1024-thread blocks (UVHTTP_WS_PLAN_WIDE=1; A/B)
     uint32_t plan_no_ticket;   // UVHTTP_WS_PLAN_TICKET=0: blockIdx order instead of tickets
     int walk_mode;             // stream frame discovery: 0 automatic, 1 lane, 2 wave
     void* ss_mem;              // stream-decode scratch
@@ -3301,6 +3301,8 @@ int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out) {
     // the fused path scans its records with k_plan's look-back by default (C4: 133-136 us per
     // step against 144-145 for reduce-then-scan, profiles/r03p6_*); UVHTTP_WS_REC_SCAN=3pass
     e->rec_lookback = 1;
+    e->plan_wide = 0;  // 1024-thread blocks measured slower on C4 (1690 vs 1785 GiB/s, r03p7)
+    if (const char* pw = getenv("UVHTTP_WS_PLAN_WIDE")) e->plan_wide = atoi(pw) != 0;
     if (const char* rs = getenv("UVHTTP_WS_REC_SCAN")) e->rec_lookback = strcmp(rs, "3pass") != 0;
     e->build_frames_max = 4096;
     if (const char* bf = getenv("UVHTTP_WS_BUILD_FRAMES")) e->build_frames_max = strtoull(bf, nullptr, 10);
@@ -3555,9 +3557,22 @@ static void launch_plan(uvhttp_ws_gpu_engine_t* e, BatchArgs& a, uint32_t n_cap,
         fpt = 1;
         while (fpt < 16 && ((uint64_t)n_cap + kBlock * fpt - 1) / (kBlock * fpt) > max_blocks) fpt *= 2;
     }
+    a.no_ticket = e->plan_no_ticket;
+    if (a.recs && e->plan_wide) {
+        // records: 1024-thread blocks, so the per-lane state-machine chain is 4x shorter at
+        // the same block count (occupancy 4 waves / SIMD instead of 1)
+        int wf = 1;
+        while (wf < 4 && ((uint64_t)n_cap + 1024 * wf - 1) / (1024 * wf) > 256) wf *= 2;
+        const uint32_t wper = 1024 * wf;
+        a.plan_frames = wper;
+        const uint32_t wgrid = n_cap ? (n_cap + wper - 1) / wper : 1;
+        if (wf == 1) hipLaunchKernelGGL((k_plan<1, 1024>), dim3(wgrid), dim3(1024), 0, s, a, d_desc, d_msgs, e->ws);
+        else if (wf == 2) hipLaunchKernelGGL((k_plan<2, 1024>), dim3(wgrid), dim3(1024), 0, s, a, d_desc, d_msgs, e->ws);
+        else hipLaunchKernelGGL((k_plan<4, 1024>), dim3(wgrid), dim3(1024), 0, s, a, d_desc, d_msgs, e->ws);
+        return;
+    }
     const uint32_t per = kBlock * fpt;
     a.plan_frames = per;
-    a.no_ticket = e->plan_no_ticket;
     const uint32_t grid = n_cap ? (n_cap + per - 1) / per : 1;
     switch (fpt) {
         case 1: hipLaunchKernelGGL(k_plan<1>, dim3(grid), dim3(kBlock), 0, s, a, d_desc, d_msgs, e->ws); break;
