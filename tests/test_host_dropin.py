@@ -68,8 +68,9 @@ def test_struct_abi():
     assert U.UvhttpConfig.websocket_max_frame_size.offset == 64
     assert C.sizeof(U.FrameDesc) == 32 and C.sizeof(U.MessageDesc) == 32
     # batcher structs (include/uvhttp_ws_amd.h, checked against gcc's layout)
-    assert C.sizeof(U.BatcherConfig) == 64 and U.BatcherConfig.on_ready.offset == 48
-    assert C.sizeof(U.BatcherStats) == 168 and U.BatcherStats.blocked_ms.offset == 112
+    assert C.sizeof(U.BatcherConfig) == 72 and U.BatcherConfig.on_ready.offset == 48
+    assert U.BatcherConfig.on_tls_handback.offset == 64
+    assert C.sizeof(U.BatcherStats) == 192 and U.BatcherStats.blocked_ms.offset == 112
 
 
 def test_null_and_empty():

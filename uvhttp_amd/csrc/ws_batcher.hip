@@ -31,15 +31,26 @@
 #include <unordered_set>
 #include <vector>
 
+#include "uvhttp_tls_amd.h"
 #include "uvhttp_ws_amd.h"
 
 extern "C" void uvhttp_ws_amd_copy_stream(void* dst, const void* src, size_t len);  // ws_host.c
+
+// TLS connections (uvhttp_ws_amd_batcher_set_tls): a queue's TLS connections are laid out
+// after the plain ones in the device wire as ciphertext (the previous flushes' unconsumed
+// bytes, then the new reads); the flush opens their records (uvhttp_tls_gpu_open_records),
+// turns every delivered record into one process_data call (uvhttp_tls_gpu_ws_streams: the
+// chunks mbedtls_ssl_read returns, src/uvhttp_connection.c:1128-1158) and decodes the
+// plaintext with decode_reads, next to the plain connections' decode.
 
 namespace {
 
 constexpr uint32_t kMaxFramesPerFlush = 1u << 26;  // decode_reads' frame limit (ws_gpu.hip)
 constexpr uint64_t kUploadPiece = 8ull << 20;        // arena bytes per early H2D
 constexpr uint32_t kMinFrames = 65536;              // initial descriptor capacity per queue
+// room a TLS connection's carry may need when the queue is staged: at most one incomplete
+// record (5-byte header + 2^14 content + 256 bytes of AEAD expansion, RFC 8446 §5.2)
+constexpr uint64_t kTlsCarryMax = 5 + 16384 + 256 + 16;
 
 struct QueuedRead {
     uint64_t off;  // in the queue's arena
@@ -51,6 +62,16 @@ struct ConnSlot {
     std::vector<uint32_t> reads;  // indices into Queue::reads, arrival order
     uint64_t bytes;               // queued read bytes
     bool dropped;                 // forgotten, or failed in an earlier queue
+    bool tls;                     // ciphertext reads of a TLS connection
+};
+
+// a TLS connection's read side: its key, the sequence number of its next record and the
+// ciphertext a flush did not consume (an incomplete record: it waits for more bytes, as in
+// mbedtls's input buffer)
+struct TlsConn {
+    uvhttp_tls_key_t key;
+    uint64_t seq;
+    std::vector<uint8_t> carry;
 };
 
 inline uint64_t align16(uint64_t x) { return (x + 15) & ~(uint64_t)15; }
@@ -94,12 +115,31 @@ struct BatchQueue {
     GatherSeg *h_seg = nullptr, *d_seg = nullptr;
     uint32_t max_frames = 0;
     hipEvent_t up_ev = nullptr, done_ev = nullptr;
+    // TLS connections (allocated with the first set_tls)
+    bool tls_ready = false;
+    uint32_t n_tls_slots = 0;       // TLS slots queued
+    uint8_t *d_plain = nullptr, *h_plain = nullptr;  // opened plaintext (wire_cap bytes)
+    uvhttp_tls_key_t *h_keys = nullptr, *d_keys = nullptr;
+    uvhttp_tls_stream_t *h_tst = nullptr, *d_tst = nullptr;
+    uvhttp_tls_result_t *h_tres = nullptr, *d_tres = nullptr;
+    uvhttp_tls_record_t* d_trecs = nullptr;
+    uint64_t* d_wread_end = nullptr;
+    uint32_t trec_cap = 0;
+    uvhttp_ws_stream_t *h_wst = nullptr, *d_wst = nullptr;
+    uvhttp_ws_stream_result_t *h_wres = nullptr, *d_wres = nullptr;
+    uvhttp_ws_frame_desc_t *h_wdesc = nullptr, *d_wdesc = nullptr;
+    uint32_t wdesc_cap = 0;
+    uint64_t *h_poff = nullptr, *d_poff = nullptr;
     // the flush in flight
     bool in_flight = false;
     int launch_rc = 0;
-    uint32_t nk = 0;               // connections staged
+    uint32_t nk = 0;               // plain connections staged
     uint64_t pos = 0;              // wire bytes staged
+    uint32_t nt = 0;               // TLS connections staged
+    uint64_t tls_base = 0, tls_bytes = 0, plain_cap = 0;
     std::vector<uint32_t> slot_k;  // slot -> stream index (UINT32_MAX: not staged)
+    std::vector<uint64_t> carry_off;  // TLS slot -> its staged carry in h_arena (offset, len)
+    std::vector<uint64_t> carry_len;
     std::chrono::steady_clock::time_point t_submit;
 };
 
@@ -117,6 +157,8 @@ struct uvhttp_ws_amd_batcher {
     uint64_t wire_cap = 0;
     uint32_t fail_every = 0;  // test hook (UVHTTP_WS_BATCHER_FAIL_EVERY=k): every k-th device
     uint32_t launches = 0;    // launch reports ELAUNCH before enqueueing anything
+    uvhttp_tls_gpu_engine_t* teng = nullptr;  // record open (first set_tls)
+    std::unordered_map<uvhttp_ws_connection_t*, TlsConn> tls;
     uvhttp_ws_amd_batcher_stats_t st;
 };
 
@@ -143,6 +185,82 @@ void free_queue(BatchQueue& q) {
     (void)hipFree(q.d_seg);
     if (q.up_ev) (void)hipEventDestroy(q.up_ev);
     if (q.done_ev) (void)hipEventDestroy(q.done_ev);
+    (void)hipHostFree(q.h_plain);
+    (void)hipHostFree(q.h_keys);
+    (void)hipHostFree(q.h_tst);
+    (void)hipHostFree(q.h_tres);
+    (void)hipHostFree(q.h_wst);
+    (void)hipHostFree(q.h_wres);
+    (void)hipHostFree(q.h_wdesc);
+    (void)hipHostFree(q.h_poff);
+    (void)hipFree(q.d_plain);
+    (void)hipFree(q.d_keys);
+    (void)hipFree(q.d_tst);
+    (void)hipFree(q.d_tres);
+    (void)hipFree(q.d_trecs);
+    (void)hipFree(q.d_wread_end);
+    (void)hipFree(q.d_wst);
+    (void)hipFree(q.d_wres);
+    (void)hipFree(q.d_wdesc);
+    (void)hipFree(q.d_poff);
+}
+
+// the TLS side of a queue: per-connection tables (max_connections), the plaintext buffer;
+// records and their descriptors grow per flush (grow_tls)
+bool alloc_tls(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
+    if (q.tls_ready) return true;
+    const size_t ns = b->cfg.max_connections;
+    q.tls_ready =
+        hipHostMalloc((void**)&q.h_plain, b->wire_cap, hipHostMallocDefault) == hipSuccess &&
+        hipHostMalloc((void**)&q.h_keys, ns * sizeof(uvhttp_tls_key_t), hipHostMallocDefault) == hipSuccess &&
+        hipHostMalloc((void**)&q.h_tst, ns * sizeof(uvhttp_tls_stream_t), hipHostMallocDefault) == hipSuccess &&
+        hipHostMalloc((void**)&q.h_tres, ns * sizeof(uvhttp_tls_result_t), hipHostMallocDefault) == hipSuccess &&
+        hipHostMalloc((void**)&q.h_wst, ns * sizeof(uvhttp_ws_stream_t), hipHostMallocDefault) == hipSuccess &&
+        hipHostMalloc((void**)&q.h_wres, ns * sizeof(uvhttp_ws_stream_result_t), hipHostMallocDefault) == hipSuccess &&
+        hipHostMalloc((void**)&q.h_poff, ns * sizeof(uint64_t), hipHostMallocDefault) == hipSuccess &&
+        hipMalloc((void**)&q.d_plain, b->wire_cap) == hipSuccess &&
+        hipMalloc((void**)&q.d_keys, ns * sizeof(uvhttp_tls_key_t)) == hipSuccess &&
+        hipMalloc((void**)&q.d_tst, ns * sizeof(uvhttp_tls_stream_t)) == hipSuccess &&
+        hipMalloc((void**)&q.d_tres, ns * sizeof(uvhttp_tls_result_t)) == hipSuccess &&
+        hipMalloc((void**)&q.d_wst, ns * sizeof(uvhttp_ws_stream_t)) == hipSuccess &&
+        hipMalloc((void**)&q.d_wres, ns * sizeof(uvhttp_ws_stream_result_t)) == hipSuccess &&
+        hipMalloc((void**)&q.d_poff, ns * sizeof(uint64_t)) == hipSuccess;
+    return q.tls_ready;
+}
+
+// records (and the read table, one entry per record) for nr records, plaintext frame
+// descriptors for nf frames
+int grow_tls(uvhttp_ws_amd_batcher_t* b, BatchQueue& q, uint64_t nr, uint64_t nf) {
+    if (nr > q.trec_cap) {
+        uint64_t want = 2ull * q.trec_cap > nr ? 2ull * q.trec_cap : nr;
+        if (want > (1u << 28)) want = 1u << 28;
+        if (want < nr) return UVHTTP_WS_GPU_ENOMEM;
+        (void)hipFree(q.d_trecs);
+        (void)hipFree(q.d_wread_end);
+        q.d_trecs = nullptr;
+        q.d_wread_end = nullptr;
+        q.trec_cap = 0;
+        if (hipMalloc((void**)&q.d_trecs, want * sizeof(uvhttp_tls_record_t)) != hipSuccess ||
+            hipMalloc((void**)&q.d_wread_end, want * sizeof(uint64_t)) != hipSuccess)
+            return UVHTTP_WS_GPU_ENOMEM;
+        q.trec_cap = (uint32_t)want;
+    }
+    if (nf > q.wdesc_cap) {
+        uint64_t want = 2ull * q.wdesc_cap > nf ? 2ull * q.wdesc_cap : nf;
+        if (want > kMaxFramesPerFlush) want = kMaxFramesPerFlush;
+        if (want < nf) return UVHTTP_WS_GPU_ENOMEM;
+        (void)hipHostFree(q.h_wdesc);
+        (void)hipFree(q.d_wdesc);
+        q.h_wdesc = nullptr;
+        q.d_wdesc = nullptr;
+        q.wdesc_cap = 0;
+        if (hipHostMalloc((void**)&q.h_wdesc, want * sizeof(uvhttp_ws_frame_desc_t), hipHostMallocDefault) != hipSuccess ||
+            hipMalloc((void**)&q.d_wdesc, want * sizeof(uvhttp_ws_frame_desc_t)) != hipSuccess ||
+            uvhttp_ws_gpu_engine_reserve(b->eng, (uint32_t)want, b->wire_cap, 0) != 0)
+            return UVHTTP_WS_GPU_ENOMEM;
+        q.wdesc_cap = (uint32_t)want;
+    }
+    return 0;
 }
 
 bool alloc_queue(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
@@ -178,6 +296,7 @@ void release(uvhttp_ws_amd_batcher_t* b) {
         if (b->up) (void)hipStreamDestroy(b->up);
         if (b->cs) (void)hipStreamDestroy(b->cs);
         uvhttp_ws_gpu_engine_free(b->eng);
+        if (b->teng) uvhttp_tls_gpu_engine_free(b->teng);
         (void)hipSetDevice(prev);
     }
     delete b;
@@ -194,7 +313,12 @@ void clear_queue(BatchQueue& q) {
     q.launch_rc = 0;
     q.nk = 0;
     q.pos = 0;
+    q.nt = 0;
+    q.n_tls_slots = 0;
+    q.tls_bytes = q.plain_cap = 0;
     q.slot_k.clear();
+    q.carry_off.clear();
+    q.carry_len.clear();
 }
 
 // device batcher: the arena bytes not yet sent go to HBM on the upload stream
@@ -219,6 +343,7 @@ void flush_host(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
     b->st.host_flushes++;
     b->delivering++;
     for (size_t k = 0; k < q.slots.size(); ++k) {
+        if (q.slots[k].tls) continue;  // ciphertext: only the device opens records
         for (size_t j = 0; j < q.slots[k].reads.size(); ++j) {
             if (q.slots[k].dropped || b->failed.count(q.slots[k].conn)) break;
             const QueuedRead r = q.reads[q.slots[k].reads[j]];
@@ -256,24 +381,35 @@ int grow_desc(uvhttp_ws_amd_batcher_t* b, BatchQueue& q, uint64_t nf) {
 }
 
 // Stage q's connections (recv-buffer prefixes from their current state, read tables) and
-// enqueue H2D -> gather -> decode_reads -> D2H.  Returns 0 when launched, 1 when the queue
+// enqueue H2D -> gather -> decode_reads -> D2H (and, for TLS connections, open_records ->
+// ws_streams -> decode_reads on the plaintext).  Returns 0 when launched, 1 when the queue
 // must be decoded on the host instead (it does not fit the device layout), < 0 on an error.
 int launch_device(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
     uint64_t pos = 0;
-    uint32_t nr = 0, nk = 0, nseg = 0;
+    uint32_t nr = 0, nk = 0, nt = 0, nseg = 0;
     q.slot_k.assign(q.slots.size(), UINT32_MAX);
-    // room check first: prefixes go after the reads in the arena, and the device layout
-    // (16-byte aligned connections) must fit the device wire
-    uint64_t prefix = 0, layout = 0;
+    q.carry_off.assign(q.slots.size(), 0);
+    q.carry_len.assign(q.slots.size(), 0);
+    auto live = [&](const ConnSlot& s) {
+        return !s.dropped && !b->failed.count(s.conn) && (!s.tls || b->tls.count(s.conn));
+    };
+    // room check first: prefixes (and TLS carries) go after the reads in the arena, and the
+    // device layout (16-byte aligned connections) must fit the device wire; a TLS
+    // connection's plaintext reservation (prefix + at most its ciphertext) must fit d_plain
+    uint64_t extra = 0, layout = 0, plain_need = 0;
     for (const ConnSlot& s : q.slots) {
-        if (s.dropped || b->failed.count(s.conn)) continue;
-        prefix += s.conn->recv_buffer_pos;
-        layout = align16(layout) + s.conn->recv_buffer_pos + s.bytes;
+        if (!live(s)) continue;
+        const uint64_t carry = s.tls ? b->tls[s.conn].carry.size() : 0;
+        extra += s.conn->recv_buffer_pos + carry;
+        layout = align16(layout) + (s.tls ? carry : s.conn->recv_buffer_pos) + s.bytes + 16;
+        if (s.tls) plain_need = align16(plain_need) + s.conn->recv_buffer_pos + carry + s.bytes + 16;
     }
-    if (q.arena_len + prefix > b->wire_cap || layout > b->wire_cap) return 1;
+    if (q.arena_len + extra > b->wire_cap || layout > b->wire_cap || plain_need > b->wire_cap)
+        return 1;
+    // plain connections first
     for (size_t k = 0; k < q.slots.size(); ++k) {
         ConnSlot& s = q.slots[k];
-        if (s.dropped || b->failed.count(s.conn)) continue;
+        if (s.tls || !live(s)) continue;
         uvhttp_ws_connection_t* c = s.conn;
         pos = align16(pos);
         const uint64_t begin = pos;
@@ -298,12 +434,65 @@ int launch_device(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
     }
     q.nk = nk;
     q.pos = pos;
-    if (!nk) return 1;  // nothing left to decode (all dropped): the host path is a no-op
+    // TLS connections: ciphertext (carry, then reads) after the plain layout; their
+    // recv-buffer prefixes stay in the arena, where ws_streams copies them from
+    const uint64_t tls_base = align16(pos);
+    uint64_t tpos = tls_base, plain_cap = 0;
+    for (size_t k = 0; k < q.slots.size(); ++k) {
+        ConnSlot& s = q.slots[k];
+        if (!s.tls || !live(s)) continue;
+        uvhttp_ws_connection_t* c = s.conn;
+        TlsConn& t = b->tls[c];
+        tpos = align16(tpos);
+        const uint64_t cbegin = tpos;
+        if (!t.carry.empty()) {
+            const uint64_t off = q.arena_len;
+            memcpy(q.h_arena + off, t.carry.data(), t.carry.size());
+            q.arena_len += t.carry.size();
+            q.h_seg[nseg++] = GatherSeg{off, tpos, (uint64_t)t.carry.size()};
+            q.carry_off[k] = off;
+            q.carry_len[k] = t.carry.size();
+            tpos += t.carry.size();
+        }
+        for (uint32_t r : s.reads) {
+            const QueuedRead& qr = q.reads[r];
+            if (qr.len) q.h_seg[nseg++] = GatherSeg{qr.off, tpos, qr.len};
+            tpos += qr.len;
+        }
+        q.h_poff[nt] = q.arena_len;
+        if (c->recv_buffer_pos) {
+            memcpy(q.h_arena + q.arena_len, c->recv_buffer, c->recv_buffer_pos);
+            q.arena_len += c->recv_buffer_pos;
+        }
+        uvhttp_tls_stream_t ts;
+        memset(&ts, 0, sizeof(ts));
+        ts.begin = cbegin - tls_base;
+        ts.len = tpos - cbegin;
+        ts.seq = t.seq;
+        ts.key = nt;
+        ts.ws_prefix = (uint32_t)c->recv_buffer_pos;
+        q.h_tst[nt] = ts;
+        q.h_keys[nt] = t.key;
+        uvhttp_ws_stream_init(c, 0, 0, &q.h_wst[nt]);  // ws_streams sets begin / len / reads
+        plain_cap = align16(plain_cap) + c->recv_buffer_pos + (tpos - cbegin) + 16;
+        q.slot_k[k] = nt++;
+    }
+    q.nt = nt;
+    q.tls_base = tls_base;
+    q.tls_bytes = tpos - tls_base;
+    q.plain_cap = plain_cap;
+    if (!nk && !nt) return 1;  // nothing left to decode (all dropped): the host path is a no-op
     // frames this flush can hold: a server connection's frames are >= 6 bytes except a
     // failing last one, so bytes / 6 + connections bounds them for servers (a client-side
     // connection that exceeds it reports ERR_CAPACITY and is re-run on the host)
     const int g = grow_desc(b, q, pos / 6 + nk + 1);
     if (g) return g;
+    // records: every counted record but a connection's stopping one has >= 5 + 16 bytes
+    const uint64_t max_records = q.tls_bytes / 21 + nt + 1;
+    if (nt) {
+        const int gt = grow_tls(b, q, max_records, plain_cap / 6 + nt + 1);
+        if (gt) return gt;
+    }
     if (b->fail_every && ++b->launches % b->fail_every == 0) return UVHTTP_WS_GPU_ELAUNCH;
     hipStream_t s = b->cs;
     upload_tail(b, q);
@@ -315,20 +504,53 @@ int launch_device(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
         hipLaunchKernelGGL(k_batcher_gather, dim3(nseg), dim3(256), 0, s, q.d_arena, q.d_wire, q.d_seg);
         h = hipGetLastError();
     }
-    if (h == hipSuccess)
-        h = hipMemcpyAsync(q.d_streams, q.h_streams, nk * sizeof(uvhttp_ws_stream_t),
-                           hipMemcpyHostToDevice, s);
-    if (h == hipSuccess && nr)
-        h = hipMemcpyAsync(q.d_read_end, q.h_read_end, nr * sizeof(uint64_t), hipMemcpyHostToDevice, s);
     int rc = UVHTTP_WS_GPU_OK;
-    if (h == hipSuccess)
-        rc = uvhttp_ws_gpu_decode_reads(b->eng, q.d_wire, pos, q.d_streams, nk, q.d_read_end, nr,
-                                        q.max_frames, q.d_desc, q.d_results, s);
-    if (h == hipSuccess && rc == UVHTTP_WS_GPU_OK)
-        h = hipMemcpyAsync(q.h_results, q.d_results, nk * sizeof(uvhttp_ws_stream_result_t),
-                           hipMemcpyDeviceToHost, s);
-    if (h == hipSuccess && rc == UVHTTP_WS_GPU_OK)
-        h = hipMemcpyAsync(q.h_wire, q.d_wire, pos, hipMemcpyDeviceToHost, s);
+    if (nk) {
+        if (h == hipSuccess)
+            h = hipMemcpyAsync(q.d_streams, q.h_streams, nk * sizeof(uvhttp_ws_stream_t),
+                               hipMemcpyHostToDevice, s);
+        if (h == hipSuccess && nr)
+            h = hipMemcpyAsync(q.d_read_end, q.h_read_end, nr * sizeof(uint64_t), hipMemcpyHostToDevice, s);
+        if (h == hipSuccess)
+            rc = uvhttp_ws_gpu_decode_reads(b->eng, q.d_wire, pos, q.d_streams, nk, q.d_read_end, nr,
+                                            q.max_frames, q.d_desc, q.d_results, s);
+        if (h == hipSuccess && rc == UVHTTP_WS_GPU_OK)
+            h = hipMemcpyAsync(q.h_results, q.d_results, nk * sizeof(uvhttp_ws_stream_result_t),
+                               hipMemcpyDeviceToHost, s);
+        if (h == hipSuccess && rc == UVHTTP_WS_GPU_OK)
+            h = hipMemcpyAsync(q.h_wire, q.d_wire, pos, hipMemcpyDeviceToHost, s);
+    }
+    if (nt && h == hipSuccess && rc == UVHTTP_WS_GPU_OK) {
+        h = hipMemcpyAsync(q.d_keys, q.h_keys, nt * sizeof(uvhttp_tls_key_t), hipMemcpyHostToDevice, s);
+        if (h == hipSuccess)
+            h = hipMemcpyAsync(q.d_tst, q.h_tst, nt * sizeof(uvhttp_tls_stream_t), hipMemcpyHostToDevice, s);
+        if (h == hipSuccess)
+            h = hipMemcpyAsync(q.d_wst, q.h_wst, nt * sizeof(uvhttp_ws_stream_t), hipMemcpyHostToDevice, s);
+        if (h == hipSuccess)
+            h = hipMemcpyAsync(q.d_poff, q.h_poff, nt * sizeof(uint64_t), hipMemcpyHostToDevice, s);
+        if (h == hipSuccess) {
+            rc = uvhttp_tls_gpu_open_records(b->teng, q.d_wire + tls_base, q.tls_bytes, q.d_keys, nt,
+                                             q.d_tst, nt, q.d_trecs, (uint32_t)max_records, q.d_tres,
+                                             q.d_plain, plain_cap, s);
+            if (!rc)
+                rc = uvhttp_tls_gpu_ws_streams(b->teng, q.d_tres, q.d_trecs, nt, q.d_tst, q.d_arena,
+                                               q.d_poff, q.d_plain, q.d_wst, q.d_wread_end, s);
+            if (!rc)
+                rc = uvhttp_ws_gpu_decode_reads(b->eng, q.d_plain, plain_cap, q.d_wst, nt,
+                                                q.d_wread_end, (uint32_t)max_records, q.wdesc_cap,
+                                                q.d_wdesc, q.d_wres, s);
+            if (rc) rc = UVHTTP_WS_GPU_ELAUNCH;
+        }
+        if (h == hipSuccess && !rc)
+            h = hipMemcpyAsync(q.h_tres, q.d_tres, nt * sizeof(uvhttp_tls_result_t), hipMemcpyDeviceToHost, s);
+        if (h == hipSuccess && !rc)
+            h = hipMemcpyAsync(q.h_wres, q.d_wres, nt * sizeof(uvhttp_ws_stream_result_t),
+                               hipMemcpyDeviceToHost, s);
+        if (h == hipSuccess && !rc)
+            h = hipMemcpyAsync(q.h_wst, q.d_wst, nt * sizeof(uvhttp_ws_stream_t), hipMemcpyDeviceToHost, s);
+        if (h == hipSuccess && !rc)
+            h = hipMemcpyAsync(q.h_plain, q.d_plain, plain_cap, hipMemcpyDeviceToHost, s);
+    }
     if (h == hipSuccess && rc == UVHTTP_WS_GPU_OK) h = hipEventRecord(q.done_ev, s);
     if (h == hipSuccess && rc == UVHTTP_WS_GPU_OK && b->cfg.on_ready)
         h = hipLaunchHostFunc(s, b->cfg.on_ready, b->cfg.ready_ctx);
@@ -336,8 +558,57 @@ int launch_device(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
     return rc;
 }
 
+// bytes [from, end) of a TLS slot's staged ciphertext (its carry, then its reads)
+std::vector<uint8_t> tls_tail(const BatchQueue& q, size_t k, uint64_t from) {
+    std::vector<uint8_t> out;
+    uint64_t at = 0;
+    auto take = [&](const uint8_t* p, uint64_t n) {
+        if (at + n > from) {
+            const uint64_t skip = from > at ? from - at : 0;
+            out.insert(out.end(), p + skip, p + n);
+        }
+        at += n;
+    };
+    take(q.h_arena + q.carry_off[k], q.carry_len[k]);
+    for (uint32_t r : q.slots[k].reads) take(q.h_arena + q.reads[r].off, q.reads[r].len);
+    return out;
+}
+
+// the connection's TLS handling ends here (CONTROL record): everything from that record on,
+// including ciphertext it has queued in the accumulating queue since, goes back to the caller
+void tls_handback(uvhttp_ws_amd_batcher_t* b, uvhttp_ws_connection_t* conn,
+                  std::vector<uint8_t> bytes, uint64_t next_seq, int status) {
+    BatchQueue& acc = b->q[b->cur];
+    auto it = acc.slot_of.find(conn);
+    if (it != acc.slot_of.end() && acc.slots[it->second].tls) {
+        ConnSlot& s = acc.slots[it->second];
+        for (uint32_t r : s.reads)
+            bytes.insert(bytes.end(), acc.h_arena + acc.reads[r].off,
+                         acc.h_arena + acc.reads[r].off + acc.reads[r].len);
+        s.dropped = true;
+        acc.slot_of.erase(it);
+    }
+    b->tls.erase(conn);
+    b->st.tls_handbacks++;
+    if (b->cfg.on_tls_handback)
+        b->cfg.on_tls_handback(b->cfg.ctx, conn, bytes.data(), bytes.size(), next_seq, status);
+}
+
+// a TLS slot's queue could not be opened on the device: its connection fails (the records
+// cannot be decrypted on the host)
+void fail_tls_slots(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
+    for (size_t k = 0; k < q.slots.size(); ++k) {
+        ConnSlot& s = q.slots[k];
+        if (!s.tls || s.dropped || b->failed.count(s.conn)) continue;
+        s.dropped = true;
+        b->tls.erase(s.conn);
+        report_failure(b, s.conn, UVHTTP_ERROR_INVALID_PARAM);
+    }
+}
+
 // q's decode has finished (or failed): deliver it, or decode it on the host when the
-// device could not (nothing of q has been delivered before this point).
+// device could not (nothing of q has been delivered before this point; TLS connections,
+// which the host cannot open, fail instead).
 int complete_device(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
     int rc = q.launch_rc;
     if (!rc) {
@@ -346,7 +617,7 @@ int complete_device(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
         else rc = uvhttp_ws_gpu_engine_sync(b->eng, b->cs);  // device-side give-ups
         b->st.wait_ms += ms_since(tw);
     }
-    uint64_t frames = 0;
+    uint64_t frames = 0, wframes = 0;
     bool capacity = false;
     if (!rc) {
         for (uint32_t k = 0; k < q.nk; ++k) {
@@ -355,22 +626,39 @@ int complete_device(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
             const uint64_t e = (uint64_t)r.first_frame + r.n_frames;
             if (r.n_frames && e > frames) frames = e;
         }
+        for (uint32_t k = 0; k < q.nt; ++k) {
+            const uvhttp_ws_stream_result_t& r = q.h_wres[k];
+            const uint64_t e = (uint64_t)r.first_frame + r.n_frames;
+            if (r.first_status != UVHTTP_WS_FRAME_ERR_CAPACITY && r.n_frames && e > wframes) wframes = e;
+        }
         if (!capacity && frames &&
             hipMemcpy(q.h_desc, q.d_desc, frames * sizeof(uvhttp_ws_frame_desc_t),
                       hipMemcpyDeviceToHost) != hipSuccess)
             rc = UVHTTP_WS_GPU_ELAUNCH;
+        if (!rc && wframes &&
+            hipMemcpy(q.h_wdesc, q.d_wdesc, wframes * sizeof(uvhttp_ws_frame_desc_t),
+                      hipMemcpyDeviceToHost) != hipSuccess)
+            rc = UVHTTP_WS_GPU_ELAUNCH;
     }
-    if (rc || capacity) {
-        // the host decodes the queue instead (the reads are still in the pinned arena and
-        // no connection has seen any of them); a device error is counted and returned
-        if (capacity) b->st.capacity_flushes++;
-        if (rc) b->st.device_errors++;
+    if (rc) {
+        // the host decodes the plain connections instead (their reads are still in the
+        // pinned arena and no connection has seen any of them); a device error is counted
+        // and returned
+        b->st.device_errors++;
         flush_host(b, q);
+        fail_tls_slots(b, q);
         return rc;
     }
+    if (capacity) {  // more plain frames than the descriptors hold (client connections)
+        b->st.capacity_flushes++;
+        flush_host(b, q);
+    } else {
+        b->st.device_bytes += q.pos;
+        b->st.device_frames += frames;
+    }
     b->st.device_flushes++;
-    b->st.device_bytes += q.pos;
-    b->st.device_frames += frames;
+    b->st.device_bytes += q.tls_bytes;
+    b->st.device_frames += wframes;
     // deliver, connection by connection (callbacks may forget connections as we go)
     const auto td = std::chrono::steady_clock::now();
     b->delivering++;
@@ -378,12 +666,53 @@ int complete_device(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
         if (q.slot_k[k] == UINT32_MAX || q.slots[k].dropped) continue;
         const uint32_t j = q.slot_k[k];
         uvhttp_ws_connection_t* conn = q.slots[k].conn;
-        const uvhttp_error_t dr =
-            uvhttp_ws_deliver_stream(conn, q.h_wire, q.h_desc, &q.h_streams[j], &q.h_results[j]);
-        b->st.device_reads += q.h_results[j].calls;
-        if (dr != UVHTTP_OK) {
+        if (!q.slots[k].tls) {
+            if (capacity) continue;  // (decoded by the host above)
+            const uvhttp_error_t dr =
+                uvhttp_ws_deliver_stream(conn, q.h_wire, q.h_desc, &q.h_streams[j], &q.h_results[j]);
+            b->st.device_reads += q.h_results[j].calls;
+            if (dr != UVHTTP_OK) {
+                q.slots[k].dropped = true;
+                report_failure(b, conn, dr);
+            }
+            continue;
+        }
+        // TLS: the records delivered, each one process_data call on its content
+        const uvhttp_tls_result_t tr = q.h_tres[j];
+        if (tr.first_status == UVHTTP_TLS_REC_ERR_KEY || tr.first_status == UVHTTP_TLS_REC_ERR_CAPACITY ||
+            q.h_wres[j].first_status == UVHTTP_WS_FRAME_ERR_CAPACITY) {
             q.slots[k].dropped = true;
-            report_failure(b, conn, dr);
+            b->tls.erase(conn);
+            report_failure(b, conn, UVHTTP_ERROR_INVALID_PARAM);
+            continue;
+        }
+        bool ws_failed = false;
+        if (tr.n_delivered) {  // (no complete record: mbedtls_ssl_read returned WANT_READ)
+            const uvhttp_error_t dr =
+                uvhttp_ws_deliver_stream(conn, q.h_plain, q.h_wdesc, &q.h_wst[j], &q.h_wres[j]);
+            b->st.device_reads += q.h_wres[j].calls;
+            b->st.tls_records += tr.n_delivered;
+            b->st.tls_bytes += tr.consumed_bytes;
+            if (dr != UVHTTP_OK) {
+                q.slots[k].dropped = true;
+                b->tls.erase(conn);
+                report_failure(b, conn, dr);
+                ws_failed = true;
+            }
+        }
+        if (ws_failed || q.slots[k].dropped) continue;  // (forgotten from a callback)
+        auto ti = b->tls.find(conn);
+        if (ti == b->tls.end()) continue;
+        std::vector<uint8_t> rest = tls_tail(q, k, tr.consumed_bytes);
+        if (tr.first_status == UVHTTP_TLS_REC_CONTROL) {
+            tls_handback(b, conn, std::move(rest), tr.next_seq, tr.first_status);
+        } else if (tr.status != 0) {  // bad MAC / overflow / bad type / version: close
+            q.slots[k].dropped = true;
+            b->tls.erase(ti);
+            report_failure(b, conn, UVHTTP_ERROR_INVALID_PARAM);
+        } else {  // an incomplete record (or none) waits for the next reads
+            ti->second.seq = tr.next_seq;
+            ti->second.carry.swap(rest);
         }
     }
     b->delivering--;
@@ -421,7 +750,7 @@ int start_flush(uvhttp_ws_amd_batcher_t* b, bool wait) {
     if (q.reads.empty()) return rc;
     b->st.flushes++;
     b->cur ^= 1;  // reads submitted from now on (callbacks included) queue in the other one
-    if (b->eng && q.bytes >= b->cfg.min_device_bytes) {
+    if (b->eng && (q.bytes >= b->cfg.min_device_bytes || q.n_tls_slots)) {
         int prev = 0;
         (void)hipGetDevice(&prev);
         if (prev != b->cfg.device) (void)hipSetDevice(b->cfg.device);
@@ -433,6 +762,7 @@ int start_flush(uvhttp_ws_amd_batcher_t* b, bool wait) {
         if (lr == 1) {
             b->st.fallback_flushes++;
             flush_host(b, q);
+            fail_tls_slots(b, q);
             clear_queue(q);
         } else {
             // launched, or a launch error that complete_device turns into a host decode
@@ -553,15 +883,20 @@ int uvhttp_ws_amd_batcher_flush(uvhttp_ws_amd_batcher_t* b) {
     return rc;
 }
 
-uvhttp_error_t uvhttp_ws_amd_batcher_submit_read(uvhttp_ws_amd_batcher_t* b,
-                                                 struct uvhttp_ws_connection* conn,
-                                                 const uint8_t* data, size_t len) {
-    if (!b || !conn || (!data && len)) return UVHTTP_ERROR_INVALID_PARAM;
+}  // extern "C"
+
+namespace {
+
+// queue one read (plain bytes, or a TLS connection's ciphertext)
+uvhttp_error_t queue_read(uvhttp_ws_amd_batcher_t* b, uvhttp_ws_connection_t* conn,
+                          const uint8_t* data, size_t len, bool tls) {
     if (b->failed.count(conn)) return UVHTTP_ERROR_INVALID_PARAM;
     BatchQueue* q = &b->q[b->cur];
     auto it = q->slot_of.find(conn);
     bool fresh = it == q->slot_of.end();
-    const uint64_t pre = align16(conn->recv_buffer_pos) + 16;
+    if (!fresh && q->slots[it->second].tls != tls) return UVHTTP_ERROR_INVALID_PARAM;
+    const uint64_t carry = tls ? kTlsCarryMax : 0;
+    const uint64_t pre = align16(conn->recv_buffer_pos) + 16 + carry;
     const uint64_t need = (uint64_t)len + (fresh ? pre : 0);
     if (q->staged + need > b->cfg.max_bytes || q->reads.size() + 1 > b->cfg.max_reads ||
         (fresh && q->slots.size() + 1 > b->cfg.max_connections)) {
@@ -571,7 +906,20 @@ uvhttp_error_t uvhttp_ws_amd_batcher_submit_read(uvhttp_ws_amd_batcher_t* b,
         Blocked bl{b};
         (void)start_flush(b, true);  // (a device error there was decoded on the host and counted)
         if (b->failed.count(conn)) return UVHTTP_ERROR_INVALID_PARAM;
-        if (pre + len > b->cfg.max_bytes) {
+        if (tls && !b->tls.count(conn)) return UVHTTP_ERROR_INVALID_PARAM;  // handed back
+        const uint64_t pre2 = align16(conn->recv_buffer_pos) + 16 + carry;
+        if (pre2 + len > b->cfg.max_bytes) {
+            if (tls) {
+                // ciphertext can be cut anywhere (records reassemble across flushes): queue it
+                // in halves of a flush
+                const size_t piece = (size_t)(b->cfg.max_bytes / 2);
+                if (piece == 0 || pre2 + piece > b->cfg.max_bytes) return UVHTTP_ERROR_INVALID_PARAM;
+                for (size_t o = 0; o < len; o += piece) {
+                    const uvhttp_error_t rc = queue_read(b, conn, data + o, len - o < piece ? len - o : piece, true);
+                    if (rc != UVHTTP_OK) return rc;
+                }
+                return UVHTTP_OK;
+            }
             // larger than a whole flush: every earlier read of the connection must be
             // delivered first, then the read is decoded here (nothing of it is queued)
             (void)finish_inflight(b, true);
@@ -589,9 +937,10 @@ uvhttp_error_t uvhttp_ws_amd_batcher_submit_read(uvhttp_ws_amd_batcher_t* b,
     uint32_t k;
     if (fresh) {
         k = (uint32_t)q->slots.size();
-        q->slots.push_back(ConnSlot{conn, {}, 0, false});
+        q->slots.push_back(ConnSlot{conn, {}, 0, false, tls});
         q->slot_of[conn] = k;
         q->staged += pre;
+        if (tls) q->n_tls_slots++;
     } else {
         k = it->second;
     }
@@ -607,7 +956,8 @@ uvhttp_error_t uvhttp_ws_amd_batcher_submit_read(uvhttp_ws_amd_batcher_t* b,
         b->st.copy_ms += ms_since(tc);
         q->arena_len += len;
         // a queue large enough for the device streams to HBM while it fills
-        if (q->bytes + len >= b->cfg.min_device_bytes && q->arena_len - q->uploaded >= kUploadPiece) {
+        if ((q->bytes + len >= b->cfg.min_device_bytes || q->n_tls_slots) &&
+            q->arena_len - q->uploaded >= kUploadPiece) {
             int prev = 0;
             (void)hipGetDevice(&prev);
             if (prev != b->cfg.device) (void)hipSetDevice(b->cfg.device);
@@ -625,9 +975,60 @@ uvhttp_error_t uvhttp_ws_amd_batcher_submit_read(uvhttp_ws_amd_batcher_t* b,
     return UVHTTP_OK;
 }
 
+}  // namespace
+
+extern "C" {
+
+uvhttp_error_t uvhttp_ws_amd_batcher_submit_read(uvhttp_ws_amd_batcher_t* b,
+                                                 struct uvhttp_ws_connection* conn,
+                                                 const uint8_t* data, size_t len) {
+    if (!b || !conn || (!data && len)) return UVHTTP_ERROR_INVALID_PARAM;
+    if (b->tls.count(conn)) return UVHTTP_ERROR_INVALID_PARAM;  // a TLS connection's reads are ciphertext
+    return queue_read(b, conn, data, len, false);
+}
+
+int uvhttp_ws_amd_batcher_set_tls(uvhttp_ws_amd_batcher_t* b, struct uvhttp_ws_connection* conn,
+                                  const void* tls_key, uint64_t read_seq) {
+    if (!b || !conn || !tls_key) return UVHTTP_WS_GPU_EINVAL;
+    if (!b->eng) return UVHTTP_WS_GPU_ENODEV;  // no host AEAD: TLS needs the device
+    // plain reads of this connection still queued would be decoded after ciphertext that
+    // follows them: flush them first
+    for (int i = 0; i < 2; ++i) {
+        auto it = b->q[i].slot_of.find(conn);
+        if (it != b->q[i].slot_of.end() && !b->q[i].slots[it->second].tls && !b->delivering) {
+            Blocked bl{b};
+            (void)start_flush(b, true);
+            (void)finish_inflight(b, true);
+            break;
+        }
+    }
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    if (prev != b->cfg.device) (void)hipSetDevice(b->cfg.device);
+    bool ok = true;
+    if (!b->teng) ok = uvhttp_tls_gpu_engine_create(b->cfg.device, &b->teng) == UVHTTP_TLS_GPU_OK;
+    if (ok) ok = alloc_tls(b, b->q[0]) && alloc_tls(b, b->q[1]);
+    if (prev != b->cfg.device) (void)hipSetDevice(prev);
+    if (!ok) return UVHTTP_WS_GPU_ENOMEM;
+    TlsConn& t = b->tls[conn];
+    memcpy(&t.key, tls_key, sizeof(t.key));
+    t.seq = read_seq;
+    t.carry.clear();
+    return UVHTTP_WS_GPU_OK;
+}
+
+uvhttp_error_t uvhttp_ws_amd_batcher_submit_tls_read(uvhttp_ws_amd_batcher_t* b,
+                                                     struct uvhttp_ws_connection* conn,
+                                                     const uint8_t* ciphertext, size_t len) {
+    if (!b || !conn || (!ciphertext && len)) return UVHTTP_ERROR_INVALID_PARAM;
+    if (!b->tls.count(conn)) return UVHTTP_ERROR_INVALID_PARAM;  // not (or no longer) TLS here
+    return queue_read(b, conn, ciphertext, len, true);
+}
+
 void uvhttp_ws_amd_batcher_forget(uvhttp_ws_amd_batcher_t* b, struct uvhttp_ws_connection* conn) {
     if (!b || !conn) return;
     b->failed.erase(conn);
+    b->tls.erase(conn);
     for (int i = 0; i < 2; ++i) {
         BatchQueue& q = b->q[i];
         auto it = q.slot_of.find(conn);
