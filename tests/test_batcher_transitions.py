@@ -224,6 +224,19 @@ def test_capacity_and_device_failure_fall_back_to_host():
         assert len(prod.events) == len(orc.events()) == 12000
     b.close()
 
+    # server connections: 6-byte frames (empty masked payloads) beyond the initial 65 536
+    # descriptors but within the bytes / 6 bound: the decode re-runs on the device with more
+    b = U.Batcher(device=0, min_device_bytes=0)
+    prod = U.WsConnection(1, 16 << 20, 64 << 20)
+    orc = _oracle.OracleConn(1, 16 << 20, 64 << 20, record=1)
+    data = b"".join(_frame(2, 1, b"", rng.randbytes(4), True, 0) for _ in range(70000))
+    assert b.submit(prod, data) == 0 and orc.process_data(data) == 0
+    assert b.flush() == 0
+    st = b.stats()
+    assert st["capacity_flushes"] == 0 and st["host_reads"] == 0 and st["device_frames"] == 70000
+    assert len(prod.events) == len(orc.events()) == 70000
+    b.close()
+
     os.environ["UVHTTP_WS_BATCHER_FAIL_EVERY"] = "1"
     try:
         b = U.Batcher(device=0, min_device_bytes=0)

@@ -25,6 +25,7 @@
 
 #include <chrono>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <unordered_map>
@@ -136,6 +137,8 @@ struct BatchQueue {
     uint32_t nk = 0;               // plain connections staged
     uint64_t pos = 0;              // wire bytes staged
     uint32_t nt = 0;               // TLS connections staged
+    uint32_t nr = 0;               // plain reads staged
+    uint64_t max_records = 0;      // TLS record capacity of the launch
     uint64_t tls_base = 0, tls_bytes = 0, plain_cap = 0;
     std::vector<uint32_t> slot_k;  // slot -> stream index (UINT32_MAX: not staged)
     std::vector<uint64_t> carry_off;  // TLS slot -> its staged carry in h_arena (offset, len)
@@ -482,28 +485,41 @@ int launch_device(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
     q.tls_bytes = tpos - tls_base;
     q.plain_cap = plain_cap;
     if (!nk && !nt) return 1;  // nothing left to decode (all dropped): the host path is a no-op
-    // frames this flush can hold: a server connection's frames are >= 6 bytes except a
-    // failing last one, so bytes / 6 + connections bounds them for servers (a client-side
-    // connection that exceeds it reports ERR_CAPACITY and is re-run on the host)
-    const int g = grow_desc(b, q, pos / 6 + nk + 1);
-    if (g) return g;
+    // descriptors: the decode runs with the capacity the queue has (grown by earlier
+    // flushes); a decode with more frames reports ERR_CAPACITY without touching a byte and
+    // complete_device re-runs it with more (pre-sizing for the worst case — 6-byte frames —
+    // pinned GiBs of host memory per queue and stalled the loop for 100s of ms)
     // records: every counted record but a connection's stopping one has >= 5 + 16 bytes
     const uint64_t max_records = q.tls_bytes / 21 + nt + 1;
+    q.nr = nr;
+    q.max_records = max_records;
     if (nt) {
-        const int gt = grow_tls(b, q, max_records, plain_cap / 6 + nt + 1);
+        const int gt = grow_tls(b, q, max_records, q.wdesc_cap ? q.wdesc_cap : kMinFrames);
         if (gt) return gt;
     }
     if (b->fail_every && ++b->launches % b->fail_every == 0) return UVHTTP_WS_GPU_ELAUNCH;
     hipStream_t s = b->cs;
+    // UVHTTP_WS_BATCHER_TRACE=1: host time of each enqueue step on stderr (diagnostics)
+    static const bool trace = getenv("UVHTTP_WS_BATCHER_TRACE") != nullptr;
+    auto tp = std::chrono::steady_clock::now();
+    auto mark = [&](const char* what) {
+        if (!trace) return;
+        fprintf(stderr, "[batcher] %-12s %8.3f ms\n", what, ms_since(tp));
+        tp = std::chrono::steady_clock::now();
+    };
     upload_tail(b, q);
+    mark("upload_tail");
     hipError_t h = hipEventRecord(q.up_ev, b->up);
     if (h == hipSuccess) h = hipStreamWaitEvent(s, q.up_ev, 0);
+    mark("up_event");
     if (h == hipSuccess && nseg)
         h = hipMemcpyAsync(q.d_seg, q.h_seg, nseg * sizeof(GatherSeg), hipMemcpyHostToDevice, s);
+    mark("seg_h2d");
     if (h == hipSuccess && nseg) {
         hipLaunchKernelGGL(k_batcher_gather, dim3(nseg), dim3(256), 0, s, q.d_arena, q.d_wire, q.d_seg);
         h = hipGetLastError();
     }
+    mark("gather");
     int rc = UVHTTP_WS_GPU_OK;
     if (nk) {
         if (h == hipSuccess)
@@ -511,14 +527,23 @@ int launch_device(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
                                hipMemcpyHostToDevice, s);
         if (h == hipSuccess && nr)
             h = hipMemcpyAsync(q.d_read_end, q.h_read_end, nr * sizeof(uint64_t), hipMemcpyHostToDevice, s);
+        mark("tables_h2d");
         if (h == hipSuccess)
             rc = uvhttp_ws_gpu_decode_reads(b->eng, q.d_wire, pos, q.d_streams, nk, q.d_read_end, nr,
                                             q.max_frames, q.d_desc, q.d_results, s);
+        mark("decode_reads");
         if (h == hipSuccess && rc == UVHTTP_WS_GPU_OK)
             h = hipMemcpyAsync(q.h_results, q.d_results, nk * sizeof(uvhttp_ws_stream_result_t),
                                hipMemcpyDeviceToHost, s);
         if (h == hipSuccess && rc == UVHTTP_WS_GPU_OK)
             h = hipMemcpyAsync(q.h_wire, q.d_wire, pos, hipMemcpyDeviceToHost, s);
+        // the descriptors too, all the capacity (the frame count is only known on the device):
+        // a synchronous copy after completion queued behind the next queue's uploads on the
+        // copy engine and blocked the loop for milliseconds
+        if (h == hipSuccess && rc == UVHTTP_WS_GPU_OK)
+            h = hipMemcpyAsync(q.h_desc, q.d_desc, (size_t)q.max_frames * sizeof(uvhttp_ws_frame_desc_t),
+                               hipMemcpyDeviceToHost, s);
+        mark("d2h");
     }
     if (nt && h == hipSuccess && rc == UVHTTP_WS_GPU_OK) {
         h = hipMemcpyAsync(q.d_keys, q.h_keys, nt * sizeof(uvhttp_tls_key_t), hipMemcpyHostToDevice, s);
@@ -550,6 +575,9 @@ int launch_device(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
             h = hipMemcpyAsync(q.h_wst, q.d_wst, nt * sizeof(uvhttp_ws_stream_t), hipMemcpyDeviceToHost, s);
         if (h == hipSuccess && !rc)
             h = hipMemcpyAsync(q.h_plain, q.d_plain, plain_cap, hipMemcpyDeviceToHost, s);
+        if (h == hipSuccess && !rc)
+            h = hipMemcpyAsync(q.h_wdesc, q.d_wdesc, (size_t)q.wdesc_cap * sizeof(uvhttp_ws_frame_desc_t),
+                               hipMemcpyDeviceToHost, s);
     }
     if (h == hipSuccess && rc == UVHTTP_WS_GPU_OK) h = hipEventRecord(q.done_ev, s);
     if (h == hipSuccess && rc == UVHTTP_WS_GPU_OK && b->cfg.on_ready)
@@ -606,6 +634,50 @@ void fail_tls_slots(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
     }
 }
 
+// A decode whose frames did not fit its descriptors reported ERR_CAPACITY and unmasked
+// nothing: grow the descriptors (up to the bytes / 6 + connections bound of server frames)
+// and run it again on the device, synchronously (rare: capacities only grow).
+int rerun_over_capacity(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
+    auto over = [](const uvhttp_ws_stream_result_t* r, uint32_t n) {
+        for (uint32_t k = 0; k < n; ++k)
+            if (r[k].first_status == UVHTTP_WS_FRAME_ERR_CAPACITY) return true;
+        return false;
+    };
+    hipStream_t s = b->cs;
+    const uint64_t bound = q.pos / 6 + q.nk + 1;
+    while (q.nk && over(q.h_results, q.nk) && q.max_frames < bound) {
+        const uint64_t want = 8ull * q.max_frames < bound ? 8ull * q.max_frames : bound;
+        if (grow_desc(b, q, want)) break;  // (left over capacity: the host decodes it)
+        int rc = uvhttp_ws_gpu_decode_reads(b->eng, q.d_wire, q.pos, q.d_streams, q.nk, q.d_read_end,
+                                            q.nr, q.max_frames, q.d_desc, q.d_results, s);
+        if (!rc && (hipMemcpyAsync(q.h_results, q.d_results, q.nk * sizeof(uvhttp_ws_stream_result_t),
+                                   hipMemcpyDeviceToHost, s) != hipSuccess ||
+                    hipMemcpyAsync(q.h_wire, q.d_wire, q.pos, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                    hipMemcpyAsync(q.h_desc, q.d_desc, (size_t)q.max_frames * sizeof(uvhttp_ws_frame_desc_t),
+                                   hipMemcpyDeviceToHost, s) != hipSuccess))
+            rc = UVHTTP_WS_GPU_ELAUNCH;
+        if (!rc) rc = uvhttp_ws_gpu_engine_sync(b->eng, s);
+        if (rc) return rc;
+    }
+    const uint64_t wbound = q.plain_cap / 6 + q.nt + 1;
+    while (q.nt && over(q.h_wres, q.nt) && q.wdesc_cap < wbound) {
+        const uint64_t want = 8ull * q.wdesc_cap < wbound ? 8ull * q.wdesc_cap : wbound;
+        if (grow_tls(b, q, q.max_records, want)) break;
+        int rc = uvhttp_ws_gpu_decode_reads(b->eng, q.d_plain, q.plain_cap, q.d_wst, q.nt,
+                                            q.d_wread_end, (uint32_t)q.max_records, q.wdesc_cap,
+                                            q.d_wdesc, q.d_wres, s);
+        if (!rc && (hipMemcpyAsync(q.h_wres, q.d_wres, q.nt * sizeof(uvhttp_ws_stream_result_t),
+                                   hipMemcpyDeviceToHost, s) != hipSuccess ||
+                    hipMemcpyAsync(q.h_plain, q.d_plain, q.plain_cap, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                    hipMemcpyAsync(q.h_wdesc, q.d_wdesc, (size_t)q.wdesc_cap * sizeof(uvhttp_ws_frame_desc_t),
+                                   hipMemcpyDeviceToHost, s) != hipSuccess))
+            rc = UVHTTP_WS_GPU_ELAUNCH;
+        if (!rc) rc = uvhttp_ws_gpu_engine_sync(b->eng, s);
+        if (rc) return rc;
+    }
+    return UVHTTP_WS_GPU_OK;
+}
+
 // q's decode has finished (or failed): deliver it, or decode it on the host when the
 // device could not (nothing of q has been delivered before this point; TLS connections,
 // which the host cannot open, fail instead).
@@ -619,6 +691,7 @@ int complete_device(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
     }
     uint64_t frames = 0, wframes = 0;
     bool capacity = false;
+    if (!rc) rc = rerun_over_capacity(b, q);
     if (!rc) {
         for (uint32_t k = 0; k < q.nk; ++k) {
             const uvhttp_ws_stream_result_t& r = q.h_results[k];
@@ -631,14 +704,7 @@ int complete_device(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
             const uint64_t e = (uint64_t)r.first_frame + r.n_frames;
             if (r.first_status != UVHTTP_WS_FRAME_ERR_CAPACITY && r.n_frames && e > wframes) wframes = e;
         }
-        if (!capacity && frames &&
-            hipMemcpy(q.h_desc, q.d_desc, frames * sizeof(uvhttp_ws_frame_desc_t),
-                      hipMemcpyDeviceToHost) != hipSuccess)
-            rc = UVHTTP_WS_GPU_ELAUNCH;
-        if (!rc && wframes &&
-            hipMemcpy(q.h_wdesc, q.d_wdesc, wframes * sizeof(uvhttp_ws_frame_desc_t),
-                      hipMemcpyDeviceToHost) != hipSuccess)
-            rc = UVHTTP_WS_GPU_ELAUNCH;
+        // (the descriptors came back with the results: launch_device / rerun_over_capacity)
     }
     if (rc) {
         // the host decodes the plain connections instead (their reads are still in the
