@@ -149,6 +149,28 @@ def test_key_and_capacity_errors(torch, eng):
     check(torch, eng, wire, keys, st, out_cap=100)                # layout over capacity
 
 
+def test_key_slot_cache(torch, eng):
+    """k_tls_keys keeps a slot's schedule when the same key comes again: a repeated batch, a
+    changed iv byte, a slot made invalid and then valid again, and keys moved between slots
+    must all open exactly as the oracle does."""
+    wire, keys, st = _random_batch(91, 40, [100, 3000, 16384], faults=False)
+    check(torch, eng, wire, keys, st)
+    check(torch, eng, wire, keys, st)                  # every slot cached
+    k2 = keys.copy()
+    k2[0]["iv"][5] ^= 1                                # same key bytes, other iv: rebuilt
+    check(torch, eng, wire, k2, st)
+    k3 = keys.copy()
+    k3[3]["key_len"] = 24                              # invalid ...
+    check(torch, eng, wire, k3, st)
+    check(torch, eng, wire, keys, st)                  # ... and valid again
+    perm = np.roll(np.arange(len(keys)), 1)            # keys moved between slots
+    st2 = st.copy()
+    st2["key"] = perm[st["key"]]
+    k4 = keys.copy()
+    k4[perm] = keys
+    check(torch, eng, wire, k4, st2)
+
+
 def _seal_dev(torch, eng, src, descs, keys, out_bytes):
     out = torch.zeros(out_bytes, dtype=torch.uint8, device="cuda")
     eng.seal_records(_dev(torch, src), _dev(torch, descs), len(descs), _dev(torch, keys),

@@ -55,8 +55,11 @@ constexpr int kCryptWaves = kCryptWG / 64;
                            // 16-word tables (one per nibble: conflict-free ds_read_b32)
 #endif
 #ifndef TLS_TE_COPIES_REC
-#define TLS_TE_COPIES_REC 16  // copies for the one-record-per-wave kernels (32 would make every
-                              // ds_read_b32 conflict-free, but measured 397 vs 465 GB/s: occupancy)
+#define TLS_TE_COPIES_REC 64  // copies for the one-record-per-wave kernels: 32 or more make every
+                              // ds_read_b32 conflict-free (lane l reads copy l % 32, one bank);
+                              // 64 (one per lane) also let one v_perm_b32 form the address
+                              // (round 3, 16 KiB records: 16 copies x 4 waves 483 GB/s, 32 x 8
+                              // 529, 64 x 16 589; profiles/r03_tls_aes_ab.txt)
 #endif
 #ifndef TLS_GHASH8
 #define TLS_GHASH8 2       // Horner multiplier H^64 one byte per step: 1 through an 8-bit table
@@ -85,8 +88,22 @@ constexpr int kCryptWaves = kCryptWG / 64;
 #else
 #define CHACHA_ATTR __launch_bounds__(kCryptWG)
 #endif
-constexpr uint32_t kTeShift = TLS_TE_COPIES == 32 ? 5 : TLS_TE_COPIES == 16 ? 4 : 3;
-constexpr uint32_t kTeShiftRec = TLS_TE_COPIES_REC == 32 ? 5 : TLS_TE_COPIES_REC == 16 ? 4 : 3;
+#ifndef TLS_OPEN_WAVES
+#define TLS_OPEN_WAVES 16  // waves per workgroup of the one-record-per-wave AES-GCM kernels
+                           // (k_tls_open / k_tls_seal): they share one T-table copy set
+#endif
+#ifndef TLS_OPEN_WPE
+#define TLS_OPEN_WPE TLS_WPE  // >0: amdgpu_waves_per_eu hint for those two kernels
+#endif
+constexpr int kOpenWaves = TLS_OPEN_WAVES;
+constexpr int kOpenWG = 64 * kOpenWaves;
+#if TLS_OPEN_WPE > 0
+#define OPEN_ATTR __launch_bounds__(kOpenWG) __attribute__((amdgpu_waves_per_eu(TLS_OPEN_WPE)))
+#else
+#define OPEN_ATTR __launch_bounds__(kOpenWG)
+#endif
+[[maybe_unused]] constexpr uint32_t kTeShift = TLS_TE_COPIES == 64 ? 6 : TLS_TE_COPIES == 32 ? 5 : TLS_TE_COPIES == 16 ? 4 : 3;
+[[maybe_unused]] constexpr uint32_t kTeShiftRec = TLS_TE_COPIES_REC == 64 ? 6 : TLS_TE_COPIES_REC == 32 ? 5 : TLS_TE_COPIES_REC == 16 ? 4 : 3;
 
 struct U128 {  // a GCM block as a big-endian 128-bit value (bit 0 of the spec = MSB of hi)
     uint64_t hi, lo;
@@ -95,14 +112,17 @@ struct U128 {  // a GCM block as a big-endian 128-bit value (bit 0 of the spec =
 // Per key slot, built by k_tls_keys (2 KiB).
 struct __attribute__((aligned(64))) KeySched {
     U128 tab[7][16];   // AES-GCM: 4-bit Shoup tables of H^(2^k), k = 0..6
+    U128 tab3[16];     // AES-GCM: the table of H^3 (the packed kernel's lane combine)
     uint32_t rk[60];   // AES: FIPS-197 round-key words, big-endian; ChaCha20: key words [0..7], LE
     uint32_t nr;       // 10 / 14 (AES), 20 (ChaCha20); 0 = invalid key
     uint32_t version;  // UVHTTP_TLS_VERSION_12 / _13
     uint32_t iv[3];    // AES-GCM: iv as big-endian words; ChaCha20: little-endian words
     uint32_t cipher;   // UVHTTP_TLS_CIPHER_*
     uint32_t pad[10];
+    uvhttp_tls_key_t src;  // the key this slot was built from (key_len 0: none): a call that
+                           // passes the same key again skips the expansion
 };
-static_assert(sizeof(KeySched) == 2112, "key schedule layout");
+static_assert(sizeof(KeySched) == 2432, "key schedule layout");
 
 // One counted record (walk -> crypto -> finalize).
 struct RecWork {
@@ -196,10 +216,22 @@ __device__ inline uint64_t gf_last8(uint32_t r) {
 }
 
 // X . P with P's 4-bit table T (in LDS): Horner in x^4 from the last nibble of X
+#ifndef TLS_MUL_CHUNK
+#define TLS_MUL_CHUNK 16   // >0: the packed kernel's gf_mul_tab loads its table entries CHUNK
+                           // Horner steps at a time (bounds the entries loaded ahead: 214 -> 108
+                           // VGPRs, 2 -> 4 waves per SIMD)
+#endif
+template <int CHUNK = 0>
 __device__ inline U128 gf_mul_tab(U128 x, const U128* __restrict__ t) {
     U128 z = t[x.lo & 0xF];
 #pragma unroll
     for (int k = 30; k >= 0; --k) {
+        if (CHUNK > 0 && k % (CHUNK > 0 ? CHUNK : 1) == 0 && k < 30) {
+            // the remaining nibbles of x pass through an empty asm that also reads z: their
+            // table loads cannot be hoisted above this step (the compiler would otherwise load
+            // all 32 entries up front: 128 VGPRs)
+            asm volatile("" : "+v"(x.lo), "+v"(x.hi) : "v"(z.lo));
+        }
         const uint32_t n = k >= 16 ? (uint32_t)(x.lo >> ((31 - k) * 4)) & 0xF
                                    : (uint32_t)(x.hi >> ((15 - k) * 4)) & 0xF;
         const uint32_t r = (uint32_t)z.lo & 0xF;
@@ -315,7 +347,8 @@ __device__ inline void fill_red8(uint32_t* red8) {
 __device__ inline uint32_t ror32(uint32_t x, int s) { return (x >> s) | (x << (32 - s)); }
 __device__ inline uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
-// AES rounds R0 .. NR of one block with the T-table accessor te(x) (Te0[x]); rk = big-endian
+// AES rounds R0 .. NR of one block with the T-table accessor te(s, k) (Te0[byte k of s], byte 0
+// = least significant; k is always a constant); rk = big-endian
 // round keys; s0..s3 = the state entering round R0; the ciphertext goes to out.  NR is a
 // template argument so every round-key index is a constant (the keys stay in scalar registers
 // when rk is wave-uniform).
@@ -334,28 +367,28 @@ __device__ inline void aes_rounds(const uint32_t* __restrict__ rk, uint32_t s0, 
     constexpr uint32_t nr = NR;
 #pragma unroll
     for (uint32_t r = R0; r < nr; ++r) {
-        const uint32_t t0 = xor3(xor3(te(s0 >> 24), ror32(te((s1 >> 16) & 0xFF), 8), ror32(te((s2 >> 8) & 0xFF), 16)),
-                                 ror32(te(s3 & 0xFF), 24), rk[4 * r]);
-        const uint32_t t1 = xor3(xor3(te(s1 >> 24), ror32(te((s2 >> 16) & 0xFF), 8), ror32(te((s3 >> 8) & 0xFF), 16)),
-                                 ror32(te(s0 & 0xFF), 24), rk[4 * r + 1]);
-        const uint32_t t2 = xor3(xor3(te(s2 >> 24), ror32(te((s3 >> 16) & 0xFF), 8), ror32(te((s0 >> 8) & 0xFF), 16)),
-                                 ror32(te(s1 & 0xFF), 24), rk[4 * r + 2]);
-        const uint32_t t3 = xor3(xor3(te(s3 >> 24), ror32(te((s0 >> 16) & 0xFF), 8), ror32(te((s1 >> 8) & 0xFF), 16)),
-                                 ror32(te(s2 & 0xFF), 24), rk[4 * r + 3]);
+        const uint32_t t0 = xor3(xor3(te(s0, 3), ror32(te(s1, 2), 8), ror32(te(s2, 1), 16)),
+                                 ror32(te(s3, 0), 24), rk[4 * r]);
+        const uint32_t t1 = xor3(xor3(te(s1, 3), ror32(te(s2, 2), 8), ror32(te(s3, 1), 16)),
+                                 ror32(te(s0, 0), 24), rk[4 * r + 1]);
+        const uint32_t t2 = xor3(xor3(te(s2, 3), ror32(te(s3, 2), 8), ror32(te(s0, 1), 16)),
+                                 ror32(te(s1, 0), 24), rk[4 * r + 2]);
+        const uint32_t t3 = xor3(xor3(te(s3, 3), ror32(te(s0, 2), 8), ror32(te(s1, 1), 16)),
+                                 ror32(te(s2, 0), 24), rk[4 * r + 3]);
         s0 = t0, s1 = t1, s2 = t2, s3 = t3;
     }
     // last round: the S-box byte is byte 2 of Te0[x]; v_perm_b32 moves two of them into place
     // (selector bytes 4-7 pick from the first operand, 0-3 from the second, 0x0C gives zero)
     const uint32_t* k = rk + 4 * nr;
-    auto word = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t key) {
-        const uint32_t hi = __builtin_amdgcn_perm(te(a), te(b), 0x06020C0Cu);
-        const uint32_t lo = __builtin_amdgcn_perm(te(c), te(d), 0x0C0C0602u);
+    auto word = [&](uint32_t ta, uint32_t tb, uint32_t tc, uint32_t td, uint32_t key) {
+        const uint32_t hi = __builtin_amdgcn_perm(ta, tb, 0x06020C0Cu);
+        const uint32_t lo = __builtin_amdgcn_perm(tc, td, 0x0C0C0602u);
         return or_xor(hi, lo, key);
     };
-    out[0] = word(s0 >> 24, (s1 >> 16) & 0xFF, (s2 >> 8) & 0xFF, s3 & 0xFF, k[0]);
-    out[1] = word(s1 >> 24, (s2 >> 16) & 0xFF, (s3 >> 8) & 0xFF, s0 & 0xFF, k[1]);
-    out[2] = word(s2 >> 24, (s3 >> 16) & 0xFF, (s0 >> 8) & 0xFF, s1 & 0xFF, k[2]);
-    out[3] = word(s3 >> 24, (s0 >> 16) & 0xFF, (s1 >> 8) & 0xFF, s2 & 0xFF, k[3]);
+    out[0] = word(te(s0, 3), te(s1, 2), te(s2, 1), te(s3, 0), k[0]);
+    out[1] = word(te(s1, 3), te(s2, 2), te(s3, 1), te(s0, 0), k[1]);
+    out[2] = word(te(s2, 3), te(s3, 2), te(s0, 1), te(s1, 0), k[2]);
+    out[3] = word(te(s3, 3), te(s0, 2), te(s1, 1), te(s2, 0), k[3]);
 }
 
 template <int NR, typename TE>
@@ -386,16 +419,16 @@ __device__ inline CtrCache ctr_cache(const uint32_t* __restrict__ rk, const uint
     const uint32_t s0 = nonce[0] ^ rk[0], s1 = nonce[1] ^ rk[1], s2 = nonce[2] ^ rk[2];
     const uint32_t s3 = rk[3];  // bytes 12, 13 of the counter are zero; 14, 15 vary
     CtrCache c;
-    c.c0 = te(s0 >> 24) ^ ror32(te((s1 >> 16) & 0xFF), 8) ^ ror32(te((s2 >> 8) & 0xFF), 16) ^ rk[4];
-    c.c1 = te(s1 >> 24) ^ ror32(te((s2 >> 16) & 0xFF), 8) ^ ror32(te(s0 & 0xFF), 24) ^ rk[5];
-    const uint32_t t2 = te(s2 >> 24) ^ ror32(te((s3 >> 16) & 0xFF), 8) ^ ror32(te((s0 >> 8) & 0xFF), 16) ^
-                        ror32(te(s1 & 0xFF), 24) ^ rk[6];
-    const uint32_t t3 = te(s3 >> 24) ^ ror32(te((s0 >> 16) & 0xFF), 8) ^ ror32(te((s1 >> 8) & 0xFF), 16) ^
-                        ror32(te(s2 & 0xFF), 24) ^ rk[7];
-    c.d0 = ror32(te((t2 >> 8) & 0xFF), 16) ^ ror32(te(t3 & 0xFF), 24) ^ rk[8];
-    c.d1 = ror32(te((t2 >> 16) & 0xFF), 8) ^ ror32(te((t3 >> 8) & 0xFF), 16) ^ rk[9];
-    c.d2 = te(t2 >> 24) ^ ror32(te((t3 >> 16) & 0xFF), 8) ^ rk[10];
-    c.d3 = te(t3 >> 24) ^ ror32(te(t2 & 0xFF), 24) ^ rk[11];
+    c.c0 = te(s0, 3) ^ ror32(te(s1, 2), 8) ^ ror32(te(s2, 1), 16) ^ rk[4];
+    c.c1 = te(s1, 3) ^ ror32(te(s2, 2), 8) ^ ror32(te(s0, 0), 24) ^ rk[5];
+    const uint32_t t2 = te(s2, 3) ^ ror32(te(s3, 2), 8) ^ ror32(te(s0, 1), 16) ^
+                        ror32(te(s1, 0), 24) ^ rk[6];
+    const uint32_t t3 = te(s3, 3) ^ ror32(te(s0, 2), 8) ^ ror32(te(s1, 1), 16) ^
+                        ror32(te(s2, 0), 24) ^ rk[7];
+    c.d0 = ror32(te(t2, 1), 16) ^ ror32(te(t3, 0), 24) ^ rk[8];
+    c.d1 = ror32(te(t2, 2), 8) ^ ror32(te(t3, 1), 16) ^ rk[9];
+    c.d2 = te(t2, 3) ^ ror32(te(t3, 2), 8) ^ rk[10];
+    c.d3 = te(t3, 3) ^ ror32(te(t2, 0), 24) ^ rk[11];
     return c;
 }
 
@@ -404,12 +437,12 @@ template <int NR, typename TE>
 __device__ inline void aes_ctr_cached(const uint32_t* __restrict__ rk, const CtrCache& c, uint32_t ctr,
                                       uint32_t out[4], TE te) {
     const uint32_t s3 = rk[3] ^ ctr;
-    const uint32_t t0 = c.c0 ^ ror32(te(s3 & 0xFF), 24);
-    const uint32_t t1 = c.c1 ^ ror32(te((s3 >> 8) & 0xFF), 16);
-    const uint32_t u0 = xor3(te(t0 >> 24), ror32(te((t1 >> 16) & 0xFF), 8), c.d0);
-    const uint32_t u1 = xor3(te(t1 >> 24), ror32(te(t0 & 0xFF), 24), c.d1);
-    const uint32_t u2 = xor3(ror32(te((t0 >> 8) & 0xFF), 16), ror32(te(t1 & 0xFF), 24), c.d2);
-    const uint32_t u3 = xor3(ror32(te((t0 >> 16) & 0xFF), 8), ror32(te((t1 >> 8) & 0xFF), 16), c.d3);
+    const uint32_t t0 = c.c0 ^ ror32(te(s3, 0), 24);
+    const uint32_t t1 = c.c1 ^ ror32(te(s3, 1), 16);
+    const uint32_t u0 = xor3(te(t0, 3), ror32(te(t1, 2), 8), c.d0);
+    const uint32_t u1 = xor3(te(t1, 3), ror32(te(t0, 0), 24), c.d1);
+    const uint32_t u2 = xor3(ror32(te(t0, 1), 16), ror32(te(t1, 0), 24), c.d2);
+    const uint32_t u3 = xor3(ror32(te(t0, 2), 8), ror32(te(t1, 1), 16), c.d3);
     aes_rounds<NR, 3>(rk, u0, u1, u2, u3, out, te);
 }
 
@@ -456,10 +489,19 @@ __global__ __launch_bounds__(kBlock) void k_tls_keys(const uvhttp_tls_key_t* key
     const uvhttp_tls_key_t k = keys[i];
     KeySched* o = ks + i;
     if (!key_valid(k)) {
+        o->src.key_len = 0;
         o->nr = 0;
         o->version = 0;
         return;
     }
+    {  // the slot already holds this key (the workspace is zeroed when allocated)
+        const uvhttp_tls_key_t& c = o->src;
+        bool same = c.key_len == k.key_len && c.version == k.version && c.cipher == k.cipher;
+        for (int j = 0; j < 32 && same; ++j) same = c.key[j] == k.key[j];
+        for (int j = 0; j < 12 && same; ++j) same = c.iv[j] == k.iv[j];
+        if (same) return;
+    }
+    o->src.key_len = 0;  // (rebuilding)
     o->cipher = k.cipher;
     o->version = k.version;
     if (k.cipher == UVHTTP_TLS_CIPHER_CHACHA20_POLY1305) {  // RFC 8439: little-endian words
@@ -470,6 +512,7 @@ __global__ __launch_bounds__(kBlock) void k_tls_keys(const uvhttp_tls_key_t* key
             o->iv[j] = (uint32_t)k.iv[4 * j] | ((uint32_t)k.iv[4 * j + 1] << 8) |
                        ((uint32_t)k.iv[4 * j + 2] << 16) | ((uint32_t)k.iv[4 * j + 3] << 24);
         o->nr = 20;
+        o->src = k;
         return;
     }
     auto sb = [&](uint32_t x) { return (te0[x] >> 16) & 0xFF; };
@@ -498,14 +541,20 @@ __global__ __launch_bounds__(kBlock) void k_tls_keys(const uvhttp_tls_key_t* key
         o->iv[j] = ((uint32_t)k.iv[4 * j] << 24) | ((uint32_t)k.iv[4 * j + 1] << 16) |
                    ((uint32_t)k.iv[4 * j + 2] << 8) | k.iv[4 * j + 3];
     uint32_t z[4] = {0, 0, 0, 0};
-    aes_encrypt(w, nr, z, [&](uint32_t x) { return te0[x]; });
+    aes_encrypt(w, nr, z, [&](uint32_t v, int k) { return te0[(v >> (8 * k)) & 0xFF]; });
     U128 p{((uint64_t)z[0] << 32) | z[1], ((uint64_t)z[2] << 32) | z[3]};
+    const U128 h = p;
+    U128 t[16];
     for (int l = 0; l < 7; ++l) {
-        U128 t[16];
         gf_table(p, t);
         for (int v = 0; v < 16; ++v) o->tab[l][v] = t[v];
+        if (l == 1) {  // p = H^2
+            gf_table(gf_mul_slow(p, h), t);
+            for (int v = 0; v < 16; ++v) o->tab3[v] = t[v];
+        }
         p = gf_mul_slow(p, p);
     }
+    o->src = k;
 }
 
 // ---- record walk ------------------------------------------------------------------------
@@ -555,10 +604,10 @@ __device__ inline uint32_t walk(const TlsArgs& a, uint32_t s, uint64_t* cap_out,
     const uint8_t* p = a.wire + st.begin;
     uint32_t n = 0;
     uint64_t pos = 0, cap = st.ws_prefix;
-    while (L - pos >= 5) {
-        const uint32_t type = p[pos], ver = be16(p + pos + 1), len = be16(p + pos + 3);
+    // one record: false = the walk ends here (header failure: counted; incomplete: not)
+    auto step = [&](uint32_t type, uint32_t ver, uint32_t len) {
         const int32_t hs = header_status(k.version, k.cipher, type, ver, len);
-        if (!hs && L - pos - 5 < len) break;  // incomplete: waits for more bytes
+        if (!hs && L - pos - 5 < len) return false;  // incomplete: waits for more bytes
         if (size_bits && !hs)
             *size_bits |= len <= (k.cipher == UVHTTP_TLS_CIPHER_AES_GCM ? kPackMaxLenAes : kPackMaxLen) ? 1u : 2u;
         if (WRITE) {
@@ -576,9 +625,41 @@ __device__ inline uint32_t walk(const TlsArgs& a, uint32_t s, uint64_t* cap_out,
             a.work[first + n] = w;
         }
         ++n;
-        if (hs) break;
+        if (hs) return false;
         cap += record_cap(k.version, k.cipher, len);
         pos += 5 + (uint64_t)len;
+        return true;
+    };
+    // The walk is a chain of dependent header loads (one memory round trip per record).  With
+    // the header at pos known, the headers kSpec records ahead are loaded at once on the guess
+    // that the records have the same length (a connection's full-size records); each guess is
+    // used while it holds, so a run of equal records costs one round trip per kSpec + 1.
+    constexpr int kSpec = 3;
+    while (L - pos >= 5) {
+        const uint32_t type = p[pos], ver = be16(p + pos + 1), len = be16(p + pos + 3);
+        const uint64_t stride = 5 + (uint64_t)len;
+        uint32_t gt[kSpec], gv[kSpec], gl[kSpec];
+        bool have[kSpec];
+#pragma unroll
+        for (int j = 0; j < kSpec; ++j) {
+            const uint64_t q = pos + (j + 1) * stride;
+            have[j] = q <= L && L - q >= 5;
+            if (have[j]) gt[j] = p[q], gv[j] = be16(p + q + 1), gl[j] = be16(p + q + 3);
+        }
+        if (!step(type, ver, len)) break;
+        bool go = true;
+#pragma unroll
+        for (int j = 0; j < kSpec; ++j) {
+            // pos advanced by stride per record of length len: the guess is the next header
+            // while every earlier guessed record had length len
+            if (!go || !have[j]) break;
+            if (!step(gt[j], gv[j], gl[j])) {
+                go = false;
+                break;
+            }
+            if (gl[j] != len) break;
+        }
+        if (!go) break;
     }
     *cap_out = cap;
     return n;
@@ -777,7 +858,17 @@ __device__ Lanes gcm_lanes(const KeySched* __restrict__ ks, const uint32_t* te, 
     const uint32_t m = nblk + 2;             // AAD, ciphertext blocks, length block
     const uint32_t J = (m + 63) / 64;
     const uint32_t pad = 64 * J - m;
-    auto te_lds = [&](uint32_t x) { return te[(x << kTeShiftRec) | lane32]; };
+#if TLS_TE_COPIES_REC == 64
+    // entry x of lane l's copy at byte 256 x + 4 l: one v_perm_b32 builds the address from the
+    // state byte and the lane offset (no extract + shift-or)
+    const uint32_t lane4 = lane32 << 2;
+    const uint8_t* te8 = reinterpret_cast<const uint8_t*>(te);
+    auto te_lds = [&](uint32_t v, int k) {
+        return *reinterpret_cast<const uint32_t*>(te8 + __builtin_amdgcn_perm(v, lane4, 0x0C0C0000u | ((4u + k) << 8)));
+    };
+#else
+    auto te_lds = [&](uint32_t v, int k) { return te[(((v >> (8 * k)) & 0xFF) << kTeShiftRec) | lane32]; };
+#endif
     const uint32_t* __restrict__ rk = ks->rk;
     U128 acc{0, 0};
     uint32_t ej0[4] = {0, 0, 0, 0};
@@ -870,18 +961,19 @@ __device__ Lanes gcm_lanes(const KeySched* __restrict__ ks, const uint32_t* te, 
 // the same combine for the workgroup's four records at once, through LDS: at level t the
 // 4 x 32 / 2^t pairs are spread over the workgroup's threads, so the four trees cost about two
 // wave-wide multiplies per record instead of seven (s_acc[w][l] = record w, lane l)
+template <int W>
 [[maybe_unused]] __device__ inline void wg_tree(U128 (*s_acc)[64], const U128 (*tabs)[7][16]) {
 #pragma unroll
     for (int t = 0; t < 6; ++t) {
         const uint32_t per = 32u >> t;  // pairs per record at this level
-        if (threadIdx.x < kCryptWaves * per) {
+        if (threadIdx.x < W * per) {
             const uint32_t w = threadIdx.x / per, p = threadIdx.x % per;
             const uint32_t l = p << (t + 1), r = l + (1u << t);
             s_acc[w][l] = gf_xor(gf_mul_tab(s_acc[w][l], tabs[w][t]), s_acc[w][r]);
         }
         __syncthreads();
     }
-    if (threadIdx.x < kCryptWaves) s_acc[threadIdx.x][0] = gf_mul_tab(s_acc[threadIdx.x][0], tabs[threadIdx.x][0]);
+    if (threadIdx.x < W) s_acc[threadIdx.x][0] = gf_mul_tab(s_acc[threadIdx.x][0], tabs[threadIdx.x][0]);
     __syncthreads();
 }
 
@@ -1215,7 +1307,7 @@ __device__ inline void load_tables(const KeySched* ks, U128 (*tabs)[16]) {
 
 template <uint32_t COPIES = TLS_TE_COPIES>
 __device__ inline void fill_te(const uint32_t* te0, uint32_t* te) {
-    constexpr uint32_t sh = COPIES == 32 ? 5 : COPIES == 16 ? 4 : 3;
+    constexpr uint32_t sh = COPIES == 64 ? 6 : COPIES == 32 ? 5 : COPIES == 16 ? 4 : 3;
     for (uint32_t i = threadIdx.x; i < 256 * COPIES; i += blockDim.x) te[i] = te0[i >> sh];
     __syncthreads();
 }
@@ -1474,13 +1566,29 @@ __device__ inline U128 shfl_down128_w(U128 v, int d) {
 constexpr int kAesSeg = TLS_AES_SEG;         // lanes per record in k_tls_open_aes_packed
 constexpr int kAesSegLog = kAesSeg == 16 ? 4 : kAesSeg == 8 ? 3 : kAesSeg == 4 ? 2 : 1;
 constexpr int kAesPackW = 64 / kAesSeg;      // records per wave
+#ifndef TLS_RK_STRIDE
+#define TLS_RK_STRIDE 60   // words per record of staged round keys (60 = AES-256's schedule):
+                           // record k starts 4 k banks lower, so the records of a ds_read_b128
+                           // lane group hit different banks (64: 4-way conflicts)
+#endif
+constexpr int kRkStride = TLS_RK_STRIDE;
+#ifndef TLS_PACK_GTREE
+#define TLS_PACK_GTREE 1   // 1: the lane combine of k_tls_open_aes_packed reads H^(2^t) from the
+                           // key schedule in global memory; only H^SEG (Horner) is staged in LDS
+#endif
+constexpr int kPackTabs = TLS_PACK_GTREE ? 1 : kAesSegLog + 1;  // staged tables per record
+#ifndef TLS_PACK_AES_WAVES
+#define TLS_PACK_AES_WAVES 16  // waves per workgroup of k_tls_open_aes_packed (they share the T-table)
+#endif
+constexpr int kPackAesWaves = TLS_PACK_AES_WAVES;
+constexpr int kPackAesWG = 64 * kPackAesWaves;
 static_assert((1 << kAesSegLog) == kAesSeg && kAesPackW % kPack == 0, "AES segment size");
 
 // records r0 .. r0 + 64/SEG - 1, each skipped when its group of kPack holds a long AES record
 // (that group goes to k_tls_open)
 template <int SEG, int LOG>
-__device__ void aes_open_packed(const TlsArgs& a, uint32_t r0, const uint32_t* te, uint32_t (*s_rk)[64],
-                                U128 (*s_tab)[LOG + 1][16]) {
+__device__ void aes_open_packed(const TlsArgs& a, uint32_t r0, const uint32_t* te, uint32_t (*s_rk)[kRkStride],
+                                U128 (*s_tab)[kPackTabs][16]) {
     const uint32_t lane = threadIdx.x & 63, k = lane / SEG, u = lane % SEG;
     const uint32_t r = r0 + k;
     const uint32_t n = a.n_total[0];
@@ -1503,8 +1611,8 @@ __device__ void aes_open_packed(const TlsArgs& a, uint32_t r0, const uint32_t* t
     if (act) {  // the segment's round keys and H^(2^t) tables, t = 0..LOG
         for (uint32_t i = u; i < 60; i += SEG) s_rk[k][i] = ks->rk[i];
 #pragma unroll
-        for (int i = 0; i <= LOG; ++i)
-            for (uint32_t e = u; e < 16; e += SEG) s_tab[k][i][e] = ks->tab[i][e];
+        for (int i = 0; i < kPackTabs; ++i)
+            for (uint32_t e = u; e < 16; e += SEG) s_tab[k][i][e] = ks->tab[TLS_PACK_GTREE ? LOG : i][e];
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1555,8 +1663,16 @@ __device__ void aes_open_packed(const TlsArgs& a, uint32_t r0, const uint32_t* t
         if (o > J) J = o;
     }
     J = __builtin_amdgcn_readfirstlane(J);
+#if TLS_TE_COPIES == 64
+    const uint32_t lane4 = lane << 2;  // (layout as in gcm_lanes)
+    const uint8_t* te8 = reinterpret_cast<const uint8_t*>(te);
+    auto te_lds = [&](uint32_t v, int k) {
+        return *reinterpret_cast<const uint32_t*>(te8 + __builtin_amdgcn_perm(v, lane4, 0x0C0C0000u | ((4u + k) << 8)));
+    };
+#else
     const uint32_t lane_te = lane & (TLS_TE_COPIES - 1);
-    auto te_lds = [&](uint32_t x) { return te[(x << kTeShift) | lane_te]; };
+    auto te_lds = [&](uint32_t v, int k) { return te[(((v >> (8 * k)) & 0xFF) << kTeShift) | lane_te]; };
+#endif
     U128 acc{0, 0};
     uint32_t ej0[4] = {0, 0, 0, 0};
     LastNz nz{0, {0, 0, 0, 0}};
@@ -1594,11 +1710,21 @@ __device__ void aes_open_packed(const TlsArgs& a, uint32_t r0, const uint32_t* t
         } else if ((uint32_t)q == m - 1) {
             x = U128{(uint64_t)alen * 8, (uint64_t)clen * 8};
         }
-        acc = j == 0 ? x : gf_xor(gf_mul_tab(acc, s_tab[k][LOG]), x);  // Horner, H^SEG
+        acc = j == 0 ? x : gf_xor(gf_mul_tab<TLS_MUL_CHUNK>(acc, s_tab[k][kPackTabs - 1]), x);  // Horner, H^SEG
     }
+    if constexpr (SEG == 4 && TLS_PACK_GTREE) {
+        // lane u's sum takes H^(4 - u) (the tree below, unrolled: a0 H^4 + a1 H^3 + a2 H^2 +
+        // a3 H): one multiply per lane instead of three, then two shuffle-XORs into lane 0
+        const U128* tp = u == 0 ? ks->tab[2] : u == 1 ? ks->tab3 : u == 2 ? ks->tab[1] : ks->tab[0];
+        acc = gf_mul_tab<TLS_MUL_CHUNK>(acc, tp);
+        acc = gf_xor(acc, shfl_down128_w<SEG>(acc, 1));
+        acc = gf_xor(acc, shfl_down128_w<SEG>(acc, 2));
+    } else {
 #pragma unroll
-    for (int t = 0; t < LOG; ++t) acc = gf_xor(gf_mul_tab(acc, s_tab[k][t]), shfl_down128_w<SEG>(acc, 1 << t));
-    acc = gf_mul_tab(acc, s_tab[k][0]);
+        for (int t = 0; t < LOG; ++t)
+            acc = gf_xor(gf_mul_tab<TLS_MUL_CHUNK>(acc, TLS_PACK_GTREE ? ks->tab[t] : s_tab[k][t]), shfl_down128_w<SEG>(acc, 1 << t));
+        acc = gf_mul_tab<TLS_MUL_CHUNK>(acc, TLS_PACK_GTREE ? ks->tab[0] : s_tab[k][0]);
+    }
     uint32_t e[4];
 #pragma unroll
     for (int b = 0; b < 4; ++b) e[b] = __shfl(ej0[b], (int)pad, SEG);  // E(K, J0): round 0, lane pad
@@ -1644,19 +1770,19 @@ __device__ inline void open_status(const TlsArgs& a, uint32_t r, const CryptOut&
     a.work[r].content_len = cl;
 }
 
-__global__ CRYPT_ATTR void k_tls_open(TlsArgs a) {
+__global__ OPEN_ATTR void k_tls_open(TlsArgs a) {
     __shared__ uint32_t te[256 * TLS_TE_COPIES_REC];
-    __shared__ U128 tabs[kCryptWaves][7][16];
+    __shared__ U128 tabs[kOpenWaves][7][16];
 #if TLS_GHASH8
-    __shared__ U128 t8s[kCryptWaves][TLS_GHASH8 == 2 ? 16 : 256];
+    __shared__ U128 t8s[kOpenWaves][TLS_GHASH8 == 2 ? 16 : 256];
     U128* t8 = t8s[threadIdx.x >> 6];
 #else
     U128* t8 = nullptr;
 #endif
 #if TLS_WG_TREE
-    __shared__ U128 s_acc[kCryptWaves][64];
+    __shared__ U128 s_acc[kOpenWaves][64];
 #endif
-    __shared__ uint32_t red8[256];
+    __shared__ uint32_t red8[TLS_RED8 == 2 ? 32 : 256];
     if (!(a.n_total[2] & 32u)) return;  // no AES-GCM record too long to pack
     fill_red8(red8);
     fill_te<TLS_TE_COPIES_REC>(a.te0, te);
@@ -1667,7 +1793,7 @@ __global__ CRYPT_ATTR void k_tls_open(TlsArgs a) {
     // k_tls_open_aes_packed) and opens them one per round; rounds are workgroup-uniform (the
     // shared combine has barriers); r is wave-uniform: readfirstlane makes the record and
     // key-schedule loads scalar
-    for (uint32_t gb = blockIdx.x * kCryptWaves; gb * kPack < n; gb += gridDim.x * kCryptWaves) {
+    for (uint32_t gb = blockIdx.x * kOpenWaves; gb * kPack < n; gb += gridDim.x * kOpenWaves) {
     const uint32_t g = __builtin_amdgcn_readfirstlane(gb + wave);
     const bool grp = g * kPack < n && group_has_long(a, g, n, UVHTTP_TLS_CIPHER_AES_GCM);
     for (uint32_t i = 0; i < kPack; ++i) {
@@ -1735,7 +1861,7 @@ __global__ CRYPT_ATTR void k_tls_open(TlsArgs a) {
         if (__syncthreads_or(active)) {
             s_acc[wave][lane] = L.acc;
             __syncthreads();
-            wg_tree(s_acc, tabs);
+            wg_tree<kOpenWaves>(s_acc, tabs);
             ghash = s_acc[wave][0];
         }
 #else
@@ -1747,15 +1873,23 @@ __global__ CRYPT_ATTR void k_tls_open(TlsArgs a) {
     }
 }
 
-__global__ CRYPT_ATTR void k_tls_open_aes_packed(TlsArgs a) {
+#ifndef TLS_PACK_AES_WPE
+#define TLS_PACK_AES_WPE 4  // >0: amdgpu_waves_per_eu hint for k_tls_open_aes_packed
+#endif
+#if TLS_PACK_AES_WPE > 0
+#define PACK_AES_ATTR __launch_bounds__(kPackAesWG) __attribute__((amdgpu_waves_per_eu(TLS_PACK_AES_WPE)))
+#else
+#define PACK_AES_ATTR __launch_bounds__(kPackAesWG)
+#endif
+__global__ PACK_AES_ATTR void k_tls_open_aes_packed(TlsArgs a) {
     __shared__ uint32_t te[256 * TLS_TE_COPIES];
-    __shared__ uint32_t s_rk[kCryptWaves][kAesPackW][64];
-    __shared__ U128 s_tab[kCryptWaves][kAesPackW][kAesSegLog + 1][16];
+    __shared__ uint32_t s_rk[kPackAesWaves][kAesPackW][kRkStride];
+    __shared__ U128 s_tab[kPackAesWaves][kAesPackW][kPackTabs][16];
     if (!(a.n_total[2] & 16u)) return;  // no short AES-GCM record
     fill_te(a.te0, te);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t n = a.n_total[0];
-    for (uint32_t g = blockIdx.x * kCryptWaves + wave; g * kAesPackW < n; g += gridDim.x * kCryptWaves)
+    for (uint32_t g = blockIdx.x * kPackAesWaves + wave; g * kAesPackW < n; g += gridDim.x * kPackAesWaves)
         aes_open_packed<kAesSeg, kAesSegLog>(a, g * kAesPackW, te, s_rk[wave], s_tab[wave]);
 }
 
@@ -1827,24 +1961,24 @@ __device__ inline bool seal_prep(const SealArgs& a, uint32_t r, uint32_t cipher,
     return sr->out_off + 5 + *rlen <= a.out_cap && sr->src_off + sr->plain_len <= a.src_len;
 }
 
-__global__ CRYPT_ATTR void k_tls_seal(SealArgs a) {
+__global__ OPEN_ATTR void k_tls_seal(SealArgs a) {
     __shared__ uint32_t te[256 * TLS_TE_COPIES_REC];
-    __shared__ U128 tabs[kCryptWaves][7][16];
+    __shared__ U128 tabs[kOpenWaves][7][16];
 #if TLS_GHASH8
-    __shared__ U128 t8s[kCryptWaves][TLS_GHASH8 == 2 ? 16 : 256];
+    __shared__ U128 t8s[kOpenWaves][TLS_GHASH8 == 2 ? 16 : 256];
     U128* t8 = t8s[threadIdx.x >> 6];
 #else
     U128* t8 = nullptr;
 #endif
 #if TLS_WG_TREE
-    __shared__ U128 s_acc[kCryptWaves][64];
+    __shared__ U128 s_acc[kOpenWaves][64];
 #endif
-    __shared__ uint32_t red8[256];
+    __shared__ uint32_t red8[TLS_RED8 == 2 ? 32 : 256];
     fill_red8(red8);
     fill_te<TLS_TE_COPIES_REC>(a.te0, te);
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t cur = 0xFFFFFFFFu, cur8 = 0xFFFFFFFFu;  // key slots of the wave's 4-bit / 8-bit tables
-    for (uint32_t rb = blockIdx.x * kCryptWaves; rb < a.n; rb += gridDim.x * kCryptWaves) {
+    for (uint32_t rb = blockIdx.x * kOpenWaves; rb < a.n; rb += gridDim.x * kOpenWaves) {
         const uint32_t r = __builtin_amdgcn_readfirstlane(rb + wave);
         uvhttp_tls_seal_t sr;
         const KeySched* ks = a.sched;
@@ -1900,7 +2034,7 @@ __global__ CRYPT_ATTR void k_tls_seal(SealArgs a) {
         if (__syncthreads_or(active)) {
             s_acc[wave][lane] = L.acc;
             __syncthreads();
-            wg_tree(s_acc, tabs);
+            wg_tree<kOpenWaves>(s_acc, tabs);
             ghash = s_acc[wave][0];
         }
 #else
@@ -1974,35 +2108,46 @@ __global__ __launch_bounds__(kBlock) void k_tls_finalize(TlsArgs a) {
     }
     uint64_t plain = 0;
     bool stopped = false, moved = false;
-    for (uint32_t j = 0; j < sw.n_rec; ++j) {
-        const RecWork w = a.work[r.first_record + j];
-        uvhttp_tls_record_t o;
-        o.rec_off = w.rec_off;
-        o.out_off = 0;
-        o.content_len = 0;
-        o.stream = s;
-        o.type = 0;
-        o.reserved = 0;
-        o.reserved2 = 0;
-        if (stopped) {
-            o.status = UVHTTP_TLS_REC_SKIPPED;
-        } else {
-            o.status = (int8_t)w.status;
-            o.type = (uint8_t)w.type;
-            o.content_len = w.content_len;
-            if (w.status == UVHTTP_TLS_REC_OK) {
-                o.out_off = r.out_off + plain;
-                if (o.out_off != w.spec_off) moved = true;
-                plain += w.content_len;
-                r.n_delivered++;
-                r.consumed_bytes = w.rec_off - st.begin + 5 + w.len;
+    // the lane's records four at a time: the four loads are issued before the stores (the
+    // stores could alias them as far as the compiler knows, which serialised one load per record)
+    constexpr uint32_t kAhead = 4;
+    for (uint32_t j0 = 0; j0 < sw.n_rec; j0 += kAhead) {
+        RecWork wb[kAhead];
+#pragma unroll
+        for (uint32_t i = 0; i < kAhead; ++i)
+            if (j0 + i < sw.n_rec) wb[i] = a.work[r.first_record + j0 + i];
+#pragma unroll
+        for (uint32_t i = 0; i < kAhead; ++i) {
+            if (j0 + i >= sw.n_rec) break;
+            const RecWork& w = wb[i];
+            uvhttp_tls_record_t o;
+            o.rec_off = w.rec_off;
+            o.out_off = 0;
+            o.content_len = 0;
+            o.stream = s;
+            o.type = 0;
+            o.reserved = 0;
+            o.reserved2 = 0;
+            if (stopped) {
+                o.status = UVHTTP_TLS_REC_SKIPPED;
             } else {
-                stopped = true;
-                r.first_status = w.status;
-                r.status = w.status < 0 ? -1 : 0;
+                o.status = (int8_t)w.status;
+                o.type = (uint8_t)w.type;
+                o.content_len = w.content_len;
+                if (w.status == UVHTTP_TLS_REC_OK) {
+                    o.out_off = r.out_off + plain;
+                    if (o.out_off != w.spec_off) moved = true;
+                    plain += w.content_len;
+                    r.n_delivered++;
+                    r.consumed_bytes = w.rec_off - st.begin + 5 + w.len;
+                } else {
+                    stopped = true;
+                    r.first_status = w.status;
+                    r.status = w.status < 0 ? -1 : 0;
+                }
             }
+            a.records[r.first_record + j0 + i] = o;
         }
-        a.records[r.first_record + j] = o;
     }
     r.next_seq = st.seq + r.n_delivered;
     r.plain_len = plain;
@@ -2139,6 +2284,14 @@ static int tls_reserve(uvhttp_tls_gpu_engine_t* e, uint32_t keys, uint32_t strea
     }
     char* b = (char*)e->ws;
     e->sched = (KeySched*)(b + o_sched);
+    // no slot holds a key yet (KeySched.src.key_len 0)
+    const hipError_t hz = hipMemset(e->ws, 0, o_work);
+    if (hz != hipSuccess) {
+        (void)hipFree(e->ws);
+        e->ws = nullptr;
+        e->cap_keys = e->cap_streams = e->cap_records = 0;
+        return tls_err(e, UVHTTP_TLS_GPU_ENOMEM, "hipMemset tls key slots", hz);
+    }
     e->work = (RecWork*)(b + o_work);
     e->sw = (StreamWork*)(b + o_sw);
     e->blk = (uint64_t*)(b + o_blk);
@@ -2305,8 +2458,16 @@ int uvhttp_tls_gpu_open_records(uvhttp_tls_gpu_engine_t* e, const uint8_t* wire,
     const uint32_t need = (max_records + kCryptWaves - 1) / kCryptWaves;
     const uint32_t grid = need < (uint32_t)e->crypt_grid ? (need ? need : 1) : (uint32_t)e->crypt_grid;
     const int tk = tls_timing_begin(e, s);
-    hipLaunchKernelGGL(k_tls_open, dim3(grid), dim3(kCryptWG), 0, s, a);
-    hipLaunchKernelGGL(k_tls_open_aes_packed, dim3(grid), dim3(kCryptWG), 0, s, a);
+    // k_tls_open: a wave per group of kPack records, kOpenWaves waves per workgroup
+    const uint32_t need_o = (max_records + kPack * kOpenWaves - 1) / (kPack * kOpenWaves);
+    const uint32_t cap_o = (uint32_t)e->crypt_grid * kCryptWaves / kOpenWaves;
+    const uint32_t grid_o = need_o < cap_o ? (need_o ? need_o : 1) : cap_o;
+    hipLaunchKernelGGL(k_tls_open, dim3(grid_o), dim3(kOpenWG), 0, s, a);
+    // k_tls_open_aes_packed: kAesPackW records per wave, kPackAesWaves waves per workgroup
+    const uint32_t need_p = (max_records + kAesPackW * kPackAesWaves - 1) / (kAesPackW * kPackAesWaves);
+    const uint32_t cap_p = (uint32_t)e->crypt_grid * kCryptWaves / kPackAesWaves;
+    const uint32_t grid_p = need_p < cap_p ? (need_p ? need_p : 1) : cap_p;
+    hipLaunchKernelGGL(k_tls_open_aes_packed, dim3(grid_p), dim3(kPackAesWG), 0, s, a);
     hipLaunchKernelGGL(k_tls_open_chacha, dim3(grid), dim3(kCryptWG), 0, s, a);
     hipLaunchKernelGGL(k_tls_open_chacha_packed, dim3(grid), dim3(kCryptWG), 0, s, a);
     tls_timing_end(e, tk, s);
@@ -2342,7 +2503,9 @@ int uvhttp_tls_gpu_seal_records(uvhttp_tls_gpu_engine_t* e, const uint8_t* src, 
     const uint32_t need = (n_records + kCryptWaves - 1) / kCryptWaves;
     const uint32_t grid = need < (uint32_t)e->crypt_grid ? need : (uint32_t)e->crypt_grid;
     const int tk = tls_timing_begin(e, s);
-    hipLaunchKernelGGL(k_tls_seal, dim3(grid), dim3(kCryptWG), 0, s, a);
+    const uint32_t need_s = (n_records + kOpenWaves - 1) / kOpenWaves;
+    const uint32_t cap_s = (uint32_t)e->crypt_grid * kCryptWaves / kOpenWaves;
+    hipLaunchKernelGGL(k_tls_seal, dim3(need_s < cap_s ? need_s : cap_s), dim3(kOpenWG), 0, s, a);
     hipLaunchKernelGGL(k_tls_seal_chacha, dim3(grid), dim3(kCryptWG), 0, s, a);
     tls_timing_end(e, tk, s);
     const hipError_t h = hipGetLastError();
