@@ -360,6 +360,11 @@ class GpuWorkload:
         self.build_dev = self.streams_dev = None
         self.kernel = {"compact": "k_gather_compact", "build": "kb_emit",
                        "build_masked": "kb_emit"}.get(mode, "k_unmask_inplace")
+        # in place, a batch of equal-stride small frames takes the fused path (ws_gpu.hip
+        # run_decode: payload before plan, stride <= UVHTTP_WS_FUSED_MAX, default 2560 B)
+        fused_max = int(os.environ.get("UVHTTP_WS_FUSED_MAX", "2560") or 2560)
+        if mode == "inplace" and os.environ.get("UVHTTP_WS_FUSED", "1") != "0" and 64 <= stride <= fused_max:
+            self.kernel = "k_unmask_stride"
         if mode.startswith("build"):
             # send side: frame n payloads of the config (server echo: unmasked; client: masked)
             import numpy as np

@@ -14,7 +14,7 @@ import statistics
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ("k_unmask_inplace", "k_gather_compact")
+KERNELS = ("k_unmask_inplace", "k_gather_compact", "k_unmask_stride")
 # written under gpurun_out/ (the only directory merged back from the GPU box); copy the
 # files into profiles/ to commit them
 EVID = os.path.join(REPO, "gpurun_out", "evidence")
@@ -31,6 +31,21 @@ def counter_rows(d, name):
                 if any(k in kn for k in KERNELS) and row.get("Counter_Name") == name:
                     vals.append(float(row["Counter_Value"]))
     return vals
+
+
+def per_kernel(d, name):
+    """median counter value per launch of every decode kernel (torch / runtime kernels left out)"""
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    vals = {}
+    for f in files:
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                kn = row.get("Kernel_Name", "")
+                if row.get("Counter_Name") != name or "at::native" in kn or "rocclr" in kn or "k_gen_" in kn:
+                    continue
+                short = kn.replace("(anonymous namespace)::", "").split("(")[0].split("<")[0].split()[-1]
+                vals.setdefault(short, []).append(float(row["Counter_Value"]))
+    return {k: statistics.median(v) for k, v in vals.items()}
 
 
 def main():
@@ -63,11 +78,15 @@ def main():
     if fetch and write:
         res["hbm_bytes_per_launch"] = int((2 * res["fetch_size_kib_per_launch"]
                                            + res["write_size_kib_per_launch"]) * 1024)
+    fk, wk = per_kernel(os.path.join(out, "fetch"), "FETCH_SIZE"), per_kernel(os.path.join(out, "write"), "WRITE_SIZE")
+    res["per_kernel_hbm_bytes"] = {k: int((2 * fk[k] + wk.get(k, 0.0)) * 1024) for k in fk}
+    res["step_hbm_bytes"] = sum(res["per_kernel_hbm_bytes"].values())
     if bench:
         res["alg_bytes_per_launch"] = bench["roofline"]["alg_bytes_per_launch"]
         res["bench_avg_kernel_us"] = bench["roofline"]["avg_kernel_us"]
         if res.get("hbm_bytes_per_launch"):
             res["traffic_over_alg"] = round(res["hbm_bytes_per_launch"] / res["alg_bytes_per_launch"], 4)
+        res["step_traffic_over_alg"] = round(res["step_hbm_bytes"] / res["alg_bytes_per_launch"], 4)
     dst = os.path.join(EVID, f"traffic_{cfg}_{mode}.json")
     with open(dst, "w") as fh:
         json.dump(res, fh, indent=1)

@@ -12,7 +12,7 @@ OUT=$ROOT/gpurun_out/prof_${TAG}_${CFG}_${MODE}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
-ARGS="$ROOT/bench.py --config $CFG --mode $MODE --no-cpu-baseline --no-c5-base"
+ARGS="$ROOT/bench.py --config $CFG --mode $MODE --no-cpu-baseline --no-c5-base --no-ceiling"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run \
   -- python3 $ARGS --steps 20 --warmup 5 > "$OUT/bench_trace.json" 2> "$OUT/trace.err"
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run \
