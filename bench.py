@@ -653,15 +653,17 @@ def main():
 def e2e_live(local, conns=1024, frames=4, size=65536, flushes=20):
     """The live shape end to end (tests/c/batcher_e2e.c): 16 KiB libuv reads of `conns`
     connections queued in the batcher, one device flush per round (stage, H2D,
-    decode_reads, D2H, on_message per connection); the same reads through the host decoder
+    decode_reads, D2H, on_message per connection), synchronous and asynchronous
+    (flush_async + poll on on_ready); the same reads through the host decoder
     on one core beside it.  PCIe- and host-memcpy-bound; recorded in DESIGN.md, never the
     metric."""
     exe = os.path.join(REPO, "tests", "c", "_build", "batcher_e2e")
     out = {}
-    for name, dev in (("device", local), ("host_1core", -1)):
+    for name, dev, asy in (("device", local, 0), ("device_async", local, 1), ("host_1core", -1, 0)):
         p = subprocess.run([exe, "--conns", str(conns), "--frames", str(frames), "--size",
                             str(size), "--flushes", str(flushes if dev >= 0 else 3),
-                            "--device", str(dev)], capture_output=True, text=True, timeout=600)
+                            "--device", str(dev), "--async", str(asy)],
+                           capture_output=True, text=True, timeout=600)
         out[name] = json.loads(p.stdout.strip().splitlines()[-1]) if p.returncode == 0 else \
             {"error": p.returncode, "stderr": p.stderr[-300:]}
     return out

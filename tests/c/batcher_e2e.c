@@ -7,10 +7,17 @@
  * reference-shaped CPU rate.  Prints one JSON line.
  *
  * --async 1: one flush_async per round (the loop's uv_check), so the device decodes round k
- * while the loop takes the reads of round k+1; the last round is flushed synchronously.
+ * while the loop takes the reads of round k+1; the last round is flushed synchronously.  The
+ * batcher's on_ready (a HIP host callback once a flush's results are in host memory) sets a
+ * flag the loop checks between connections' reads — what a uv_async_t does in a libuv loop,
+ * whose async handles run in the same poll phase as the read callbacks — and poll() then
+ * delivers that flush and starts the one flush_async asked for meanwhile.  The staging
+ * capacity is 1.4 rounds, so reads that arrive while a flush is pending join the queue
+ * instead of making submit_read wait.
  *
  *   batcher_e2e --conns N --frames M --size S --read R --flushes F --device D [--async 1]
  */
+#include <stdatomic.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -27,6 +34,12 @@ static int on_message(uvhttp_ws_connection_t* c, const char* d, size_t n, int op
     g_msgs++;
     g_bytes += n;
     return 0;
+}
+
+static atomic_int g_ready;
+static void on_ready(void* ctx) {
+    (void)ctx;
+    atomic_store(&g_ready, 1);
 }
 
 static double now_s(void) {
@@ -73,9 +86,13 @@ int main(int argc, char** argv) {
     uvhttp_ws_amd_batcher_config_init(&cfg);
     cfg.device = device;
     cfg.min_device_bytes = 0;
-    cfg.max_bytes = (uint64_t)conns * (slen + 64) + (1u << 20);
+    /* (async: 1.4 rounds — decode_reads' frame bound, max_bytes / 6 + connections < 2^26,
+     * caps one flush near 384 MiB) */
+    const uint64_t round = (uint64_t)conns * (slen + 64);
+    cfg.max_bytes = (async ? round + round * 2 / 5 : round) + (1u << 20);
     cfg.max_connections = (uint32_t)conns;
-    cfg.max_reads = (uint32_t)((size_t)conns * (slen / rd + 2));
+    cfg.max_reads = (uint32_t)((size_t)(async ? 2 : 1) * conns * (slen / rd + 2));
+    if (async) cfg.on_ready = on_ready;
     uvhttp_ws_amd_batcher_t* b = NULL;
     if (uvhttp_ws_amd_batcher_create(&cfg, &b) != 0) {
         fprintf(stderr, "batcher_create failed\n");
@@ -92,9 +109,15 @@ int main(int argc, char** argv) {
             t0 = now_s();
         }
         const double ts = now_s();
-        for (int c = 0; c < conns; ++c)
+        for (int c = 0; c < conns; ++c) {
             for (size_t o = 0; o < slen; o += rd)
                 if (uvhttp_ws_amd_batcher_submit_read(b, cs[c], stream + o, o + rd <= slen ? rd : slen - o)) return 2;
+            /* the loop's uv_async handle: a finished flush is delivered between reads */
+            if (async && atomic_load_explicit(&g_ready, memory_order_relaxed)) {
+                atomic_store(&g_ready, 0);
+                if (uvhttp_ws_amd_batcher_poll(b) < 0) return 3;
+            }
+        }
         const double tf = now_s();
         /* async: the loop's uv_async wake-up (poll) and uv_check (flush_async) */
         if (async && uvhttp_ws_amd_batcher_poll(b) < 0) return 3;

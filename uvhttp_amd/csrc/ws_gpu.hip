@@ -3213,6 +3213,8 @@ struct uvhttp_ws_gpu_engine {
     uint64_t wr_cap;
     int wr_rec_on;             // UVHTTP_WS_WALK_REC=0: k_stream_desc gathers every header (A/B)
     int walk_single_off;       // UVHTTP_WS_WALK_SINGLE=0: always walk twice (tests, A/B)
+    int time_chain;            // UVHTTP_WS_TIME_CHAIN=1: stream decode timing brackets the whole
+                               // kernel chain (walk .. payload), not only the payload kernel
     void* bs_mem;              // send-side output-map records (BuildRec per map tile)
     uint64_t bs_tiles;
     int build_small;           // emit shape for frames < 4 KiB (UVHTTP_WS_BUILD_SMALL, tuning)
@@ -3313,6 +3315,7 @@ int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out) {
     if (const char* wr = getenv("UVHTTP_WS_WALK_REC")) e->wr_rec_on = atoi(wr) != 0;
     if (const char* wm = getenv("UVHTTP_WS_WALK"))
         e->walk_mode = strcmp(wm, "lane") == 0 ? 1 : strcmp(wm, "wave") == 0 ? 2 : 0;
+    if (const char* tc = getenv("UVHTTP_WS_TIME_CHAIN")) e->time_chain = atoi(tc) != 0;
     *out = e;
     return UVHTTP_WS_GPU_OK;
 }
@@ -3870,6 +3873,7 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     // a wave per connection when the waves fill the chip in about one round, else a lane
     // (UVHTTP_WS_WALK=lane|wave pins it)
     const bool wave_walk = e->walk_mode ? e->walk_mode == 2 : n_streams <= 16384;
+    const int tk_chain = e->time_chain ? timing_begin(e, s) : -1;
     if (wave_walk) {
         if (w.single) hipLaunchKernelGGL(k_swalk_wave<2>, dim3(nwb), dim3(kBlock), 0, s, w);
         else hipLaunchKernelGGL(k_swalk_wave<0>, dim3(nwb), dim3(kBlock), 0, s, w);
@@ -3911,7 +3915,7 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     const uint64_t tile_bytes = (uint64_t)blk * vpt * 16;
     const uint64_t n_ptiles = (wire_len + tile_bytes - 1) / tile_bytes;
     const uint64_t max_tiles = (1ull << 24);
-    const int tk = timing_begin(e, s);
+    const int tk = e->time_chain ? -1 : timing_begin(e, s);
     for (uint64_t tb = 0; tb < n_ptiles; tb += max_tiles) {
         const uint32_t grid_p = (uint32_t)((n_ptiles - tb) < max_tiles ? (n_ptiles - tb) : max_tiles);
 #define UVWS_LAUNCH(B, V)                                                                        \
@@ -3928,6 +3932,7 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
 #undef UVWS_LAUNCH
     }
     timing_end(e, tk, s);
+    timing_end(e, tk_chain, s);
     const hipError_t h = hipGetLastError();
     if (prev != e->device) (void)hipSetDevice(prev);
     if (h != hipSuccess) return set_err(e, UVHTTP_WS_GPU_ELAUNCH, "launch", h);
