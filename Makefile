@@ -11,7 +11,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Iinclude -Wall -Werror 
             -mcode-object-version=5
 CFLAGS := -O2 -DNDEBUG -fPIC -std=gnu11 -Iinclude -Wall -Wextra -Werror
 
-all: $(LIB) oracle ctests
+all: $(LIB) oracle ctests probes
 
 $(BUILD)/ws_gpu.o: uvhttp_amd/csrc/ws_gpu.hip include/uvhttp_ws_amd.h
 	@mkdir -p $(BUILD)
@@ -41,6 +41,13 @@ oracle:
 ctests: $(LIB) oracle
 	$(MAKE) -C tests/c
 
+# measurement tools run on the GPU box (PCIe ceilings beside the live-shape e2e)
+probes: tools/bin/pcie_probe
+
+tools/bin/pcie_probe: tools/pcie_probe.hip
+	@mkdir -p tools/bin
+	$(HIPCC) --offload-arch=$(ARCH) -O2 -o $@ $<
+
 asm: uvhttp_amd/csrc/ws_gpu.hip uvhttp_amd/csrc/tls_gpu.hip
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -Wno-unused-command-line-argument --cuda-device-only -S -o $(BUILD)/ws_gpu.s uvhttp_amd/csrc/ws_gpu.hip
@@ -51,4 +58,4 @@ clean:
 	$(MAKE) -C oracle clean
 	$(MAKE) -C tests/c clean
 
-.PHONY: all oracle ctests clean asm
+.PHONY: all oracle ctests probes clean asm

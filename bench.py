@@ -341,6 +341,7 @@ class GpuWorkload:
         _, plen, frag, mm = CONFIGS[cfg]
         first, n, passes = shard_plan(cfg, rank, world)
         self.plen, self.n, self.passes, self.mode, self.mm = plen, n, passes, mode, mm
+        self.use_graph = bool(getattr(args, "graph", False))
         self.stride = stride = U.gen_frame_stride(plen)
         self.wire_len = wire_len = stride * n
         self.eng = eng = U.GpuEngine(local)
@@ -358,6 +359,7 @@ class GpuWorkload:
             self.msgs = torch.empty(n * 32, dtype=torch.uint8, device=dev)
         eng.reserve(n, wire_len, n * plen if self.arena is not None else 0)
         self.build_dev = self.streams_dev = None
+        self.graph = None
         self.kernel = {"compact": "k_gather_compact", "build": "kb_emit",
                        "build_masked": "kb_emit"}.get(mode, "k_unmask_inplace")
         # in place, a batch of equal-stride small frames takes the fused path (ws_gpu.hip
@@ -417,8 +419,29 @@ class GpuWorkload:
                                msgs=self.msgs, summary=self.summ, stream=stream)
 
     def step(self):
+        if self.graph is not None:
+            self.graph.replay()
+            return
         for _ in range(self.passes):
             self.one_pass()
+
+    def capture(self):
+        """--graph: one step captured as a HIP graph (torch.cuda.CUDAGraph), replayed per step —
+        one submission per step instead of one per kernel.  The engine's calls see a capturing
+        stream (ws_gpu.hip call_begin: device-side epochs, no timing events), so the roofline
+        then has no kernel time; used to tell dispatch-path idle from kernel time."""
+        t = self.torch
+        self.sync()
+        cs = t.cuda.Stream()
+        g = t.cuda.CUDAGraph()
+        old = self.stream
+        self.stream = cs
+        with t.cuda.graph(g, stream=cs):
+            for _ in range(self.passes):
+                self.one_pass()
+        self.stream = old
+        self.graph = g
+        self.sync()
 
     def sync(self):
         self.torch.cuda.synchronize()
@@ -479,6 +502,9 @@ def timed_run(wl, steps, warmup, world):
     for _ in range(warmup):
         wl.step()
     wl.sync()
+    if getattr(wl, "use_graph", False):
+        wl.capture()
+        wl.step()
     wl.check()
     wl.kernel_time()  # discard warmup events
     wl.set_timing(True)
@@ -538,6 +564,8 @@ def main():
     ap.add_argument("--rotate", type=int, default=1,
                     help="decode R copies of the batch round-robin (cold-cache rates)")
     ap.add_argument("--no-ceiling", action="store_true", help="skip the copy-ceiling timing")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay each step as one captured HIP graph (diagnostic: no kernel timing)")
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)  # launcher tests
     args = ap.parse_args()
 
@@ -642,6 +670,8 @@ def main():
             out["spawned_from_gpu_process"] = os.environ["UVHTTP_WS_SPAWNED_FROM_GPU_PROCESS"] == "1"
         if args.rotate > 1:
             out["config"]["rotate"] = args.rotate
+        if args.graph:
+            out["config"]["graph"] = True
         if world == 1 and not args.no_cpu_baseline and not args.stub:
             out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
         out.update(extra)
@@ -666,6 +696,17 @@ def e2e_live(local, conns=1024, frames=4, size=65536, flushes=20):
                            capture_output=True, text=True, timeout=600)
         out[name] = json.loads(p.stdout.strip().splitlines()[-1]) if p.returncode == 0 else \
             {"error": p.returncode, "stderr": p.stderr[-300:]}
+    # the PCIe ceiling of this box for the same bytes (tools/pcie_probe.hip): one flush's wire up
+    # and down; the live shape cannot beat batcher_shape_ms per 256 MiB round
+    probe = os.path.join(REPO, "tools", "bin", "pcie_probe")
+    if os.path.exists(probe):
+        p = subprocess.run([probe, "256", "2"], capture_output=True, text=True, timeout=300)
+        if p.returncode == 0:
+            pc = json.loads(p.stdout.strip().splitlines()[-1])
+            wire = conns * frames * (size + (10 if size >= 65536 else 4 if size >= 126 else 2) + 4)
+            pc["ceiling_GiBs_for_this_payload"] = round(
+                conns * frames * size / (pc["batcher_shape_ms"] / 1e3 * wire / pc["bytes"]) / GIB, 2)
+            out["pcie"] = pc
     return out
 
 
