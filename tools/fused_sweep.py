@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Fused stride path vs k_plan-first path (UVHTTP_WS_FUSED=0), interleaved in one process,
 over frame sizes: the whole in-place decode step (torch events around K steps) per size.
-Sets the automatic choice in run_decode (kFusedMaxAvg).
+Sets the automatic choice in run_decode (kFusedMaxAvg); FUSED_TILES=BxV,... adds fused
+engines with those payload tiles (UVHTTP_WS_FUSED_TILE).
 
   python tools/fused_sweep.py [plen,plen,...] [rounds]
 """
@@ -34,8 +35,12 @@ def main():
         [50, 120, 250, 500, 1000, 2000, 4000, 8000, 16000]
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
     K = 20
-    engs = {"fused": engine({"UVHTTP_WS_FUSED": "1", "UVHTTP_WS_FUSED_MAX": "1099511627776"}),
-            "plan_first": engine({"UVHTTP_WS_FUSED": "0"})}
+    engs = {"fused": engine({"UVHTTP_WS_FUSED": "1", "UVHTTP_WS_FUSED_MAX": "1099511627776"})}
+    # FUSED_TILES=256x4,512x4: the fused path with those payload tiles too (UVHTTP_WS_FUSED_TILE)
+    for t in filter(None, os.environ.get("FUSED_TILES", "").split(",")):
+        engs["fused_" + t] = engine({"UVHTTP_WS_FUSED": "1", "UVHTTP_WS_FUSED_MAX": "1099511627776",
+                                     "UVHTTP_WS_FUSED_TILE": t})
+    engs["plan_first"] = engine({"UVHTTP_WS_FUSED": "0"})
     st = torch.cuda.current_stream()
     for plen in plens:
         stride = U.gen_frame_stride(plen)

@@ -1218,7 +1218,9 @@ __global__ __launch_bounds__(BLOCK) void k_unmask_inplace(
 constexpr uint64_t kFusedMinStride = 64;
 // above this many wire bytes per frame the headers are few and the k_plan-first path is
 // faster (its payload pass overlaps the descriptor lookup with the loads; tools/fused_sweep.py,
-// profiles/r03p8_fused_sweep.txt: fused wins by 7 us at 2 KiB frames, loses by 4 at 3 KiB)
+// profiles/r03p8_fused_sweep.txt: fused wins by 7 us at 2 KiB frames, loses by 4 at 3 KiB).
+// 16 KiB fused tiles made the sweep favour fusing up to 8 KiB (r03p35_fused_tiles.txt), but
+// the C2 bench itself (4 KiB frames) lost 5 % fused: 2217-2255 vs 2357-2367 GiB/s (r03p36)
 constexpr uint64_t kFusedMaxAvg = 2560;
 
 template <int BLOCK, int VPT>
@@ -3213,6 +3215,8 @@ struct uvhttp_ws_gpu_engine {
     uint64_t wr_cap;
     int wr_rec_on;             // UVHTTP_WS_WALK_REC=0: k_stream_desc gathers every header (A/B)
     int walk_single_off;       // UVHTTP_WS_WALK_SINGLE=0: always walk twice (tests, A/B)
+    int fused_block, fused_vpt;  // UVHTTP_WS_FUSED_TILE=BxV: the fused payload pass's tile (A/B)
+    uint32_t fixup_blocks;     // k_fixup grid cap (UVHTTP_WS_FIXUP_BLOCKS, A/B)
     int time_chain;            // UVHTTP_WS_TIME_CHAIN=1: stream decode timing brackets the whole
                                // kernel chain (walk .. payload), not only the payload kernel
     void* bs_mem;              // send-side output-map records (BuildRec per map tile)
@@ -3316,6 +3320,16 @@ int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out) {
     if (const char* wm = getenv("UVHTTP_WS_WALK"))
         e->walk_mode = strcmp(wm, "lane") == 0 ? 1 : strcmp(wm, "wave") == 0 ? 2 : 0;
     if (const char* tc = getenv("UVHTTP_WS_TIME_CHAIN")) e->time_chain = atoi(tc) != 0;
+    e->fixup_blocks = 1024;
+    if (const char* fx = getenv("UVHTTP_WS_FIXUP_BLOCKS")) e->fixup_blocks = (uint32_t)strtoul(fx, nullptr, 10);
+    if (e->fixup_blocks == 0) e->fixup_blocks = 1;
+    if (const char* ft = getenv("UVHTTP_WS_FUSED_TILE")) {
+        int fb = 0, fv = 0;
+        if (sscanf(ft, "%dx%d", &fb, &fv) == 2) {
+            e->fused_block = fb;
+            e->fused_vpt = fv;
+        }
+    }
     *out = e;
     return UVHTTP_WS_GPU_OK;
 }
@@ -3646,11 +3660,18 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
     if (fused) {
         a.recs = reinterpret_cast<FrameRec*>(e->ws.recs);
         a.stride_inv = 1.0 / (double)b->frame_stride;
+        // 16 KiB tiles at every fused frame size: the tile's LDS staging, parse and barriers
+        // are paid per tile, so the fused pass wants larger tiles than the plain payload
+        // kernel (r03p34: 256x4 97.9 us on C4, 256x2 112.6, 64x1 182.7; r03p35: 32 KiB tiles
+        // lose, 256x8 +16 %, 512x4 +5 %)
         int fb = e->tile_block, fv = e->tile_vpt;
-        const uint64_t favg = b->wire_len / a.n;
         if (!fb) {
-            fb = favg >= 32768 ? 64 : 256;
-            fv = favg >= 32768 ? 1 : favg >= 2048 ? 2 : 4;
+            fb = 256;
+            fv = 4;
+        }
+        if (e->fused_block) {
+            fb = e->fused_block;
+            fv = e->fused_vpt;
         }
         const uint64_t ft = (uint64_t)fb * fv * 16;
         const uint64_t f_tiles = (b->wire_len + ft - 1) / ft;
@@ -3661,7 +3682,11 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
 #define UVWS_FUSED(B, V) \
     if (fb == B && fv == V) hipLaunchKernelGGL((k_unmask_stride<B, V>), dim3(grid_p), dim3(B), 0, s, a, tb); else
             UVWS_FUSED(64, 1) UVWS_FUSED(64, 2) UVWS_FUSED(64, 4) UVWS_FUSED(128, 1)
-            UVWS_FUSED(128, 2) UVWS_FUSED(256, 1) UVWS_FUSED(256, 2) UVWS_FUSED(256, 4) {}
+            UVWS_FUSED(128, 2) UVWS_FUSED(256, 1) UVWS_FUSED(256, 2) UVWS_FUSED(256, 4)
+            UVWS_FUSED(256, 8) UVWS_FUSED(512, 4) UVWS_FUSED(512, 8) {
+                if (prev != e->device) (void)hipSetDevice(prev);
+                return set_err(e, UVHTTP_WS_GPU_EINVAL, "unsupported fused tile shape", hipSuccess);
+            }
 #undef UVWS_FUSED
         }
         timing_end(e, ftk, s);
@@ -3677,7 +3702,8 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
                                d_msgs, e->ws);
         }
         const uint32_t fx = (a.n + kBlock - 1) / kBlock;
-        hipLaunchKernelGGL(k_fixup, dim3(fx < 1024 ? fx : 1024), dim3(kBlock), 0, s, a, d_desc, e->ws);
+        hipLaunchKernelGGL(k_fixup, dim3(fx < e->fixup_blocks ? fx : e->fixup_blocks), dim3(kBlock), 0, s,
+                           a, d_desc, e->ws);
         hipError_t hf = hipGetLastError();
         if (prev != e->device) (void)hipSetDevice(prev);
         if (hf != hipSuccess) return set_err(e, UVHTTP_WS_GPU_ELAUNCH, "launch", hf);
