@@ -37,9 +37,27 @@ static int on_message(uvhttp_ws_connection_t* c, const char* d, size_t n, int op
 }
 
 static atomic_int g_ready;
+/* --trace 1: a timeline of the loop's batcher calls and the on_ready wake-ups (stderr) */
+static int g_trace;
+static double g_t0;
+static double now_s(void);
+#define TRACE_MAX 4096
+static struct { double t; char what; int a, b; } g_ev[TRACE_MAX];
+static atomic_int g_nev;
+static void trace(char what, int a, int b) {
+    if (!g_trace) return;
+    const int k = atomic_fetch_add(&g_nev, 1);
+    if (k < TRACE_MAX) {
+        g_ev[k].t = now_s();
+        g_ev[k].what = what;
+        g_ev[k].a = a;
+        g_ev[k].b = b;
+    }
+}
 static void on_ready(void* ctx) {
     (void)ctx;
     atomic_store(&g_ready, 1);
+    trace('R', 0, 0);
 }
 
 static double now_s(void) {
@@ -59,6 +77,7 @@ int main(int argc, char** argv) {
         else if (!strcmp(argv[i], "--flushes")) flushes = atoi(argv[i + 1]);
         else if (!strcmp(argv[i], "--device")) device = atoi(argv[i + 1]);
         else if (!strcmp(argv[i], "--async")) async = atoi(argv[i + 1]);
+        else if (!strcmp(argv[i], "--trace")) g_trace = atoi(argv[i + 1]);
     }
     /* one connection's stream: M masked BINARY frames of S bytes (every connection sends
      * the same bytes; keys differ per frame) */
@@ -107,21 +126,36 @@ int main(int argc, char** argv) {
             g_msgs = g_bytes = 0;
             uvhttp_ws_amd_batcher_stats(b, &st0);
             t0 = now_s();
+            g_t0 = t0;
         }
         const double ts = now_s();
+        uvhttp_ws_amd_batcher_stats_t sx;
+        uvhttp_ws_amd_batcher_stats(b, &sx);
+        trace('S', it, (int)sx.async_flushes);
         for (int c = 0; c < conns; ++c) {
             for (size_t o = 0; o < slen; o += rd)
                 if (uvhttp_ws_amd_batcher_submit_read(b, cs[c], stream + o, o + rd <= slen ? rd : slen - o)) return 2;
             /* the loop's uv_async handle: a finished flush is delivered between reads */
             if (async && atomic_load_explicit(&g_ready, memory_order_relaxed)) {
                 atomic_store(&g_ready, 0);
-                if (uvhttp_ws_amd_batcher_poll(b) < 0) return 3;
+                const int pr = uvhttp_ws_amd_batcher_poll(b);
+                uvhttp_ws_amd_batcher_stats(b, &sx);
+                trace('P', pr, (int)sx.async_flushes);
+                if (pr < 0) return 3;
             }
         }
         const double tf = now_s();
+        trace('E', it, 0);
         /* async: the loop's uv_async wake-up (poll) and uv_check (flush_async) */
-        if (async && uvhttp_ws_amd_batcher_poll(b) < 0) return 3;
+        if (async) {
+            const int pr = uvhttp_ws_amd_batcher_poll(b);
+            uvhttp_ws_amd_batcher_stats(b, &sx);
+            trace('p', pr, (int)sx.async_flushes);
+            if (pr < 0) return 3;
+        }
         if ((async ? uvhttp_ws_amd_batcher_flush_async(b) : uvhttp_ws_amd_batcher_flush(b)) != 0) return 3;
+        uvhttp_ws_amd_batcher_stats(b, &sx);
+        trace('F', (int)sx.device_flushes, (int)sx.async_flushes);
         if (it >= 0) {
             t_submit += tf - ts;
             t_flush += now_s() - tf;
@@ -151,6 +185,14 @@ int main(int argc, char** argv) {
            (st.copy_ms - st0.copy_ms) / flushes, (st.upload_ms - st0.upload_ms) / flushes,
            (st.stage_ms - st0.stage_ms) / flushes, (st.wait_ms - st0.wait_ms) / flushes,
            (st.deliver_ms - st0.deliver_ms) / flushes);
+    if (g_trace) {
+        /* S = round starts (round, flushes started), E = its reads queued, P / p = poll on
+         * on_ready / after the round (result, flushes started), F = flush_async returned
+         * (flushes delivered, started), R = on_ready fired (HIP callback thread) */
+        const int ne = atomic_load(&g_nev) < TRACE_MAX ? atomic_load(&g_nev) : TRACE_MAX;
+        for (int k = 0; k < ne; ++k)
+            fprintf(stderr, "%9.3f ms  %c %d %d\n", (g_ev[k].t - g_t0) * 1e3, g_ev[k].what, g_ev[k].a, g_ev[k].b);
+    }
     uvhttp_ws_amd_batcher_free(b);
     for (int c = 0; c < conns; ++c) uvhttp_ws_connection_free(cs[c]);
     free(cs);

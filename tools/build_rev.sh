@@ -6,13 +6,19 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 REV=${1:?usage: build_rev.sh REV}
 TMP=$(mktemp -d)
 mkdir -p "$TMP/include" "$TMP/csrc" "$ROOT/tools/bin"
-git -C "$ROOT" show "$REV:include/uvhttp_ws_amd.h" > "$TMP/include/uvhttp_ws_amd.h"
-git -C "$ROOT" show "$REV:uvhttp_amd/csrc/ws_gpu.hip" > "$TMP/csrc/ws_gpu.hip"
-git -C "$ROOT" show "$REV:uvhttp_amd/csrc/ws_host.c" > "$TMP/csrc/ws_host.c"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I"$TMP/include" \
-  -mcode-object-version=5 -c -o "$TMP/ws_gpu.o" "$TMP/csrc/ws_gpu.hip"
+# every source of the library (the ctypes mirror binds all of its symbols)
+for h in uvhttp_ws_amd.h uvhttp_tls_amd.h; do
+  git -C "$ROOT" show "$REV:include/$h" > "$TMP/include/$h"
+done
+for f in ws_gpu.hip tls_gpu.hip ws_batcher.hip ws_host.c; do
+  git -C "$ROOT" show "$REV:uvhttp_amd/csrc/$f" > "$TMP/csrc/$f"
+done
+for f in ws_gpu tls_gpu ws_batcher; do
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I"$TMP/include" \
+    -mcode-object-version=5 -c -o "$TMP/$f.o" "$TMP/csrc/$f.hip"
+done
 gcc -O2 -DNDEBUG -fPIC -std=gnu11 -I"$TMP/include" -c -o "$TMP/ws_host.o" "$TMP/csrc/ws_host.c"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$ROOT/tools/bin/libws_$REV.so" \
-  "$TMP/ws_gpu.o" "$TMP/ws_host.o"
+  "$TMP/ws_gpu.o" "$TMP/tls_gpu.o" "$TMP/ws_batcher.o" "$TMP/ws_host.o"
 rm -rf "$TMP"
 echo "$ROOT/tools/bin/libws_$REV.so"

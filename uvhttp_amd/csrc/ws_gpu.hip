@@ -1223,14 +1223,49 @@ constexpr uint64_t kFusedMinStride = 64;
 // the C2 bench itself (4 KiB frames) lost 5 % fused: 2217-2255 vs 2357-2367 GiB/s (r03p36)
 constexpr uint64_t kFusedMaxAvg = 2560;
 
+// x / s for x < 2^24 (tile-relative offsets): a float reciprocal and one correction step
+__device__ inline uint32_t div_small(uint32_t x, uint32_t s, float inv_s) {
+    uint32_t q = (uint32_t)((float)x * inv_s);
+    if (q * s > x) --q;
+    else if ((q + 1) * s <= x) ++q;
+    return q;
+}
+
+// a payload bound relative to the tile start t0 as int32: far bounds are clamped to
+// [-64, kT + 64], a start keeping its value mod 4 (the key's byte phase for the tile's vectors)
+__device__ inline int32_t rel_clamp(uint64_t x, uint64_t t0, uint64_t kT, bool keep_phase) {
+    if (x < t0 && t0 - x > 64) {
+        const int32_t ph = keep_phase ? (int32_t)((t0 - x) & 3u) : 0;
+        return -64 - ph;  // (x - t0) mod 4 == (-ph) mod 4
+    }
+    if (x >= t0 + kT + 64) return (int32_t)(kT + 64);
+    return (int32_t)((int64_t)x - (int64_t)t0);
+}
+
+// add_mask on tile-relative int32 positions (vector at r, payload [ps, pe))
+__device__ inline void add_mask_rel(u32x4& m, int32_t r, int32_t ps, int32_t pe, uint32_t key) {
+    if (pe <= r || ps >= r + 16) return;
+    const uint32_t rk = rotr32(key, 8u * (uint32_t)((r - ps) & 3));
+    if (ps <= r && r + 16 <= pe) {
+        m = u32x4{rk, rk, rk, rk};
+        return;
+    }
+    const int lo = ps > r ? ps - r : 0;
+    const int hi = pe < r + 16 ? pe - r : 16;
+    m.x |= rk & lane_bytes(lo, hi, 0);
+    m.y |= rk & lane_bytes(lo, hi, 1);
+    m.z |= rk & lane_bytes(lo, hi, 2);
+    m.w |= rk & lane_bytes(lo, hi, 3);
+}
+
 template <int BLOCK, int VPT>
 __global__ __launch_bounds__(BLOCK) void k_unmask_stride(BatchArgs a, uint64_t tile_base) {
     constexpr uint64_t kT = (uint64_t)BLOCK * VPT * 16;
     constexpr int kMaxF = (int)(kT / kFusedMinStride) + 2;  // frames touching one tile
     __shared__ u32x4 s_tile[BLOCK * VPT + 1];               // the tile + the 16 bytes after
-    __shared__ uint64_t s_ps[kMaxF];
-    __shared__ uint64_t s_pe[kMaxF];
-    __shared__ uint32_t s_key[kMaxF];
+    // each frame's payload [ps, pe) relative to t0, clamped to int32 keeping ps mod 4 (the
+    // key's byte phase), and key: one 16-byte LDS entry, read with one ds_read_b128
+    __shared__ int4 s_fr[kMaxF];
     __shared__ u32x4 s_h0;                                  // header of the frame covering t0
 
     const uint64_t t0 = (tile_base + blockIdx.x) * kT;
@@ -1303,25 +1338,37 @@ __global__ __launch_bounds__(BLOCK) void k_unmask_stride(BatchArgs a, uint64_t t
         (void)parse_hdr(a, f, seg_info(a, f, n), o, hv, d);
         if (o >= t0) a.recs[f] = rec_of(d);  // (a frame that started earlier: its own tile)
         const bool ok = d.status == UVHTTP_WS_FRAME_OK;
-        s_ps[j] = d.payload_off;
-        s_pe[j] = d.payload_off + (ok ? d.payload_len : 0);
-        s_key[j] = d.masking_key;
+        s_fr[j] = int4{rel_clamp(d.payload_off, t0, kT, true),
+                       rel_clamp(d.payload_off + (ok ? d.payload_len : 0), t0, kT, false),
+                       (int32_t)d.masking_key, 0};
     }
     __syncthreads();
 
+    // a payload lies inside its frame's slot, so only frames jl..jh (relative to fbase) can
+    // touch the vector at tile offset r: frame of byte r = (r + d0) / S, d0 = t0 - obase.
+    // 32-bit tile-relative arithmetic (r + d0 + 15 < kT + 2 S; a tile at or past the last
+    // frame's start holds that frame alone, however far it reaches)
+    const bool last_only = fbase + 1 >= n;
+    const uint32_t S32 = (uint32_t)S;
+    const uint32_t d0 = last_only ? 0u : (uint32_t)(t0 - obase);
+    const float inv_s = 1.0f / (float)S32;
+    const uint32_t jmax = fb - fbase;
     u32x4 m[VPT];
 #pragma unroll
     for (int v = 0; v < VPT; ++v) {
         m[v] = u32x4{0, 0, 0, 0};
         if (va[v] >= vend) continue;
-        // a payload lies inside its frame's slot: only frames lo..hi can touch this vector
-        const uint64_t ql = div_stride(a, va[v]);
-        const uint32_t lo = (uint32_t)(ql < n ? ql : n - 1);
-        const uint64_t qh = div_stride(a, va[v] + 15);
-        const uint32_t hi = (uint32_t)(qh < fb ? qh : fb);
-        for (uint32_t f = lo; f <= hi; ++f) {
-            const uint32_t j = f - fbase;
-            add_mask(m[v], va[v], s_ps[j], s_pe[j], s_key[j]);
+        const uint32_t r = (uint32_t)((v * BLOCK + threadIdx.x) * 16);
+        uint32_t jl = 0, jh = 0;
+        if (!last_only) {
+            jl = div_small(r + d0, S32, inv_s);
+            jh = div_small(r + 15 + d0, S32, inv_s);
+            jl = jl < jmax ? jl : jmax;
+            jh = jh < jmax ? jh : jmax;
+        }
+        for (uint32_t j = jl; j <= jh; ++j) {
+            const int4 fr = s_fr[j];
+            add_mask_rel(m[v], (int32_t)r, fr.x, fr.y, (uint32_t)fr.z);
         }
     }
     const uint64_t room = vend > t0 ? vend - t0 : 0;
