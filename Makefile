@@ -42,11 +42,16 @@ ctests: $(LIB) oracle
 	$(MAKE) -C tests/c
 
 # measurement tools run on the GPU box (PCIe ceilings beside the live-shape e2e)
-probes: tools/bin/pcie_probe
+probes: tools/bin/pcie_probe tools/bin/copy_probe
 
 tools/bin/pcie_probe: tools/pcie_probe.hip
 	@mkdir -p tools/bin
 	$(HIPCC) --offload-arch=$(ARCH) -O2 -o $@ $<
+
+# host-only (HIP runtime API, no kernels): g++, so the AVX variants can use target attributes
+tools/bin/copy_probe: tools/copy_probe.cpp $(BUILD)/ws_host.o
+	@mkdir -p tools/bin
+	g++ -O2 -std=c++17 -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include -Iinclude -o $@ $^ -L$(ROCM)/lib -lamdhip64 -Wl,-rpath,$(ROCM)/lib
 
 asm: uvhttp_amd/csrc/ws_gpu.hip uvhttp_amd/csrc/tls_gpu.hip
 	@mkdir -p $(BUILD)

@@ -689,10 +689,12 @@ def e2e_live(local, conns=1024, frames=4, size=65536, flushes=20):
     metric."""
     exe = os.path.join(REPO, "tests", "c", "_build", "batcher_e2e")
     out = {}
+    # device runs: the loop thread on the GPU's NUMA node (--pin 1; INTEGRATION.md §3)
     for name, dev, asy in (("device", local, 0), ("device_async", local, 1), ("host_1core", -1, 0)):
         p = subprocess.run([exe, "--conns", str(conns), "--frames", str(frames), "--size",
                             str(size), "--flushes", str(flushes if dev >= 0 else 3),
-                            "--device", str(dev), "--async", str(asy)],
+                            "--device", str(dev), "--async", str(asy),
+                            "--pin", "1" if dev >= 0 else "0"],
                            capture_output=True, text=True, timeout=600)
         out[name] = json.loads(p.stdout.strip().splitlines()[-1]) if p.returncode == 0 else \
             {"error": p.returncode, "stderr": p.stderr[-300:]}

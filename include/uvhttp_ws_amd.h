@@ -660,6 +660,12 @@ uvhttp_error_t uvhttp_ws_amd_batcher_submit_tls_read(uvhttp_ws_amd_batcher_t* b,
                                                      const uint8_t* ciphertext, size_t len);
 int uvhttp_ws_amd_batcher_stats(const uvhttp_ws_amd_batcher_t* b,
                                 uvhttp_ws_amd_batcher_stats_t* out);
+/* NUMA node of the batcher's GPU (its PCI device's sysfs numa_node), or -1 (host-only batcher,
+ * or not known).  Run the loop thread that calls submit_read on this node: submit_read copies
+ * each read into pinned memory that HIP places next to the GPU, and on the MI355X box that copy
+ * ran at 91 GB/s from the GPU's node against 48 GB/s from the other socket — the live shape end
+ * to end 38 vs 22 GiB/s (profiles/r03p44_numa_copy_e2e.txt). */
+int uvhttp_ws_amd_batcher_numa_node(const uvhttp_ws_amd_batcher_t* b);
 
 /* Library identity, for the loader checks in tests/. */
 const char* uvhttp_ws_amd_version(void);

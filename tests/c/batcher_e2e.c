@@ -11,12 +11,13 @@
  * batcher's on_ready (a HIP host callback once a flush's results are in host memory) sets a
  * flag the loop checks between connections' reads — what a uv_async_t does in a libuv loop,
  * whose async handles run in the same poll phase as the read callbacks — and poll() then
- * delivers that flush and starts the one flush_async asked for meanwhile.  The staging
- * capacity is 1.4 rounds, so reads that arrive while a flush is pending join the queue
- * instead of making submit_read wait.
+ * delivers that flush and starts the one flush_async asked for meanwhile.
  *
  *   batcher_e2e --conns N --frames M --size S --read R --flushes F --device D [--async 1]
+ *               [--pin 1: loop thread on the GPU's NUMA node] [--trace 1]
  */
+#define _GNU_SOURCE
+#include <sched.h>
 #include <stdatomic.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -67,7 +68,8 @@ static double now_s(void) {
 }
 
 int main(int argc, char** argv) {
-    int conns = 1024, frames = 4, flushes = 20, device = 0, async = 0;
+    int conns = 1024, frames = 4, flushes = 20, device = 0, async = 0, pin = 0;
+    double cap_rounds = 1.0;
     size_t size = 65536, rd = 16384;
     for (int i = 1; i + 1 < argc; i += 2) {
         if (!strcmp(argv[i], "--conns")) conns = atoi(argv[i + 1]);
@@ -78,6 +80,8 @@ int main(int argc, char** argv) {
         else if (!strcmp(argv[i], "--device")) device = atoi(argv[i + 1]);
         else if (!strcmp(argv[i], "--async")) async = atoi(argv[i + 1]);
         else if (!strcmp(argv[i], "--trace")) g_trace = atoi(argv[i + 1]);
+        else if (!strcmp(argv[i], "--pin")) pin = atoi(argv[i + 1]);
+        else if (!strcmp(argv[i], "--cap")) cap_rounds = atof(argv[i + 1]);
     }
     /* one connection's stream: M masked BINARY frames of S bytes (every connection sends
      * the same bytes; keys differ per frame) */
@@ -105,10 +109,14 @@ int main(int argc, char** argv) {
     uvhttp_ws_amd_batcher_config_init(&cfg);
     cfg.device = device;
     cfg.min_device_bytes = 0;
-    /* (async: 1.4 rounds — decode_reads' frame bound, max_bytes / 6 + connections < 2^26,
-     * caps one flush near 384 MiB) */
+    /* staging capacity in rounds (--cap, default 1): with 1 a read that arrives while the
+     * previous flush is still on the device waits for it at the round boundary (backpressure),
+     * so every flush carries one round; above 1 the waiting queue absorbs the next round's
+     * first reads, and when the loop outruns PCIe the flushes grow, each D2H gets longer and
+     * the queue overflows mid-round anyway (1.4: 21.5 vs 24+ GiB/s, r03p45).  decode_reads'
+     * frame bound (max_bytes / 6 + connections < 2^26) caps a flush near 384 MiB. */
     const uint64_t round = (uint64_t)conns * (slen + 64);
-    cfg.max_bytes = (async ? round + round * 2 / 5 : round) + (1u << 20);
+    cfg.max_bytes = (uint64_t)((double)round * cap_rounds) + (1u << 20);
     cfg.max_connections = (uint32_t)conns;
     cfg.max_reads = (uint32_t)((size_t)(async ? 2 : 1) * conns * (slen / rd + 2));
     if (async) cfg.on_ready = on_ready;
@@ -116,6 +124,28 @@ int main(int argc, char** argv) {
     if (uvhttp_ws_amd_batcher_create(&cfg, &b) != 0) {
         fprintf(stderr, "batcher_create failed\n");
         return 1;
+    }
+    /* --pin 1: the loop thread onto the GPU's NUMA node (uvhttp_ws_amd_batcher_numa_node), as
+     * INTEGRATION.md §3 asks of a server */
+    const int node = uvhttp_ws_amd_batcher_numa_node(b);
+    int pinned = -1;
+    if (pin && node >= 0) {
+        char path[96], list[4096];
+        snprintf(path, sizeof(path), "/sys/devices/system/node/node%d/cpulist", node);
+        FILE* f = fopen(path, "r");
+        if (f && fgets(list, sizeof(list), f)) {
+            cpu_set_t set;
+            CPU_ZERO(&set);
+            for (char* p = list; *p && *p != '\n';) {
+                char* e;
+                long lo = strtol(p, &e, 10), hi = lo;
+                if (*e == '-') hi = strtol(e + 1, &e, 10);
+                for (long c = lo; c <= hi && c < CPU_SETSIZE; ++c) CPU_SET((int)c, &set);
+                p = (*e == ',') ? e + 1 : e;
+            }
+            if (sched_setaffinity(0, sizeof(set), &set) == 0) pinned = node;
+        }
+        if (f) fclose(f);
     }
     double t0 = 0, t_submit = 0, t_flush = 0;
     uvhttp_ws_amd_batcher_stats_t st0;
@@ -172,7 +202,8 @@ int main(int argc, char** argv) {
            "\"frames_per_conn\": %d, \"payload\": %zu, \"read\": %zu, \"flushes\": %d, "
            "\"ms_per_flush\": %.3f, \"messages_ok\": %d, \"device_flushes\": %llu, "
            "\"device_ms_total\": %.1f, \"async\": %d, \"submit_ms_per_flush\": %.3f, "
-           "\"flush_call_ms_per_flush\": %.3f, \"blocked_ms_per_flush\": %.3f, "
+           "\"flush_call_ms_per_flush\": %.3f, \"blocked_ms_per_flush\": %.3f, \"gpu_numa_node\": %d, \"pinned_node\": %d, "
+           "\"host_flushes\": %llu, \"fallback_flushes\": %llu, \"capacity_flushes\": %llu, \"device_errors\": %llu, "
            "\"max_blocked_ms\": %.3f, \"per_flush_ms\": {\"copy\": %.3f, \"upload\": %.3f, "
            "\"stage\": %.3f, \"wait\": %.3f, \"deliver\": %.3f}}\n",
            device >= 0 ? "device batcher (stage, H2D, decode_reads, D2H, deliver)"
@@ -181,7 +212,11 @@ int main(int argc, char** argv) {
            el * 1e3 / flushes, g_msgs == (uint64_t)conns * frames * flushes,
            (unsigned long long)(st.device_flushes - st0.device_flushes), st.device_ms - st0.device_ms,
            async, t_submit * 1e3 / flushes, t_flush * 1e3 / flushes,
-           (st.blocked_ms - st0.blocked_ms) / flushes, st.max_blocked_ms,
+           (st.blocked_ms - st0.blocked_ms) / flushes, node, pinned,
+           (unsigned long long)(st.host_flushes - st0.host_flushes),
+           (unsigned long long)(st.fallback_flushes - st0.fallback_flushes),
+           (unsigned long long)(st.capacity_flushes - st0.capacity_flushes),
+           (unsigned long long)(st.device_errors - st0.device_errors), st.max_blocked_ms,
            (st.copy_ms - st0.copy_ms) / flushes, (st.upload_ms - st0.upload_ms) / flushes,
            (st.stage_ms - st0.stage_ms) / flushes, (st.wait_ms - st0.wait_ms) / flushes,
            (st.deliver_ms - st0.deliver_ms) / flushes);

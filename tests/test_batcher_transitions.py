@@ -256,3 +256,62 @@ def test_capacity_and_device_failure_fall_back_to_host():
     for p in pairs:
         p.check(b, L)
     b.close()
+
+
+def test_numa_node_host_only_is_unknown():
+    """uvhttp_ws_amd_batcher_numa_node: a host-only batcher has no GPU node (-1)"""
+    import uvhttp_amd as U
+    b = U.Batcher(device=-1)
+    assert b.numa_node() == -1
+    b.close()
+
+
+@pytest.mark.gpu
+def test_numa_node_of_the_device():
+    """the device batcher reports its GPU's NUMA node from sysfs (or -1 where sysfs has none);
+    the value matches the PCI device's numa_node file"""
+    import glob
+    import uvhttp_amd as U
+    b = U.Batcher(device=0, min_device_bytes=0)
+    node = b.numa_node()
+    nodes = {int(open(f).read()) for f in glob.glob("/sys/class/drm/card*/device/numa_node")}
+    assert node == -1 or node in nodes
+    b.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [5, 6])
+def test_async_split_frames_stay_on_the_device(seed):
+    """The live shape's async loop with a staging capacity of about one round: a flush cuts
+    frames of the next round in two, and the connections' next reads are queued while that
+    flush is still in flight.  Their recv-buffer prefix at staging time must be accounted from
+    the in-flight reads too (prefix_bound), or the queue outgrows the device layout and falls
+    back to the host decoder.  No fallback, and every transcript equals the oracle's."""
+    import uvhttp_amd as U
+    rng = random.Random(seed)
+    pairs = []
+    for _ in range(12):
+        frames, _ = _frames(rng, 6, False, bad=False)  # complete, valid frames
+        data = b"".join(frames)
+        pairs.append(Pair(U, rng, mf=16 * 1024 * 1024, mm=64 * 1024 * 1024,
+                          reads=[data[i:i + 4096] for i in range(0, len(data), 4096)]))
+    per_round = sum(len(r) for p in pairs for r in p.reads) // 3
+    b = U.Batcher(device=0, min_device_bytes=0, max_bytes=per_round + 64 * 1024)
+    while any(p.next < len(p.reads) for p in pairs):
+        for _ in range(len(pairs)):
+            p = rng.choice(pairs)
+            for _ in range(rng.randint(1, 6)):
+                if p.next < len(p.reads):
+                    p.feed(b, p.reads[p.next])
+                    p.next += 1
+            if b.in_flight() and rng.random() < 0.5:
+                assert b.poll() in (0, 1)
+        assert b.flush_async() == 0
+    assert b.flush() == 0
+    st = b.stats()
+    assert st["fallback_flushes"] == 0 and st["host_flushes"] == 0, st
+    assert st["device_flushes"] >= 2
+    L = _oracle.load()
+    for p in pairs:
+        p.check(b, L)
+    b.close()

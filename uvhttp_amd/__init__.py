@@ -268,6 +268,7 @@ def load_library(path: str) -> C.CDLL:
                                                            vp, C.c_size_t]),
         "uvhttp_ws_amd_batcher_forget": (None, [vp, C.POINTER(WsConnectionStruct)]),
         "uvhttp_ws_amd_batcher_stats": (C.c_int, [vp, C.POINTER(BatcherStats)]),
+        "uvhttp_ws_amd_batcher_numa_node": (C.c_int, [vp]),
         # TLS record layer (include/uvhttp_tls_amd.h)
         "uvhttp_tls_gpu_engine_create": (C.c_int, [C.c_int, C.POINTER(vp)]),
         "uvhttp_tls_gpu_engine_free": (None, [vp]),
@@ -790,6 +791,10 @@ class Batcher:
         s = BatcherStats()
         self._L.uvhttp_ws_amd_batcher_stats(self.h, C.byref(s))
         return s.as_dict()
+
+    def numa_node(self) -> int:
+        """uvhttp_ws_amd_batcher_numa_node: the GPU's NUMA node (-1: host-only or unknown)"""
+        return self._L.uvhttp_ws_amd_batcher_numa_node(self.h)
 
     def close(self):
         if getattr(self, "h", None):

@@ -36,6 +36,7 @@
 #include "uvhttp_ws_amd.h"
 
 extern "C" void uvhttp_ws_amd_copy_stream(void* dst, const void* src, size_t len);  // ws_host.c
+extern "C" void uvhttp_ws_amd_copy_fence(void);  // ws_host.c: streaming stores -> visible to DMA
 
 // TLS connections (uvhttp_ws_amd_batcher_set_tls): a queue's TLS connections are laid out
 // after the plain ones in the device wire as ciphertext (the previous flushes' unconsumed
@@ -338,6 +339,7 @@ void clear_queue(BatchQueue& q) {
 // device batcher: the arena bytes not yet sent go to HBM on the upload stream
 void upload_tail(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
     if (q.arena_len > q.uploaded) {
+        uvhttp_ws_amd_copy_fence();  // the reads' streaming stores before the DMA engine reads them
         (void)hipMemcpyAsync(q.d_arena + q.uploaded, q.h_arena + q.uploaded,
                              q.arena_len - q.uploaded, hipMemcpyHostToDevice, b->up);
         q.uploaded = q.arena_len;
@@ -964,6 +966,21 @@ int uvhttp_ws_amd_batcher_flush(uvhttp_ws_amd_batcher_t* b) {
 
 namespace {
 
+// The recv-buffer prefix a connection will have when the accumulating queue is staged: what it
+// holds now, plus — while the queue in flight still has reads of it — at most those bytes (its
+// delivery leaves their unconsumed tail in recv_buffer).  Accounting with the current size alone
+// let a queue outgrow the device layout once a flush had cut a frame in two (the async live shape
+// then fell back to the host decoder for 3-6 of 20 flushes, r03p47).
+uint64_t prefix_bound(const uvhttp_ws_amd_batcher_t* b, const uvhttp_ws_connection_t* conn) {
+    uint64_t pos = conn->recv_buffer_pos;
+    const BatchQueue& other = b->q[b->cur ^ 1];
+    if (other.in_flight) {
+        const auto it = other.slot_of.find(const_cast<uvhttp_ws_connection_t*>(conn));
+        if (it != other.slot_of.end()) pos += other.slots[it->second].bytes;
+    }
+    return pos;
+}
+
 // queue one read (plain bytes, or a TLS connection's ciphertext)
 uvhttp_error_t queue_read(uvhttp_ws_amd_batcher_t* b, uvhttp_ws_connection_t* conn,
                           const uint8_t* data, size_t len, bool tls) {
@@ -973,7 +990,7 @@ uvhttp_error_t queue_read(uvhttp_ws_amd_batcher_t* b, uvhttp_ws_connection_t* co
     bool fresh = it == q->slot_of.end();
     if (!fresh && q->slots[it->second].tls != tls) return UVHTTP_ERROR_INVALID_PARAM;
     const uint64_t carry = tls ? kTlsCarryMax : 0;
-    const uint64_t pre = align16(conn->recv_buffer_pos) + 16 + carry;
+    const uint64_t pre = align16(prefix_bound(b, conn)) + 16 + carry;
     const uint64_t need = (uint64_t)len + (fresh ? pre : 0);
     if (q->staged + need > b->cfg.max_bytes || q->reads.size() + 1 > b->cfg.max_reads ||
         (fresh && q->slots.size() + 1 > b->cfg.max_connections)) {
@@ -984,7 +1001,7 @@ uvhttp_error_t queue_read(uvhttp_ws_amd_batcher_t* b, uvhttp_ws_connection_t* co
         (void)start_flush(b, true);  // (a device error there was decoded on the host and counted)
         if (b->failed.count(conn)) return UVHTTP_ERROR_INVALID_PARAM;
         if (tls && !b->tls.count(conn)) return UVHTTP_ERROR_INVALID_PARAM;  // handed back
-        const uint64_t pre2 = align16(conn->recv_buffer_pos) + 16 + carry;
+        const uint64_t pre2 = align16(prefix_bound(b, conn)) + 16 + carry;
         if (pre2 + len > b->cfg.max_bytes) {
             if (tls) {
                 // ciphertext can be cut anywhere (records reassemble across flushes): queue it
@@ -1115,6 +1132,22 @@ void uvhttp_ws_amd_batcher_forget(uvhttp_ws_amd_batcher_t* b, struct uvhttp_ws_c
         // the arena, unreferenced)
         if (i == b->cur) q.slot_of.erase(it);
     }
+}
+
+int uvhttp_ws_amd_batcher_numa_node(const uvhttp_ws_amd_batcher_t* b) {
+    if (!b || !b->eng) return -1;
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, (int)sizeof(bus) - 1, b->cfg.device) != hipSuccess) return -1;
+    for (char* c = bus; *c; ++c)
+        if (*c >= 'A' && *c <= 'F') *c = (char)(*c - 'A' + 'a');  // sysfs spells hex in lower case
+    char path[160];
+    snprintf(path, sizeof(path), "/sys/bus/pci/devices/%s/numa_node", bus);
+    FILE* f = fopen(path, "r");
+    if (!f) return -1;
+    int node = -1;
+    if (fscanf(f, "%d", &node) != 1) node = -1;
+    fclose(f);
+    return node;
 }
 
 int uvhttp_ws_amd_batcher_stats(const uvhttp_ws_amd_batcher_t* b,

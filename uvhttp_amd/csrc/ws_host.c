@@ -434,18 +434,37 @@ uvhttp_error_t uvhttp_ws_deliver_stream(struct uvhttp_ws_connection* c, const ui
 }
 
 /* Copy of a read into the batcher's pinned arena (ws_batcher.hip; internal).  The arena is
- * only read again by the DMA engine, so whole 16-byte vectors go out with non-temporal stores:
- * no read-for-ownership of the destination lines, no cache pollution (glibc memcpy switches
- * to streaming stores only far above libuv's 16 KiB reads). */
-#include <emmintrin.h>
-__attribute__((visibility("hidden"))) void uvhttp_ws_amd_copy_stream(void* dst, const void* src,
-                                                                     size_t len) {
-    uint8_t* d = (uint8_t*)dst;
-    const uint8_t* s = (const uint8_t*)src;
-    if (len < 1024) {
-        memcpy(d, s, len);
-        return;
+ * only read again by the DMA engine, so whole vectors go out with non-temporal stores: no
+ * read-for-ownership of the destination lines, no cache pollution (glibc memcpy switches to
+ * streaming stores only far above libuv's 16 KiB reads).  32-byte AVX2 streaming stores where
+ * the CPU has them: 91 GB/s into pinned memory on the MI355X box's EPYC 9575F against 54-59 GB/s
+ * for 16-byte SSE2 ones and 45 GB/s for memcpy (tools/copy_probe.cpp,
+ * profiles/r03p42_copy_probe.jsonl). */
+#include <immintrin.h>
+
+__attribute__((target("avx2"))) static void copy_stream_avx2(uint8_t* d, const uint8_t* s, size_t len) {
+    const size_t head = (32u - ((uintptr_t)d & 31u)) & 31u;
+    memcpy(d, s, head);
+    d += head;
+    s += head;
+    len -= head;
+    size_t i = 0;
+    for (; i + 128 <= len; i += 128) {
+        const __m256i a = _mm256_loadu_si256((const __m256i*)(s + i));
+        const __m256i b = _mm256_loadu_si256((const __m256i*)(s + i + 32));
+        const __m256i c = _mm256_loadu_si256((const __m256i*)(s + i + 64));
+        const __m256i e = _mm256_loadu_si256((const __m256i*)(s + i + 96));
+        _mm256_stream_si256((__m256i*)(d + i), a);
+        _mm256_stream_si256((__m256i*)(d + i + 32), b);
+        _mm256_stream_si256((__m256i*)(d + i + 64), c);
+        _mm256_stream_si256((__m256i*)(d + i + 96), e);
     }
+    for (; i + 32 <= len; i += 32)
+        _mm256_stream_si256((__m256i*)(d + i), _mm256_loadu_si256((const __m256i*)(s + i)));
+    memcpy(d + i, s + i, len - i);
+}
+
+static void copy_stream_sse2(uint8_t* d, const uint8_t* s, size_t len) {
     const size_t head = (16u - ((uintptr_t)d & 15u)) & 15u;
     memcpy(d, s, head);
     d += head;
@@ -464,6 +483,25 @@ __attribute__((visibility("hidden"))) void uvhttp_ws_amd_copy_stream(void* dst, 
     }
     for (; i + 16 <= len; i += 16)
         _mm_stream_si128((__m128i*)(d + i), _mm_loadu_si128((const __m128i*)(s + i)));
-    _mm_sfence();
     memcpy(d + i, s + i, len - i);
+}
+
+/* The streaming stores of copy_stream are weakly ordered: make them visible before a DMA engine
+ * reads the arena (the batcher calls this before each H2D of it).  One fence per upload, not one
+ * per 16 KiB read: a fence per call cost a third of the copy rate (58.8 vs 91 GB/s,
+ * profiles/r03p44_numa_copy_e2e.txt). */
+__attribute__((visibility("hidden"))) void uvhttp_ws_amd_copy_fence(void) { _mm_sfence(); }
+
+__attribute__((visibility("hidden"))) void uvhttp_ws_amd_copy_stream(void* dst, const void* src,
+                                                                     size_t len) {
+    static int have_avx2 = -1;
+    if (len < 1024) {
+        memcpy(dst, src, len);
+        return;
+    }
+    if (have_avx2 < 0) have_avx2 = __builtin_cpu_supports("avx2") ? 1 : 0;
+    if (have_avx2)
+        copy_stream_avx2((uint8_t*)dst, (const uint8_t*)src, len);
+    else
+        copy_stream_sse2((uint8_t*)dst, (const uint8_t*)src, len);
 }
