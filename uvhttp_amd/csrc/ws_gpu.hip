@@ -3355,7 +3355,7 @@ int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out) {
     // step against 144-145 for reduce-then-scan, profiles/r03p6_*); UVHTTP_WS_REC_SCAN=3pass
     e->rec_lookback = 1;
     e->plan_wide = 0;  // 1024-thread blocks measured slower on C4 (1690 vs 1785 GiB/s, r03p7)
-    if (const char* pw = getenv("UVHTTP_WS_PLAN_WIDE")) e->plan_wide = atoi(pw) != 0;
+    if (const char* pw = getenv("UVHTTP_WS_PLAN_WIDE")) e->plan_wide = atoi(pw);
     if (const char* rs = getenv("UVHTTP_WS_REC_SCAN")) e->rec_lookback = strcmp(rs, "3pass") != 0;
     e->build_frames_max = 4096;
     if (const char* bf = getenv("UVHTTP_WS_BUILD_FRAMES")) e->build_frames_max = strtoull(bf, nullptr, 10);
@@ -3622,6 +3622,16 @@ static void launch_plan(uvhttp_ws_gpu_engine_t* e, BatchArgs& a, uint32_t n_cap,
         while (fpt < 16 && ((uint64_t)n_cap + kBlock * fpt - 1) / (kBlock * fpt) > max_blocks) fpt *= 2;
     }
     a.no_ticket = e->plan_no_ticket;
+    if (a.recs && e->plan_wide >= 2) {
+        // records, A/B (UVHTTP_WS_PLAN_WIDE=2 / 3): 512-thread blocks, 8 or 16 frames per lane
+        const int f5 = e->plan_wide == 3 ? 16 : 8;
+        const uint32_t per5 = 512u * (uint32_t)f5;
+        a.plan_frames = per5;
+        const uint32_t g5 = n_cap ? (n_cap + per5 - 1) / per5 : 1;
+        if (f5 == 8) hipLaunchKernelGGL((k_plan<8, 512>), dim3(g5), dim3(512), 0, s, a, d_desc, d_msgs, e->ws);
+        else hipLaunchKernelGGL((k_plan<16, 512>), dim3(g5), dim3(512), 0, s, a, d_desc, d_msgs, e->ws);
+        return;
+    }
     if (a.recs && e->plan_wide) {
         // records: 1024-thread blocks, so the per-lane state-machine chain is 4x shorter at
         // the same block count (occupancy 4 waves / SIMD instead of 1)
