@@ -117,3 +117,15 @@ def test_host_decoder_fuzz_under_asan_ubsan(built, seed):
                        capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr[-4000:]
     assert "clean" in p.stdout
+
+
+@pytest.mark.parametrize("sse2", ["0", "1"])
+def test_batcher_read_copy_under_asan_ubsan(built, sse2):
+    """the batcher's read copy into its pinned arena (ws_host.c uvhttp_ws_amd_copy_stream: AVX2
+    or SSE2 streaming stores, one fence per upload) equals memcpy at every length / alignment
+    tried and writes nothing outside the destination (tests/c/copy_check.c)"""
+    exe = os.path.join(BUILD, "copy_check")
+    p = subprocess.run([exe], env=dict(os.environ, UVHTTP_WS_COPY_SSE2=sse2),
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert p.stdout.startswith("ok")
