@@ -27,9 +27,10 @@ def torch():
     return t
 
 
-@pytest.fixture(scope="module", params=["lane", "wave", "wave-norec", "wave-twopass"])
+@pytest.fixture(scope="module", params=["lane", "lane-twopass", "wave", "wave-norec", "wave-twopass"])
 def eng(torch, request):
-    """Every frame-discovery walk (a lane per connection; a wave per connection, single pass
+    """Every frame-discovery walk (a lane per connection, single pass or two walks; a wave per
+    connection, single pass
     through the offset scratch — with the fast path's frame records or re-reading every header
     in k_stream_desc — or the two-walk fallback) must decode alike."""
     import os

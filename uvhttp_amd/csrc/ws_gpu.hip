@@ -3915,9 +3915,16 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     if (prev != e->device) (void)hipSetDevice(e->device);
     hipStream_t s = (hipStream_t)stream;
 
+    // a wave per connection when the waves fill the chip in about one round, else a lane
+    // (UVHTTP_WS_WALK=lane|wave pins it)
+    const bool wave_walk = e->walk_mode ? e->walk_mode == 2 : n_streams <= 16384;
+    // single pass (starts written into per-connection slices) unless UVHTTP_WS_WALK_SINGLE=0.
+    // (The idle between calls of some C2 stream runs, DESIGN.md §5, is not the slices: with
+    // the lane walk in two passes and no slice scratch, 2 of 10 runs idled all the same, r03p51.)
+    const bool single_ok = e->walk_single_off == 0;
     // slices: connection s's starts at walk_tmp[begin / 2 + s ...] (4-byte entries)
     const uint64_t want = wire_len / 2 + n_streams + 1;
-    if (e->walk_single_off == 0 && !e->capturing && want * 4 <= (8ull << 30) && want > e->wt_cap) {
+    if (single_ok && !e->capturing && want * 4 <= (8ull << 30) && want > e->wt_cap) {
         if (e->wt_mem) (void)hipFree(e->wt_mem);
         e->wt_mem = nullptr;
         e->wt_cap = 0;
@@ -3925,7 +3932,8 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     }
     // the wave walk's frame records (8 bytes per slice entry) while slices and records stay
     // within 8 GiB together; larger calls gather every header again in k_stream_desc
-    if (e->walk_single_off == 0 && !e->capturing && want * 12 <= (8ull << 30) && want > e->wr_cap) {
+    // (only the wave walk writes and reads them: none for the lane walk — 1 GB less for C2)
+    if (single_ok && wave_walk && !e->capturing && want * 12 <= (8ull << 30) && want > e->wr_cap) {
         if (e->wr_mem) (void)hipFree(e->wr_mem);
         e->wr_mem = nullptr;
         e->wr_cap = 0;
@@ -3939,7 +3947,7 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     w.max_frames = max_frames;
     w.read_end = d_read_end;
     w.n_reads_total = n_reads_total;
-    w.single = (e->walk_single_off == 0 && e->wt_cap >= want) ? 1u : 0u;
+    w.single = (single_ok && e->wt_cap >= want) ? 1u : 0u;
     w.results = d_results;
     w.desc = d_desc;
     w.tile_first = e->ws.tile_first;
@@ -3953,9 +3961,6 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     w.agg = e->ss.agg;
     const uint32_t nsb = (n_streams + kBlock - 1) / kBlock;
     const uint32_t nwb = (n_streams + kBlock / 64 - 1) / (kBlock / 64);
-    // a wave per connection when the waves fill the chip in about one round, else a lane
-    // (UVHTTP_WS_WALK=lane|wave pins it)
-    const bool wave_walk = e->walk_mode ? e->walk_mode == 2 : n_streams <= 16384;
     const int tk_chain = e->time_chain ? timing_begin(e, s) : -1;
     if (wave_walk) {
         if (w.single) hipLaunchKernelGGL(k_swalk_wave<2>, dim3(nwb), dim3(kBlock), 0, s, w);
