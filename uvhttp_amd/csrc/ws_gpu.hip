@@ -1258,7 +1258,7 @@ __device__ inline void add_mask_rel(u32x4& m, int32_t r, int32_t ps, int32_t pe,
     m.w |= rk & lane_bytes(lo, hi, 3);
 }
 
-template <int BLOCK, int VPT>
+template <int BLOCK, int VPT, int AUX = 18>
 __global__ __launch_bounds__(BLOCK) void k_unmask_stride(BatchArgs a, uint64_t tile_base) {
     constexpr uint64_t kT = (uint64_t)BLOCK * VPT * 16;
     constexpr int kMaxF = (int)(kT / kFusedMinStride) + 2;  // frames touching one tile
@@ -1380,7 +1380,7 @@ __global__ __launch_bounds__(BLOCK) void k_unmask_stride(BatchArgs a, uint64_t t
             const u32x4 x = data[v] ^ m[v];
             __builtin_amdgcn_raw_buffer_store_b128(
                 __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, x), rs,
-                (uint32_t)(va[v] - t0), 0, 18);
+                (uint32_t)(va[v] - t0), 0, AUX);
         }
     }
     if (full_end != vend && full_end >= t0 && full_end < t0 + kT) {
@@ -3264,6 +3264,7 @@ struct uvhttp_ws_gpu_engine {
     int walk_single_off;       // UVHTTP_WS_WALK_SINGLE=0: always walk twice (tests, A/B)
     int fused_block, fused_vpt;  // UVHTTP_WS_FUSED_TILE=BxV: the fused payload pass's tile (A/B)
     uint32_t fixup_blocks;     // k_fixup grid cap (UVHTTP_WS_FIXUP_BLOCKS, A/B)
+    int fused_aux;             // fused payload stores' cache-policy bits (UVHTTP_WS_FUSED_AUX, A/B)
     int time_chain;            // UVHTTP_WS_TIME_CHAIN=1: stream decode timing brackets the whole
                                // kernel chain (walk .. payload), not only the payload kernel
     void* bs_mem;              // send-side output-map records (BuildRec per map tile)
@@ -3367,6 +3368,8 @@ int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out) {
     if (const char* wm = getenv("UVHTTP_WS_WALK"))
         e->walk_mode = strcmp(wm, "lane") == 0 ? 1 : strcmp(wm, "wave") == 0 ? 2 : 0;
     if (const char* tc = getenv("UVHTTP_WS_TIME_CHAIN")) e->time_chain = atoi(tc) != 0;
+    e->fused_aux = 18;
+    if (const char* fa = getenv("UVHTTP_WS_FUSED_AUX")) e->fused_aux = atoi(fa);
     e->fixup_blocks = 1024;
     if (const char* fx = getenv("UVHTTP_WS_FIXUP_BLOCKS")) e->fixup_blocks = (uint32_t)strtoul(fx, nullptr, 10);
     if (e->fixup_blocks == 0) e->fixup_blocks = 1;
@@ -3736,8 +3739,17 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
         const int ftk = timing_begin(e, s);
         for (uint64_t tb = 0; tb < f_tiles; tb += f_max) {
             const uint32_t grid_p = (uint32_t)((f_tiles - tb) < f_max ? (f_tiles - tb) : f_max);
-#define UVWS_FUSED(B, V) \
-    if (fb == B && fv == V) hipLaunchKernelGGL((k_unmask_stride<B, V>), dim3(grid_p), dim3(B), 0, s, a, tb); else
+#define UVWS_FUSED(B, V)                                                                         \
+    if (fb == B && fv == V) {                                                                    \
+        if (B == 256 && V == 4 && e->fused_aux == 2)                                             \
+            hipLaunchKernelGGL((k_unmask_stride<256, 4, 2>), dim3(grid_p), dim3(B), 0, s, a, tb);  \
+        else if (B == 256 && V == 4 && e->fused_aux == 0)                                        \
+            hipLaunchKernelGGL((k_unmask_stride<256, 4, 0>), dim3(grid_p), dim3(B), 0, s, a, tb);  \
+        else if (B == 256 && V == 4 && e->fused_aux == 16)                                       \
+            hipLaunchKernelGGL((k_unmask_stride<256, 4, 16>), dim3(grid_p), dim3(B), 0, s, a, tb); \
+        else                                                                                     \
+            hipLaunchKernelGGL((k_unmask_stride<B, V>), dim3(grid_p), dim3(B), 0, s, a, tb);      \
+    } else
             UVWS_FUSED(64, 1) UVWS_FUSED(64, 2) UVWS_FUSED(64, 4) UVWS_FUSED(128, 1)
             UVWS_FUSED(128, 2) UVWS_FUSED(256, 1) UVWS_FUSED(256, 2) UVWS_FUSED(256, 4)
             UVWS_FUSED(256, 8) UVWS_FUSED(512, 4) UVWS_FUSED(512, 8) {
