@@ -529,7 +529,7 @@ __device__ inline void resolve_one(const BatchArgs& a, uvhttp_ws_message_desc_t*
     // 0 also owns the bytes before its start); the max-of-tag claim keeps the smallest frame
     // when a bad offset table makes slots overlap.  (The fused stride path's payload pass
     // finds frames by arithmetic: no tile map.)
-    if (!a.recs) {
+    if (!a.recs || a.arena) {  // (compact decodes: k_scatter_compact reads this map too)
         const uint64_t o = frame_start(a, i);
         uint64_t end = (i + 1 < n) ? frame_start(a, i + 1) : a.wire_len;
         if (end > a.wire_len) end = a.wire_len;
@@ -1342,6 +1342,8 @@ __global__ __launch_bounds__(BLOCK) void k_unmask_stride(BatchArgs a, uint64_t t
                        rel_clamp(d.payload_off + (ok ? d.payload_len : 0), t0, kT, false),
                        (int32_t)d.masking_key, 0};
     }
+    // AUX < 0: the records-only pass of a compact stride decode (the wire stays masked)
+    if constexpr (AUX < 0) return;
     __syncthreads();
 
     // a payload lies inside its frame's slot, so only frames jl..jh (relative to fbase) can
@@ -1380,7 +1382,7 @@ __global__ __launch_bounds__(BLOCK) void k_unmask_stride(BatchArgs a, uint64_t t
             const u32x4 x = data[v] ^ m[v];
             __builtin_amdgcn_raw_buffer_store_b128(
                 __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, x), rs,
-                (uint32_t)(va[v] - t0), 0, AUX);
+                (uint32_t)(va[v] - t0), 0, AUX < 0 ? 0 : AUX);
         }
     }
     if (full_end != vend && full_end >= t0 && full_end < t0 + kT) {
@@ -3265,6 +3267,7 @@ struct uvhttp_ws_gpu_engine {
     int fused_block, fused_vpt;  // UVHTTP_WS_FUSED_TILE=BxV: the fused payload pass's tile (A/B)
     uint32_t fixup_blocks;     // k_fixup grid cap (UVHTTP_WS_FIXUP_BLOCKS, A/B)
     int fused_aux;             // fused payload stores' cache-policy bits (UVHTTP_WS_FUSED_AUX, A/B)
+    int compact_recs;          // compact stride batches: records pass + k_plan on records
     int time_chain;            // UVHTTP_WS_TIME_CHAIN=1: stream decode timing brackets the whole
                                // kernel chain (walk .. payload), not only the payload kernel
     void* bs_mem;              // send-side output-map records (BuildRec per map tile)
@@ -3368,6 +3371,8 @@ int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out) {
     if (const char* wm = getenv("UVHTTP_WS_WALK"))
         e->walk_mode = strcmp(wm, "lane") == 0 ? 1 : strcmp(wm, "wave") == 0 ? 2 : 0;
     if (const char* tc = getenv("UVHTTP_WS_TIME_CHAIN")) e->time_chain = atoi(tc) != 0;
+    e->compact_recs = 0;  // (UVHTTP_WS_COMPACT_RECS=1: under evaluation)
+    if (const char* cr = getenv("UVHTTP_WS_COMPACT_RECS")) e->compact_recs = atoi(cr) != 0;
     e->fused_aux = 18;
     if (const char* fa = getenv("UVHTTP_WS_FUSED_AUX")) e->fused_aux = atoi(fa);
     e->fixup_blocks = 1024;
@@ -3777,6 +3782,25 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
         if (prev != e->device) (void)hipSetDevice(prev);
         if (hf != hipSuccess) return set_err(e, UVHTTP_WS_GPU_ELAUNCH, "launch", hf);
         return UVHTTP_WS_GPU_OK;
+    }
+    // compact stride batches of small frames: a records-only pass over the wire (linear reads;
+    // k_plan's scattered header gather costs as much as reading everything),
+    // then k_plan on the records (UVHTTP_WS_COMPACT_RECS=1; off by default)
+    const uint64_t cavg = a.n ? b->wire_len / a.n : 0;
+    const bool rec_compact = arena && e->compact_recs && !b->frame_off && a.n > 0 &&
+                             cavg <= e->fused_max_avg && cavg < kScatterAvg && e->compact_mode != 1 &&
+                             b->frame_stride >= kFusedMinStride && b->wire_len > 0 &&
+                             b->wire_len < (1ull << 52) &&
+                             (uint64_t)(a.n - 1) <= (b->wire_len - 1) / b->frame_stride;
+    if (rec_compact) {
+        a.recs = reinterpret_cast<FrameRec*>(e->ws.recs);
+        a.stride_inv = 1.0 / (double)b->frame_stride;
+        constexpr uint64_t kRt = 256ull * 4 * 16;
+        const uint64_t r_tiles = (b->wire_len + kRt - 1) / kRt;
+        for (uint64_t tb = 0; tb < r_tiles; tb += (1ull << 24)) {
+            const uint32_t grid_r = (uint32_t)((r_tiles - tb) < (1ull << 24) ? (r_tiles - tb) : (1ull << 24));
+            hipLaunchKernelGGL((k_unmask_stride<256, 4, -1>), dim3(grid_r), dim3(256), 0, s, a, tb);
+        }
     }
     launch_plan(e, a, a.n, d_desc, d_msgs, s);
     // payload kernel tile shape: explicit (set_tile) or by average wire bytes per frame
