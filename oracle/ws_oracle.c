@@ -95,6 +95,7 @@ void oracle_apply_mask(uint8_t* data, size_t len, const uint8_t* key) {
 enum { EV_MESSAGE = 1, EV_CLOSE = 2, EV_PONG = 3, EV_CLOSE_ECHO = 4 };
 
 typedef void (*orc_unmask_hook)(void* ctx, const uint8_t* payload, uint64_t len, int opcode);
+struct orc_conn_frame;
 
 typedef struct {
     int is_server;
@@ -120,7 +121,22 @@ typedef struct {
     int last_msg_opcode;
     orc_unmask_hook hook;
     void* hook_ctx;
+    /* harness: bytes drained from the front of recv_buffer by completed frames over the
+     * connection's life (stream offset of recv_buffer[0]) and a per-completed-frame hook */
+    uint64_t consumed;
+    void (*frame_hook)(void* ctx, struct orc_conn_frame* f);
+    void* frame_ctx;
 } orc_conn_t;
+
+/* harness: one completed frame as the frame hook sees it (before recv_buffer is drained) */
+typedef struct orc_conn_frame {
+    uint64_t stream_off;     /* stream offset of the frame's first header byte */
+    uint64_t payload_len;
+    const uint8_t* payload;  /* unmasked payload inside recv_buffer (NULL if empty) */
+    uint32_t key;            /* masking key bytes k0..k3, k0 = low byte (0 if unmasked) */
+    uint8_t opcode, fin, mask, header_size;
+    int msg_end;             /* this data frame delivered a message (on_message fired) */
+} orc_conn_frame_t;
 
 /* :71-109 (defaults include/uvhttp_defaults.h:171-194) */
 orc_conn_t* oracle_conn_new(int is_server, int max_frame_size, int max_message_size,
@@ -314,6 +330,7 @@ int oracle_process_data(orc_conn_t* c, const uint8_t* data, size_t len) {
             }
         }
         if (c->hook) c->hook(c->hook_ctx, payload, h.payload_length, h.opcode);
+        const uint64_t msgs_before = c->n_messages; /* harness (frame hook) */
 
         if (h.opcode <= 0x2) { /* TEXT / BINARY / CONTINUATION, :950-1015 */
             if (c->frag == NULL) {
@@ -369,6 +386,23 @@ int oracle_process_data(orc_conn_t* c, const uint8_t* data, size_t len) {
             if (c->has_wrapper) ev_push(c, EV_PONG, 0xA, payload, h.payload_length);
         }
         /* PONG and reserved opcodes: nothing (:1085) */
+
+        if (c->frame_hook) { /* harness: the frame is complete; recv_buffer not yet drained */
+            orc_conn_frame_t f;
+            f.stream_off = c->consumed;
+            f.payload_len = h.payload_length;
+            f.payload = payload;
+            f.key = h.mask ? (uint32_t)c->rbuf[hs] | (uint32_t)c->rbuf[hs + 1] << 8 |
+                                 (uint32_t)c->rbuf[hs + 2] << 16 | (uint32_t)c->rbuf[hs + 3] << 24
+                           : 0;
+            f.opcode = h.opcode;
+            f.fin = h.fin;
+            f.mask = h.mask;
+            f.header_size = (uint8_t)hs;
+            f.msg_end = c->n_messages != msgs_before;
+            c->frame_hook(c->frame_ctx, &f);
+        }
+        c->consumed += total;
 
         size_t rem = c->rbuf_pos - total; /* :1087-1093 */
         if (rem) memmove(c->rbuf, c->rbuf + total, rem);
@@ -610,6 +644,125 @@ uint64_t oracle_stream_decode(const uint8_t* wire, uint64_t len, size_t chunk,
     if (digest) *digest = c->digest;
     oracle_conn_free(c);
     return bytes;
+}
+
+/* ---- stream driver: the device stream contract of include/uvhttp_ws_amd.h ---------------- */
+/* Many connections, each fed its process_data calls (src/uvhttp_connection.c:1128-1164:
+ * one call per read until a call fails) — the checker of uvhttp_ws_gpu_decode_streams /
+ * _decode_reads at any size.  Layouts == uvhttp_ws_stream_t (64 B). */
+typedef struct {
+    uint64_t begin, len, recv_buffer_size, pending_bytes;
+    int32_t pending_opcode, max_frame_size, max_message_size, is_server;
+    uint32_t first_read, n_reads;
+    uint64_t reserved;
+} orc_stream_t;
+
+/* per connection: what its process_data calls returned and left (64 B) */
+typedef struct {
+    uint32_t n_frames;      /* frames completed (delivered) */
+    uint32_t calls;         /* calls that ran, a failing one included */
+    int32_t rc;             /* the last call's return */
+    int32_t reason;         /* R_* of the failure (0 if none) */
+    uint64_t consumed;      /* bytes drained by completed frames */
+    uint64_t recv_pos;      /* bytes left in recv_buffer */
+    uint64_t recv_size;
+    uint64_t frag_size;     /* open fragmented message (0 = none) */
+    int32_t frag_opcode;
+    uint32_t n_messages;
+    uint64_t digest;        /* FNV-1a 64 over delivered message bytes (pending prefix = zeros;
+                               only when asked: it is a byte-serial loop) */
+} orc_stream_out_t;
+
+/* per completed frame, connections in order (32 B) */
+typedef struct {
+    uint64_t payload_off;   /* absolute wire offset of the payload */
+    uint64_t payload_len;
+    uint32_t key;
+    uint8_t opcode, flags, header_size, reserved; /* flags: 1 FIN, 2 MASK, 0x20 MSG_END */
+    uint32_t conn;
+    uint32_t wire_len;
+} orc_stream_frame_t;
+
+typedef struct {
+    uint8_t* wire;          /* delivered payloads are written back unmasked here */
+    uint64_t begin;
+    orc_stream_frame_t* frames;
+    uint64_t cap, n;
+    uint32_t conn;
+} orc_stream_ctx_t;
+
+static void stream_frame_hook(void* vctx, orc_conn_frame_t* f) {
+    orc_stream_ctx_t* x = (orc_stream_ctx_t*)vctx;
+    const uint64_t poff = x->begin + f->stream_off + f->header_size + (f->mask ? 4 : 0);
+    if (f->payload_len && f->payload) memcpy(x->wire + poff, f->payload, (size_t)f->payload_len);
+    if (x->n < x->cap) {
+        orc_stream_frame_t* o = &x->frames[x->n];
+        o->payload_off = poff;
+        o->payload_len = f->payload_len;
+        o->key = f->key;
+        o->opcode = f->opcode;
+        o->flags = (uint8_t)((f->fin ? 1 : 0) | (f->mask ? 2 : 0) | (f->msg_end ? 0x20 : 0));
+        o->header_size = f->header_size;
+        o->reserved = 0;
+        o->conn = x->conn;
+        uint64_t wl = f->header_size + (f->mask ? 4 : 0) + f->payload_len;
+        o->wire_len = wl > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)wl;
+    }
+    x->n++;
+}
+
+/* Returns the number of completed frames over all connections (frames beyond max_frames
+ * are counted, not stored).  wire is decoded in place like the device's stream decode. */
+uint64_t oracle_decode_streams(uint8_t* wire, const orc_stream_t* s, uint32_t n,
+                               const uint64_t* read_end, orc_stream_out_t* out,
+                               orc_stream_frame_t* frames, uint64_t max_frames, int digest) {
+    orc_stream_ctx_t x;
+    memset(&x, 0, sizeof(x));
+    x.wire = wire;
+    x.frames = frames;
+    x.cap = frames ? max_frames : 0;
+    for (uint32_t k = 0; k < n; ++k) {
+        const orc_stream_t* st = &s[k];
+        orc_stream_out_t* o = &out[k];
+        memset(o, 0, sizeof(*o));
+        orc_conn_t* c = oracle_conn_new(st->is_server, st->max_frame_size, st->max_message_size, 0);
+        if (!c) abort();
+        c->digest_on = digest;
+        if (oracle_conn_set_recv_state(c, (size_t)st->recv_buffer_size, NULL, 0) != ORC_OK) abort();
+        if (st->pending_bytes) { /* an open fragmented message from earlier calls (zeros) */
+            c->frag = (uint8_t*)calloc(1, (size_t)st->pending_bytes);
+            if (!c->frag) abort();
+            c->frag_size = c->frag_cap = (size_t)st->pending_bytes;
+            c->frag_opcode = st->pending_opcode;
+        }
+        x.begin = st->begin;
+        x.conn = k;
+        uint64_t before = x.n;
+        c->frame_hook = stream_frame_hook;
+        c->frame_ctx = &x;
+        uint32_t nr = st->n_reads ? st->n_reads : 1;
+        uint64_t pos = 0;
+        for (uint32_t r = 0; r < nr; ++r) {
+            uint64_t end = st->n_reads ? read_end[st->first_read + r] : st->len;
+            o->calls++;
+            o->rc = oracle_process_data(c, wire + st->begin + pos, (size_t)(end - pos));
+            pos = end;
+            if (o->rc != ORC_OK) {
+                o->reason = c->last_reason;
+                break;
+            }
+        }
+        o->n_frames = (uint32_t)(x.n - before);
+        o->consumed = c->consumed;
+        o->recv_pos = c->rbuf_pos;
+        o->recv_size = c->rbuf_size;
+        o->frag_size = oracle_conn_frag_size(c);
+        o->frag_opcode = c->frag_opcode;
+        o->n_messages = (uint32_t)c->n_messages;
+        o->digest = c->digest;
+        oracle_conn_free(c);
+    }
+    return x.n;
 }
 
 /* ---- send side: uvhttp_ws_build_frame (:204-285) --------------------------------------- */

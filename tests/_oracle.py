@@ -72,6 +72,7 @@ def load():
         "oracle_gen_plain": (None, [vp, u32, u64, u64]),
         "oracle_unmask_frames": (u64, [vp, u32, u64]),
         "oracle_stream_decode": (u64, [vp, u64, sz, C.c_int, C.c_int, C.POINTER(u64)]),
+        "oracle_decode_streams": (u64, [vp, vp, u32, vp, vp, vp, u64, C.c_int]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -221,6 +222,41 @@ def decode_batch(wire: np.ndarray, n_frames, stride=None, offsets=None, wire_len
     nm = sd["n_messages"]
     return dict(wire=w, arena=arena, status=status[:n_frames], summary=sd,
                 msg_off=msg_off[:nm], msg_len=msg_len[:nm], msg_opcode=msg_op[:nm])
+
+
+STREAM_DT = np.dtype([("begin", "<u8"), ("len", "<u8"), ("recv_buffer_size", "<u8"),
+                      ("pending_bytes", "<u8"), ("pending_opcode", "<i4"),
+                      ("max_frame_size", "<i4"), ("max_message_size", "<i4"),
+                      ("is_server", "<i4"), ("first_read", "<u4"), ("n_reads", "<u4"),
+                      ("reserved", "<u8")])
+STREAM_OUT_DT = np.dtype([("n_frames", "<u4"), ("calls", "<u4"), ("rc", "<i4"), ("reason", "<i4"),
+                          ("consumed", "<u8"), ("recv_pos", "<u8"), ("recv_size", "<u8"),
+                          ("frag_size", "<u8"), ("frag_opcode", "<i4"), ("n_messages", "<u4"),
+                          ("digest", "<u8")])
+STREAM_FRAME_DT = np.dtype([("payload_off", "<u8"), ("payload_len", "<u8"), ("key", "<u4"),
+                            ("opcode", "u1"), ("flags", "u1"), ("header_size", "u1"),
+                            ("reserved", "u1"), ("conn", "<u4"), ("wire_len", "<u4")])
+assert STREAM_DT.itemsize == 64 and STREAM_OUT_DT.itemsize == 64
+assert STREAM_FRAME_DT.itemsize == 32
+
+
+def decode_streams(wire: np.ndarray, streams: np.ndarray, read_end=None, max_frames=None,
+                   digest=False):
+    """Oracle of uvhttp_ws_gpu_decode_streams / _decode_reads: every connection fed its
+    process_data calls (one per read, until a call fails).  `wire` (uint8) is decoded IN
+    PLACE (completed frames' payloads unmasked).  -> (per-connection outcomes STREAM_OUT_DT,
+    completed frames STREAM_FRAME_DT in connection order)."""
+    L = load()
+    assert wire.dtype == np.uint8 and wire.flags.c_contiguous
+    st = np.ascontiguousarray(streams).view(STREAM_DT)
+    n = st.size
+    re = None if read_end is None else np.ascontiguousarray(read_end, dtype=np.uint64)
+    out = np.zeros(max(1, n), STREAM_OUT_DT)
+    cap = max_frames if max_frames is not None else 0
+    frames = np.zeros(max(1, cap), STREAM_FRAME_DT)
+    total = L.oracle_decode_streams(_ptr(wire), _ptr(st), n, _ptr(re), _ptr(out),
+                                    _ptr(frames) if cap else None, cap, 1 if digest else 0)
+    return out[:n], frames[:min(total, cap)], int(total)
 
 
 def gen_frames(n_frames, payload_len, seed, opcode0=2, fragmented=False, force_keys=False,

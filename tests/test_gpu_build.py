@@ -156,3 +156,26 @@ def test_build_then_decode_roundtrip(torch, eng):
     for i, f in enumerate(frames):
         got = w[d[i]["payload_off"]:d[i]["payload_off"] + d[i]["payload_len"]]
         assert np.array_equal(got, src[f["payload_off"]:f["payload_off"] + f["payload_len"]])
+
+
+# uvhttp_server_ws_broadcast (src/uvhttp_server.c:1626-1657) sends ONE payload to every open
+# connection through uvhttp_ws_send_text -> uvhttp_ws_send_frame (src/uvhttp_websocket.c:
+# 509-531, 595-600): a TEXT frame, FIN set, masked only when the connection is a client's.
+# As a batch that is n descriptors over the same source bytes.
+@pytest.mark.parametrize("plen,n", [(1, 5000), (125, 2048), (126, 3000), (1000, 4096),
+                                    (4096, 16384), (65535, 300), (65536, 257), (70000, 64)])
+def test_broadcast_shared_payload(torch, eng, plen, n):
+    rng = random.Random(plen * 7 + n)
+    src = np.frombuffer(rng.randbytes(plen + 37), np.uint8).copy()
+    for masked in (0, 1):  # server connections; client connections (each its own key)
+        frames = np.zeros(n, BUILD_DT)
+        frames["payload_off"], frames["payload_len"] = 37, plen
+        frames["opcode"], frames["fin"], frames["mask"] = 1, 1, masked
+        frames["key"] = [rng.getrandbits(32) for _ in range(n)]
+        exp, total, out, off = _build(torch, eng, src, frames)
+        assert int(off[n]) == total
+        assert out[:total].tobytes() == b"".join(exp)
+        if not masked:  # every connection receives the identical frame
+            one = len(exp[0])
+            assert total == n * one
+            assert (out[:total].reshape(n, one) == np.frombuffer(exp[0], np.uint8)).all()

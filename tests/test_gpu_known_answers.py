@@ -208,13 +208,14 @@ def test_mask_known_answers_device(torch, eng, known_answers, offset):
             assert bytes(buf[offset:offset + len(data)].cpu().numpy()) == data, case["id"]
 
 
-@pytest.mark.parametrize("cfg", ["c2", "c4"])
+@pytest.mark.parametrize("cfg", ["c2", "c3", "c4"])
 def test_full_config_summary_vs_oracle_decode_batch(torch, eng, cfg):
-    """BASELINE C2 / C4 at full size: the device summary and all frame statuses equal the
+    """BASELINE C2 / C3 / C4 at full size: the device summary and all frame statuses equal the
     oracle's process_data-per-frame decode of the identical frames, field by field (C4 also
     with the default 64 MiB max_message_size, where the reference rejects frame 262 144)."""
     import uvhttp_amd as U
-    n, plen, frag = {"c2": (65536, 4096, False), "c4": (1048576, 256, True)}[cfg]
+    n, plen, frag = {"c2": (65536, 4096, False), "c3": (65536, 65536, False),
+                     "c4": (1048576, 256, True)}[cfg]
     stride = U.gen_frame_stride(plen)
     wl = stride * n
     host, _ = _oracle.gen_frames(n, plen, 0x5EED0001, fragmented=frag, force_keys=True, total=n)
