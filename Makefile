@@ -29,7 +29,13 @@ $(BUILD)/ws_host.o: uvhttp_amd/csrc/ws_host.c include/uvhttp_ws_amd.h
 	@mkdir -p $(BUILD)
 	$(CC) $(CFLAGS) -c -o $@ $<
 
-$(LIB): $(BUILD)/ws_gpu.o $(BUILD)/tls_gpu.o $(BUILD)/ws_batcher.o $(BUILD)/ws_host.o
+# host-only C++ (the multi-GPU batcher group): no device code, no HIP headers
+$(BUILD)/ws_batcher_group.o: uvhttp_amd/csrc/ws_batcher_group.cpp include/uvhttp_ws_amd.h
+	@mkdir -p $(BUILD)
+	$(CXX) -O2 -fPIC -std=c++17 -Iinclude -Wall -Wextra -Werror -c -o $@ $<
+
+$(LIB): $(BUILD)/ws_gpu.o $(BUILD)/tls_gpu.o $(BUILD)/ws_batcher.o $(BUILD)/ws_host.o \
+        $(BUILD)/ws_batcher_group.o
 	@mkdir -p $(dir $@)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 

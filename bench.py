@@ -360,8 +360,17 @@ class GpuWorkload:
         eng.reserve(n, wire_len, n * plen if self.arena is not None else 0)
         self.build_dev = self.streams_dev = None
         self.graph = None
-        self.kernel = {"compact": "k_gather_compact", "build": "kb_emit",
-                       "build_masked": "kb_emit"}.get(mode, "k_unmask_inplace")
+        # the payload kernel that actually runs (ws_gpu.hip run_decode): a compact decode takes
+        # the wire-driven scatter below 16 KiB of wire per frame, the arena-driven gather above
+        # (UVHTTP_WS_COMPACT=gather|scatter pins it); the send side's small-frame kernel below
+        # 4 KiB per frame (UVHTTP_WS_BUILD_FRAMES)
+        cm = os.environ.get("UVHTTP_WS_COMPACT", "")
+        scatter = cm == "scatter" or (cm != "gather" and stride < 16384)
+        small_build = stride < int(os.environ.get("UVHTTP_WS_BUILD_FRAMES", "4096") or 0)
+        self.kernel = {"compact": "k_scatter_compact" if scatter else "k_gather_compact",
+                       "build": "kb_emit_frames" if small_build else "kb_emit",
+                       "build_masked": "kb_emit_frames" if small_build else "kb_emit",
+                       }.get(mode, "k_unmask_inplace")
         # in place, a batch of equal-stride small frames takes the fused path (ws_gpu.hip
         # run_decode: payload before plan, stride <= UVHTTP_WS_FUSED_MAX, default 2560 B)
         fused_max = int(os.environ.get("UVHTTP_WS_FUSED_MAX", "2560") or 2560)
@@ -471,6 +480,24 @@ class GpuWorkload:
         avg = ms / 1e3 / k
         return 2 * self.wire_len / avg / 1e9, avg * 1e6
 
+    def timeline(self, calls=16):
+        """Device-side kernel stamps (uvhttp_ws_gpu_engine_set_stamps) over `calls` more steps
+        after the timed region, same process and buffers: when each kernel of a call ran on the
+        device, so the payload kernel's own duration (no timing event beside it) and the gaps
+        between kernels and between calls are measured where they happen.  None for the send
+        side (its kernels are not stamped)."""
+        if self.build_dev is not None or self.graph is not None:
+            return None
+        eng = self.eng
+        eng.set_stamps(True)
+        eng.read_stamps()  # drop anything older
+        for _ in range(min(calls, 15)):
+            self.one_pass()
+        self.sync()
+        recs = eng.read_stamps()
+        eng.set_stamps(False)
+        return summarize_stamps(recs)
+
     def check(self):
         """Every frame of the shard must have been delivered (the decode really ran)."""
         n = self.n
@@ -493,6 +520,37 @@ class GpuWorkload:
                   "streams_dev", "s_desc"):
             setattr(self, k, None)
         self.torch.cuda.empty_cache()
+
+
+def summarize_stamps(recs):
+    """Per-call device timeline -> medians: payload-kernel duration, whole chain (first
+    kernel start .. last kernel end), the gap at every kernel boundary inside a call, and the
+    idle between one call's last kernel and the next call's first."""
+    import statistics
+    calls = {}
+    for call, kern, b, e in recs:
+        calls.setdefault(call, []).append((b, e, kern))
+    order = sorted(calls)
+    if not order:
+        return None
+    med = lambda xs: round(statistics.median(xs) / 1e3, 2) if xs else None  # noqa: E731
+    pay, chain, inter, gaps = [], [], [], {}
+    prev_end = None
+    for c in order:
+        ks = sorted(calls[c])
+        chain.append(ks[-1][1] - ks[0][0])
+        pay += [e - b for b, e, k in ks if k == "payload"]
+        for (b0, e0, k0), (b1, e1, k1) in zip(ks, ks[1:]):
+            gaps.setdefault(f"{k0}->{k1}", []).append(b1 - e0)
+        if prev_end is not None and c - 1 in calls:
+            inter.append(ks[0][0] - prev_end)
+        prev_end = max(e for _, e, _ in ks)
+    return {"calls": len(order), "kernels": [k for _, _, k in sorted(calls[order[-1]])],
+            "payload_us": med(pay), "chain_us": med(chain),
+            "gap_between_calls_us": med(inter),
+            "gap_between_calls_max_us": round(max(inter) / 1e3, 2) if inter else None,
+            "gaps_us": {k: med(v) for k, v in gaps.items()},
+            "source": "device wall clock (uvhttp_ws_gpu_engine_read_stamps), medians"}
 
 
 def timed_run(wl, steps, warmup, world):
@@ -564,6 +622,8 @@ def main():
     ap.add_argument("--rotate", type=int, default=1,
                     help="decode R copies of the batch round-robin (cold-cache rates)")
     ap.add_argument("--no-ceiling", action="store_true", help="skip the copy-ceiling timing")
+    ap.add_argument("--no-stamps", action="store_true",
+                    help="skip the device-timeline (kernel stamp) steps after the timed region")
     ap.add_argument("--graph", action="store_true",
                     help="replay each step as one captured HIP graph (diagnostic: no kernel timing)")
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)  # launcher tests
@@ -609,7 +669,21 @@ def main():
     ceiling = None
     if rank == 0 and not args.stub and not args.no_ceiling:
         ceiling = wl.copy_ceiling()
+    tl = None
+    if rank == 0 and not args.stub and not args.no_stamps:
+        tl = wl.timeline()
     wl.close()
+    # the dominant kernel's duration: the device stamps' payload-kernel median when stamped
+    # (no timing event beside the kernel), else the sampled HIP events; a kernel of the step
+    # cannot outlast the step
+    event_us = avg_kernel_s * 1e6 if k_n else None
+    stamped = bool(tl and tl.get("payload_us"))
+    kern_us = tl["payload_us"] if stamped else event_us
+    step_us = el_max / args.steps * 1e6
+    if stamped:
+        assert kern_us <= step_us / passes, (kern_us, step_us, passes)
+    if kern_us:
+        achieved = alg_bytes / (kern_us / 1e6) / 1e9
 
     extra = {}
     if rank == 0 and world == 1 and not args.stub:
@@ -653,7 +727,10 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                 "traffic": traffic,
                 "alg_bytes_per_launch": alg_bytes,
-                "avg_kernel_us": round(avg_kernel_s * 1e6, 2) if k_n else None,
+                "avg_kernel_us": round(kern_us, 2) if kern_us else None,
+                "avg_kernel_source": "device stamps (median of the timeline calls)" if stamped
+                                     else "hip events (sampled launches)",
+                "event_kernel_us": round(event_us, 2) if event_us else None,
                 "launches_timed": k_n,
                 "copy_ceiling": None if ceiling is None else {
                     "kernel": "k_apply_mask (uvhttp_ws_gpu_apply_mask over the whole wire)",
@@ -664,6 +741,14 @@ def main():
             },
             "host_issue_us_per_step": round(getattr(wl, "host_issue_s", 0.0) / args.steps * 1e6, 2),
         }
+        if tl:
+            out["device_timeline"] = tl
+        if cfg == "c5":
+            out["config"]["c5_model"] = (
+                "each rank decodes its contiguous share of the 8388608 frames as passes of one "
+                "resident 1048576-frame chunk (generated once; alternate passes re-mask it): the "
+                "bytes moved per pass are the chunk's, the frames past the first chunk are not "
+                "materialised")
         if args.stub:
             out["stub"] = True
         if "UVHTTP_WS_SPAWNED_FROM_GPU_PROCESS" in os.environ:

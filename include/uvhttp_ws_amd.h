@@ -334,6 +334,34 @@ const char* uvhttp_ws_gpu_engine_last_error(const uvhttp_ws_gpu_engine_t* eng);
  * summaries / results say so too, and nothing of them was unmasked), else OK. */
 int uvhttp_ws_gpu_engine_sync(uvhttp_ws_gpu_engine_t* eng, void* stream);
 
+/* Device-side kernel stamps (diagnostics).  With stamps on, every kernel of a decode call
+ * records on the GPU's constant wall clock when its first workgroups started and when its
+ * last wave ended, so the time between the kernels of a call — and between one call's last
+ * kernel and the next call's first — is read off the device timeline rather than inferred
+ * from host events.  The engine keeps the last 16 calls; read_stamps returns one record per
+ * (call, kernel) it holds, in call then start order, and clears them.  Costs one atomic per
+ * wave while on; off (the default) it costs one untaken branch per kernel.  Calls made while
+ * their stream is captured are not stamped. */
+#define UVHTTP_WS_STAMP_WALK 0        /* k_swalk_lane / k_swalk_wave (frame discovery) */
+#define UVHTTP_WS_STAMP_WALK_SCAN 1   /* k_swalk_scan (first frame per connection) */
+#define UVHTTP_WS_STAMP_WALK2 2       /* second walk (two-pass mode) */
+#define UVHTTP_WS_STAMP_STREAM_DESC 3 /* k_stream_desc / k_stream_desc_lane */
+#define UVHTTP_WS_STAMP_CLAIMS 4      /* k_stream_claims */
+#define UVHTTP_WS_STAMP_PAYLOAD 5     /* the payload kernel (unmask / scatter / gather) */
+#define UVHTTP_WS_STAMP_PLAN 6        /* k_plan */
+#define UVHTTP_WS_STAMP_FIXUP 7       /* k_fixup (fused stride path) */
+#define UVHTTP_WS_STAMP_FINALIZE 8    /* k_finalize */
+typedef struct {
+    uint32_t call;      /* the call's tag (increases by one per decode call, mod 2^24) */
+    uint32_t kernel;    /* UVHTTP_WS_STAMP_* */
+    uint64_t begin_ns;  /* device wall clock, ns: earliest sampled workgroup start */
+    uint64_t end_ns;    /* latest wave end */
+} uvhttp_ws_gpu_stamp_t;
+int uvhttp_ws_gpu_engine_set_stamps(uvhttp_ws_gpu_engine_t* eng, int enable);
+/* Waits for the device; *n_out = records written (at most cap). */
+int uvhttp_ws_gpu_engine_read_stamps(uvhttp_ws_gpu_engine_t* eng, uvhttp_ws_gpu_stamp_t* out,
+                                     uint32_t cap, uint32_t* n_out);
+
 /* Streams and graphs.  An engine owns one workspace, so its calls must execute one after
  * another: when a call names a different stream than the previous call, the engine makes the
  * new stream wait for the work already queued on the old one (an event), so calls from
@@ -564,6 +592,10 @@ typedef void (*uvhttp_ws_amd_ready_cb)(void* ctx);
  * of its first record.  The batcher forgets the connection's TLS state: the caller hands the
  * bytes to mbedtls (mbedtls_ssl_read, as src/uvhttp_connection.c:1128-1144 does) and may
  * register the connection again with uvhttp_ws_amd_batcher_set_tls (e.g. after a KeyUpdate). */
+/* first_status of a handback that is not about a record: the device could not open this
+ * connection's queued records (a device or launch error, or a queue that did not fit the device
+ * layout).  Nothing of them was delivered; `ciphertext` is all of it from next_seq on. */
+#define UVHTTP_WS_BATCHER_HANDBACK_DEVICE (-100)
 typedef void (*uvhttp_ws_amd_tls_handback_cb)(void* ctx, struct uvhttp_ws_connection* conn,
                                               const uint8_t* ciphertext, size_t len,
                                               uint64_t next_seq, int first_status);
@@ -602,6 +634,13 @@ typedef struct {
     uint64_t tls_records;                 /* TLS records opened and delivered on the device */
     uint64_t tls_bytes;                   /* their ciphertext bytes */
     uint64_t tls_handbacks;               /* connections handed back (on_tls_handback) */
+    uint64_t desc_refetches;              /* flushes whose descriptors outgrew the copy-back
+                                             high-water mark (rest fetched on completion) */
+    uint64_t blocked_calls;               /* batcher calls counted in blocked_ms */
+    double blocked_p50_ms, blocked_p99_ms;  /* their distribution (the last 65 536 calls) */
+    double max_blocked_wait_ms;           /* the longest call's split: waiting for the device */
+    double max_blocked_stage_ms;          /*   staging + enqueueing */
+    double max_blocked_deliver_ms;        /*   delivering (callbacks included) */
 } uvhttp_ws_amd_batcher_stats_t;
 void uvhttp_ws_amd_batcher_config_init(uvhttp_ws_amd_batcher_config_t* cfg);
 /* UVHTTP_WS_GPU_ENODEV if cfg->device >= 0 names no usable MI355X (no silent host mode) */
@@ -652,12 +691,16 @@ void uvhttp_ws_amd_batcher_forget(uvhttp_ws_amd_batcher_t* b, struct uvhttp_ws_c
  * (:1139-1144).  TLS queues always decode on the device (the host decoder has no AEAD):
  * set_tls returns UVHTTP_WS_GPU_ENODEV for a host-only batcher.  A connection is either
  * plain or TLS: submit_read on a TLS connection (and submit_tls_read on a plain one) is
- * UVHTTP_ERROR_INVALID_PARAM. */
+ * UVHTTP_ERROR_INVALID_PARAM.  set_tls flushes the connection's queued plain reads first; from
+ * inside a batcher callback, where no flush can run, it returns UVHTTP_WS_GPU_EINVAL while such
+ * reads are queued (call it again after the flush). */
 int uvhttp_ws_amd_batcher_set_tls(uvhttp_ws_amd_batcher_t* b, struct uvhttp_ws_connection* conn,
                                   const void* tls_key /* uvhttp_tls_key_t */, uint64_t read_seq);
 uvhttp_error_t uvhttp_ws_amd_batcher_submit_tls_read(uvhttp_ws_amd_batcher_t* b,
                                                      struct uvhttp_ws_connection* conn,
                                                      const uint8_t* ciphertext, size_t len);
+/* Zero the counters (e.g. after a warm-up), so stats() describes what follows. */
+void uvhttp_ws_amd_batcher_reset_stats(uvhttp_ws_amd_batcher_t* b);
 int uvhttp_ws_amd_batcher_stats(const uvhttp_ws_amd_batcher_t* b,
                                 uvhttp_ws_amd_batcher_stats_t* out);
 /* NUMA node of the batcher's GPU (its PCI device's sysfs numa_node), or -1 (host-only batcher,
@@ -666,6 +709,44 @@ int uvhttp_ws_amd_batcher_stats(const uvhttp_ws_amd_batcher_t* b,
  * ran at 91 GB/s from the GPU's node against 48 GB/s from the other socket — the live shape end
  * to end 38 vs 22 GiB/s (profiles/r03p44_numa_copy_e2e.txt). */
 int uvhttp_ws_amd_batcher_numa_node(const uvhttp_ws_amd_batcher_t* b);
+
+/* ---- batcher group: the live path over several GPUs ------------------------------------ */
+/* One batcher per device (the same config, cfg->device replaced by devices[k]; a device may be
+ * listed twice, -1 = a host-decoder member).  Each connection is pinned to one member on its
+ * first call — the member with the fewest live connections — until group_forget, so its reads
+ * keep their process_data order (the member guarantees it) while different connections flush
+ * over different PCIe links.  flush_async / poll / flush fan out to every member (flush: every
+ * member's queue is handed over before any is waited for); poll returns the queues delivered
+ * (summed) or the first error.  Callbacks are the members' (cfg's).  Not thread-safe, like the
+ * batcher: one loop thread owns the group.  A loop thread copies reads at full rate only into
+ * members on its own NUMA node (uvhttp_ws_amd_batcher_numa_node): on a two-socket node run one
+ * loop per socket, each with a group of that socket's GPUs. */
+typedef struct uvhttp_ws_amd_batcher_group uvhttp_ws_amd_batcher_group_t;
+int uvhttp_ws_amd_batcher_group_create(const uvhttp_ws_amd_batcher_config_t* cfg, const int* devices,
+                                       int n_devices, uvhttp_ws_amd_batcher_group_t** out);
+void uvhttp_ws_amd_batcher_group_free(uvhttp_ws_amd_batcher_group_t* g);
+int uvhttp_ws_amd_batcher_group_size(const uvhttp_ws_amd_batcher_group_t* g);
+/* member i (its stats, NUMA node), or NULL */
+uvhttp_ws_amd_batcher_t* uvhttp_ws_amd_batcher_group_batcher(uvhttp_ws_amd_batcher_group_t* g, int i);
+/* the member a connection is pinned to (pins it now if it is new) */
+int uvhttp_ws_amd_batcher_group_member(uvhttp_ws_amd_batcher_group_t* g, struct uvhttp_ws_connection* conn);
+uvhttp_error_t uvhttp_ws_amd_batcher_group_submit_read(uvhttp_ws_amd_batcher_group_t* g,
+                                                       struct uvhttp_ws_connection* conn,
+                                                       const uint8_t* data, size_t len);
+int uvhttp_ws_amd_batcher_group_set_tls(uvhttp_ws_amd_batcher_group_t* g, struct uvhttp_ws_connection* conn,
+                                        const void* tls_key, uint64_t read_seq);
+uvhttp_error_t uvhttp_ws_amd_batcher_group_submit_tls_read(uvhttp_ws_amd_batcher_group_t* g,
+                                                           struct uvhttp_ws_connection* conn,
+                                                           const uint8_t* ciphertext, size_t len);
+int uvhttp_ws_amd_batcher_group_flush_async(uvhttp_ws_amd_batcher_group_t* g);
+int uvhttp_ws_amd_batcher_group_poll(uvhttp_ws_amd_batcher_group_t* g);
+int uvhttp_ws_amd_batcher_group_flush(uvhttp_ws_amd_batcher_group_t* g);
+int uvhttp_ws_amd_batcher_group_in_flight(const uvhttp_ws_amd_batcher_group_t* g);
+void uvhttp_ws_amd_batcher_group_forget(uvhttp_ws_amd_batcher_group_t* g, struct uvhttp_ws_connection* conn);
+/* counters summed over the members; max_blocked / percentiles: the worst member's */
+int uvhttp_ws_amd_batcher_group_stats(const uvhttp_ws_amd_batcher_group_t* g,
+                                      uvhttp_ws_amd_batcher_stats_t* out);
+void uvhttp_ws_amd_batcher_group_reset_stats(uvhttp_ws_amd_batcher_group_t* g);
 
 /* Library identity, for the loader checks in tests/. */
 const char* uvhttp_ws_amd_version(void);

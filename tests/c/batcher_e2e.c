@@ -154,6 +154,8 @@ int main(int argc, char** argv) {
         if (it == 0) {
             if (async && uvhttp_ws_amd_batcher_flush(b) != 0) return 3;  /* drain the warm-up */
             g_msgs = g_bytes = 0;
+            /* the timed flushes only: every counter, percentile and maximum from here on */
+            uvhttp_ws_amd_batcher_reset_stats(b);
             uvhttp_ws_amd_batcher_stats(b, &st0);
             t0 = now_s();
             g_t0 = t0;
@@ -204,7 +206,10 @@ int main(int argc, char** argv) {
            "\"device_ms_total\": %.1f, \"async\": %d, \"submit_ms_per_flush\": %.3f, "
            "\"flush_call_ms_per_flush\": %.3f, \"blocked_ms_per_flush\": %.3f, \"gpu_numa_node\": %d, \"pinned_node\": %d, "
            "\"host_flushes\": %llu, \"fallback_flushes\": %llu, \"capacity_flushes\": %llu, \"device_errors\": %llu, "
-           "\"max_blocked_ms\": %.3f, \"per_flush_ms\": {\"copy\": %.3f, \"upload\": %.3f, "
+           "\"max_blocked_ms\": %.3f, \"blocked_calls\": %llu, \"blocked_p50_ms\": %.3f, "
+           "\"blocked_p99_ms\": %.3f, \"max_blocked_split_ms\": {\"wait\": %.3f, \"stage\": %.3f, "
+           "\"deliver\": %.3f}, \"desc_refetches\": %llu, "
+           "\"per_flush_ms\": {\"copy\": %.3f, \"upload\": %.3f, "
            "\"stage\": %.3f, \"wait\": %.3f, \"deliver\": %.3f}}\n",
            device >= 0 ? "device batcher (stage, H2D, decode_reads, D2H, deliver)"
                        : "host decoder (process_data per read, 1 core)",
@@ -217,6 +222,9 @@ int main(int argc, char** argv) {
            (unsigned long long)(st.fallback_flushes - st0.fallback_flushes),
            (unsigned long long)(st.capacity_flushes - st0.capacity_flushes),
            (unsigned long long)(st.device_errors - st0.device_errors), st.max_blocked_ms,
+           (unsigned long long)st.blocked_calls, st.blocked_p50_ms, st.blocked_p99_ms,
+           st.max_blocked_wait_ms, st.max_blocked_stage_ms, st.max_blocked_deliver_ms,
+           (unsigned long long)st.desc_refetches,
            (st.copy_ms - st0.copy_ms) / flushes, (st.upload_ms - st0.upload_ms) / flushes,
            (st.stage_ms - st0.stage_ms) / flushes, (st.wait_ms - st0.wait_ms) / flushes,
            (st.deliver_ms - st0.deliver_ms) / flushes);

@@ -1,0 +1,97 @@
+"""The batcher group (uvhttp_ws_amd_batcher_group_*): the live path over several devices.
+
+Every connection is pinned to one member for its life, so its reads keep the order the
+reference's on_websocket_read gives them (process_data per read until one fails,
+src/uvhttp_connection.c:1098-1175) while different connections flush through different members.
+Each connection is checked against the oracle fed the same reads: callback transcript, failure,
+recv-buffer and fragment state.  Host-decoder members (-1) run here on the CPU; groups with device
+members (two members on GPU 0, or a GPU and a host member) are marked gpu."""
+import random
+
+import pytest
+
+from test_batcher_transitions import Pair, _conn_reads
+
+GROUPS = [[-1, -1, -1], [-1],
+          pytest.param([0, 0], marks=pytest.mark.gpu, id="gpu0x2"),
+          pytest.param([0, -1], marks=pytest.mark.gpu, id="gpu0+host")]
+
+
+def _need(devices):
+    if max(devices) >= 0:
+        import torch
+        if not torch.cuda.is_available():
+            pytest.skip("no GPU")
+
+
+def _drive(b, rng, pairs, forget_some=False):
+    while any(p.next < len(p.reads) for p in pairs):
+        for p in rng.sample(pairs, len(pairs)):
+            if p.next >= len(p.reads) or rng.random() < 0.3:
+                continue
+            p.feed(b, p.reads[p.next])
+            p.next += 1
+            if forget_some and not p.dead and rng.random() < 0.01:
+                b.forget(p.prod)
+                p.dead = True
+        act = rng.random()
+        if act < 0.3:
+            assert b.flush() == 0
+        elif act < 0.6:
+            assert b.flush_async() == 0
+        elif act < 0.8:
+            assert b.poll() >= 0
+    assert b.flush() == 0
+    assert not b.in_flight()
+
+
+@pytest.mark.parametrize("devices", GROUPS)
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_group_matches_process_data(devices, seed):
+    _need(devices)
+    import uvhttp_amd as U
+    import _oracle
+    rng = random.Random(600 + seed)
+    b = U.BatcherGroup(devices, min_device_bytes=0, max_bytes=[64 << 10, 1 << 20, 8 << 20][seed - 1],
+                       max_connections=64, max_reads=4000)
+    assert b.size() == len(devices)
+    pairs = [Pair(U, rng, reads=_conn_reads(rng, big=70000 if seed == 1 else 0)) for _ in range(45)]
+    _drive(b, rng, pairs, forget_some=seed == 3)
+    L = _oracle.load()
+    for p in pairs:
+        p.check(b, L)
+    # every member served connections, each connection stayed on its member
+    members = [b.member(p.prod) for p in pairs if not p.dead]
+    for m in range(len(devices)):
+        assert members.count(m) >= 1
+    st = b.stats()
+    per = [b.member_stats(m)["flushes"] for m in range(len(devices))]
+    assert st["flushes"] == sum(per)
+    b.close()
+
+
+def test_group_pinning_and_balance():
+    """first call pins a connection to the least-loaded member (ties: round robin); it stays
+    there across flushes; forget releases its place"""
+    import uvhttp_amd as U
+    b = U.BatcherGroup([-1, -1, -1, -1])
+    conns = [U.WsConnection(1) for _ in range(10)]
+    ms = [b.member(c) for c in conns]
+    assert sorted(ms) == [0, 0, 0, 1, 1, 1, 2, 2, 3, 3]
+    assert [b.member(c) for c in conns] == ms  # pinned
+    frame = b"\x82\x85" + b"\x01\x02\x03\x04" + bytes(x ^ k for x, k in zip(b"hello", b"\x01\x02\x03\x04\x01"))
+    for c in conns:
+        assert b.submit(c, frame) == 0
+    assert b.flush() == 0
+    assert all([e[2] for e in c.events if e[0] == "message"] == [b"hello"] for c in conns)
+    assert [b.member(c) for c in conns] == ms
+    b.forget(conns[3])  # member 3 drops to one connection... (conns[3] is on member ms[3])
+    fresh = U.WsConnection(1)
+    assert b.member(fresh) == ms[3]
+    b.close()
+
+
+def test_group_rejects_bad_config():
+    import uvhttp_amd as U
+    with pytest.raises(U.GpuError):
+        U.BatcherGroup([])

@@ -164,3 +164,121 @@ def test_tls_rules(torch):
     assert dev.submit_tls(d, b"\x17\x03\x03") == -1  # not registered
     dev.close()
     host.close()
+
+
+def _seal_stream(rng, key, seq0, plain, rec=16384):
+    recs, pos, j = [], 0, 0
+    while pos < len(plain):
+        n = min(len(plain) - pos, rec)
+        recs.append(O.tls_seal(key, seq0 + j, 23, plain[pos:pos + n]))
+        pos += n
+        j += 1
+    return b"".join(recs)
+
+
+@pytest.mark.parametrize("pattern", ["async", "sync"])
+def test_tls_bulk_upload_larger_than_flushes(torch, pattern):
+    """ONE TLS connection sending far more than a flush holds (a bulk upload, > 2 x max_bytes),
+    in reads up to 1.5 x max_bytes, while earlier queues are still in flight: every read is
+    taken (the in-flight queue's bytes made the staging bound refuse it before),
+    and the connection sees exactly the oracle's process_data per record."""
+    import uvhttp_amd as U
+    rng = random.Random(4400 + len(pattern))
+    mb = 1 << 20
+    b = U.Batcher(device=0, min_device_bytes=0, max_bytes=mb)
+    key = O.tls_key(rng.randbytes(16), rng.randbytes(12), O.TLS13, O.AES_GCM)
+    seq0 = 77
+    mf, mm = 16 * 1024 * 1024, 64 * 1024 * 1024
+    prod = U.WsConnection(1, mf, mm)
+    orc = O.OracleConn(1, mf, mm, record=1)
+    plain = b"".join(_frame(2, 1, rng.randbytes(rng.choice([1000, 60000, 300000])), rng.randbytes(4))
+                     for _ in range(14))
+    cipher = _seal_stream(rng, key, seq0, plain)
+    assert len(cipher) > 2 * mb
+    assert b.set_tls(prod, key.tobytes(), seq0) == 0
+    pos = 0
+    while pos < len(cipher):
+        n = rng.choice([16384, 200000, mb // 2, mb + mb // 2])
+        assert b.submit_tls(prod, cipher[pos:pos + n]) == 0, pos
+        pos += n
+        if pattern == "async":
+            assert b.flush_async() == 0
+            assert b.poll() in (0, 1)
+    assert b.flush() == 0
+    key_ = C.addressof(prod.ptr.contents)
+    assert key_ not in b.failures and key_ not in b.handbacks
+    st = np.zeros(1, O.TLS_STREAM_DT)
+    st[0] = (0, len(cipher), seq0, 0, 0)
+    recs, res, out = O.tls_open_batch(np.frombuffer(cipher, np.uint8), key, st, out_cap=len(cipher))
+    reads = [out[r["out_off"]:r["out_off"] + r["content_len"]].tobytes()
+             for r in recs[:int(res[0]["n_delivered"])]]
+    assert orc.process_reads(reads)[0] == 0
+    pev = [(k, a, p) for k, a, p in prod.events if k == "message"]
+    oev = [(k, a, p) for k, a, p in orc.events() if k == "message"]
+    assert len(pev) == 14 and pev == oev
+    b.close()
+
+
+def test_tls_device_error_hands_ciphertext_back(torch, monkeypatch):
+    """A device or launch error on a queue holding TLS connections (injected: every launch
+    fails) neither fails nor closes them: their ciphertext — all of it from the next record on
+    — goes back to the caller for mbedtls (status UVHTTP_WS_BATCHER_HANDBACK_DEVICE = -100,
+    ADVICE r03); plain connections of the same queue are decoded by the host decoder."""
+    import uvhttp_amd as U
+    monkeypatch.setenv("UVHTTP_WS_BATCHER_FAIL_EVERY", "1")
+    rng = random.Random(4500)
+    b = U.Batcher(device=0, min_device_bytes=0, max_bytes=4 << 20)
+    monkeypatch.delenv("UVHTTP_WS_BATCHER_FAIL_EVERY")
+    conns = []
+    for k in range(5):
+        key = O.tls_key(rng.randbytes(32), rng.randbytes(12), O.TLS12, O.CHACHA)
+        prod = U.WsConnection(1)
+        cipher = _seal_stream(rng, key, 1000 * k, _ws_frames(rng, 6), rec=700)
+        assert b.set_tls(prod, key.tobytes(), 1000 * k) == 0
+        conns.append((prod, cipher, 1000 * k))
+    plain_conn = U.WsConnection(1)
+    orc = O.OracleConn(1, record=1)
+    pf = _ws_frames(rng, 5)
+    for prod, cipher, _ in conns:
+        cut = len(cipher) // 3
+        assert b.submit_tls(prod, cipher[:cut]) == 0
+        assert b.submit_tls(prod, cipher[cut:]) == 0
+    assert b.submit(plain_conn, pf) == 0
+    rc = b.flush()
+    assert rc == -4  # ELAUNCH: the injected device error, reported
+    assert orc.process_data(pf) == 0
+    assert [e for e in plain_conn.events if e[0] == "message"] == \
+        [e for e in orc.events() if e[0] == "message"]
+    for prod, cipher, seq in conns:
+        key_ = C.addressof(prod.ptr.contents)
+        assert key_ not in b.failures
+        data, next_seq, status = b.handbacks[key_]
+        assert status == -100 and next_seq == seq and data == cipher
+        assert not [e for e in prod.events if e[0] == "message"]
+    st = b.stats()
+    assert st["device_errors"] == 1 and st["tls_handbacks"] == 5
+    b.close()
+
+
+def test_set_tls_inside_callback_with_queued_plain_reads(torch):
+    """set_tls from a batcher callback while the connection still has plain reads queued cannot
+    flush them first: it is refused (EINVAL) instead of registering a TLS connection whose plain
+    reads would then be unreachable; after the flush it succeeds."""
+    import uvhttp_amd as U
+    b = U.Batcher(device=0, min_device_bytes=0)
+    a, c = U.WsConnection(1), U.WsConnection(1)
+    key = O.tls_key(bytes(range(16)), bytes(12), O.TLS13).tobytes()
+    seen = []
+
+    def hook(conn, ev):
+        if not seen:
+            seen.append(b.set_tls(c, key, 5))
+
+    a.hook = hook
+    assert b.submit(a, _frame(2, 1, b"first", b"\x01\x02\x03\x04")) == 0
+    assert b.submit(c, _frame(2, 1, b"second", b"\x05\x06\x07\x08")) == 0
+    assert b.flush() == 0
+    assert seen == [-1]
+    assert [e[2] for e in c.events if e[0] == "message"] == [b"second"]
+    assert b.set_tls(c, key, 5) == 0
+    b.close()

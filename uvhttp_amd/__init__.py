@@ -105,6 +105,16 @@ STREAM_RESULT_DT = _np_dtype(StreamResult)
 STREAM_RESULT_BYTES = C.sizeof(StreamResult)
 
 
+class GpuStamp(C.Structure):
+    """uvhttp_ws_gpu_stamp_t (24 B)."""
+    _fields_ = [("call", C.c_uint32), ("kernel", C.c_uint32), ("begin_ns", C.c_uint64),
+                ("end_ns", C.c_uint64)]
+
+
+STAMP_KERNELS = {0: "walk", 1: "walk_scan", 2: "walk2", 3: "stream_desc", 4: "claims",
+                 5: "payload", 6: "plan", 7: "fixup", 8: "finalize"}
+
+
 class Batch(C.Structure):
     _fields_ = [("wire", C.c_void_p), ("wire_len", C.c_uint64), ("frame_off", C.c_void_p),
                 ("frame_stride", C.c_uint64), ("n_frames", C.c_uint32),
@@ -179,7 +189,10 @@ class BatcherStats(C.Structure):
                                    "direct_reads")] + \
         [(k, C.c_double) for k in ("blocked_ms", "max_blocked_ms", "wait_ms", "copy_ms",
                                    "upload_ms", "stage_ms", "deliver_ms")] + \
-        [(k, C.c_uint64) for k in ("tls_records", "tls_bytes", "tls_handbacks")]
+        [(k, C.c_uint64) for k in ("tls_records", "tls_bytes", "tls_handbacks", "desc_refetches",
+                                   "blocked_calls")] + \
+        [(k, C.c_double) for k in ("blocked_p50_ms", "blocked_p99_ms", "max_blocked_wait_ms",
+                                   "max_blocked_stage_ms", "max_blocked_deliver_ms")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -230,6 +243,8 @@ def load_library(path: str) -> C.CDLL:
                                                        C.POINTER(u64)]),
         "uvhttp_ws_gpu_engine_last_error": (C.c_char_p, [vp]),
         "uvhttp_ws_gpu_engine_sync": (C.c_int, [vp, vp]),
+        "uvhttp_ws_gpu_engine_set_stamps": (C.c_int, [vp, C.c_int]),
+        "uvhttp_ws_gpu_engine_read_stamps": (C.c_int, [vp, vp, u32, C.POINTER(u32)]),
         "uvhttp_ws_gpu_decode_inplace": (C.c_int, [vp, C.POINTER(Batch), vp, vp, vp]),
         "uvhttp_ws_gpu_decode_compact": (C.c_int, [vp, C.POINTER(Batch), vp, u64, vp, vp, vp,
                                                    vp]),
@@ -268,6 +283,26 @@ def load_library(path: str) -> C.CDLL:
                                                            vp, C.c_size_t]),
         "uvhttp_ws_amd_batcher_forget": (None, [vp, C.POINTER(WsConnectionStruct)]),
         "uvhttp_ws_amd_batcher_stats": (C.c_int, [vp, C.POINTER(BatcherStats)]),
+        "uvhttp_ws_amd_batcher_reset_stats": (None, [vp]),
+        "uvhttp_ws_amd_batcher_group_create": (C.c_int, [C.POINTER(BatcherConfig), vp, C.c_int,
+                                                         C.POINTER(vp)]),
+        "uvhttp_ws_amd_batcher_group_free": (None, [vp]),
+        "uvhttp_ws_amd_batcher_group_size": (C.c_int, [vp]),
+        "uvhttp_ws_amd_batcher_group_batcher": (vp, [vp, C.c_int]),
+        "uvhttp_ws_amd_batcher_group_member": (C.c_int, [vp, C.POINTER(WsConnectionStruct)]),
+        "uvhttp_ws_amd_batcher_group_submit_read": (C.c_int, [vp, C.POINTER(WsConnectionStruct),
+                                                              vp, C.c_size_t]),
+        "uvhttp_ws_amd_batcher_group_set_tls": (C.c_int, [vp, C.POINTER(WsConnectionStruct), vp,
+                                                         C.c_uint64]),
+        "uvhttp_ws_amd_batcher_group_submit_tls_read": (C.c_int, [vp, C.POINTER(WsConnectionStruct),
+                                                                 vp, C.c_size_t]),
+        "uvhttp_ws_amd_batcher_group_flush_async": (C.c_int, [vp]),
+        "uvhttp_ws_amd_batcher_group_poll": (C.c_int, [vp]),
+        "uvhttp_ws_amd_batcher_group_flush": (C.c_int, [vp]),
+        "uvhttp_ws_amd_batcher_group_in_flight": (C.c_int, [vp]),
+        "uvhttp_ws_amd_batcher_group_forget": (None, [vp, C.POINTER(WsConnectionStruct)]),
+        "uvhttp_ws_amd_batcher_group_stats": (C.c_int, [vp, C.POINTER(BatcherStats)]),
+        "uvhttp_ws_amd_batcher_group_reset_stats": (None, [vp]),
         "uvhttp_ws_amd_batcher_numa_node": (C.c_int, [vp]),
         # TLS record layer (include/uvhttp_tls_amd.h)
         "uvhttp_tls_gpu_engine_create": (C.c_int, [C.c_int, C.POINTER(vp)]),
@@ -282,6 +317,8 @@ def load_library(path: str) -> C.CDLL:
         "uvhttp_tls_gpu_ws_streams": (C.c_int, [vp, vp, vp, u32, vp, vp, vp, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
+        if path != LIB_PATH and not hasattr(L, name):
+            continue  # an older build loaded beside the tree's for an A/B run (tools/ab_lib.py)
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
@@ -441,6 +478,20 @@ class GpuEngine:
         self._check(self._L.uvhttp_ws_gpu_engine_kernel_time(self.h, C.byref(ms), C.byref(n)),
                     "kernel_time")
         return ms.value, n.value
+
+    def set_stamps(self, on=True):
+        """device-side kernel stamps (include/uvhttp_ws_amd.h): on / off"""
+        self._check(self._L.uvhttp_ws_gpu_engine_set_stamps(self.h, 1 if on else 0), "set_stamps")
+
+    def read_stamps(self):
+        """-> [(call, kernel name, begin_ns, end_ns)] of the calls the engine still holds
+        (waits for the device; clears them)"""
+        buf = (GpuStamp * 256)()
+        n = C.c_uint32(0)
+        self._check(self._L.uvhttp_ws_gpu_engine_read_stamps(self.h, buf, 256, C.byref(n)),
+                    "read_stamps")
+        return [(r.call, STAMP_KERNELS.get(r.kernel, str(r.kernel)), r.begin_ns, r.end_ns)
+                for r in buf[:n.value]]
 
     def alloc_outputs(self, n_frames):
         t = self.torch
@@ -806,3 +857,84 @@ class Batcher:
             self.close()
         except Exception:
             pass
+
+
+class BatcherGroup(Batcher):
+    """uvhttp_ws_amd_batcher_group_t: one batcher per device (-1 = host decoder), each
+    connection pinned to one member; the Batcher methods route / fan out."""
+
+    _P = "uvhttp_ws_amd_batcher_group_"
+
+    def __init__(self, devices, min_device_bytes=0, max_bytes=32 << 20, max_connections=16384,
+                 max_reads=1 << 18):
+        L = lib()
+        self._L = L
+        cfg = BatcherConfig()
+        L.uvhttp_ws_amd_batcher_config_init(C.byref(cfg))
+        cfg.min_device_bytes, cfg.max_bytes = min_device_bytes, max_bytes
+        cfg.max_connections, cfg.max_reads = max_connections, max_reads
+        self.failures, self.handbacks = {}, {}
+        self._cb = FAILURE_CB(self._on_failure)
+        cfg.on_failure = self._cb
+        self._hb = TLS_HANDBACK_CB(self._on_handback)
+        cfg.on_tls_handback = self._hb
+        devs = (C.c_int * len(devices))(*devices)
+        h = C.c_void_p()
+        rc = L.uvhttp_ws_amd_batcher_group_create(C.byref(cfg), devs, len(devices), C.byref(h))
+        if rc != 0:
+            raise GpuError(f"uvhttp_ws_amd_batcher_group_create rc={rc}")
+        self.h = h
+
+    def _fn(self, name):
+        return getattr(self._L, self._P + name)
+
+    def member(self, conn) -> int:
+        return self._fn("member")(self.h, conn.ptr)
+
+    def size(self) -> int:
+        return self._fn("size")(self.h)
+
+    def member_stats(self, i) -> dict:
+        s = BatcherStats()
+        self._L.uvhttp_ws_amd_batcher_stats(self._fn("batcher")(self.h, i), C.byref(s))
+        return s.as_dict()
+
+    def set_tls(self, conn, key_bytes, read_seq):
+        kb = (C.c_uint8 * 64).from_buffer_copy(bytes(key_bytes))
+        return self._fn("set_tls")(self.h, conn.ptr, kb, read_seq)
+
+    def submit_tls(self, conn, data):
+        buf = (C.c_uint8 * max(1, len(data))).from_buffer_copy(bytes(data) or b"\0")
+        return self._fn("submit_tls_read")(self.h, conn.ptr, buf, len(data))
+
+    def submit(self, conn, data):
+        buf = (C.c_uint8 * max(1, len(data))).from_buffer_copy(bytes(data) or b"\0")
+        return self._fn("submit_read")(self.h, conn.ptr, buf, len(data))
+
+    def flush(self):
+        return self._fn("flush")(self.h)
+
+    def flush_async(self):
+        return self._fn("flush_async")(self.h)
+
+    def poll(self):
+        return self._fn("poll")(self.h)
+
+    def in_flight(self):
+        return bool(self._fn("in_flight")(self.h))
+
+    def forget(self, conn):
+        self._fn("forget")(self.h, conn.ptr)
+
+    def stats(self):
+        s = BatcherStats()
+        self._fn("stats")(self.h, C.byref(s))
+        return s.as_dict()
+
+    def numa_node(self):
+        return -1
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._fn("free")(self.h)
+            self.h = None

@@ -23,6 +23,7 @@
 // has been delivered (flush_async completes it first), so its state is always current.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <stdint.h>
 #include <stdio.h>
@@ -127,6 +128,7 @@ struct BatchQueue {
     uvhttp_ws_frame_desc_t *h_desc = nullptr, *d_desc = nullptr;
     GatherSeg *h_seg = nullptr, *d_seg = nullptr;
     uint32_t max_frames = 0;
+    uint64_t desc_copied = 0, wdesc_copied = 0;  // descriptors the launch copies back
     hipEvent_t up_ev = nullptr, done_ev = nullptr;
     // TLS connections (allocated with the first set_tls)
     bool tls_ready = false;
@@ -174,7 +176,13 @@ struct uvhttp_ws_amd_batcher {
     uint32_t launches = 0;    // launch reports ELAUNCH before enqueueing anything
     uvhttp_tls_gpu_engine_t* teng = nullptr;  // record open (first set_tls)
     std::unordered_map<uvhttp_ws_connection_t*, TlsConn> tls;
+    // descriptors a launch copies back: a high-water mark of recent flushes' frame counts (the
+    // count itself is only known on the device); a flush with more fetches the rest after it
+    // completes (desc_refetches)
+    uint64_t desc_hint = 4096, wdesc_hint = 4096;
     uvhttp_ws_amd_batcher_stats_t st;
+    std::vector<float> blocked;  // ms of each blocked call (ring of the last kBlockedKeep)
+    uint64_t blocked_n = 0;
 };
 
 namespace {
@@ -550,11 +558,13 @@ int launch_device(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
                                hipMemcpyDeviceToHost, s);
         if (h == hipSuccess && rc == UVHTTP_WS_GPU_OK)
             h = hipMemcpyAsync(q.h_wire, q.d_wire, pos, hipMemcpyDeviceToHost, s);
-        // the descriptors too, all the capacity (the frame count is only known on the device):
-        // a synchronous copy after completion queued behind the next queue's uploads on the
-        // copy engine and blocked the loop for milliseconds
+        // the descriptors too, as many as recent flushes used (the frame count is only known
+        // on the device): a synchronous copy of all of them after completion queued behind the
+        // next queue's uploads on the copy engine and blocked the loop for milliseconds, and
+        // copying the whole capacity moved up to bytes / 6 descriptors per flush
+        q.desc_copied = b->desc_hint < q.max_frames ? b->desc_hint : q.max_frames;
         if (h == hipSuccess && rc == UVHTTP_WS_GPU_OK)
-            h = hipMemcpyAsync(q.h_desc, q.d_desc, (size_t)q.max_frames * sizeof(uvhttp_ws_frame_desc_t),
+            h = hipMemcpyAsync(q.h_desc, q.d_desc, (size_t)q.desc_copied * sizeof(uvhttp_ws_frame_desc_t),
                                hipMemcpyDeviceToHost, s);
         mark("d2h");
     }
@@ -588,8 +598,9 @@ int launch_device(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
             h = hipMemcpyAsync(q.h_wst, q.d_wst, nt * sizeof(uvhttp_ws_stream_t), hipMemcpyDeviceToHost, s);
         if (h == hipSuccess && !rc)
             h = hipMemcpyAsync(q.h_plain, q.d_plain, plain_cap, hipMemcpyDeviceToHost, s);
+        q.wdesc_copied = b->wdesc_hint < q.wdesc_cap ? b->wdesc_hint : q.wdesc_cap;
         if (h == hipSuccess && !rc)
-            h = hipMemcpyAsync(q.h_wdesc, q.d_wdesc, (size_t)q.wdesc_cap * sizeof(uvhttp_ws_frame_desc_t),
+            h = hipMemcpyAsync(q.h_wdesc, q.d_wdesc, (size_t)q.wdesc_copied * sizeof(uvhttp_ws_frame_desc_t),
                                hipMemcpyDeviceToHost, s);
     }
     if (h == hipSuccess && rc == UVHTTP_WS_GPU_OK) h = hipEventRecord(q.done_ev, s);
@@ -635,16 +646,31 @@ void tls_handback(uvhttp_ws_amd_batcher_t* b, uvhttp_ws_connection_t* conn,
         b->cfg.on_tls_handback(b->cfg.ctx, conn, bytes.data(), bytes.size(), next_seq, status);
 }
 
-// a TLS slot's queue could not be opened on the device: its connection fails (the records
-// cannot be decrypted on the host)
-void fail_tls_slots(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
+// A queue's TLS slots could not be opened on the device (a device or launch error, or a queue
+// that did not fit the device layout).  Nothing of them was delivered and their ciphertext is
+// intact — the connection's carry plus its reads in this queue — so it goes back to the caller
+// from the connection's next record on (on_tls_handback, status
+// UVHTTP_WS_BATCHER_HANDBACK_DEVICE): mbedtls reads it on the host, as it would have without the
+// batcher.  Only with no handback callback does the connection fail (the host has no AEAD).
+void handback_tls_slots(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
+    b->delivering++;  // (the callback runs as a delivery's: no nested flushes)
     for (size_t k = 0; k < q.slots.size(); ++k) {
         ConnSlot& s = q.slots[k];
         if (!s.tls || s.dropped || b->failed.count(s.conn)) continue;
         s.dropped = true;
-        b->tls.erase(s.conn);
-        report_failure(b, s.conn, UVHTTP_ERROR_INVALID_PARAM);
+        auto ti = b->tls.find(s.conn);
+        if (ti == b->tls.end()) continue;  // (forgotten meanwhile)
+        if (!b->cfg.on_tls_handback) {
+            b->tls.erase(ti);
+            report_failure(b, s.conn, UVHTTP_ERROR_INVALID_PARAM);
+            continue;
+        }
+        std::vector<uint8_t> bytes = ti->second.carry;
+        for (uint32_t r : s.reads)
+            bytes.insert(bytes.end(), q.h_arena + q.reads[r].off, q.h_arena + q.reads[r].off + q.reads[r].len);
+        tls_handback(b, s.conn, std::move(bytes), ti->second.seq, UVHTTP_WS_BATCHER_HANDBACK_DEVICE);
     }
+    b->delivering--;
 }
 
 // A decode whose frames did not fit its descriptors reported ERR_CAPACITY and unmasked
@@ -669,6 +695,7 @@ int rerun_over_capacity(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
                     hipMemcpyAsync(q.h_desc, q.d_desc, (size_t)q.max_frames * sizeof(uvhttp_ws_frame_desc_t),
                                    hipMemcpyDeviceToHost, s) != hipSuccess))
             rc = UVHTTP_WS_GPU_ELAUNCH;
+        q.desc_copied = q.max_frames;
         if (!rc) rc = uvhttp_ws_gpu_engine_sync(b->eng, s);
         if (rc) return rc;
     }
@@ -685,16 +712,55 @@ int rerun_over_capacity(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
                     hipMemcpyAsync(q.h_wdesc, q.d_wdesc, (size_t)q.wdesc_cap * sizeof(uvhttp_ws_frame_desc_t),
                                    hipMemcpyDeviceToHost, s) != hipSuccess))
             rc = UVHTTP_WS_GPU_ELAUNCH;
+        q.wdesc_copied = q.wdesc_cap;
         if (!rc) rc = uvhttp_ws_gpu_engine_sync(b->eng, s);
         if (rc) return rc;
     }
     return UVHTTP_WS_GPU_OK;
 }
 
+// descriptors [copied, used) of a finished decode, when the launch copied back fewer than it
+// produced (synchronous; rare once the high-water mark has seen the flush shape)
+int fetch_rest(uvhttp_ws_amd_batcher_t* b, const uvhttp_ws_frame_desc_t* d, uvhttp_ws_frame_desc_t* h,
+               uint64_t copied, uint64_t used) {
+    if (used <= copied) return 0;
+    b->st.desc_refetches++;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    if (prev != b->cfg.device) (void)hipSetDevice(b->cfg.device);
+    const hipError_t h2 = hipMemcpy(h + copied, d + copied,
+                                    (size_t)(used - copied) * sizeof(uvhttp_ws_frame_desc_t),
+                                    hipMemcpyDeviceToHost);
+    if (prev != b->cfg.device) (void)hipSetDevice(prev);
+    return h2 == hipSuccess ? 0 : UVHTTP_WS_GPU_ELAUNCH;
+}
+
+// the next launches' copy-back: a quarter above this flush's frames, decaying by 1/8 per flush
+uint64_t next_hint(uint64_t hint, uint64_t frames) {
+    const uint64_t want = frames + frames / 4 + 256;
+    const uint64_t decayed = hint - hint / 8;
+    return want > decayed ? want : decayed;
+}
+
 // q's decode has finished (or failed): deliver it, or decode it on the host when the
 // device could not (nothing of q has been delivered before this point; TLS connections,
 // which the host cannot open, fail instead).
+// the batcher's device is current for the scope (a group's members live on different GPUs, and
+// a re-run grows device buffers: they must land on this batcher's device)
+struct DeviceScope {
+    int prev = -1, dev;
+    explicit DeviceScope(int d) : dev(d) {
+        if (dev < 0) return;
+        (void)hipGetDevice(&prev);
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceScope() {
+        if (dev >= 0 && prev >= 0 && prev != dev) (void)hipSetDevice(prev);
+    }
+};
+
 int complete_device(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
+    DeviceScope ds(b->cfg.device);
     int rc = q.launch_rc;
     if (!rc) {
         const auto tw = std::chrono::steady_clock::now();
@@ -717,7 +783,12 @@ int complete_device(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
             const uint64_t e = (uint64_t)r.first_frame + r.n_frames;
             if (r.first_status != UVHTTP_WS_FRAME_ERR_CAPACITY && r.n_frames && e > wframes) wframes = e;
         }
-        // (the descriptors came back with the results: launch_device / rerun_over_capacity)
+        // the descriptors came back with the results (launch_device / rerun_over_capacity)
+        // up to the high-water mark; a flush with more frames fetches the rest now
+        rc = fetch_rest(b, q.d_desc, q.h_desc, q.desc_copied, capacity ? 0 : frames);
+        if (!rc) rc = fetch_rest(b, q.d_wdesc, q.h_wdesc, q.wdesc_copied, wframes);
+        b->desc_hint = next_hint(b->desc_hint, frames);
+        if (q.nt) b->wdesc_hint = next_hint(b->wdesc_hint, wframes);
     }
     if (rc) {
         // the host decodes the plain connections instead (their reads are still in the
@@ -725,7 +796,7 @@ int complete_device(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
         // and returned
         b->st.device_errors++;
         flush_host(b, q);
-        fail_tls_slots(b, q);
+        handback_tls_slots(b, q);
         return rc;
     }
     if (capacity) {  // more plain frames than the descriptors hold (client connections)
@@ -841,7 +912,7 @@ int start_flush(uvhttp_ws_amd_batcher_t* b, bool wait) {
         if (lr == 1) {
             b->st.fallback_flushes++;
             flush_host(b, q);
-            fail_tls_slots(b, q);
+            handback_tls_slots(b, q);
             clear_queue(q);
         } else {
             // launched, or a launch error that complete_device turns into a host decode
@@ -856,14 +927,27 @@ int start_flush(uvhttp_ws_amd_batcher_t* b, bool wait) {
     return rc;
 }
 
-// loop-thread time spent inside one batcher call (waiting, staging, delivering)
+constexpr size_t kBlockedKeep = 65536;
+
+// loop-thread time spent inside one batcher call (waiting, staging, delivering): summed, kept
+// per call for the percentiles, and the longest call's split by phase
 struct Blocked {
     uvhttp_ws_amd_batcher_t* b;
     std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    double wait0 = b->st.wait_ms, stage0 = b->st.stage_ms, deliver0 = b->st.deliver_ms;
     ~Blocked() {
         const double ms = ms_since(t0);
         b->st.blocked_ms += ms;
-        if (ms > b->st.max_blocked_ms) b->st.max_blocked_ms = ms;
+        b->st.blocked_calls++;
+        if (b->blocked.size() < kBlockedKeep) b->blocked.push_back((float)ms);
+        else b->blocked[b->blocked_n % kBlockedKeep] = (float)ms;
+        b->blocked_n++;
+        if (ms > b->st.max_blocked_ms) {
+            b->st.max_blocked_ms = ms;
+            b->st.max_blocked_wait_ms = b->st.wait_ms - wait0;
+            b->st.max_blocked_stage_ms = b->st.stage_ms - stage0;
+            b->st.max_blocked_deliver_ms = b->st.deliver_ms - deliver0;
+        }
     }
 };
 
@@ -1001,7 +1085,15 @@ uvhttp_error_t queue_read(uvhttp_ws_amd_batcher_t* b, uvhttp_ws_connection_t* co
         (void)start_flush(b, true);  // (a device error there was decoded on the host and counted)
         if (b->failed.count(conn)) return UVHTTP_ERROR_INVALID_PARAM;
         if (tls && !b->tls.count(conn)) return UVHTTP_ERROR_INVALID_PARAM;  // handed back
-        const uint64_t pre2 = align16(prefix_bound(b, conn)) + 16 + carry;
+        uint64_t pre2 = align16(prefix_bound(b, conn)) + 16 + carry;
+        if (pre2 + len > b->cfg.max_bytes && b->q[b->cur ^ 1].in_flight) {
+            // too large only because the queue just handed over still holds reads of this
+            // connection (prefix_bound counts them): deliver it, then the prefix is exact
+            (void)finish_inflight(b, true);
+            if (b->failed.count(conn)) return UVHTTP_ERROR_INVALID_PARAM;
+            if (tls && !b->tls.count(conn)) return UVHTTP_ERROR_INVALID_PARAM;
+            pre2 = align16(prefix_bound(b, conn)) + 16 + carry;
+        }
         if (pre2 + len > b->cfg.max_bytes) {
             if (tls) {
                 // ciphertext can be cut anywhere (records reassemble across flushes): queue it
@@ -1089,7 +1181,10 @@ int uvhttp_ws_amd_batcher_set_tls(uvhttp_ws_amd_batcher_t* b, struct uvhttp_ws_c
     // follows them: flush them first
     for (int i = 0; i < 2; ++i) {
         auto it = b->q[i].slot_of.find(conn);
-        if (it != b->q[i].slot_of.end() && !b->q[i].slots[it->second].tls && !b->delivering) {
+        if (it != b->q[i].slot_of.end() && !b->q[i].slots[it->second].tls) {
+            // (inside a batcher callback no flush can run: refuse rather than register a TLS
+            // connection whose queued plain reads would then be unreachable)
+            if (b->delivering) return UVHTTP_WS_GPU_EINVAL;
             Blocked bl{b};
             (void)start_flush(b, true);
             (void)finish_inflight(b, true);
@@ -1150,10 +1245,25 @@ int uvhttp_ws_amd_batcher_numa_node(const uvhttp_ws_amd_batcher_t* b) {
     return node;
 }
 
+void uvhttp_ws_amd_batcher_reset_stats(uvhttp_ws_amd_batcher_t* b) {
+    if (!b) return;
+    memset(&b->st, 0, sizeof(b->st));
+    b->blocked.clear();
+    b->blocked_n = 0;
+}
+
 int uvhttp_ws_amd_batcher_stats(const uvhttp_ws_amd_batcher_t* b,
                                 uvhttp_ws_amd_batcher_stats_t* out) {
     if (!b || !out) return UVHTTP_WS_GPU_EINVAL;
     *out = b->st;
+    if (!b->blocked.empty()) {
+        std::vector<float> v(b->blocked);
+        const size_t i50 = (v.size() - 1) / 2, i99 = (v.size() - 1) * 99 / 100;
+        std::nth_element(v.begin(), v.begin() + i50, v.end());
+        out->blocked_p50_ms = v[i50];
+        std::nth_element(v.begin(), v.begin() + i99, v.end());
+        out->blocked_p99_ms = v[i99];
+    }
     return UVHTTP_WS_GPU_OK;
 }
 

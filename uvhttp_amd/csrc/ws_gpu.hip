@@ -274,6 +274,51 @@ struct BatchArgs {
     uvhttp_ws_batch_summary_t* summary;  // batch mode: written by k_finalize
     uint32_t plan_frames;    // frames per k_plan block (kBlock * FPT)
     uint32_t no_ticket;      // k_plan orders blocks by blockIdx (experiment: UVHTTP_WS_PLAN_TICKET=0)
+    uint64_t* stamp;         // device-side kernel stamps (diagnostics), or null
+};
+
+// ------------------------------------------------------------------------------------
+// Device-side kernel stamps (diagnostics, uvhttp_ws_gpu_engine_set_stamps).  With stamps
+// on, each kernel records when its first workgroups started and when its waves ended on the
+// GPU's constant wall clock, so the gaps between the kernels of a call and between
+// consecutive calls are read off the device timeline.  Plain vector stores only — atomics on
+// one address from every wave of a 262 144-workgroup payload kernel serialise across the XCDs
+// (a C3 kernel took 11 ms with them): the first 256 workgroups store their start into their own
+// word, every wave its end into word (wave index mod 4096), so each word ends up holding one
+// of the last waves to run.  Slots form a ring keyed by the call's epoch and every word is
+// tagged (epoch << 40) | t, so the reader keeps the newest call of each slot without a reset.
+// ------------------------------------------------------------------------------------
+constexpr uint32_t kStampRing = 16, kStampKinds = 16, kStampBegin = 256, kStampEnd = 4096;
+constexpr uint64_t kStampPer = kStampBegin + kStampEnd;
+constexpr uint64_t kStampLow = (1ull << 40) - 1;
+constexpr uint64_t kStampWords = (uint64_t)kStampRing * kStampKinds * kStampPer;
+// experiment builds (-DUVWS_PLAN_PHASES, tools/build_variant.sh): k_plan's per-block phase
+// times follow the ring, 8 words per block (uvhttp_ws_gpu_engine_debug_phases)
+constexpr uint64_t kPhaseWords = 8 * 8192;
+constexpr uint64_t kStampAlloc = kStampWords + kPhaseWords;
+
+__device__ inline uint64_t* stamp_slot(uint64_t* st, uint32_t epoch, uint32_t kind) {
+    return st + ((uint64_t)(epoch % kStampRing) * kStampKinds + kind) * kStampPer;
+}
+__device__ inline uint64_t stamp_word(uint32_t epoch) {
+    return ((uint64_t)(epoch & 0xFFFFFFu) << 40) | ((uint64_t)wall_clock64() & kStampLow);
+}
+
+struct StampScope {
+    uint64_t* st;
+    uint32_t epoch, kind;
+    __device__ StampScope(uint64_t* st_, uint32_t epoch_, uint32_t kind_) : st(st_), epoch(epoch_), kind(kind_) {
+        if (st && threadIdx.x == 0 && blockIdx.x < kStampBegin)
+            stamp_slot(st, epoch, kind)[blockIdx.x] = stamp_word(epoch);
+    }
+    // runs at every return of the kernel: the first active lane of each wave stores its end
+    __device__ ~StampScope() {
+        if (!st) return;
+        const uint64_t act = __ballot(1);
+        if ((threadIdx.x & 63) != (uint32_t)__builtin_ctzll(act)) return;
+        const uint32_t w = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % kStampEnd;
+        stamp_slot(st, epoch, kind)[kStampBegin + w] = stamp_word(epoch);
+    }
 };
 
 // every kernel of a call resolves its epoch: a captured call reads the one the replay's
@@ -795,6 +840,7 @@ template <int FPT, int NT = kBlock>
 __global__ __launch_bounds__(NT) void k_plan(BatchArgs a, uvhttp_ws_frame_desc_t* desc,
                                                  uvhttp_ws_message_desc_t* msgs, Workspace ws) {
     resolve_epoch(a, ws);
+    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_PLAN);
     __shared__ uint32_t s_ticket;
     if (threadIdx.x == 0) {
         uint32_t t = blockIdx.x;
@@ -809,6 +855,27 @@ __global__ __launch_bounds__(NT) void k_plan(BatchArgs a, uvhttp_ws_frame_desc_t
     const uint32_t b = s_ticket;
     const uint32_t n = nframes(a);
     const uint32_t i0 = (b * NT + threadIdx.x) * FPT;
+#ifdef UVWS_PLAN_PHASES
+    // per block: [0] start (after the ticket) [1] thread 0's pass 1 done [2] block scan done
+    // [3] look-back done [4] thread 0's pass 2 done [5] latest wave end, [6] blockIdx, [7] CU id
+    unsigned long long* ph = a.stamp && b < 8192 ? reinterpret_cast<unsigned long long*>(a.stamp + kStampWords + 8ull * b) : nullptr;
+    auto phase = [&](int k) {
+        if (ph && threadIdx.x == 0) ph[k] = (unsigned long long)wall_clock64();
+    };
+    phase(0);
+    if (ph && threadIdx.x == 0) {
+        ph[6] = blockIdx.x;
+        ph[7] = __smid();
+    }
+    struct PhaseEnd {
+        unsigned long long* p;
+        __device__ ~PhaseEnd() {
+            if (p && (threadIdx.x & 63) == 0) atomicMax(p + 5, (unsigned long long)wall_clock64());
+        }
+    } phase_end_{ph};
+#else
+    auto phase = [](int) {};
+#endif
     if (FPT == 1) {
         SegInfo g;
         uvhttp_ws_frame_desc_t d;
@@ -860,10 +927,14 @@ __global__ __launch_bounds__(NT) void k_plan(BatchArgs a, uvhttp_ws_frame_desc_t
             if (i < n) tagg = scan_combine(tagg, parse_hdr(a, i, seg_info(a, i, n), o[k], hv[k], dv[k]));
         }
     }
+    phase(1);
     ScanElem agg;
     const ScanElem local = block_exclusive_scan<NT>(tagg, &agg);
+    phase(2);
     ScanElem run = scan_combine(lookback_prefix<NT>(ws, b, agg, a.epoch, a.max_polls), local);
+    phase(3);
     plan_pass2<FPT>(a, desc, msgs, ws, i0, n, run, dv);
+    phase(4);
 }
 
 // ------------------------------------------------------------------------------------
@@ -995,6 +1066,7 @@ __device__ inline void finalize_frames(const BatchArgs& a, uvhttp_ws_frame_desc_
 __global__ __launch_bounds__(kBlock) void k_finalize(BatchArgs a, uvhttp_ws_frame_desc_t* desc,
                                                      Workspace ws) {
     resolve_epoch(a, ws);
+    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_FINALIZE);
     finalize_frames(a, desc, ws, blockIdx.x, kBlock, first_bad_of(a, ws, a.n));
 }
 
@@ -1186,6 +1258,7 @@ template <int BLOCK, int VPT, int STORE_AUX = 0>
 __global__ __launch_bounds__(BLOCK) void k_unmask_inplace(
     BatchArgs a, const uvhttp_ws_frame_desc_t* __restrict__ desc, Workspace ws,
     uint64_t tile_base) {
+    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_PAYLOAD);
     uint32_t n, nb;
     unmask_tile<BLOCK, VPT, STORE_AUX>(a, desc, ws, tile_base, n, nb);  // resolves the epoch
     // batch in-place decode: the first ceil(n / BLOCK) workgroups then do k_finalize's work
@@ -1260,6 +1333,7 @@ __device__ inline void add_mask_rel(u32x4& m, int32_t r, int32_t ps, int32_t pe,
 
 template <int BLOCK, int VPT, int AUX = 18>
 __global__ __launch_bounds__(BLOCK) void k_unmask_stride(BatchArgs a, uint64_t tile_base) {
+    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_PAYLOAD);
     constexpr uint64_t kT = (uint64_t)BLOCK * VPT * 16;
     constexpr int kMaxF = (int)(kT / kFusedMinStride) + 2;  // frames touching one tile
     __shared__ u32x4 s_tile[BLOCK * VPT + 1];               // the tile + the 16 bytes after
@@ -1423,6 +1497,7 @@ __device__ inline void remask_range(uint8_t* wire, uint64_t ps, uint64_t pe, uin
 __global__ __launch_bounds__(kBlock) void k_fixup(BatchArgs a, uvhttp_ws_frame_desc_t* desc,
                                                   Workspace ws) {
     resolve_epoch(a, ws);
+    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_FIXUP);
     const uint32_t n = a.n;
     const uint32_t nb = first_bad_of(a, ws, n);
     const bool fault = device_fault(a, ws);
@@ -1636,6 +1711,7 @@ __global__ __launch_bounds__(BLOCK) void k_gather_compact(
     BatchArgs a, const uvhttp_ws_frame_desc_t* __restrict__ desc, Workspace ws,
     uint64_t arena_bytes_cap, uint64_t tile_base) {
     resolve_epoch(a, ws);
+    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_PAYLOAD);
     const uint32_t n = nframes(a);
     gather_tile<BLOCK, VPT>(a, desc, ws, arena_bytes_cap, tile_base, n, first_bad_of(a, ws, n));
     // (k_finalize stays a launch of its own here: folding it in like k_scatter_compact cost
@@ -1800,6 +1876,7 @@ template <int BLOCK, int VPT>
 __global__ __launch_bounds__(BLOCK) void k_scatter_compact(
     BatchArgs a, const uvhttp_ws_frame_desc_t* __restrict__ desc, Workspace ws,
     uint64_t arena_bytes_cap, uint64_t tile_base) {
+    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_PAYLOAD);
     scatter_tile<BLOCK, VPT>(a, desc, ws, arena_bytes_cap, tile_base);
     // k_finalize's work at the end of the first ceil(n / BLOCK) workgroups, as the in-place
     // kernel does (statuses after the first failure, control payloads unmasked in the wire —
@@ -1852,6 +1929,7 @@ struct WalkArgs {
     uint32_t epoch;            // this call's tag (dev_epoch: ctl[kCtlEpoch])
     uint32_t dev_epoch;
     const uint32_t* ctl;
+    uint64_t* stamp;           // device-side kernel stamps (diagnostics), or null
 };
 
 // process_data's buffer growth: returns false on failure (*out = size then), else the size
@@ -2143,6 +2221,7 @@ __device__ inline uint32_t walk_lane(const WalkArgs& w, uint32_t s, uint32_t lf)
 
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void k_swalk_lane(WalkArgs w) {
+    StampScope stamp_(w.stamp, w.epoch, MODE == 1 ? UVHTTP_WS_STAMP_WALK2 : UVHTTP_WS_STAMP_WALK);
     const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t lf = MODE == 1 ? lane_first(w, s) : 0;  // (before any thread leaves)
     uint32_t count = 0;
@@ -2415,6 +2494,7 @@ __device__ inline void walk_wave(const WalkArgs& w, uint32_t s, uint8_t* ring) {
 
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void k_swalk_wave(WalkArgs w) {
+    StampScope stamp_(w.stamp, w.epoch, MODE == 1 ? UVHTTP_WS_STAMP_WALK2 : UVHTTP_WS_STAMP_WALK);
     __shared__ __attribute__((aligned(16))) uint8_t ring[kBlock / 64][kRingBytes];
     // readfirstlane: the connection (and all walk state derived from it) is wave-uniform, so
     // it lives in scalar registers and the walk's branches are scalar branches
@@ -2430,6 +2510,7 @@ __global__ __launch_bounds__(kBlock) void k_swalk_wave(WalkArgs w) {
 // 16384 connections) writes every connection's first frame itself.  Each thread takes a
 // contiguous chunk: sum it, scan the sums across the block, then write the chunk's prefixes.
 __global__ __launch_bounds__(kBlock) void k_swalk_scan(WalkArgs w, uint32_t lane_mode) {
+    StampScope stamp_(w.stamp, w.epoch, UVHTTP_WS_STAMP_WALK_SCAN);
     const uint32_t m = lane_mode ? (w.n_streams + kBlock - 1) / kBlock : w.n_streams;
     const uint32_t per = (m + kBlock - 1) / kBlock;
     const uint32_t beg = threadIdx.x * per;
@@ -2506,6 +2587,7 @@ __device__ inline void capacity_result(uvhttp_ws_stream_result_t& r) {
 
 // lane mode: one lane per connection (few frames each) writes its descriptors in order
 __global__ __launch_bounds__(kBlock) void k_stream_desc_lane(WalkArgs w) {
+    StampScope stamp_(w.stamp, w.epoch, UVHTTP_WS_STAMP_STREAM_DESC);
     const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t first = lane_first(w, s);
     if (s >= w.n_streams) return;
@@ -2539,6 +2621,7 @@ __global__ __launch_bounds__(kBlock) void k_stream_desc_lane(WalkArgs w) {
 // before the frame in its connection), MSG_END, the failing frame's status, and each
 // frame's end for the tile claims.  Capacity overflow: every result says so, nothing else.
 __global__ __launch_bounds__(kBlock) void k_stream_desc(WalkArgs w) {
+    StampScope stamp_(w.stamp, w.epoch, UVHTTP_WS_STAMP_STREAM_DESC);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint32_t s = blockIdx.x * (kBlock / 64) + wave;
     if (s >= w.n_streams) return;
@@ -2635,6 +2718,7 @@ __global__ __launch_bounds__(kBlock) void k_stream_desc(WalkArgs w) {
 __global__ __launch_bounds__(kBlock) void k_stream_claims(BatchArgs a, Workspace ws,
                                                           const uint64_t* frame_end) {
     resolve_epoch(a, ws);
+    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_CLAIMS);
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t n = nframes(a);
     if (i >= n) return;
@@ -3278,6 +3362,8 @@ struct uvhttp_ws_gpu_engine {
     uint32_t* ctl;             // device control words (kCtl*), own allocation
     uint32_t faults_seen;      // ctl[kCtlFaults] at the last engine_sync
     uint32_t max_polls;        // look-back wait bound (UVHTTP_WS_MAX_POLLS: tests)
+    uint64_t* stamp_mem;       // device-side kernel stamps (kStampWords), null until enabled
+    int stamp_on;
     int capturing;             // the current call is being captured into a graph
     hipStream_t last_stream;   // stream of the previous call (calls are serialised on it)
     int have_last;
@@ -3400,6 +3486,7 @@ void uvhttp_ws_gpu_engine_free(uvhttp_ws_gpu_engine_t* e) {
     if (e->wt_mem) (void)hipFree(e->wt_mem);
     if (e->wr_mem) (void)hipFree(e->wr_mem);
     if (e->ctl) (void)hipFree(e->ctl);
+    if (e->stamp_mem) (void)hipFree(e->stamp_mem);
     if (e->order_ev) (void)hipEventDestroy(e->order_ev);
     for (int k = 0; k < e->ev_created; ++k) (void)hipEventDestroy(e->ev[k]);
     (void)hipSetDevice(prev);
@@ -3546,6 +3633,101 @@ int uvhttp_ws_gpu_engine_kernel_time(uvhttp_ws_gpu_engine_t* e, double* ms, uint
     e->launches = 0;
     return UVHTTP_WS_GPU_OK;
 }
+
+int uvhttp_ws_gpu_engine_set_stamps(uvhttp_ws_gpu_engine_t* e, int enable) {
+    if (!e) return UVHTTP_WS_GPU_EINVAL;
+    if (enable && !e->stamp_mem) {
+        int prev = 0;
+        (void)hipGetDevice(&prev);
+        (void)hipSetDevice(e->device);
+        hipError_t h = hipMalloc(&e->stamp_mem, kStampAlloc * 8);
+        if (h == hipSuccess) h = hipMemset(e->stamp_mem, 0, kStampAlloc * 8);
+        if (h == hipSuccess) h = hipDeviceSynchronize();
+        (void)hipSetDevice(prev);
+        if (h != hipSuccess) {
+            if (e->stamp_mem) (void)hipFree(e->stamp_mem);
+            e->stamp_mem = nullptr;
+            return set_err(e, UVHTTP_WS_GPU_ENOMEM, "hipMalloc stamps", h);
+        }
+    }
+    e->stamp_on = enable ? 1 : 0;
+    return UVHTTP_WS_GPU_OK;
+}
+
+int uvhttp_ws_gpu_engine_read_stamps(uvhttp_ws_gpu_engine_t* e, uvhttp_ws_gpu_stamp_t* out,
+                                     uint32_t cap, uint32_t* n_out) {
+    if (!e || (!out && cap) || !n_out) return UVHTTP_WS_GPU_EINVAL;
+    *n_out = 0;
+    if (!e->stamp_mem) return UVHTTP_WS_GPU_OK;
+    uint64_t* host = (uint64_t*)malloc(kStampWords * 8);
+    if (!host) return UVHTTP_WS_GPU_ENOMEM;
+    int prev = 0, khz = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(e->device);
+    hipError_t h = hipDeviceSynchronize();
+    if (h == hipSuccess) h = hipMemcpy(host, e->stamp_mem, kStampWords * 8, hipMemcpyDeviceToHost);
+    if (h == hipSuccess) h = hipMemset(e->stamp_mem, 0, kStampWords * 8);
+    if (h == hipSuccess) h = hipDeviceSynchronize();
+    if (h == hipSuccess && hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, e->device) != hipSuccess)
+        khz = 0;
+    (void)hipSetDevice(prev);
+    if (h != hipSuccess) {
+        free(host);
+        return set_err(e, UVHTTP_WS_GPU_ELAUNCH, "read stamps", h);
+    }
+    if (khz <= 0) khz = 100000;  // gfx9 wall clock: 100 MHz
+    uint32_t n = 0;
+    for (uint32_t r = 0; r < kStampRing; ++r) {
+        for (uint32_t k = 0; k < kStampKinds; ++k) {
+            const uint64_t* sl = host + ((uint64_t)r * kStampKinds + k) * kStampPer;
+            uint64_t tag = 0;  // the newest call that stamped this slot
+            for (uint64_t j = 0; j < kStampPer; ++j) tag = (sl[j] >> 40) > tag ? (sl[j] >> 40) : tag;
+            if (!tag) continue;
+            uint64_t b = ~0ull, en = 0;
+            for (uint64_t j = 0; j < kStampPer; ++j) {
+                if ((sl[j] >> 40) != tag) continue;
+                const uint64_t t = sl[j] & kStampLow;
+                if (j < kStampBegin) b = t < b ? t : b;
+                else en = t > en ? t : en;
+            }
+            if (b == ~0ull || !en) continue;
+            if (n < cap) {
+                out[n].call = (uint32_t)tag;
+                out[n].kernel = k;
+                out[n].begin_ns = b * 1000000ull / (uint64_t)khz;
+                out[n].end_ns = en * 1000000ull / (uint64_t)khz;
+            }
+            ++n;
+        }
+    }
+    free(host);
+    if (n > cap) n = cap;
+    // call order (tags increase by one per call), then start order within a call
+    for (uint32_t i = 1; i < n; ++i) {
+        const uvhttp_ws_gpu_stamp_t x = out[i];
+        uint32_t j = i;
+        while (j > 0 && (out[j - 1].call > x.call ||
+                         (out[j - 1].call == x.call && out[j - 1].begin_ns > x.begin_ns))) {
+            out[j] = out[j - 1];
+            --j;
+        }
+        out[j] = x;
+    }
+    *n_out = n;
+    return UVHTTP_WS_GPU_OK;
+}
+
+#ifdef UVWS_PLAN_PHASES
+// experiment builds only: copy k_plan's per-block phase words (8 per block) and clear them
+extern "C" int uvhttp_ws_gpu_engine_debug_phases(uvhttp_ws_gpu_engine_t* e, uint64_t* out, uint32_t blocks) {
+    if (!e || !e->stamp_mem || blocks > 8192) return UVHTTP_WS_GPU_EINVAL;
+    (void)hipDeviceSynchronize();
+    hipError_t h = hipMemcpy(out, e->stamp_mem + kStampWords, 64ull * blocks, hipMemcpyDeviceToHost);
+    if (h == hipSuccess) h = hipMemset(e->stamp_mem + kStampWords, 0, 8 * kPhaseWords);
+    if (h == hipSuccess) h = hipDeviceSynchronize();
+    return h == hipSuccess ? 0 : UVHTTP_WS_GPU_ELAUNCH;
+}
+#endif
 
 static int timing_begin(uvhttp_ws_gpu_engine_t* e, hipStream_t s) {
     if (!e->timing || e->capturing) return -1;
@@ -3714,6 +3896,7 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
     a.max_polls = e->max_polls;
     a.dev_epoch = e->capturing ? 1u : 0u;
     a.epoch = next_epoch(e, s);
+    a.stamp = (e->stamp_on && !e->capturing) ? e->stamp_mem : nullptr;
 
     // stride batches in place: the fused path (payload pass parses the headers, k_plan runs
     // on its records, k_fixup undoes what a failure must leave untouched)
@@ -3995,6 +4178,7 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     w.sc.walk_tmp = (uint32_t*)e->wt_mem;
     w.sc.walk_rec = (w.single && e->wr_cap >= want && e->wr_rec_on) ? (uint2*)e->wr_mem : nullptr;
     w.agg = e->ss.agg;
+    w.stamp = (e->stamp_on && !e->capturing) ? e->stamp_mem : nullptr;
     const uint32_t nsb = (n_streams + kBlock - 1) / kBlock;
     const uint32_t nwb = (n_streams + kBlock / 64 - 1) / (kBlock / 64);
     const int tk_chain = e->time_chain ? timing_begin(e, s) : -1;
@@ -4024,6 +4208,7 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     a.max_polls = e->max_polls;
     a.dev_epoch = w.dev_epoch;
     a.epoch = w.epoch;
+    a.stamp = w.stamp;
     // (the wave path's k_stream_desc claimed the tile map already)
     if (!wave_walk)
         hipLaunchKernelGGL(k_stream_claims, dim3((cap + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a,

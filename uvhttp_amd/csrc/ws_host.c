@@ -439,7 +439,9 @@ uvhttp_error_t uvhttp_ws_deliver_stream(struct uvhttp_ws_connection* c, const ui
  * streaming stores only far above libuv's 16 KiB reads).  32-byte AVX2 streaming stores where
  * the CPU has them: 91 GB/s into pinned memory on the MI355X box's EPYC 9575F against 54-59 GB/s
  * for 16-byte SSE2 ones and 45 GB/s for memcpy (tools/copy_probe.cpp,
- * profiles/r03p42_copy_probe.jsonl). */
+ * profiles/r03p42_copy_probe.jsonl).  Other targets (the host decoder builds anywhere) copy
+ * with memcpy and fence with a full barrier. */
+#if defined(__x86_64__) || defined(__i386__)
 #include <immintrin.h>
 
 __attribute__((target("avx2"))) static void copy_stream_avx2(uint8_t* d, const uint8_t* s, size_t len) {
@@ -491,9 +493,15 @@ static void copy_stream_sse2(uint8_t* d, const uint8_t* s, size_t len) {
  * per 16 KiB read: a fence per call cost a third of the copy rate (58.8 vs 91 GB/s,
  * profiles/r03p44_numa_copy_e2e.txt). */
 __attribute__((visibility("hidden"))) void uvhttp_ws_amd_copy_fence(void) { _mm_sfence(); }
+#else
+__attribute__((visibility("hidden"))) void uvhttp_ws_amd_copy_fence(void) {
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+}
+#endif
 
 __attribute__((visibility("hidden"))) void uvhttp_ws_amd_copy_stream(void* dst, const void* src,
                                                                      size_t len) {
+#if defined(__x86_64__) || defined(__i386__)
     static int have_avx2 = -1;
     if (len < 1024) {
         memcpy(dst, src, len);
@@ -507,4 +515,7 @@ __attribute__((visibility("hidden"))) void uvhttp_ws_amd_copy_stream(void* dst, 
         copy_stream_avx2((uint8_t*)dst, (const uint8_t*)src, len);
     else
         copy_stream_sse2((uint8_t*)dst, (const uint8_t*)src, len);
+#else
+    memcpy(dst, src, len);
+#endif
 }
