@@ -300,24 +300,45 @@ constexpr uint64_t kStampAlloc = kStampWords + kPhaseWords;
 __device__ inline uint64_t* stamp_slot(uint64_t* st, uint32_t epoch, uint32_t kind) {
     return st + ((uint64_t)(epoch % kStampRing) * kStampKinds + kind) * kStampPer;
 }
+// the constant-rate wall clock (100 MHz).  Inline asm without a memory clobber: the builtin
+// counts as a memory access, so a clock read at a kernel's start turned every later uniform
+// workspace load into a vector load (the compiler could no longer prove them unclobbered)
+__device__ inline uint64_t stamp_clock() {
+    uint64_t t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t));
+    return t;
+}
 __device__ inline uint64_t stamp_word(uint32_t epoch) {
-    return ((uint64_t)(epoch & 0xFFFFFFu) << 40) | ((uint64_t)wall_clock64() & kStampLow);
+    return ((uint64_t)(epoch & 0xFFFFFFu) << 40) | (stamp_clock() & kStampLow);
 }
 
+// One per kernel; both words are stored when the workgroup's threads return (no store may come
+// first: a global store ahead of the payload kernels' uniform workspace loads — tile map,
+// first_bad, descriptors — turns them into vector loads, and so does a clock read, which the
+// compiler must treat as a memory access: C3's payload kernel took 1.92 ms instead of 1.25
+// with stamps off, profiles/r04_ab_stampoff2.txt).  So the kernels whose uniform loads matter
+// (payload kernels, walks, descriptors: at_start = false) read no clock at their start; their
+// "begin" is the earliest END among their first 256 workgroups — late by one workgroup's
+// duration (about 1-3 us for the payload tiles).  The others (k_plan, scans, fix-ups) read the
+// clock when they start.
 struct StampScope {
     uint64_t* st;
     uint32_t epoch, kind;
-    __device__ StampScope(uint64_t* st_, uint32_t epoch_, uint32_t kind_) : st(st_), epoch(epoch_), kind(kind_) {
-        if (st && threadIdx.x == 0 && blockIdx.x < kStampBegin)
-            stamp_slot(st, epoch, kind)[blockIdx.x] = stamp_word(epoch);
-    }
-    // runs at every return of the kernel: the first active lane of each wave stores its end
+    uint64_t t0;
+    __device__ StampScope(uint64_t* st_, uint32_t epoch_, uint32_t kind_, bool at_start = true)
+        : st(st_), epoch(epoch_), kind(kind_), t0(at_start ? stamp_clock() : 0) {}
+    // runs at every return of the kernel: thread 0 of the first workgroups stores the start,
+    // the first active lane of each wave its end
     __device__ ~StampScope() {
         if (!st) return;
+        uint64_t* sl = stamp_slot(st, epoch, kind);
+        const uint64_t tag = (uint64_t)(epoch & 0xFFFFFFu) << 40;
+        const uint64_t now = stamp_clock();
+        if (threadIdx.x == 0 && blockIdx.x < kStampBegin) sl[blockIdx.x] = tag | ((t0 ? t0 : now) & kStampLow);
         const uint64_t act = __ballot(1);
         if ((threadIdx.x & 63) != (uint32_t)__builtin_ctzll(act)) return;
         const uint32_t w = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % kStampEnd;
-        stamp_slot(st, epoch, kind)[kStampBegin + w] = stamp_word(epoch);
+        sl[kStampBegin + w] = tag | (now & kStampLow);
     }
 };
 
@@ -809,6 +830,17 @@ __device__ inline ScanElem rec_pass1(const BatchArgs& a, uint32_t i0, uint32_t n
     return tagg;
 }
 
+// one descriptor store (UVWS_DESC_NT, experiment: two streaming 16-byte stores)
+__device__ inline void store_desc(uvhttp_ws_frame_desc_t* desc, uint32_t i, const uvhttp_ws_frame_desc_t& d) {
+#ifdef UVWS_DESC_NT
+    const u32x4* w = reinterpret_cast<const u32x4*>(&d);
+    __builtin_nontemporal_store(w[0], reinterpret_cast<u32x4*>(desc + i));
+    __builtin_nontemporal_store(w[1], reinterpret_cast<u32x4*>(desc + i) + 1);
+#else
+    desc[i] = d;
+#endif
+}
+
 // pass 2: the state machine in frame order from the lane's exclusive prefix `run`; each
 // descriptor is stored once
 template <int FPT>
@@ -824,7 +856,7 @@ __device__ inline void plan_pass2(const BatchArgs& a, uvhttp_ws_frame_desc_t* de
             if (dv[k].status == UVHTTP_WS_FRAME_OK) e = scan_elem_of(dv[k], (int32_t)i, g.head);
             else if (g.head) e.bits = kHead;
             resolve_one(a, msgs, ws, i, n, g, run, dv[k]);
-            desc[i] = dv[k];
+            store_desc(desc, i, dv[k]);
             run = scan_combine(run, e);
         }
     }
@@ -1258,7 +1290,7 @@ template <int BLOCK, int VPT, int STORE_AUX = 0>
 __global__ __launch_bounds__(BLOCK) void k_unmask_inplace(
     BatchArgs a, const uvhttp_ws_frame_desc_t* __restrict__ desc, Workspace ws,
     uint64_t tile_base) {
-    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_PAYLOAD);
+    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_PAYLOAD, false);
     uint32_t n, nb;
     unmask_tile<BLOCK, VPT, STORE_AUX>(a, desc, ws, tile_base, n, nb);  // resolves the epoch
     // batch in-place decode: the first ceil(n / BLOCK) workgroups then do k_finalize's work
@@ -1333,7 +1365,7 @@ __device__ inline void add_mask_rel(u32x4& m, int32_t r, int32_t ps, int32_t pe,
 
 template <int BLOCK, int VPT, int AUX = 18>
 __global__ __launch_bounds__(BLOCK) void k_unmask_stride(BatchArgs a, uint64_t tile_base) {
-    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_PAYLOAD);
+    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_PAYLOAD, false);
     constexpr uint64_t kT = (uint64_t)BLOCK * VPT * 16;
     constexpr int kMaxF = (int)(kT / kFusedMinStride) + 2;  // frames touching one tile
     __shared__ u32x4 s_tile[BLOCK * VPT + 1];               // the tile + the 16 bytes after
@@ -1711,7 +1743,7 @@ __global__ __launch_bounds__(BLOCK) void k_gather_compact(
     BatchArgs a, const uvhttp_ws_frame_desc_t* __restrict__ desc, Workspace ws,
     uint64_t arena_bytes_cap, uint64_t tile_base) {
     resolve_epoch(a, ws);
-    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_PAYLOAD);
+    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_PAYLOAD, false);
     const uint32_t n = nframes(a);
     gather_tile<BLOCK, VPT>(a, desc, ws, arena_bytes_cap, tile_base, n, first_bad_of(a, ws, n));
     // (k_finalize stays a launch of its own here: folding it in like k_scatter_compact cost
@@ -1730,6 +1762,31 @@ __global__ __launch_bounds__(BLOCK) void k_gather_compact(
 // ------------------------------------------------------------------------------------
 // bytes [0, n) of v (little-endian) to p, n <= 16
 __device__ inline void store_lo_bytes(uint8_t* p, unsigned __int128 v, int n) {
+#ifdef UVWS_SCATTER_NT
+    // (experiment: streaming stores, so no dirty arena lines are left behind in the caches)
+    if (n == 16) {
+        const u32x4 x = {(uint32_t)v, (uint32_t)(v >> 32), (uint32_t)(v >> 64), (uint32_t)(v >> 96)};
+        __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(p));
+        return;
+    }
+    if (n & 8) {
+        __builtin_nontemporal_store((uint64_t)v, reinterpret_cast<uint64_t*>(p));
+        p += 8;
+        v >>= 64;
+    }
+    if (n & 4) {
+        __builtin_nontemporal_store((uint32_t)v, reinterpret_cast<uint32_t*>(p));
+        p += 4;
+        v >>= 32;
+    }
+    if (n & 2) {
+        __builtin_nontemporal_store((uint16_t)v, reinterpret_cast<uint16_t*>(p));
+        p += 2;
+        v >>= 16;
+    }
+    if (n & 1) __builtin_nontemporal_store((uint8_t)v, p);
+    return;
+#endif
     if (n == 16) {
         __builtin_memcpy(p, &v, 16);
         return;
@@ -1876,7 +1933,7 @@ template <int BLOCK, int VPT>
 __global__ __launch_bounds__(BLOCK) void k_scatter_compact(
     BatchArgs a, const uvhttp_ws_frame_desc_t* __restrict__ desc, Workspace ws,
     uint64_t arena_bytes_cap, uint64_t tile_base) {
-    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_PAYLOAD);
+    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_PAYLOAD, false);
     scatter_tile<BLOCK, VPT>(a, desc, ws, arena_bytes_cap, tile_base);
     // k_finalize's work at the end of the first ceil(n / BLOCK) workgroups, as the in-place
     // kernel does (statuses after the first failure, control payloads unmasked in the wire —
@@ -2221,7 +2278,7 @@ __device__ inline uint32_t walk_lane(const WalkArgs& w, uint32_t s, uint32_t lf)
 
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void k_swalk_lane(WalkArgs w) {
-    StampScope stamp_(w.stamp, w.epoch, MODE == 1 ? UVHTTP_WS_STAMP_WALK2 : UVHTTP_WS_STAMP_WALK);
+    StampScope stamp_(w.stamp, w.epoch, MODE == 1 ? UVHTTP_WS_STAMP_WALK2 : UVHTTP_WS_STAMP_WALK, false);
     const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t lf = MODE == 1 ? lane_first(w, s) : 0;  // (before any thread leaves)
     uint32_t count = 0;
@@ -2494,7 +2551,7 @@ __device__ inline void walk_wave(const WalkArgs& w, uint32_t s, uint8_t* ring) {
 
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void k_swalk_wave(WalkArgs w) {
-    StampScope stamp_(w.stamp, w.epoch, MODE == 1 ? UVHTTP_WS_STAMP_WALK2 : UVHTTP_WS_STAMP_WALK);
+    StampScope stamp_(w.stamp, w.epoch, MODE == 1 ? UVHTTP_WS_STAMP_WALK2 : UVHTTP_WS_STAMP_WALK, false);
     __shared__ __attribute__((aligned(16))) uint8_t ring[kBlock / 64][kRingBytes];
     // readfirstlane: the connection (and all walk state derived from it) is wave-uniform, so
     // it lives in scalar registers and the walk's branches are scalar branches
@@ -2587,7 +2644,7 @@ __device__ inline void capacity_result(uvhttp_ws_stream_result_t& r) {
 
 // lane mode: one lane per connection (few frames each) writes its descriptors in order
 __global__ __launch_bounds__(kBlock) void k_stream_desc_lane(WalkArgs w) {
-    StampScope stamp_(w.stamp, w.epoch, UVHTTP_WS_STAMP_STREAM_DESC);
+    StampScope stamp_(w.stamp, w.epoch, UVHTTP_WS_STAMP_STREAM_DESC, false);
     const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t first = lane_first(w, s);
     if (s >= w.n_streams) return;
@@ -2621,7 +2678,7 @@ __global__ __launch_bounds__(kBlock) void k_stream_desc_lane(WalkArgs w) {
 // before the frame in its connection), MSG_END, the failing frame's status, and each
 // frame's end for the tile claims.  Capacity overflow: every result says so, nothing else.
 __global__ __launch_bounds__(kBlock) void k_stream_desc(WalkArgs w) {
-    StampScope stamp_(w.stamp, w.epoch, UVHTTP_WS_STAMP_STREAM_DESC);
+    StampScope stamp_(w.stamp, w.epoch, UVHTTP_WS_STAMP_STREAM_DESC, false);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint32_t s = blockIdx.x * (kBlock / 64) + wave;
     if (s >= w.n_streams) return;
