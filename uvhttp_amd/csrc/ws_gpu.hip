@@ -308,9 +308,6 @@ __device__ inline uint64_t stamp_clock() {
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t));
     return t;
 }
-__device__ inline uint64_t stamp_word(uint32_t epoch) {
-    return ((uint64_t)(epoch & 0xFFFFFFu) << 40) | (stamp_clock() & kStampLow);
-}
 
 // One per kernel; both words are stored when the workgroup's threads return (no store may come
 // first: a global store ahead of the payload kernels' uniform workspace loads — tile map,
