@@ -287,6 +287,7 @@ struct BatchArgs {
 // word, every wave its end into word (wave index mod 4096), so each word ends up holding one
 // of the last waves to run.  Slots form a ring keyed by the call's epoch and every word is
 // tagged (epoch << 40) | t, so the reader keeps the newest call of each slot without a reset.
+// (Ends are stored by the last 4096 waves of a launch only, below.)
 // ------------------------------------------------------------------------------------
 constexpr uint32_t kStampRing = 16, kStampKinds = 16, kStampBegin = 256, kStampEnd = 4096;
 constexpr uint64_t kStampPer = kStampBegin + kStampEnd;
@@ -332,10 +333,16 @@ struct StampScope {
         const uint64_t tag = (uint64_t)(epoch & 0xFFFFFFu) << 40;
         const uint64_t now = stamp_clock();
         if (threadIdx.x == 0 && blockIdx.x < kStampBegin) sl[blockIdx.x] = tag | ((t0 ? t0 : now) & kStampLow);
+        // ends: the last kStampEnd waves of the launch only (dispatch is in order, so the last
+        // wave to finish is among them for the uniform payload tiles; every wave of the walk
+        // and plan launches, which have fewer) — a store from each of a C3 payload kernel's
+        // 262 144 waves slowed it by 12 %
+        const uint32_t wpb = blockDim.x >> 6;
+        const uint64_t wi = (uint64_t)blockIdx.x * wpb + (threadIdx.x >> 6);
+        if (wi + kStampEnd < (uint64_t)gridDim.x * wpb) return;
         const uint64_t act = __ballot(1);
         if ((threadIdx.x & 63) != (uint32_t)__builtin_ctzll(act)) return;
-        const uint32_t w = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % kStampEnd;
-        sl[kStampBegin + w] = tag | (now & kStampLow);
+        sl[kStampBegin + wi % kStampEnd] = tag | (now & kStampLow);
     }
 };
 
