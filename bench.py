@@ -376,6 +376,11 @@ class GpuWorkload:
         fused_max = int(os.environ.get("UVHTTP_WS_FUSED_MAX", "2560") or 2560)
         if mode == "inplace" and os.environ.get("UVHTTP_WS_FUSED", "1") != "0" and 64 <= stride <= fused_max:
             self.kernel = "k_unmask_stride"
+        # compact, the same stride range: the speculative pass (k_unmask_stride writing the
+        # arena, ws_gpu.hip run_decode) unless UVHTTP_WS_SPEC=0
+        spec_max = int(os.environ.get("UVHTTP_WS_SPEC_MAX", "2560") or 2560)
+        if mode == "compact" and os.environ.get("UVHTTP_WS_SPEC", "1") != "0" and 64 <= stride <= spec_max:
+            self.kernel = "k_unmask_stride (speculative compact pass)"
         if mode.startswith("build"):
             # send side: frame n payloads of the config (server echo: unmasked; client: masked)
             import numpy as np

@@ -386,7 +386,10 @@ int uvhttp_ws_gpu_decode_inplace(uvhttp_ws_gpu_engine_t* eng, const uvhttp_ws_ba
  * d_arena at the exclusive prefix sum of data payload lengths, so every message —
  * including a fragmented one (uvhttp_ws_fragment_append, :781-822) — is one contiguous
  * arena range described by d_msgs.  Control-frame payloads are unmasked in place in the
- * wire.  d_msgs needs room for n_frames entries; arena_cap must cover the data payload. */
+ * wire.  d_msgs needs room for n_frames entries; arena_cap must cover the data payload.
+ * Arena bytes past summary->arena_bytes (up to arena_cap) are scratch: a fixed-stride batch is
+ * decoded speculatively, and when it fails part-way the payloads of frames after the failure
+ * may have been written there. */
 int uvhttp_ws_gpu_decode_compact(uvhttp_ws_gpu_engine_t* eng, const uvhttp_ws_batch_t* batch,
                                  uint8_t* d_arena, uint64_t arena_cap,
                                  uvhttp_ws_frame_desc_t* d_desc,

@@ -197,6 +197,8 @@ struct Workspace {
     uint32_t* counters;    // [0] block ticket, [1] blocks done; reset by the last block
     uint64_t* tile_first;  // [n_tiles]: tagged first frame whose slot contains the tile start
     uint64_t* first_bad;   // [1]: tagged first failing frame of the batch
+    uint64_t* spec_bad;    // [1]: tagged first delivered frame the speculative compact pass
+                           // did not place (its arena offset or layout is not the uniform one)
     uint64_t* arena_first; // [n_arena_tiles]: tagged first data frame of the arena tile
     uint32_t* ctl;         // control words outside the clearable workspace (see kCtl*)
     void* recs;            // [n_frames] FrameRec: the fused stride path's parsed headers
@@ -275,6 +277,8 @@ struct BatchArgs {
     uint32_t plan_frames;    // frames per k_plan block (kBlock * FPT)
     uint32_t no_ticket;      // k_plan orders blocks by blockIdx (experiment: UVHTTP_WS_PLAN_TICKET=0)
     uint64_t* stamp;         // device-side kernel stamps (diagnostics), or null
+    uint64_t spec_P;         // compact stride batch, speculative pass: the uniform payload length
+                             // (frame i's payload at arena offset i * spec_P); 0 = none
 };
 
 // ------------------------------------------------------------------------------------
@@ -658,6 +662,14 @@ __device__ inline void resolve_one(const BatchArgs& a, uvhttp_ws_message_desc_t*
         d.status = (int8_t)st;
     }
     if (st != UVHTTP_WS_FRAME_OK) tag_claim(ws.first_bad, a.epoch, i);
+    // speculative compact pass (stride batches): it placed frame i's payload at i * spec_P when
+    // the frame looked uniform locally; a delivered frame anywhere else (a control frame, another
+    // length, an offset moved by an earlier frame) sends the call to the full scatter (k_spec_fix)
+    else if (a.spec_P && (!is_data_op(d.opcode) || d.payload_len != a.spec_P ||
+                          ex.data_pay != (uint64_t)i * a.spec_P ||
+                          d.header_size + ((d.flags & UVHTTP_WS_FLAG_MASK) ? 4u : 0u) !=
+                              a.frame_stride - a.spec_P))
+        tag_claim(ws.spec_bad, a.epoch, i);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1071,7 +1083,7 @@ __device__ void write_summary(const BatchArgs& a, const uvhttp_ws_frame_desc_t* 
 // kernel runs it at the end of its first blocks and the decode needs no third launch)
 __device__ inline void finalize_frames(const BatchArgs& a, uvhttp_ws_frame_desc_t* desc,
                                        const Workspace& ws, uint32_t blk, uint32_t nthr,
-                                       uint32_t nb) {
+                                       uint32_t nb, bool controls = true) {
     const uint32_t i = blk * nthr + threadIdx.x;
     if (device_fault(a, ws)) {  // nothing was delivered (the payload pass saw first_bad = 0)
         if (i < a.n) desc[i].status = UVHTTP_WS_FRAME_SKIPPED;
@@ -1087,7 +1099,7 @@ __device__ inline void finalize_frames(const BatchArgs& a, uvhttp_ws_frame_desc_
     }
     if (i < a.n) {
         if (i > nb) desc[i].status = UVHTTP_WS_FRAME_SKIPPED;
-        if (a.arena && i < nb) {
+        if (a.arena && i < nb && controls) {
             const uvhttp_ws_frame_desc_t d = desc[i];
             if (d.opcode > 2 && d.payload_len) {
                 const uint32_t key = d.masking_key;
@@ -1331,6 +1343,27 @@ constexpr uint64_t kFusedMinStride = 64;
 // 16 KiB fused tiles made the sweep favour fusing up to 8 KiB (r03p35_fused_tiles.txt), but
 // the C2 bench itself (4 KiB frames) lost 5 % fused: 2217-2255 vs 2357-2367 GiB/s (r03p36)
 constexpr uint64_t kFusedMaxAvg = 2560;
+// k_unmask_stride's third role (AUX == kSpecCompact): the speculative pass of a compact stride
+// batch (run_decode)
+constexpr int kSpecCompact = 100;
+
+// 16 bytes at byte offset r of an LDS-staged tile, from the two aligned vectors around it
+__device__ inline u32x4 lds_window(const u32x4* tile, uint32_t r) {
+    const u32x4 v0 = tile[r >> 4], v1 = tile[(r >> 4) + 1];
+    uint64_t x0 = v0.x | ((uint64_t)v0.y << 32), x1 = v0.z | ((uint64_t)v0.w << 32);
+    uint64_t x2 = v1.x | ((uint64_t)v1.y << 32);
+    const uint64_t x3 = v1.z | ((uint64_t)v1.w << 32);
+    const uint32_t dd = r & 15;
+    if (dd & 8) {
+        x0 = x1;
+        x1 = x2;
+        x2 = x3;
+    }
+    const uint32_t sh = (dd & 7) * 8;
+    const uint64_t r0 = sh ? (x0 >> sh) | (x1 << (64 - sh)) : x0;
+    const uint64_t r1 = sh ? (x1 >> sh) | (x2 << (64 - sh)) : x1;
+    return u32x4{(uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)r1, (uint32_t)(r1 >> 32)};
+}
 
 // x / s for x < 2^24 (tile-relative offsets): a float reciprocal and one correction step
 __device__ inline uint32_t div_small(uint32_t x, uint32_t s, float inv_s) {
@@ -1423,38 +1456,90 @@ __global__ __launch_bounds__(BLOCK) void k_unmask_stride(BatchArgs a, uint64_t t
     for (uint32_t j = threadIdx.x; j < nf; j += BLOCK) {
         const uint32_t f = fbase + j;
         const uint64_t o = (uint64_t)f * S;
-        u32x4 hv;
-        if (o < t0) {
-            hv = s_h0;
-        } else {
-            // 16 bytes at tile offset r from the two aligned LDS vectors around it
-            const uint64_t r = o - t0;
-            const u32x4 v0 = s_tile[r >> 4], v1 = s_tile[(r >> 4) + 1];
-            uint64_t x0 = v0.x | ((uint64_t)v0.y << 32), x1 = v0.z | ((uint64_t)v0.w << 32);
-            uint64_t x2 = v1.x | ((uint64_t)v1.y << 32);
-            const uint64_t x3 = v1.z | ((uint64_t)v1.w << 32);
-            const uint32_t dd = (uint32_t)(r & 15);
-            if (dd & 8) {
-                x0 = x1;
-                x1 = x2;
-                x2 = x3;
-            }
-            const uint32_t s = (dd & 7) * 8;
-            const uint64_t r0 = s ? (x0 >> s) | (x1 << (64 - s)) : x0;
-            const uint64_t r1 = s ? (x1 >> s) | (x2 << (64 - s)) : x1;
-            hv = u32x4{(uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)r1, (uint32_t)(r1 >> 32)};
-        }
+        // (a header starting in the tile: 16 bytes at its tile offset from LDS)
+        const u32x4 hv = o < t0 ? s_h0 : lds_window(s_tile, (uint32_t)(o - t0));
         uvhttp_ws_frame_desc_t d;
         (void)parse_hdr(a, f, seg_info(a, f, n), o, hv, d);
         if (o >= t0) a.recs[f] = rec_of(d);  // (a frame that started earlier: its own tile)
         const bool ok = d.status == UVHTTP_WS_FRAME_OK;
+        // speculative compact pass: the frame is uniform (a locally valid data frame with the
+        // batch's uniform payload length and header + key bytes), so it goes to f * spec_P
+        const bool uniform = AUX == kSpecCompact && ok && d.opcode <= 2 && d.payload_len == a.spec_P &&
+                             d.header_size + ((d.flags & UVHTTP_WS_FLAG_MASK) ? 4u : 0u) == S - a.spec_P;
         s_fr[j] = int4{rel_clamp(d.payload_off, t0, kT, true),
                        rel_clamp(d.payload_off + (ok ? d.payload_len : 0), t0, kT, false),
-                       (int32_t)d.masking_key, 0};
+                       (int32_t)d.masking_key, uniform ? 1 : 0};
     }
     // AUX < 0: the records-only pass of a compact stride decode (the wire stays masked)
     if constexpr (AUX < 0) return;
     __syncthreads();
+    if constexpr (AUX == kSpecCompact) {
+        // The speculative compact pass: the tile's payload bytes of uniform frames go to arena
+        // offset f * P + q (P = spec_P, q = byte within the payload) — where the compact decode
+        // puts them when every frame before f is uniform and delivered, which k_plan checks
+        // (ws.spec_bad; k_spec_fix redoes the call with the full scatter otherwise).  The bytes
+        // of wire [t0, e) land in one contiguous arena range [X0, X1), written as aligned
+        // 16-byte vectors assembled from the tile in LDS (streaming stores: no dirty lines left
+        // for the next kernel's reads), bytewise only at the range's two ends and around a
+        // frame that is not uniform.  The wire itself stays masked, as in every compact decode.
+        const uint64_t P = a.spec_P, D = S - P;  // D: header + key bytes of a uniform frame
+        const uint64_t e = t0 + kT < vend ? t0 + kT : vend;
+        if (e <= t0) return;
+        const uint64_t pa = (uint64_t)fbase * S + D;  // fbase's payload start
+        const uint64_t X0 = (uint64_t)fbase * P + (t0 > pa ? t0 - pa : 0);
+        const uint64_t qe = div_stride(a, e - 1);
+        const uint64_t fe = qe < n ? qe : n - 1;
+        const uint64_t pe = fe * S + D;
+        uint64_t X1 = fe * P + (e > pe ? (e - pe < P ? e - pe : P) : 0);
+        if (X1 > a.arena_cap) X1 = a.arena_cap;
+        if (X0 >= X1) return;
+        const uint64_t base = X0 & ~(uint64_t)15;
+        const uint32_t nvec = (uint32_t)((X1 - base + 15) >> 4);
+        const uint32_t P32 = (uint32_t)P;
+        const float inv_p = 1.0f / (float)P32;
+        const uint64_t room = a.arena_cap - base;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            a.arena + base, 0, (int)(room < kT + 64 ? room : kT + 64), 0x00020000);
+        for (uint32_t k = threadIdx.x; k < nvec; k += BLOCK) {
+            const uint64_t ov = base + 16ull * k;
+            const uint64_t lo = ov > X0 ? ov : X0, hi = ov + 16 < X1 ? ov + 16 : X1;
+            unsigned __int128 acc = 0;
+            uint32_t valid = 0;
+            for (uint64_t x = lo; x < hi;) {
+                // frame of arena byte x relative to fbase (x - fbase * P < kT + 2 P: 32-bit)
+                const uint32_t rx = (uint32_t)(x - (uint64_t)fbase * P);
+                const uint32_t jr = div_small(rx, P32, inv_p);
+                const uint32_t q = rx - jr * P32;
+                uint64_t run_end = x + (P32 - q);
+                if (run_end > hi) run_end = hi;
+                const int4 fr = s_fr[jr];
+                if (fr.w) {
+                    const uint32_t len = (uint32_t)(run_end - x), off = (uint32_t)(x - ov);
+                    const uint32_t rw = (uint32_t)(((uint64_t)fbase + jr) * S + D + q - t0);
+                    const uint32_t rk = rotr32((uint32_t)fr.z, 8u * (q & 3u));
+                    const u32x4 w = lds_window(s_tile, rw) ^ u32x4{rk, rk, rk, rk};
+                    const unsigned __int128 v = ((unsigned __int128)(((uint64_t)w.w << 32) | w.z) << 64) |
+                                                (((uint64_t)w.y << 32) | w.x);
+                    const unsigned __int128 m = len >= 16 ? ~(unsigned __int128)0
+                                                          : (((unsigned __int128)1 << (8 * len)) - 1);
+                    acc |= (v & m) << (8 * off);
+                    valid |= ((1u << len) - 1u) << off;
+                }
+                x = run_end;
+            }
+            if (valid == 0xFFFFu) {
+                const u32x4 outv = {(uint32_t)acc, (uint32_t)(acc >> 32), (uint32_t)(acc >> 64),
+                                    (uint32_t)(acc >> 96)};
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, outv), rs,
+                    (uint32_t)(ov - base), 0, 18);
+            } else if (valid) {
+                for (uint32_t bq = 0; bq < 16; ++bq)
+                    if (valid & (1u << bq)) a.arena[ov + bq] = (uint8_t)(acc >> (8 * bq));
+            }
+        }
+        return;
+    }
 
     // a payload lies inside its frame's slot, so only frames jl..jh (relative to fbase) can
     // touch the vector at tile offset r: frame of byte r = (r + d0) / S, d0 = t0 - obase.
@@ -1819,14 +1904,14 @@ __device__ inline void store_lo_bytes(uint8_t* p, unsigned __int128 v, int n) {
 template <int BLOCK, int VPT>
 __device__ __forceinline__ void scatter_tile(
     BatchArgs a, const uvhttp_ws_frame_desc_t* __restrict__ desc, const Workspace& ws,
-    uint64_t arena_bytes_cap, uint64_t tile_base) {
+    uint64_t arena_bytes_cap, uint64_t tile) {
     constexpr uint64_t kT = (uint64_t)BLOCK * VPT * 16;
     __shared__ uint64_t s_ps[BLOCK];  // wire offset of the payload
     __shared__ uint64_t s_pe[BLOCK];  // its end (== start: not a delivered data frame)
     __shared__ uint64_t s_ao[BLOCK];  // arena offset
     __shared__ uint32_t s_key[BLOCK];
 
-    const uint64_t t0 = (tile_base + blockIdx.x) * kT;
+    const uint64_t t0 = tile * kT;
     const uint64_t vend = a.wire_len;
     const uint64_t full_end = vend & ~(uint64_t)15;
     const uint64_t clamp_va = full_end ? full_end - 16 : 0;
@@ -1938,7 +2023,7 @@ __global__ __launch_bounds__(BLOCK) void k_scatter_compact(
     BatchArgs a, const uvhttp_ws_frame_desc_t* __restrict__ desc, Workspace ws,
     uint64_t arena_bytes_cap, uint64_t tile_base) {
     StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_PAYLOAD, false);
-    scatter_tile<BLOCK, VPT>(a, desc, ws, arena_bytes_cap, tile_base);
+    scatter_tile<BLOCK, VPT>(a, desc, ws, arena_bytes_cap, tile_base + blockIdx.x);
     // k_finalize's work at the end of the first ceil(n / BLOCK) workgroups, as the in-place
     // kernel does (statuses after the first failure, control payloads unmasked in the wire —
     // bytes no tile reads —, the summary): one launch fewer, C4 compact 1274 -> 1293 GiB/s,
@@ -1948,6 +2033,27 @@ __global__ __launch_bounds__(BLOCK) void k_scatter_compact(
         finalize_frames(a, const_cast<uvhttp_ws_frame_desc_t*>(desc), ws,
                         (uint32_t)(tile_base + blockIdx.x), BLOCK, first_bad_of(a, ws, a.n));
     }
+}
+
+// After k_plan on the speculative compact pass's records: when every delivered frame sat where
+// the pass put it (ws.spec_bad past the first failure) only the summary remains (and SKIPPED
+// statuses after a failure); otherwise the whole batch is scattered again from the wire by the
+// same workgroups (grid-stride over the wire tiles; the tile map k_plan claimed), control
+// payloads unmasked in the wire, as a k_plan-first compact decode does.
+__global__ __launch_bounds__(kBlock) void k_spec_fix(BatchArgs a, uvhttp_ws_frame_desc_t* desc,
+                                                     Workspace ws, uint64_t n_tiles) {
+    resolve_epoch(a, ws);
+    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_FIXUP);
+    const uint32_t n = a.n;
+    const uint32_t nb = first_bad_of(a, ws, n);
+    const bool slow = tag_get(*ws.spec_bad, a.epoch, n) < nb && !device_fault(a, ws);
+    if (slow) {
+        for (uint64_t t = blockIdx.x; t < n_tiles; t += gridDim.x)
+            scatter_tile<kBlock, 4>(a, desc, ws, a.arena_cap, t);
+    }
+    const uint32_t nblk = (n + kBlock - 1) / kBlock;
+    for (uint32_t blk = blockIdx.x; blk < (nblk ? nblk : 1); blk += gridDim.x)
+        finalize_frames(a, desc, ws, blk, kBlock, nb, slow);
 }
 // ------------------------------------------------------------------------------------
 // Stream decode (uvhttp_ws_gpu_decode_streams / _decode_reads): many connections, each with
@@ -3413,6 +3519,8 @@ struct uvhttp_ws_gpu_engine {
     uint32_t fixup_blocks;     // k_fixup grid cap (UVHTTP_WS_FIXUP_BLOCKS, A/B)
     int fused_aux;             // fused payload stores' cache-policy bits (UVHTTP_WS_FUSED_AUX, A/B)
     int compact_recs;          // compact stride batches: records pass + k_plan on records
+    int spec_on;               // compact stride batches: the speculative pass (UVHTTP_WS_SPEC=0: off)
+    uint64_t spec_max_avg;     // ... up to this many wire bytes per frame (UVHTTP_WS_SPEC_MAX)
     int time_chain;            // UVHTTP_WS_TIME_CHAIN=1: stream decode timing brackets the whole
                                // kernel chain (walk .. payload), not only the payload kernel
     void* bs_mem;              // send-side output-map records (BuildRec per map tile)
@@ -3520,6 +3628,10 @@ int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out) {
     if (const char* tc = getenv("UVHTTP_WS_TIME_CHAIN")) e->time_chain = atoi(tc) != 0;
     e->compact_recs = 0;  // (UVHTTP_WS_COMPACT_RECS=1: under evaluation)
     if (const char* cr = getenv("UVHTTP_WS_COMPACT_RECS")) e->compact_recs = atoi(cr) != 0;
+    e->spec_on = 1;
+    if (const char* sp2 = getenv("UVHTTP_WS_SPEC")) e->spec_on = atoi(sp2) != 0;
+    e->spec_max_avg = kFusedMaxAvg;
+    if (const char* sm = getenv("UVHTTP_WS_SPEC_MAX")) e->spec_max_avg = strtoull(sm, nullptr, 10);
     e->fused_aux = 18;
     if (const char* fa = getenv("UVHTTP_WS_FUSED_AUX")) e->fused_aux = atoi(fa);
     e->fixup_blocks = 1024;
@@ -3637,6 +3749,7 @@ int uvhttp_ws_gpu_engine_reserve(uvhttp_ws_gpu_engine_t* e, uint32_t max_frames,
     e->ws.counters = (uint32_t*)(b + off_cnt);
     e->ws.tile_first = (uint64_t*)(b + off_tiles);
     e->ws.first_bad = (uint64_t*)(b + off_bad);
+    e->ws.spec_bad = e->ws.first_bad + 1;  // (off_bad reserves 16 bytes)
     e->ws.arena_first = (uint64_t*)(b + off_arena);
     e->ws.recs = b + off_recs;
     e->ws.ctl = e->ctl;
@@ -3908,6 +4021,19 @@ static void launch_plan(uvhttp_ws_gpu_engine_t* e, BatchArgs& a, uint32_t n_cap,
     }
 }
 
+// The uniform payload length of a stride batch: P with header(P) + 4 + P == stride, header(P)
+// the minimal encoding (2 / 4 / 10 bytes) — what a masked frame filling its slot carries; 0 when
+// no such P exists (strides 132 and 133, or below 6)
+static uint64_t spec_payload(uint64_t stride) {
+    static const uint64_t hs[3] = {2, 4, 10};
+    for (uint64_t h : hs) {
+        if (stride < h + 4) continue;
+        const uint64_t p = stride - h - 4;
+        if ((p < 126 ? 2u : p < 65536 ? 4u : 10u) == h) return p;
+    }
+    return 0;
+}
+
 static int check_batch(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b,
                        const void* d_desc, const void* d_summary) {
     if (!e || !b || !d_desc || !d_summary) return UVHTTP_WS_GPU_EINVAL;
@@ -4025,6 +4151,37 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
         hipError_t hf = hipGetLastError();
         if (prev != e->device) (void)hipSetDevice(prev);
         if (hf != hipSuccess) return set_err(e, UVHTTP_WS_GPU_ELAUNCH, "launch", hf);
+        return UVHTTP_WS_GPU_OK;
+    }
+    // compact stride batches of small frames, speculatively: the payload pass
+    // parses the headers (records) and writes every uniform frame's payload to f * P right
+    // away; k_plan on the records checks that every delivered frame is where it went, and
+    // k_spec_fix redoes the batch with the full scatter when one is not
+    const uint64_t spec_p = spec_payload(b->frame_stride);
+    const bool spec = arena && !b->frame_off && e->spec_on && a.n > 0 && spec_p &&
+                      b->wire_len / a.n <= e->spec_max_avg && e->compact_mode != 1 &&
+                      b->frame_stride >= kFusedMinStride && b->wire_len > 0 &&
+                      b->wire_len < (1ull << 52) && arena_cap < (1ull << 52) &&
+                      (uint64_t)(a.n - 1) <= (b->wire_len - 1) / b->frame_stride;
+    if (spec) {
+        a.recs = reinterpret_cast<FrameRec*>(e->ws.recs);
+        a.stride_inv = 1.0 / (double)b->frame_stride;
+        a.spec_P = spec_p;
+        constexpr uint64_t kSt = 256ull * 4 * 16;
+        const uint64_t s_tiles = (b->wire_len + kSt - 1) / kSt;
+        const int stk = timing_begin(e, s);
+        for (uint64_t tb = 0; tb < s_tiles; tb += (1ull << 24)) {
+            const uint32_t grid_s = (uint32_t)((s_tiles - tb) < (1ull << 24) ? (s_tiles - tb) : (1ull << 24));
+            hipLaunchKernelGGL((k_unmask_stride<256, 4, kSpecCompact>), dim3(grid_s), dim3(256), 0, s, a, tb);
+        }
+        timing_end(e, stk, s);
+        launch_plan(e, a, a.n, d_desc, d_msgs, s);
+        const uint32_t nblk = (a.n + kBlock - 1) / kBlock;
+        hipLaunchKernelGGL(k_spec_fix, dim3(nblk < 1024 ? nblk : 1024), dim3(kBlock), 0, s, a, d_desc,
+                           e->ws, s_tiles);
+        const hipError_t hs = hipGetLastError();
+        if (prev != e->device) (void)hipSetDevice(prev);
+        if (hs != hipSuccess) return set_err(e, UVHTTP_WS_GPU_ELAUNCH, "launch", hs);
         return UVHTTP_WS_GPU_OK;
     }
     // compact stride batches of small frames: a records-only pass over the wire (linear reads;
