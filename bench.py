@@ -684,10 +684,15 @@ def main():
     event_us = avg_kernel_s * 1e6 if k_n else None
     stamped = bool(tl and tl.get("payload_us"))
     kern_us = tl["payload_us"] if stamped else event_us
+    kern_src = "device stamps (median of the timeline calls)" if stamped else "hip events (sampled launches)"
     step_us = el_max / args.steps * 1e6
-    if stamped:
-        assert kern_us <= step_us / passes, (kern_us, step_us, passes)
+    if kern_us and kern_us > step_us / passes:
+        # a kernel of the step cannot outlast the step: a measurement that says so was perturbed
+        # (the stamped calls or the event markers); the step itself bounds the kernel
+        kern_src += f" exceeded the step ({kern_us:.1f} us): step time used"
+        kern_us = step_us / passes
     if kern_us:
+        assert kern_us <= step_us / passes + 1e-6
         achieved = alg_bytes / (kern_us / 1e6) / 1e9
 
     extra = {}
@@ -733,8 +738,7 @@ def main():
                 "traffic": traffic,
                 "alg_bytes_per_launch": alg_bytes,
                 "avg_kernel_us": round(kern_us, 2) if kern_us else None,
-                "avg_kernel_source": "device stamps (median of the timeline calls)" if stamped
-                                     else "hip events (sampled launches)",
+                "avg_kernel_source": kern_src,
                 "event_kernel_us": round(event_us, 2) if event_us else None,
                 "launches_timed": k_n,
                 "copy_ceiling": None if ceiling is None else {

@@ -333,17 +333,20 @@ struct StampScope {
     // the first active lane of each wave its end
     __device__ ~StampScope() {
         if (!st) return;
+        // ends: the last kStampEnd waves of the launch only (dispatch is in order, so the last
+        // wave to finish is among them for the uniform payload tiles; every wave of the walk
+        // and plan launches, which have fewer) — a clock read and store in each of a C3
+        // payload kernel's 262 144 waves slowed it by 12 %
+        const uint32_t wpb = blockDim.x >> 6;
+        const uint64_t wi = (uint64_t)blockIdx.x * wpb + (threadIdx.x >> 6);
+        const bool first = threadIdx.x == 0 && blockIdx.x < kStampBegin;
+        const bool tail = wi + kStampEnd >= (uint64_t)gridDim.x * wpb;
+        if (!first && !tail) return;
         uint64_t* sl = stamp_slot(st, epoch, kind);
         const uint64_t tag = (uint64_t)(epoch & 0xFFFFFFu) << 40;
         const uint64_t now = stamp_clock();
-        if (threadIdx.x == 0 && blockIdx.x < kStampBegin) sl[blockIdx.x] = tag | ((t0 ? t0 : now) & kStampLow);
-        // ends: the last kStampEnd waves of the launch only (dispatch is in order, so the last
-        // wave to finish is among them for the uniform payload tiles; every wave of the walk
-        // and plan launches, which have fewer) — a store from each of a C3 payload kernel's
-        // 262 144 waves slowed it by 12 %
-        const uint32_t wpb = blockDim.x >> 6;
-        const uint64_t wi = (uint64_t)blockIdx.x * wpb + (threadIdx.x >> 6);
-        if (wi + kStampEnd < (uint64_t)gridDim.x * wpb) return;
+        if (first) sl[blockIdx.x] = tag | ((t0 ? t0 : now) & kStampLow);
+        if (!tail) return;
         const uint64_t act = __ballot(1);
         if ((threadIdx.x & 63) != (uint32_t)__builtin_ctzll(act)) return;
         sl[kStampBegin + wi % kStampEnd] = tag | (now & kStampLow);
