@@ -321,14 +321,29 @@ __device__ inline uint64_t stamp_clock() {
 // with stamps off, profiles/r04_ab_stampoff2.txt).  So the kernels whose uniform loads matter
 // (payload kernels, walks, descriptors: at_start = false) read no clock at their start; their
 // "begin" is the earliest END among their first 256 workgroups — late by one workgroup's
-// duration (about 1-3 us for the payload tiles).  The others (k_plan, scans, fix-ups) read the
-// clock when they start.
+// duration — unless the kernel reads it through anchor_s / anchor_v (the payload kernels, the
+// walks and k_stream_desc do).  The others (k_plan, scans, fix-ups) read the clock when they start.
 struct StampScope {
     uint64_t* st;
     uint32_t epoch, kind;
     uint64_t t0;
     __device__ StampScope(uint64_t* st_, uint32_t epoch_, uint32_t kind_, bool at_start = true)
         : st(st_), epoch(epoch_), kind(kind_), t0(at_start ? stamp_clock() : 0) {}
+    // The start clock of a kernel whose uniform loads must stay scalar: read by an asm that is
+    // not a memory access (so it clobbers nothing) and is pinned before the kernel's first
+    // loads by passing the index they are computed from through it (v is returned unchanged).
+    __device__ uint32_t anchor_s(uint32_t v) {
+        uint64_t t;
+        asm("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t), "+s"(v));
+        t0 = t;
+        return v;
+    }
+    __device__ uint32_t anchor_v(uint32_t v) {
+        uint64_t t;
+        asm("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t), "+v"(v));
+        t0 = t;
+        return v;
+    }
     // runs at every return of the kernel: thread 0 of the first workgroups stores the start,
     // the first active lane of each wave its end
     __device__ ~StampScope() {
@@ -1172,13 +1187,13 @@ template <int BLOCK, int VPT, int STORE_AUX>
 __device__ __forceinline__ void unmask_tile(BatchArgs a,
                                             const uvhttp_ws_frame_desc_t* __restrict__ desc,
                                             const Workspace& ws, uint64_t tile_base,
-                                            uint32_t& n_out, uint32_t& nb_out) {
+                                            uint32_t& n_out, uint32_t& nb_out, StampScope& ss) {
     constexpr uint64_t kT = (uint64_t)BLOCK * VPT * 16;
     __shared__ uint64_t s_ps[BLOCK];
     __shared__ uint64_t s_pe[BLOCK];
     __shared__ uint32_t s_key[BLOCK];
 
-    const uint64_t t0 = (tile_base + blockIdx.x) * kT;
+    const uint64_t t0 = (tile_base + ss.anchor_s(blockIdx.x)) * kT;
     const uint64_t vend = a.wire_len;
     // loads are clamped to the last whole vector so they can be issued unconditionally;
     // the one vector straddling the end of the wire is finished bytewise
@@ -1311,7 +1326,7 @@ __global__ __launch_bounds__(BLOCK) void k_unmask_inplace(
     uint64_t tile_base) {
     StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_PAYLOAD, false);
     uint32_t n, nb;
-    unmask_tile<BLOCK, VPT, STORE_AUX>(a, desc, ws, tile_base, n, nb);  // resolves the epoch
+    unmask_tile<BLOCK, VPT, STORE_AUX>(a, desc, ws, tile_base, n, nb, stamp_);  // resolves the epoch
     // batch in-place decode: the first ceil(n / BLOCK) workgroups then do k_finalize's work
     // (statuses after the first failure become SKIPPED — frames no tile reads — and the
     // summary); the launch covers max(tiles, those blocks).  After the tile, so the tile's
@@ -1414,7 +1429,7 @@ __global__ __launch_bounds__(BLOCK) void k_unmask_stride(BatchArgs a, uint64_t t
     __shared__ int4 s_fr[kMaxF];
     __shared__ u32x4 s_h0;                                  // header of the frame covering t0
 
-    const uint64_t t0 = (tile_base + blockIdx.x) * kT;
+    const uint64_t t0 = (tile_base + stamp_.anchor_s(blockIdx.x)) * kT;
     const uint64_t vend = a.wire_len;
     const uint64_t full_end = vend & ~(uint64_t)15;
     const uint64_t clamp_va = full_end ? full_end - 16 : 0;
@@ -2026,7 +2041,7 @@ __global__ __launch_bounds__(BLOCK) void k_scatter_compact(
     BatchArgs a, const uvhttp_ws_frame_desc_t* __restrict__ desc, Workspace ws,
     uint64_t arena_bytes_cap, uint64_t tile_base) {
     StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_PAYLOAD, false);
-    scatter_tile<BLOCK, VPT>(a, desc, ws, arena_bytes_cap, tile_base + blockIdx.x);
+    scatter_tile<BLOCK, VPT>(a, desc, ws, arena_bytes_cap, tile_base + stamp_.anchor_s(blockIdx.x));
     // k_finalize's work at the end of the first ceil(n / BLOCK) workgroups, as the in-place
     // kernel does (statuses after the first failure, control payloads unmasked in the wire —
     // bytes no tile reads —, the summary): one launch fewer, C4 compact 1274 -> 1293 GiB/s,
@@ -2392,7 +2407,7 @@ __device__ inline uint32_t walk_lane(const WalkArgs& w, uint32_t s, uint32_t lf)
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void k_swalk_lane(WalkArgs w) {
     StampScope stamp_(w.stamp, w.epoch, MODE == 1 ? UVHTTP_WS_STAMP_WALK2 : UVHTTP_WS_STAMP_WALK, false);
-    const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t s = stamp_.anchor_v(blockIdx.x * kBlock + threadIdx.x);
     const uint32_t lf = MODE == 1 ? lane_first(w, s) : 0;  // (before any thread leaves)
     uint32_t count = 0;
     if (s < w.n_streams) count = walk_lane<MODE>(w, s, lf);
@@ -2669,7 +2684,7 @@ __global__ __launch_bounds__(kBlock) void k_swalk_wave(WalkArgs w) {
     // readfirstlane: the connection (and all walk state derived from it) is wave-uniform, so
     // it lives in scalar registers and the walk's branches are scalar branches
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t s = blockIdx.x * (kBlock / 64) + wave;
+    const uint32_t s = stamp_.anchor_s(blockIdx.x * (kBlock / 64) + wave);
     if (s >= w.n_streams) return;
     if (MODE == 1 && !w.results[s].n_frames) return;
     walk_wave<MODE>(w, s, ring[wave]);
@@ -2758,7 +2773,7 @@ __device__ inline void capacity_result(uvhttp_ws_stream_result_t& r) {
 // lane mode: one lane per connection (few frames each) writes its descriptors in order
 __global__ __launch_bounds__(kBlock) void k_stream_desc_lane(WalkArgs w) {
     StampScope stamp_(w.stamp, w.epoch, UVHTTP_WS_STAMP_STREAM_DESC, false);
-    const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t s = stamp_.anchor_v(blockIdx.x * kBlock + threadIdx.x);
     const uint32_t first = lane_first(w, s);
     if (s >= w.n_streams) return;
     uvhttp_ws_stream_result_t r = w.results[s];
@@ -2793,7 +2808,7 @@ __global__ __launch_bounds__(kBlock) void k_stream_desc_lane(WalkArgs w) {
 __global__ __launch_bounds__(kBlock) void k_stream_desc(WalkArgs w) {
     StampScope stamp_(w.stamp, w.epoch, UVHTTP_WS_STAMP_STREAM_DESC, false);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const uint32_t s = blockIdx.x * (kBlock / 64) + wave;
+    const uint32_t s = stamp_.anchor_s(blockIdx.x * (kBlock / 64) + wave);
     if (s >= w.n_streams) return;
     uvhttp_ws_stream_result_t r = w.results[s];
     r.first_frame = w.agg[s];  // (k_swalk_scan's prefix)
