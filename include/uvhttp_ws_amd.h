@@ -521,9 +521,10 @@ int uvhttp_ws_gpu_build_frames(uvhttp_ws_gpu_engine_t* eng, const uint8_t* d_src
 
 /* ---- host-memory pipeline (libuv read buffers in, decoded payloads out) ---------------- */
 /* A pipeline owns `depth` slots.  Each slot = a pinned host staging buffer (the caller
- * writes masked frames there, e.g. hands it out from the libuv alloc callback), a device
- * wire buffer, its own engine (workspace) and its own HIP stream, so slot k's H2D copy,
- * slot k-1's kernels and slot k-2's D2H copy overlap.  submit() enqueues
+ * writes masked frames there, e.g. hands it out from the libuv alloc callback) and a device
+ * wire buffer.  Every slot's H2D copy runs on the pipeline's upload stream and its decode and
+ * D2H copy on its compute stream (behind an event), so slot k's upload overlaps slot k-1's
+ * kernels and download on the two copy queues.  submit() enqueues
  *   H2D(wire[0, wire_len)) -> decode_inplace -> D2H(wire, desc, summary)
  * and returns at once; wait() blocks until the slot's decoded bytes, descriptors and
  * summary are back in pinned host memory (the in-place contract: delivered payloads are
