@@ -485,6 +485,14 @@ class GpuWorkload:
         avg = ms / 1e3 / k
         return 2 * self.wire_len / avg / 1e9, avg * 1e6
 
+    def stamp_timed(self):
+        """streams mode keeps the device stamps on during the timed steps (the idle between calls
+        some runs show happens there); timeline() then reads the last 15 timed calls"""
+        if self.streams_dev is not None:
+            self.eng.set_stamps(True)
+            self.eng.read_stamps()
+            self.stamped_timed = True
+
     def timeline(self, calls=16):
         """Device-side kernel stamps (uvhttp_ws_gpu_engine_set_stamps) over `calls` more steps
         after the timed region, same process and buffers: when each kernel of a call ran on the
@@ -494,6 +502,13 @@ class GpuWorkload:
         if self.build_dev is not None or self.graph is not None:
             return None
         eng = self.eng
+        if getattr(self, "stamped_timed", False):
+            recs = eng.read_stamps()  # the last timed calls
+            eng.set_stamps(False)
+            out = summarize_stamps(recs)
+            if out:
+                out["calls_from"] = "the last timed steps (stamps on while timed)"
+            return out
         eng.set_stamps(True)
         eng.read_stamps()  # drop anything older
         for _ in range(min(calls, 15)):
@@ -501,7 +516,10 @@ class GpuWorkload:
         self.sync()
         recs = eng.read_stamps()
         eng.set_stamps(False)
-        return summarize_stamps(recs)
+        out = summarize_stamps(recs)
+        if out:
+            out["calls_from"] = "15 more steps after the timed region"
+        return out
 
     def check(self):
         """Every frame of the shard must have been delivered (the decode really ran)."""
@@ -570,6 +588,8 @@ def timed_run(wl, steps, warmup, world):
         wl.step()
     wl.check()
     wl.kernel_time()  # discard warmup events
+    if hasattr(wl, "stamp_timed") and not getattr(wl, "no_stamps", False):
+        wl.stamp_timed()
     wl.set_timing(True)
     if world > 1:
         dist.barrier()
@@ -656,6 +676,7 @@ def main():
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
     wl = (StubWorkload if args.stub else GpuWorkload)(args, cfg, rank, world, local)
+    wl.no_stamps = args.no_stamps
     el_max, k_ms, k_n = timed_run(wl, args.steps, args.warmup, world)
     n, plen, passes, stride = wl.n, wl.plen, wl.passes, wl.stride
     payload_per_rank = n * plen * passes

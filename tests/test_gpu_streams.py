@@ -302,6 +302,36 @@ def test_streams_per_read_calls(torch, eng, hooks, seed):
     _run_cases(torch, eng, U, cases, rng, 8192, use_reads=True)
 
 
+def test_streams_every_cut(torch, eng, hooks):
+    """A connection's bytes cut at every point of the headers and around every frame boundary
+    (7-, 16- and 64-bit lengths, masked, an empty frame, control frames): one connection per cut
+    in one launch, as one call and as 1-byte-then-rest calls.  A read that ends inside an
+    extended length (b0 b1 of a 126 / 127 header and nothing more) must only buffer."""
+    import uvhttp_amd as U
+    rng = random.Random(31)
+    frames = [_frame(1, 1, rng.randbytes(126), rng.randbytes(4)),
+              _frame(2, 0, b"", rng.randbytes(4)),
+              _frame(0, 0, rng.randbytes(70000), rng.randbytes(4), len_form=64),
+              _frame(9, 1, rng.randbytes(5), rng.randbytes(4)),
+              _frame(0, 1, rng.randbytes(125), rng.randbytes(4)),
+              _frame(2, 1, rng.randbytes(300), rng.randbytes(4))]
+    data = b"".join(frames)
+    cuts, at = set(), 0
+    for f in frames:
+        cuts.update(range(at, at + 16))
+        cuts.update(range(at + len(f) - 3, at + len(f) + 1))
+        at += len(f)
+    cuts = sorted(c for c in cuts if 0 <= c <= len(data))
+    for use_reads in (False, True):
+        for mm in (64 * 1024 * 1024, 0):
+            cases = []
+            for c in cuts:
+                prod = U.WsConnection(1, 16 * 1024 * 1024, mm, user_data=True)
+                orc = _oracle.OracleConn(1, 16 * 1024 * 1024, mm, record=1, wrapper=True)
+                cases.append((prod, orc, [data[:1], data[1:c]] if use_reads else [data[:c]]))
+            _run_cases(torch, eng, U, cases, rng, 4096, use_reads=use_reads)
+
+
 def _small_frames(rng, total, plen=256):
     out = []
     while sum(len(f) for f in out) < total:

@@ -348,23 +348,23 @@ struct StampScope {
     // the first active lane of each wave its end
     __device__ ~StampScope() {
         if (!st) return;
-        // ends: the last kStampEnd waves of the launch only (dispatch is in order, so the last
-        // wave to finish is among them for the uniform payload tiles; every wave of the walk
-        // and plan launches, which have fewer) — a clock read and store in each of a C3
-        // payload kernel's 262 144 waves slowed it by 12 %
-        const uint32_t wpb = blockDim.x >> 6;
-        const uint64_t wi = (uint64_t)blockIdx.x * wpb + (threadIdx.x >> 6);
+        // ends: every wave of the first 1024 workgroups (all of them in the walk, plan and scan
+        // launches), then one workgroup in 64 — the last of those to finish ends within one
+        // workgroup's time of the kernel.  Nothing from the dispatch packet (grid or block
+        // size): a load of it in each of a C3 payload kernel's 262 144 waves, like a clock read
+        // and store in each, slowed the stamped kernel by 12 %.
         const bool first = threadIdx.x == 0 && blockIdx.x < kStampBegin;
-        const bool tail = wi + kStampEnd >= (uint64_t)gridDim.x * wpb;
-        if (!first && !tail) return;
+        const bool sample = blockIdx.x < 1024 || (blockIdx.x & 63) == 63;
+        if (!first && !sample) return;
         uint64_t* sl = stamp_slot(st, epoch, kind);
         const uint64_t tag = (uint64_t)(epoch & 0xFFFFFFu) << 40;
         const uint64_t now = stamp_clock();
         if (first) sl[blockIdx.x] = tag | ((t0 ? t0 : now) & kStampLow);
-        if (!tail) return;
+        if (!sample) return;
         const uint64_t act = __ballot(1);
         if ((threadIdx.x & 63) != (uint32_t)__builtin_ctzll(act)) return;
-        sl[kStampBegin + wi % kStampEnd] = tag | (now & kStampLow);
+        const uint32_t blk = blockIdx.x < 1024 ? blockIdx.x : 1024 + (blockIdx.x >> 6);
+        sl[kStampBegin + (blk * 4 + ((threadIdx.x >> 6) & 3)) % kStampEnd] = tag | (now & kStampLow);
     }
 };
 
@@ -876,7 +876,9 @@ __device__ inline void store_desc(uvhttp_ws_frame_desc_t* desc, uint32_t i, cons
 }
 
 // pass 2: the state machine in frame order from the lane's exclusive prefix `run`; each
-// descriptor is stored once
+// descriptor is stored once.  (Staging a wave's descriptors in LDS to store them as whole
+// streaming lines measured 2.5 % slower on C4: the LDS round trip costs more than the partial
+// lines it saves.)
 template <int FPT>
 __device__ inline void plan_pass2(const BatchArgs& a, uvhttp_ws_frame_desc_t* desc,
                                   uvhttp_ws_message_desc_t* msgs, const Workspace& ws, uint32_t i0,
