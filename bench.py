@@ -805,10 +805,14 @@ def e2e_live(local, conns=1024, frames=4, size=65536, flushes=20):
     exe = os.path.join(REPO, "tests", "c", "_build", "batcher_e2e")
     out = {}
     # device runs: the loop thread on the GPU's NUMA node (--pin 1)
-    for name, dev, asy in (("device", local, 0), ("device_async", local, 1), ("host_1core", -1, 0)):
+    # (device_async_half: queues of half a round — the loop, when it outruns PCIe, waits on
+    # a flush twice per round for half as long: the blocked-call tail a server sizing max_bytes
+    # below its round sees)
+    for name, dev, asy, cap in (("device", local, 0, 1.0), ("device_async", local, 1, 1.0),
+                                ("device_async_half", local, 1, 0.5), ("host_1core", -1, 0, 1.0)):
         p = subprocess.run([exe, "--conns", str(conns), "--frames", str(frames), "--size",
                             str(size), "--flushes", str(flushes if dev >= 0 else 3),
-                            "--device", str(dev), "--async", str(asy),
+                            "--device", str(dev), "--async", str(asy), "--cap", str(cap),
                             "--pin", "1" if dev >= 0 else "0"],
                            capture_output=True, text=True, timeout=600)
         out[name] = json.loads(p.stdout.strip().splitlines()[-1]) if p.returncode == 0 else \

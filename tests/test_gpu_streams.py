@@ -332,6 +332,26 @@ def test_streams_every_cut(torch, eng, hooks):
             _run_cases(torch, eng, U, cases, rng, 4096, use_reads=use_reads)
 
 
+def test_streams_wire_ends_in_header(torch, eng, hooks):
+    """The launch's wire ends inside a header (one connection, wire_len = its bytes): the
+    walks' bounded block loads must still see every byte before wire_len (a range check at
+    dword granularity once read a 2-byte wire 81 FE as zeros — an "unmasked" frame — and
+    failed the connection; tests/test_batcher_group.py seed 2 found it)."""
+    import uvhttp_amd as U
+    rng = random.Random(32)
+    heads = [_frame(1, 1, rng.randbytes(126), rng.randbytes(4)),
+             _frame(2, 1, rng.randbytes(70000), rng.randbytes(4), len_form=64),
+             _frame(2, 1, rng.randbytes(5), rng.randbytes(4))]
+    for f in heads:
+        for c in list(range(1, 19)) + [len(f) - 1, len(f)]:
+            for use_reads in (False, True):
+                prod = U.WsConnection(1, 16 * 1024 * 1024, 0, user_data=True)
+                orc = _oracle.OracleConn(1, 16 * 1024 * 1024, 0, record=1, wrapper=True)
+                reads = [f[:1], f[1:c]] if use_reads else [f[:c]]
+                _run_cases(torch, eng, U, [(prod, orc, reads)], random.Random(0), 64,
+                           use_reads=use_reads)
+
+
 def _small_frames(rng, total, plen=256):
     out = []
     while sum(len(f) for f in out) < total:

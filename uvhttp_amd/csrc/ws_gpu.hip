@@ -2424,7 +2424,7 @@ __global__ __launch_bounds__(kBlock) void k_swalk_lane(WalkArgs w) {
 // of the current header and the next) plus a 16-byte mirror of slot 0 after slot 1, so the
 // ten bytes of any header are one run of LDS bytes; the block after those is in flight in
 // registers, issued when the walk entered the current block.  Block loads are buffer loads
-// bounded by the wire's end (bytes past it read as 0): no per-lane branches.  Every lane
+// bounded by the wire's last 16-byte granule (bytes past it read as 0): no per-lane branches.  Every lane
 // reads the same header bytes (broadcast) and readfirstlane makes them scalar, so the header
 // decode, the checks and the state machine run on the scalar unit with uniform branches.
 // Frame starts are collected one per lane and stored 64 at a time.
@@ -2435,7 +2435,12 @@ constexpr uint32_t kRingBytes = 2 * kWalkBlk + 16;
 __device__ inline void walk_load_block(const WalkArgs& w, uint64_t blk, u32x4 v[kWalkVec]) {
     const int lane = threadIdx.x & 63;
     const uint64_t base = blk * kWalkBlk;
-    const uint64_t room = w.wire_len > base ? w.wire_len - base : 0;
+    // the range check drops every dword that is not wholly inside num_records (a wire ending
+    // two bytes into a 16-bit-length header read as zeros: an "unmasked" frame), so the range is
+    // the wire rounded up to its 16-byte granule — the wire is 16-byte aligned, so the granule
+    // never crosses a page; its bytes past wire_len are never used (every decision is checked
+    // against the call's end)
+    const uint64_t room = w.wire_len > base ? ((w.wire_len - base + 15) & ~(uint64_t)15) : 0;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t*>(w.wire + (room ? base : 0)), 0, (int)(room < kWalkBlk ? room : kWalkBlk),
         0x00020000);
