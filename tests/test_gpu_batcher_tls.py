@@ -191,8 +191,8 @@ def test_tls_bulk_upload_larger_than_flushes(torch, pattern):
     mf, mm = 16 * 1024 * 1024, 64 * 1024 * 1024
     prod = U.WsConnection(1, mf, mm)
     orc = O.OracleConn(1, mf, mm, record=1)
-    plain = b"".join(_frame(2, 1, rng.randbytes(rng.choice([1000, 60000, 300000])), rng.randbytes(4))
-                     for _ in range(14))
+    sizes = [1000, 300000, 300000] * 4 + [60000, 300000]  # 14 frames, 2.76 MB
+    plain = b"".join(_frame(2, 1, rng.randbytes(p), rng.randbytes(4)) for p in sizes)
     cipher = _seal_stream(rng, key, seq0, plain)
     assert len(cipher) > 2 * mb
     assert b.set_tls(prod, key.tobytes(), seq0) == 0
