@@ -805,11 +805,13 @@ def e2e_live(local, conns=1024, frames=4, size=65536, flushes=20):
     exe = os.path.join(REPO, "tests", "c", "_build", "batcher_e2e")
     out = {}
     # device runs: the loop thread on the GPU's NUMA node (--pin 1)
-    # (device_async_half: queues of half a round — the loop, when it outruns PCIe, waits on
-    # a flush twice per round for half as long: the blocked-call tail a server sizing max_bytes
-    # below its round sees)
-    for name, dev, asy, cap in (("device", local, 0, 1.0), ("device_async", local, 1, 1.0),
-                                ("device_async_half", local, 1, 0.5), ("host_1core", -1, 0, 1.0)):
+    # async: queues of half a round (max_bytes = half the bytes one loop pass reads, the sizing
+    # INTEGRATION.md §3 recommends) — a loop that outruns PCIe waits on a flush twice per round
+    # for half as long, and copies overlap better: 40 GiB/s with p99 blocked < 1 ms where whole-
+    # round queues gave 23-40 GiB/s and p99 3.6-8 ms (profiles/r04_bench_e2e.json);
+    # device_async_round keeps the whole-round queues for comparison
+    for name, dev, asy, cap in (("device", local, 0, 1.0), ("device_async", local, 1, 0.5),
+                                ("device_async_round", local, 1, 1.0), ("host_1core", -1, 0, 1.0)):
         p = subprocess.run([exe, "--conns", str(conns), "--frames", str(frames), "--size",
                             str(size), "--flushes", str(flushes if dev >= 0 else 3),
                             "--device", str(dev), "--async", str(asy), "--cap", str(cap),

@@ -3,7 +3,7 @@
 
   python tools/ab_lib.py LIB_A LIB_B cfg:mode [cfg:mode ...]     (mode: inplace | compact)
 
-LIB_B may be "tree" for the in-tree build.  Each round runs K decode steps with engine A,
+LIB_B may be "tree" for the in-tree build.  AB_STAMPS=1 turns engine B's device stamps on.  Each round runs K decode steps with engine A,
 then K with engine B, on the same device buffers; reports the median whole-step time
 (torch events around the K steps) and the median payload-kernel time (engine timing)."""
 import os
@@ -28,6 +28,8 @@ def main():
         cfg, mode = pair.split(":")
         n, plen, frag = CFG[cfg]
         engs = [U.GpuEngine(0, library=L) for L in libs]
+        if os.environ.get("AB_STAMPS"):  # B with device stamps on (A off): their runtime cost
+            engs[1].set_stamps(True)
         stride = U.gen_frame_stride(plen)
         wl = stride * n
         wire = torch.empty(wl + 64, dtype=torch.uint8, device="cuda")

@@ -288,10 +288,10 @@ struct BatchArgs {
 // consecutive calls are read off the device timeline.  Plain vector stores only — atomics on
 // one address from every wave of a 262 144-workgroup payload kernel serialise across the XCDs
 // (a C3 kernel took 11 ms with them): the first 256 workgroups store their start into their own
-// word, every wave its end into word (wave index mod 4096), so each word ends up holding one
-// of the last waves to run.  Slots form a ring keyed by the call's epoch and every word is
-// tagged (epoch << 40) | t, so the reader keeps the newest call of each slot without a reset.
-// (Ends are stored by the last 4096 waves of a launch only, below.)
+// word, a sample of the waves (below) its end into one of 4096 words, so the latest of those
+// words is within a few workgroups of the kernel's end.  Slots form a ring keyed by the call's
+// epoch and every word is tagged (epoch << 40) | t, so the reader keeps the newest call of each
+// slot without a reset.
 // ------------------------------------------------------------------------------------
 constexpr uint32_t kStampRing = 16, kStampKinds = 16, kStampBegin = 256, kStampEnd = 4096;
 constexpr uint64_t kStampPer = kStampBegin + kStampEnd;
@@ -349,12 +349,14 @@ struct StampScope {
     __device__ ~StampScope() {
         if (!st) return;
         // ends: every wave of the first 1024 workgroups (all of them in the walk, plan and scan
-        // launches), then one workgroup in 64 — the last of those to finish ends within one
-        // workgroup's time of the kernel.  Nothing from the dispatch packet (grid or block
-        // size): a load of it in each of a C3 payload kernel's 262 144 waves, like a clock read
-        // and store in each, slowed the stamped kernel by 12 %.
+        // launches), then one workgroup in 64 up to workgroup 65 536 and one in 1024 past it —
+        // the last of those to finish ends within 64 (1024) workgroups' time of the kernel.
+        // Each end store costs: one in 64 of a C3 payload kernel's 4.2 M workgroups slowed it
+        // by 6 %, one in 1024 by 0.2 % (profiles/r04_stamps_runtime_ab.txt).  Nothing from the
+        // dispatch packet (grid or block size): a load of it in each wave cost as much.
         const bool first = threadIdx.x == 0 && blockIdx.x < kStampBegin;
-        const bool sample = blockIdx.x < 1024 || (blockIdx.x & 63) == 63;
+        const uint32_t b = blockIdx.x;
+        const bool sample = b < 1024 || (b < 65536 ? (b & 63) == 63 : (b & 1023) == 1023);
         if (!first && !sample) return;
         uint64_t* sl = stamp_slot(st, epoch, kind);
         const uint64_t tag = (uint64_t)(epoch & 0xFFFFFFu) << 40;
@@ -363,7 +365,7 @@ struct StampScope {
         if (!sample) return;
         const uint64_t act = __ballot(1);
         if ((threadIdx.x & 63) != (uint32_t)__builtin_ctzll(act)) return;
-        const uint32_t blk = blockIdx.x < 1024 ? blockIdx.x : 1024 + (blockIdx.x >> 6);
+        const uint32_t blk = b < 1024 ? b : b < 65536 ? 1024 + (b >> 6) : 2048 + (b >> 10);
         sl[kStampBegin + (blk * 4 + ((threadIdx.x >> 6) & 3)) % kStampEnd] = tag | (now & kStampLow);
     }
 };
