@@ -723,8 +723,10 @@ def main():
             # the N>1 lines (default config C5) divide by this: same metric, same unit
             extra["c5_base"] = extra["c5_1gpu"]["value"]
         if args.e2e:
+            warm = e2e_warmup(local)
             extra["e2e_pcie"] = e2e_rate(n, plen, stride, CONFIGS[cfg][3], local)
             extra["e2e_live"] = e2e_live(local)
+            extra["e2e_live"]["warmup_runs"] = warm
 
     if rank == 0:
         out = {
@@ -793,6 +795,26 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def e2e_warmup(local, max_runs=6):
+    """PCIe/host-path warm-up before the e2e numbers: on a fresh box the first few seconds of
+    host<->device traffic run slower (the live harness: 17 then 24 then 40 GiB/s in three
+    consecutive processes, the same 40 after; tools/e2e_order.sh,
+    profiles/r04_e2e_order.jsonl) — the link's power state ramps with sustained traffic.  Runs
+    the async live harness until two consecutive runs agree within 5 %; returns their values."""
+    exe = os.path.join(REPO, "tests", "c", "_build", "batcher_e2e")
+    vals = []
+    for _ in range(max_runs):
+        p = subprocess.run([exe, "--conns", "1024", "--frames", "4", "--size", "65536", "--flushes",
+                            "20", "--device", str(local), "--async", "1", "--cap", "0.5", "--pin", "1"],
+                           capture_output=True, text=True, timeout=300)
+        if p.returncode != 0:
+            break
+        vals.append(json.loads(p.stdout.strip().splitlines()[-1])["value"])
+        if len(vals) >= 2 and abs(vals[-1] - vals[-2]) <= 0.05 * vals[-1]:
+            break
+    return vals
 
 
 def e2e_live(local, conns=1024, frames=4, size=65536, flushes=20):
