@@ -1525,6 +1525,23 @@ __global__ __launch_bounds__(BLOCK) void k_unmask_stride(BatchArgs a, uint64_t t
         for (uint32_t k = threadIdx.x; k < nvec; k += BLOCK) {
             const uint64_t ov = base + 16ull * k;
             const uint64_t lo = ov > X0 ? ov : X0, hi = ov + 16 < X1 ? ov + 16 : X1;
+            // the common vector: inside the range and inside one uniform frame's payload (every
+            // vector when P is a multiple of 16) — one window of the tile XOR the rotated key
+            if (lo == ov && hi == ov + 16) {
+                const uint32_t rx = (uint32_t)(ov - (uint64_t)fbase * P);
+                const uint32_t jr = div_small(rx, P32, inv_p);
+                const uint32_t q = rx - jr * P32;
+                const int4 fr = s_fr[jr];
+                if (q + 16 <= P32 && fr.w) {
+                    const uint32_t rw = (uint32_t)(((uint64_t)fbase + jr) * S + D + q - t0);
+                    const uint32_t rk = rotr32((uint32_t)fr.z, 8u * (q & 3u));
+                    const u32x4 outv = lds_window(s_tile, rw) ^ u32x4{rk, rk, rk, rk};
+                    __builtin_amdgcn_raw_buffer_store_b128(
+                        __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, outv), rs,
+                        (uint32_t)(ov - base), 0, 18);
+                    continue;
+                }
+            }
             unsigned __int128 acc = 0;
             uint32_t valid = 0;
             for (uint64_t x = lo; x < hi;) {
