@@ -623,7 +623,9 @@ __device__ inline void resolve_one(const BatchArgs& a, uvhttp_ws_message_desc_t*
     // 0 also owns the bytes before its start); the max-of-tag claim keeps the smallest frame
     // when a bad offset table makes slots overlap.  (The fused stride path's payload pass
     // finds frames by arithmetic: no tile map.)
-    if (!a.recs || a.arena) {  // (compact decodes: k_scatter_compact reads this map too)
+    // (the speculative compact decode claims none: its fallback scatter finds a stride batch's
+    // frames by arithmetic, tile_first_of)
+    if ((!a.recs || a.arena) && !a.spec_P) {  // (compact decodes: k_scatter_compact reads this map too)
         const uint64_t o = frame_start(a, i);
         uint64_t end = (i + 1 < n) ? frame_start(a, i + 1) : a.wire_len;
         if (end > a.wire_len) end = a.wire_len;
@@ -672,7 +674,7 @@ __device__ inline void resolve_one(const BatchArgs& a, uvhttp_ws_message_desc_t*
                 }
             }
             // arena tiles whose first byte lies in this data frame's payload
-            if (a.arena && d.payload_len) {
+            if (a.arena && d.payload_len && !a.spec_P) {  // (only k_gather_compact reads them)
                 const uint64_t lo = ex.data_pay, hi = ex.data_pay + d.payload_len;
                 for (uint64_t t = (lo + kMapTile - 1) / kMapTile; t * kMapTile < hi && t < a.n_arena_tiles;
                      ++t)
@@ -1940,6 +1942,19 @@ __device__ inline void store_lo_bytes(uint8_t* p, unsigned __int128 v, int n) {
     if (n & 1) *p = (uint8_t)v;
 }
 
+// the first frame whose slot holds map tile c's first byte (k_plan's claims, resolve_one);
+// the speculative compact decode claims nothing — its frames sit at i * stride, so the frame
+// is found by arithmetic (frame n - 1's slot runs to the end of the wire)
+__device__ inline uint32_t tile_first_of(const BatchArgs& a, const Workspace& ws, uint64_t c) {
+    if (a.spec_P) {
+        const uint64_t x = c * kMapTile;
+        if (x >= a.wire_len || a.n == 0) return kNoFrame;
+        const uint64_t q = div_stride(a, x);
+        return q < a.n ? (uint32_t)q : a.n - 1;
+    }
+    return tag_get(ws.tile_first[c], a.epoch, kNoFrame);
+}
+
 template <int BLOCK, int VPT>
 __device__ __forceinline__ void scatter_tile(
     BatchArgs a, const uvhttp_ws_frame_desc_t* __restrict__ desc, const Workspace& ws,
@@ -1979,8 +1994,8 @@ __device__ __forceinline__ void scatter_tile(
     if (nb == 0 || n == 0 || t0 >= vend) return;
     const uint32_t last = (nb < n ? nb : n) - 1;
     const uint64_t c0 = t0 / kMapTile, c1 = (t0 + kT - 1) / kMapTile + 1;
-    const uint32_t f0 = tag_get(ws.tile_first[c0], a.epoch, kNoFrame);
-    uint32_t f1 = (c1 < a.n_tiles) ? tag_get(ws.tile_first[c1], a.epoch, kNoFrame) : last;
+    const uint32_t f0 = tile_first_of(a, ws, c0);
+    uint32_t f1 = (c1 < a.n_tiles) ? tile_first_of(a, ws, c1) : last;
     if (f0 > last) return;
     if (f1 > last || f1 < f0) f1 = last;
 
