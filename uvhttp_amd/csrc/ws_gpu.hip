@@ -908,7 +908,7 @@ __device__ inline void plan_pass2(const BatchArgs& a, uvhttp_ws_frame_desc_t* de
 // pass 2 (after the block's prefix is known) re-reads their descriptors and runs the state
 // machine in frame order.  The block holding the last ticket resets the counter for the
 // next call.
-template <int FPT, int NT = kBlock>
+template <int FPT, int NT = kBlock, bool REC = false>
 __global__ __launch_bounds__(NT) void k_plan(BatchArgs a, uvhttp_ws_frame_desc_t* desc,
                                                  uvhttp_ws_message_desc_t* msgs, Workspace ws) {
     resolve_epoch(a, ws);
@@ -948,6 +948,46 @@ __global__ __launch_bounds__(NT) void k_plan(BatchArgs a, uvhttp_ws_frame_desc_t
 #else
     auto phase = [](int) {};
 #endif
+    if constexpr (REC) {
+        // records path: the lane's 16-byte records stay in registers across the scan (64
+        // registers; the 32-byte descriptors built from them took 128 and spilled at 16 frames
+        // per lane) and pass 2 rebuilds each descriptor from its record
+        ScanElem tagg = scan_identity();
+        FrameRec r[FPT];
+        const uint32_t ilast = n ? n - 1 : 0;
+#pragma unroll
+        for (int k = 0; k < FPT; ++k) r[k] = a.recs[i0 + k < n ? i0 + k : ilast];
+#pragma unroll
+        for (int k = 0; k < FPT; ++k) {
+            const uint32_t i = i0 + k;
+            if (i < n) {
+                uvhttp_ws_frame_desc_t d;
+                desc_of_rec(r[k], (uint64_t)i * a.frame_stride, d);
+                tagg = scan_combine(tagg, elem_of_parsed(d, i, i == 0));
+            }
+        }
+        phase(1);
+        ScanElem agg;
+        const ScanElem local = block_exclusive_scan<NT>(tagg, &agg);
+        phase(2);
+        ScanElem run = scan_combine(lookback_prefix<NT>(ws, b, agg, a.epoch, a.max_polls), local);
+        phase(3);
+#pragma unroll
+        for (int k = 0; k < FPT; ++k) {
+            const uint32_t i = i0 + k;
+            if (i < n) {
+                uvhttp_ws_frame_desc_t d;
+                desc_of_rec(r[k], (uint64_t)i * a.frame_stride, d);
+                const SegInfo g = seg_info(a, i, n);
+                const ScanElem e = elem_of_parsed(d, i, g.head);
+                resolve_one(a, msgs, ws, i, n, g, run, d);
+                store_desc(desc, i, d);
+                run = scan_combine(run, e);
+            }
+        }
+        phase(4);
+        return;
+    }
     if (FPT == 1) {
         SegInfo g;
         uvhttp_ws_frame_desc_t d;
@@ -4071,6 +4111,16 @@ static void launch_plan(uvhttp_ws_gpu_engine_t* e, BatchArgs& a, uint32_t n_cap,
     const uint32_t per = kBlock * fpt;
     a.plan_frames = per;
     const uint32_t grid = n_cap ? (n_cap + per - 1) / per : 1;
+    if (a.recs) {  // the records-only instantiation (its registers sized for records alone)
+        switch (fpt) {
+            case 1: hipLaunchKernelGGL((k_plan<1, kBlock, true>), dim3(grid), dim3(kBlock), 0, s, a, d_desc, d_msgs, e->ws); break;
+            case 2: hipLaunchKernelGGL((k_plan<2, kBlock, true>), dim3(grid), dim3(kBlock), 0, s, a, d_desc, d_msgs, e->ws); break;
+            case 4: hipLaunchKernelGGL((k_plan<4, kBlock, true>), dim3(grid), dim3(kBlock), 0, s, a, d_desc, d_msgs, e->ws); break;
+            case 8: hipLaunchKernelGGL((k_plan<8, kBlock, true>), dim3(grid), dim3(kBlock), 0, s, a, d_desc, d_msgs, e->ws); break;
+            default: hipLaunchKernelGGL((k_plan<16, kBlock, true>), dim3(grid), dim3(kBlock), 0, s, a, d_desc, d_msgs, e->ws); break;
+        }
+        return;
+    }
     switch (fpt) {
         case 1: hipLaunchKernelGGL(k_plan<1>, dim3(grid), dim3(kBlock), 0, s, a, d_desc, d_msgs, e->ws); break;
         case 2: hipLaunchKernelGGL(k_plan<2>, dim3(grid), dim3(kBlock), 0, s, a, d_desc, d_msgs, e->ws); break;
