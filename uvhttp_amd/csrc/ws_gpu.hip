@@ -1913,7 +1913,8 @@ __global__ __launch_bounds__(BLOCK) void k_gather_compact(
     BatchArgs a, const uvhttp_ws_frame_desc_t* __restrict__ desc, Workspace ws,
     uint64_t arena_bytes_cap, uint64_t tile_base) {
     resolve_epoch(a, ws);
-    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_PAYLOAD, false);
+    // (no device stamp here: a StampScope in this kernel cost 2.6-2.8 % on C3 compact even with
+    // stamps off, profiles/r04_gather_stamp_ab.txt — its timeline shows plan and finalize only)
     const uint32_t n = nframes(a);
     gather_tile<BLOCK, VPT>(a, desc, ws, arena_bytes_cap, tile_base, n, first_bad_of(a, ws, n));
     // (k_finalize stays a launch of its own here: folding it in like k_scatter_compact cost
