@@ -3,7 +3,8 @@
 
   python tools/ab_lib.py LIB_A LIB_B cfg:mode [cfg:mode ...]     (mode: inplace | compact)
 
-LIB_B may be "tree" for the in-tree build.  AB_STAMPS=1 turns engine B's device stamps on.  Each round runs K decode steps with engine A,
+LIB_B may be "tree" for the in-tree build.  AB_STAMPS=1 turns engine B's device stamps on;
+AB_ENV_B="K=V,..." sets environment switches for engine B only.  Each round runs K decode steps with engine A,
 then K with engine B, on the same device buffers; reports the median whole-step time
 (torch events around the K steps) and the median payload-kernel time (engine timing)."""
 import os
@@ -27,7 +28,19 @@ def main():
     for pair in sys.argv[3:]:
         cfg, mode = pair.split(":")
         n, plen, frag = CFG[cfg]
-        engs = [U.GpuEngine(0, library=L) for L in libs]
+        engs = [U.GpuEngine(0, library=libs[0])]
+        # AB_ENV_B="K=V[,K=V]": environment switches for engine B only (read at engine creation)
+        env_b = dict(kv.split("=", 1) for kv in os.environ.get("AB_ENV_B", "").split(",") if kv)
+        old = {k: os.environ.get(k) for k in env_b}
+        os.environ.update(env_b)
+        try:
+            engs.append(U.GpuEngine(0, library=libs[1]))
+        finally:
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
         if os.environ.get("AB_STAMPS"):  # B with device stamps on (A off): their runtime cost
             engs[1].set_stamps(True)
         stride = U.gen_frame_stride(plen)
