@@ -1282,13 +1282,15 @@ __device__ __forceinline__ void unmask_tile(BatchArgs a,
     if (f1 - f0 < 2) {
         // fast path (frames of ~8 KiB and up): at most two frames touch the tile; their
         // descriptors are uniform scalar loads
+        // (the whole descriptor in one go, no branch on its status: a status test ahead of the
+        // other fields made the stream decode wait for one more dependent round trip per tile)
         for (uint32_t f = f0; f <= f1; ++f) {
-            if (a.streams && desc[f].status != UVHTTP_WS_FRAME_OK) continue;  // undelivered
-            const uint64_t ps = desc[f].payload_off;
-            const uint64_t pe = ps + desc[f].payload_len;
-            const uint32_t key = desc[f].masking_key;
+            const uvhttp_ws_frame_desc_t d = desc[f];
+            const bool ok = !a.streams || d.status == UVHTTP_WS_FRAME_OK;  // undelivered: empty
+            const uint64_t ps = d.payload_off;
+            const uint64_t pe = ps + (ok ? d.payload_len : 0);
 #pragma unroll
-            for (int v = 0; v < VPT; ++v) add_mask(m[v], va[v], ps, pe, key);
+            for (int v = 0; v < VPT; ++v) add_mask(m[v], va[v], ps, pe, d.masking_key);
         }
     } else {
         // general path: stage BLOCK frame ranges per round in LDS, binary-search per vector
