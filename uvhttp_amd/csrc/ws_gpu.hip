@@ -1282,15 +1282,27 @@ __device__ __forceinline__ void unmask_tile(BatchArgs a,
     if (f1 - f0 < 2) {
         // fast path (frames of ~8 KiB and up): at most two frames touch the tile; their
         // descriptors are uniform scalar loads
-        // (the whole descriptor in one go, no branch on its status: a status test ahead of the
-        // other fields made the stream decode wait for one more dependent round trip per tile)
-        for (uint32_t f = f0; f <= f1; ++f) {
-            const uvhttp_ws_frame_desc_t d = desc[f];
-            const bool ok = !a.streams || d.status == UVHTTP_WS_FRAME_OK;  // undelivered: empty
-            const uint64_t ps = d.payload_off;
-            const uint64_t pe = ps + (ok ? d.payload_len : 0);
+        if (a.streams) {
+            // stream decode: the whole descriptor in one go, no branch on its status (a status
+            // test ahead of the other fields cost one more dependent round trip per tile: C3
+            // streams 1403 -> 1351 us, profiles/r04_streams_desc_load_ab.txt)
+            for (uint32_t f = f0; f <= f1; ++f) {
+                const uvhttp_ws_frame_desc_t d = desc[f];
+                const uint64_t ps = d.payload_off;
+                const uint64_t pe = ps + (d.status == UVHTTP_WS_FRAME_OK ? d.payload_len : 0);
 #pragma unroll
-            for (int v = 0; v < VPT; ++v) add_mask(m[v], va[v], ps, pe, d.masking_key);
+                for (int v = 0; v < VPT; ++v) add_mask(m[v], va[v], ps, pe, d.masking_key);
+            }
+        } else {
+            // batch decode: frames below nb are delivered; the three fields only (loading the
+            // whole 32-byte descriptor here cost C3 in place 7 %, profiles/r04_desc_load_ab.txt)
+            for (uint32_t f = f0; f <= f1; ++f) {
+                const uint64_t ps = desc[f].payload_off;
+                const uint64_t pe = ps + desc[f].payload_len;
+                const uint32_t key = desc[f].masking_key;
+#pragma unroll
+                for (int v = 0; v < VPT; ++v) add_mask(m[v], va[v], ps, pe, key);
+            }
         }
     } else {
         // general path: stage BLOCK frame ranges per round in LDS, binary-search per vector
@@ -3737,6 +3749,10 @@ int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out) {
     e->fused_aux = 18;
     if (const char* fa = getenv("UVHTTP_WS_FUSED_AUX")) e->fused_aux = atoi(fa);
     e->fixup_blocks = 1024;
+    if (const char* tl = getenv("UVHTTP_WS_TILE")) {  // payload tile shape "BxV" (A/B; 0x0 = auto)
+        int tb = 0, tv = 0;
+        if (sscanf(tl, "%dx%d", &tb, &tv) == 2) (void)uvhttp_ws_gpu_engine_set_tile(e, tb, tv);  // (validated)
+    }
     if (const char* fx = getenv("UVHTTP_WS_FIXUP_BLOCKS")) e->fixup_blocks = (uint32_t)strtoul(fx, nullptr, 10);
     if (e->fixup_blocks == 0) e->fixup_blocks = 1;
     if (const char* ft = getenv("UVHTTP_WS_FUSED_TILE")) {
