@@ -1266,6 +1266,7 @@ __device__ __forceinline__ void unmask_tile(BatchArgs a,
     const uint32_t last = (nb < n ? nb : n) - 1;
     // frames overlapping [t0, t0 + kT): from the first frame of the coarse map tile holding
     // t0 to the first frame of the coarse tile after the one holding the tile's last byte
+    // (loading the two map entries ahead of the test above changed nothing, r04_hoist_ab.txt)
     const uint64_t c0 = t0 / kMapTile, c1 = (t0 + kT - 1) / kMapTile + 1;
     const uint32_t f0 = tag_get(ws.tile_first[c0], a.epoch, kNoFrame);
     uint32_t f1 = (c1 < a.n_tiles) ? tag_get(ws.tile_first[c1], a.epoch, kNoFrame) : last;
@@ -1287,11 +1288,12 @@ __device__ __forceinline__ void unmask_tile(BatchArgs a,
             // test ahead of the other fields cost one more dependent round trip per tile: C3
             // streams 1403 -> 1351 us, profiles/r04_streams_desc_load_ab.txt)
             for (uint32_t f = f0; f <= f1; ++f) {
-                const uvhttp_ws_frame_desc_t d = desc[f];
-                const uint64_t ps = d.payload_off;
-                const uint64_t pe = ps + (d.status == UVHTTP_WS_FRAME_OK ? d.payload_len : 0);
+                const uint64_t ps = desc[f].payload_off;
+                const uint64_t len = desc[f].payload_len;
+                const uint32_t key = desc[f].masking_key;
+                const uint64_t pe = ps + (desc[f].status == UVHTTP_WS_FRAME_OK ? len : 0);
 #pragma unroll
-                for (int v = 0; v < VPT; ++v) add_mask(m[v], va[v], ps, pe, d.masking_key);
+                for (int v = 0; v < VPT; ++v) add_mask(m[v], va[v], ps, pe, key);
             }
         } else {
             // batch decode: frames below nb are delivered; the three fields only (loading the
@@ -4343,6 +4345,9 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
         if (!arena || scatter) {
             blk = avg >= 32768 ? 64 : 256;
             vpt = avg >= 32768 ? 1 : avg >= 2048 ? 2 : 4;
+            // the scatter kernel wants 16 KiB tiles at 2-16 KiB frames too (C2 compact 86.2 ->
+            // 84.3 us, profiles/r04_tile_ab.txt)
+            if (scatter && avg >= 2048 && avg < 16384) vpt = 4;
         } else {
             blk = avg >= 2048 ? 64 : 256;
             vpt = 2;
