@@ -1284,14 +1284,17 @@ __device__ __forceinline__ void unmask_tile(BatchArgs a,
         // fast path (frames of ~8 KiB and up): at most two frames touch the tile; their
         // descriptors are uniform scalar loads
         if (a.streams) {
-            // stream decode: the whole descriptor in one go, no branch on its status (a status
-            // test ahead of the other fields cost one more dependent round trip per tile: C3
-            // streams 1403 -> 1351 us, profiles/r04_streams_desc_load_ab.txt)
+            // stream decode: a delivered frame's payload only (undelivered: an empty range), no
+            // branch on the status (r04_streams_desc_load_ab.txt)
             for (uint32_t f = f0; f <= f1; ++f) {
                 const uint64_t ps = desc[f].payload_off;
                 const uint64_t len = desc[f].payload_len;
                 const uint32_t key = desc[f].masking_key;
-                const uint64_t pe = ps + (desc[f].status == UVHTTP_WS_FRAME_OK ? len : 0);
+                // the status byte through its 32-bit word (opcode, flags, header_size, status):
+                // a byte field cannot be a scalar load, and as a vector load its wait also waited
+                // for the tile's data loads, serialising the mask work behind them
+                const uint32_t w6 = reinterpret_cast<const uint32_t*>(desc + f)[6];
+                const uint64_t pe = ps + ((int8_t)(w6 >> 24) == UVHTTP_WS_FRAME_OK ? len : 0);
 #pragma unroll
                 for (int v = 0; v < VPT; ++v) add_mask(m[v], va[v], ps, pe, key);
             }
