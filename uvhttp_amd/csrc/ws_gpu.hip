@@ -1229,6 +1229,10 @@ __device__ inline bool any_bits(const u32x4& m) { return (m.x | m.y | m.z | m.w)
 // store-path cache policy of the payload pass: 0 = global_store nt; 18 = buffer_store with
 // sc1|nt (write-through, not kept in L2), measured 1.7 % faster for the 64x1 shape
 // (tools/stream_probe.hip, profiles/r01_stream_probe_policy.txt)
+#ifndef UVWS_FAST_FRAMES
+#define UVWS_FAST_FRAMES 8
+#endif
+constexpr uint32_t kFastFrames = UVWS_FAST_FRAMES;  // scalar-descriptor path up to this many frames
 template <int BLOCK, int VPT, int STORE_AUX>
 __device__ __forceinline__ void unmask_tile(BatchArgs a,
                                             const uvhttp_ws_frame_desc_t* __restrict__ desc,
@@ -1280,9 +1284,10 @@ __device__ __forceinline__ void unmask_tile(BatchArgs a,
     // (a stride-layout variant that finds a vector's frame by arithmetic and loads its
     // descriptor per lane measured slower than staging the tile's frames in LDS: C4 96 -> 117
     // us, C2 89 -> 96 us — many lanes re-loading the same 32-byte descriptors)
-    if (f1 - f0 < 2) {
-        // fast path (frames of ~8 KiB and up): at most two frames touch the tile; their
-        // descriptors are uniform scalar loads
+    if (f1 - f0 < kFastFrames) {
+        // fast path: a few frames touch the tile; their descriptors are uniform scalar loads
+        // (lgkmcnt: the mask work starts when they arrive, not behind the tile's data loads,
+        // which a per-lane descriptor load would wait for on the in-order vmcnt)
         if (a.streams) {
             // stream decode: a delivered frame's payload only (undelivered: an empty range), no
             // branch on the status (r04_streams_desc_load_ab.txt)
