@@ -487,7 +487,8 @@ class GpuWorkload:
 
     def stamp_timed(self):
         """streams mode keeps the device stamps on during the timed steps (the idle between calls
-        some runs show happens there); timeline() then reads the last 15 timed calls"""
+        some runs show happens there); timeline() then reads the last 128 timed calls (the
+        engine's stamp ring)"""
         if self.streams_dev is not None:
             self.eng.set_stamps(True)
             self.eng.read_stamps()
@@ -507,7 +508,7 @@ class GpuWorkload:
             eng.set_stamps(False)
             out = summarize_stamps(recs)
             if out:
-                out["calls_from"] = "the last timed steps (stamps on while timed)"
+                out["calls_from"] = "the timed steps (stamps on while timed; up to the last 128)"
             return out
         eng.set_stamps(True)
         eng.read_stamps()  # drop anything older
@@ -568,12 +569,18 @@ def summarize_stamps(recs):
         if prev_end is not None and c - 1 in calls:
             inter.append(ks[0][0] - prev_end)
         prev_end = max(e for _, e, _ in ks)
+    mean = lambda xs: round(sum(xs) / len(xs) / 1e3, 2) if xs else None  # noqa: E731
     return {"calls": len(order), "kernels": [k for _, _, k in sorted(calls[order[-1]])],
             "payload_us": med(pay), "chain_us": med(chain),
             "gap_between_calls_us": med(inter),
             "gap_between_calls_max_us": round(max(inter) / 1e3, 2) if inter else None,
             "gaps_us": {k: med(v) for k, v in gaps.items()},
-            "source": "device wall clock (uvhttp_ws_gpu_engine_read_stamps), medians"}
+            # means and maxima too: an idle that comes in bursts moves these, not the medians
+            "chain_mean_us": mean(chain),
+            "gap_between_calls_mean_us": mean(inter),
+            "gaps_mean_us": {k: mean(v) for k, v in gaps.items()},
+            "gaps_max_us": {k: round(max(v) / 1e3, 2) for k, v in gaps.items()},
+            "source": "device wall clock (uvhttp_ws_gpu_engine_read_stamps), medians unless named"}
 
 
 def timed_run(wl, steps, warmup, world):

@@ -486,9 +486,9 @@ class GpuEngine:
     def read_stamps(self):
         """-> [(call, kernel name, begin_ns, end_ns)] of the calls the engine still holds
         (waits for the device; clears them)"""
-        buf = (GpuStamp * 256)()
+        buf = (GpuStamp * 4096)()
         n = C.c_uint32(0)
-        self._check(self._L.uvhttp_ws_gpu_engine_read_stamps(self.h, buf, 256, C.byref(n)),
+        self._check(self._L.uvhttp_ws_gpu_engine_read_stamps(self.h, buf, 4096, C.byref(n)),
                     "read_stamps")
         return [(r.call, STAMP_KERNELS.get(r.kernel, str(r.kernel)), r.begin_ns, r.end_ns)
                 for r in buf[:n.value]]

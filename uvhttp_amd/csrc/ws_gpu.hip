@@ -293,7 +293,7 @@ struct BatchArgs {
 // epoch and every word is tagged (epoch << 40) | t, so the reader keeps the newest call of each
 // slot without a reset.
 // ------------------------------------------------------------------------------------
-constexpr uint32_t kStampRing = 16, kStampKinds = 16, kStampBegin = 256, kStampEnd = 4096;
+constexpr uint32_t kStampRing = 128, kStampKinds = 16, kStampBegin = 256, kStampEnd = 4096;
 constexpr uint64_t kStampPer = kStampBegin + kStampEnd;
 constexpr uint64_t kStampLow = (1ull << 40) - 1;
 constexpr uint64_t kStampWords = (uint64_t)kStampRing * kStampKinds * kStampPer;
