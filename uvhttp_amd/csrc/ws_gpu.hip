@@ -139,6 +139,42 @@ __device__ inline ScanElem shfl_down_elem(const ScanElem& e, int delta) {
     return r;
 }
 
+// One DPP move of every word of a scan element: lanes the pattern gives no source (or whose
+// row the row mask leaves out) get the identity, which scan_combine(identity, x) ignores.
+// DPP moves are VALU operations: no LDS round trip per word as with ds_bpermute (__shfl_up).
+template <int CTRL, int RMASK>
+__device__ inline ScanElem dpp_elem(const ScanElem& e) {
+    auto mv = [](uint32_t old, uint32_t x) -> uint32_t {
+        return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)x, CTRL, RMASK, 0xF, false);
+    };
+    auto mv64 = [&](uint64_t x) -> uint64_t {
+        return (uint64_t)mv(0u, (uint32_t)x) | ((uint64_t)mv(0u, (uint32_t)(x >> 32)) << 32);
+    };
+    ScanElem r;
+    r.last_data = (int32_t)mv(0xFFFFFFFFu, (uint32_t)e.last_data);
+    r.last_start = (int32_t)mv(0xFFFFFFFFu, (uint32_t)e.last_start);
+    r.data_pay = mv64(e.data_pay);
+    r.all_pay = mv64(e.all_pay);
+    r.seg_pay = mv64(e.seg_pay);
+    r.n_fin = mv(0u, e.n_fin);
+    r.n_close = mv(0u, e.n_close);
+    r.bits = mv(0u, e.bits);
+    return r;
+}
+
+// inclusive wave scan (lane i ends with v[0] (+) ... (+) v[i]): within rows of 16 by row_shr
+// 1, 2, 4, 8, then across rows by row_bcast:15 (rows 1 and 3 take the row before's total) and
+// row_bcast:31 (rows 2 and 3 take rows 0-1's)
+__device__ inline ScanElem wave_inclusive_scan(ScanElem v) {
+    v = scan_combine(dpp_elem<0x111, 0xF>(v), v);
+    v = scan_combine(dpp_elem<0x112, 0xF>(v), v);
+    v = scan_combine(dpp_elem<0x114, 0xF>(v), v);
+    v = scan_combine(dpp_elem<0x118, 0xF>(v), v);
+    v = scan_combine(dpp_elem<0x142, 0xA>(v), v);
+    v = scan_combine(dpp_elem<0x143, 0xC>(v), v);
+    return v;
+}
+
 // ordered wave reduction: lane 0 ends with v[63] (+) ... (+) v[0] — lane 63 is the OLDEST
 __device__ inline ScanElem wave_reduce_newest_first(ScanElem v) {
     const int lane = threadIdx.x & 63;
@@ -158,12 +194,16 @@ __device__ ScanElem block_exclusive_scan(ScanElem v, ScanElem* total) {
     __shared__ ScanElem wave_tot[NT / 64];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
+#ifdef UVWS_SCAN_BPERMUTE
     ScanElem inc = v;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
         ScanElem o = shfl_up_elem(inc, d);
         if (lane >= d) inc = scan_combine(o, inc);
     }
+#else
+    const ScanElem inc = wave_inclusive_scan(v);
+#endif
     if (lane == 63) wave_tot[wave] = inc;
     __syncthreads();
     ScanElem wave_pre = scan_identity();
@@ -1001,13 +1041,17 @@ __global__ __launch_bounds__(NT) void k_plan(BatchArgs a, uvhttp_ws_frame_desc_t
                 elem = parse_one(a, i0, g, d);
             }
         }
+        phase(1);
         ScanElem agg;
         const ScanElem local = block_exclusive_scan<NT>(elem, &agg);
+        phase(2);
         const ScanElem pre = lookback_prefix<NT>(ws, b, agg, a.epoch, a.max_polls);
+        phase(3);
         if (i0 < n) {
             resolve_one(a, msgs, ws, i0, n, g, scan_combine(pre, local), d);
             desc[i0] = d;
         }
+        phase(4);
         return;
     }
     // pass 1: all header loads of the lane's frames in flight together, then parse into
