@@ -827,7 +827,11 @@ __device__ ScanElem lookback_prefix(const Workspace& ws, uint32_t b, const ScanE
     uint32_t polls = 0;              // uniform: every thread counts the same rounds
     bool gave_up = false;
     for (;;) {
+#ifdef UVWS_LOOKBACK_BPERMUTE
         const int64_t j = end - 1 - t;  // larger t = older block
+#else
+        const int64_t j = end - NT + t;  // larger t = newer block (window order = lane order)
+#endif
         ScanElem v = scan_identity();
         bool is_p = j < 0, ready = j < 0;  // lanes before block 0: identity "P"
         for (;;) {
@@ -849,6 +853,7 @@ __device__ ScanElem lookback_prefix(const Workspace& ws, uint32_t b, const ScanE
             // back off so waiting blocks do not flood memory while predecessors still parse
             __builtin_amdgcn_s_sleep(8);
         }
+#ifdef UVWS_LOOKBACK_BPERMUTE
         // nearest published prefix (smallest t with P)
         if (t == 0) s_kstar = NT;
         __syncthreads();
@@ -867,6 +872,27 @@ __device__ ScanElem lookback_prefix(const Workspace& ws, uint32_t b, const ScanE
             run = scan_combine(w, run);
             s_go = (kstar < NT || gave_up) ? 0 : 1;
         }
+#else
+        // nearest published prefix: the largest t with P; the window from it to the newest
+        // block, combined in lane order by the DPP wave scan (lane 63 holds the wave's part)
+        if (t == 0) s_kstar = -1;
+        __syncthreads();
+        const uint64_t pm = __ballot(is_p);
+        if (lane == 0 && pm) atomicMax(&s_kstar, wave * 64 + 63 - __builtin_clzll(pm));
+        __syncthreads();
+        const int kstar = s_kstar;
+        if (t < kstar || j < 0) v = scan_identity();
+        v = wave_inclusive_scan(v);
+        if (lane == 63) s_wave[wave] = v;
+        __syncthreads();
+        if (t == 0) {
+            ScanElem w = scan_identity();
+#pragma unroll
+            for (int k = 0; k < NT / 64; ++k) w = scan_combine(w, s_wave[k]);
+            run = scan_combine(w, run);
+            s_go = (kstar >= 0 || gave_up) ? 0 : 1;
+        }
+#endif
         __syncthreads();
         if (!s_go) break;
         end -= NT;
