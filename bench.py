@@ -814,12 +814,14 @@ def main():
         dist.destroy_process_group()
 
 
-def e2e_warmup(local, max_runs=6):
+def e2e_warmup(local, min_runs=4, max_runs=8):
     """PCIe/host-path warm-up before the e2e numbers: on a fresh box the first few seconds of
     host<->device traffic run slower (the live harness: 17 then 24 then 40 GiB/s in three
     consecutive processes, the same 40 after; tools/e2e_order.sh,
     profiles/r04_e2e_order.jsonl) — the link's power state ramps with sustained traffic.  Runs
-    the async live harness until two consecutive runs agree within 5 %; returns their values."""
+    the async live harness at least min_runs times (two runs of a cold box can agree at the cold
+    rate: 24.1, 23.7 GiB/s, then 40 — r04_pipeline_sweep2.jsonl) and until two consecutive runs
+    agree within 5 %; returns their values."""
     exe = os.path.join(REPO, "tests", "c", "_build", "batcher_e2e")
     vals = []
     for _ in range(max_runs):
@@ -829,7 +831,7 @@ def e2e_warmup(local, max_runs=6):
         if p.returncode != 0:
             break
         vals.append(json.loads(p.stdout.strip().splitlines()[-1])["value"])
-        if len(vals) >= 2 and abs(vals[-1] - vals[-2]) <= 0.05 * vals[-1]:
+        if len(vals) >= min_runs and abs(vals[-1] - vals[-2]) <= 0.05 * vals[-1]:
             break
     return vals
 
