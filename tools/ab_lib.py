@@ -17,7 +17,9 @@ import torch  # noqa: E402
 
 import uvhttp_amd as U  # noqa: E402
 
-CFG = {"c2": (65536, 4096, False), "c3": (65536, 65536, False), "c4": (1048576, 256, True)}
+CFG = {"c2": (65536, 4096, False), "c3": (65536, 65536, False), "c4": (1048576, 256, True),
+       # (extra frame sizes for shape rules: same 256 MiB of payload)
+       "f2k": (131072, 2048, False), "f8k": (32768, 8192, False), "f16k": (16384, 16384, False)}
 
 
 def main():

@@ -1299,6 +1299,17 @@ __device__ inline bool any_bits(const u32x4& m) { return (m.x | m.y | m.z | m.w)
 // store-path cache policy of the payload pass: 0 = global_store nt; 18 = buffer_store with
 // sc1|nt (write-through, not kept in L2), measured 1.7 % faster for the 64x1 shape
 // (tools/stream_probe.hip, profiles/r01_stream_probe_policy.txt)
+// the in-place payload kernel's tile shape by average wire bytes per frame (tools/ab_lib.py
+// UVHTTP_WS_TILE sweeps, profiles/r04_tile_sizes_ab.txt): since the scalar-descriptor path takes
+// up to kFastFrames frames per tile, small tiles win from 2.5 KiB frames up — 2 KiB tiles
+// (64 x 2) at 2.5-12 KiB frames (C2 +1.5-2.5 %, 8 KiB +4 %), 1 KiB tiles (64 x 1) above (16 KiB
+// +7 %, 64 KiB as before); 256 x 2 / 256 x 4 below
+__host__ inline void inplace_tile_shape(uint64_t avg, int& blk, int& vpt) {
+    if (avg >= 12288) blk = 64, vpt = 1;
+    else if (avg >= 2560) blk = 64, vpt = 2;
+    else blk = 256, vpt = avg >= 2048 ? 2 : 4;
+}
+
 #ifndef UVWS_FAST_FRAMES
 #define UVWS_FAST_FRAMES 8
 #endif
@@ -4420,12 +4431,14 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
     // scatter kernel, larger ones the arena-driven gather (UVHTTP_WS_COMPACT=gather|scatter)
     const bool scatter = arena && (e->compact_mode ? e->compact_mode == 2 : avg < kScatterAvg);
     if (!blk) {
-        if (!arena || scatter) {
+        if (!arena) {
+            inplace_tile_shape(avg, blk, vpt);
+        } else if (scatter) {
             blk = avg >= 32768 ? 64 : 256;
             vpt = avg >= 32768 ? 1 : avg >= 2048 ? 2 : 4;
             // the scatter kernel wants 16 KiB tiles at 2-16 KiB frames too (C2 compact 86.2 ->
             // 84.3 us, profiles/r04_tile_ab.txt)
-            if (scatter && avg >= 2048 && avg < 16384) vpt = 4;
+            if (avg >= 2048 && avg < 16384) vpt = 4;
         } else {
             blk = avg >= 2048 ? 64 : 256;
             vpt = 2;
@@ -4647,8 +4660,7 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     int blk = e->tile_block, vpt = e->tile_vpt;
     if (!blk) {
         const uint64_t avg = max_frames ? wire_len / max_frames : wire_len;
-        blk = avg >= 32768 ? 64 : 256;
-        vpt = avg >= 32768 ? 1 : avg >= 2048 ? 2 : 4;
+        inplace_tile_shape(avg, blk, vpt);
     }
     const uint64_t tile_bytes = (uint64_t)blk * vpt * 16;
     const uint64_t n_ptiles = (wire_len + tile_bytes - 1) / tile_bytes;
