@@ -558,12 +558,14 @@ def summarize_stamps(recs):
     if not order:
         return None
     med = lambda xs: round(statistics.median(xs) / 1e3, 2) if xs else None  # noqa: E731
-    pay, chain, inter, gaps = [], [], [], {}
+    pay, chain, inter, gaps, durs = [], [], [], {}, {}
     prev_end = None
     for c in order:
         ks = sorted(calls[c])
         chain.append(ks[-1][1] - ks[0][0])
         pay += [e - b for b, e, k in ks if k == "payload"]
+        for b, e, k in ks:
+            durs.setdefault(k, []).append(e - b)
         for (b0, e0, k0), (b1, e1, k1) in zip(ks, ks[1:]):
             gaps.setdefault(f"{k0}->{k1}", []).append(b1 - e0)
         if prev_end is not None and c - 1 in calls:
@@ -575,6 +577,7 @@ def summarize_stamps(recs):
             "gap_between_calls_us": med(inter),
             "gap_between_calls_max_us": round(max(inter) / 1e3, 2) if inter else None,
             "gaps_us": {k: med(v) for k, v in gaps.items()},
+            "kernels_us": {k: med(v) for k, v in durs.items()},
             # means and maxima too: an idle that comes in bursts moves these, not the medians
             "chain_mean_us": mean(chain),
             "gap_between_calls_mean_us": mean(inter),
