@@ -1021,8 +1021,38 @@ __global__ __launch_bounds__(NT) void k_plan(BatchArgs a, uvhttp_ws_frame_desc_t
         ScanElem tagg = scan_identity();
         FrameRec r[FPT];
         const uint32_t ilast = n ? n - 1 : 0;
+#ifdef UVWS_REC_LDS
+        if constexpr (FPT == 16 && NT == kBlock) {
+            // experiment: coalesced record loads (load k of a wave reads 64 consecutive records),
+            // handed to their owner lanes through LDS (one pad vector per 16 records keeps the
+            // owner reads, 272 bytes apart, off a single bank)
+            __shared__ u32x4 s_rec[NT / 64][64 * FPT + 64];
+            const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+            const uint32_t wbase = (b * NT + wv * 64) * FPT;
+            const u32x4* rv = reinterpret_cast<const u32x4*>(a.recs);
+            u32x4 tmp[FPT];
 #pragma unroll
-        for (int k = 0; k < FPT; ++k) r[k] = a.recs[i0 + k < n ? i0 + k : ilast];
+            for (int k = 0; k < FPT; ++k) {
+                const uint32_t idx = wbase + k * 64 + lane;
+                tmp[k] = rv[idx < n ? idx : ilast];
+            }
+#pragma unroll
+            for (int k = 0; k < FPT; ++k) {
+                const uint32_t j = k * 64 + lane;
+                s_rec[wv][j + (j >> 4)] = tmp[k];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < FPT; ++k) {
+                const u32x4 v = s_rec[wv][lane * 17 + k];
+                __builtin_memcpy(&r[k], &v, sizeof v);
+            }
+        } else
+#endif
+        {
+#pragma unroll
+            for (int k = 0; k < FPT; ++k) r[k] = a.recs[i0 + k < n ? i0 + k : ilast];
+        }
 #pragma unroll
         for (int k = 0; k < FPT; ++k) {
             const uint32_t i = i0 + k;
