@@ -6,12 +6,14 @@ CC ?= gcc
 ARCH ?= gfx950
 BUILD := uvhttp_amd/build
 LIB := uvhttp_amd/lib/libuvhttp_ws_amd.so
+# the same library with the batcher's fault-injection hook compiled in (tests only)
+TESTLIB := uvhttp_amd/lib/libuvhttp_ws_amd_testhooks.so
 
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Iinclude -Wall -Werror \
             -mcode-object-version=5
 CFLAGS := -O2 -DNDEBUG -fPIC -std=gnu11 -Iinclude -Wall -Wextra -Werror
 
-all: $(LIB) oracle ctests probes
+all: $(LIB) $(TESTLIB) oracle ctests probes
 
 $(BUILD)/ws_gpu.o: uvhttp_amd/csrc/ws_gpu.hip include/uvhttp_ws_amd.h
 	@mkdir -p $(BUILD)
@@ -25,6 +27,10 @@ $(BUILD)/ws_batcher.o: uvhttp_amd/csrc/ws_batcher.hip include/uvhttp_ws_amd.h
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
+$(BUILD)/ws_batcher_testhooks.o: uvhttp_amd/csrc/ws_batcher.hip include/uvhttp_ws_amd.h
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -DUVWS_TEST_HOOKS -c -o $@ $<
+
 $(BUILD)/ws_host.o: uvhttp_amd/csrc/ws_host.c include/uvhttp_ws_amd.h
 	@mkdir -p $(BUILD)
 	$(CC) $(CFLAGS) -c -o $@ $<
@@ -36,6 +42,11 @@ $(BUILD)/ws_batcher_group.o: uvhttp_amd/csrc/ws_batcher_group.cpp include/uvhttp
 
 $(LIB): $(BUILD)/ws_gpu.o $(BUILD)/tls_gpu.o $(BUILD)/ws_batcher.o $(BUILD)/ws_host.o \
         $(BUILD)/ws_batcher_group.o
+	@mkdir -p $(dir $@)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+
+$(TESTLIB): $(BUILD)/ws_gpu.o $(BUILD)/tls_gpu.o $(BUILD)/ws_batcher_testhooks.o $(BUILD)/ws_host.o \
+            $(BUILD)/ws_batcher_group.o
 	@mkdir -p $(dir $@)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 

@@ -551,15 +551,15 @@ def summarize_stamps(recs):
     kernel start .. last kernel end), the gap at every kernel boundary inside a call, and the
     idle between one call's last kernel and the next call's first."""
     import statistics
-    calls = {}
+    calls = {}  # in the order read_stamps returns them: oldest call first (tags wrap)
     for call, kern, b, e in recs:
         calls.setdefault(call, []).append((b, e, kern))
-    order = sorted(calls)
+    order = list(calls)
     if not order:
         return None
     med = lambda xs: round(statistics.median(xs) / 1e3, 2) if xs else None  # noqa: E731
     pay, chain, inter, gaps, durs = [], [], [], {}, {}
-    prev_end = None
+    prev_end, prev_c = None, None
     for c in order:
         ks = sorted(calls[c])
         chain.append(ks[-1][1] - ks[0][0])
@@ -568,9 +568,9 @@ def summarize_stamps(recs):
             durs.setdefault(k, []).append(e - b)
         for (b0, e0, k0), (b1, e1, k1) in zip(ks, ks[1:]):
             gaps.setdefault(f"{k0}->{k1}", []).append(b1 - e0)
-        if prev_end is not None and c - 1 in calls:
+        if prev_end is not None and (c - prev_c) % ((1 << 24) - 1) == 1:  # consecutive calls
             inter.append(ks[0][0] - prev_end)
-        prev_end = max(e for _, e, _ in ks)
+        prev_end, prev_c = max(e for _, e, _ in ks), c
     mean = lambda xs: round(sum(xs) / len(xs) / 1e3, 2) if xs else None  # noqa: E731
     return {"calls": len(order), "kernels": [k for _, _, k in sorted(calls[order[-1]])],
             "payload_us": med(pay), "chain_us": med(chain),

@@ -355,7 +355,8 @@ int uvhttp_ws_gpu_engine_sync(uvhttp_ws_gpu_engine_t* eng, void* stream);
 #define UVHTTP_WS_STAMP_FIXUP 7       /* k_fixup (fused stride path) */
 #define UVHTTP_WS_STAMP_FINALIZE 8    /* k_finalize */
 typedef struct {
-    uint32_t call;      /* the call's tag (increases by one per decode call, mod 2^24) */
+    uint32_t call;      /* the call's tag: 1 .. 2^24 - 1, one more per decode call (after
+                           2^24 - 1 wraps to 1); records come oldest call first */
     uint32_t kernel;    /* UVHTTP_WS_STAMP_* */
     uint64_t begin_ns;  /* device wall clock, ns: earliest sampled workgroup start */
     uint64_t end_ns;    /* latest wave end */
@@ -735,11 +736,14 @@ void uvhttp_ws_amd_batcher_group_free(uvhttp_ws_amd_batcher_group_t* g);
 int uvhttp_ws_amd_batcher_group_size(const uvhttp_ws_amd_batcher_group_t* g);
 /* member i (its stats, NUMA node), or NULL */
 uvhttp_ws_amd_batcher_t* uvhttp_ws_amd_batcher_group_batcher(uvhttp_ws_amd_batcher_group_t* g, int i);
-/* the member a connection is pinned to (pins it now if it is new) */
+/* the member a connection is pinned to, or -1 if it is not pinned (a query: never pins) */
 int uvhttp_ws_amd_batcher_group_member(uvhttp_ws_amd_batcher_group_t* g, struct uvhttp_ws_connection* conn);
 uvhttp_error_t uvhttp_ws_amd_batcher_group_submit_read(uvhttp_ws_amd_batcher_group_t* g,
                                                        struct uvhttp_ws_connection* conn,
                                                        const uint8_t* data, size_t len);
+/* TLS records open only on device members: a new connection is pinned among them, and one
+ * pinned to a host-decoder member moves to a device member when the host member holds nothing
+ * of it (reads queued, a failure mark); otherwise, or with no device member, UVHTTP_WS_GPU_ENODEV */
 int uvhttp_ws_amd_batcher_group_set_tls(uvhttp_ws_amd_batcher_group_t* g, struct uvhttp_ws_connection* conn,
                                         const void* tls_key, uint64_t read_seq);
 uvhttp_error_t uvhttp_ws_amd_batcher_group_submit_tls_read(uvhttp_ws_amd_batcher_group_t* g,

@@ -63,3 +63,10 @@ def test_product_does_not_reference_oracle():
             assert "libws_oracle" not in txt and "import _oracle" not in txt, p
     blob = open(U.LIB_PATH, "rb").read()
     assert b"libws_oracle" not in blob and b"oracle_" not in blob
+
+
+def test_fault_injection_only_in_the_test_build():
+    """The batcher's fault-injection variable is read only by the test build
+    (libuvhttp_ws_amd_testhooks.so, -DUVWS_TEST_HOOKS); the product library has no such hook."""
+    assert b"UVHTTP_WS_BATCHER_FAIL_EVERY" not in open(U.LIB_PATH, "rb").read()
+    assert b"UVHTTP_WS_BATCHER_FAIL_EVERY" in open(U.TESTHOOKS_LIB_PATH, "rb").read()

@@ -71,23 +71,83 @@ def test_group_matches_process_data(devices, seed):
 
 
 def test_group_pinning_and_balance():
-    """first call pins a connection to the least-loaded member (ties: round robin); it stays
-    there across flushes; forget releases its place"""
+    """a connection's first read pins it to the least-loaded member (ties: round robin); it
+    stays there across flushes; forget releases its place; member() is a query that never pins"""
     import uvhttp_amd as U
     b = U.BatcherGroup([-1, -1, -1, -1])
     conns = [U.WsConnection(1) for _ in range(10)]
-    ms = [b.member(c) for c in conns]
-    assert sorted(ms) == [0, 0, 0, 1, 1, 1, 2, 2, 3, 3]
-    assert [b.member(c) for c in conns] == ms  # pinned
+    assert [b.member(c) for c in conns] == [-1] * 10  # asking does not pin
     frame = b"\x82\x85" + b"\x01\x02\x03\x04" + bytes(x ^ k for x, k in zip(b"hello", b"\x01\x02\x03\x04\x01"))
     for c in conns:
         assert b.submit(c, frame) == 0
+    ms = [b.member(c) for c in conns]
+    assert sorted(ms) == [0, 0, 0, 1, 1, 1, 2, 2, 3, 3]
     assert b.flush() == 0
     assert all([e[2] for e in c.events if e[0] == "message"] == [b"hello"] for c in conns)
-    assert [b.member(c) for c in conns] == ms
-    b.forget(conns[3])  # member 3 drops to one connection... (conns[3] is on member ms[3])
+    assert [b.member(c) for c in conns] == ms  # pinned across the flush
+    b.forget(conns[3])  # its member drops to the fewest connections
+    assert b.member(conns[3]) == -1
     fresh = U.WsConnection(1)
-    assert b.member(fresh) == ms[3]
+    assert b.member(fresh) == -1
+    assert b.submit(fresh, frame) == 0 and b.member(fresh) == ms[3]
+    assert b.flush() == 0
+    b.close()
+
+
+def test_group_tls_needs_a_device_member():
+    """TLS records open only on a device member: in a host-only group set_tls pins nothing and
+    returns ENODEV"""
+    import uvhttp_amd as U
+    b = U.BatcherGroup([-1, -1])
+    c = U.WsConnection(1)
+    assert b.set_tls(c, bytes(64), 0) == -2
+    assert b.member(c) == -1
+    b.close()
+
+
+@pytest.mark.gpu
+def test_group_tls_in_a_mixed_group():
+    """in a [GPU, host] group every TLS connection goes to the device member — new
+    ones, and ones already pinned to the host member that hold nothing there yet (their reads
+    were delivered); a connection with reads still queued on the host member stays (ENODEV).
+    Each TLS connection's records then decode against the oracle."""
+    _need([0])
+    import uvhttp_amd as U
+    import _oracle as O
+    from test_gpu_batcher_tls import _seal_stream
+    from test_gpu_tls_ws_chain import _ws_frames
+    rng = random.Random(77)
+    b = U.BatcherGroup([0, -1], min_device_bytes=0, max_bytes=4 << 20)
+    frame = b"\x82\x80" + rng.randbytes(4)
+    conns = []
+    for k in range(6):
+        prod = U.WsConnection(1)
+        if k % 2:  # first a plain read, delivered by whichever member it pinned to
+            assert b.submit(prod, frame) == 0
+            assert b.flush() == 0
+        key = O.tls_key(rng.randbytes(16), rng.randbytes(12), O.TLS13, O.AES_GCM)
+        assert b.set_tls(prod, key.tobytes(), 0) == 0, k
+        assert b.member(prod) == 0
+        frames = _ws_frames(rng, 6, small=True)
+        cipher = _seal_stream(rng, key, 0, frames, rec=900)
+        assert b.submit_tls(prod, cipher) == 0
+        conns.append((prod, frames, k % 2))
+    # a plain read queued on the host member: that connection cannot move
+    busy = [U.WsConnection(1) for _ in range(2)]
+    for c in busy:
+        assert b.submit(c, frame) == 0
+    stuck = [c for c in busy if b.member(c) == 1]
+    assert stuck, [b.member(c) for c in busy]
+    assert b.set_tls(stuck[0], bytes(64), 0) == -2 and b.member(stuck[0]) == 1
+    assert b.flush() == 0
+    for prod, frames, pre in conns:
+        orc = O.OracleConn(1, record=1)
+        if pre:
+            assert orc.process_data(frame) == 0
+        assert orc.process_data(frames) == 0
+        pev = [e for e in prod.events if e[0] == "message"]
+        oev = [e for e in orc.events() if e[0] == "message"]
+        assert pev == oev and len(pev) >= 1
     b.close()
 
 

@@ -239,7 +239,7 @@ def test_capacity_and_device_failure_fall_back_to_host():
 
     os.environ["UVHTTP_WS_BATCHER_FAIL_EVERY"] = "1"
     try:
-        b = U.Batcher(device=0, min_device_bytes=0)
+        b = U.Batcher(device=0, min_device_bytes=0, library=U.test_hooks_library())
     finally:
         del os.environ["UVHTTP_WS_BATCHER_FAIL_EVERY"]
     pairs = [Pair(U, rng, reads=_conn_reads(rng)) for _ in range(10)]

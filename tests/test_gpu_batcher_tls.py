@@ -227,7 +227,7 @@ def test_tls_device_error_hands_ciphertext_back(torch, monkeypatch):
     import uvhttp_amd as U
     monkeypatch.setenv("UVHTTP_WS_BATCHER_FAIL_EVERY", "1")
     rng = random.Random(4500)
-    b = U.Batcher(device=0, min_device_bytes=0, max_bytes=4 << 20)
+    b = U.Batcher(device=0, min_device_bytes=0, max_bytes=4 << 20, library=U.test_hooks_library())
     monkeypatch.delenv("UVHTTP_WS_BATCHER_FAIL_EVERY")
     conns = []
     for k in range(5):

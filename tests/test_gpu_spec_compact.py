@@ -199,3 +199,36 @@ def test_speculation_off_matches(torch, eng, monkeypatch):
             _compare(ref, got, compact=True)
     finally:
         e0.close()
+
+
+@pytest.mark.parametrize("stride", [64, 264, 1000])
+def test_arena_smaller_than_the_batch(torch, eng, stride):
+    """an arena that ends part-way through a uniform batch (caps that are not a
+    multiple of 16 too).  The speculative pass clamps its writes at arena_cap: statuses, summary
+    and messages equal the oracle's (which copies only the frames that fit), every frame that
+    fits whole is in the arena, and nothing is written past arena_cap."""
+    from test_gpu_parity import GUARD, _guard_ok, _guarded, _to_dev
+    import _oracle
+    rng = random.Random(stride)
+    n = 2000
+    p = _uniform_p(stride)
+    wire = _stride_batch(rng, n, stride, frag=0.3)
+    for cap in (p * n // 2 + 5, (p * n // 3) & ~15, p * 3 + 1, 17, p * n - 1):
+        ref = _oracle.decode_batch(wire, n, stride=stride, max_message_size=0, compact=True,
+                                   arena_cap=cap)
+        dw = _to_dev(torch, wire)
+        arena_all, arena = _guarded(torch, cap)
+        desc, msgs, summ = eng.decode_compact(dw, n, arena, stride=stride, max_message_size=0,
+                                              wire_len=wire.size)
+        torch.cuda.synchronize()
+        s = eng.read_summary(summ)
+        assert s == ref["summary"], (cap, s, ref["summary"])
+        assert np.array_equal(eng.read_desc(desc, n)["status"], ref["status"])
+        assert np.array_equal(dw[: wire.size].cpu().numpy(), ref["wire"])
+        m = eng.read_msgs(msgs, s["n_messages"])
+        assert np.array_equal(m["arena_off"], ref["msg_off"]) and np.array_equal(m["len"], ref["msg_len"])
+        whole = (cap // p) * p  # the frames that fit whole
+        got = arena.cpu().numpy()
+        assert np.array_equal(got[:whole], ref["arena"][:whole]), cap
+        assert _guard_ok(arena_all, cap), f"write past arena_cap {cap}"
+        assert GUARD == 0xA5

@@ -29,8 +29,9 @@ def _check_calls(recs, kernels_expected, calls):
         assert e >= b, (call, kern, b, e)
         by_call.setdefault(call, []).append((b, e, kern))
     assert len(by_call) == calls
-    order = sorted(by_call)
-    assert order == list(range(order[0], order[0] + calls))  # consecutive epochs
+    order = list(by_call)  # read_stamps returns the oldest call first (tags wrap at 2^24 - 1)
+    assert all(1 <= c < (1 << 24) for c in order)
+    assert [(c - order[0]) % ((1 << 24) - 1) for c in order] == list(range(calls))  # consecutive
     prev_end = 0
     for c in order:
         ks = sorted(by_call[c])

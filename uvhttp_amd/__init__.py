@@ -25,6 +25,8 @@ __all__ = [
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libuvhttp_ws_amd.so")
+# the same library built with -DUVWS_TEST_HOOKS (the batcher's fault injection); tests only
+TESTHOOKS_LIB_PATH = os.path.join(_HERE, "lib", "libuvhttp_ws_amd_testhooks.so")
 
 OPCODES = dict(CONTINUATION=0x0, TEXT=0x1, BINARY=0x2, CLOSE=0x8, PING=0x9, PONG=0xA)
 FRAME_STATUS = {
@@ -211,6 +213,18 @@ def lib() -> C.CDLL:
     return _LIB
 
 
+_TESTHOOKS = None
+
+
+def test_hooks_library() -> C.CDLL:
+    """The test build (UVHTTP_WS_BATCHER_FAIL_EVERY honoured); the product library ignores the
+    variable.  Tests pass it as Batcher(..., library=...)."""
+    global _TESTHOOKS
+    if _TESTHOOKS is None:
+        _TESTHOOKS = load_library(TESTHOOKS_LIB_PATH)
+    return _TESTHOOKS
+
+
 def load_library(path: str) -> C.CDLL:
     """Load a build of libuvhttp_ws_amd.so from `path` and declare its entry points (lib()
     uses the in-tree build; tools/ab_lib.py loads a second build beside it for A/B runs)."""
@@ -317,7 +331,7 @@ def load_library(path: str) -> C.CDLL:
         "uvhttp_tls_gpu_ws_streams": (C.c_int, [vp, vp, vp, u32, vp, vp, vp, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
-        if path != LIB_PATH and not hasattr(L, name):
+        if path not in (LIB_PATH, TESTHOOKS_LIB_PATH) and not hasattr(L, name):
             continue  # an older build loaded beside the tree's for an A/B run (tools/ab_lib.py)
         fn = getattr(L, name)
         fn.restype = res
@@ -785,8 +799,8 @@ class Batcher:
     device=-1 runs the host decoder only; failures arrive in self.failures {conn ptr: rc}."""
 
     def __init__(self, device=-1, min_device_bytes=0, max_bytes=32 << 20,
-                 max_connections=16384, max_reads=1 << 18):
-        L = lib()
+                 max_connections=16384, max_reads=1 << 18, library: C.CDLL = None):
+        L = library or lib()
         self._L = L
         cfg = BatcherConfig()
         L.uvhttp_ws_amd_batcher_config_init(C.byref(cfg))

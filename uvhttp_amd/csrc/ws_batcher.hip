@@ -172,8 +172,13 @@ struct uvhttp_ws_amd_batcher {
     hipStream_t up = nullptr;  // H2D of the arenas
     hipStream_t cs = nullptr;  // gather, decode, D2H
     uint64_t wire_cap = 0;
-    uint32_t fail_every = 0;  // test hook (UVHTTP_WS_BATCHER_FAIL_EVERY=k): every k-th device
-    uint32_t launches = 0;    // launch reports ELAUNCH before enqueueing anything
+#ifdef UVWS_TEST_HOOKS
+    // fault injection, compiled only into the test build (libuvhttp_ws_amd_testhooks.so):
+    // UVHTTP_WS_BATCHER_FAIL_EVERY=k makes every k-th device launch report ELAUNCH before
+    // enqueueing anything
+    uint32_t fail_every = 0;
+    uint32_t launches = 0;
+#endif
     uvhttp_tls_gpu_engine_t* teng = nullptr;  // record open (first set_tls)
     std::unordered_map<uvhttp_ws_connection_t*, TlsConn> tls;
     // descriptors a launch copies back: a high-water mark of recent flushes' frame counts (the
@@ -518,7 +523,9 @@ int launch_device(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
         const int gt = grow_tls(b, q, max_records, q.wdesc_cap ? q.wdesc_cap : kMinFrames);
         if (gt) return gt;
     }
+#ifdef UVWS_TEST_HOOKS
     if (b->fail_every && ++b->launches % b->fail_every == 0) return UVHTTP_WS_GPU_ELAUNCH;
+#endif
     hipStream_t s = b->cs;
     // UVHTTP_WS_BATCHER_TRACE=1: host time of each enqueue step on stderr (diagnostics)
     static const bool trace = getenv("UVHTTP_WS_BATCHER_TRACE") != nullptr;
@@ -990,7 +997,9 @@ int uvhttp_ws_amd_batcher_create(const uvhttp_ws_amd_batcher_config_t* cfg,
             return rc;
         }
         b->wire_cap = cfg->max_bytes + 16ull * cfg->max_connections + 64;
+#ifdef UVWS_TEST_HOOKS
         if (const char* fe = getenv("UVHTTP_WS_BATCHER_FAIL_EVERY")) b->fail_every = (uint32_t)atoi(fe);
+#endif
         int prev = 0;
         (void)hipGetDevice(&prev);
         (void)hipSetDevice(cfg->device);
@@ -1227,6 +1236,20 @@ void uvhttp_ws_amd_batcher_forget(uvhttp_ws_amd_batcher_t* b, struct uvhttp_ws_c
         // the arena, unreferenced)
         if (i == b->cur) q.slot_of.erase(it);
     }
+}
+
+// library-internal (the batcher group): 1 while the batcher holds anything of `conn` — reads
+// queued or in flight, a failure mark, TLS state — so the group may move it to another member
+__attribute__((visibility("hidden"))) int uvhttp_ws_amd_batcher_holds_conn(
+    const uvhttp_ws_amd_batcher_t* b, const uvhttp_ws_connection_t* conn) {
+    uvhttp_ws_connection_t* c = const_cast<uvhttp_ws_connection_t*>(conn);
+    if (b->failed.count(c) || b->tls.count(c)) return 1;
+    for (int i = 0; i < 2; ++i) {
+        const BatchQueue& q = b->q[i];
+        auto it = q.slot_of.find(c);
+        if (it != q.slot_of.end() && !q.slots[it->second].dropped) return 1;
+    }
+    return 0;
 }
 
 int uvhttp_ws_amd_batcher_numa_node(const uvhttp_ws_amd_batcher_t* b) {

@@ -21,8 +21,14 @@
 
 #include "uvhttp_ws_amd.h"
 
+// ws_batcher.hip (library-internal): 1 while the batcher holds anything of `conn` (queued
+// reads, a failure mark, TLS state)
+extern "C" int uvhttp_ws_amd_batcher_holds_conn(const uvhttp_ws_amd_batcher_t* b,
+                                                const uvhttp_ws_connection_t* conn);
+
 struct uvhttp_ws_amd_batcher_group {
     std::vector<uvhttp_ws_amd_batcher_t*> members;
+    std::vector<int> devices;    // each member's device (-1: host decoder)
     std::vector<uint64_t> live;  // connections pinned to each member
     std::unordered_map<uvhttp_ws_connection_t*, uint32_t> member_of;
     uint32_t next = 0;  // round-robin start among equally loaded members
@@ -30,21 +36,30 @@ struct uvhttp_ws_amd_batcher_group {
 
 namespace {
 
-// the member a connection belongs to; a new connection goes to the member with the fewest
-// live connections (ties: round robin), and stays there until forget
-uint32_t member_for(uvhttp_ws_amd_batcher_group_t* g, uvhttp_ws_connection_t* conn) {
-    auto it = g->member_of.find(conn);
-    if (it != g->member_of.end()) return it->second;
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+
+// pin a new connection to the member with the fewest live connections (ties: round robin),
+// among the device members only when device_only; kNone if there is no such member
+uint32_t pin(uvhttp_ws_amd_batcher_group_t* g, uvhttp_ws_connection_t* conn, bool device_only) {
     const uint32_t n = (uint32_t)g->members.size();
-    uint32_t best = g->next % n;
+    uint32_t best = kNone;
     for (uint32_t k = 0; k < n; ++k) {
         const uint32_t m = (g->next + k) % n;
-        if (g->live[m] < g->live[best]) best = m;
+        if (device_only && g->devices[m] < 0) continue;
+        if (best == kNone || g->live[m] < g->live[best]) best = m;
     }
+    if (best == kNone) return kNone;
     g->next = best + 1;
     g->live[best]++;
     g->member_of.emplace(conn, best);
     return best;
+}
+
+// the member a connection belongs to (pinned on its first read, until forget)
+uint32_t member_for(uvhttp_ws_amd_batcher_group_t* g, uvhttp_ws_connection_t* conn) {
+    auto it = g->member_of.find(conn);
+    if (it != g->member_of.end()) return it->second;
+    return pin(g, conn, false);
 }
 
 // fold a member's flush / poll result into the group's: the first error wins, else the sum
@@ -73,6 +88,7 @@ int uvhttp_ws_amd_batcher_group_create(const uvhttp_ws_amd_batcher_config_t* cfg
             return rc;
         }
         g->members.push_back(b);
+        g->devices.push_back(devices[k]);
         g->live.push_back(0);
     }
     *out = g;
@@ -95,7 +111,8 @@ uvhttp_ws_amd_batcher_t* uvhttp_ws_amd_batcher_group_batcher(uvhttp_ws_amd_batch
 
 int uvhttp_ws_amd_batcher_group_member(uvhttp_ws_amd_batcher_group_t* g, struct uvhttp_ws_connection* conn) {
     if (!g || !conn) return -1;
-    return (int)member_for(g, conn);
+    auto it = g->member_of.find(conn);  // a query: never pins
+    return it == g->member_of.end() ? -1 : (int)it->second;
 }
 
 uvhttp_error_t uvhttp_ws_amd_batcher_group_submit_read(uvhttp_ws_amd_batcher_group_t* g,
@@ -108,7 +125,20 @@ uvhttp_error_t uvhttp_ws_amd_batcher_group_submit_read(uvhttp_ws_amd_batcher_gro
 int uvhttp_ws_amd_batcher_group_set_tls(uvhttp_ws_amd_batcher_group_t* g, struct uvhttp_ws_connection* conn,
                                         const void* tls_key, uint64_t read_seq) {
     if (!g || !conn) return UVHTTP_WS_GPU_EINVAL;
-    return uvhttp_ws_amd_batcher_set_tls(g->members[member_for(g, conn)], conn, tls_key, read_seq);
+    // TLS records open only on a device member (a host decoder has no AEAD): a new connection
+    // is pinned among the device members; one pinned to a host member moves when that member
+    // holds nothing of it yet (its reads so far were all delivered)
+    auto it = g->member_of.find(conn);
+    uint32_t m = it == g->member_of.end() ? kNone : it->second;
+    if (m != kNone && g->devices[m] < 0) {
+        if (uvhttp_ws_amd_batcher_holds_conn(g->members[m], conn)) return UVHTTP_WS_GPU_ENODEV;
+        g->live[m]--;
+        g->member_of.erase(it);
+        m = kNone;
+    }
+    if (m == kNone) m = pin(g, conn, true);
+    if (m == kNone) return UVHTTP_WS_GPU_ENODEV;
+    return uvhttp_ws_amd_batcher_set_tls(g->members[m], conn, tls_key, read_seq);
 }
 
 uvhttp_error_t uvhttp_ws_amd_batcher_group_submit_tls_read(uvhttp_ws_amd_batcher_group_t* g,

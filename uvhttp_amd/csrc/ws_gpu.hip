@@ -25,6 +25,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <vector>
+
 #include "uvhttp_ws_amd.h"
 
 namespace {
@@ -336,12 +338,15 @@ struct BatchArgs {
 constexpr uint32_t kStampRing = 128, kStampKinds = 16, kStampBegin = 256, kStampEnd = 4096;
 constexpr uint64_t kStampPer = kStampBegin + kStampEnd;
 constexpr uint64_t kStampLow = (1ull << 40) - 1;
+constexpr uint32_t kStampTagPeriod = (1u << 24) - 1;
 constexpr uint64_t kStampWords = (uint64_t)kStampRing * kStampKinds * kStampPer;
 // experiment builds (-DUVWS_PLAN_PHASES, tools/build_variant.sh): k_plan's per-block phase
 // times follow the ring, 8 words per block (uvhttp_ws_gpu_engine_debug_phases)
 constexpr uint64_t kPhaseWords = 8 * 8192;
 constexpr uint64_t kStampAlloc = kStampWords + kPhaseWords;
 
+// a stamp word's call tag: 1 .. 2^24 - 1, never 0 (0 marks an unused word), one more per call
+__host__ __device__ inline uint32_t stamp_tag(uint32_t epoch) { return epoch % kStampTagPeriod + 1u; }
 __device__ inline uint64_t* stamp_slot(uint64_t* st, uint32_t epoch, uint32_t kind) {
     return st + ((uint64_t)(epoch % kStampRing) * kStampKinds + kind) * kStampPer;
 }
@@ -368,7 +373,7 @@ struct StampScope {
     uint32_t epoch, kind;
     uint64_t t0;
     __device__ StampScope(uint64_t* st_, uint32_t epoch_, uint32_t kind_, bool at_start = true)
-        : st(st_), epoch(epoch_), kind(kind_), t0(at_start ? stamp_clock() : 0) {}
+        : st(st_), epoch(epoch_), kind(kind_), t0(at_start && st_ ? stamp_clock() : 0) {}
     // The start clock of a kernel whose uniform loads must stay scalar: read by an asm that is
     // not a memory access (so it clobbers nothing) and is pinned before the kernel's first
     // loads by passing the index they are computed from through it (v is returned unchanged).
@@ -399,7 +404,7 @@ struct StampScope {
         const bool sample = b < 1024 || (b < 65536 ? (b & 63) == 63 : (b & 1023) == 1023);
         if (!first && !sample) return;
         uint64_t* sl = stamp_slot(st, epoch, kind);
-        const uint64_t tag = (uint64_t)(epoch & 0xFFFFFFu) << 40;
+        const uint64_t tag = (uint64_t)stamp_tag(epoch) << 40;
         const uint64_t now = stamp_clock();
         if (first) sl[blockIdx.x] = tag | ((t0 ? t0 : now) & kStampLow);
         if (!sample) return;
@@ -4089,12 +4094,22 @@ int uvhttp_ws_gpu_engine_read_stamps(uvhttp_ws_gpu_engine_t* e, uvhttp_ws_gpu_st
         return set_err(e, UVHTTP_WS_GPU_ELAUNCH, "read stamps", h);
     }
     if (khz <= 0) khz = 100000;  // gfx9 wall clock: 100 MHz
+    // a call's age: how many calls ago it ran, from the latest call's tag (tags wrap after
+    // 2^24 - 1 calls, so neither "largest tag" nor the tag order is the call order)
+    const uint32_t cur = stamp_tag(e->epoch);
+    auto age = [&](uint64_t t) -> uint32_t {
+        return (uint32_t)((cur + (uint64_t)kStampTagPeriod - t) % kStampTagPeriod);
+    };
     uint32_t n = 0;
+    std::vector<uint32_t> ages;
     for (uint32_t r = 0; r < kStampRing; ++r) {
         for (uint32_t k = 0; k < kStampKinds; ++k) {
             const uint64_t* sl = host + ((uint64_t)r * kStampKinds + k) * kStampPer;
             uint64_t tag = 0;  // the newest call that stamped this slot
-            for (uint64_t j = 0; j < kStampPer; ++j) tag = (sl[j] >> 40) > tag ? (sl[j] >> 40) : tag;
+            for (uint64_t j = 0; j < kStampPer; ++j) {
+                const uint64_t t = sl[j] >> 40;
+                if (t && (!tag || age(t) < age(tag))) tag = t;
+            }
             if (!tag) continue;
             uint64_t b = ~0ull, en = 0;
             for (uint64_t j = 0; j < kStampPer; ++j) {
@@ -4109,22 +4124,25 @@ int uvhttp_ws_gpu_engine_read_stamps(uvhttp_ws_gpu_engine_t* e, uvhttp_ws_gpu_st
                 out[n].kernel = k;
                 out[n].begin_ns = b * 1000000ull / (uint64_t)khz;
                 out[n].end_ns = en * 1000000ull / (uint64_t)khz;
+                ages.push_back(age(tag));
             }
             ++n;
         }
     }
     free(host);
     if (n > cap) n = cap;
-    // call order (tags increase by one per call), then start order within a call
+    // call order (oldest first), then start order within a call
     for (uint32_t i = 1; i < n; ++i) {
         const uvhttp_ws_gpu_stamp_t x = out[i];
+        const uint32_t xa = ages[i];
         uint32_t j = i;
-        while (j > 0 && (out[j - 1].call > x.call ||
-                         (out[j - 1].call == x.call && out[j - 1].begin_ns > x.begin_ns))) {
+        while (j > 0 && (ages[j - 1] < xa || (ages[j - 1] == xa && out[j - 1].begin_ns > x.begin_ns))) {
             out[j] = out[j - 1];
+            ages[j] = ages[j - 1];
             --j;
         }
         out[j] = x;
+        ages[j] = xa;
     }
     *n_out = n;
     return UVHTTP_WS_GPU_OK;
