@@ -661,6 +661,9 @@ def main():
                     help="skip the device-timeline (kernel stamp) steps after the timed region")
     ap.add_argument("--graph", action="store_true",
                     help="replay each step as one captured HIP graph (diagnostic: no kernel timing)")
+    ap.add_argument("--oversubscribe", action="store_true",
+                    help="allow more ranks than GPUs: rank r uses device LOCAL_RANK %% visible "
+                         "(launcher readiness runs on a one-GPU box; the ranks share one HBM)")
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)  # launcher tests
     args = ap.parse_args()
 
@@ -669,8 +672,9 @@ def main():
         # environment / KFD topology and starts fresh rank processes
         if not args.stub:
             have = visible_gpus()
-            if have < args.gpus:
-                raise SystemExit(f"--gpus {args.gpus} but only {have} GPU(s) visible")
+            if have < args.gpus and not args.oversubscribe:
+                raise SystemExit(f"--gpus {args.gpus} but only {have} GPU(s) visible "
+                                 "(--oversubscribe maps several ranks to one device)")
         raise SystemExit(spawn_ranks(args.gpus))
 
     rank = int(os.environ.get("RANK", "0"))
@@ -685,7 +689,11 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
-    wl = (StubWorkload if args.stub else GpuWorkload)(args, cfg, rank, world, local)
+    device = local
+    if args.oversubscribe and not args.stub:
+        import torch
+        device = local % max(1, torch.cuda.device_count())  # counts devices, no HIP context
+    wl = (StubWorkload if args.stub else GpuWorkload)(args, cfg, rank, world, device)
     wl.no_stamps = args.no_stamps
     el_max, k_ms, k_n = timed_run(wl, args.steps, args.warmup, world)
     n, plen, passes, stride = wl.n, wl.plen, wl.passes, wl.stride
@@ -708,6 +716,17 @@ def main():
     tl = None
     if rank == 0 and not args.stub and not args.no_stamps:
         tl = wl.timeline()
+    # every rank ran check() before and after its timed steps (a failing rank exits non-zero);
+    # count the ranks that got here, and the devices they ran on
+    ranks_checked, devices = world, [device]
+    if world > 1:
+        import torch
+        t = torch.tensor([1.0])
+        dist.all_reduce(t)
+        ranks_checked = int(t.item())
+        got = [None] * world
+        dist.all_gather_object(got, device)
+        devices = got
     wl.close()
     # the dominant kernel's duration: the device stamps' payload-kernel median when stamped
     # (no timing event beside the kernel), else the sampled HIP events; a kernel of the step
@@ -801,6 +820,14 @@ def main():
                 "resident 1048576-frame chunk (generated once; alternate passes re-mask it): the "
                 "bytes moved per pass are the chunk's, the frames past the first chunk are not "
                 "materialised")
+        if world > 1:
+            out["ranks_checked"] = ranks_checked
+            out["rank_devices"] = devices
+        if args.oversubscribe:
+            out["oversubscribed"] = len(set(devices)) < world
+            out["config"]["oversubscribe_note"] = (
+                "launcher readiness: ranks share devices (LOCAL_RANK % visible), so they share "
+                "one HBM — not a scaling measurement")
         if args.stub:
             out["stub"] = True
         if "UVHTTP_WS_SPAWNED_FROM_GPU_PROCESS" in os.environ:

@@ -84,6 +84,8 @@ def test_bench_self_spawns_ranks(world):
     # the shard each rank timed: 8 388 608 / world frames in resident passes
     assert out["config"]["frames_per_gpu"] == 8388608 // world
     assert out["steps"] == 3 and out["ms_per_step"] > 0
+    # every rank got past its post-run check, each on its own device
+    assert out["ranks_checked"] == world and out["rank_devices"] == list(range(world))
     # the parent spawned its ranks without importing torch / touching HIP
     assert out["spawned_from_gpu_process"] is False
 
