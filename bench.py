@@ -342,6 +342,7 @@ class GpuWorkload:
         first, n, passes = shard_plan(cfg, rank, world)
         self.plen, self.n, self.passes, self.mode, self.mm = plen, n, passes, mode, mm
         self.use_graph = bool(getattr(args, "graph", False))
+        self.no_desc = bool(getattr(args, "no_desc", False)) and mode in ("inplace", "compact")
         self.stride = stride = U.gen_frame_stride(plen)
         self.wire_len = wire_len = stride * n
         self.eng = eng = U.GpuEngine(local)
@@ -376,6 +377,11 @@ class GpuWorkload:
         fused_max = int(os.environ.get("UVHTTP_WS_FUSED_MAX", "2560") or 2560)
         if mode == "inplace" and os.environ.get("UVHTTP_WS_FUSED", "1") != "0" and 64 <= stride <= fused_max:
             self.kernel = "k_unmask_stride"
+            # summary-only: the one-pass decode (its summary tail after it) when the message
+            # limit cannot bind (ws_gpu.hip run_decode)
+            if self.no_desc and stride >= 140 and os.environ.get("UVHTTP_WS_SUMMARY_FAST", "1") != "0" \
+                    and (mm == 0 or n * (stride - 8) <= mm):
+                self.kernel = "k_unmask_stride (summary-only one-pass decode)"
         # compact, the same stride range: the speculative pass (k_unmask_stride writing the
         # arena, ws_gpu.hip run_decode) unless UVHTTP_WS_SPEC=0
         spec_max = int(os.environ.get("UVHTTP_WS_SPEC_MAX", "2560") or 2560)
@@ -426,11 +432,12 @@ class GpuWorkload:
         elif self.arena is None:
             eng.decode_inplace(self.wire, self.n, stride=self.stride, max_message_size=self.mm,
                                wire_len=self.wire_len, desc=self.desc, summary=self.summ,
-                               stream=stream)
+                               stream=stream, no_desc=self.no_desc)
         else:
             eng.decode_compact(self.wire, self.n, self.arena, stride=self.stride,
                                max_message_size=self.mm, wire_len=self.wire_len, desc=self.desc,
-                               msgs=self.msgs, summary=self.summ, stream=stream)
+                               msgs=self.msgs, summary=self.summ, stream=stream,
+                               no_desc=self.no_desc)
 
     def step(self):
         if self.graph is not None:
@@ -661,6 +668,10 @@ def main():
                     help="skip the device-timeline (kernel stamp) steps after the timed region")
     ap.add_argument("--graph", action="store_true",
                     help="replay each step as one captured HIP graph (diagnostic: no kernel timing)")
+    ap.add_argument("--no-desc", action="store_true",
+                    help="inplace / compact: d_desc = NULL (summary-only decode: no per-frame "
+                         "descriptors; fixed-stride batches of >= 140 B frames in place take the "
+                         "one-pass decode)")
     ap.add_argument("--oversubscribe", action="store_true",
                     help="allow more ranks than GPUs: rank r uses device LOCAL_RANK %% visible "
                          "(launcher readiness runs on a one-GPU box; the ranks share one HBM)")
@@ -783,7 +794,7 @@ def main():
             "data": "synthetic (splitmix64 payload + per-frame keys, generated on device)",
             "config": {
                 "workload": WORKLOAD[cfg],
-                "mode": args.mode,
+                "mode": args.mode + ("_summary_only" if getattr(wl, "no_desc", False) else ""),
                 "frames_per_gpu": n * passes,
                 "decode_passes_per_step": passes,
                 "payload_bytes_per_frame": plen,
@@ -881,12 +892,18 @@ def e2e_live(local, conns=1024, frames=4, size=65536, flushes=20):
     # for half as long, and copies overlap better: 40 GiB/s with p99 blocked < 1 ms where whole-
     # round queues gave 23-40 GiB/s and p99 3.6-8 ms (profiles/r04_bench_e2e.json);
     # device_async_round keeps the whole-round queues for comparison
-    for name, dev, asy, cap in (("device", local, 0, 1.0), ("device_async", local, 1, 0.5),
-                                ("device_async_round", local, 1, 1.0), ("host_1core", -1, 0, 1.0)):
+    # read models (tests/c/batcher_e2e.c --reads): "submit" — the bytes are already in a buffer
+    # and submit_read copies them into the pinned arena; "kcopy" — the socket read is modelled as
+    # a copy into a 16 KiB libuv buffer, then submit_read (the reference's shape: two copies on
+    # the loop thread); "zc" — alloc_read / commit_read, the socket read lands in the arena (one)
+    for name, dev, asy, cap, reads in (
+            ("device", local, 0, 1.0, "submit"), ("device_async", local, 1, 0.5, "submit"),
+            ("device_async_kcopy", local, 1, 0.5, "kcopy"), ("device_async_zc", local, 1, 0.5, "zc"),
+            ("device_async_round", local, 1, 1.0, "submit"), ("host_1core", -1, 0, 1.0, "submit")):
         p = subprocess.run([exe, "--conns", str(conns), "--frames", str(frames), "--size",
                             str(size), "--flushes", str(flushes if dev >= 0 else 3),
                             "--device", str(dev), "--async", str(asy), "--cap", str(cap),
-                            "--pin", "1" if dev >= 0 else "0"],
+                            "--pin", "1" if dev >= 0 else "0", "--reads", reads],
                            capture_output=True, text=True, timeout=600)
         out[name] = json.loads(p.stdout.strip().splitlines()[-1]) if p.returncode == 0 else \
             {"error": p.returncode, "stderr": p.stderr[-300:]}

@@ -649,6 +649,7 @@ typedef struct {
     double max_blocked_wait_ms;           /* the longest call's split: waiting for the device */
     double max_blocked_stage_ms;          /*   staging + enqueueing */
     double max_blocked_deliver_ms;        /*   delivering (callbacks included) */
+    uint64_t zero_copy_reads;             /* reads queued through alloc_read / commit_read */
 } uvhttp_ws_amd_batcher_stats_t;
 void uvhttp_ws_amd_batcher_config_init(uvhttp_ws_amd_batcher_config_t* cfg);
 /* UVHTTP_WS_GPU_ENODEV if cfg->device >= 0 names no usable MI355X (no silent host mode) */
@@ -664,6 +665,22 @@ void uvhttp_ws_amd_batcher_free(uvhttp_ws_amd_batcher_t* b);
 uvhttp_error_t uvhttp_ws_amd_batcher_submit_read(uvhttp_ws_amd_batcher_t* b,
                                                  struct uvhttp_ws_connection* conn,
                                                  const uint8_t* data, size_t len);
+/* Zero-copy reads: the loop's uv_alloc_cb / uv_read_cb pair (src/uvhttp_connection.c:128-158,
+ * 1098-1175).  alloc_read returns space for conn's next read inside the queue's own (pinned)
+ * staging arena — *buf, *len bytes, len <= suggested (less when the read would not fit a whole
+ * flush); libuv reads the socket straight into it; commit_read then queues the nread bytes
+ * exactly as submit_read(conn, buf, nread) would, without copying them.  nread = 0 (EAGAIN, EOF,
+ * an error) gives the space back.  One allocation is outstanding at a time: libuv calls the
+ * read callback right after the alloc callback for the same stream; any other batcher call in
+ * between (a flush may hand the queue over) makes commit_read refuse with
+ * UVHTTP_ERROR_INVALID_PARAM, as does a commit for another connection or nread > *len.
+ * alloc_read may hand a full queue over first, like submit_read.  TLS connections: the space
+ * takes ciphertext (as submit_tls_read). */
+uvhttp_error_t uvhttp_ws_amd_batcher_alloc_read(uvhttp_ws_amd_batcher_t* b,
+                                                struct uvhttp_ws_connection* conn, size_t suggested,
+                                                uint8_t** buf, size_t* len);
+uvhttp_error_t uvhttp_ws_amd_batcher_commit_read(uvhttp_ws_amd_batcher_t* b,
+                                                 struct uvhttp_ws_connection* conn, size_t nread);
 /* Hand everything queued to the decoder and return (see "Asynchronous flushes").  Never waits
  * for the device: when a queue is still in flight the request is remembered and poll() starts
  * this queue right after delivering that one (until then reads keep joining it; a read that
@@ -746,6 +763,12 @@ uvhttp_error_t uvhttp_ws_amd_batcher_group_submit_read(uvhttp_ws_amd_batcher_gro
  * of it (reads queued, a failure mark); otherwise, or with no device member, UVHTTP_WS_GPU_ENODEV */
 int uvhttp_ws_amd_batcher_group_set_tls(uvhttp_ws_amd_batcher_group_t* g, struct uvhttp_ws_connection* conn,
                                         const void* tls_key, uint64_t read_seq);
+/* zero-copy reads through the connection's member (pinned on its first alloc_read) */
+uvhttp_error_t uvhttp_ws_amd_batcher_group_alloc_read(uvhttp_ws_amd_batcher_group_t* g,
+                                                      struct uvhttp_ws_connection* conn, size_t suggested,
+                                                      uint8_t** buf, size_t* len);
+uvhttp_error_t uvhttp_ws_amd_batcher_group_commit_read(uvhttp_ws_amd_batcher_group_t* g,
+                                                       struct uvhttp_ws_connection* conn, size_t nread);
 uvhttp_error_t uvhttp_ws_amd_batcher_group_submit_tls_read(uvhttp_ws_amd_batcher_group_t* g,
                                                            struct uvhttp_ws_connection* conn,
                                                            const uint8_t* ciphertext, size_t len);

@@ -14,7 +14,14 @@
  * delivers that flush and starts the one flush_async asked for meanwhile.
  *
  *   batcher_e2e --conns N --frames M --size S --read R --flushes F --device D [--async 1]
- *               [--pin 1: loop thread on the GPU's NUMA node] [--trace 1]
+ *               [--pin 1: loop thread on the GPU's NUMA node] [--trace 1] [--reads MODEL]
+ *
+ * --reads: how a socket read reaches the batcher.  "submit" (default): the bytes are already in
+ * libuv's buffer (the stream itself) and submit_read copies them into the staging arena — the
+ * socket's own copy is not modelled.  "kcopy": the socket read is modelled as a memcpy into a
+ * 16 KiB libuv buffer, then submit_read copies again (the reference shape, src/uvhttp_connection.c:
+ * 128-158 + 1163).  "zc": alloc_read hands out arena space, the socket read (memcpy) lands there,
+ * commit_read queues it — one copy, the socket's own.
  */
 #define _GNU_SOURCE
 #include <sched.h>
@@ -69,6 +76,7 @@ static double now_s(void) {
 
 int main(int argc, char** argv) {
     int conns = 1024, frames = 4, flushes = 20, device = 0, async = 0, pin = 0;
+    const char* reads_model = "submit";
     double cap_rounds = 1.0;
     size_t size = 65536, rd = 16384;
     for (int i = 1; i + 1 < argc; i += 2) {
@@ -82,6 +90,7 @@ int main(int argc, char** argv) {
         else if (!strcmp(argv[i], "--trace")) g_trace = atoi(argv[i + 1]);
         else if (!strcmp(argv[i], "--pin")) pin = atoi(argv[i + 1]);
         else if (!strcmp(argv[i], "--cap")) cap_rounds = atof(argv[i + 1]);
+        else if (!strcmp(argv[i], "--reads")) reads_model = argv[i + 1];
     }
     /* one connection's stream: M masked BINARY frames of S bytes (every connection sends
      * the same bytes; keys differ per frame) */
@@ -147,6 +156,8 @@ int main(int argc, char** argv) {
         }
         if (f) fclose(f);
     }
+    const int zc = !strcmp(reads_model, "zc"), kcopy = !strcmp(reads_model, "kcopy");
+    uint8_t* rbuf = (uint8_t*)malloc(rd);  /* kcopy: libuv's read buffer */
     double t0 = 0, t_submit = 0, t_flush = 0;
     uvhttp_ws_amd_batcher_stats_t st0;
     memset(&st0, 0, sizeof(st0));
@@ -165,8 +176,25 @@ int main(int argc, char** argv) {
         uvhttp_ws_amd_batcher_stats(b, &sx);
         trace('S', it, (int)sx.async_flushes);
         for (int c = 0; c < conns; ++c) {
-            for (size_t o = 0; o < slen; o += rd)
-                if (uvhttp_ws_amd_batcher_submit_read(b, cs[c], stream + o, o + rd <= slen ? rd : slen - o)) return 2;
+            for (size_t o = 0; o < slen; o += rd) {
+                const size_t len = o + rd <= slen ? rd : slen - o;
+                if (zc) {  /* uv_alloc_cb -> the socket read into the arena -> uv_read_cb */
+                    for (size_t got = 0; got < len;) {
+                        uint8_t* buf = NULL;
+                        size_t cap = 0;
+                        if (uvhttp_ws_amd_batcher_alloc_read(b, cs[c], len - got, &buf, &cap)) return 2;
+                        const size_t k = cap < len - got ? cap : len - got;
+                        memcpy(buf, stream + o + got, k);
+                        if (uvhttp_ws_amd_batcher_commit_read(b, cs[c], k)) return 2;
+                        got += k;
+                    }
+                } else if (kcopy) {
+                    memcpy(rbuf, stream + o, len);
+                    if (uvhttp_ws_amd_batcher_submit_read(b, cs[c], rbuf, len)) return 2;
+                } else if (uvhttp_ws_amd_batcher_submit_read(b, cs[c], stream + o, len)) {
+                    return 2;
+                }
+            }
             /* the loop's uv_async handle: a finished flush is delivered between reads */
             if (async && atomic_load_explicit(&g_ready, memory_order_relaxed)) {
                 atomic_store(&g_ready, 0);
@@ -200,7 +228,7 @@ int main(int argc, char** argv) {
     uvhttp_ws_amd_batcher_stats_t st;
     uvhttp_ws_amd_batcher_stats(b, &st);
     const double payload = (double)size * frames * conns * flushes;
-    printf("{\"path\": \"%s\", \"value\": %.3f, \"unit\": \"GiB/s\", \"conns\": %d, "
+    printf("{\"path\": \"%s\", \"reads\": \"%s\", \"zero_copy_reads\": %llu, \"value\": %.3f, \"unit\": \"GiB/s\", \"conns\": %d, "
            "\"frames_per_conn\": %d, \"payload\": %zu, \"read\": %zu, \"flushes\": %d, "
            "\"ms_per_flush\": %.3f, \"messages_ok\": %d, \"device_flushes\": %llu, "
            "\"device_ms_total\": %.1f, \"async\": %d, \"submit_ms_per_flush\": %.3f, "
@@ -213,7 +241,7 @@ int main(int argc, char** argv) {
            "\"stage\": %.3f, \"wait\": %.3f, \"deliver\": %.3f}}\n",
            device >= 0 ? "device batcher (stage, H2D, decode_reads, D2H, deliver)"
                        : "host decoder (process_data per read, 1 core)",
-           payload / el / (1024.0 * 1024 * 1024), conns, frames, size, rd, flushes,
+           reads_model, (unsigned long long)(st.zero_copy_reads - st0.zero_copy_reads), payload / el / (1024.0 * 1024 * 1024), conns, frames, size, rd, flushes,
            el * 1e3 / flushes, g_msgs == (uint64_t)conns * frames * flushes,
            (unsigned long long)(st.device_flushes - st0.device_flushes), st.device_ms - st0.device_ms,
            async, t_submit * 1e3 / flushes, t_flush * 1e3 / flushes,
@@ -240,5 +268,6 @@ int main(int argc, char** argv) {
     for (int c = 0; c < conns; ++c) uvhttp_ws_connection_free(cs[c]);
     free(cs);
     free(stream);
+    free(rbuf);
     return 0;
 }

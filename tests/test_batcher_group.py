@@ -45,9 +45,10 @@ def _drive(b, rng, pairs, forget_some=False):
     assert not b.in_flight()
 
 
+@pytest.mark.parametrize("zc", [False, True], ids=["submit", "zero_copy"])
 @pytest.mark.parametrize("devices", GROUPS)
 @pytest.mark.parametrize("seed", [1, 2, 3])
-def test_group_matches_process_data(devices, seed):
+def test_group_matches_process_data(devices, seed, zc):
     _need(devices)
     import uvhttp_amd as U
     import _oracle
@@ -55,7 +56,7 @@ def test_group_matches_process_data(devices, seed):
     b = U.BatcherGroup(devices, min_device_bytes=0, max_bytes=[64 << 10, 1 << 20, 8 << 20][seed - 1],
                        max_connections=64, max_reads=4000)
     assert b.size() == len(devices)
-    pairs = [Pair(U, rng, reads=_conn_reads(rng, big=70000 if seed == 1 else 0)) for _ in range(45)]
+    pairs = [Pair(U, rng, reads=_conn_reads(rng, big=70000 if seed == 1 else 0), zc=zc) for _ in range(45)]
     _drive(b, rng, pairs, forget_some=seed == 3)
     L = _oracle.load()
     for p in pairs:

@@ -48,7 +48,7 @@ def _conn_reads(rng, big=0):
 class Pair:
     """A product connection and its oracle twin fed the same reads."""
 
-    def __init__(self, U, rng, mf=None, mm=None, reads=None):
+    def __init__(self, U, rng, mf=None, mm=None, reads=None, zc=False):
         mf = mf or rng.choice([16 * 1024 * 1024, 65536, 4000])
         mm = mm if mm is not None else rng.choice([64 * 1024 * 1024, 9000, 0])
         self.prod = U.WsConnection(1, mf, mm, user_data=False)
@@ -58,6 +58,7 @@ class Pair:
         self.orc_failed = False
         self.submit_failed = False
         self.dead = False  # forgotten and freed
+        self.zc = zc  # reads through alloc_read / commit_read (the libuv alloc + read shape)
 
     @property
     def key(self):
@@ -66,6 +67,19 @@ class Pair:
     def feed(self, b, data):
         """one read: to the batcher and (until it fails) to the oracle"""
         if self.orc_failed or self.submit_failed or self.dead:
+            return
+        if self.zc:
+            # the socket read lands in the staging arena; a short allocation splits it into
+            # several reads, which the oracle gets as the same process_data calls
+            rc, pieces = b.submit_zero_copy(self.prod, data)
+            pos = 0
+            for k in pieces:
+                if self.orc.process_data(data[pos:pos + k]) != 0:
+                    self.orc_failed = True
+                    break
+                pos += k
+            if rc != 0:
+                self.submit_failed = True
             return
         rc = b.submit(self.prod, data)
         # (a read larger than a flush is decoded inside submit_read: its rc is process_data's)
@@ -117,20 +131,23 @@ def _drive(U, b, rng, pairs):
     assert not b.in_flight()
 
 
+@pytest.mark.parametrize("zc", [False, True], ids=["submit", "zero_copy"])
 @pytest.mark.parametrize("device", DEVICES)
 @pytest.mark.parametrize("seed", [1, 2])
-def test_overflow_and_oversize_reads(device, seed):
-    """tiny queue limits: flushes start inside submit_read; 70 000-byte reads exceed a whole
-    flush (max_bytes 48 KiB) and are decoded directly, after the connection's queued reads"""
+def test_overflow_and_oversize_reads(device, seed, zc):
+    """tiny queue limits: flushes start inside submit_read (alloc_read); 70 000-byte reads
+    exceed a whole flush (max_bytes 48 KiB) and are decoded directly, after the connection's
+    queued reads — or, zero-copy, land in pieces of what one flush holds"""
     _need_device(device)
     import uvhttp_amd as U
     rng = random.Random(seed)
     b = U.Batcher(device=device, min_device_bytes=0, max_bytes=48 * 1024,
                   max_connections=6, max_reads=40)
-    pairs = [Pair(U, rng, reads=_conn_reads(rng, big=70000)) for _ in range(24)]
+    pairs = [Pair(U, rng, reads=_conn_reads(rng, big=70000), zc=zc) for _ in range(24)]
     _drive(U, b, rng, pairs)
     st = b.stats()
-    assert st["direct_reads"] > 0 and st["flushes"] > 10
+    assert st["flushes"] > 10
+    assert st["zero_copy_reads"] > 0 if zc else st["direct_reads"] > 0
     if device >= 0:
         assert st["device_flushes"] > 0 and st["async_flushes"] > 0
     L = _oracle.load()
@@ -139,8 +156,9 @@ def test_overflow_and_oversize_reads(device, seed):
     b.close()
 
 
+@pytest.mark.parametrize("zc", [False, True], ids=["submit", "zero_copy"])
 @pytest.mark.parametrize("device", DEVICES)
-def test_submit_and_forget_from_callbacks(device):
+def test_submit_and_forget_from_callbacks(device, zc):
     """on_message of the 'driver' connections submits a read for a 'chained' connection (it
     lands in the queue being filled, never the one being delivered) and forgets a 'victim'
     connection mid-stream, re-creating a fresh connection that then gets reads of its own"""
@@ -150,12 +168,12 @@ def test_submit_and_forget_from_callbacks(device):
     b = U.Batcher(device=device, min_device_bytes=0)
     key = b"\x11\x22\x33\x44"
     # chained connections: their whole stream is submitted from callbacks, one read per event
-    chained = [Pair(U, rng, mf=16 << 20, mm=64 << 20,
+    chained = [Pair(U, rng, mf=16 << 20, mm=64 << 20, zc=zc,
                     reads=_conn_reads(rng)) for _ in range(6)]
-    victims = [Pair(U, rng, mf=16 << 20, mm=64 << 20,
+    victims = [Pair(U, rng, mf=16 << 20, mm=64 << 20, zc=zc,
                     reads=[_frame(2, 1, rng.randbytes(100), key, True, 0)] * 40) for _ in range(4)]
     fresh = []
-    drivers = [Pair(U, rng, mf=16 << 20, mm=64 << 20,
+    drivers = [Pair(U, rng, mf=16 << 20, mm=64 << 20, zc=zc,
                     reads=[_frame(1, 1, b"tick %d" % i, key, True, 0) for i in range(60)])
                for _ in range(3)]
 
@@ -169,7 +187,7 @@ def test_submit_and_forget_from_callbacks(device):
             b.forget(v.prod)
             v.dead = True
             v.prod.close()  # a new connection may now get the same address
-            n = Pair(U, rng, mf=16 << 20, mm=64 << 20, reads=_conn_reads(rng))
+            n = Pair(U, rng, mf=16 << 20, mm=64 << 20, reads=_conn_reads(rng), zc=zc)
             fresh.append(n)
             n.feed(b, n.reads[0])
             n.next = 1

@@ -329,9 +329,10 @@ def test_device_apply_mask(torch, eng, off):
         assert bytes(d[: n + off].cpu().numpy().tobytes()) == bytes(exp)
 
 
-def _full_config(torch, eng, n, plen, fragmented, compact, chunk=4096):
+def _full_config(torch, eng, n, plen, fragmented, compact, chunk=4096, no_desc=False):
     """Full-size BASELINE config: device-generated, device-decoded, every frame checked
-    against the oracle's decode of the identical oracle-generated frames."""
+    against the oracle's decode of the identical oracle-generated frames (no_desc: the
+    summary-only decode, d_desc = NULL)."""
     import uvhttp_amd as U
     stride = U.gen_frame_stride(plen)
     wl = stride * n
@@ -343,14 +344,16 @@ def _full_config(torch, eng, n, plen, fragmented, compact, chunk=4096):
         desc, msgs, summ = eng.decode_compact(d, n, arena, stride=stride, max_message_size=mm,
                                               wire_len=wl)
     else:
-        desc, summ = eng.decode_inplace(d, n, stride=stride, max_message_size=mm, wire_len=wl)
+        desc, summ = eng.decode_inplace(d, n, stride=stride, max_message_size=mm, wire_len=wl,
+                                        no_desc=no_desc)
     torch.cuda.synchronize()
     s = eng.read_summary(summ)
     assert s["n_delivered"] == n and s["status"] == 0
-    assert s["payload_bytes"] == n * plen
-    assert s["n_messages"] == (1 if fragmented else n)
-    st = eng.read_desc(desc, n)["status"]
-    assert not st.any()
+    assert s["payload_bytes"] == n * plen and s["consumed_bytes"] == wl
+    assert s["n_messages"] == (1 if fragmented else n) and s["pending_bytes"] == 0
+    if not no_desc:
+        st = eng.read_desc(desc, n)["status"]
+        assert not st.any()
     hs = stride - 4 - plen
     for first in range(0, n, chunk):
         cnt = min(chunk, n - first)
@@ -386,6 +389,16 @@ def test_config_c4_full(torch, eng, compact):
     _full_config(torch, eng, 1048576, 256, True, compact, chunk=131072)
 
 
+@pytest.mark.parametrize("cfg", ["c2", "c4"])
+def test_config_full_summary_only(torch, eng, cfg):
+    """d_desc = NULL at full size: C4 takes the one-pass summary-only decode, C2 (4 KiB frames,
+    above the fused range) the descriptor path with the engine's scratch"""
+    if cfg == "c4":
+        _full_config(torch, eng, 1048576, 256, True, False, chunk=131072, no_desc=True)
+    else:
+        _full_config(torch, eng, 65536, 4096, False, False, no_desc=True)
+
+
 def test_config_c4_default_limit_rejects(torch, eng):
     """With the default 64 MiB max_message_size the reference rejects C4 at frame 262 144
     (SURVEY §0); the device path reports the same frame and reason."""
@@ -400,6 +413,17 @@ def test_config_c4_default_limit_rejects(torch, eng):
     s = eng.read_summary(summ)
     assert s["n_delivered"] == 262144 and s["first_status"] == -8 and s["status"] == -1
     assert s["pending_bytes"] == 262144 * 256
+    # summary-only (the limit can bind, so not the one-pass decode): the same summary, and the
+    # wire as before (the second decode delivers nothing new: it re-masks nothing it did not
+    # unmask, so run it on a fresh copy)
+    d2 = torch.empty(stride * n + 64, dtype=torch.uint8, device="cuda")
+    eng.gen_frames(d2, n, plen, SEED, opcode0=2, fragmented=True)
+    _, summ2 = eng.decode_inplace(d2, n, stride=stride, max_message_size=MM, wire_len=stride * n,
+                                  no_desc=True)
+    torch.cuda.synchronize()
+    assert eng.read_summary(summ2) == s
+    assert torch.equal(d2[: stride * n], d[: stride * n])
+    del d2
     # frames before the rejected one unmasked, it and every later frame left masked
     for i in (0, 262143, 262144, 262145, n - 1):
         got = d[i * stride:(i + 1) * stride].cpu().numpy()

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Interleaved A/B of two builds of libuvhttp_ws_amd.so in ONE process on one device.
 
-  python tools/ab_lib.py LIB_A LIB_B cfg:mode [cfg:mode ...]     (mode: inplace | compact)
+  python tools/ab_lib.py LIB_A LIB_B cfg:mode [cfg:mode ...]     (mode: inplace | inplace_nd | compact)
 
 LIB_B may be "tree" for the in-tree build.  AB_STAMPS=1 turns engine B's device stamps on;
 AB_ENV_B="K=V,..." sets environment switches for engine B only.  Each round runs K decode steps with engine A,
@@ -60,9 +60,9 @@ def main():
         def run(k):
             e = engs[k]
             desc, summ, arena, msgs = outs[k]
-            if mode == "inplace":
+            if mode in ("inplace", "inplace_nd"):
                 e.decode_inplace(wire, n, stride=stride, max_message_size=mm, wire_len=wl,
-                                 desc=desc, summary=summ, stream=st)
+                                 desc=desc, summary=summ, stream=st, no_desc=mode == "inplace_nd")
             else:
                 e.decode_compact(wire, n, arena, stride=stride, max_message_size=mm,
                                  wire_len=wl, desc=desc, msgs=msgs, summary=summ, stream=st)

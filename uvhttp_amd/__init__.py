@@ -194,7 +194,8 @@ class BatcherStats(C.Structure):
         [(k, C.c_uint64) for k in ("tls_records", "tls_bytes", "tls_handbacks", "desc_refetches",
                                    "blocked_calls")] + \
         [(k, C.c_double) for k in ("blocked_p50_ms", "blocked_p99_ms", "max_blocked_wait_ms",
-                                   "max_blocked_stage_ms", "max_blocked_deliver_ms")]
+                                   "max_blocked_stage_ms", "max_blocked_deliver_ms")] + \
+        [("zero_copy_reads", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -287,6 +288,13 @@ def load_library(path: str) -> C.CDLL:
         "uvhttp_ws_amd_batcher_free": (None, [vp]),
         "uvhttp_ws_amd_batcher_submit_read": (C.c_int, [vp, C.POINTER(WsConnectionStruct), vp,
                                                         C.c_size_t]),
+        "uvhttp_ws_amd_batcher_alloc_read": (C.c_int, [vp, C.POINTER(WsConnectionStruct), C.c_size_t,
+                                                       C.POINTER(vp), C.POINTER(C.c_size_t)]),
+        "uvhttp_ws_amd_batcher_commit_read": (C.c_int, [vp, C.POINTER(WsConnectionStruct), C.c_size_t]),
+        "uvhttp_ws_amd_batcher_group_alloc_read": (C.c_int, [vp, C.POINTER(WsConnectionStruct), C.c_size_t,
+                                                             C.POINTER(vp), C.POINTER(C.c_size_t)]),
+        "uvhttp_ws_amd_batcher_group_commit_read": (C.c_int, [vp, C.POINTER(WsConnectionStruct),
+                                                              C.c_size_t]),
         "uvhttp_ws_amd_batcher_flush": (C.c_int, [vp]),
         "uvhttp_ws_amd_batcher_flush_async": (C.c_int, [vp]),
         "uvhttp_ws_amd_batcher_poll": (C.c_int, [vp]),
@@ -529,23 +537,34 @@ class GpuEngine:
 
     def decode_inplace(self, wire, n_frames, stride=None, offsets=None,
                        max_frame_size=16 * 1024 * 1024, max_message_size=64 * 1024 * 1024,
-                       is_server=1, wire_len=None, desc=None, summary=None, stream=None):
-        if desc is None or summary is None:
-            desc, summary = self.alloc_outputs(n_frames)
+                       is_server=1, wire_len=None, desc=None, summary=None, stream=None,
+                       no_desc=False):
+        """no_desc=True: d_desc = NULL, a summary-only decode (include/uvhttp_ws_amd.h);
+        returns (None, summary)"""
+        if summary is None or (desc is None and not no_desc):
+            d0, s0 = self.alloc_outputs(n_frames)
+            desc = d0 if desc is None else desc
+            summary = s0 if summary is None else summary
+        if no_desc:
+            desc = None
         b = self._batch(wire, n_frames, stride, offsets, max_frame_size, max_message_size,
                         is_server, wire_len)
         self._check(self._L.uvhttp_ws_gpu_decode_inplace(
-            self.h, C.byref(b), C.c_void_p(desc.data_ptr()), C.c_void_p(summary.data_ptr()),
-            self._stream(stream)), "decode_inplace")
+            self.h, C.byref(b), C.c_void_p(desc.data_ptr() if desc is not None else None),
+            C.c_void_p(summary.data_ptr()), self._stream(stream)), "decode_inplace")
         return desc, summary
 
     def decode_compact(self, wire, n_frames, arena, stride=None, offsets=None,
                        max_frame_size=16 * 1024 * 1024, max_message_size=64 * 1024 * 1024,
                        is_server=1, wire_len=None, desc=None, msgs=None, summary=None,
-                       stream=None):
+                       stream=None, no_desc=False):
         t = self.torch
-        if desc is None or summary is None:
-            desc, summary = self.alloc_outputs(n_frames)
+        if summary is None or (desc is None and not no_desc):
+            d0, s0 = self.alloc_outputs(n_frames)
+            desc = d0 if desc is None else desc
+            summary = s0 if summary is None else summary
+        if no_desc:
+            desc = None
         if msgs is None:
             msgs = t.empty(max(1, n_frames) * self.MSG_BYTES, dtype=t.uint8,
                            device=f"cuda:{self.device}")
@@ -553,7 +572,7 @@ class GpuEngine:
                         is_server, wire_len)
         self._check(self._L.uvhttp_ws_gpu_decode_compact(
             self.h, C.byref(b), C.c_void_p(arena.data_ptr()), arena.numel(),
-            C.c_void_p(desc.data_ptr()), C.c_void_p(msgs.data_ptr()),
+            C.c_void_p(desc.data_ptr() if desc is not None else None), C.c_void_p(msgs.data_ptr()),
             C.c_void_p(summary.data_ptr()), self._stream(stream)), "decode_compact")
         return desc, msgs, summary
 
@@ -837,6 +856,38 @@ class Batcher:
         buf = (C.c_uint8 * max(1, len(data))).from_buffer_copy(bytes(data) or b"\0")
         return self._L.uvhttp_ws_amd_batcher_submit_read(self.h, conn.ptr, buf, len(data))
 
+    _ZC = "uvhttp_ws_amd_batcher_"
+
+    def alloc(self, conn: "WsConnection", suggested: int):
+        """uvhttp_ws_amd_batcher_alloc_read -> (rc, address, length): space in the staging arena
+        for conn's next read"""
+        buf, n = C.c_void_p(), C.c_size_t()
+        rc = getattr(self._L, self._ZC + "alloc_read")(self.h, conn.ptr, suggested, C.byref(buf),
+                                                       C.byref(n))
+        return rc, buf.value, n.value
+
+    def commit(self, conn: "WsConnection", nread: int) -> int:
+        return getattr(self._L, self._ZC + "commit_read")(self.h, conn.ptr, nread)
+
+    def submit_zero_copy(self, conn: "WsConnection", data: bytes):
+        """the libuv shape of one socket read of `data`: alloc_read, the read into the returned
+        space (a memmove here), commit_read — in pieces when the space is shorter, as a socket
+        would deliver them.  -> (rc, [lengths of the pieces committed]); a failing commit's piece
+        is listed (a read no flush can hold is decoded at commit: rc is process_data's)"""
+        pos, pieces = 0, []
+        while pos < len(data):
+            rc, addr, n = self.alloc(conn, len(data) - pos)
+            if rc != 0:
+                return rc, pieces
+            k = min(n, len(data) - pos)
+            C.memmove(addr, data[pos:pos + k], k)
+            rc = self.commit(conn, k)
+            pieces.append(k)  # (consumed even when commit fails: a direct decode's rc)
+            if rc != 0:
+                return rc, pieces
+            pos += k
+        return 0, pieces
+
     def flush(self) -> int:
         return self._L.uvhttp_ws_amd_batcher_flush(self.h)
 
@@ -878,6 +929,7 @@ class BatcherGroup(Batcher):
     connection pinned to one member; the Batcher methods route / fan out."""
 
     _P = "uvhttp_ws_amd_batcher_group_"
+    _ZC = _P
 
     def __init__(self, devices, min_device_bytes=0, max_bytes=32 << 20, max_connections=16384,
                  max_reads=1 << 18):

@@ -31,6 +31,8 @@
 #include <string.h>
 #include <unordered_map>
 #include <unordered_set>
+#include <memory>
+#include <utility>
 #include <vector>
 
 #include "uvhttp_tls_amd.h"
@@ -79,6 +81,23 @@ struct TlsConn {
 
 inline uint64_t align16(uint64_t x) { return (x + 15) & ~(uint64_t)15; }
 
+// the host-only arena grows by resize() without zero-filling: alloc_read hands the new bytes
+// to the socket read, which writes them
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = NoInitAlloc<U>;
+    };
+    NoInitAlloc() = default;
+    template <class U>
+    NoInitAlloc(const NoInitAlloc<U>&) {}
+    template <class U>
+    void construct(U* p) { ::new ((void*)p) U; }
+    template <class U, class... A>
+    void construct(U* p, A&&... a) { ::new ((void*)p) U(std::forward<A>(a)...); }
+};
+
 struct GatherSeg {  // arena[src, src + len) -> wire[dst, dst + len)
     uint64_t src, dst, len;
 };
@@ -111,7 +130,8 @@ double ms_since(std::chrono::steady_clock::time_point t0) {
 
 // One queue: the reads of one flush, and (device batcher) the buffers its decode uses.
 struct BatchQueue {
-    std::vector<uint8_t> arena;  // host-only batcher: the queued reads
+    std::vector<uint8_t, NoInitAlloc<uint8_t>> arena;  // host-only batcher: the queued reads
+    uint64_t gen = 0;            // bumped whenever the queue is cleared (zero-copy reads check it)
     uint8_t* h_arena = nullptr;  // device batcher: the reads, pinned (wire_cap bytes), then
     uint64_t arena_len = 0;      // the recv-buffer prefixes staged at flush time
     uint64_t uploaded = 0;       // h_arena[0, uploaded) is already on its way to d_arena
@@ -186,6 +206,17 @@ struct uvhttp_ws_amd_batcher {
     // completes (desc_refetches)
     uint64_t desc_hint = 4096, wdesc_hint = 4096;
     uvhttp_ws_amd_batcher_stats_t st;
+    // the zero-copy read handed out by alloc_read and not yet committed: space at arena offset
+    // `off` of queue `qi` (generation `gen`), `cap` bytes, for `conn`
+    struct {
+        uvhttp_ws_connection_t* conn = nullptr;
+        int qi = 0;
+        uint64_t gen = 0, off = 0, cap = 0;
+        bool tls = false;
+        bool direct = false;  // the space is `direct` below: decoded at commit (submit_read's
+                              // path for a read no flush can hold)
+    } pend;
+    std::vector<uint8_t, NoInitAlloc<uint8_t>> direct;
     std::vector<float> blocked;  // ms of each blocked call (ring of the last kBlockedKeep)
     uint64_t blocked_n = 0;
 };
@@ -331,6 +362,7 @@ void release(uvhttp_ws_amd_batcher_t* b) {
 }
 
 void clear_queue(BatchQueue& q) {
+    q.gen++;
     q.arena.clear();
     q.arena_len = q.uploaded = 0;
     q.reads.clear();
@@ -1074,82 +1106,64 @@ uint64_t prefix_bound(const uvhttp_ws_amd_batcher_t* b, const uvhttp_ws_connecti
     return pos;
 }
 
-// queue one read (plain bytes, or a TLS connection's ciphertext)
-uvhttp_error_t queue_read(uvhttp_ws_amd_batcher_t* b, uvhttp_ws_connection_t* conn,
-                          const uint8_t* data, size_t len, bool tls) {
-    if (b->failed.count(conn)) return UVHTTP_ERROR_INVALID_PARAM;
+// The device layout a fresh slot of conn reserves in a queue: its recv-buffer prefix (aligned)
+// + 16, and room for a TLS connection's carried incomplete record
+uint64_t slot_prefix(const uvhttp_ws_amd_batcher_t* b, const uvhttp_ws_connection_t* conn, bool tls) {
+    return align16(prefix_bound(b, conn)) + 16 + (tls ? kTlsCarryMax : 0);
+}
+
+// Bytes a read of conn may have in the accumulating queue without handing it over (0: none)
+uint64_t read_room(const uvhttp_ws_amd_batcher_t* b, uvhttp_ws_connection_t* conn, bool tls) {
+    const BatchQueue& q = b->q[b->cur];
+    const bool fresh = q.slot_of.find(conn) == q.slot_of.end();
+    const uint64_t used = q.staged + (fresh ? slot_prefix(b, conn, tls) : 0);
+    if (used >= b->cfg.max_bytes || q.reads.size() + 1 > b->cfg.max_reads ||
+        (fresh && q.slots.size() + 1 > b->cfg.max_connections))
+        return 0;
+    return b->cfg.max_bytes - used;
+}
+
+// Make room in the accumulating queue for a read of `len` bytes of conn: a full queue is handed
+// to the decoder first.  0: it fits now; 1: it is larger than a whole flush (the queue before it
+// was handed over and, if it held reads of conn, delivered); -1: refused (inside a callback, where
+// no flush can run, or conn failed / was handed back meanwhile).
+int make_room(uvhttp_ws_amd_batcher_t* b, uvhttp_ws_connection_t* conn, uint64_t len, bool tls) {
+    if (read_room(b, conn, tls) >= len) return 0;
+    // the queue is full: hand it to the decoder first (not from inside a callback, where
+    // the flush being delivered cannot be finished: the read is refused there)
+    if (b->delivering) return -1;
+    Blocked bl{b};
+    (void)start_flush(b, true);  // (a device error there was decoded on the host and counted)
+    if (b->failed.count(conn)) return -1;
+    if (tls && !b->tls.count(conn)) return -1;  // handed back
+    if (slot_prefix(b, conn, tls) + len > b->cfg.max_bytes && b->q[b->cur ^ 1].in_flight) {
+        // too large only because the queue just handed over still holds reads of this
+        // connection (prefix_bound counts them): deliver it, then the prefix is exact
+        (void)finish_inflight(b, true);
+        if (b->failed.count(conn)) return -1;
+        if (tls && !b->tls.count(conn)) return -1;
+    }
+    return slot_prefix(b, conn, tls) + len > b->cfg.max_bytes ? 1 : 0;
+}
+
+// Record a read of `len` bytes already at arena offset `off` of the accumulating queue (the
+// queue has room: make_room / read_room)
+void record_read(uvhttp_ws_amd_batcher_t* b, uvhttp_ws_connection_t* conn, uint64_t off, uint64_t len,
+                 bool tls) {
     BatchQueue* q = &b->q[b->cur];
     auto it = q->slot_of.find(conn);
-    bool fresh = it == q->slot_of.end();
-    if (!fresh && q->slots[it->second].tls != tls) return UVHTTP_ERROR_INVALID_PARAM;
-    const uint64_t carry = tls ? kTlsCarryMax : 0;
-    const uint64_t pre = align16(prefix_bound(b, conn)) + 16 + carry;
-    const uint64_t need = (uint64_t)len + (fresh ? pre : 0);
-    if (q->staged + need > b->cfg.max_bytes || q->reads.size() + 1 > b->cfg.max_reads ||
-        (fresh && q->slots.size() + 1 > b->cfg.max_connections)) {
-        // the queue is full: hand it to the decoder first (not from inside a callback, where
-        // the flush being delivered cannot be finished: the read is refused there)
-        if (b->delivering) return UVHTTP_ERROR_INVALID_PARAM;
-        Blocked bl{b};
-        (void)start_flush(b, true);  // (a device error there was decoded on the host and counted)
-        if (b->failed.count(conn)) return UVHTTP_ERROR_INVALID_PARAM;
-        if (tls && !b->tls.count(conn)) return UVHTTP_ERROR_INVALID_PARAM;  // handed back
-        uint64_t pre2 = align16(prefix_bound(b, conn)) + 16 + carry;
-        if (pre2 + len > b->cfg.max_bytes && b->q[b->cur ^ 1].in_flight) {
-            // too large only because the queue just handed over still holds reads of this
-            // connection (prefix_bound counts them): deliver it, then the prefix is exact
-            (void)finish_inflight(b, true);
-            if (b->failed.count(conn)) return UVHTTP_ERROR_INVALID_PARAM;
-            if (tls && !b->tls.count(conn)) return UVHTTP_ERROR_INVALID_PARAM;
-            pre2 = align16(prefix_bound(b, conn)) + 16 + carry;
-        }
-        if (pre2 + len > b->cfg.max_bytes) {
-            if (tls) {
-                // ciphertext can be cut anywhere (records reassemble across flushes): queue it
-                // in halves of a flush
-                const size_t piece = (size_t)(b->cfg.max_bytes / 2);
-                if (piece == 0 || pre2 + piece > b->cfg.max_bytes) return UVHTTP_ERROR_INVALID_PARAM;
-                for (size_t o = 0; o < len; o += piece) {
-                    const uvhttp_error_t rc = queue_read(b, conn, data + o, len - o < piece ? len - o : piece, true);
-                    if (rc != UVHTTP_OK) return rc;
-                }
-                return UVHTTP_OK;
-            }
-            // larger than a whole flush: every earlier read of the connection must be
-            // delivered first, then the read is decoded here (nothing of it is queued)
-            (void)finish_inflight(b, true);
-            if (b->failed.count(conn)) return UVHTTP_ERROR_INVALID_PARAM;
-            const uvhttp_error_t rc = uvhttp_ws_process_data(conn, data, len);
-            b->st.host_reads++;
-            b->st.direct_reads++;
-            if (rc != UVHTTP_OK) b->failed.insert(conn);
-            return rc;
-        }
-        q = &b->q[b->cur];
-        it = q->slot_of.find(conn);
-        fresh = it == q->slot_of.end();
-    }
     uint32_t k;
-    if (fresh) {
+    if (it == q->slot_of.end()) {
         k = (uint32_t)q->slots.size();
         q->slots.push_back(ConnSlot{conn, {}, 0, false, tls});
         q->slot_of[conn] = k;
-        q->staged += pre;
+        q->staged += slot_prefix(b, conn, tls);
         if (tls) q->n_tls_slots++;
     } else {
         k = it->second;
     }
-    uint64_t off;
-    if (!b->eng) {
-        off = q->arena.size();
-        q->arena.insert(q->arena.end(), data, data + len);
-    } else {
-        off = q->arena_len;
-        if (off + len > b->wire_cap) return UVHTTP_ERROR_INVALID_PARAM;  // (cannot happen)
-        const auto tc = std::chrono::steady_clock::now();
-        if (len) uvhttp_ws_amd_copy_stream(q->h_arena + off, data, len);
-        b->st.copy_ms += ms_since(tc);
-        q->arena_len += len;
+    if (b->eng) {
+        q->arena_len = off + len;
         // a queue large enough for the device streams to HBM while it fills
         if ((q->bytes + len >= b->cfg.min_device_bytes || q->n_tls_slots) &&
             q->arena_len - q->uploaded >= kUploadPiece) {
@@ -1167,6 +1181,55 @@ uvhttp_error_t queue_read(uvhttp_ws_amd_batcher_t* b, uvhttp_ws_connection_t* co
     q->slots[k].bytes += len;
     q->staged += len;
     q->bytes += len;
+}
+
+// queue one read (plain bytes, or a TLS connection's ciphertext)
+uvhttp_error_t queue_read(uvhttp_ws_amd_batcher_t* b, uvhttp_ws_connection_t* conn,
+                          const uint8_t* data, size_t len, bool tls) {
+    if (b->failed.count(conn)) return UVHTTP_ERROR_INVALID_PARAM;
+    {
+        const BatchQueue& q = b->q[b->cur];
+        auto it = q.slot_of.find(conn);
+        if (it != q.slot_of.end() && q.slots[it->second].tls != tls) return UVHTTP_ERROR_INVALID_PARAM;
+    }
+    const int room = make_room(b, conn, len, tls);
+    if (room < 0) return UVHTTP_ERROR_INVALID_PARAM;
+    if (room == 1) {
+        if (tls) {
+            // ciphertext can be cut anywhere (records reassemble across flushes): queue it
+            // in halves of a flush
+            const size_t piece = (size_t)(b->cfg.max_bytes / 2);
+            if (piece == 0 || slot_prefix(b, conn, true) + piece > b->cfg.max_bytes)
+                return UVHTTP_ERROR_INVALID_PARAM;
+            for (size_t o = 0; o < len; o += piece) {
+                const uvhttp_error_t rc = queue_read(b, conn, data + o, len - o < piece ? len - o : piece, true);
+                if (rc != UVHTTP_OK) return rc;
+            }
+            return UVHTTP_OK;
+        }
+        // larger than a whole flush: every earlier read of the connection must be
+        // delivered first, then the read is decoded here (nothing of it is queued)
+        (void)finish_inflight(b, true);
+        if (b->failed.count(conn)) return UVHTTP_ERROR_INVALID_PARAM;
+        const uvhttp_error_t rc = uvhttp_ws_process_data(conn, data, len);
+        b->st.host_reads++;
+        b->st.direct_reads++;
+        if (rc != UVHTTP_OK) b->failed.insert(conn);
+        return rc;
+    }
+    BatchQueue* q = &b->q[b->cur];
+    uint64_t off;
+    if (!b->eng) {
+        off = q->arena.size();
+        q->arena.insert(q->arena.end(), data, data + len);
+    } else {
+        off = q->arena_len;
+        if (off + len > b->wire_cap) return UVHTTP_ERROR_INVALID_PARAM;  // (cannot happen)
+        const auto tc = std::chrono::steady_clock::now();
+        if (len) uvhttp_ws_amd_copy_stream(q->h_arena + off, data, len);
+        b->st.copy_ms += ms_since(tc);
+    }
+    record_read(b, conn, off, len, tls);
     return UVHTTP_OK;
 }
 
@@ -1180,6 +1243,95 @@ uvhttp_error_t uvhttp_ws_amd_batcher_submit_read(uvhttp_ws_amd_batcher_t* b,
     if (!b || !conn || (!data && len)) return UVHTTP_ERROR_INVALID_PARAM;
     if (b->tls.count(conn)) return UVHTTP_ERROR_INVALID_PARAM;  // a TLS connection's reads are ciphertext
     return queue_read(b, conn, data, len, false);
+}
+
+uvhttp_error_t uvhttp_ws_amd_batcher_alloc_read(uvhttp_ws_amd_batcher_t* b,
+                                                struct uvhttp_ws_connection* conn, size_t suggested,
+                                                uint8_t** buf, size_t* len) {
+    if (!b || !conn || !buf || !len) return UVHTTP_ERROR_INVALID_PARAM;
+    *buf = nullptr;
+    *len = 0;
+    b->pend.conn = nullptr;  // (an allocation never committed is dropped)
+    if (b->failed.count(conn)) return UVHTTP_ERROR_INVALID_PARAM;
+    const bool tls = b->tls.count(conn) != 0;
+    {
+        const BatchQueue& q = b->q[b->cur];
+        auto it = q.slot_of.find(conn);
+        if (it != q.slot_of.end() && q.slots[it->second].tls != tls) return UVHTTP_ERROR_INVALID_PARAM;
+    }
+    uint64_t want = suggested ? suggested : 65536;
+    if (read_room(b, conn, tls) < want) {
+        // a full queue is handed over first; a read larger than a whole flush gets what one
+        // flush holds (the socket delivers the rest to the next read)
+        if (make_room(b, conn, want, tls) < 0) return UVHTTP_ERROR_INVALID_PARAM;
+        const uint64_t room = read_room(b, conn, tls);
+        if (room == 0) {
+            // not even one byte fits a flush beside the connection's recv-buffer prefix: the
+            // read is decoded at commit, after the connection's earlier reads (submit_read's
+            // direct path; make_room delivered them if they were in flight)
+            if (tls) return UVHTTP_ERROR_INVALID_PARAM;
+            b->direct.resize(want);
+            b->pend.conn = conn;
+            b->pend.cap = want;
+            b->pend.tls = false;
+            b->pend.direct = true;
+            *buf = b->direct.data();
+            *len = (size_t)want;
+            return UVHTTP_OK;
+        }
+        if (room < want) want = room;
+    }
+    BatchQueue& q = b->q[b->cur];
+    uint64_t off;
+    uint8_t* base;
+    if (!b->eng) {
+        off = q.arena.size();
+        q.arena.resize(off + want);  // (no fill: the read writes it)
+        base = q.arena.data();
+    } else {
+        off = q.arena_len;
+        if (off + want > b->wire_cap) return UVHTTP_ERROR_INVALID_PARAM;  // (cannot happen)
+        base = q.h_arena;
+    }
+    b->pend.conn = conn;
+    b->pend.qi = b->cur;
+    b->pend.gen = q.gen;
+    b->pend.off = off;
+    b->pend.cap = want;
+    b->pend.tls = tls;
+    b->pend.direct = false;
+    *buf = base + off;
+    *len = (size_t)want;
+    return UVHTTP_OK;
+}
+
+uvhttp_error_t uvhttp_ws_amd_batcher_commit_read(uvhttp_ws_amd_batcher_t* b,
+                                                 struct uvhttp_ws_connection* conn, size_t nread) {
+    if (!b || !conn) return UVHTTP_ERROR_INVALID_PARAM;
+    const auto p = b->pend;
+    b->pend.conn = nullptr;
+    if (p.conn != conn || nread > p.cap) return UVHTTP_ERROR_INVALID_PARAM;
+    if (p.direct) {
+        if (nread == 0) return UVHTTP_OK;
+        if (b->delivering) return UVHTTP_ERROR_INVALID_PARAM;  // (alloc_read refused there already)
+        (void)finish_inflight(b, true);
+        if (b->failed.count(conn)) return UVHTTP_ERROR_INVALID_PARAM;
+        const uvhttp_error_t rc = uvhttp_ws_process_data(conn, b->direct.data(), nread);
+        b->st.host_reads++;
+        b->st.direct_reads++;
+        b->st.zero_copy_reads++;
+        if (rc != UVHTTP_OK) b->failed.insert(conn);
+        return rc;
+    }
+    // the allocation must be in the queue still accumulating (no flush since)
+    if (p.qi != b->cur || b->q[p.qi].gen != p.gen) return UVHTTP_ERROR_INVALID_PARAM;
+    BatchQueue& q = b->q[b->cur];
+    if (!b->eng) q.arena.resize(p.off + nread);
+    if (nread == 0) return UVHTTP_OK;  // nothing read (EAGAIN, or EOF / an error the caller handles)
+    if (b->failed.count(conn)) return UVHTTP_ERROR_INVALID_PARAM;  // (forgotten meanwhile: cannot happen)
+    record_read(b, conn, p.off, nread, p.tls);
+    b->st.zero_copy_reads++;
+    return UVHTTP_OK;
 }
 
 int uvhttp_ws_amd_batcher_set_tls(uvhttp_ws_amd_batcher_t* b, struct uvhttp_ws_connection* conn,
@@ -1225,6 +1377,7 @@ uvhttp_error_t uvhttp_ws_amd_batcher_submit_tls_read(uvhttp_ws_amd_batcher_t* b,
 
 void uvhttp_ws_amd_batcher_forget(uvhttp_ws_amd_batcher_t* b, struct uvhttp_ws_connection* conn) {
     if (!b || !conn) return;
+    if (b->pend.conn == conn) b->pend.conn = nullptr;  // its uncommitted allocation too
     b->failed.erase(conn);
     b->tls.erase(conn);
     for (int i = 0; i < 2; ++i) {

@@ -141,6 +141,21 @@ int uvhttp_ws_amd_batcher_group_set_tls(uvhttp_ws_amd_batcher_group_t* g, struct
     return uvhttp_ws_amd_batcher_set_tls(g->members[m], conn, tls_key, read_seq);
 }
 
+uvhttp_error_t uvhttp_ws_amd_batcher_group_alloc_read(uvhttp_ws_amd_batcher_group_t* g,
+                                                      struct uvhttp_ws_connection* conn, size_t suggested,
+                                                      uint8_t** buf, size_t* len) {
+    if (!g || !conn) return UVHTTP_ERROR_INVALID_PARAM;
+    return uvhttp_ws_amd_batcher_alloc_read(g->members[member_for(g, conn)], conn, suggested, buf, len);
+}
+
+uvhttp_error_t uvhttp_ws_amd_batcher_group_commit_read(uvhttp_ws_amd_batcher_group_t* g,
+                                                       struct uvhttp_ws_connection* conn, size_t nread) {
+    if (!g || !conn) return UVHTTP_ERROR_INVALID_PARAM;
+    auto it = g->member_of.find(conn);
+    if (it == g->member_of.end()) return UVHTTP_ERROR_INVALID_PARAM;  // (no alloc_read before)
+    return uvhttp_ws_amd_batcher_commit_read(g->members[it->second], conn, nread);
+}
+
 uvhttp_error_t uvhttp_ws_amd_batcher_group_submit_tls_read(uvhttp_ws_amd_batcher_group_t* g,
                                                            struct uvhttp_ws_connection* conn,
                                                            const uint8_t* ciphertext, size_t len) {
@@ -220,6 +235,7 @@ int uvhttp_ws_amd_batcher_group_stats(const uvhttp_ws_amd_batcher_group_t* g,
         out->tls_handbacks += s.tls_handbacks;
         out->desc_refetches += s.desc_refetches;
         out->blocked_calls += s.blocked_calls;
+        out->zero_copy_reads += s.zero_copy_reads;
         // per-call distributions do not add up: the worst member's
         if (s.max_blocked_ms > out->max_blocked_ms) {
             out->max_blocked_ms = s.max_blocked_ms;

@@ -244,6 +244,7 @@ struct Workspace {
     uint64_t* arena_first; // [n_arena_tiles]: tagged first data frame of the arena tile
     uint32_t* ctl;         // control words outside the clearable workspace (see kCtl*)
     void* recs;            // [n_frames] FrameRec: the fused stride path's parsed headers
+    void* parts;           // [n_frames / 4096 + 2] TilePart: summary-only decode, per k_sum_scan block
 };
 
 // ctl words (their own allocation, never cleared with the workspace)
@@ -291,6 +292,51 @@ struct alignas(16) FrameRec {
 };
 static_assert(sizeof(FrameRec) == 16, "one 16-byte load per record");
 constexpr uint8_t kRecHasLen = 0x80;
+
+// Summary-only decode (uvhttp_ws_gpu_decode_inplace with d_desc == NULL, stride batches): what
+// the batch summary needs from a run of consecutive frames, in frame order, up to the run's
+// first failure — one per k_sum_scan block, combined by k_sum_tail.
+struct alignas(16) TilePart {
+    uint64_t pay;   // payload bytes of the frames (src/uvhttp_websocket.c: all delivered frames)
+    uint64_t seg;   // data payload since the latest start (all of it when the run has no start)
+    uint32_t nfin;  // data frames with FIN: completed messages
+    uint32_t ls;    // latest start (non-CONT data frame), kNoFrame if none
+    uint32_t last;  // latest data frame, kNoFrame if none
+    uint32_t bits;  // kPartOpen: `last` leaves a message open; kPartClosed: a CLOSE was delivered
+    uint32_t ff;    // the run's first failing frame (the run stops before it), kNoFrame if none
+    uint32_t pad[3];
+};
+static_assert(sizeof(TilePart) == 48, "three 16-byte words");
+constexpr uint32_t kPartOpen = 1u, kPartClosed = 2u;
+
+__device__ __host__ inline TilePart part_identity() {
+    TilePart p;
+    p.pay = 0;
+    p.seg = 0;
+    p.nfin = 0;
+    p.ls = kNoFrame;
+    p.last = kNoFrame;
+    p.bits = 0;
+    p.ff = kNoFrame;
+    p.pad[0] = p.pad[1] = p.pad[2] = 0;
+    return p;
+}
+
+
+// a followed by b: a run that failed ends the combined run there
+__device__ __host__ inline TilePart part_combine(const TilePart& a, const TilePart& b) {
+    if (a.ff != kNoFrame) return a;
+    TilePart r;
+    r.ff = b.ff;
+    r.pad[0] = r.pad[1] = r.pad[2] = 0;
+    r.pay = a.pay + b.pay;
+    r.nfin = a.nfin + b.nfin;
+    r.ls = b.ls != kNoFrame ? b.ls : a.ls;
+    r.seg = b.ls != kNoFrame ? b.seg : a.seg + b.seg;
+    r.last = b.last != kNoFrame ? b.last : a.last;
+    r.bits = ((b.last != kNoFrame ? b.bits : a.bits) & kPartOpen) | ((a.bits | b.bits) & kPartClosed);
+    return r;
+}
 
 struct BatchArgs {
     uint8_t* wire;
@@ -1588,6 +1634,38 @@ __device__ inline int32_t rel_clamp(uint64_t x, uint64_t t0, uint64_t kT, bool k
     return (int32_t)((int64_t)x - (int64_t)t0);
 }
 
+// summary-only decode: what the fragment state machine and the summary need of one parsed frame
+constexpr uint64_t kSumMinStride = 140;  // a control frame (<= 125 B of payload, header <= 10 B
+                                         // even non-minimal, + key) is shorter than any slot
+constexpr uint32_t kSiOk = 1u, kSiData = 2u, kSiFin = 4u, kSiStart = 8u, kSiZero = 16u, kSiClose = 32u;
+constexpr uint32_t kSiHmShift = 8;  // header + key bytes in bits 8..15 (payload = slot - them)
+__device__ constexpr uint32_t kHm[6] = {2u, 4u, 6u, 8u, 10u, 14u};  // every header + key size
+__device__ inline uint32_t sum_info(const uvhttp_ws_frame_desc_t& d) {
+    uint32_t x = ((uint32_t)d.header_size + ((d.flags & UVHTTP_WS_FLAG_MASK) ? 4u : 0u)) << kSiHmShift;
+    if (d.status == UVHTTP_WS_FRAME_OK) x |= kSiOk;
+    if (d.opcode <= 2) x |= kSiData;
+    if (d.opcode == 1 || d.opcode == 2) x |= kSiStart;
+    if (d.flags & UVHTTP_WS_FLAG_FIN) x |= kSiFin;
+    if (d.payload_len == 0) x |= kSiZero;
+    if (d.opcode == 8) x |= kSiClose;
+    return x;
+}
+// the data frame leaves a message open: FIN = 0 and not a zero-length start, whose empty first
+// fragment allocates nothing (src/uvhttp_websocket.c:794-816 + :964; kLastOpen in the scan)
+__device__ inline bool si_open(uint32_t x) {
+    return (x & kSiData) && !(x & kSiFin) && !((x & kSiStart) && (x & kSiZero));
+}
+// the one byte per frame the summary-only payload pass leaves for k_sum_scan: locally valid,
+// data frame, FIN, start, leaves a message open, and the header + key size class (kHm)
+constexpr uint32_t kI8Ok = 1u, kI8Data = 2u, kI8Fin = 4u, kI8Start = 8u, kI8Open = 16u, kI8HmShift = 5;
+__device__ inline uint8_t info8_of(const uvhttp_ws_frame_desc_t& d) {
+    const uint32_t x = sum_info(d);
+    const uint32_t hm = x >> kSiHmShift;
+    const uint32_t c = hm == 2 ? 0u : hm == 4 ? 1u : hm == 6 ? 2u : hm == 8 ? 3u : hm == 10 ? 4u : 5u;
+    return (uint8_t)(((x & kSiOk) ? kI8Ok : 0u) | ((x & kSiData) ? kI8Data : 0u) |
+                     ((x & kSiFin) ? kI8Fin : 0u) | ((x & kSiStart) ? kI8Start : 0u) |
+                     (si_open(x) ? kI8Open : 0u) | (c << kI8HmShift));
+}
 // add_mask on tile-relative int32 positions (vector at r, payload [ps, pe))
 __device__ inline void add_mask_rel(u32x4& m, int32_t r, int32_t ps, int32_t pe, uint32_t key) {
     if (pe <= r || ps >= r + 16) return;
@@ -1604,8 +1682,8 @@ __device__ inline void add_mask_rel(u32x4& m, int32_t r, int32_t ps, int32_t pe,
     m.w |= rk & lane_bytes(lo, hi, 3);
 }
 
-template <int BLOCK, int VPT, int AUX = 18>
-__global__ __launch_bounds__(BLOCK) void k_unmask_stride(BatchArgs a, uint64_t tile_base) {
+template <int BLOCK, int VPT, int AUX = 18, bool SUM = false>
+__global__ __launch_bounds__(BLOCK) void k_unmask_stride(BatchArgs a, Workspace ws, uint64_t tile_base) {
     StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_PAYLOAD, false);
     constexpr uint64_t kT = (uint64_t)BLOCK * VPT * 16;
     constexpr int kMaxF = (int)(kT / kFusedMinStride) + 2;  // frames touching one tile
@@ -1664,7 +1742,12 @@ __global__ __launch_bounds__(BLOCK) void k_unmask_stride(BatchArgs a, uint64_t t
         const u32x4 hv = o < t0 ? s_h0 : lds_window(s_tile, (uint32_t)(o - t0));
         uvhttp_ws_frame_desc_t d;
         (void)parse_hdr(a, f, seg_info(a, f, n), o, hv, d);
-        if (o >= t0) a.recs[f] = rec_of(d);  // (a frame that started earlier: its own tile)
+        if (o >= t0) {  // (a frame that started earlier: its own tile's)
+            // summary-only decode: one info byte per frame (k_sum_scan runs the state machine
+            // on them); else the frame's 16-byte record for k_plan
+            if constexpr (SUM) reinterpret_cast<uint8_t*>(a.recs)[f] = info8_of(d);
+            else a.recs[f] = rec_of(d);
+        }
         const bool ok = d.status == UVHTTP_WS_FRAME_OK;
         // speculative compact pass: the frame is uniform (a locally valid data frame with the
         // batch's uniform payload length and header + key bytes), so it goes to f * spec_P
@@ -1870,6 +1953,209 @@ __global__ __launch_bounds__(kBlock) void k_fixup(BatchArgs a, uvhttp_ws_frame_d
         desc_of_rec(r, i * a.frame_stride, d);
         remask_range(a.wire, d.payload_off, d.payload_off + d.payload_len, d.masking_key);
     }
+}
+
+// ------------------------------------------------------------------------------------
+// Summary-only decode, after k_unmask_stride<..., SUM = true> (which left one info byte per
+// frame and unmasked every locally valid frame):
+//   k_sum_scan  16 frames per thread: the fragment state machine — with every frame before a
+//               delivered one delivered, no control frame filling a slot but the last (stride >=
+//               kSumMinStride) and no max_message_size check able to fire (run_decode's bound),
+//               the state before frame f is "the latest data frame before f left a message
+//               open" (src/uvhttp_websocket.c:950-1015: CONT needs an open message, a start must
+//               not meet one) — then the summary's sums up to the first failure, per block
+//               (ordered); a block with a failure claims first_bad;
+//   k_sum_tail  with first_bad final: every block re-masks the frames the payload pass
+//               unmasked from the first failure on (headers intact: parsed again from the wire);
+//               block 0 combines the scan blocks' parts in order, adds the last frame's (the
+//               scan leaves it out: its slot may be longer than the stride) and writes the
+//               summary (write_summary's fields).
+// No block waits for another: nothing here can give up.  (Computing the parts inside the
+// payload pass, one per tile, cost that bandwidth-bound kernel 7 us on C4: 91.8 -> 99.2.)
+// ------------------------------------------------------------------------------------
+__device__ inline TilePart shfl_down_part(const TilePart& p, int d) {
+    TilePart r;
+    r.pay = __shfl_down(p.pay, d, 64);
+    r.seg = __shfl_down(p.seg, d, 64);
+    r.nfin = __shfl_down(p.nfin, d, 64);
+    r.ls = __shfl_down(p.ls, d, 64);
+    r.last = __shfl_down(p.last, d, 64);
+    r.bits = __shfl_down(p.bits, d, 64);
+    r.ff = __shfl_down(p.ff, d, 64);
+    r.pad[0] = r.pad[1] = r.pad[2] = 0;
+    return r;
+}
+
+// ordered reduction over the block's NT threads (thread t holds element t): thread 0 gets all
+template <int NT>
+__device__ TilePart block_reduce_parts(const TilePart& v) {
+    __shared__ TilePart s_p[NT];
+    s_p[threadIdx.x] = v;
+    __syncthreads();
+    TilePart r = part_identity();
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+#pragma unroll
+        for (int k = 0; k < NT / 64; ++k) r = part_combine(r, s_p[lane * (NT / 64) + k]);
+        // lane l holds [l, l + 2d) after step d
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const TilePart o = shfl_down_part(r, d);
+            if (lane + d < 64) r = part_combine(r, o);
+        }
+    }
+    __syncthreads();
+    return r;
+}
+
+// frames per k_sum_scan thread: one 4-byte load of info bytes.  (16 per thread — one 16-byte
+// load — left one wave per SIMD walking its frames serially: 10.4 us on C4; rocprofv3, r05k)
+constexpr uint32_t kScanFpt = 4;
+
+__global__ __launch_bounds__(kBlock) void k_sum_scan(BatchArgs a, Workspace ws) {
+    resolve_epoch(a, ws);
+    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_PLAN);
+    const uint32_t n = a.n;
+    const uint64_t S = a.frame_stride;
+    const uint8_t* info = reinterpret_cast<const uint8_t*>(a.recs);
+    const uint32_t F0 = (blockIdx.x * kBlock + threadIdx.x) * kScanFpt;
+#ifdef UVWS_SCAN_NOP
+    return;  // experiment: the launch alone (wrong summaries)
+#endif
+    // (info bytes past n are never used; the buffer holds at least n + 16)
+    const uint32_t w = F0 < n ? *reinterpret_cast<const uint32_t*>(info + F0) : 0u;
+    // the frame before this thread's first: the previous lane's last byte (lane 0: a load)
+    const uint32_t up = __shfl_up(w, 1, 64);
+    uint32_t pb = (threadIdx.x & 63) ? up >> 24 : (F0 > 0 && F0 < n ? info[F0 - 1] : 0u);
+    TilePart acc = part_identity();
+#pragma unroll
+    for (uint32_t k = 0; k < kScanFpt; ++k) {
+        const uint32_t f = F0 + k;
+        if (f >= n) break;
+        const uint32_t x = (w >> (8 * k)) & 0xFF;
+        uint32_t p = f ? pb : 0u;  // (nothing before frame 0: no message open)
+        // frames that are not data frames — reserved opcodes 3-7, which the reference delivers
+        // leaving the fragment state as it was — may sit between f and the data frame that
+        // decides: walk back to it; each such frame is walked over by one data frame at most
+        if ((x & kI8Ok) && (x & kI8Data) && f > 0 && (p & kI8Ok) && !(p & kI8Data)) {
+            for (uint32_t g = f - 1;;) {
+                if (g == 0) {
+                    p = 0u;
+                    break;
+                }
+                --g;
+                const uint32_t gi = g >= F0 ? (w >> (8 * (g - F0))) & 0xFF : info[g];
+                if (!(gi & kI8Ok)) {  // a failure before f decides the batch anyway
+                    p = 0u;
+                    break;
+                }
+                if (gi & kI8Data) {
+                    p = gi;
+                    break;
+                }
+            }
+        }
+        if (!(x & kI8Ok) || ((x & kI8Data) && ((p & kI8Open) != 0) == ((x & kI8Start) != 0))) {
+            acc.ff = f;
+            break;
+        }
+        if (f + 1 < n) {  // (the last frame's part is the tail's)
+            const uint64_t plen = S - kHm[x >> kI8HmShift];
+            acc.pay += plen;
+            if (x & kI8Data) {
+                if (x & kI8Start) {
+                    acc.ls = f;
+                    acc.seg = plen;
+                } else {
+                    acc.seg += plen;
+                }
+                acc.nfin += (x & kI8Fin) ? 1u : 0u;
+                acc.last = f;
+                acc.bits = (x & kI8Open) ? kPartOpen : 0u;
+            }
+        }
+        pb = x;
+    }
+#ifdef UVWS_SCAN_NORED
+    const TilePart bp = acc;  // experiment: no block reduction (wrong summaries)
+#else
+    const TilePart bp = block_reduce_parts<kBlock>(acc);
+#endif
+    if (threadIdx.x == 0) {
+        reinterpret_cast<TilePart*>(ws.parts)[blockIdx.x] = bp;
+        if (bp.ff != kNoFrame) tag_claim(ws.first_bad, a.epoch, bp.ff);
+    }
+}
+
+constexpr uint32_t kSumTailGrid = 128;  // k_sum_tail blocks (all re-mask after a failure)
+
+__global__ __launch_bounds__(kBlock) void k_sum_tail(BatchArgs a, Workspace ws, uint32_t n_parts) {
+    resolve_epoch(a, ws);
+    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_FIXUP);
+    const uint32_t n = a.n;
+    const uint64_t S = a.frame_stride;
+    // the last frame's header (its part of the summary), read first
+    uvhttp_ws_frame_desc_t dl;
+    if (blockIdx.x == 0 && threadIdx.x == 0) (void)parse_one(a, n - 1, seg_info(a, n - 1, n), dl);
+    const uint32_t nb = first_bad_of(a, ws, n);
+    if (nb < n) {  // a failure: restore the frames the payload pass unmasked from it on
+        const uint64_t wave = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+        const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
+        for (uint64_t i = nb + wave; i < n; i += nwaves) {
+            uvhttp_ws_frame_desc_t d;
+            (void)parse_one(a, (uint32_t)i, seg_info(a, (uint32_t)i, n), d);
+            if (d.status == UVHTTP_WS_FRAME_OK && d.payload_len)
+                remask_range(a.wire, d.payload_off, d.payload_off + d.payload_len, d.masking_key);
+        }
+    }
+    if (blockIdx.x != 0) return;
+    // block 0: the scan blocks' parts in order, each thread a run of consecutive ones
+    const TilePart* parts = reinterpret_cast<const TilePart*>(ws.parts);
+    const uint32_t per = (n_parts + kBlock - 1) / kBlock;
+    const uint32_t p0 = threadIdx.x * per;
+    TilePart acc = part_identity();
+    constexpr uint32_t kU = 8;  // loads in flight per thread
+    for (uint32_t pb = p0; pb < p0 + per && pb < n_parts; pb += kU) {
+        TilePart r[kU];
+#pragma unroll
+        for (uint32_t k = 0; k < kU; ++k)
+            r[k] = pb + k < p0 + per && pb + k < n_parts ? parts[pb + k] : part_identity();
+#pragma unroll
+        for (uint32_t k = 0; k < kU; ++k) acc = part_combine(acc, r[k]);
+    }
+    TilePart tot = block_reduce_parts<kBlock>(acc);
+    if (threadIdx.x != 0) return;
+    uvhttp_ws_batch_summary_t sm;
+    sm.n_frames = n;
+    sm.n_delivered = nb < n ? nb : n;
+    sm.first_status = 0;
+    sm.state_closed = 0;
+    if (nb < n) {  // its local status, or (locally valid) the fragment check's
+        uvhttp_ws_frame_desc_t d;
+        (void)parse_one(a, nb, seg_info(a, nb, n), d);
+        sm.first_status = d.status != UVHTTP_WS_FRAME_OK ? d.status : UVHTTP_WS_FRAME_ERR_FRAGMENT;
+        sm.consumed_bytes = (uint64_t)nb * S;
+    } else {  // the last frame was delivered: its part
+        const uint32_t x = sum_info(dl);
+        TilePart lp = part_identity();
+        lp.pay = dl.payload_len;
+        if (x & kSiData) {
+            lp.seg = dl.payload_len;
+            lp.nfin = (x & kSiFin) ? 1u : 0u;
+            lp.ls = (x & kSiStart) ? n - 1 : kNoFrame;
+            lp.last = n - 1;
+            lp.bits = si_open(x) ? kPartOpen : 0u;
+        }
+        tot = part_combine(tot, lp);
+        sm.state_closed = (x & kSiClose) ? 1u : 0u;
+        sm.consumed_bytes = (uint64_t)(n - 1) * S + dl.wire_len;
+    }
+    sm.status = sm.first_status < 0 ? -1 : 0;
+    sm.payload_bytes = tot.pay;
+    sm.n_messages = tot.nfin;
+    sm.arena_bytes = 0;
+    sm.pending_bytes = (tot.last != kNoFrame && (tot.bits & kPartOpen)) ? tot.seg : 0;
+    *a.summary = sm;
 }
 
 // ------------------------------------------------------------------------------------
@@ -3768,6 +4054,9 @@ struct uvhttp_ws_gpu_engine {
     int build_small;           // emit shape for frames < 4 KiB (UVHTTP_WS_BUILD_SMALL, tuning)
     uint64_t build_frames_max; // frame-grouped LDS emit below this average frame (UVHTTP_WS_BUILD_FRAMES; 0 = off)
     int compact_mode;          // 0 automatic, 1 arena-driven gather, 2 wire-driven scatter
+    int sum_fast;              // summary-only stride decode in one payload pass (UVHTTP_WS_SUMMARY_FAST=0: off)
+    uvhttp_ws_frame_desc_t* dscr;  // descriptor scratch for d_desc == NULL calls
+    uint64_t dscr_cap;
     uint32_t* ctl;             // device control words (kCtl*), own allocation
     uint32_t faults_seen;      // ctl[kCtlFaults] at the last engine_sync
     uint32_t max_polls;        // look-back wait bound (UVHTTP_WS_MAX_POLLS: tests)
@@ -3875,6 +4164,8 @@ int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out) {
     e->fused_aux = 18;
     if (const char* fa = getenv("UVHTTP_WS_FUSED_AUX")) e->fused_aux = atoi(fa);
     e->fixup_blocks = 1024;
+    e->sum_fast = 1;
+    if (const char* sf = getenv("UVHTTP_WS_SUMMARY_FAST")) e->sum_fast = atoi(sf) != 0;
     if (const char* tl = getenv("UVHTTP_WS_TILE")) {  // payload tile shape "BxV" (A/B; 0x0 = auto)
         int tb = 0, tv = 0;
         if (sscanf(tl, "%dx%d", &tb, &tv) == 2) (void)uvhttp_ws_gpu_engine_set_tile(e, tb, tv);  // (validated)
@@ -3902,6 +4193,7 @@ void uvhttp_ws_gpu_engine_free(uvhttp_ws_gpu_engine_t* e) {
     if (e->bs_mem) (void)hipFree(e->bs_mem);
     if (e->wt_mem) (void)hipFree(e->wt_mem);
     if (e->wr_mem) (void)hipFree(e->wr_mem);
+    if (e->dscr) (void)hipFree(e->dscr);
     if (e->ctl) (void)hipFree(e->ctl);
     if (e->stamp_mem) (void)hipFree(e->stamp_mem);
     if (e->order_ev) (void)hipEventDestroy(e->order_ev);
@@ -3965,7 +4257,8 @@ int uvhttp_ws_gpu_engine_reserve(uvhttp_ws_gpu_engine_t* e, uint32_t max_frames,
     size_t off_bad = align_up(off_tiles + tl * sizeof(uint64_t), 256);
     size_t off_arena = align_up(off_bad + 16, 256);
     size_t off_recs = align_up(off_arena + at * sizeof(uint64_t), 256);
-    size_t bytes = align_up(off_recs + (size_t)fr * 16, 256);
+    size_t off_parts = align_up(off_recs + (size_t)fr * 16, 256);
+    size_t bytes = align_up(off_parts + ((size_t)fr / (kBlock * kScanFpt) + 2) * sizeof(TilePart), 256);
     int prev = 0;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(e->device);
@@ -3996,6 +4289,7 @@ int uvhttp_ws_gpu_engine_reserve(uvhttp_ws_gpu_engine_t* e, uint32_t max_frames,
     e->ws.spec_bad = e->ws.first_bad + 1;  // (off_bad reserves 16 bytes)
     e->ws.arena_first = (uint64_t*)(b + off_arena);
     e->ws.recs = b + off_recs;
+    e->ws.parts = b + off_parts;
     e->ws.ctl = e->ctl;
     e->ws_bytes = bytes;
     e->cap_frames = fr;
@@ -4301,9 +4595,41 @@ static uint64_t spec_payload(uint64_t stride) {
     return 0;
 }
 
+// Largest payload a delivered frame of `slot` wire bytes can declare: the shortest header
+// that encodes it (7-bit up to 125, 16-bit up to 65535 — non-minimal forms are legal,
+// src/uvhttp_websocket.c:133-185), plus the key a server requires
+static uint64_t max_payload_in(uint64_t slot, int32_t is_server) {
+    const uint64_t m = is_server ? 4u : 0u;
+    uint64_t best = 0;
+    if (slot >= 2 + m) best = slot - 2 - m < 125 ? slot - 2 - m : 125;
+    if (slot >= 4 + m) {
+        const uint64_t p = slot - 4 - m < 65535 ? slot - 4 - m : 65535;
+        best = p > best ? p : best;
+    }
+    if (slot >= 10 + m && slot - 10 - m > best) best = slot - 10 - m;
+    return best;
+}
+
+// the engine's descriptor scratch for calls that pass d_desc == NULL on a path that needs
+// descriptors internally (grown on demand; a captured call must not grow it)
+static uvhttp_ws_frame_desc_t* desc_scratch(uvhttp_ws_gpu_engine_t* e, uint32_t n) {
+    const uint64_t want = n ? n : 1;
+    if (e->dscr && e->dscr_cap >= want) return e->dscr;
+    if (e->capturing) return nullptr;
+    if (e->dscr) (void)hipFree(e->dscr);
+    e->dscr = nullptr;
+    e->dscr_cap = 0;
+    if (hipMalloc(&e->dscr, want * sizeof(uvhttp_ws_frame_desc_t)) != hipSuccess) {
+        e->dscr = nullptr;
+        return nullptr;
+    }
+    e->dscr_cap = want;
+    return e->dscr;
+}
+
 static int check_batch(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b,
-                       const void* d_desc, const void* d_summary) {
-    if (!e || !b || !d_desc || !d_summary) return UVHTTP_WS_GPU_EINVAL;
+                       const void* d_summary) {
+    if (!e || !b || !d_summary) return UVHTTP_WS_GPU_EINVAL;
     if (b->n_frames && !b->wire) return set_err(e, UVHTTP_WS_GPU_EINVAL, "wire is NULL", hipSuccess);
     if (((uintptr_t)b->wire) & 15u)
         return set_err(e, UVHTTP_WS_GPU_EINVAL, "wire must be 16-byte aligned", hipSuccess);
@@ -4317,7 +4643,7 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
                       uint64_t arena_cap, uvhttp_ws_frame_desc_t* d_desc,
                       uvhttp_ws_message_desc_t* d_msgs, uvhttp_ws_batch_summary_t* d_summary,
                       void* stream) {
-    int rc = check_batch(e, b, d_desc, d_summary);
+    int rc = check_batch(e, b, d_summary);
     if (rc) return rc;
     CallScope scope{e};
     call_begin(e, (hipStream_t)stream);
@@ -4378,19 +4704,51 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
         const uint64_t ft = (uint64_t)fb * fv * 16;
         const uint64_t f_tiles = (b->wire_len + ft - 1) / ft;
         const uint64_t f_max = (1ull << 24);
+        // Summary-only decode (d_desc == NULL): the payload pass also runs the fragment state
+        // machine (the previous frame decides it when every frame before a delivered one is a
+        // data frame — stride >= kSumMinStride — and no message can reach max_message_size: the
+        // bound below) and leaves one TilePart per tile; k_sum_tail writes the summary and undoes
+        // a failure.  No records, no k_plan, no descriptors.
+        const uint64_t lim = (uint64_t)(int64_t)b->max_message_size;
+        const uint64_t last_slot = b->wire_len - (uint64_t)(a.n - 1) * b->frame_stride;
+        const uint64_t msg_bound = (uint64_t)(a.n - 1) * max_payload_in(b->frame_stride, b->is_server) +
+                                   max_payload_in(last_slot, b->is_server);
+        const bool sum_fast = !d_desc && e->sum_fast && fb == 256 && fv == 4 && e->fused_aux == 18 &&
+                              b->frame_stride >= kSumMinStride && (lim == 0 || msg_bound <= lim);
+        if (sum_fast) {
+            a.recs = reinterpret_cast<FrameRec*>(e->ws.recs);  // (the info bytes: 1 per frame)
+            const int stk = timing_begin(e, s);
+            for (uint64_t tb = 0; tb < f_tiles; tb += f_max) {
+                const uint32_t grid_p = (uint32_t)((f_tiles - tb) < f_max ? (f_tiles - tb) : f_max);
+                hipLaunchKernelGGL((k_unmask_stride<256, 4, 18, true>), dim3(grid_p), dim3(256), 0, s, a,
+                                   e->ws, tb);
+            }
+            timing_end(e, stk, s);
+            const uint32_t n_parts = (a.n + kBlock * kScanFpt - 1) / (kBlock * kScanFpt);
+            hipLaunchKernelGGL(k_sum_scan, dim3(n_parts), dim3(kBlock), 0, s, a, e->ws);
+            hipLaunchKernelGGL(k_sum_tail, dim3(kSumTailGrid), dim3(kBlock), 0, s, a, e->ws, n_parts);
+            hipError_t hs = hipGetLastError();
+            if (prev != e->device) (void)hipSetDevice(prev);
+            if (hs != hipSuccess) return set_err(e, UVHTTP_WS_GPU_ELAUNCH, "launch", hs);
+            return UVHTTP_WS_GPU_OK;
+        }
+        if (!d_desc && !(d_desc = desc_scratch(e, a.n))) {
+            if (prev != e->device) (void)hipSetDevice(prev);
+            return set_err(e, UVHTTP_WS_GPU_ENOMEM, "descriptor scratch (reserve before capturing)", hipSuccess);
+        }
         const int ftk = timing_begin(e, s);
         for (uint64_t tb = 0; tb < f_tiles; tb += f_max) {
             const uint32_t grid_p = (uint32_t)((f_tiles - tb) < f_max ? (f_tiles - tb) : f_max);
 #define UVWS_FUSED(B, V)                                                                         \
     if (fb == B && fv == V) {                                                                    \
         if (B == 256 && V == 4 && e->fused_aux == 2)                                             \
-            hipLaunchKernelGGL((k_unmask_stride<256, 4, 2>), dim3(grid_p), dim3(B), 0, s, a, tb);  \
+            hipLaunchKernelGGL((k_unmask_stride<256, 4, 2>), dim3(grid_p), dim3(B), 0, s, a, e->ws, tb);  \
         else if (B == 256 && V == 4 && e->fused_aux == 0)                                        \
-            hipLaunchKernelGGL((k_unmask_stride<256, 4, 0>), dim3(grid_p), dim3(B), 0, s, a, tb);  \
+            hipLaunchKernelGGL((k_unmask_stride<256, 4, 0>), dim3(grid_p), dim3(B), 0, s, a, e->ws, tb);  \
         else if (B == 256 && V == 4 && e->fused_aux == 16)                                       \
-            hipLaunchKernelGGL((k_unmask_stride<256, 4, 16>), dim3(grid_p), dim3(B), 0, s, a, tb); \
+            hipLaunchKernelGGL((k_unmask_stride<256, 4, 16>), dim3(grid_p), dim3(B), 0, s, a, e->ws, tb); \
         else                                                                                     \
-            hipLaunchKernelGGL((k_unmask_stride<B, V>), dim3(grid_p), dim3(B), 0, s, a, tb);      \
+            hipLaunchKernelGGL((k_unmask_stride<B, V>), dim3(grid_p), dim3(B), 0, s, a, e->ws, tb); \
     } else
             UVWS_FUSED(64, 1) UVWS_FUSED(64, 2) UVWS_FUSED(64, 4) UVWS_FUSED(128, 1)
             UVWS_FUSED(128, 2) UVWS_FUSED(256, 1) UVWS_FUSED(256, 2) UVWS_FUSED(256, 4)
@@ -4420,6 +4778,12 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
         if (hf != hipSuccess) return set_err(e, UVHTTP_WS_GPU_ELAUNCH, "launch", hf);
         return UVHTTP_WS_GPU_OK;
     }
+    // every other path keeps per-frame descriptors internally: a caller without them gets the
+    // engine's scratch
+    if (!d_desc && !(d_desc = desc_scratch(e, a.n))) {
+        if (prev != e->device) (void)hipSetDevice(prev);
+        return set_err(e, UVHTTP_WS_GPU_ENOMEM, "descriptor scratch (reserve before capturing)", hipSuccess);
+    }
     // compact stride batches of small frames, speculatively: the payload pass
     // parses the headers (records) and writes every uniform frame's payload to f * P right
     // away; k_plan on the records checks that every delivered frame is where it went, and
@@ -4439,7 +4803,7 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
         const int stk = timing_begin(e, s);
         for (uint64_t tb = 0; tb < s_tiles; tb += (1ull << 24)) {
             const uint32_t grid_s = (uint32_t)((s_tiles - tb) < (1ull << 24) ? (s_tiles - tb) : (1ull << 24));
-            hipLaunchKernelGGL((k_unmask_stride<256, 4, kSpecCompact>), dim3(grid_s), dim3(256), 0, s, a, tb);
+            hipLaunchKernelGGL((k_unmask_stride<256, 4, kSpecCompact>), dim3(grid_s), dim3(256), 0, s, a, e->ws, tb);
         }
         timing_end(e, stk, s);
         launch_plan(e, a, a.n, d_desc, d_msgs, s);
@@ -4467,7 +4831,7 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
         const uint64_t r_tiles = (b->wire_len + kRt - 1) / kRt;
         for (uint64_t tb = 0; tb < r_tiles; tb += (1ull << 24)) {
             const uint32_t grid_r = (uint32_t)((r_tiles - tb) < (1ull << 24) ? (r_tiles - tb) : (1ull << 24));
-            hipLaunchKernelGGL((k_unmask_stride<256, 4, -1>), dim3(grid_r), dim3(256), 0, s, a, tb);
+            hipLaunchKernelGGL((k_unmask_stride<256, 4, -1>), dim3(grid_r), dim3(256), 0, s, a, e->ws, tb);
         }
     }
     launch_plan(e, a, a.n, d_desc, d_msgs, s);
