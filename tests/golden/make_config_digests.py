@@ -11,9 +11,12 @@ oracle/ws_oracle.c (oracle_gen_frames).  Per config this records
   payload  sha256 of the unmasked payload stream in frame order (what decode_compact's arena
            holds; for C4 the one reassembled 256 MiB message)
   decoded  sha256 of the whole wire after an in-place decode (headers and keys unchanged)
-C5 (8 388 608 frames, 512 GiB) records the payload digest of the frames sampled by
-tests/test_gpu_parity.py::test_config_c5_chunk (every 4099th frame of a 1 048 576-frame pass
-plus the last), concatenated in index order.
+C5 (8 388 608 frames, 512 GiB) records, for one resident pass of 1 048 576 frames (68.7 GB of
+wire; every rank's pass at N = 8 has this shape), the sha256 of the decoded wire of every
+4096-frame chunk ("decoded_chunks", in order) and the sha256 of those digests concatenated
+("decoded": a checksum of checksums), which tests/test_gpu_parity.py::test_config_c5_chunk
+compares byte for byte through; and the payload digest of a sample of frames (every 4099th plus
+the last), kept for the CPU test.
 
 Run:  python tests/golden/make_config_digests.py   (rewrites config_digests.json here)
 """
@@ -72,12 +75,37 @@ def c5_digest():
             "payload_sample": h.hexdigest()}
 
 
+C5_CHUNK_FRAMES = 4096
+
+
+def c5_chunk_digest(k):
+    """sha256 of the oracle-decoded wire of C5 pass frames [4096 k, 4096 (k + 1))"""
+    n, plen = C5
+    L = _oracle.load()
+    stride = int(L.oracle_gen_stride(plen))
+    ow, _ = _oracle.gen_frames(n, plen, SEED, force_keys=True, first=k * C5_CHUNK_FRAMES,
+                               count=C5_CHUNK_FRAMES, total=n)
+    L.oracle_unmask_frames(_oracle._ptr(ow), C5_CHUNK_FRAMES, stride)
+    return hashlib.sha256(ow).hexdigest()
+
+
+def c5_chunk_digests(threads=8):
+    """every chunk's digest, computed on `threads` threads (the oracle's C calls and sha256 run
+    outside the GIL)"""
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(threads) as ex:
+        return list(ex.map(c5_chunk_digest, range(C5[0] // C5_CHUNK_FRAMES)))
+
+
 def main():
     out = {"seed": SEED, "generator": "oracle/ws_oracle.c oracle_gen_frames (force_keys=1)"}
     for name, (n, plen, frag) in CONFIGS.items():
         out[name] = config_digests(n, plen, frag)
         print(name, out[name], flush=True)
     out["c5_pass"] = c5_digest()
+    chunks = c5_chunk_digests()
+    out["c5_pass"].update({"chunk_frames": C5_CHUNK_FRAMES, "decoded_chunks": chunks,
+                           "decoded": hashlib.sha256("".join(chunks).encode()).hexdigest()})
     with open(os.path.join(HERE, "config_digests.json"), "w") as fh:
         json.dump(out, fh, indent=1)
         fh.write("\n")

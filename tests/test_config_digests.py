@@ -36,8 +36,21 @@ def test_oracle_reproduces_digests(cfg):
 
 
 def test_oracle_reproduces_c5_sample():
-    assert _mk().c5_digest() == DIG["c5_pass"]
+    want = {k: DIG["c5_pass"][k] for k in ("frames", "payload_len", "sample", "payload_sample")}
+    assert _mk().c5_digest() == want
     _ = _oracle  # oracle library built by the fixture chain
+
+
+def test_oracle_reproduces_c5_chunks():
+    """three of the 256 chunk digests of the whole C5 pass (the GPU test checks all of them)"""
+    import hashlib
+    m = _mk()
+    c5 = DIG["c5_pass"]
+    chunks = c5["decoded_chunks"]
+    assert len(chunks) * c5["chunk_frames"] == c5["frames"]
+    assert hashlib.sha256("".join(chunks).encode()).hexdigest() == c5["decoded"]
+    for k in (0, 127, len(chunks) - 1):
+        assert m.c5_chunk_digest(k) == chunks[k], k
 
 
 def _sha_dev(t, nbytes, chunk=256 << 20):

@@ -506,7 +506,10 @@ def _check_slot(pipe, slot, wire, offs):
 
 def test_config_c5_chunk(torch, eng):
     """One C5 pass: 1 048 576 x 64 KiB frames (68.7 GB of wire, > 2^32 work-items of payload
-    tiles).  Summary and statuses exact; sampled frames checked byte for byte."""
+    tiles; each rank's pass at N = 8).  Summary and statuses exact; sampled frames checked byte
+    for byte against the oracle here, and EVERY byte of the decoded wire through the sha256 of
+    each 4096-frame chunk, against the oracle's digests committed in
+    tests/golden/config_digests.json (tests/golden/make_config_digests.py)."""
     import uvhttp_amd as U
     n, plen = 1048576, 65536
     stride = U.gen_frame_stride(plen)
@@ -524,6 +527,22 @@ def test_config_c5_chunk(torch, eng):
         ow, _ = _oracle.gen_frames(n, plen, SEED, force_keys=True, first=i, count=1, total=n)
         _oracle.load().oracle_unmask_frames(_oracle._ptr(ow), 1, stride)
         assert np.array_equal(got, ow), i
+    import hashlib
+    import json
+    import os
+    from concurrent.futures import ThreadPoolExecutor
+    with open(os.path.join(os.path.dirname(__file__), "golden", "config_digests.json")) as fh:
+        c5 = json.load(fh)["c5_pass"]
+    cf = c5["chunk_frames"]
+    assert c5["frames"] == n and len(c5["decoded_chunks"]) * cf == n
+
+    def chunk_digest(k):  # (the copy and sha256 run outside the GIL)
+        return hashlib.sha256(d[k * cf * stride:(k + 1) * cf * stride].cpu().numpy()).hexdigest()
+    with ThreadPoolExecutor(8) as ex:
+        got = list(ex.map(chunk_digest, range(n // cf)))
+    bad = [k for k, (g, w) in enumerate(zip(got, c5["decoded_chunks"])) if g != w]
+    assert not bad, f"decoded chunks differ from the oracle's: {bad[:8]}"
+    assert hashlib.sha256("".join(got).encode()).hexdigest() == c5["decoded"]
     del d
     torch.cuda.empty_cache()
 

@@ -5289,6 +5289,9 @@ struct uvhttp_ws_gpu_pipeline {
     uvhttp_ws_gpu_engine_t* eng;  // one workspace: the decodes run in order on `cs`
     hipStream_t up, cs;
     PipeSlot* slots;
+    int ahead;        // an upload starts once the slot submitted `ahead` submissions earlier is done
+    int recent[16];   // slots of the latest submissions (ring)
+    uint64_t n_sub;   // submissions so far
 };
 
 void uvhttp_ws_gpu_pipeline_free(uvhttp_ws_gpu_pipeline_t* p) {
@@ -5329,6 +5332,8 @@ int uvhttp_ws_gpu_pipeline_create(int device, int depth, uint64_t slot_bytes,
     p->depth = depth;
     p->slot_bytes = slot_bytes;
     p->slot_frames = slot_frames;
+    p->ahead = 0;
+    if (const char* pa = getenv("UVHTTP_WS_PIPE_AHEAD")) p->ahead = atoi(pa);
     p->slots = (PipeSlot*)calloc((size_t)depth, sizeof(PipeSlot));
     if (!p->slots) {
         free(p);
@@ -5389,7 +5394,9 @@ int uvhttp_ws_gpu_pipeline_submit(uvhttp_ws_gpu_pipeline_t* p, int slot, uint64_
     (void)hipSetDevice(p->device);
     // upload stream: the slot's bytes (its previous round was waited for, so d_wire is free)
     hipError_t h = hipSuccess;
-    if (wire_len) h = hipMemcpyAsync(s.d_wire, s.h_wire, wire_len, hipMemcpyHostToDevice, p->up);
+    if (p->ahead > 0 && p->n_sub >= (uint64_t)p->ahead)
+        h = hipStreamWaitEvent(p->up, p->slots[p->recent[(p->n_sub - p->ahead) % 16]].done_ev, 0);
+    if (h == hipSuccess && wire_len) h = hipMemcpyAsync(s.d_wire, s.h_wire, wire_len, hipMemcpyHostToDevice, p->up);
     if (h == hipSuccess && use_offsets && n_frames)
         h = hipMemcpyAsync(s.d_off, s.h_off, (size_t)n_frames * 8, hipMemcpyHostToDevice, p->up);
     if (h == hipSuccess) h = hipEventRecord(s.up_ev, p->up);
@@ -5417,7 +5424,11 @@ int uvhttp_ws_gpu_pipeline_submit(uvhttp_ws_gpu_pipeline_t* p, int slot, uint64_
                            p->cs);
     if (!rc && h == hipSuccess) h = hipEventRecord(s.done_ev, p->cs);
     if (!rc && h != hipSuccess) rc = UVHTTP_WS_GPU_ELAUNCH;
-    if (!rc) s.busy = 1;
+    if (!rc) {
+        s.busy = 1;
+        p->recent[p->n_sub % 16] = slot;
+        p->n_sub++;
+    }
     (void)hipSetDevice(prev);
     return rc;
 }
