@@ -3035,9 +3035,7 @@ __device__ inline void walk_wave(const WalkArgs& w, uint32_t s, uint8_t* ring) {
             // a final fragment) stop after their first frame; anything else leaves for the
             // general code.  All lanes compute with vector registers; each step's outcome is
             // made uniform by readfirstlane.
-            if (cur == ~0ull || c.grow_fail) return;
-            uint64_t cur_rel = cur - st.begin / kWalkBlk;  // ring block, stream-relative
-            const uint32_t off0 = (uint32_t)(st.begin % kWalkBlk), par0 = (uint32_t)((st.begin / kWalkBlk) & 1);
+            if (c.grow_fail) return;
             const uint32_t end32 = (uint32_t)c.end;
             const uint64_t mf = (uint64_t)(int64_t)st.max_frame_size;
             const uint64_t lim = (uint64_t)(int64_t)st.max_message_size;
@@ -3059,19 +3057,12 @@ __device__ inline void walk_wave(const WalkArgs& w, uint32_t s, uint8_t* ring) {
                       plen > mf || (plen >> 31);  // (a length of 2^31 or more: general code)
                 wl = need + 4u * m + (uint32_t)plen;
             };
-            auto parse_ring = [&](uint32_t p, uint32_t& b0, uint32_t& wl, uint64_t& plen, bool& bad) {
-                const uint32_t off = off0 + p;
-                const uint32_t r = (((par0 + off / kWalkBlk) & 1) * kWalkBlk) + off % kWalkBlk;
-                uint32_t hb[10];
-#pragma unroll
-                for (int q = 0; q < 10; ++q) hb[q] = ring[r + q];
-                decode(hb, b0, wl, plen, bad);
-            };
-            // (also the frame's record for k_stream_desc: key and header bytes, kNoRec for a
-            // 64-bit length)
-            auto parse_global = [&](uint64_t p, uint32_t& b0, uint32_t& wl, uint64_t& plen, bool& bad,
-                                    uint2& rec) {
-                const u32x4 v = load16_at(w.wire, w.wire_len, st.begin + p);
+            // a header's 16 bytes (issued apart from the decode, so several are in flight), then
+            // its fields and the frame's record for k_stream_desc: key and header bytes, kNoRec
+            // for a 64-bit length
+            auto fetch = [&](uint64_t p) { return load16_at(w.wire, w.wire_len, st.begin + p); };
+            auto decode16 = [&](const u32x4& v, uint32_t& b0, uint32_t& wl, uint64_t& plen, bool& bad,
+                                uint2& rec) {
                 const uint32_t x[4] = {v.x, v.y, v.z, v.w};
                 uint32_t hb[10];
 #pragma unroll
@@ -3082,6 +3073,10 @@ __device__ inline void walk_wave(const WalkArgs& w, uint32_t s, uint8_t* ring) {
                 rec = code < 127 ? uint2{(hb[1] & 0x80) ? key : 0u, hb[0] | (hb[1] << 8) | ((uint32_t)plen << 16)}
                                  : uint2{0u, kNoRec};
             };
+            // kG groups of 64 speculative frames per step: lane l of group g takes frame
+            // 1 + l + 64 g, so one step decides up to 64 kG frames with kG loads in flight per
+            // lane (64 per step measured 40 us for C4's 4096 x 256 frames: four dependent gathers)
+            constexpr uint32_t kG = 4, kRun = 64 * kG;
             uint32_t wlp = 0;          // the previous step's frame length
             bool have0 = false;        // frame 0's header carried from the previous step
             uint32_t cb0 = 0, cwl = 0;  // (its fields)
@@ -3097,23 +3092,15 @@ __device__ inline void walk_wave(const WalkArgs& w, uint32_t s, uint8_t* ring) {
                 if (have0) {
                     b00 = cb0, wl0 = cwl, plen0 = cplen, bad0 = cbad, rec0 = crec;
                 } else {
-                    // frame 0 from the ring: header in the ring's current block (or, after a
-                    // run, in the next one: the ring advances here), else the general code
-                    const uint32_t off = off0 + pos;
-                    if (off / kWalkBlk == cur_rel + 1) {
-                        walk_store_block(ring, cur + 2, pf);
-                        walk_load_block(w, cur + 3, pf);
-                        ++cur;
-                        ++cur_rel;
-                        wave_sync_lds();
-                    }
-                    if (off / kWalkBlk != cur_rel) break;  // (uniform)
-                    parse_ring(pos, b00, wl0, plen0, bad0);
+                    // frame 0 straight from global memory (every lane the same 16 bytes): the
+                    // general code's LDS ring of 4 KiB blocks is loaded only when it runs
+                    decode16(fetch(pos), b00, wl0, plen0, bad0, rec0);
                     b00 = __builtin_amdgcn_readfirstlane(b00);
                     wl0 = __builtin_amdgcn_readfirstlane(wl0);
                     plen0 = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(plen0 >> 32)) << 32) |
                             __builtin_amdgcn_readfirstlane((uint32_t)plen0);
                     bad0 = __builtin_amdgcn_readfirstlane((uint32_t)bad0) != 0;
+                    rec0 = uint2{__builtin_amdgcn_readfirstlane(rec0.x), __builtin_amdgcn_readfirstlane(rec0.y)};
                 }
                 const uint32_t op0 = b00 & 0x0F, fin0 = b00 >> 7;
                 const bool data0 = op0 <= 2;
@@ -3125,40 +3112,80 @@ __device__ inline void walk_wave(const WalkArgs& w, uint32_t s, uint8_t* ring) {
                 const uint32_t kind = !data0 ? 0u : (op0 != 0 && fin0) ? 1u : (op0 == 0 && !fin0) ? 2u : 3u;
                 uint32_t n = 1;
                 have0 = false;
-                uint2 recl{0u, kNoRec};  // lane l: the record of frame l + 1 (its header, parsed)
+                uint2 recl[kG];  // lane l of group g: the record of frame 1 + l + 64 g
+#pragma unroll
+                for (uint32_t g = 0; g < kG; ++g) recl[g] = uint2{0u, kNoRec};
                 if (kind != 3 && wl0 == wlp) {
-                    // lane l speculates on frame l + 1 (frames 1 .. 64), so the frame after the
-                    // run — the next step's frame 0 — was always read, even after a full run
-                    const uint32_t f = lane + 1;
-                    const uint64_t pl = (uint64_t)pos + (uint64_t)f * wl0;
-                    uint32_t b0l = 0, wll = 0;
-                    uint64_t plenl = 0;
-                    bool badl = true;
-                    const bool hdr_in = pl + 10 <= end32;
-                    if (hdr_in) parse_global(pl, b0l, wll, plenl, badl, recl);
-                    const bool okl = hdr_in && pl + wl0 <= end32 && !badl && b0l == b00 && wll == wl0 &&
-                                     plenl == plen0 &&
-                                     (kind != 2 || lim == 0 || acc + (uint64_t)(f + 1) * plen0 <= lim);
-                    const uint64_t good = __ballot(okl);
-                    // frame 0 plus the leading accepted frames, at most 64 per step
-                    const uint32_t m = ~good == 0 ? 64u : (uint32_t)__builtin_ctzll(~good);
-                    n = __builtin_amdgcn_readfirstlane(m + 1 < 64u ? m + 1 : 64u);
-                    // frame n (the first not taken) is the next step's frame 0; lane n - 1 read it
-                    const uint32_t hin = __builtin_amdgcn_readlane((uint32_t)hdr_in, n - 1);
-                    if (hin) {
+                    // speculation: frames 1 .. kRun all have frame 0's length, so the frame after
+                    // the run — the next step's frame 0 — was always read, even after a full run
+                    u32x4 hv[kG];
+                    bool hin[kG];
+#pragma unroll
+                    for (uint32_t g = 0; g < kG; ++g) {  // every load first
+                        const uint64_t pl = (uint64_t)pos + (uint64_t)(lane + 1 + 64 * g) * wl0;
+                        hin[g] = pl + 10 <= end32;
+                        hv[g] = hin[g] ? fetch(pl) : u32x4{0u, 0u, 0u, 0u};
+                    }
+                    uint64_t good[kG];
+                    uint32_t b0l[kG], wll[kG];
+                    uint64_t plenl[kG];
+                    bool badl[kG];
+#pragma unroll
+                    for (uint32_t g = 0; g < kG; ++g) {
+                        const uint32_t f = lane + 1 + 64 * g;
+                        const uint64_t pl = (uint64_t)pos + (uint64_t)f * wl0;
+                        b0l[g] = 0, wll[g] = 0, plenl[g] = 0, badl[g] = true;
+                        if (hin[g]) decode16(hv[g], b0l[g], wll[g], plenl[g], badl[g], recl[g]);
+                        const bool okl = hin[g] && pl + wl0 <= end32 && !badl[g] && b0l[g] == b00 &&
+                                         wll[g] == wl0 && plenl[g] == plen0 &&
+                                         (kind != 2 || lim == 0 || acc + (uint64_t)(f + 1) * plen0 <= lim);
+                        good[g] = __ballot(okl);
+                    }
+                    // frame 0 plus the leading accepted frames, at most kRun per step
+                    uint32_t m = 0;
+#pragma unroll
+                    for (uint32_t g = 0; g < kG; ++g) {
+                        if (m == 64 * g) m += ~good[g] == 0 ? 64u : (uint32_t)__builtin_ctzll(~good[g]);
+                    }
+                    n = __builtin_amdgcn_readfirstlane(m + 1 < kRun ? m + 1 : kRun);
+                    // frame n (the first not taken) is the next step's frame 0: lane (n - 1) % 64
+                    // of group (n - 1) / 64 read it
+                    const uint32_t gn = (n - 1) / 64, ln = (n - 1) % 64;
+                    uint32_t hsel = 0, b0s = 0, wls = 0, pl0 = 0, pl1 = 0, bads = 0, rx = 0, ry = 0;
+#pragma unroll
+                    for (uint32_t g = 0; g < kG; ++g) {
+                        if (g == gn) {  // (uniform)
+                            hsel = __builtin_amdgcn_readlane((uint32_t)hin[g], ln);
+                            b0s = __builtin_amdgcn_readlane(b0l[g], ln);
+                            wls = __builtin_amdgcn_readlane(wll[g], ln);
+                            pl1 = __builtin_amdgcn_readlane((uint32_t)(plenl[g] >> 32), ln);
+                            pl0 = __builtin_amdgcn_readlane((uint32_t)plenl[g], ln);
+                            bads = __builtin_amdgcn_readlane((uint32_t)badl[g], ln);
+                            rx = __builtin_amdgcn_readlane(recl[g].x, ln);
+                            ry = __builtin_amdgcn_readlane(recl[g].y, ln);
+                        }
+                    }
+                    if (hsel) {
                         have0 = true;
-                        cb0 = __builtin_amdgcn_readlane(b0l, n - 1);
-                        cwl = __builtin_amdgcn_readlane(wll, n - 1);
-                        cplen = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(plenl >> 32), n - 1) << 32) |
-                                __builtin_amdgcn_readlane((uint32_t)plenl, n - 1);
-                        cbad = __builtin_amdgcn_readlane((uint32_t)badl, n - 1) != 0;
-                        crec = uint2{__builtin_amdgcn_readlane(recl.x, n - 1), __builtin_amdgcn_readlane(recl.y, n - 1)};
+                        cb0 = b0s, cwl = wls, cplen = ((uint64_t)pl1 << 32) | pl0, cbad = bads != 0;
+                        crec = uint2{rx, ry};
                     }
                 }
-                // lane l emits frame l: its record is lane l - 1's (frame 0's is the carried one)
-                uint2 rece{__shfl_up(recl.x, 1, 64), __shfl_up(recl.y, 1, 64)};
-                if (lane == 0) rece = rec0;
-                emit_lane((uint64_t)pos + (uint64_t)lane * wl0, cnt + lane, lane < n, rece);
+                // lane l emits frames l + 64 g: the record of frame j >= 1 is lane (j - 1) % 64
+                // of group (j - 1) / 64 (frame 0's is the carried one)
+                uint2 prevg = rec0;  // group g - 1's lane 63 (frame 64 g's record)
+#pragma unroll
+                for (uint32_t g = 0; g < kG; ++g) {
+                    if (64 * g >= n) break;  // (uniform)
+                    const uint32_t j = 64 * g + lane;
+                    // record of frame j = recl[(j - 1) / 64] at lane (j - 1) % 64: for lane
+                    // l >= 1 that is group g's lane l - 1, for lane 0 group g - 1's lane 63 (or,
+                    // frame 0, the carried one) — the shuffle runs on every lane
+                    const uint2 up{__shfl_up(recl[g].x, 1, 64), __shfl_up(recl[g].y, 1, 64)};
+                    const uint2 rj = lane ? up : prevg;
+                    emit_lane((uint64_t)pos + (uint64_t)j * wl0, cnt + j, j < n, rj);
+                    prevg = uint2{__builtin_amdgcn_readlane(recl[g].x, 63), __builtin_amdgcn_readlane(recl[g].y, 63)};
+                }
                 if (kind == 2) {
                     acc += (uint64_t)n * plen0;
                 } else if (kind == 3) {  // one frame: a start without FIN or a final fragment
