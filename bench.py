@@ -387,6 +387,9 @@ class GpuWorkload:
         spec_max = int(os.environ.get("UVHTTP_WS_SPEC_MAX", "2560") or 2560)
         if mode == "compact" and os.environ.get("UVHTTP_WS_SPEC", "1") != "0" and 64 <= stride <= spec_max:
             self.kernel = "k_unmask_stride (speculative compact pass)"
+            if self.no_desc and stride >= 140 and os.environ.get("UVHTTP_WS_SUMMARY_FAST", "1") != "0" \
+                    and (mm == 0 or n * (stride - 8) <= mm):
+                self.kernel = "k_unmask_stride (summary-only speculative compact pass)"
         if mode.startswith("build"):
             # send side: frame n payloads of the config (server echo: unmasked; client: masked)
             import numpy as np

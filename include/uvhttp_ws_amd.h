@@ -381,7 +381,15 @@ int uvhttp_ws_gpu_engine_read_stamps(uvhttp_ws_gpu_engine_t* eng, uvhttp_ws_gpu_
 /* In-place decode: parse + validate every frame, run the fragment state machine, then
  * unmask the payload of every delivered frame in place in batch->wire (the reference
  * unmasks inside recv_buffer, src/uvhttp_websocket.c:937-947).  d_desc (n_frames
- * entries) and d_summary are device pointers.  Asynchronous on `stream`. */
+ * entries) and d_summary are device pointers.  Asynchronous on `stream`.
+ * d_desc may be NULL (summary-only decode): the wire and d_summary come out exactly as with
+ * descriptors, and no per-frame output is written.  A fixed-stride batch of small frames
+ * (stride >= 140 bytes, every frame able to fit the message limit) then runs as one payload
+ * pass writing an info byte per frame plus two short kernels (fragment state machine and
+ * summary; after a failure the frames from it on are masked again); any other batch is decoded
+ * into descriptors in engine scratch (grown on demand, so reserve or run one uncaptured call
+ * of the shape before capturing a graph).  For a caller that only needs "every frame delivered"
+ * or the first failure, e.g. a server that re-walks delivered frames on the host. */
 int uvhttp_ws_gpu_decode_inplace(uvhttp_ws_gpu_engine_t* eng, const uvhttp_ws_batch_t* batch,
                                  uvhttp_ws_frame_desc_t* d_desc,
                                  uvhttp_ws_batch_summary_t* d_summary, void* stream);
@@ -393,7 +401,8 @@ int uvhttp_ws_gpu_decode_inplace(uvhttp_ws_gpu_engine_t* eng, const uvhttp_ws_ba
  * wire.  d_msgs needs room for n_frames entries; arena_cap must cover the data payload.
  * Arena bytes past summary->arena_bytes (up to arena_cap) are scratch: a fixed-stride batch is
  * decoded speculatively, and when it fails part-way the payloads of frames after the failure
- * may have been written there. */
+ * may have been written there.  d_desc may be NULL (descriptors then go to engine scratch;
+ * the arena, d_msgs and d_summary are the same). */
 int uvhttp_ws_gpu_decode_compact(uvhttp_ws_gpu_engine_t* eng, const uvhttp_ws_batch_t* batch,
                                  uint8_t* d_arena, uint64_t arena_cap,
                                  uvhttp_ws_frame_desc_t* d_desc,
@@ -532,7 +541,10 @@ int uvhttp_ws_gpu_build_frames(uvhttp_ws_gpu_engine_t* eng, const uint8_t* d_src
  *   H2D(wire[0, wire_len)) -> decode_inplace -> D2H(wire, desc, summary)
  * and returns at once; wait() blocks until the slot's decoded bytes, descriptors and
  * summary are back in pinned host memory (the in-place contract: delivered payloads are
- * unmasked inside the slot buffer). */
+ * unmasked inside the slot buffer).  At most three submissions are in flight: submit() first
+ * waits for the submission three back to finish, so depth 4 and up give the caller more slots
+ * to fill while three are in flight (with more queued, the copies ran at 22-27 instead of 44
+ * GiB/s on MI355X). */
 typedef struct uvhttp_ws_gpu_pipeline uvhttp_ws_gpu_pipeline_t;
 int uvhttp_ws_gpu_pipeline_create(int device, int depth, uint64_t slot_bytes,
                                   uint32_t slot_frames, uvhttp_ws_gpu_pipeline_t** out);

@@ -342,7 +342,7 @@ def _full_config(torch, eng, n, plen, fragmented, compact, chunk=4096, no_desc=F
     if compact:
         arena = torch.empty(n * plen + 64, dtype=torch.uint8, device="cuda")
         desc, msgs, summ = eng.decode_compact(d, n, arena, stride=stride, max_message_size=mm,
-                                              wire_len=wl)
+                                              wire_len=wl, no_desc=no_desc)
     else:
         desc, summ = eng.decode_inplace(d, n, stride=stride, max_message_size=mm, wire_len=wl,
                                         no_desc=no_desc)
@@ -389,14 +389,16 @@ def test_config_c4_full(torch, eng, compact):
     _full_config(torch, eng, 1048576, 256, True, compact, chunk=131072)
 
 
+@pytest.mark.parametrize("compact", [False, True])
 @pytest.mark.parametrize("cfg", ["c2", "c4"])
-def test_config_full_summary_only(torch, eng, cfg):
-    """d_desc = NULL at full size: C4 takes the one-pass summary-only decode, C2 (4 KiB frames,
-    above the fused range) the descriptor path with the engine's scratch"""
+def test_config_full_summary_only(torch, eng, cfg, compact):
+    """d_desc = NULL at full size: C4 takes the summary-only decode (in place: one payload pass
+    + scan + tail; compact: the speculative pass + scan + tail + message table), C2 (4 KiB
+    frames, above the fused range) the descriptor paths with the engine's scratch"""
     if cfg == "c4":
-        _full_config(torch, eng, 1048576, 256, True, False, chunk=131072, no_desc=True)
+        _full_config(torch, eng, 1048576, 256, True, compact, chunk=131072, no_desc=True)
     else:
-        _full_config(torch, eng, 65536, 4096, False, False, no_desc=True)
+        _full_config(torch, eng, 65536, 4096, False, compact, no_desc=True)
 
 
 def test_config_c4_default_limit_rejects(torch, eng):
@@ -449,15 +451,17 @@ def test_tile_shapes_identical(torch, eng, shape):
         eng.set_tile(0, 0)
 
 
-def test_pipeline_and_delivery(torch, eng):
+@pytest.mark.parametrize("depth", [3, 5, 8])
+def test_pipeline_and_delivery(torch, eng, depth):
     """Host-memory pipeline: batches written into pinned slots, decoded on the device with
     overlapped copies, delivered to a connection; bytes, statuses, summaries and the callback
-    transcript equal the oracle's per-frame process_data."""
+    transcript equal the oracle's per-frame process_data.  Depths above 3 keep three
+    submissions in flight (submit waits for the one three back)."""
     import uvhttp_amd as U
-    pipe = U.GpuPipeline(0, depth=3, slot_bytes=4 << 20, slot_frames=4096)
+    pipe = U.GpuPipeline(0, depth=depth, slot_bytes=4 << 20, slot_frames=4096)
     rng = random.Random(4242)
     batches = []
-    for b in range(7):
+    for b in range(7 + depth):
         sizes = [[0, 5, 125, 126, 1000], [4096, 20000], [65536, 70000]][b % 3]
         n = rng.choice([1, 40, 300]) if b % 3 == 0 else rng.choice([1, 20, 50])
         wire, offs = _rand_batch(rng, n, sizes, p_ctrl=0.1, p_frag=0.3,
@@ -466,7 +470,7 @@ def test_pipeline_and_delivery(torch, eng):
         batches.append((wire, offs))
     inflight = {}
     for k, (wire, offs) in enumerate(batches):
-        slot = k % 3
+        slot = k % depth
         if slot in inflight:
             _check_slot(pipe, *inflight.pop(slot))
         buf = pipe.buffer(slot)

@@ -252,7 +252,9 @@ constexpr int kCtlEpoch = 0;     // device epoch of graph-captured calls
 constexpr int kCtlDone = 1;      // k_epoch's last-block counter
 constexpr int kCtlFaultEp = 2;   // epoch of the latest call whose look-back gave up
 constexpr int kCtlFaults = 3;    // running count of such calls (engine_sync compares it)
-constexpr int kCtlWords = 4;
+constexpr int kCtlGate = 4;      // epoch of the latest summary-only compact call whose speculation
+                                 // failed (its k_plan + k_spec_fix then run, k_sum_msgs does not)
+constexpr int kCtlWords = 5;
 // epochs: host-issued tags run 1 .. kMaxHostEpoch, device-issued ones (captured calls)
 // kMaxHostEpoch + 1 .. kMaxEpoch, so a replayed graph never meets a tag a host call left
 constexpr uint32_t kMaxHostEpoch = kMaxEpoch / 2;
@@ -302,12 +304,13 @@ struct alignas(16) TilePart {
     uint32_t nfin;  // data frames with FIN: completed messages
     uint32_t ls;    // latest start (non-CONT data frame), kNoFrame if none
     uint32_t last;  // latest data frame, kNoFrame if none
-    uint32_t bits;  // kPartOpen: `last` leaves a message open; kPartClosed: a CLOSE was delivered
+    uint32_t bits;  // kPartOpen: `last` leaves a message open; kPartClosed: a CLOSE was delivered;
+                    // kPartBin: `ls` is a BINARY start (compact: the message's opcode)
     uint32_t ff;    // the run's first failing frame (the run stops before it), kNoFrame if none
     uint32_t pad[3];
 };
 static_assert(sizeof(TilePart) == 48, "three 16-byte words");
-constexpr uint32_t kPartOpen = 1u, kPartClosed = 2u;
+constexpr uint32_t kPartOpen = 1u, kPartClosed = 2u, kPartBin = 4u;
 
 __device__ __host__ inline TilePart part_identity() {
     TilePart p;
@@ -334,7 +337,8 @@ __device__ __host__ inline TilePart part_combine(const TilePart& a, const TilePa
     r.ls = b.ls != kNoFrame ? b.ls : a.ls;
     r.seg = b.ls != kNoFrame ? b.seg : a.seg + b.seg;
     r.last = b.last != kNoFrame ? b.last : a.last;
-    r.bits = ((b.last != kNoFrame ? b.bits : a.bits) & kPartOpen) | ((a.bits | b.bits) & kPartClosed);
+    r.bits = ((b.last != kNoFrame ? b.bits : a.bits) & kPartOpen) | ((a.bits | b.bits) & kPartClosed) |
+             ((b.ls != kNoFrame ? b.bits : a.bits) & kPartBin);
     return r;
 }
 
@@ -367,6 +371,8 @@ struct BatchArgs {
     uint64_t* stamp;         // device-side kernel stamps (diagnostics), or null
     uint64_t spec_P;         // compact stride batch, speculative pass: the uniform payload length
                              // (frame i's payload at arena offset i * spec_P); 0 = none
+    uint32_t gate;           // k_plan / k_spec_fix run only when ws.ctl[kCtlGate] holds this call's
+                             // epoch (the summary-only compact decode's fallback)
 };
 
 // ------------------------------------------------------------------------------------
@@ -1029,6 +1035,7 @@ template <int FPT, int NT = kBlock, bool REC = false>
 __global__ __launch_bounds__(NT) void k_plan(BatchArgs a, uvhttp_ws_frame_desc_t* desc,
                                                  uvhttp_ws_message_desc_t* msgs, Workspace ws) {
     resolve_epoch(a, ws);
+    if (a.gate && ws.ctl[kCtlGate] != a.epoch) return;  // (summary-only compact: speculation held)
     StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_PLAN);
     __shared__ uint32_t s_ticket;
     if (threadIdx.x == 0) {
@@ -1656,15 +1663,19 @@ __device__ inline bool si_open(uint32_t x) {
     return (x & kSiData) && !(x & kSiFin) && !((x & kSiStart) && (x & kSiZero));
 }
 // the one byte per frame the summary-only payload pass leaves for k_sum_scan: locally valid,
-// data frame, FIN, start, leaves a message open, and the header + key size class (kHm)
-constexpr uint32_t kI8Ok = 1u, kI8Data = 2u, kI8Fin = 4u, kI8Start = 8u, kI8Open = 16u, kI8HmShift = 5;
+// data frame, FIN, start, BINARY (a compact decode's message opcode), and the header + key size
+// class (kHm)
+constexpr uint32_t kI8Ok = 1u, kI8Data = 2u, kI8Fin = 4u, kI8Start = 8u, kI8Bin = 16u, kI8HmShift = 5;
+// a data frame that is not the batch's last leaves a message open iff it has no FIN: its payload
+// fills a slot of >= kSumMinStride bytes, so it is never a zero-length start (si_open)
+__device__ inline bool i8_open(uint32_t x) { return (x & kI8Data) && !(x & kI8Fin); }
 __device__ inline uint8_t info8_of(const uvhttp_ws_frame_desc_t& d) {
     const uint32_t x = sum_info(d);
     const uint32_t hm = x >> kSiHmShift;
     const uint32_t c = hm == 2 ? 0u : hm == 4 ? 1u : hm == 6 ? 2u : hm == 8 ? 3u : hm == 10 ? 4u : 5u;
     return (uint8_t)(((x & kSiOk) ? kI8Ok : 0u) | ((x & kSiData) ? kI8Data : 0u) |
                      ((x & kSiFin) ? kI8Fin : 0u) | ((x & kSiStart) ? kI8Start : 0u) |
-                     (si_open(x) ? kI8Open : 0u) | (c << kI8HmShift));
+                     (d.opcode == 2 ? kI8Bin : 0u) | (c << kI8HmShift));
 }
 // add_mask on tile-relative int32 positions (vector at r, payload [ps, pe))
 __device__ inline void add_mask_rel(u32x4& m, int32_t r, int32_t ps, int32_t pe, uint32_t key) {
@@ -2012,22 +2023,28 @@ __device__ TilePart block_reduce_parts(const TilePart& v) {
 // load — left one wave per SIMD walking its frames serially: 10.4 us on C4; rocprofv3, r05k)
 constexpr uint32_t kScanFpt = 4;
 
+// a frame the speculative compact pass placed at f * P: a data frame whose header + key take
+// the slot's D = stride - P bytes (the payload then fills the rest: P bytes)
+__device__ inline bool i8_uniform(uint32_t x, uint64_t D) {
+    return (x & kI8Data) && kHm[x >> kI8HmShift] == D;
+}
+
+template <bool COMPACT>
 __global__ __launch_bounds__(kBlock) void k_sum_scan(BatchArgs a, Workspace ws) {
     resolve_epoch(a, ws);
     StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_PLAN);
     const uint32_t n = a.n;
     const uint64_t S = a.frame_stride;
+    const uint64_t D = S - a.spec_P;
     const uint8_t* info = reinterpret_cast<const uint8_t*>(a.recs);
     const uint32_t F0 = (blockIdx.x * kBlock + threadIdx.x) * kScanFpt;
-#ifdef UVWS_SCAN_NOP
-    return;  // experiment: the launch alone (wrong summaries)
-#endif
     // (info bytes past n are never used; the buffer holds at least n + 16)
     const uint32_t w = F0 < n ? *reinterpret_cast<const uint32_t*>(info + F0) : 0u;
     // the frame before this thread's first: the previous lane's last byte (lane 0: a load)
     const uint32_t up = __shfl_up(w, 1, 64);
     uint32_t pb = (threadIdx.x & 63) ? up >> 24 : (F0 > 0 && F0 < n ? info[F0 - 1] : 0u);
     TilePart acc = part_identity();
+    uint32_t sb = kNoFrame;  // compact: the thread's first delivered frame not at f * P
 #pragma unroll
     for (uint32_t k = 0; k < kScanFpt; ++k) {
         const uint32_t f = F0 + k;
@@ -2055,7 +2072,7 @@ __global__ __launch_bounds__(kBlock) void k_sum_scan(BatchArgs a, Workspace ws) 
                 }
             }
         }
-        if (!(x & kI8Ok) || ((x & kI8Data) && ((p & kI8Open) != 0) == ((x & kI8Start) != 0))) {
+        if (!(x & kI8Ok) || ((x & kI8Data) && i8_open(p) == ((x & kI8Start) != 0))) {
             acc.ff = f;
             break;
         }
@@ -2066,30 +2083,86 @@ __global__ __launch_bounds__(kBlock) void k_sum_scan(BatchArgs a, Workspace ws) 
                 if (x & kI8Start) {
                     acc.ls = f;
                     acc.seg = plen;
+                    acc.bits = (x & kI8Bin) ? kPartBin : 0u;
                 } else {
                     acc.seg += plen;
                 }
                 acc.nfin += (x & kI8Fin) ? 1u : 0u;
                 acc.last = f;
-                acc.bits = (x & kI8Open) ? kPartOpen : 0u;
+                acc.bits = (acc.bits & ~kPartOpen) | (i8_open(x) ? kPartOpen : 0u);
+            }
+            if constexpr (COMPACT) {
+                if (sb == kNoFrame && !i8_uniform(x, D)) sb = f;
             }
         }
         pb = x;
     }
-#ifdef UVWS_SCAN_NORED
-    const TilePart bp = acc;  // experiment: no block reduction (wrong summaries)
-#else
+    if constexpr (COMPACT) {
+        if (sb != kNoFrame) tag_claim(ws.spec_bad, a.epoch, sb);  // (rare: a batch off the fast path)
+    }
     const TilePart bp = block_reduce_parts<kBlock>(acc);
-#endif
     if (threadIdx.x == 0) {
         reinterpret_cast<TilePart*>(ws.parts)[blockIdx.x] = bp;
         if (bp.ff != kNoFrame) tag_claim(ws.first_bad, a.epoch, bp.ff);
     }
 }
 
+__device__ inline TilePart shfl_up_part(const TilePart& p, int d) {
+    TilePart r;
+    r.pay = __shfl_up(p.pay, d, 64);
+    r.seg = __shfl_up(p.seg, d, 64);
+    r.nfin = __shfl_up(p.nfin, d, 64);
+    r.ls = __shfl_up(p.ls, d, 64);
+    r.last = __shfl_up(p.last, d, 64);
+    r.bits = __shfl_up(p.bits, d, 64);
+    r.ff = __shfl_up(p.ff, d, 64);
+    r.pad[0] = r.pad[1] = r.pad[2] = 0;
+    return r;
+}
+
+// ordered exclusive scan over the block's NT threads (thread t gets elements 0 .. t-1
+// combined); *total gets all of them
+template <int NT>
+__device__ TilePart block_exscan_parts(const TilePart& v, TilePart* total) {
+    __shared__ TilePart s_x[NT];
+    __shared__ TilePart s_tot;
+    s_x[threadIdx.x] = v;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        constexpr int K = NT / 64;
+        const int lane = threadIdx.x;
+        TilePart r = part_identity();
+#pragma unroll
+        for (int k = 0; k < K; ++k) r = part_combine(r, s_x[lane * K + k]);
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const TilePart o = shfl_up_part(r, d);
+            if (lane >= d) r = part_combine(o, r);
+        }
+        TilePart ex = shfl_up_part(r, 1);
+        if (lane == 0) ex = part_identity();
+        if (lane == 63) s_tot = r;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const TilePart el = s_x[lane * K + k];
+            s_x[lane * K + k] = ex;
+            ex = part_combine(ex, el);
+        }
+    }
+    __syncthreads();
+    *total = s_tot;
+    return s_x[threadIdx.x];
+}
+
 constexpr uint32_t kSumTailGrid = 128;  // k_sum_tail blocks (all re-mask after a failure)
 
-__global__ __launch_bounds__(kBlock) void k_sum_tail(BatchArgs a, Workspace ws, uint32_t n_parts) {
+// COMPACT (the speculative compact pass ran, the wire stays masked: nothing to restore): one
+// block, which also leaves the parts' exclusive prefixes for k_sum_msgs, writes the last frame's
+// message and decides the speculation — when a delivered frame is not where the pass put it,
+// ctl[kCtlGate] = epoch hands the call to k_plan + k_spec_fix and no summary is written here
+template <bool COMPACT>
+__global__ __launch_bounds__(kBlock) void k_sum_tail(BatchArgs a, Workspace ws, uint32_t n_parts,
+                                                     uvhttp_ws_message_desc_t* msgs) {
     resolve_epoch(a, ws);
     StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_FIXUP);
     const uint32_t n = a.n;
@@ -2098,7 +2171,8 @@ __global__ __launch_bounds__(kBlock) void k_sum_tail(BatchArgs a, Workspace ws, 
     uvhttp_ws_frame_desc_t dl;
     if (blockIdx.x == 0 && threadIdx.x == 0) (void)parse_one(a, n - 1, seg_info(a, n - 1, n), dl);
     const uint32_t nb = first_bad_of(a, ws, n);
-    if (nb < n) {  // a failure: restore the frames the payload pass unmasked from it on
+    const uint32_t sb = COMPACT ? tag_get(*ws.spec_bad, a.epoch, n) : n;
+    if (!COMPACT && nb < n) {  // a failure: restore the frames the payload pass unmasked from it on
         const uint64_t wave = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
         const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
         for (uint64_t i = nb + wave; i < n; i += nwaves) {
@@ -2110,21 +2184,51 @@ __global__ __launch_bounds__(kBlock) void k_sum_tail(BatchArgs a, Workspace ws, 
     }
     if (blockIdx.x != 0) return;
     // block 0: the scan blocks' parts in order, each thread a run of consecutive ones
-    const TilePart* parts = reinterpret_cast<const TilePart*>(ws.parts);
+    TilePart* parts = reinterpret_cast<TilePart*>(ws.parts);
     const uint32_t per = (n_parts + kBlock - 1) / kBlock;
     const uint32_t p0 = threadIdx.x * per;
     TilePart acc = part_identity();
     constexpr uint32_t kU = 8;  // loads in flight per thread
+    TilePart r[kU];             // (the last run's parts: all of them when per <= kU)
     for (uint32_t pb = p0; pb < p0 + per && pb < n_parts; pb += kU) {
-        TilePart r[kU];
 #pragma unroll
         for (uint32_t k = 0; k < kU; ++k)
             r[k] = pb + k < p0 + per && pb + k < n_parts ? parts[pb + k] : part_identity();
 #pragma unroll
         for (uint32_t k = 0; k < kU; ++k) acc = part_combine(acc, r[k]);
     }
-    TilePart tot = block_reduce_parts<kBlock>(acc);
+    TilePart tot;
+    if constexpr (COMPACT) {
+        // each part replaced by the combination of the parts before it
+        TilePart ex = block_exscan_parts<kBlock>(acc, &tot);
+        if (per <= kU) {
+#pragma unroll
+            for (uint32_t k = 0; k < kU; ++k) {
+                if (k < per && p0 + k < n_parts) {
+                    parts[p0 + k] = ex;
+                    ex = part_combine(ex, r[k]);
+                }
+            }
+        } else {
+            for (uint32_t pb = p0; pb < p0 + per && pb < n_parts; ++pb) {
+                const TilePart v = parts[pb];
+                parts[pb] = ex;
+                ex = part_combine(ex, v);
+            }
+        }
+    } else {
+        tot = block_reduce_parts<kBlock>(acc);
+    }
     if (threadIdx.x != 0) return;
+    if constexpr (COMPACT) {
+        const uint64_t P = a.spec_P;
+        const bool last_off = nb >= n && !(dl.opcode <= 2 && dl.payload_len == P &&
+                                           dl.header_size + ((dl.flags & UVHTTP_WS_FLAG_MASK) ? 4u : 0u) == S - P);
+        if (sb < nb || last_off) {
+            ws.ctl[kCtlGate] = a.epoch;
+            return;
+        }
+    }
     uvhttp_ws_batch_summary_t sm;
     sm.n_frames = n;
     sm.n_delivered = nb < n ? nb : n;
@@ -2146,6 +2250,19 @@ __global__ __launch_bounds__(kBlock) void k_sum_tail(BatchArgs a, Workspace ws, 
             lp.last = n - 1;
             lp.bits = si_open(x) ? kPartOpen : 0u;
         }
+        if constexpr (COMPACT) {
+            if (x & kSiFin) {  // its message (a uniform data frame here: every frame is P bytes)
+                const uint32_t s0 = (x & kSiStart) ? n - 1 : tot.ls;
+                uvhttp_ws_message_desc_t m;
+                m.arena_off = (uint64_t)s0 * a.spec_P;
+                m.len = (uint64_t)(n - s0) * a.spec_P;
+                m.first_frame = s0;
+                m.last_frame = n - 1;
+                m.opcode = s0 == n - 1 ? dl.opcode : (tot.bits & kPartBin) ? 2 : 1;
+                m.reserved = 0;
+                msgs[tot.nfin] = m;
+            }
+        }
         tot = part_combine(tot, lp);
         sm.state_closed = (x & kSiClose) ? 1u : 0u;
         sm.consumed_bytes = (uint64_t)(n - 1) * S + dl.wire_len;
@@ -2153,9 +2270,92 @@ __global__ __launch_bounds__(kBlock) void k_sum_tail(BatchArgs a, Workspace ws, 
     sm.status = sm.first_status < 0 ? -1 : 0;
     sm.payload_bytes = tot.pay;
     sm.n_messages = tot.nfin;
-    sm.arena_bytes = 0;
+    sm.arena_bytes = COMPACT ? tot.pay : 0;  // (compact: every delivered frame is a data frame)
     sm.pending_bytes = (tot.last != kNoFrame && (tot.bits & kPartOpen)) ? tot.seg : 0;
     *a.summary = sm;
+}
+
+// block-wide exclusive scans of one count (sum) and one frame mark (max) per thread
+__device__ inline void block_exscan_sum_max(uint32_t c, uint32_t l, uint32_t& ec, uint32_t& el) {
+    __shared__ uint32_t s_c[kBlock / 64], s_l[kBlock / 64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t ic = c, il = l;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t oc = __shfl_up(ic, d, 64), ol = __shfl_up(il, d, 64);
+        if (lane >= d) {
+            ic += oc;
+            il = ol > il ? ol : il;
+        }
+    }
+    uint32_t xl = __shfl_up(il, 1, 64);
+    if (lane == 0) xl = 0;
+    if (lane == 63) {
+        s_c[wv] = ic;
+        s_l[wv] = il;
+    }
+    __syncthreads();
+    uint32_t bc = 0, bl = 0;
+    for (int k = 0; k < wv; ++k) {
+        bc += s_c[k];
+        bl = s_l[k] > bl ? s_l[k] : bl;
+    }
+    ec = bc + ic - c;
+    el = xl > bl ? xl : bl;
+}
+
+// Summary-only compact decode, after k_sum_tail: the message table.  With every frame before
+// the first failure a uniform data frame (the speculation held), message m ends at the m-th FIN
+// frame f and starts at the latest start s <= f: arena [s P, (f + 1) P), frames s..f.  Each
+// thread takes its k_sum_scan frames again; the block's prefix (messages and latest start before
+// it) is the part prefix k_sum_tail left.  The last frame's message is the tail's.
+__global__ __launch_bounds__(kBlock) void k_sum_msgs(BatchArgs a, Workspace ws,
+                                                     uvhttp_ws_message_desc_t* msgs) {
+    resolve_epoch(a, ws);
+    if (ws.ctl[kCtlGate] == a.epoch) return;  // the batch went to the full compact decode
+    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_FINALIZE);
+    const uint32_t n = a.n;
+    const uint32_t nb = first_bad_of(a, ws, n);
+    const uint32_t end = nb < n - 1 ? nb : n - 1;
+    const uint64_t P = a.spec_P;
+    const uint8_t* info = reinterpret_cast<const uint8_t*>(a.recs);
+    const uint32_t F0 = (blockIdx.x * kBlock + threadIdx.x) * kScanFpt;
+    const uint32_t w = F0 < n ? *reinterpret_cast<const uint32_t*>(info + F0) : 0u;
+    uint32_t cnt = 0, ls1 = 0;  // FIN frames; latest start + 1 (0: none)
+    // (a start before this thread's frames: its info byte, or — before the block — the prefix's
+    // kPartBin)
+#pragma unroll
+    for (uint32_t k = 0; k < kScanFpt; ++k) {
+        const uint32_t f = F0 + k, x = (w >> (8 * k)) & 0xFF;
+        if (f < end) {
+            cnt += (x & kI8Fin) ? 1u : 0u;
+            if (x & kI8Start) ls1 = f + 1;
+        }
+    }
+    uint32_t ec, el;
+    block_exscan_sum_max(cnt, ls1, ec, el);
+    if (!cnt) return;
+    const TilePart pre = reinterpret_cast<const TilePart*>(ws.parts)[blockIdx.x];
+    uint32_t m = pre.nfin + ec;
+    uint32_t ls = el ? el - 1 : pre.ls;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanFpt; ++k) {
+        const uint32_t f = F0 + k, x = (w >> (8 * k)) & 0xFF;
+        if (f >= end) break;
+        if (x & kI8Start) ls = f;
+        if (x & kI8Fin) {
+            const uint32_t xs = ls >= F0 ? (w >> (8 * (ls - F0))) & 0xFF
+                                : ls == pre.ls ? ((pre.bits & kPartBin) ? kI8Bin : 0u) : info[ls];
+            uvhttp_ws_message_desc_t md;
+            md.arena_off = (uint64_t)ls * P;
+            md.len = (uint64_t)(f - ls + 1) * P;
+            md.first_frame = ls;
+            md.last_frame = f;
+            md.opcode = (xs & kI8Bin) ? 2 : 1;
+            md.reserved = 0;
+            msgs[m++] = md;
+        }
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -2564,6 +2764,7 @@ __global__ __launch_bounds__(BLOCK) void k_scatter_compact(
 __global__ __launch_bounds__(kBlock) void k_spec_fix(BatchArgs a, uvhttp_ws_frame_desc_t* desc,
                                                      Workspace ws, uint64_t n_tiles) {
     resolve_epoch(a, ws);
+    if (a.gate && ws.ctl[kCtlGate] != a.epoch) return;  // (summary-only compact: speculation held)
     StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_FIXUP);
     const uint32_t n = a.n;
     const uint32_t nb = first_bad_of(a, ws, n);
@@ -4654,6 +4855,20 @@ static uvhttp_ws_frame_desc_t* desc_scratch(uvhttp_ws_gpu_engine_t* e, uint32_t 
     return e->dscr;
 }
 
+// The summary-only kernels' fragment state machine is exact for a stride batch when every slot
+// but the last is too long for a control frame (stride >= kSumMinStride) and no message can
+// reach max_message_size even if every frame joined it
+static bool sum_ok(const uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b) {
+    if (!e->sum_fast || b->frame_off || b->n_frames == 0 || b->frame_stride < kSumMinStride) return false;
+    const uint64_t n = b->n_frames;
+    if ((n - 1) > (b->wire_len - 1) / b->frame_stride) return false;
+    const uint64_t lim = (uint64_t)(int64_t)b->max_message_size;
+    const uint64_t last_slot = b->wire_len - (n - 1) * b->frame_stride;
+    const uint64_t msg_bound = (n - 1) * max_payload_in(b->frame_stride, b->is_server) +
+                               max_payload_in(last_slot, b->is_server);
+    return lim == 0 || msg_bound <= lim;
+}
+
 static int check_batch(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b,
                        const void* d_summary) {
     if (!e || !b || !d_summary) return UVHTTP_WS_GPU_EINVAL;
@@ -4736,12 +4951,7 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
         // data frame — stride >= kSumMinStride — and no message can reach max_message_size: the
         // bound below) and leaves one TilePart per tile; k_sum_tail writes the summary and undoes
         // a failure.  No records, no k_plan, no descriptors.
-        const uint64_t lim = (uint64_t)(int64_t)b->max_message_size;
-        const uint64_t last_slot = b->wire_len - (uint64_t)(a.n - 1) * b->frame_stride;
-        const uint64_t msg_bound = (uint64_t)(a.n - 1) * max_payload_in(b->frame_stride, b->is_server) +
-                                   max_payload_in(last_slot, b->is_server);
-        const bool sum_fast = !d_desc && e->sum_fast && fb == 256 && fv == 4 && e->fused_aux == 18 &&
-                              b->frame_stride >= kSumMinStride && (lim == 0 || msg_bound <= lim);
+        const bool sum_fast = !d_desc && fb == 256 && fv == 4 && e->fused_aux == 18 && sum_ok(e, b);
         if (sum_fast) {
             a.recs = reinterpret_cast<FrameRec*>(e->ws.recs);  // (the info bytes: 1 per frame)
             const int stk = timing_begin(e, s);
@@ -4752,8 +4962,9 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
             }
             timing_end(e, stk, s);
             const uint32_t n_parts = (a.n + kBlock * kScanFpt - 1) / (kBlock * kScanFpt);
-            hipLaunchKernelGGL(k_sum_scan, dim3(n_parts), dim3(kBlock), 0, s, a, e->ws);
-            hipLaunchKernelGGL(k_sum_tail, dim3(kSumTailGrid), dim3(kBlock), 0, s, a, e->ws, n_parts);
+            hipLaunchKernelGGL(k_sum_scan<false>, dim3(n_parts), dim3(kBlock), 0, s, a, e->ws);
+            hipLaunchKernelGGL(k_sum_tail<false>, dim3(kSumTailGrid), dim3(kBlock), 0, s, a, e->ws, n_parts,
+                               (uvhttp_ws_message_desc_t*)nullptr);
             hipError_t hs = hipGetLastError();
             if (prev != e->device) (void)hipSetDevice(prev);
             if (hs != hipSuccess) return set_err(e, UVHTTP_WS_GPU_ELAUNCH, "launch", hs);
@@ -4807,6 +5018,7 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
     }
     // every other path keeps per-frame descriptors internally: a caller without them gets the
     // engine's scratch
+    const bool no_desc = !d_desc;
     if (!d_desc && !(d_desc = desc_scratch(e, a.n))) {
         if (prev != e->device) (void)hipSetDevice(prev);
         return set_err(e, UVHTTP_WS_GPU_ENOMEM, "descriptor scratch (reserve before capturing)", hipSuccess);
@@ -4827,12 +5039,31 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
         a.spec_P = spec_p;
         constexpr uint64_t kSt = 256ull * 4 * 16;
         const uint64_t s_tiles = (b->wire_len + kSt - 1) / kSt;
+        // summary-only (d_desc == NULL): the pass leaves info bytes instead of records;
+        // k_sum_scan / k_sum_tail / k_sum_msgs run the state machine, check the speculation and
+        // write the summary and the message table; a batch that broke the speculation (a control
+        // frame, another length, ...) is decoded again by k_plan + k_spec_fix, which otherwise
+        // return at once (ctl[kCtlGate])
+        const bool sum_c = no_desc && sum_ok(e, b) && arena_cap / spec_p >= a.n;
+        if (sum_c) a.recs = reinterpret_cast<FrameRec*>(e->ws.recs);  // (the info bytes)
         const int stk = timing_begin(e, s);
         for (uint64_t tb = 0; tb < s_tiles; tb += (1ull << 24)) {
             const uint32_t grid_s = (uint32_t)((s_tiles - tb) < (1ull << 24) ? (s_tiles - tb) : (1ull << 24));
-            hipLaunchKernelGGL((k_unmask_stride<256, 4, kSpecCompact>), dim3(grid_s), dim3(256), 0, s, a, e->ws, tb);
+            if (sum_c)
+                hipLaunchKernelGGL((k_unmask_stride<256, 4, kSpecCompact, true>), dim3(grid_s), dim3(256), 0, s, a,
+                                   e->ws, tb);
+            else
+                hipLaunchKernelGGL((k_unmask_stride<256, 4, kSpecCompact>), dim3(grid_s), dim3(256), 0, s, a, e->ws, tb);
         }
         timing_end(e, stk, s);
+        if (sum_c) {
+            const uint32_t n_parts = (a.n + kBlock * kScanFpt - 1) / (kBlock * kScanFpt);
+            hipLaunchKernelGGL(k_sum_scan<true>, dim3(n_parts), dim3(kBlock), 0, s, a, e->ws);
+            hipLaunchKernelGGL(k_sum_tail<true>, dim3(1), dim3(kBlock), 0, s, a, e->ws, n_parts, d_msgs);
+            hipLaunchKernelGGL(k_sum_msgs, dim3(n_parts), dim3(kBlock), 0, s, a, e->ws, d_msgs);
+            a.recs = nullptr;  // the fallback's k_plan gathers the headers
+            a.gate = 1;
+        }
         launch_plan(e, a, a.n, d_desc, d_msgs, s);
         const uint32_t nblk = (a.n + kBlock - 1) / kBlock;
         hipLaunchKernelGGL(k_spec_fix, dim3(nblk < 1024 ? nblk : 1024), dim3(kBlock), 0, s, a, d_desc,
@@ -5316,10 +5547,19 @@ struct uvhttp_ws_gpu_pipeline {
     uvhttp_ws_gpu_engine_t* eng;  // one workspace: the decodes run in order on `cs`
     hipStream_t up, cs;
     PipeSlot* slots;
-    int ahead;        // an upload starts once the slot submitted `ahead` submissions earlier is done
+    int in_flight;    // submit first waits (host) until fewer earlier submissions are in flight
     int recent[16];   // slots of the latest submissions (ring)
     uint64_t n_sub;   // submissions so far
 };
+
+// Submissions a pipeline lets run ahead of the host.  With more than three queued, H2D / decode /
+// D2H chains of 16-256 MiB slots ran at 24-27 GiB/s (depth 4) and 16-26 (depth 8) against 43-44
+// at depth 3, at every slot size; holding the device back instead (each upload waiting on the
+// done event of the submission three earlier) did not help, bounding what the host has queued
+// does: depth 4 43.9, depth 8 43.4 GiB/s (tools/r05_pipe5.sh, profiles/r05v_pipeline_in_flight.jsonl).
+// With HSA_ENABLE_SDMA=0 depth 3 is as slow as depth 4, so the deeper queues most likely move
+// the runtime's copies off the SDMA engines; UVHTTP_WS_PIPE_IN_FLIGHT overrides (0: no bound).
+constexpr int kPipeInFlight = 3;
 
 void uvhttp_ws_gpu_pipeline_free(uvhttp_ws_gpu_pipeline_t* p) {
     if (!p) return;
@@ -5359,8 +5599,8 @@ int uvhttp_ws_gpu_pipeline_create(int device, int depth, uint64_t slot_bytes,
     p->depth = depth;
     p->slot_bytes = slot_bytes;
     p->slot_frames = slot_frames;
-    p->ahead = 0;
-    if (const char* pa = getenv("UVHTTP_WS_PIPE_AHEAD")) p->ahead = atoi(pa);
+    p->in_flight = kPipeInFlight;
+    if (const char* pf = getenv("UVHTTP_WS_PIPE_IN_FLIGHT")) p->in_flight = atoi(pf);
     p->slots = (PipeSlot*)calloc((size_t)depth, sizeof(PipeSlot));
     if (!p->slots) {
         free(p);
@@ -5421,8 +5661,10 @@ int uvhttp_ws_gpu_pipeline_submit(uvhttp_ws_gpu_pipeline_t* p, int slot, uint64_
     (void)hipSetDevice(p->device);
     // upload stream: the slot's bytes (its previous round was waited for, so d_wire is free)
     hipError_t h = hipSuccess;
-    if (p->ahead > 0 && p->n_sub >= (uint64_t)p->ahead)
-        h = hipStreamWaitEvent(p->up, p->slots[p->recent[(p->n_sub - p->ahead) % 16]].done_ev, 0);
+    // at most in_flight submissions queued: wait for the one in_flight submissions back (its
+    // slot's latest done event; a slot cycled faster than that only waits longer)
+    if (p->in_flight > 0 && p->in_flight < 16 && p->n_sub >= (uint64_t)p->in_flight)
+        h = hipEventSynchronize(p->slots[p->recent[(p->n_sub - p->in_flight) % 16]].done_ev);
     if (h == hipSuccess && wire_len) h = hipMemcpyAsync(s.d_wire, s.h_wire, wire_len, hipMemcpyHostToDevice, p->up);
     if (h == hipSuccess && use_offsets && n_frames)
         h = hipMemcpyAsync(s.d_off, s.h_off, (size_t)n_frames * 8, hipMemcpyHostToDevice, p->up);
