@@ -2,16 +2,16 @@
 uvhttp_ws_amd.h).  A fixed-stride batch of frames of >= 140 wire bytes whose messages cannot
 reach max_message_size and whose arena holds n * P bytes runs the speculative compact pass
 writing one info byte per frame instead of a 16-byte record; k_sum_scan (fragment state machine,
-speculation check), k_sum_tail (summary, the parts' prefixes, the last frame's message) and
-k_sum_msgs (message table) finish it.  A batch that breaks the speculation — a delivered frame
+speculation check, one summary part per block) and k_sum_msgs (message table; its block 0 the
+summary and the last frame's message) finish it.  A batch that breaks the speculation — a delivered frame
 that is not a data frame of the uniform length P: a reserved opcode, a non-minimal length, a
 control or short last frame — is decoded again by k_plan + k_spec_fix, which return at once
 otherwise.  Either way the summary, the message table, the arena up to arena_bytes and the wire
 must equal the oracle's compact decode (process_data per frame, src/uvhttp_websocket.c:825-1097,
 payloads appended per uvhttp_ws_fragment_append :781-822) and the descriptor path's.
 
-Which way a call went is read off the device stamps: k_sum_msgs (kind "finalize") runs only
-when the speculation held."""
+Which way a call went is read off the device stamps: k_spec_fix (kind "fixup") runs only when
+the speculation failed (or the summary-only path was not taken)."""
 import random
 
 import numpy as np
@@ -116,7 +116,7 @@ def _check(torch, engines, wire, n, stride, wl=None, mm=0, is_server=1, mf=MF, f
         assert np.array_equal(m["opcode"], ref["msg_opcode"]), k
         if k == 0 and fast is not None:
             kinds = {r[1] for r in e.read_stamps()}
-            assert ("finalize" in kinds) == fast, (fast, kinds)
+            assert ("fixup" not in kinds) == fast, (fast, kinds)
     return ref
 
 

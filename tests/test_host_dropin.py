@@ -70,7 +70,8 @@ def test_struct_abi():
     # batcher structs (include/uvhttp_ws_amd.h, checked against gcc's layout)
     assert C.sizeof(U.BatcherConfig) == 72 and U.BatcherConfig.on_ready.offset == 48
     assert U.BatcherConfig.on_tls_handback.offset == 64
-    assert C.sizeof(U.BatcherStats) == 248 and U.BatcherStats.blocked_ms.offset == 112
+    assert C.sizeof(U.BatcherStats) == 256 and U.BatcherStats.blocked_ms.offset == 112
+    assert U.BatcherStats.zero_copy_reads.offset == 248
     assert U.BatcherStats.blocked_p50_ms.offset == 208
 
 

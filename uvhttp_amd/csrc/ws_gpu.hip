@@ -2107,128 +2107,35 @@ __global__ __launch_bounds__(kBlock) void k_sum_scan(BatchArgs a, Workspace ws) 
     }
 }
 
-__device__ inline TilePart shfl_up_part(const TilePart& p, int d) {
-    TilePart r;
-    r.pay = __shfl_up(p.pay, d, 64);
-    r.seg = __shfl_up(p.seg, d, 64);
-    r.nfin = __shfl_up(p.nfin, d, 64);
-    r.ls = __shfl_up(p.ls, d, 64);
-    r.last = __shfl_up(p.last, d, 64);
-    r.bits = __shfl_up(p.bits, d, 64);
-    r.ff = __shfl_up(p.ff, d, 64);
-    r.pad[0] = r.pad[1] = r.pad[2] = 0;
-    return r;
-}
-
-// ordered exclusive scan over the block's NT threads (thread t gets elements 0 .. t-1
-// combined); *total gets all of them
-template <int NT>
-__device__ TilePart block_exscan_parts(const TilePart& v, TilePart* total) {
-    __shared__ TilePart s_x[NT];
-    __shared__ TilePart s_tot;
-    s_x[threadIdx.x] = v;
-    __syncthreads();
-    if (threadIdx.x < 64) {
-        constexpr int K = NT / 64;
-        const int lane = threadIdx.x;
-        TilePart r = part_identity();
-#pragma unroll
-        for (int k = 0; k < K; ++k) r = part_combine(r, s_x[lane * K + k]);
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const TilePart o = shfl_up_part(r, d);
-            if (lane >= d) r = part_combine(o, r);
-        }
-        TilePart ex = shfl_up_part(r, 1);
-        if (lane == 0) ex = part_identity();
-        if (lane == 63) s_tot = r;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const TilePart el = s_x[lane * K + k];
-            s_x[lane * K + k] = ex;
-            ex = part_combine(ex, el);
-        }
-    }
-    __syncthreads();
-    *total = s_tot;
-    return s_x[threadIdx.x];
-}
-
 constexpr uint32_t kSumTailGrid = 128;  // k_sum_tail blocks (all re-mask after a failure)
 
-// COMPACT (the speculative compact pass ran, the wire stays masked: nothing to restore): one
-// block, which also leaves the parts' exclusive prefixes for k_sum_msgs, writes the last frame's
-// message and decides the speculation — when a delivered frame is not where the pass put it,
-// ctl[kCtlGate] = epoch hands the call to k_plan + k_spec_fix and no summary is written here
-template <bool COMPACT>
-__global__ __launch_bounds__(kBlock) void k_sum_tail(BatchArgs a, Workspace ws, uint32_t n_parts,
-                                                     uvhttp_ws_message_desc_t* msgs) {
-    resolve_epoch(a, ws);
-    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_FIXUP);
-    const uint32_t n = a.n;
-    const uint64_t S = a.frame_stride;
-    // the last frame's header (its part of the summary), read first
-    uvhttp_ws_frame_desc_t dl;
-    if (blockIdx.x == 0 && threadIdx.x == 0) (void)parse_one(a, n - 1, seg_info(a, n - 1, n), dl);
-    const uint32_t nb = first_bad_of(a, ws, n);
-    const uint32_t sb = COMPACT ? tag_get(*ws.spec_bad, a.epoch, n) : n;
-    if (!COMPACT && nb < n) {  // a failure: restore the frames the payload pass unmasked from it on
-        const uint64_t wave = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
-        const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
-        for (uint64_t i = nb + wave; i < n; i += nwaves) {
-            uvhttp_ws_frame_desc_t d;
-            (void)parse_one(a, (uint32_t)i, seg_info(a, (uint32_t)i, n), d);
-            if (d.status == UVHTTP_WS_FRAME_OK && d.payload_len)
-                remask_range(a.wire, d.payload_off, d.payload_off + d.payload_len, d.masking_key);
-        }
-    }
-    if (blockIdx.x != 0) return;
-    // block 0: the scan blocks' parts in order, each thread a run of consecutive ones
-    TilePart* parts = reinterpret_cast<TilePart*>(ws.parts);
-    const uint32_t per = (n_parts + kBlock - 1) / kBlock;
+// the combination of parts [0, hi) in order, in every thread of the block (each thread a run
+// of consecutive parts, kU loads in flight)
+__device__ TilePart parts_prefix(const TilePart* parts, uint32_t hi) {
+    __shared__ TilePart s_res;
+    const uint32_t per = (hi + kBlock - 1) / kBlock;
     const uint32_t p0 = threadIdx.x * per;
     TilePart acc = part_identity();
-    constexpr uint32_t kU = 8;  // loads in flight per thread
-    TilePart r[kU];             // (the last run's parts: all of them when per <= kU)
-    for (uint32_t pb = p0; pb < p0 + per && pb < n_parts; pb += kU) {
+    constexpr uint32_t kU = 8;
+    for (uint32_t pb = p0; pb < p0 + per && pb < hi; pb += kU) {
+        TilePart r[kU];
 #pragma unroll
-        for (uint32_t k = 0; k < kU; ++k)
-            r[k] = pb + k < p0 + per && pb + k < n_parts ? parts[pb + k] : part_identity();
+        for (uint32_t k = 0; k < kU; ++k) r[k] = pb + k < p0 + per && pb + k < hi ? parts[pb + k] : part_identity();
 #pragma unroll
         for (uint32_t k = 0; k < kU; ++k) acc = part_combine(acc, r[k]);
     }
-    TilePart tot;
-    if constexpr (COMPACT) {
-        // each part replaced by the combination of the parts before it
-        TilePart ex = block_exscan_parts<kBlock>(acc, &tot);
-        if (per <= kU) {
-#pragma unroll
-            for (uint32_t k = 0; k < kU; ++k) {
-                if (k < per && p0 + k < n_parts) {
-                    parts[p0 + k] = ex;
-                    ex = part_combine(ex, r[k]);
-                }
-            }
-        } else {
-            for (uint32_t pb = p0; pb < p0 + per && pb < n_parts; ++pb) {
-                const TilePart v = parts[pb];
-                parts[pb] = ex;
-                ex = part_combine(ex, v);
-            }
-        }
-    } else {
-        tot = block_reduce_parts<kBlock>(acc);
-    }
-    if (threadIdx.x != 0) return;
-    if constexpr (COMPACT) {
-        const uint64_t P = a.spec_P;
-        const bool last_off = nb >= n && !(dl.opcode <= 2 && dl.payload_len == P &&
-                                           dl.header_size + ((dl.flags & UVHTTP_WS_FLAG_MASK) ? 4u : 0u) == S - P);
-        if (sb < nb || last_off) {
-            ws.ctl[kCtlGate] = a.epoch;
-            return;
-        }
-    }
+    const TilePart tot = block_reduce_parts<kBlock>(acc);
+    if (threadIdx.x == 0) s_res = tot;
+    __syncthreads();
+    return s_res;
+}
+
+// the summary of a summary-only decode from the parts of frames [0, n - 1) combined (tot), the
+// last frame's header (dl) and the first failure nb (thread 0)
+__device__ void sum_summary(const BatchArgs& a, TilePart tot, const uvhttp_ws_frame_desc_t& dl,
+                            uint32_t nb, bool compact) {
+    const uint32_t n = a.n;
+    const uint64_t S = a.frame_stride;
     uvhttp_ws_batch_summary_t sm;
     sm.n_frames = n;
     sm.n_delivered = nb < n ? nb : n;
@@ -2250,19 +2157,6 @@ __global__ __launch_bounds__(kBlock) void k_sum_tail(BatchArgs a, Workspace ws, 
             lp.last = n - 1;
             lp.bits = si_open(x) ? kPartOpen : 0u;
         }
-        if constexpr (COMPACT) {
-            if (x & kSiFin) {  // its message (a uniform data frame here: every frame is P bytes)
-                const uint32_t s0 = (x & kSiStart) ? n - 1 : tot.ls;
-                uvhttp_ws_message_desc_t m;
-                m.arena_off = (uint64_t)s0 * a.spec_P;
-                m.len = (uint64_t)(n - s0) * a.spec_P;
-                m.first_frame = s0;
-                m.last_frame = n - 1;
-                m.opcode = s0 == n - 1 ? dl.opcode : (tot.bits & kPartBin) ? 2 : 1;
-                m.reserved = 0;
-                msgs[tot.nfin] = m;
-            }
-        }
         tot = part_combine(tot, lp);
         sm.state_closed = (x & kSiClose) ? 1u : 0u;
         sm.consumed_bytes = (uint64_t)(n - 1) * S + dl.wire_len;
@@ -2270,9 +2164,33 @@ __global__ __launch_bounds__(kBlock) void k_sum_tail(BatchArgs a, Workspace ws, 
     sm.status = sm.first_status < 0 ? -1 : 0;
     sm.payload_bytes = tot.pay;
     sm.n_messages = tot.nfin;
-    sm.arena_bytes = COMPACT ? tot.pay : 0;  // (compact: every delivered frame is a data frame)
+    sm.arena_bytes = compact ? tot.pay : 0;  // (compact: every delivered frame is a data frame)
     sm.pending_bytes = (tot.last != kNoFrame && (tot.bits & kPartOpen)) ? tot.seg : 0;
     *a.summary = sm;
+}
+
+__global__ __launch_bounds__(kBlock) void k_sum_tail(BatchArgs a, Workspace ws, uint32_t n_parts) {
+    resolve_epoch(a, ws);
+    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_FIXUP);
+    const uint32_t n = a.n;
+    // the last frame's header (its part of the summary), read first
+    uvhttp_ws_frame_desc_t dl;
+    if (blockIdx.x == 0 && threadIdx.x == 0) (void)parse_one(a, n - 1, seg_info(a, n - 1, n), dl);
+    const uint32_t nb = first_bad_of(a, ws, n);
+    if (nb < n) {  // a failure: restore the frames the payload pass unmasked from it on
+        const uint64_t wave = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+        const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
+        for (uint64_t i = nb + wave; i < n; i += nwaves) {
+            uvhttp_ws_frame_desc_t d;
+            (void)parse_one(a, (uint32_t)i, seg_info(a, (uint32_t)i, n), d);
+            if (d.status == UVHTTP_WS_FRAME_OK && d.payload_len)
+                remask_range(a.wire, d.payload_off, d.payload_off + d.payload_len, d.masking_key);
+        }
+    }
+    if (blockIdx.x != 0) return;
+    // block 0: the scan blocks' parts in order
+    const TilePart tot = parts_prefix(reinterpret_cast<const TilePart*>(ws.parts), n_parts);
+    if (threadIdx.x == 0) sum_summary(a, tot, dl, nb, false);
 }
 
 // block-wide exclusive scans of one count (sum) and one frame mark (max) per thread
@@ -2304,26 +2222,76 @@ __device__ inline void block_exscan_sum_max(uint32_t c, uint32_t l, uint32_t& ec
     el = xl > bl ? xl : bl;
 }
 
-// Summary-only compact decode, after k_sum_tail: the message table.  With every frame before
-// the first failure a uniform data frame (the speculation held), message m ends at the m-th FIN
-// frame f and starts at the latest start s <= f: arena [s P, (f + 1) P), frames s..f.  Each
-// thread takes its k_sum_scan frames again; the block's prefix (messages and latest start before
-// it) is the part prefix k_sum_tail left.  The last frame's message is the tail's.
-__global__ __launch_bounds__(kBlock) void k_sum_msgs(BatchArgs a, Workspace ws,
+// what a block of k_sum_msgs needs of the scan parts before it: FIN frames (sum) and the
+// latest start with its BINARY bit as ((ls + 1) << 1 | bin) (max; 0 = none) — commutative, so
+// each thread loads the parts t, t + kBlock, ... (one 16-byte load each: nfin, ls, last, bits)
+__device__ inline void parts_fin_start(const TilePart* parts, uint32_t hi, uint32_t& nfin, uint32_t& key) {
+    __shared__ uint32_t s_c[kBlock / 64], s_k[kBlock / 64];
+    uint32_t c = 0, k = 0;
+    for (uint32_t pb = threadIdx.x; pb < hi; pb += kBlock) {
+        const u32x4 q = *reinterpret_cast<const u32x4*>(reinterpret_cast<const uint8_t*>(parts + pb) + 16);
+        c += q.x;
+        const uint32_t kk = q.y == kNoFrame ? 0u : ((q.y + 1) << 1) | ((q.w & kPartBin) ? 1u : 0u);
+        k = kk > k ? kk : k;
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        c += __shfl_xor(c, d, 64);
+        const uint32_t o = __shfl_xor(k, d, 64);
+        k = o > k ? o : k;
+    }
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        s_c[wv] = c;
+        s_k[wv] = k;
+    }
+    __syncthreads();
+    nfin = 0;
+    key = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) {
+        nfin += s_c[w];
+        key = s_k[w] > key ? s_k[w] : key;
+    }
+}
+
+// Summary-only compact decode, after k_sum_scan<true> (the parts of its blocks in ws.parts):
+// the message table and the summary.  With every frame before the first failure a uniform
+// data frame (the speculation held), message m ends at the m-th FIN frame f and starts at the
+// latest start s <= f: arena [s P, (f + 1) P), frames s..f.  Block b takes the frames of scan
+// block b again; the messages and the latest start before it come from parts [0, b) (sums and
+// maxima, so no ordered combine).  Block 0 decides the speculation — a delivered frame off the
+// uniform layout (k_sum_scan claimed spec_bad) or a last frame that is not uniform sets
+// ctl[kCtlGate] = epoch and k_plan + k_spec_fix decode the call again (messages written here
+// are then overwritten or past n_messages) — and otherwise writes the last frame's message and
+// the summary, which with every delivered frame P bytes of data needs no more than the FIN
+// count, the latest start and whether the last delivered frame left its message open.
+// (One launch after the scan; a single-block tail leaving ordered prefixes + this kernel took
+// 6.4 + 2.0 us and a boundary on C4, every block combining full parts in order 9.2 us.)
+__global__ __launch_bounds__(kBlock) void k_sum_msgs(BatchArgs a, Workspace ws, uint32_t n_parts,
                                                      uvhttp_ws_message_desc_t* msgs) {
     resolve_epoch(a, ws);
-    if (ws.ctl[kCtlGate] == a.epoch) return;  // the batch went to the full compact decode
     StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_FINALIZE);
     const uint32_t n = a.n;
-    const uint32_t nb = first_bad_of(a, ws, n);
-    const uint32_t end = nb < n - 1 ? nb : n - 1;
+    const uint64_t S = a.frame_stride;
     const uint64_t P = a.spec_P;
+    const bool head = blockIdx.x == 0;
+    uvhttp_ws_frame_desc_t dl;
+    if (head && threadIdx.x == 0) (void)parse_one(a, n - 1, seg_info(a, n - 1, n), dl);
+    const uint32_t nb = first_bad_of(a, ws, n);
+    const uint32_t sb = tag_get(*ws.spec_bad, a.epoch, n);
+    const uint32_t end = nb < n - 1 ? nb : n - 1;  // frames [0, end) here, the last one is block 0's
     const uint8_t* info = reinterpret_cast<const uint8_t*>(a.recs);
     const uint32_t F0 = (blockIdx.x * kBlock + threadIdx.x) * kScanFpt;
     const uint32_t w = F0 < n ? *reinterpret_cast<const uint32_t*>(info + F0) : 0u;
+    constexpr uint32_t kPartFrames = kBlock * kScanFpt;
+    // block 0: the parts of every frame before `end` (a part stops at its first failure)
+    const uint32_t hi = head ? (end / kPartFrames + 1 < n_parts ? end / kPartFrames + 1 : n_parts) : blockIdx.x;
+    uint32_t pre_fin, pre_key;
+    parts_fin_start(reinterpret_cast<const TilePart*>(ws.parts), hi, pre_fin, pre_key);
+    const uint32_t tot_fin = pre_fin, tot_key = pre_key;
+    if (head) pre_fin = pre_key = 0;
     uint32_t cnt = 0, ls1 = 0;  // FIN frames; latest start + 1 (0: none)
-    // (a start before this thread's frames: its info byte, or — before the block — the prefix's
-    // kPartBin)
 #pragma unroll
     for (uint32_t k = 0; k < kScanFpt; ++k) {
         const uint32_t f = F0 + k, x = (w >> (8 * k)) & 0xFF;
@@ -2334,28 +2302,79 @@ __global__ __launch_bounds__(kBlock) void k_sum_msgs(BatchArgs a, Workspace ws,
     }
     uint32_t ec, el;
     block_exscan_sum_max(cnt, ls1, ec, el);
-    if (!cnt) return;
-    const TilePart pre = reinterpret_cast<const TilePart*>(ws.parts)[blockIdx.x];
-    uint32_t m = pre.nfin + ec;
-    uint32_t ls = el ? el - 1 : pre.ls;
+    if (cnt) {
+        uint32_t m = pre_fin + ec;
+        const uint32_t pre_ls = pre_key ? (pre_key >> 1) - 1 : kNoFrame;
+        uint32_t ls = el ? el - 1 : pre_ls;
 #pragma unroll
-    for (uint32_t k = 0; k < kScanFpt; ++k) {
-        const uint32_t f = F0 + k, x = (w >> (8 * k)) & 0xFF;
-        if (f >= end) break;
-        if (x & kI8Start) ls = f;
-        if (x & kI8Fin) {
-            const uint32_t xs = ls >= F0 ? (w >> (8 * (ls - F0))) & 0xFF
-                                : ls == pre.ls ? ((pre.bits & kPartBin) ? kI8Bin : 0u) : info[ls];
-            uvhttp_ws_message_desc_t md;
-            md.arena_off = (uint64_t)ls * P;
-            md.len = (uint64_t)(f - ls + 1) * P;
-            md.first_frame = ls;
-            md.last_frame = f;
-            md.opcode = (xs & kI8Bin) ? 2 : 1;
-            md.reserved = 0;
-            msgs[m++] = md;
+        for (uint32_t k = 0; k < kScanFpt; ++k) {
+            const uint32_t f = F0 + k, x = (w >> (8 * k)) & 0xFF;
+            if (f >= end) break;
+            if (x & kI8Start) ls = f;
+            if (x & kI8Fin) {
+                // the start's opcode: its info byte, or — before the block — the prefix's bit
+                const uint32_t xs = ls >= F0 ? (w >> (8 * (ls - F0))) & 0xFF
+                                    : ls == pre_ls ? ((pre_key & 1u) ? kI8Bin : 0u) : info[ls];
+                uvhttp_ws_message_desc_t md;
+                md.arena_off = (uint64_t)ls * P;
+                md.len = (uint64_t)(f - ls + 1) * P;
+                md.first_frame = ls;
+                md.last_frame = f;
+                md.opcode = (xs & kI8Bin) ? 2 : 1;
+                md.reserved = 0;
+                msgs[m++] = md;
+            }
         }
     }
+    if (!head || threadIdx.x != 0) return;
+    const bool last_off = nb >= n && !(dl.opcode <= 2 && dl.payload_len == P &&
+                                       dl.header_size + ((dl.flags & UVHTTP_WS_FLAG_MASK) ? 4u : 0u) == S - P);
+    if (sb < nb || last_off) {
+        ws.ctl[kCtlGate] = a.epoch;
+        return;
+    }
+    uint32_t nfin = tot_fin;
+    uint32_t ls = tot_key ? (tot_key >> 1) - 1 : kNoFrame;
+    bool bin = tot_key & 1u;
+    uvhttp_ws_batch_summary_t sm;
+    sm.n_frames = n;
+    sm.state_closed = 0;
+    uint32_t nd;  // frames delivered, every one P bytes of data
+    bool open;    // the last of them leaves its message open
+    if (nb < n) {  // its local status, or (locally valid) the fragment check's
+        nd = nb;
+        uvhttp_ws_frame_desc_t d;
+        (void)parse_one(a, nb, seg_info(a, nb, n), d);
+        sm.first_status = d.status != UVHTTP_WS_FRAME_OK ? d.status : UVHTTP_WS_FRAME_ERR_FRAGMENT;
+        sm.consumed_bytes = (uint64_t)nb * S;
+        open = nb > 0 && !(info[nb - 1] & kI8Fin);
+    } else {  // every frame, the last one (a uniform data frame) included
+        nd = n;
+        sm.first_status = 0;
+        sm.consumed_bytes = (uint64_t)(n - 1) * S + dl.wire_len;
+        if (dl.opcode != 0) {
+            ls = n - 1;
+            bin = dl.opcode == 2;
+        }
+        open = !(dl.flags & UVHTTP_WS_FLAG_FIN);
+        if (!open) {  // the last frame's message
+            uvhttp_ws_message_desc_t md;
+            md.arena_off = (uint64_t)ls * P;
+            md.len = (uint64_t)(n - ls) * P;
+            md.first_frame = ls;
+            md.last_frame = n - 1;
+            md.opcode = bin ? 2 : 1;
+            md.reserved = 0;
+            msgs[nfin++] = md;
+        }
+    }
+    sm.n_delivered = nd;
+    sm.status = sm.first_status < 0 ? -1 : 0;
+    sm.payload_bytes = (uint64_t)nd * P;
+    sm.n_messages = nfin;
+    sm.arena_bytes = sm.payload_bytes;
+    sm.pending_bytes = open ? (uint64_t)(nd - ls) * P : 0;
+    *a.summary = sm;
 }
 
 // ------------------------------------------------------------------------------------
@@ -4963,8 +4982,7 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
             timing_end(e, stk, s);
             const uint32_t n_parts = (a.n + kBlock * kScanFpt - 1) / (kBlock * kScanFpt);
             hipLaunchKernelGGL(k_sum_scan<false>, dim3(n_parts), dim3(kBlock), 0, s, a, e->ws);
-            hipLaunchKernelGGL(k_sum_tail<false>, dim3(kSumTailGrid), dim3(kBlock), 0, s, a, e->ws, n_parts,
-                               (uvhttp_ws_message_desc_t*)nullptr);
+            hipLaunchKernelGGL(k_sum_tail, dim3(kSumTailGrid), dim3(kBlock), 0, s, a, e->ws, n_parts);
             hipError_t hs = hipGetLastError();
             if (prev != e->device) (void)hipSetDevice(prev);
             if (hs != hipSuccess) return set_err(e, UVHTTP_WS_GPU_ELAUNCH, "launch", hs);
@@ -5059,8 +5077,7 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
         if (sum_c) {
             const uint32_t n_parts = (a.n + kBlock * kScanFpt - 1) / (kBlock * kScanFpt);
             hipLaunchKernelGGL(k_sum_scan<true>, dim3(n_parts), dim3(kBlock), 0, s, a, e->ws);
-            hipLaunchKernelGGL(k_sum_tail<true>, dim3(1), dim3(kBlock), 0, s, a, e->ws, n_parts, d_msgs);
-            hipLaunchKernelGGL(k_sum_msgs, dim3(n_parts), dim3(kBlock), 0, s, a, e->ws, d_msgs);
+            hipLaunchKernelGGL(k_sum_msgs, dim3(n_parts), dim3(kBlock), 0, s, a, e->ws, n_parts, d_msgs);
             a.recs = nullptr;  // the fallback's k_plan gathers the headers
             a.gate = 1;
         }
