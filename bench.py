@@ -224,16 +224,21 @@ def cpu_baseline_threads(L, orc, cfg_name, seconds):
 
 
 def pmc_traffic(cfg_name, mode):
-    """HBM bytes per payload-kernel launch measured with rocprofv3 PMC counters (collected by
-    tools/profile.sh into profiles/, FETCH_SIZE doubled per the gfx950 calibration)."""
-    p = os.path.join(REPO, "profiles", f"traffic_{cfg_name}_{mode}.json")
+    """(HBM bytes per payload-kernel launch, source) measured with rocprofv3 PMC counters
+    (collected by tools/profile.sh / tools/pmc_traffic.py into profiles/, FETCH_SIZE doubled per
+    the gfx950 calibration); source names the file and the run tag it came from."""
+    name = f"traffic_{cfg_name}_{mode}.json"
+    p = os.path.join(REPO, "profiles", name)
     if not os.path.exists(p):
-        return None
+        return None, None
     try:
         with open(p) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
+            d = json.load(f)
     except (OSError, ValueError):
-        return None
+        return None, None
+    src = f"profiles/{name}" + (f" (run {d['tag']}, kernel avg {d.get('payload_kernel_avg_ns_rocprof', 0) / 1e3:.1f} us)"
+                                if d.get("tag") else "")
+    return d.get("hbm_bytes_per_launch"), src
 
 
 def free_port():
@@ -723,7 +728,7 @@ def main():
         alg_bytes = n * (plen + header_size(plen) + (4 if args.mode == "build_masked" else 0) + plen)
     avg_kernel_s = (k_ms / 1e3 / k_n) if k_n else float("nan")
     achieved = alg_bytes / avg_kernel_s / 1e9 if k_n else None
-    traffic = pmc_traffic(cfg, args.mode)
+    traffic, traffic_src = pmc_traffic(cfg, args.mode + ("_summary_only" if getattr(args, "no_desc", False) else ""))
     ceiling = None
     if rank == 0 and not args.stub and not args.no_ceiling:
         ceiling = wl.copy_ceiling()
@@ -812,6 +817,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                 "traffic": traffic,
+                "traffic_source": traffic_src,
                 "alg_bytes_per_launch": alg_bytes,
                 "avg_kernel_us": round(kern_us, 2) if kern_us else None,
                 "avg_kernel_source": kern_src,
