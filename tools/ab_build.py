@@ -33,7 +33,7 @@ def main():
     dev = "cuda"
     d = torch.from_numpy(fr.view(np.uint8).copy()).to(dev)
     src = torch.randint(0, 256, (n * plen + 64,), dtype=torch.uint8, device=dev)
-    outs = [torch.empty(n * (plen + 14) + 64, dtype=torch.uint8, device=dev) for _ in engs]
+    outs = [torch.zeros(n * (plen + 14) + 64, dtype=torch.uint8, device=dev) for _ in engs]
     offs = [torch.zeros(n + 1, dtype=torch.int64, device=dev) for _ in engs]
     st = torch.cuda.current_stream()
     K, R = 20, 7
@@ -58,7 +58,7 @@ def main():
                 kern[k].append(ms / max(cnt, 1))
     ref = outs[0]
     for k, p in enumerate(libs):
-        same = bool(torch.equal(outs[k], ref))
+        same = bool(torch.equal(outs[k], ref)) and bool(torch.equal(offs[k], offs[0]))
         print(f"{sys.argv[1]} {os.path.basename(p):24s} step {statistics.median(step[k]) * 1e3:8.1f} us  "
               f"kb_emit {statistics.median(kern[k]) * 1e3:8.1f} us  same_as_first={same}", flush=True)
 

@@ -3709,6 +3709,7 @@ struct BuildArgs {
     uint32_t map_shift;  // log2 of the map tile (>= the emit tile; ~ the average frame size)
     uint32_t epoch;      // tag of this call's map records (stale records never match)
     uint32_t group;      // kb_emit_frames: frames per workgroup (<= kEmitF)
+    uint32_t n_groups;   // grp[n_groups] = the total output bytes
     const uint32_t* ctl; // captured calls (dev_epoch): the epoch is ctl[kCtlEpoch]
     uint32_t dev_epoch;
 };
@@ -3723,12 +3724,39 @@ __device__ inline uint64_t build_size(const uvhttp_ws_build_desc_t& f) {
 }
 
 
+// per 256-frame block: the frames' sizes, their offsets within the block (out_off, made final by
+// kb_emit_frames or kb_offsets) and the block's total (blk)
 __global__ __launch_bounds__(kBlock) void kb_size(BuildArgs b) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     const uint64_t sz = i < b.n ? build_size(b.frames[i]) : 0;
     uint64_t total;
-    (void)block_exclusive_sum_u64(sz, &total);
+    const uint64_t local = block_exclusive_sum_u64(sz, &total);
+    if (i < b.n) b.out_off[i] = local;
     if (threadIdx.x == 0) b.blk[blockIdx.x] = total;
+}
+
+// the block totals' exclusive prefixes in one workgroup when there are at most kScanOne of them
+// (batches of <= 1 M frames; one launch instead of kb_scan_groups + kb_scan_top): blk[k] becomes
+// the prefix, grp[0 .. n_groups) = 0 and grp[n_groups] the total, the two-level layout's meaning
+constexpr uint32_t kScanOnePer = 16, kScanOne = kBlock * kScanOnePer;
+__global__ __launch_bounds__(kBlock) void kb_scan_one(BuildArgs b, uint32_t n_blocks) {
+    uint64_t v[kScanOnePer], run = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanOnePer; ++k) {
+        const uint32_t g = threadIdx.x * kScanOnePer + k;
+        v[k] = g < n_blocks ? b.blk[g] : 0;
+        run += v[k];
+    }
+    uint64_t total;
+    uint64_t pre = block_exclusive_sum_u64(run, &total);
+#pragma unroll
+    for (uint32_t k = 0; k < kScanOnePer; ++k) {
+        const uint32_t g = threadIdx.x * kScanOnePer + k;
+        if (g < n_blocks) b.blk[g] = pre;
+        pre += v[k];
+    }
+    for (uint32_t g = threadIdx.x; g < b.n_groups; g += kBlock) b.grp[g] = 0;
+    if (threadIdx.x == 0) b.grp[b.n_groups] = total;
 }
 
 __global__ __launch_bounds__(kBlock) void kb_scan_groups(BuildArgs b, uint32_t n_blocks) {
@@ -3963,11 +3991,18 @@ __global__ __launch_bounds__(BLOCK) void kb_emit(BuildArgs b, uint64_t tile_base
 // unaligned 16-byte source load — no per-tile map records and no per-vector frame search
 // over the whole tile.
 constexpr uint32_t kEmitF = 256;         // frames per workgroup at most (one per thread; FMAX)
-constexpr uint32_t kEmitWin = 20480;     // LDS window bytes (64 frames of <= 300 bytes: one window)
+#ifndef UVWS_EMIT_WIN
+#define UVWS_EMIT_WIN 20480
+#endif
+constexpr uint32_t kEmitWin = UVWS_EMIT_WIN;  // LDS window bytes (64 frames of <= 300 bytes: one window)
 constexpr uint32_t kEmitItems = 1280;    // item -> frame table entries (one-window workgroups; 5 per thread)
 
 template <int BLOCK, int FMAX>
-__global__ __launch_bounds__(BLOCK) void kb_emit_frames(BuildArgs b) {
+__global__ __launch_bounds__(BLOCK)
+#ifdef UVWS_EMIT_WPE
+__attribute__((amdgpu_waves_per_eu(UVWS_EMIT_WPE)))
+#endif
+void kb_emit_frames(BuildArgs b) {
     __shared__ u32x4 s_win[kEmitWin / 16];
     __shared__ uint64_t s_ps[FMAX], s_fe[FMAX], s_sp[FMAX], s_st[FMAX];
     __shared__ uint32_t s_key[FMAX];
@@ -3977,18 +4012,31 @@ __global__ __launch_bounds__(BLOCK) void kb_emit_frames(BuildArgs b) {
     __shared__ uint8_t s_fof[kEmitItems];  // frame of item q (a workgroup with one window)
     __shared__ uint32_t s_wsum[BLOCK / 64];
 
-    const uint64_t total = b.out_off[b.n];
-    if (total > b.out_cap) return;  // nothing is written (as kb_emit)
+    // the offsets: kb_size left each frame's within its 256-frame block, the scans the blocks'
+    // (grp + blk); this kernel writes the final ones (the API's out_off) — also when the output
+    // does not fit, where nothing else is written (as kb_emit)
+    const uint64_t total = b.grp[b.n_groups];
     const uint32_t f0 = blockIdx.x * b.group;
     if (f0 >= b.n) return;
     const uint32_t nf = b.n - f0 < b.group ? b.n - f0 : b.group;
+    if (total > b.out_cap) {
+        if (threadIdx.x < nf) {
+            const uint32_t f = f0 + threadIdx.x;
+            b.out_off[f] += b.grp[f / (kBlock * kBlock)] + b.blk[f / kBlock];
+            if (f + 1 == b.n) b.out_off[b.n] = total;
+        }
+        return;
+    }
     static_assert(BLOCK >= FMAX && FMAX <= 256, "one thread per frame; frame ids fit a byte");
     {
         const uint32_t j = threadIdx.x, lane = j & 63, wave = j >> 6;
         uint32_t nv = 0;
         if (j < nf) {
-            const uvhttp_ws_build_desc_t d = b.frames[f0 + j];
-            const uint64_t st = b.out_off[f0 + j];
+            const uint32_t f = f0 + j;
+            const uvhttp_ws_build_desc_t d = b.frames[f];
+            const uint64_t st = b.out_off[f] + b.grp[f / (kBlock * kBlock)] + b.blk[f / kBlock];
+            b.out_off[f] = st;
+            if (f + 1 == b.n) b.out_off[b.n] = total;
             uint32_t hm;
             s_img[j] = build_header(d, &hm);
             s_st[j] = st;
@@ -4090,17 +4138,18 @@ __global__ __launch_bounds__(BLOCK) void kb_emit_frames(BuildArgs b) {
         if (one && b.src_len >= 16) {
             // every item's 16-byte source load issued before any LDS work (an out-of-range
             // window loads from offset 0 and is redone bytewise below)
+            // (only the loaded vectors stay in registers across the loads' flight; the item's
+            // addresses are recomputed from LDS afterwards: 96 -> fewer VGPRs)
             constexpr int kIpt = kEmitItems / BLOCK;
             u32x4 w[kIpt];
-            uint64_t oa[kIpt];
-            int64_t ws[kIpt];
 #pragma unroll
             for (int k = 0; k < kIpt; ++k) {
                 const uint32_t q = threadIdx.x + k * BLOCK;
                 const uint32_t j = q < nitems ? s_fof[q] : 0;
-                ws[k] = item_src(q < nitems ? q : s_cp[0], j, &oa[k]);
-                const bool ok = ws[k] >= 0 && (uint64_t)ws[k] + 16 <= b.src_len;
-                __builtin_memcpy(&w[k], b.src + (ok ? ws[k] : 0), 16);
+                uint64_t oa;
+                const int64_t ws = item_src(q < nitems ? q : s_cp[0], j, &oa);
+                const bool ok = ws >= 0 && (uint64_t)ws + 16 <= b.src_len;
+                __builtin_memcpy(&w[k], b.src + (ok ? ws : 0), 16);
             }
             __builtin_amdgcn_sched_barrier(0);
             put_headers();
@@ -4108,8 +4157,11 @@ __global__ __launch_bounds__(BLOCK) void kb_emit_frames(BuildArgs b) {
             for (int k = 0; k < kIpt; ++k) {
                 const uint32_t q = threadIdx.x + k * BLOCK;
                 if (q >= nitems) continue;
-                if (!(ws[k] >= 0 && (uint64_t)ws[k] + 16 <= b.src_len)) w[k] = load16_any(b.src, ws[k], b.src_len);
-                put_item(s_fof[q], oa[k], w[k]);
+                const uint32_t j = s_fof[q];
+                uint64_t oa;
+                const int64_t ws = item_src(q, j, &oa);
+                if (!(ws >= 0 && (uint64_t)ws + 16 <= b.src_len)) w[k] = load16_any(b.src, ws, b.src_len);
+                put_item(j, oa, w[k]);
             }
         } else {
             put_headers();
@@ -5451,10 +5503,21 @@ int uvhttp_ws_gpu_build_frames(uvhttp_ws_gpu_engine_t* e, const uint8_t* d_src, 
     b.epoch = next_epoch(e, s);
     const uint32_t grid_f = n_frames ? (n_frames + kBlock - 1) / kBlock : 1;
     const uint32_t n_groups = (grid_f + kBlock - 1) / kBlock;
+    b.n_groups = n_groups;
+    // sizes -> offsets: kb_size (within 256-frame blocks) and the scan of the block totals (one
+    // workgroup up to 1 M frames); the grouped emit finishes the offsets itself, the tile emit
+    // needs kb_offsets' map records (C4 send side: kb_scan_groups + kb_scan_top + kb_offsets were
+    // 4.8 + 4.6 + 8.6 us of a 130 us step, profiles/r05pmc_c4_build_kernel_stats.csv)
     hipLaunchKernelGGL(kb_size, dim3(grid_f), dim3(kBlock), 0, s, b);
-    hipLaunchKernelGGL(kb_scan_groups, dim3(n_groups), dim3(kBlock), 0, s, b, grid_f);
-    hipLaunchKernelGGL(kb_scan_top, dim3(1), dim3(kBlock), 0, s, b, n_groups);
-    hipLaunchKernelGGL(kb_offsets, dim3(grid_f), dim3(kBlock), 0, s, b, n_groups);
+    if (grid_f <= kScanOne) {
+        hipLaunchKernelGGL(kb_scan_one, dim3(1), dim3(kBlock), 0, s, b, grid_f);
+    } else {
+        hipLaunchKernelGGL(kb_scan_groups, dim3(n_groups), dim3(kBlock), 0, s, b, grid_f);
+        hipLaunchKernelGGL(kb_scan_top, dim3(1), dim3(kBlock), 0, s, b, n_groups);
+    }
+    const uint64_t avg0 = n_frames ? out_cap / n_frames : out_cap;
+    if (!(n_frames && avg0 < e->build_frames_max))
+        hipLaunchKernelGGL(kb_offsets, dim3(grid_f), dim3(kBlock), 0, s, b, n_groups);
     if (!n_frames) {
         // d_out_off[0] = 0 (total) for an empty batch
         (void)hipMemsetAsync(d_out_off, 0, 8, s);
@@ -5464,6 +5527,7 @@ int uvhttp_ws_gpu_build_frames(uvhttp_ws_gpu_engine_t* e, const uint8_t* d_src, 
         // frames per workgroup: as many as keep an average group inside one LDS window and
         // the item table (payload vectors ~ avg / 16 + 1 per frame)
         uint64_t g = kEmitItems / (avg / 16 + 2);
+        if (g > kEmitWin / (avg + 16)) g = kEmitWin / (avg + 16);
         if (g > kEmitF) g = kEmitF;
         if (g < 1) g = 1;
         // up to 64 frames the smaller LDS footprint keeps 6 workgroups per CU (256-byte frames:
