@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Interleaved A/B of two builds of libuvhttp_ws_amd.so in ONE process on one device.
 
-  python tools/ab_lib.py LIB_A LIB_B cfg:mode [cfg:mode ...]     (mode: inplace | inplace_nd | compact)
+  python tools/ab_lib.py LIB_A LIB_B cfg:mode [cfg:mode ...]     (mode: inplace | inplace_nd | compact | streams)
 
 LIB_B may be "tree" for the in-tree build.  AB_STAMPS=1 turns engine B's device stamps on;
 AB_ENV_B="K=V,..." sets environment switches for engine B only.  Each round runs K decode steps with engine A,
@@ -50,6 +50,21 @@ def main():
         wire = torch.empty(wl + 64, dtype=torch.uint8, device="cuda")
         engs[0].gen_frames(wire, n, plen, 7, opcode0=2, fragmented=frag)
         mm = 256 << 20
+        sdev = None
+        if mode == "streams":  # bench.py's layout: 4096 connections when fragmented, else one per frame
+            import numpy as np
+            conns = 4096 if frag else n
+            per = n // conns
+            sa = np.zeros(conns, dtype=U.STREAM_DT)
+            sa["begin"] = np.arange(conns, dtype=np.uint64) * per * stride
+            sa["len"] = per * stride
+            sa["recv_buffer_size"] = max(65536, per * stride)
+            sa["max_frame_size"], sa["max_message_size"], sa["is_server"] = 16 << 20, mm, 1
+            if frag:
+                sa["pending_bytes"][1:] = 1
+                sa["pending_opcode"] = 2
+            sdev = torch.from_numpy(sa.view(np.uint8).copy()).to("cuda")
+            sres = [torch.empty(conns * U.STREAM_RESULT_BYTES, dtype=torch.uint8, device="cuda") for _ in engs]
         outs = []
         for e in engs:
             desc, summ = e.alloc_outputs(n)
@@ -60,7 +75,9 @@ def main():
         def run(k):
             e = engs[k]
             desc, summ, arena, msgs = outs[k]
-            if mode in ("inplace", "inplace_nd"):
+            if mode == "streams":
+                e.decode_streams(wire, sdev, conns, n, desc=desc, results=sres[k], wire_len=wl, stream=st)
+            elif mode in ("inplace", "inplace_nd"):
                 e.decode_inplace(wire, n, stride=stride, max_message_size=mm, wire_len=wl,
                                  desc=desc, summary=summ, stream=st, no_desc=mode == "inplace_nd")
             else:
@@ -87,8 +104,13 @@ def main():
                     step[k].append(a.elapsed_time(b) / K)
                     kern[k].append(ms / max(cnt, 1))
         for k in (0, 1):
-            s = engs[k].read_summary(outs[k][1])
-            if not os.environ.get("AB_NOCHECK"):  # experiment builds may decode wrongly
+            if os.environ.get("AB_NOCHECK"):  # experiment builds may decode wrongly
+                continue
+            if mode == "streams":
+                rs = engs[k].read_stream_results(sres[k], conns)
+                assert all(x.status == 0 for x in rs) and sum(x.n_delivered for x in rs) == n, names[k]
+            else:
+                s = engs[k].read_summary(outs[k][1])
                 assert s["n_delivered"] == n and s["status"] == 0, (names[k], s)
         ms = [statistics.median(x) for x in step]
         ks = [statistics.median(x) for x in kern]
