@@ -353,7 +353,11 @@ int uvhttp_ws_gpu_engine_sync(uvhttp_ws_gpu_engine_t* eng, void* stream);
 #define UVHTTP_WS_STAMP_PAYLOAD 5     /* the payload kernel (unmask / scatter / gather) */
 #define UVHTTP_WS_STAMP_PLAN 6        /* k_plan */
 #define UVHTTP_WS_STAMP_FIXUP 7       /* k_fixup (fused stride path) */
-#define UVHTTP_WS_STAMP_FINALIZE 8    /* k_finalize */
+#define UVHTTP_WS_STAMP_FINALIZE 8    /* k_finalize; summary-only compact: k_sum_msgs */
+#define UVHTTP_WS_STAMP_BUILD_SIZE 9  /* send side: kb_size (the emit kernels stamp as PAYLOAD) */
+#define UVHTTP_WS_STAMP_BUILD_SCAN 10 /* kb_scan_one / kb_scan_groups */
+#define UVHTTP_WS_STAMP_BUILD_SCAN2 11 /* kb_scan_top */
+#define UVHTTP_WS_STAMP_BUILD_OFFSETS 12 /* kb_offsets (tile emit only) */
 typedef struct {
     uint32_t call;      /* the call's tag: 1 .. 2^24 - 1, one more per decode call (after
                            2^24 - 1 wraps to 1); records come oldest call first */

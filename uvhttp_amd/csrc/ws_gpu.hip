@@ -3712,6 +3712,7 @@ struct BuildArgs {
     uint32_t n_groups;   // grp[n_groups] = the total output bytes
     const uint32_t* ctl; // captured calls (dev_epoch): the epoch is ctl[kCtlEpoch]
     uint32_t dev_epoch;
+    uint64_t* stamp;     // device-side kernel stamps (diagnostics), or null
 };
 
 __device__ inline void resolve_epoch(BuildArgs& b) {
@@ -3727,6 +3728,7 @@ __device__ inline uint64_t build_size(const uvhttp_ws_build_desc_t& f) {
 // per 256-frame block: the frames' sizes, their offsets within the block (out_off, made final by
 // kb_emit_frames or kb_offsets) and the block's total (blk)
 __global__ __launch_bounds__(kBlock) void kb_size(BuildArgs b) {
+    StampScope stamp_(b.stamp, b.epoch, UVHTTP_WS_STAMP_BUILD_SIZE);
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     const uint64_t sz = i < b.n ? build_size(b.frames[i]) : 0;
     uint64_t total;
@@ -3740,6 +3742,7 @@ __global__ __launch_bounds__(kBlock) void kb_size(BuildArgs b) {
 // the prefix, grp[0 .. n_groups) = 0 and grp[n_groups] the total, the two-level layout's meaning
 constexpr uint32_t kScanOnePer = 16, kScanOne = kBlock * kScanOnePer;
 __global__ __launch_bounds__(kBlock) void kb_scan_one(BuildArgs b, uint32_t n_blocks) {
+    StampScope stamp_(b.stamp, b.epoch, UVHTTP_WS_STAMP_BUILD_SCAN);
     uint64_t v[kScanOnePer], run = 0;
 #pragma unroll
     for (uint32_t k = 0; k < kScanOnePer; ++k) {
@@ -3760,6 +3763,7 @@ __global__ __launch_bounds__(kBlock) void kb_scan_one(BuildArgs b, uint32_t n_bl
 }
 
 __global__ __launch_bounds__(kBlock) void kb_scan_groups(BuildArgs b, uint32_t n_blocks) {
+    StampScope stamp_(b.stamp, b.epoch, UVHTTP_WS_STAMP_BUILD_SCAN);
     const uint32_t k = blockIdx.x * kBlock + threadIdx.x;
     const uint64_t v = k < n_blocks ? b.blk[k] : 0;
     uint64_t total;
@@ -3769,6 +3773,7 @@ __global__ __launch_bounds__(kBlock) void kb_scan_groups(BuildArgs b, uint32_t n
 }
 
 __global__ __launch_bounds__(kBlock) void kb_scan_top(BuildArgs b, uint32_t n_groups) {
+    StampScope stamp_(b.stamp, b.epoch, UVHTTP_WS_STAMP_BUILD_SCAN2);
     constexpr int kPer = 4;
     uint64_t v[kPer], run = 0;
 #pragma unroll
@@ -3817,6 +3822,7 @@ __device__ inline u32x4 build_header(const uvhttp_ws_build_desc_t& d, uint32_t* 
 
 __global__ __launch_bounds__(kBlock) void kb_offsets(BuildArgs b, uint32_t n_groups) {
     resolve_epoch(b);
+    StampScope stamp_(b.stamp, b.epoch, UVHTTP_WS_STAMP_BUILD_OFFSETS);
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     const uint64_t sz = i < b.n ? build_size(b.frames[i]) : 0;
     uint64_t total;
@@ -3877,6 +3883,7 @@ __device__ inline void build_vector(const BuildArgs& b, uint64_t oa, uint64_t fs
 template <int BLOCK, int VPT>
 __global__ __launch_bounds__(BLOCK) void kb_emit(BuildArgs b, uint64_t tile_base) {
     resolve_epoch(b);
+    StampScope stamp_(b.stamp, b.epoch, UVHTTP_WS_STAMP_PAYLOAD, false);
     constexpr uint64_t kT = (uint64_t)BLOCK * VPT * 16;
     __shared__ uint64_t s_start[BLOCK];  // frame start in out
     __shared__ uint64_t s_pstart[BLOCK]; // payload start in out
@@ -3885,7 +3892,7 @@ __global__ __launch_bounds__(BLOCK) void kb_emit(BuildArgs b, uint64_t tile_base
     __shared__ uint32_t s_key[BLOCK];    // 0 for server frames (XOR no-op)
     __shared__ u32x4 s_hdr[BLOCK];       // header image (<= 14 bytes)
 
-    const uint64_t t0 = (tile_base + blockIdx.x) * kT;
+    const uint64_t t0 = (tile_base + stamp_.anchor_s(blockIdx.x)) * kT;
     // map tiles are a power of two >= kT (host), so the tile lies inside map tile c0
     const uint64_t c0 = t0 >> b.map_shift, c1 = c0 + 1;
     if (c0 >= b.n_map) return;
@@ -4012,11 +4019,12 @@ void kb_emit_frames(BuildArgs b) {
     __shared__ uint8_t s_fof[kEmitItems];  // frame of item q (a workgroup with one window)
     __shared__ uint32_t s_wsum[BLOCK / 64];
 
+    StampScope stamp_(b.stamp, b.epoch, UVHTTP_WS_STAMP_PAYLOAD, false);
     // the offsets: kb_size left each frame's within its 256-frame block, the scans the blocks'
     // (grp + blk); this kernel writes the final ones (the API's out_off) — also when the output
     // does not fit, where nothing else is written (as kb_emit)
     const uint64_t total = b.grp[b.n_groups];
-    const uint32_t f0 = blockIdx.x * b.group;
+    const uint32_t f0 = stamp_.anchor_s(blockIdx.x) * b.group;
     if (f0 >= b.n) return;
     const uint32_t nf = b.n - f0 < b.group ? b.n - f0 : b.group;
     if (total > b.out_cap) {
@@ -5501,6 +5509,7 @@ int uvhttp_ws_gpu_build_frames(uvhttp_ws_gpu_engine_t* e, const uint8_t* d_src, 
     b.ctl = e->ctl;
     b.dev_epoch = e->capturing ? 1u : 0u;
     b.epoch = next_epoch(e, s);
+    b.stamp = (e->stamp_on && !e->capturing) ? e->stamp_mem : nullptr;
     const uint32_t grid_f = n_frames ? (n_frames + kBlock - 1) / kBlock : 1;
     const uint32_t n_groups = (grid_f + kBlock - 1) / kBlock;
     b.n_groups = n_groups;
