@@ -513,9 +513,9 @@ class GpuWorkload:
         """Device-side kernel stamps (uvhttp_ws_gpu_engine_set_stamps) over `calls` more steps
         after the timed region, same process and buffers: when each kernel of a call ran on the
         device, so the payload kernel's own duration (no timing event beside it) and the gaps
-        between kernels and between calls are measured where they happen.  None for the send
-        side (its kernels are not stamped)."""
-        if self.build_dev is not None or self.graph is not None:
+        between kernels and between calls are measured where they happen (the send side's
+        kernels too: kb_size, the scans, the emit kernel as "payload")."""
+        if self.graph is not None:
             return None
         eng = self.eng
         if getattr(self, "stamped_timed", False):
