@@ -156,6 +156,25 @@ def test_graph_capture_replay_changing_batches(torch):
         assert got == ref["summary"], (k, got, ref["summary"])
         assert np.array_equal(wire[:wl].cpu().numpy(), ref["wire"]), k
         assert np.array_equal(eng.read_desc(desc, n)["status"], ref["status"]), k
+    # host calls after the replays, then replays again: the workspace holds the replays' tags,
+    # whose device epochs are larger than any host call's — the host call's claims (first
+    # failure, tile maps) must still win over them (round 5: they did not, and a host call after
+    # a replay delivered frames after a failure)
+    for k in [2, 0, 3]:
+        host = load(k)
+        eng.decode_inplace(wire, n, offsets=offs, wire_len=wl, desc=desc, summary=summ, stream=s)
+        s.synchronize()
+        ref = _oracle.decode_batch(host, n, offsets=batches[k][1], wire_len=wl)
+        assert eng.read_summary(summ) == ref["summary"], ("host after replay", k)
+        assert np.array_equal(wire[:wl].cpu().numpy(), ref["wire"]), ("host after replay", k)
+        assert np.array_equal(eng.read_desc(desc, n)["status"], ref["status"]), ("host after replay", k)
+        host = load((k + 1) % 4)
+        t.cuda.synchronize()
+        g.replay()
+        t.cuda.synchronize()
+        ref = _oracle.decode_batch(host, n, offsets=batches[(k + 1) % 4][1], wire_len=wl)
+        assert eng.read_summary(summ) == ref["summary"], ("replay after host", k)
+        assert np.array_equal(wire[:wl].cpu().numpy(), ref["wire"]), ("replay after host", k)
     eng.sync()
     eng.close()
 
@@ -225,5 +244,23 @@ def test_graph_capture_replay_stride_batches(torch):
         assert eng.read_summary(summ) == ref["summary"], k
         assert np.array_equal(wire[:wl].cpu().numpy(), ref["wire"]), k
         assert np.array_equal(eng.read_desc(desc, n)["status"], ref["status"]), k
+    # host calls (fused path, summary-only, compact) after the replays: their failure claims must
+    # displace the replays' larger-epoch tags
+    for k, mode in ((1, "desc"), (3, "no_desc"), (1, "compact")):
+        host = np.frombuffer(batches[k], np.uint8).copy()
+        wire[:wl].copy_(t.from_numpy(host))
+        ref = _oracle.decode_batch(host, n, stride=stride, wire_len=wl, compact=mode == "compact",
+                                   arena_cap=wl + 64)
+        if mode == "compact":
+            arena = t.zeros(wl + 64, dtype=t.uint8, device="cuda")
+            eng.decode_compact(wire, n, arena, stride=stride, wire_len=wl, desc=desc, summary=summ, stream=s)
+        else:
+            eng.decode_inplace(wire, n, stride=stride, wire_len=wl, desc=desc, summary=summ, stream=s,
+                               no_desc=mode == "no_desc")
+        s.synchronize()
+        assert eng.read_summary(summ) == ref["summary"], ("host after replay", k, mode)
+        assert np.array_equal(wire[:wl].cpu().numpy(), ref["wire"]), ("host after replay", k, mode)
+        g.replay()
+        t.cuda.synchronize()
     eng.sync()
     eng.close()

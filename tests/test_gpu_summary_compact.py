@@ -262,3 +262,20 @@ def test_repeated_calls_and_graph(torch, engines):
         assert np.array_equal(m["arena_off"], ref["msg_off"])
         assert np.array_equal(m["len"], ref["msg_len"])
     assert GUARD and U
+
+
+@pytest.mark.parametrize("n", [1, 2, 3])
+def test_tiny_batches(torch, engines, n):
+    """one to three frames: the last frame's part and message are block 0's alone (fragments
+    open or closed, a failure at frame 0, a control or reserved-opcode last frame)"""
+    rng = random.Random(100 + n)
+    stride = 264
+    p = _uniform_p(stride)
+    for frag in (0.0, 1.0):
+        _check(torch, engines, _batch(rng, n, stride, frag=frag), n, stride, fast=True)
+    _check(torch, engines, _batch(rng, n, stride, tweak=_tweak("rsv", 0, p)), n, stride, fast=True)
+    _check(torch, engines, _batch(rng, n, stride, tweak=_tweak("reserved_opcode", n - 1, p)), n, stride,
+           fast=False)
+    w = _batch(rng, n - 1, stride, frag=0.0) if n > 1 else np.zeros(0, np.uint8)
+    last = np.frombuffer(_frame(9, 1, b"pi", rng.randbytes(4)), np.uint8)
+    _check(torch, engines, np.concatenate([w, last]), n, stride, fast=False)

@@ -332,3 +332,19 @@ def test_repeated_calls_and_graph(torch, engines):
         assert e.read_summary(summ) == ref["summary"]
         assert np.array_equal(d[: w.size].cpu().numpy(), ref["wire"])
     assert GUARD and U
+
+
+@pytest.mark.parametrize("n", [1, 2, 3])
+def test_tiny_batches(torch, engines, n):
+    """one to three frames: the last frame's part is the tail's alone"""
+    rng = random.Random(200 + n)
+    stride = 264
+    p, _ = _payload_for(stride)
+    for frag in (0.0, 1.0):
+        _check(torch, engines, _batch(rng, n, stride, frag=frag), n, stride)
+    for kind in ("rsv", "bad_opcode"):
+        _check(torch, engines, _batch(rng, n, stride, tweak=_fail_tweak(kind, n - 1, p)), n, stride)
+    w = _batch(rng, n - 1, stride, frag=0.0) if n > 1 else np.zeros(0, np.uint8)
+    last = np.frombuffer(_frame(8, 1, b"\x03\xe8", rng.randbytes(4)), np.uint8)
+    r = _check(torch, engines, np.concatenate([w, last]), n, stride)
+    assert r["summary"]["state_closed"] == 1

@@ -265,8 +265,22 @@ constexpr uint32_t kMaxHostEpoch = kMaxEpoch / 2;
 __device__ inline uint64_t tag_of(uint32_t epoch, uint32_t frame) {
     return ((uint64_t)epoch << 32) | (uint32_t)~frame;
 }
+// A host call after graph replays meets entries the replays tagged with their (larger, device)
+// epochs, which a max never displaces: such an entry is replaced by compare-and-swap (then this
+// call's claims order by max again).  The common case is one atomicMax.
 __device__ inline void tag_claim(uint64_t* p, uint32_t epoch, uint32_t frame) {
-    atomicMax(reinterpret_cast<unsigned long long*>(p), (unsigned long long)tag_of(epoch, frame));
+    unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
+    const unsigned long long mine = tag_of(epoch, frame);
+    unsigned long long cur = atomicMax(q, mine);
+    while ((uint32_t)(cur >> 32) > epoch) {  // a later epoch's entry
+        const unsigned long long seen = atomicCAS(q, cur, mine);
+        if (seen == cur) return;
+        cur = seen;
+        if ((uint32_t)(cur >> 32) <= epoch) {  // another claim of this call replaced it first
+            atomicMax(q, mine);
+            return;
+        }
+    }
 }
 __device__ inline uint32_t tag_get(uint64_t v, uint32_t epoch, uint32_t none) {
     return (uint32_t)(v >> 32) == epoch ? ~(uint32_t)v : none;
