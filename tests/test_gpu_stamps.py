@@ -91,3 +91,32 @@ def test_stamps_stream_decode(torch):
         assert all(x.status == 0 and x.n_delivered == 1 for x in r)
     finally:
         eng.close()
+
+
+def test_stamps_send_side(torch):
+    """the send side stamps its kernels too: kb_size, the block scan and the emit kernel (as
+    "payload"; the tile emit adds kb_offsets), one call after another"""
+    import numpy as np
+    import uvhttp_amd as U
+    eng = U.GpuEngine(0)
+    try:
+        for n, plen, kinds in ((65536, 256, {"build_size", "build_scan", "payload"}),
+                               (2048, 16384, {"build_size", "build_scan", "build_offsets", "payload"})):
+            fr = np.zeros(n, dtype=[("po", "<u8"), ("pl", "<u8"), ("key", "<u4"), ("op", "u1"),
+                                    ("fin", "u1"), ("mask", "u1"), ("r0", "u1"), ("r1", "<u8")])
+            fr["po"] = np.arange(n, dtype=np.uint64) * plen
+            fr["pl"], fr["op"], fr["fin"] = plen, 2, 1
+            d = torch.from_numpy(fr.view(np.uint8).copy()).to("cuda")
+            src = torch.randint(0, 256, (n * plen + 64,), dtype=torch.uint8, device="cuda")
+            out = torch.zeros(n * (plen + 14) + 64, dtype=torch.uint8, device="cuda")
+            eng.set_stamps(True)
+            eng.read_stamps()
+            for _ in range(3):
+                off = eng.build_frames(src, d, n, out)
+            torch.cuda.synchronize()
+            recs = eng.read_stamps()
+            eng.set_stamps(False)
+            _check_calls(recs, kinds, 3)
+            assert int(off[n].item()) == n * (plen + (2 if plen < 126 else 4 if plen < 65536 else 10))
+    finally:
+        eng.close()
