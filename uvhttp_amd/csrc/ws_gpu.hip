@@ -266,11 +266,17 @@ __device__ inline uint64_t tag_of(uint32_t epoch, uint32_t frame) {
     return ((uint64_t)epoch << 32) | (uint32_t)~frame;
 }
 // A host call after graph replays meets entries the replays tagged with their (larger, device)
-// epochs, which a max never displaces: such an entry is replaced by compare-and-swap (then this
-// call's claims order by max again).  The common case is one atomicMax.
-__device__ inline void tag_claim(uint64_t* p, uint32_t epoch, uint32_t frame) {
+// epochs, which a max never displaces: on an engine that has captured calls (cas: BatchArgs /
+// WalkArgs cas_claims) such an entry is replaced by compare-and-swap, then this call's claims
+// order by max again — one returning atomicMax in the common case.  Engines that never captured
+// a call cannot meet one and keep the fire-and-forget atomicMax.
+__device__ inline void tag_claim(uint64_t* p, uint32_t epoch, uint32_t frame, uint32_t cas) {
     unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
     const unsigned long long mine = tag_of(epoch, frame);
+    if (!cas) {
+        atomicMax(q, mine);
+        return;
+    }
     unsigned long long cur = atomicMax(q, mine);
     while ((uint32_t)(cur >> 32) > epoch) {  // a later epoch's entry
         const unsigned long long seen = atomicCAS(q, cur, mine);
@@ -387,6 +393,7 @@ struct BatchArgs {
                              // (frame i's payload at arena offset i * spec_P); 0 = none
     uint32_t gate;           // k_plan / k_spec_fix run only when ws.ctl[kCtlGate] holds this call's
                              // epoch (the summary-only compact decode's fallback)
+    uint32_t cas_claims;     // the engine has captured calls: tag_claim displaces later epochs
 };
 
 // ------------------------------------------------------------------------------------
@@ -745,7 +752,7 @@ __device__ inline void resolve_one(const BatchArgs& a, uvhttp_ws_message_desc_t*
         // wrapping for an offset-table entry near 2^64)
         for (uint64_t t = lo < end ? lo / kMapTile + (lo % kMapTile != 0) : a.n_tiles;
              t * kMapTile < end && t < a.n_tiles; ++t)
-            tag_claim(&ws.tile_first[t], a.epoch, i);
+            tag_claim(&ws.tile_first[t], a.epoch, i, a.cas_claims);
     }
 
     // fragment state before this frame: the latest data frame of the connection, carried
@@ -789,12 +796,12 @@ __device__ inline void resolve_one(const BatchArgs& a, uvhttp_ws_message_desc_t*
                 const uint64_t lo = ex.data_pay, hi = ex.data_pay + d.payload_len;
                 for (uint64_t t = (lo + kMapTile - 1) / kMapTile; t * kMapTile < hi && t < a.n_arena_tiles;
                      ++t)
-                    tag_claim(&ws.arena_first[t], a.epoch, i);
+                    tag_claim(&ws.arena_first[t], a.epoch, i, a.cas_claims);
             }
         }
         d.status = (int8_t)st;
     }
-    if (st != UVHTTP_WS_FRAME_OK) tag_claim(ws.first_bad, a.epoch, i);
+    if (st != UVHTTP_WS_FRAME_OK) tag_claim(ws.first_bad, a.epoch, i, a.cas_claims);
     // speculative compact pass (stride batches): it placed frame i's payload at i * spec_P when
     // the frame looked uniform locally; a delivered frame anywhere else (a control frame, another
     // length, an offset moved by an earlier frame) sends the call to the full scatter (k_spec_fix)
@@ -802,7 +809,7 @@ __device__ inline void resolve_one(const BatchArgs& a, uvhttp_ws_message_desc_t*
                           ex.data_pay != (uint64_t)i * a.spec_P ||
                           d.header_size + ((d.flags & UVHTTP_WS_FLAG_MASK) ? 4u : 0u) !=
                               a.frame_stride - a.spec_P))
-        tag_claim(ws.spec_bad, a.epoch, i);
+        tag_claim(ws.spec_bad, a.epoch, i, a.cas_claims);
 }
 
 // ------------------------------------------------------------------------------------
@@ -977,7 +984,7 @@ __device__ ScanElem lookback_prefix(const Workspace& ws, uint32_t b, const ScanE
         if (gave_up) {
             __hip_atomic_store(&ws.ctl[kCtlFaultEp], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_fetch_add(&ws.ctl[kCtlFaults], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            tag_claim(ws.first_bad, epoch, 0);  // batch mode: the payload pass unmasks nothing
+            tag_claim(ws.first_bad, epoch, 0, 1u);  // batch mode: the payload pass unmasks nothing (rare: always displaces)
         }
     }
     __syncthreads();
@@ -2112,12 +2119,12 @@ __global__ __launch_bounds__(kBlock) void k_sum_scan(BatchArgs a, Workspace ws) 
         pb = x;
     }
     if constexpr (COMPACT) {
-        if (sb != kNoFrame) tag_claim(ws.spec_bad, a.epoch, sb);  // (rare: a batch off the fast path)
+        if (sb != kNoFrame) tag_claim(ws.spec_bad, a.epoch, sb, a.cas_claims);  // (rare: a batch off the fast path)
     }
     const TilePart bp = block_reduce_parts<kBlock>(acc);
     if (threadIdx.x == 0) {
         reinterpret_cast<TilePart*>(ws.parts)[blockIdx.x] = bp;
-        if (bp.ff != kNoFrame) tag_claim(ws.first_bad, a.epoch, bp.ff);
+        if (bp.ff != kNoFrame) tag_claim(ws.first_bad, a.epoch, bp.ff, a.cas_claims);
     }
 }
 
@@ -2852,6 +2859,7 @@ struct WalkArgs {
     uint32_t dev_epoch;
     const uint32_t* ctl;
     uint64_t* stamp;           // device-side kernel stamps (diagnostics), or null
+    uint32_t cas_claims;       // the engine has captured calls (tag_claim)
 };
 
 // process_data's buffer growth: returns false on failure (*out = size then), else the size
@@ -3650,7 +3658,7 @@ __global__ __launch_bounds__(kBlock) void k_stream_desc(WalkArgs w) {
                 uint64_t hi = fe < w.wire_len ? fe : w.wire_len;
                 const uint32_t fi = r.first_frame + k;
                 for (uint64_t t = lo / kMapTile + (lo % kMapTile != 0); t * kMapTile < hi && t < w.n_tiles; ++t)
-                    tag_claim(&w.tile_first[t], epoch, fi);
+                    tag_claim(&w.tile_first[t], epoch, fi, w.cas_claims);
             }
             // message id: FIN data frames delivered before this one in the connection
             const uint64_t fm = __ballot(fin_data);
@@ -3680,7 +3688,7 @@ __global__ __launch_bounds__(kBlock) void k_stream_claims(BatchArgs a, Workspace
     uint64_t hi = frame_end[i];
     if (hi > a.wire_len) hi = a.wire_len;
     for (uint64_t t = lo / kMapTile + (lo % kMapTile != 0); t * kMapTile < hi && t < a.n_tiles; ++t)
-        tag_claim(&ws.tile_first[t], a.epoch, i);
+        tag_claim(&ws.tile_first[t], a.epoch, i, a.cas_claims);
 }
 
 
@@ -4384,6 +4392,7 @@ struct uvhttp_ws_gpu_engine {
     uint64_t* stamp_mem;       // device-side kernel stamps (kStampWords), null until enabled
     int stamp_on;
     int capturing;             // the current call is being captured into a graph
+    int captured_ever;         // a call of this engine was captured (its replays leave later epochs)
     hipStream_t last_stream;   // stream of the previous call (calls are serialised on it)
     int have_last;
     hipEvent_t order_ev;       // orders a call on a new stream after the previous stream's work
@@ -4833,6 +4842,7 @@ static void call_begin(uvhttp_ws_gpu_engine_t* e, hipStream_t s) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(s, &cs) != hipSuccess) cs = hipStreamCaptureStatusNone;
     e->capturing = cs == hipStreamCaptureStatusActive;
+    if (e->capturing) e->captured_ever = 1;
     if (!e->capturing && e->have_last && e->last_stream != s) {
         if (!e->order_ev) (void)hipEventCreateWithFlags(&e->order_ev, hipEventDisableTiming);
         if (e->order_ev && hipEventRecord(e->order_ev, e->last_stream) == hipSuccess)
@@ -5012,6 +5022,7 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
     a.dev_epoch = e->capturing ? 1u : 0u;
     a.epoch = next_epoch(e, s);
     a.stamp = (e->stamp_on && !e->capturing) ? e->stamp_mem : nullptr;
+    a.cas_claims = e->captured_ever ? 1u : 0u;
 
     // stride batches in place: the fused path (payload pass parses the headers, k_plan runs
     // on its records, k_fixup undoes what a failure must leave untouched)
@@ -5382,6 +5393,7 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     w.sc.walk_rec = (w.single && e->wr_cap >= want && e->wr_rec_on) ? (uint2*)e->wr_mem : nullptr;
     w.agg = e->ss.agg;
     w.stamp = (e->stamp_on && !e->capturing) ? e->stamp_mem : nullptr;
+    w.cas_claims = e->captured_ever ? 1u : 0u;
     const uint32_t nsb = (n_streams + kBlock - 1) / kBlock;
     const uint32_t nwb = (n_streams + kBlock / 64 - 1) / (kBlock / 64);
     const int tk_chain = e->time_chain ? timing_begin(e, s) : -1;
@@ -5412,6 +5424,7 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     a.dev_epoch = w.dev_epoch;
     a.epoch = w.epoch;
     a.stamp = w.stamp;
+    a.cas_claims = w.cas_claims;
     // (the wave path's k_stream_desc claimed the tile map already)
     if (!wave_walk)
         hipLaunchKernelGGL(k_stream_claims, dim3((cap + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a,
