@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Interleaved A/B of two builds of libuvhttp_ws_amd.so in ONE process on one device.
 
-  python tools/ab_lib.py LIB_A LIB_B cfg:mode [cfg:mode ...]     (mode: inplace | inplace_nd | compact | streams)
+  python tools/ab_lib.py LIB_A LIB_B cfg:mode [cfg:mode ...]     (mode: inplace | inplace_nd | compact | compact_nd | streams)
 
 LIB_B may be "tree" for the in-tree build.  AB_STAMPS=1 turns engine B's device stamps on;
 AB_ENV_B="K=V,..." sets environment switches for engine B only.  Each round runs K decode steps with engine A,
@@ -68,7 +68,7 @@ def main():
         outs = []
         for e in engs:
             desc, summ = e.alloc_outputs(n)
-            arena = torch.empty(n * plen + 64, dtype=torch.uint8, device="cuda") if mode == "compact" else None
+            arena = torch.empty(n * plen + 64, dtype=torch.uint8, device="cuda") if mode.startswith("compact") else None
             msgs = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
             outs.append((desc, summ, arena, msgs))
 
@@ -82,7 +82,8 @@ def main():
                                  desc=desc, summary=summ, stream=st, no_desc=mode == "inplace_nd")
             else:
                 e.decode_compact(wire, n, arena, stride=stride, max_message_size=mm,
-                                 wire_len=wl, desc=desc, msgs=msgs, summary=summ, stream=st)
+                                 wire_len=wl, desc=desc, msgs=msgs, summary=summ, stream=st,
+                                 no_desc=mode == "compact_nd")
 
         step = [[], []]
         kern = [[], []]
