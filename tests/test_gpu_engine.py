@@ -85,8 +85,10 @@ def test_lookback_give_up_is_reported(torch):
     assert torch.equal(sd, sbefore)
     with pytest.raises(U.GpuError):
         eng.sync()
-    # the stream decode has no look-back (per-connection walk + one-block scan): the same
-    # engine still decodes streams normally
+    # the stream decode has no look-back (per-connection walk + one-block scan) unless the wave
+    # walk runs fused (UVHTTP_WS_WALK_FUSE=1: k_swalk_fused finds first frames by a look-back
+    # over blocks of connections).  Fused, every block after the first gives up, so every
+    # stream reports ERR_DEVICE and nothing is unmasked ...
     st = np.zeros(64, U.STREAM_DT)
     per = w.size // 64
     idx = np.minimum(np.searchsorted(offs, np.arange(64) * per), len(offs) - 1)
@@ -94,6 +96,20 @@ def test_lookback_give_up_is_reported(torch):
     for k in range(64):
         st[k] = (cut[k], cut[k + 1] - cut[k], 1 << 30, 0, 0, 1 << 24, 1 << 26, 1, 0, 0, 0)
     sdev = torch.from_numpy(st.view(np.uint8).copy()).to("cuda")
+    eng.close()
+    eng = _engine({"UVHTTP_WS_MAX_POLLS": "0", "UVHTTP_WS_WALK_FUSE": "1"})
+    d2 = before.clone()
+    _, res = eng.decode_streams(d2, sdev, 64, 8192, wire_len=w.size)
+    torch.cuda.synchronize()
+    rs = eng.read_stream_results(res, 64)
+    assert all(r.status == -1 and r.first_status == -11 and r.n_delivered == 0 for r in rs)
+    assert torch.equal(d2, before)
+    with pytest.raises(U.GpuError):
+        eng.sync()
+    eng.close()
+    # ... while the walk, its one-block scan and k_stream_desc apart (the default) have no
+    # look-back: an engine with the same poll bound decodes the streams normally
+    eng = _engine({"UVHTTP_WS_MAX_POLLS": "0"})
     d2 = before.clone()
     _, res = eng.decode_streams(d2, sdev, 64, 8192, wire_len=w.size)
     torch.cuda.synchronize()

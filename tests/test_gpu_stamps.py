@@ -66,10 +66,22 @@ def test_stamps_batch_in_place(torch, calls):
         eng.close()
 
 
-def test_stamps_stream_decode(torch):
+@pytest.mark.parametrize("fuse", ["1", "0"])
+def test_stamps_stream_decode(torch, fuse):
+    """the wave walk, its scan and k_stream_desc, or with UVHTTP_WS_WALK_FUSE=1 the one
+    launch of k_swalk_fused (stamped as "walk")"""
+    import os
     import numpy as np
     import uvhttp_amd as U
-    eng = U.GpuEngine(0)
+    old = os.environ.get("UVHTTP_WS_WALK_FUSE")
+    os.environ["UVHTTP_WS_WALK_FUSE"] = fuse
+    try:
+        eng = U.GpuEngine(0)
+    finally:
+        if old is None:
+            os.environ.pop("UVHTTP_WS_WALK_FUSE", None)
+        else:
+            os.environ["UVHTTP_WS_WALK_FUSE"] = old
     try:
         n, plen = 8192, 4096
         wire, stride = _wire(torch, U, eng, n, plen)
@@ -86,7 +98,8 @@ def test_stamps_stream_decode(torch):
         torch.cuda.synchronize()
         recs = eng.read_stamps()
         eng.set_stamps(False)
-        _check_calls(recs, {"walk", "walk_scan", "stream_desc", "payload"}, 3)
+        _check_calls(recs, {"walk", "payload"} if fuse == "1" else
+                     {"walk", "walk_scan", "stream_desc", "payload"}, 3)
         r = eng.read_stream_results(res, n)
         assert all(x.status == 0 and x.n_delivered == 1 for x in r)
     finally:

@@ -27,17 +27,20 @@ def torch():
     return t
 
 
-@pytest.fixture(scope="module", params=["lane", "lane-twopass", "wave", "wave-norec", "wave-twopass"])
+@pytest.fixture(scope="module", params=["lane", "lane-twopass", "wave", "wave-norec", "wave-twopass",
+                                        "wave-fuse", "wave-fuse-norec"])
 def eng(torch, request):
     """Every frame-discovery walk (a lane per connection, single pass or two walks; a wave per
     connection, single pass
     through the offset scratch — with the fast path's frame records or re-reading every header
-    in k_stream_desc — or the two-walk fallback) must decode alike."""
+    for the descriptors; in one launch (k_swalk_fused) or with the scan and k_stream_desc
+    apart — or the two-walk fallback) must decode alike."""
     import os
     import uvhttp_amd as U
     env = {"UVHTTP_WS_WALK": request.param.split("-")[0],
            "UVHTTP_WS_WALK_SINGLE": "0" if request.param.endswith("twopass") else "1",
-           "UVHTTP_WS_WALK_REC": "0" if request.param.endswith("norec") else "1"}
+           "UVHTTP_WS_WALK_REC": "0" if request.param.endswith("norec") else "1",
+           "UVHTTP_WS_WALK_FUSE": "1" if "-fuse" in request.param else "0"}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:

@@ -301,6 +301,9 @@ struct StreamScratch {
     uint2* walk_rec;       // single pass, wave walk (or null): per start, the frame's key and
                            // header bytes when the walk's fast path parsed them (kNoRec: not)
     uint32_t* agg;         // [n_streams / 256 + 1] lane walk block counts -> prefixes
+    uint32_t* ctr;         // [4] k_swalk_fused: [0] block ticket, [1] connections done (both
+                           // reset by their last taker), [2] epoch of a call over capacity
+    void* srec;            // [2 n_streams] k_swalk_fused look-back records (A, P per connection)
 };
 
 // parse_hdr's result for one frame, 16 bytes (stride batches: written by the payload pass,
@@ -382,6 +385,9 @@ struct BatchArgs {
     // its descriptor says OK
     const uvhttp_ws_stream_t* streams;
     const uint32_t* n_dev;
+    uvhttp_ws_stream_result_t* s_results;  // after k_swalk_fused: results stream_fix may rewrite
+    const uint32_t* s_over;  //   (StreamScratch::ctr[2]: epoch of a call over capacity)
+    uint32_t n_streams;
     uint32_t epoch;          // tag of this call's map / first_bad entries
     uint32_t dev_epoch;      // 1: a captured call, the epoch is ws.ctl[kCtlEpoch]
     uint32_t max_polls;      // look-back wait bound (0: give up at the first wait; tests)
@@ -1580,6 +1586,22 @@ __device__ __forceinline__ void unmask_tile(BatchArgs a,
     }
 }
 
+// After k_swalk_fused: a call over capacity (ws_over = its epoch) or whose look-back gave up
+// has every connection's result rewritten — ERR_CAPACITY for those with frames, as
+// k_stream_desc; ERR_DEVICE for all (nothing was unmasked: first_bad 0).  One workgroup.
+__device__ inline void device_result(uvhttp_ws_stream_result_t& r);
+__device__ inline void capacity_result(uvhttp_ws_stream_result_t& r);
+__device__ inline void stream_fix(const BatchArgs& a, const Workspace& ws) {
+    const bool fault = ws.ctl[kCtlFaultEp] == a.epoch;
+    if (!fault && *a.s_over != a.epoch) return;
+    for (uint32_t j = threadIdx.x; j < a.n_streams; j += blockDim.x) {
+        uvhttp_ws_stream_result_t o = a.s_results[j];
+        if (fault) device_result(o);
+        else if (o.n_frames) capacity_result(o);
+        a.s_results[j] = o;
+    }
+}
+
 template <int BLOCK, int VPT, int STORE_AUX = 0>
 __global__ __launch_bounds__(BLOCK) void k_unmask_inplace(
     BatchArgs a, const uvhttp_ws_frame_desc_t* __restrict__ desc, Workspace ws,
@@ -1595,6 +1617,10 @@ __global__ __launch_bounds__(BLOCK) void k_unmask_inplace(
         resolve_epoch(a, ws);
         finalize_frames(a, const_cast<uvhttp_ws_frame_desc_t*>(desc), ws,
                         (uint32_t)(tile_base + blockIdx.x), BLOCK, nb);
+    }
+    if (a.s_results && tile_base + blockIdx.x == 0) {
+        resolve_epoch(a, ws);
+        stream_fix(a, ws);
     }
 }
 
@@ -2860,6 +2886,9 @@ struct WalkArgs {
     const uint32_t* ctl;
     uint64_t* stamp;           // device-side kernel stamps (diagnostics), or null
     uint32_t cas_claims;       // the engine has captured calls (tag_claim)
+    uint32_t max_polls;        // k_swalk_fused look-back wait bound (BatchArgs::max_polls)
+    uint32_t no_ticket;        // k_swalk_fused: blocks in blockIdx order (UVHTTP_WS_PLAN_TICKET=0)
+    uint64_t* first_bad;       // Workspace::first_bad (k_swalk_fused: a look-back give-up)
 };
 
 // process_data's buffer growth: returns false on failure (*out = size then), else the size
@@ -3210,17 +3239,20 @@ __device__ inline void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// MODE 0 / 1 / 2 as the lane walk; 3: as 2, the result returned (every lane) instead of
+// written (k_swalk_fused)
 template <int MODE>
-__device__ inline void walk_wave(const WalkArgs& w, uint32_t s, uint8_t* ring) {
+__device__ inline uvhttp_ws_stream_result_t walk_wave(const WalkArgs& w, uint32_t s, uint8_t* ring) {
     const uint32_t lane = threadIdx.x & 63;
     const uvhttp_ws_stream_t st = w.streams[s];
     const bool ok = __all(stream_ok_part(w, s, st, lane, 64));
     if (!ok) {
-        if (MODE != 1 && lane == 0) {
-            w.results[s] = layout_result(st);
+        const uvhttp_ws_stream_result_t r = layout_result(st);
+        if ((MODE == 0 || MODE == 2) && lane == 0) {
+            w.results[s] = r;
             w.agg[s] = 0;
         }
-        return;
+        return r;
     }
     // (wave mode: agg[s] holds the connection's frame count for k_swalk_scan, then its first)
     const uint64_t first = MODE == 1 ? w.agg[s] : slice_base(st, s);
@@ -3231,7 +3263,7 @@ __device__ inline void walk_wave(const WalkArgs& w, uint32_t s, uint8_t* ring) {
     auto emit_lane = [&](uint64_t pos, uint32_t idx, bool on, uint2 rec) {
         if (MODE == 0 || !on) return;
         const uint64_t f = first + idx;
-        if (MODE == 2) {
+        if (MODE >= 2) {
             w.sc.walk_tmp[f] = (uint32_t)pos;
             if (w.sc.walk_rec) w.sc.walk_rec[f] = rec;
         } else if (f < w.max_frames) {
@@ -3319,7 +3351,7 @@ __device__ inline void walk_wave(const WalkArgs& w, uint32_t s, uint8_t* ring) {
             // 1 + l + 64 g, so one step decides up to 64 kG frames with kG loads in flight per
             // lane (64 per step measured 40 us for C4's 4096 x 256 frames: four dependent gathers)
             constexpr uint32_t kG = 4, kRun = 64 * kG;
-            uint32_t wlp = 0;          // the previous step's frame length
+            uint32_t wlp = 0;          // the previous step's frame length (0: first step)
             bool have0 = false;        // frame 0's header carried from the previous step
             uint32_t cb0 = 0, cwl = 0;  // (its fields)
             uint64_t cplen = 0;
@@ -3357,7 +3389,15 @@ __device__ inline void walk_wave(const WalkArgs& w, uint32_t s, uint8_t* ring) {
                 uint2 recl[kG];  // lane l of group g: the record of frame 1 + l + 64 g
 #pragma unroll
                 for (uint32_t g = 0; g < kG; ++g) recl[g] = uint2{0u, kNoRec};
-                if (kind != 3 && wl0 == wlp) {
+#ifdef UVWS_WALK_SPEC_FIRST_OFF
+                const bool spec = wl0 == wlp;
+#else
+                // (the first step speculates on frame 0's own length: one dependent header
+                // round trip fewer per connection; a connection of unequal frames wastes one
+                // step's loads)
+                const bool spec = wl0 == wlp || wlp == 0;
+#endif
+                if (kind != 3 && spec) {
                     // speculation: frames 1 .. kRun all have frame 0's length, so the frame after
                     // the run — the next step's frame 0 — was always read, even after a full run
                     u32x4 hv[kG];
@@ -3449,9 +3489,12 @@ __device__ inline void walk_wave(const WalkArgs& w, uint32_t s, uint8_t* ring) {
                     __builtin_amdgcn_readfirstlane((uint32_t)acc);
             c.count = cnt;
         });
-    if (MODE == 1 || lane != 0) return;
-    w.results[s] = walk_result(w, st, c);
-    w.agg[s] = c.count;
+    const uvhttp_ws_stream_result_t r = walk_result(w, st, c);
+    if ((MODE == 0 || MODE == 2) && lane == 0) {
+        w.results[s] = r;
+        w.agg[s] = c.count;
+    }
+    return r;
 }
 
 template <int MODE>
@@ -3464,7 +3507,7 @@ __global__ __launch_bounds__(kBlock) void k_swalk_wave(WalkArgs w) {
     const uint32_t s = stamp_.anchor_s(blockIdx.x * (kBlock / 64) + wave);
     if (s >= w.n_streams) return;
     if (MODE == 1 && !w.results[s].n_frames) return;
-    walk_wave<MODE>(w, s, ring[wave]);
+    (void)walk_wave<MODE>(w, s, ring[wave]);
 }
 
 // first frames, total, capacity (one workgroup).  Lane mode scans the walk's per-block
@@ -3578,50 +3621,20 @@ __global__ __launch_bounds__(kBlock) void k_stream_desc_lane(WalkArgs w) {
     }
 }
 
-// k_stream_desc: one wave per connection writes its descriptors (the frames' headers re-read
-// with two aligned 16-byte loads each), the running message id (FIN data frames delivered
-// before the frame in its connection), MSG_END, the failing frame's status, and each
-// frame's end for the tile claims.  Capacity overflow: every result says so, nothing else.
-__global__ __launch_bounds__(kBlock) void k_stream_desc(WalkArgs w) {
-    StampScope stamp_(w.stamp, w.epoch, UVHTTP_WS_STAMP_STREAM_DESC, false);
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const uint32_t s = stamp_.anchor_s(blockIdx.x * (kBlock / 64) + wave);
-    if (s >= w.n_streams) return;
-    uvhttp_ws_stream_result_t r = w.results[s];
-    r.first_frame = w.agg[s];  // (k_swalk_scan's prefix)
-    const bool fits = *w.sc.n_total != 0 || r.n_frames == 0;
-    if (!fits) {
-        if (lane == 0) {
-            capacity_result(r);
-            w.results[s] = r;
-        }
-        return;
-    }
-    if (lane == 0) w.results[s].first_frame = r.first_frame;
-    if (!r.n_frames) return;
+// One wave writes connection s's descriptors (the frames' headers rebuilt from the walk's
+// records or re-read with two aligned 16-byte loads each), the running message id (FIN data
+// frames delivered before the frame in its connection), MSG_END, the failing frame's status,
+// and claims the tile map.  r: the connection's result, first_frame placed; prev_end: the
+// begin of the nearest earlier connection with frames (0: none) — k_stream_claims' rule (frame
+// i claims the map tiles whose first byte lies in [end of frame i - 1, end of frame i)) with
+// frame 0's range starting there (at or before that connection's last frame end; the
+// max-of-tag claim keeps the smallest frame, so claiming more is harmless).
+__device__ inline void stream_desc_wave(const WalkArgs& w, uint32_t s, const uvhttp_ws_stream_result_t& r,
+                                        uint64_t prev_end, uint32_t epoch) {
+    const uint32_t lane = threadIdx.x & 63;
     const uvhttp_ws_stream_t st = w.streams[s];
     const uint64_t sb = slice_base(st, s);
     uint32_t msg = 0;  // FIN data frames delivered before this chunk
-    const uint32_t epoch = w.dev_epoch ? w.ctl[kCtlEpoch] : w.epoch;
-    // k_stream_claims' rule (frame i claims the map tiles whose first byte lies in [end of
-    // frame i - 1, end of frame i)), here: frame 0 of the connection starts its range at the
-    // begin of the nearest earlier connection with frames (at or before that connection's last
-    // frame end; the max-of-tag claim keeps the smallest frame, so claiming more is harmless)
-    // (the direct predecessor first; past it, 64 connections per step by a ballot, so a long
-    // run of connections without frames costs one round trip per 64)
-    uint64_t prev_end = 0;
-    if (s > 0 && w.results[s - 1].n_frames) {
-        prev_end = w.streams[s - 1].begin;
-    } else {
-        for (int64_t base = (int64_t)s - 2; base >= 0; base -= 64) {
-            const int64_t j = base - (int64_t)lane;
-            const uint64_t m = __ballot(j >= 0 && w.results[j].n_frames != 0);
-            if (m) {
-                prev_end = w.streams[base - __builtin_ctzll(m)].begin;
-                break;
-            }
-        }
-    }
     // groups of four 64-frame chunks: every start and header load of a group is issued before
     // any is used (one chunk at a time cost two dependent round trips per 64 frames)
     constexpr int kG = 4;
@@ -3670,6 +3683,225 @@ __global__ __launch_bounds__(kBlock) void k_stream_desc(WalkArgs w) {
             msg += (uint32_t)__builtin_popcountll(fm);
         }
     }
+}
+
+// k_stream_desc: one wave per connection (stream_desc_wave) after k_swalk_scan.  Capacity
+// overflow: every result says so, nothing else.
+__global__ __launch_bounds__(kBlock) void k_stream_desc(WalkArgs w) {
+    StampScope stamp_(w.stamp, w.epoch, UVHTTP_WS_STAMP_STREAM_DESC, false);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const uint32_t s = stamp_.anchor_s(blockIdx.x * (kBlock / 64) + wave);
+    if (s >= w.n_streams) return;
+    uvhttp_ws_stream_result_t r = w.results[s];
+    r.first_frame = w.agg[s];  // (k_swalk_scan's prefix)
+    const bool fits = *w.sc.n_total != 0 || r.n_frames == 0;
+    if (!fits) {
+        if (lane == 0) {
+            capacity_result(r);
+            w.results[s] = r;
+        }
+        return;
+    }
+    if (lane == 0) w.results[s].first_frame = r.first_frame;
+    if (!r.n_frames) return;
+    // prev_end: the direct predecessor first; past it, 64 connections per step by a ballot, so
+    // a long run of connections without frames costs one round trip per 64
+    uint64_t prev_end = 0;
+    if (s > 0 && w.results[s - 1].n_frames) {
+        prev_end = w.streams[s - 1].begin;
+    } else {
+        for (int64_t base = (int64_t)s - 2; base >= 0; base -= 64) {
+            const int64_t j = base - (int64_t)lane;
+            const uint64_t m = __ballot(j >= 0 && w.results[j].n_frames != 0);
+            if (m) {
+                prev_end = w.streams[base - __builtin_ctzll(m)].begin;
+                break;
+            }
+        }
+    }
+    stream_desc_wave(w, s, r, prev_end, w.dev_epoch ? w.ctl[kCtlEpoch] : w.epoch);
+}
+
+// ---- k_swalk_fused: walk, first frame and descriptors of a connection in one launch -------
+// The wave walk in single pass (k_swalk_wave<2>), then k_swalk_scan's prefix by a decoupled
+// look-back over connections, then k_stream_desc's work — one launch where there were three
+// (C4 streams: the scan and the descriptor pass with their launch gaps were 17 us of 147).
+// Blocks take tickets in launch order (connections 4 ticket .. 4 ticket + 3, a wave each), so
+// a block only waits on blocks that already run.  Each block publishes the aggregate of its
+// four connections (A record), then its 256 threads combine their predecessors' records, 256
+// blocks per round, back to the nearest inclusive prefix (P record) — a look-back per
+// connection, 64 per round, took n / 64 dependent rounds when the walks end together: C4
+// streams 307 us per step instead of 149.  A record is one device-coherent 16-byte access:
+// frame count (saturated at 2^32 - 1), begin + 1 of the latest connection with frames (0:
+// none — k_stream_desc's prev_end), tag (epoch << 2 | kind).  Polls are bounded as k_plan's: a wave that gives up
+// publishes anyway and records the device fault.  The connection whose wave finishes last
+// (a counter) rewrites every result when the call overflowed max_frames (ERR_CAPACITY, as
+// k_stream_desc) or faulted (ERR_DEVICE: nothing delivered).
+constexpr uint32_t kSwAgg = 1, kSwPrefix = 2;
+
+struct SwVal {
+    uint32_t count;  // frames (saturated)
+    uint64_t hb;     // begin + 1 of the latest connection with frames, 0: none
+};
+
+__device__ inline SwVal sw_combine(const SwVal& e, const SwVal& l) {
+    const uint64_t c = (uint64_t)e.count + l.count;
+    return SwVal{c > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)c, l.hb ? l.hb : e.hb};
+}
+
+__device__ inline void sw_store(const WalkArgs& w, uint32_t slot, const SwVal& v, uint32_t tag) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(w.sc.srec, 0, 0x7FFFFFFF, 0x00020000);
+    const u32x4v x = {v.count, (uint32_t)v.hb, (uint32_t)(v.hb >> 32), tag};
+    __builtin_amdgcn_raw_buffer_store_b128(x, rs, slot * 16u, 0, kAuxSc1);
+}
+
+__device__ inline u32x4v sw_fetch(const WalkArgs& w, uint32_t slot) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(w.sc.srec, 0, 0x7FFFFFFF, 0x00020000);
+    return __builtin_amdgcn_raw_buffer_load_b128(rs, slot * 16u, 0, kAuxSc1);
+}
+
+// block b's exclusive prefix (every thread; records: A at 2 b, P at 2 b + 1), k_plan's
+// look-back over SwVal: 256 predecessors per round, thread t taking block end - 256 + t
+__device__ inline SwVal sw_lookback(const WalkArgs& w, uint32_t b, const SwVal& agg, uint32_t epoch,
+                                    bool& gave_up) {
+    __shared__ uint32_t s_cnt[kBlock / 64];
+    __shared__ uint64_t s_hb[kBlock / 64];
+    __shared__ int s_kstar;
+    const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const uint32_t ta = (epoch << 2) | kSwAgg, tp = (epoch << 2) | kSwPrefix;
+    gave_up = false;
+    if (b == 0) {
+        if (t == 0) sw_store(w, 1, agg, tp);
+        return SwVal{0u, 0ull};
+    }
+    if (t == 0) sw_store(w, 2 * b, agg, ta);
+    SwVal run{0u, 0ull};  // the predecessors combined so far (all newer than the next window)
+    int64_t end = b;      // window: blocks [end - 256, end), thread 255 the newest
+    uint32_t polls = 0;   // (uniform: every thread counts the same rounds)
+    for (;;) {
+        const int64_t j = end - kBlock + (int64_t)t;
+        SwVal v{0u, 0ull};
+        bool is_p = j < 0, ready = j < 0;  // (before block 0: identity "P")
+        for (;;) {
+            if (!ready) {  // both records in one round trip
+                const u32x4v xp = sw_fetch(w, 2 * (uint32_t)j + 1);
+                const u32x4v xa = sw_fetch(w, 2 * (uint32_t)j);
+                if (xp.w == tp) {
+                    v = SwVal{xp.x, xp.y | ((uint64_t)xp.z << 32)}, is_p = true, ready = true;
+                } else if (xa.w == ta) {
+                    v = SwVal{xa.x, xa.y | ((uint64_t)xa.z << 32)}, ready = true;
+                }
+            }
+            if (__syncthreads_and(ready) && w.max_polls) break;
+            if (++polls > w.max_polls) {
+                gave_up = true;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(8);
+        }
+        // from the newest published prefix (the highest thread with P) to the newest block
+        if (t == 0) s_kstar = -1;
+        __syncthreads();
+        const uint64_t pm = __ballot(is_p);
+        if (lane == 0 && pm) atomicMax(&s_kstar, (int)(wave * 64 + 63 - __builtin_clzll(pm)));
+        __syncthreads();
+        const int kstar = s_kstar;
+        if ((int)t < kstar) v = SwVal{0u, 0ull};
+        uint64_t cnt = v.count;
+#pragma unroll
+        for (int d = 32; d; d >>= 1) cnt += __shfl_xor(cnt, d, 64);
+        const uint64_t hm = __ballot(v.hb != 0);
+        uint64_t hb = 0;
+        if (hm) {
+            const uint32_t hl = 63 - __builtin_clzll(hm);
+            hb = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v.hb >> 32), hl) << 32) |
+                 __builtin_amdgcn_readlane((uint32_t)v.hb, hl);
+        }
+        if (lane == 0) {
+            s_cnt[wave] = cnt > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)cnt;
+            s_hb[wave] = hb;
+        }
+        __syncthreads();
+        SwVal win{0u, 0ull};
+#pragma unroll
+        for (int k = 0; k < kBlock / 64; ++k) win = sw_combine(win, SwVal{s_cnt[k], s_hb[k]});
+        run = sw_combine(win, run);
+        __syncthreads();  // (s_kstar, s_cnt, s_hb reused by the next round)
+        if (kstar >= 0 || gave_up) break;
+        end -= kBlock;
+    }
+    if (t == 0) sw_store(w, 2 * b + 1, sw_combine(run, agg), tp);
+    return run;
+}
+
+__device__ inline void device_result(uvhttp_ws_stream_result_t& r) {
+    capacity_result(r);
+    r.first_status = UVHTTP_WS_FRAME_ERR_DEVICE;
+}
+
+__global__ __launch_bounds__(kBlock) void k_swalk_fused(WalkArgs w) {
+    StampScope stamp_(w.stamp, w.epoch, UVHTTP_WS_STAMP_WALK, false);
+    __shared__ __attribute__((aligned(16))) uint8_t ring[kBlock / 64][kRingBytes];
+    __shared__ uint32_t s_ticket;
+    if (threadIdx.x == 0) {
+        uint32_t t = blockIdx.x;
+        if (!w.no_ticket) {
+            t = __hip_atomic_fetch_add(&w.sc.ctr[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (t + 1 == gridDim.x) __hip_atomic_store(&w.sc.ctr[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_ticket = t;
+    }
+    __syncthreads();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const uint32_t bt = __builtin_amdgcn_readfirstlane(s_ticket);
+    const uint32_t s = stamp_.anchor_s(bt * (kBlock / 64) + wave);
+    const uint32_t epoch = w.dev_epoch ? w.ctl[kCtlEpoch] : w.epoch;
+    // (a wave past the last connection still joins the block's look-back, with nothing)
+    uvhttp_ws_stream_result_t r;
+    memset(&r, 0, sizeof(r));
+    if (s < w.n_streams) r = walk_wave<3>(w, s, ring[wave]);
+    const SwVal mine{s < w.n_streams ? r.n_frames : 0u, s < w.n_streams && r.n_frames ? w.streams[s].begin + 1 : 0ull};
+    // the block's four connections in order: each wave's prefix within the block, the block's
+    // aggregate; then the block's prefix (the slice stores of each wave are ordered before its
+    // own reads by the barriers)
+    __shared__ uint32_t s_wc[kBlock / 64];
+    __shared__ uint64_t s_wh[kBlock / 64];
+    if (lane == 0) {
+        s_wc[wave] = mine.count;
+        s_wh[wave] = mine.hb;
+    }
+    __syncthreads();
+    SwVal local{0u, 0ull}, agg{0u, 0ull};
+#pragma unroll
+    for (uint32_t k = 0; k < kBlock / 64; ++k) {
+        if (k == wave) local = agg;
+        agg = sw_combine(agg, SwVal{s_wc[k], s_wh[k]});
+    }
+    bool gave_up;
+    const SwVal pre = sw_combine(sw_lookback(w, bt, agg, epoch, gave_up), local);
+    if (s >= w.n_streams) return;
+    r.first_frame = pre.count;
+    const uint64_t incl = (uint64_t)pre.count + r.n_frames;
+    const bool over = incl > w.max_frames;
+    uint32_t* ctl = const_cast<uint32_t*>(w.ctl);
+    if (lane == 0) {
+        if (gave_up) {  // k_plan's give-up: the payload kernel unmasks nothing (first_bad 0)
+            __hip_atomic_store(&ctl[kCtlFaultEp], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&ctl[kCtlFaults], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            tag_claim(w.first_bad, epoch, 0, 1u);
+        }
+        uvhttp_ws_stream_result_t o = r;
+        if (over && r.n_frames) capacity_result(o);
+        w.results[s] = o;
+        // the total (0 over capacity); a call over capacity, known from the last connection's
+        // total only, or with a device fault has every result rewritten by the payload kernel's
+        // first workgroup (stream_fix: after this kernel, so with every result visible)
+        if (s + 1 == w.n_streams) {
+            *w.sc.n_total = over ? 0u : (uint32_t)incl;
+            if (over) w.sc.ctr[2] = epoch;
+        }
+    }
+    if (!over && !gave_up && r.n_frames) stream_desc_wave(w, s, r, pre.hb ? pre.hb - 1 : 0ull, epoch);
 }
 
 // k_stream_claims: frame i claims the 16 KiB map tiles whose first byte lies in
@@ -4362,7 +4594,7 @@ struct uvhttp_ws_gpu_engine {
     uint32_t plan_no_ticket;   // UVHTTP_WS_PLAN_TICKET=0: blockIdx order instead of tickets
     int walk_mode;             // stream frame discovery: 0 automatic, 1 lane, 2 wave
     void* ss_mem;              // stream-decode scratch
-    uint32_t ss_frames, ss_reads;
+    uint32_t ss_frames, ss_reads, ss_streams;
     StreamScratch ss;
     void* wt_mem;              // single-pass walk scratch (frame starts per connection slice)
     uint64_t wt_cap;
@@ -4370,6 +4602,7 @@ struct uvhttp_ws_gpu_engine {
     uint64_t wr_cap;
     int wr_rec_on;             // UVHTTP_WS_WALK_REC=0: k_stream_desc gathers every header (A/B)
     int walk_single_off;       // UVHTTP_WS_WALK_SINGLE=0: always walk twice (tests, A/B)
+    int walk_fuse;             // UVHTTP_WS_WALK_FUSE=1: k_swalk_fused for the single-pass wave walk
     int fused_block, fused_vpt;  // UVHTTP_WS_FUSED_TILE=BxV: the fused payload pass's tile (A/B)
     uint32_t fixup_blocks;     // k_fixup grid cap (UVHTTP_WS_FIXUP_BLOCKS, A/B)
     int fused_aux;             // fused payload stores' cache-policy bits (UVHTTP_WS_FUSED_AUX, A/B)
@@ -4481,6 +4714,7 @@ int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out) {
         e->compact_mode = strcmp(cm, "gather") == 0 ? 1 : strcmp(cm, "scatter") == 0 ? 2 : 0;
     if (const char* ws = getenv("UVHTTP_WS_WALK_SINGLE")) e->walk_single_off = atoi(ws) == 0;
     e->wr_rec_on = 1;
+    if (const char* wf = getenv("UVHTTP_WS_WALK_FUSE")) e->walk_fuse = atoi(wf) != 0;
     if (const char* wr = getenv("UVHTTP_WS_WALK_REC")) e->wr_rec_on = atoi(wr) != 0;
     if (const char* wm = getenv("UVHTTP_WS_WALK"))
         e->walk_mode = strcmp(wm, "lane") == 0 ? 1 : strcmp(wm, "wave") == 0 ? 2 : 0;
@@ -5278,28 +5512,35 @@ int uvhttp_ws_gpu_decode_compact(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batc
 
 static int reserve_streams(uvhttp_ws_gpu_engine_t* e, uint32_t frames, uint32_t streams,
                            uint32_t reads) {
-    (void)streams;
     if (reads == 0) reads = 1;
-    if (e->ss_mem && frames <= e->ss_frames && reads <= e->ss_reads) return UVHTTP_WS_GPU_OK;
+    if (e->ss_mem && frames <= e->ss_frames && reads <= e->ss_reads && streams <= e->ss_streams)
+        return UVHTTP_WS_GPU_OK;
     if (e->capturing)
         return set_err(e, UVHTTP_WS_GPU_EINVAL, "stream scratch too small for a captured call",
                        hipSuccess);
     const uint32_t fr = frames > e->ss_frames ? frames : e->ss_frames;
     const uint32_t rd = reads > e->ss_reads ? reads : e->ss_reads;
+    const uint32_t sn = streams > e->ss_streams ? streams : e->ss_streams;
     size_t o_off = 0;
     size_t o_tot = align_up(o_off + (size_t)fr * 8, 256);
     size_t o_rsize = align_up(o_tot + 16, 256);
     size_t o_agg = align_up(o_rsize + (size_t)rd * 8, 256);
-    size_t bytes = align_up(o_agg + ((size_t)kMaxFrames / kBlock + 2) * 4, 256);
+    size_t o_ctr = align_up(o_agg + ((size_t)kMaxFrames / kBlock + 2) * 4, 256);
+    size_t o_srec = align_up(o_ctr + 16, 256);
+    size_t bytes = align_up(o_srec + (size_t)sn * 32, 256);
     int prev = 0;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(e->device);
     if (e->ss_mem) (void)hipFree(e->ss_mem);
     e->ss_mem = nullptr;
-    const hipError_t h = hipMalloc(&e->ss_mem, bytes);
+    hipError_t h = hipMalloc(&e->ss_mem, bytes);
+    // (zero: the counters start at 0 and no record tag matches a live epoch)
+    if (h == hipSuccess) h = hipMemset(e->ss_mem, 0, bytes);
     (void)hipSetDevice(prev);
     if (h != hipSuccess) {
-        e->ss_frames = e->ss_reads = 0;
+        if (e->ss_mem) (void)hipFree(e->ss_mem);
+        e->ss_mem = nullptr;
+        e->ss_frames = e->ss_reads = e->ss_streams = 0;
         return set_err(e, UVHTTP_WS_GPU_ENOMEM, "hipMalloc stream scratch", h);
     }
     char* b = (char*)e->ss_mem;
@@ -5307,6 +5548,9 @@ static int reserve_streams(uvhttp_ws_gpu_engine_t* e, uint32_t frames, uint32_t 
     e->ss.n_total = (uint32_t*)(b + o_tot);
     e->ss.read_size = (uint64_t*)(b + o_rsize);
     e->ss.agg = (uint32_t*)(b + o_agg);
+    e->ss.ctr = (uint32_t*)(b + o_ctr);
+    e->ss.srec = (void*)(b + o_srec);
+    e->ss_streams = sn;
     e->ss_frames = fr;
     e->ss_reads = rd;
     return UVHTTP_WS_GPU_OK;
@@ -5394,23 +5638,35 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     w.agg = e->ss.agg;
     w.stamp = (e->stamp_on && !e->capturing) ? e->stamp_mem : nullptr;
     w.cas_claims = e->captured_ever ? 1u : 0u;
+    w.max_polls = e->max_polls;
+    w.no_ticket = e->plan_no_ticket;
+    w.first_bad = e->ws.first_bad;
     const uint32_t nsb = (n_streams + kBlock - 1) / kBlock;
     const uint32_t nwb = (n_streams + kBlock / 64 - 1) / (kBlock / 64);
     const int tk_chain = e->time_chain ? timing_begin(e, s) : -1;
-    if (wave_walk) {
-        if (w.single) hipLaunchKernelGGL(k_swalk_wave<2>, dim3(nwb), dim3(kBlock), 0, s, w);
-        else hipLaunchKernelGGL(k_swalk_wave<0>, dim3(nwb), dim3(kBlock), 0, s, w);
+    // UVHTTP_WS_WALK_FUSE=1: walk, scan and descriptors in one launch (k_swalk_fused; its
+    // results are finished by the payload kernel's first workgroup, so not for an empty wire).
+    // Not the default: it measured even with the three launches (C4 142.8 vs 142.6 us per
+    // step, profiles/r05fy_*) and only without the block tickets (with them 155 us).
+    const bool fused = wave_walk && w.single && e->walk_fuse && wire_len > 0;
+    if (fused) {
+        hipLaunchKernelGGL(k_swalk_fused, dim3(nwb), dim3(kBlock), 0, s, w);
     } else {
-        if (w.single) hipLaunchKernelGGL(k_swalk_lane<2>, dim3(nsb), dim3(kBlock), 0, s, w);
-        else hipLaunchKernelGGL(k_swalk_lane<0>, dim3(nsb), dim3(kBlock), 0, s, w);
+        if (wave_walk) {
+            if (w.single) hipLaunchKernelGGL(k_swalk_wave<2>, dim3(nwb), dim3(kBlock), 0, s, w);
+            else hipLaunchKernelGGL(k_swalk_wave<0>, dim3(nwb), dim3(kBlock), 0, s, w);
+        } else {
+            if (w.single) hipLaunchKernelGGL(k_swalk_lane<2>, dim3(nsb), dim3(kBlock), 0, s, w);
+            else hipLaunchKernelGGL(k_swalk_lane<0>, dim3(nsb), dim3(kBlock), 0, s, w);
+        }
+        hipLaunchKernelGGL(k_swalk_scan, dim3(1), dim3(kBlock), 0, s, w, wave_walk ? 0u : 1u);
+        if (!w.single) {
+            if (wave_walk) hipLaunchKernelGGL(k_swalk_wave<1>, dim3(nwb), dim3(kBlock), 0, s, w);
+            else hipLaunchKernelGGL(k_swalk_lane<1>, dim3(nsb), dim3(kBlock), 0, s, w);
+        }
+        if (wave_walk) hipLaunchKernelGGL(k_stream_desc, dim3(nwb), dim3(kBlock), 0, s, w);
+        else hipLaunchKernelGGL(k_stream_desc_lane, dim3(nsb), dim3(kBlock), 0, s, w);
     }
-    hipLaunchKernelGGL(k_swalk_scan, dim3(1), dim3(kBlock), 0, s, w, wave_walk ? 0u : 1u);
-    if (!w.single) {
-        if (wave_walk) hipLaunchKernelGGL(k_swalk_wave<1>, dim3(nwb), dim3(kBlock), 0, s, w);
-        else hipLaunchKernelGGL(k_swalk_lane<1>, dim3(nsb), dim3(kBlock), 0, s, w);
-    }
-    if (wave_walk) hipLaunchKernelGGL(k_stream_desc, dim3(nwb), dim3(kBlock), 0, s, w);
-    else hipLaunchKernelGGL(k_stream_desc_lane, dim3(nsb), dim3(kBlock), 0, s, w);
 
     BatchArgs a;
     memset(&a, 0, sizeof(a));
@@ -5420,6 +5676,11 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     a.n_tiles = (wire_len + kMapTile - 1) / kMapTile;
     a.streams = d_streams;
     a.n_dev = e->ss.n_total;
+    if (fused) {  // (the payload kernel's first workgroup: stream_fix)
+        a.s_results = d_results;
+        a.s_over = e->ss.ctr + 2;
+        a.n_streams = n_streams;
+    }
     a.max_polls = e->max_polls;
     a.dev_epoch = w.dev_epoch;
     a.epoch = w.epoch;
