@@ -2889,6 +2889,7 @@ struct WalkArgs {
     uint32_t max_polls;        // k_swalk_fused look-back wait bound (BatchArgs::max_polls)
     uint32_t no_ticket;        // k_swalk_fused: blocks in blockIdx order (UVHTTP_WS_PLAN_TICKET=0)
     uint64_t* first_bad;       // Workspace::first_bad (k_swalk_fused: a look-back give-up)
+    uint32_t nt_stores;        // UVHTTP_WS_STREAM_NT=1: frame records and descriptors as streaming stores
 };
 
 // process_data's buffer growth: returns false on failure (*out = size then), else the size
@@ -3264,8 +3265,16 @@ __device__ inline uvhttp_ws_stream_result_t walk_wave(const WalkArgs& w, uint32_
         if (MODE == 0 || !on) return;
         const uint64_t f = first + idx;
         if (MODE >= 2) {
-            w.sc.walk_tmp[f] = (uint32_t)pos;
-            if (w.sc.walk_rec) w.sc.walk_rec[f] = rec;
+            if (w.nt_stores) {
+                __builtin_nontemporal_store((uint32_t)pos, &w.sc.walk_tmp[f]);
+                if (w.sc.walk_rec) {
+                    __builtin_nontemporal_store(rec.x, &w.sc.walk_rec[f].x);
+                    __builtin_nontemporal_store(rec.y, &w.sc.walk_rec[f].y);
+                }
+            } else {
+                w.sc.walk_tmp[f] = (uint32_t)pos;
+                if (w.sc.walk_rec) w.sc.walk_rec[f] = rec;
+            }
         } else if (f < w.max_frames) {
             w.sc.frame_off[f] = st.begin + pos;
         }
@@ -3678,7 +3687,13 @@ __device__ inline void stream_desc_wave(const WalkArgs& w, uint32_t s, const uvh
             const uint32_t before = msg + (uint32_t)__builtin_popcountll(fm & ((1ull << lane) - 1));
             if (act) {
                 if (d.status == UVHTTP_WS_FRAME_OK && d.opcode <= 2) d.message = before;
-                w.desc[r.first_frame + k] = d;
+                if (w.nt_stores) {
+                    const u32x4* dw = reinterpret_cast<const u32x4*>(&d);
+                    __builtin_nontemporal_store(dw[0], reinterpret_cast<u32x4*>(w.desc + r.first_frame + k));
+                    __builtin_nontemporal_store(dw[1], reinterpret_cast<u32x4*>(w.desc + r.first_frame + k) + 1);
+                } else {
+                    w.desc[r.first_frame + k] = d;
+                }
             }
             msg += (uint32_t)__builtin_popcountll(fm);
         }
@@ -4603,6 +4618,7 @@ struct uvhttp_ws_gpu_engine {
     int wr_rec_on;             // UVHTTP_WS_WALK_REC=0: k_stream_desc gathers every header (A/B)
     int walk_single_off;       // UVHTTP_WS_WALK_SINGLE=0: always walk twice (tests, A/B)
     int walk_fuse;             // UVHTTP_WS_WALK_FUSE=1: k_swalk_fused for the single-pass wave walk
+    int stream_nt;             // UVHTTP_WS_STREAM_NT=1: streaming stores in the walk and k_stream_desc (A/B)
     int fused_block, fused_vpt;  // UVHTTP_WS_FUSED_TILE=BxV: the fused payload pass's tile (A/B)
     uint32_t fixup_blocks;     // k_fixup grid cap (UVHTTP_WS_FIXUP_BLOCKS, A/B)
     int fused_aux;             // fused payload stores' cache-policy bits (UVHTTP_WS_FUSED_AUX, A/B)
@@ -4715,6 +4731,7 @@ int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out) {
     if (const char* ws = getenv("UVHTTP_WS_WALK_SINGLE")) e->walk_single_off = atoi(ws) == 0;
     e->wr_rec_on = 1;
     if (const char* wf = getenv("UVHTTP_WS_WALK_FUSE")) e->walk_fuse = atoi(wf) != 0;
+    if (const char* sn = getenv("UVHTTP_WS_STREAM_NT")) e->stream_nt = atoi(sn) != 0;
     if (const char* wr = getenv("UVHTTP_WS_WALK_REC")) e->wr_rec_on = atoi(wr) != 0;
     if (const char* wm = getenv("UVHTTP_WS_WALK"))
         e->walk_mode = strcmp(wm, "lane") == 0 ? 1 : strcmp(wm, "wave") == 0 ? 2 : 0;
@@ -5640,6 +5657,7 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     w.cas_claims = e->captured_ever ? 1u : 0u;
     w.max_polls = e->max_polls;
     w.no_ticket = e->plan_no_ticket;
+    w.nt_stores = e->stream_nt ? 1u : 0u;
     w.first_bad = e->ws.first_bad;
     const uint32_t nsb = (n_streams + kBlock - 1) / kBlock;
     const uint32_t nwb = (n_streams + kBlock / 64 - 1) / (kBlock / 64);
