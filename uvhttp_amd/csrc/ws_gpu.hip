@@ -3638,10 +3638,10 @@ __global__ __launch_bounds__(kBlock) void k_stream_desc_lane(WalkArgs w) {
 // i claims the map tiles whose first byte lies in [end of frame i - 1, end of frame i)) with
 // frame 0's range starting there (at or before that connection's last frame end; the
 // max-of-tag claim keeps the smallest frame, so claiming more is harmless).
-__device__ inline void stream_desc_wave(const WalkArgs& w, uint32_t s, const uvhttp_ws_stream_result_t& r,
-                                        uint64_t prev_end, uint32_t epoch) {
+__device__ inline void stream_desc_wave(const WalkArgs& w, uint32_t s, const uvhttp_ws_stream_t& st,
+                                        const uvhttp_ws_stream_result_t& r, uint64_t prev_end,
+                                        uint32_t epoch) {
     const uint32_t lane = threadIdx.x & 63;
-    const uvhttp_ws_stream_t st = w.streams[s];
     const uint64_t sb = slice_base(st, s);
     uint32_t msg = 0;  // FIN data frames delivered before this chunk
     // groups of four 64-frame chunks: every start and header load of a group is issued before
@@ -3707,9 +3707,17 @@ __global__ __launch_bounds__(kBlock) void k_stream_desc(WalkArgs w) {
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint32_t s = stamp_.anchor_s(blockIdx.x * (kBlock / 64) + wave);
     if (s >= w.n_streams) return;
+    // every load of the setup issued together, the predecessor's unconditionally (a chain of
+    // result -> total -> predecessor's result -> its stream was four dependent round trips)
+    const uint32_t sp = s ? s - 1 : 0;
     uvhttp_ws_stream_result_t r = w.results[s];
-    r.first_frame = w.agg[s];  // (k_swalk_scan's prefix)
-    const bool fits = *w.sc.n_total != 0 || r.n_frames == 0;
+    const uint32_t first = w.agg[s];  // (k_swalk_scan's prefix)
+    const uint32_t n_total = *w.sc.n_total;
+    const uint32_t prev_n = w.results[sp].n_frames;
+    const uint64_t prev_b = w.streams[sp].begin;
+    const uvhttp_ws_stream_t st = w.streams[s];
+    r.first_frame = first;
+    const bool fits = n_total != 0 || r.n_frames == 0;
     if (!fits) {
         if (lane == 0) {
             capacity_result(r);
@@ -3722,8 +3730,8 @@ __global__ __launch_bounds__(kBlock) void k_stream_desc(WalkArgs w) {
     // prev_end: the direct predecessor first; past it, 64 connections per step by a ballot, so
     // a long run of connections without frames costs one round trip per 64
     uint64_t prev_end = 0;
-    if (s > 0 && w.results[s - 1].n_frames) {
-        prev_end = w.streams[s - 1].begin;
+    if (s > 0 && prev_n) {
+        prev_end = prev_b;
     } else {
         for (int64_t base = (int64_t)s - 2; base >= 0; base -= 64) {
             const int64_t j = base - (int64_t)lane;
@@ -3734,7 +3742,7 @@ __global__ __launch_bounds__(kBlock) void k_stream_desc(WalkArgs w) {
             }
         }
     }
-    stream_desc_wave(w, s, r, prev_end, w.dev_epoch ? w.ctl[kCtlEpoch] : w.epoch);
+    stream_desc_wave(w, s, st, r, prev_end, w.dev_epoch ? w.ctl[kCtlEpoch] : w.epoch);
 }
 
 // ---- k_swalk_fused: walk, first frame and descriptors of a connection in one launch -------
@@ -3916,7 +3924,7 @@ __global__ __launch_bounds__(kBlock) void k_swalk_fused(WalkArgs w) {
             if (over) w.sc.ctr[2] = epoch;
         }
     }
-    if (!over && !gave_up && r.n_frames) stream_desc_wave(w, s, r, pre.hb ? pre.hb - 1 : 0ull, epoch);
+    if (!over && !gave_up && r.n_frames) stream_desc_wave(w, s, w.streams[s], r, pre.hb ? pre.hb - 1 : 0ull, epoch);
 }
 
 // k_stream_claims: frame i claims the 16 KiB map tiles whose first byte lies in
