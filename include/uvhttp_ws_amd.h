@@ -349,7 +349,7 @@ int uvhttp_ws_gpu_engine_sync(uvhttp_ws_gpu_engine_t* eng, void* stream);
 #define UVHTTP_WS_STAMP_WALK_SCAN 1   /* k_swalk_scan (first frame per connection) */
 #define UVHTTP_WS_STAMP_WALK2 2       /* second walk (two-pass mode) */
 #define UVHTTP_WS_STAMP_STREAM_DESC 3 /* k_stream_desc / k_stream_desc_lane */
-#define UVHTTP_WS_STAMP_CLAIMS 4      /* k_stream_claims */
+#define UVHTTP_WS_STAMP_CLAIMS 4      /* (k_stream_claims until round 5: unused) */
 #define UVHTTP_WS_STAMP_PAYLOAD 5     /* the payload kernel (unmask / scatter / gather) */
 #define UVHTTP_WS_STAMP_PLAN 6        /* k_plan */
 #define UVHTTP_WS_STAMP_FIXUP 7       /* k_fixup (fused stride path) */

@@ -18,7 +18,12 @@ for f in ws_gpu tls_gpu ws_batcher; do
     -mcode-object-version=5 -c -o "$TMP/$f.o" "$TMP/csrc/$f.hip"
 done
 gcc -O2 -DNDEBUG -fPIC -std=gnu11 -I"$TMP/include" -c -o "$TMP/ws_host.o" "$TMP/csrc/ws_host.c"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$ROOT/tools/bin/libws_$REV.so" \
-  "$TMP/ws_gpu.o" "$TMP/tls_gpu.o" "$TMP/ws_batcher.o" "$TMP/ws_host.o"
+OBJS="$TMP/ws_gpu.o $TMP/tls_gpu.o $TMP/ws_batcher.o $TMP/ws_host.o"
+# (the batcher group, from round 4 on)
+if git -C "$ROOT" show "$REV:uvhttp_amd/csrc/ws_batcher_group.cpp" > "$TMP/csrc/ws_batcher_group.cpp" 2>/dev/null; then
+  g++ -O2 -fPIC -std=c++17 -I"$TMP/include" -c -o "$TMP/ws_batcher_group.o" "$TMP/csrc/ws_batcher_group.cpp"
+  OBJS="$OBJS $TMP/ws_batcher_group.o"
+fi
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$ROOT/tools/bin/libws_$REV.so" $OBJS
 rm -rf "$TMP"
 echo "$ROOT/tools/bin/libws_$REV.so"

@@ -294,7 +294,7 @@ __device__ inline uint32_t tag_get(uint64_t v, uint32_t epoch, uint32_t none) {
 
 // extra scratch of the stream decode (one allocation per engine, grown on demand)
 struct StreamScratch {
-    uint64_t* frame_off;   // [max_frames] two-pass walk: frame starts; then every frame's end
+    uint64_t* frame_off;   // [max_frames] two-pass walk: frame starts
     uint32_t* n_total;     // [1] frames found (0 on capacity overflow)
     uint64_t* read_size;   // [n_reads_total] recv-buffer size after each call
     uint32_t* walk_tmp;    // single pass: per-connection slices of 32-bit frame starts
@@ -2859,11 +2859,11 @@ __global__ __launch_bounds__(kBlock) void k_spec_fix(BatchArgs a, uvhttp_ws_fram
 //   k_swalk_scan    first frame of every connection, total, capacity
 //   k_stream_desc   a wave per connection rebuilds its headers from the walk's frame records
 //                   (or re-reads them: two aligned 16-byte loads each), writes the descriptors
-//                   and message ids, and claims the tile map (lane path: writes frame ends)
-//   k_stream_claims (lane path; the wave path's k_stream_desc claims them itself) a lane per
-//   frame claims the 16 KiB map tiles the frame's end passes
+//                   and message ids, and claims the 16 KiB tiles of the payload kernel's map
+//                   (k_stream_desc_lane: a lane per connection, the same)
 //   payload kernel  (k_unmask_inplace) unmasks every delivered frame in place
-// No look-back, no bounded waits: nothing here can give up.
+// No look-back, no bounded waits: nothing here can give up (k_swalk_fused, an opt-in that
+// folds the walk, the scan and k_stream_desc into one launch, has a bounded look-back).
 // ------------------------------------------------------------------------------------
 struct WalkArgs {
     const uint8_t* wire;
@@ -3599,7 +3599,33 @@ __device__ inline void capacity_result(uvhttp_ws_stream_result_t& r) {
     r.buffered_end = 0;
 }
 
-// lane mode: one lane per connection (few frames each) writes its descriptors in order
+// The payload kernel's tile map: frame i claims the 16 KiB map tiles whose first byte lies in
+// [end of frame i - 1, end of frame i) — the first frame ending after a tile's start, where the
+// kernel's frame range for that tile must begin; the max-of-tag claim keeps the smallest frame.
+// A connection's frame 0 starts its range at its begin when the previous connection's last
+// frame ended exactly there (back to back, nothing undecoded: one claimer per tile), else at
+// the tile holding its begin: that tile, when it starts in an earlier connection's frame, is
+// claimed by that frame as well (the smaller index wins), and tiles wholly between
+// connections' frames (gaps, undecoded tails) hold no payload byte and stay unclaimed, which
+// the payload kernel skips.  (Always the tile floor cost C2 streams 8 us: four connections per
+// tile claiming it from neighbouring lanes of one instruction.)
+__device__ inline uint64_t tile_floor(uint64_t b) { return b / kMapTile * kMapTile; }
+__device__ inline uint64_t claim_start(const WalkArgs& w, uint32_t s, const uvhttp_ws_stream_t& st) {
+    if (s == 0) return tile_floor(st.begin);
+    const uvhttp_ws_stream_result_t& pr = w.results[s - 1];
+    const uint64_t pb = w.streams[s - 1].begin;
+    const bool exact = pr.n_frames != 0 && pr.status == 0 && pb + pr.consumed_bytes == st.begin;
+    return exact ? st.begin : tile_floor(st.begin);
+}
+__device__ inline void stream_claim_tiles(const WalkArgs& w, uint64_t lo, uint64_t fe, uint32_t frame,
+                                          uint32_t epoch) {
+    const uint64_t hi = fe < w.wire_len ? fe : w.wire_len;
+    for (uint64_t t = lo / kMapTile + (lo % kMapTile != 0); t * kMapTile < hi && t < w.n_tiles; ++t)
+        tag_claim(&w.tile_first[t], epoch, frame, w.cas_claims);
+}
+
+// lane mode: one lane per connection (few frames each) writes its descriptors in order and
+// claims the tile map
 __global__ __launch_bounds__(kBlock) void k_stream_desc_lane(WalkArgs w) {
     StampScope stamp_(w.stamp, w.epoch, UVHTTP_WS_STAMP_STREAM_DESC, false);
     const uint32_t s = stamp_.anchor_v(blockIdx.x * kBlock + threadIdx.x);
@@ -3616,6 +3642,8 @@ __global__ __launch_bounds__(kBlock) void k_stream_desc_lane(WalkArgs w) {
     r.first_frame = first;
     const uvhttp_ws_stream_t st = w.streams[s];
     const uint64_t sb = slice_base(st, s);
+    const uint32_t epoch = w.dev_epoch ? w.ctl[kCtlEpoch] : w.epoch;
+    uint64_t lo = claim_start(w, s, st);  // (the claim rule: stream_claim_tiles)
     uint32_t msg = 0;
     for (uint32_t k = 0; k < r.n_frames; ++k) {
         const uint64_t pos = w.single ? w.sc.walk_tmp[sb + k] : w.sc.frame_off[first + k] - st.begin;
@@ -3626,18 +3654,18 @@ __global__ __launch_bounds__(kBlock) void k_stream_desc_lane(WalkArgs w) {
         if (d.status == UVHTTP_WS_FRAME_OK && d.opcode <= 2) d.message = msg;
         msg += fin_data ? 1u : 0u;
         w.desc[first + k] = d;
-        w.sc.frame_off[first + k] = fe;
+        stream_claim_tiles(w, lo, fe, first + k, epoch);
+        lo = fe;
     }
 }
 
 // One wave writes connection s's descriptors (the frames' headers rebuilt from the walk's
 // records or re-read with two aligned 16-byte loads each), the running message id (FIN data
 // frames delivered before the frame in its connection), MSG_END, the failing frame's status,
-// and claims the tile map.  r: the connection's result, first_frame placed; prev_end: the
-// begin of the nearest earlier connection with frames (0: none) — k_stream_claims' rule (frame
-// i claims the map tiles whose first byte lies in [end of frame i - 1, end of frame i)) with
-// frame 0's range starting there (at or before that connection's last frame end; the
-// max-of-tag claim keeps the smallest frame, so claiming more is harmless).
+// and claims the tile map (stream_claim_tiles).  r: the connection's result, first_frame
+// placed; prev_end: where frame 0's claim range starts (claim_start;
+// k_swalk_fused: the begin of the nearest earlier connection with frames — more claims than
+// needed, the smallest frame still wins).
 __device__ inline void stream_desc_wave(const WalkArgs& w, uint32_t s, const uvhttp_ws_stream_t& st,
                                         const uvhttp_ws_stream_result_t& r, uint64_t prev_end,
                                         uint32_t epoch) {
@@ -3676,12 +3704,7 @@ __device__ inline void stream_desc_wave(const WalkArgs& w, uint32_t s, const uvh
             if (lane == 0) lo = prev_end;
             prev_end = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(fe >> 32), 63) << 32) |
                        __builtin_amdgcn_readlane((uint32_t)fe, 63);
-            if (act) {
-                uint64_t hi = fe < w.wire_len ? fe : w.wire_len;
-                const uint32_t fi = r.first_frame + k;
-                for (uint64_t t = lo / kMapTile + (lo % kMapTile != 0); t * kMapTile < hi && t < w.n_tiles; ++t)
-                    tag_claim(&w.tile_first[t], epoch, fi, w.cas_claims);
-            }
+            if (act) stream_claim_tiles(w, lo, fe, r.first_frame + k, epoch);
             // message id: FIN data frames delivered before this one in the connection
             const uint64_t fm = __ballot(fin_data);
             const uint32_t before = msg + (uint32_t)__builtin_popcountll(fm & ((1ull << lane) - 1));
@@ -3707,14 +3730,10 @@ __global__ __launch_bounds__(kBlock) void k_stream_desc(WalkArgs w) {
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint32_t s = stamp_.anchor_s(blockIdx.x * (kBlock / 64) + wave);
     if (s >= w.n_streams) return;
-    // every load of the setup issued together, the predecessor's unconditionally (a chain of
-    // result -> total -> predecessor's result -> its stream was four dependent round trips)
-    const uint32_t sp = s ? s - 1 : 0;
+    // every load of the setup issued together
     uvhttp_ws_stream_result_t r = w.results[s];
     const uint32_t first = w.agg[s];  // (k_swalk_scan's prefix)
     const uint32_t n_total = *w.sc.n_total;
-    const uint32_t prev_n = w.results[sp].n_frames;
-    const uint64_t prev_b = w.streams[sp].begin;
     const uvhttp_ws_stream_t st = w.streams[s];
     r.first_frame = first;
     const bool fits = n_total != 0 || r.n_frames == 0;
@@ -3727,22 +3746,7 @@ __global__ __launch_bounds__(kBlock) void k_stream_desc(WalkArgs w) {
     }
     if (lane == 0) w.results[s].first_frame = r.first_frame;
     if (!r.n_frames) return;
-    // prev_end: the direct predecessor first; past it, 64 connections per step by a ballot, so
-    // a long run of connections without frames costs one round trip per 64
-    uint64_t prev_end = 0;
-    if (s > 0 && prev_n) {
-        prev_end = prev_b;
-    } else {
-        for (int64_t base = (int64_t)s - 2; base >= 0; base -= 64) {
-            const int64_t j = base - (int64_t)lane;
-            const uint64_t m = __ballot(j >= 0 && w.results[j].n_frames != 0);
-            if (m) {
-                prev_end = w.streams[base - __builtin_ctzll(m)].begin;
-                break;
-            }
-        }
-    }
-    stream_desc_wave(w, s, st, r, prev_end, w.dev_epoch ? w.ctl[kCtlEpoch] : w.epoch);
+    stream_desc_wave(w, s, st, r, claim_start(w, s, st), w.dev_epoch ? w.ctl[kCtlEpoch] : w.epoch);
 }
 
 // ---- k_swalk_fused: walk, first frame and descriptors of a connection in one launch -------
@@ -3927,24 +3931,6 @@ __global__ __launch_bounds__(kBlock) void k_swalk_fused(WalkArgs w) {
     if (!over && !gave_up && r.n_frames) stream_desc_wave(w, s, w.streams[s], r, pre.hb ? pre.hb - 1 : 0ull, epoch);
 }
 
-// k_stream_claims: frame i claims the 16 KiB map tiles whose first byte lies in
-// [end of frame i - 1, end of frame i): the first frame ending after a tile's start, which is
-// where the payload kernel's frame range for that tile must begin (gaps between connections
-// and undecoded tails are covered by the next frame, tiles after the last frame stay
-// unclaimed and are skipped)
-__global__ __launch_bounds__(kBlock) void k_stream_claims(BatchArgs a, Workspace ws,
-                                                          const uint64_t* frame_end) {
-    resolve_epoch(a, ws);
-    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_CLAIMS);
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t n = nframes(a);
-    if (i >= n) return;
-    const uint64_t lo = i ? frame_end[i - 1] : 0;
-    uint64_t hi = frame_end[i];
-    if (hi > a.wire_len) hi = a.wire_len;
-    for (uint64_t t = lo / kMapTile + (lo % kMapTile != 0); t * kMapTile < hi && t < a.n_tiles; ++t)
-        tag_claim(&ws.tile_first[t], a.epoch, i, a.cas_claims);
-}
 
 
 // ------------------------------------------------------------------------------------
@@ -5712,10 +5698,7 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     a.epoch = w.epoch;
     a.stamp = w.stamp;
     a.cas_claims = w.cas_claims;
-    // (the wave path's k_stream_desc claimed the tile map already)
-    if (!wave_walk)
-        hipLaunchKernelGGL(k_stream_claims, dim3((cap + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a,
-                           e->ws, (const uint64_t*)e->ss.frame_off);
+    // (k_stream_desc / k_stream_desc_lane claimed the tile map)
     // payload tile shape: the frame count is only known on the device, so the caller's frame
     // capacity stands in for it (wire bytes per frame slot; the same rule as the batch decode)
     int blk = e->tile_block, vpt = e->tile_vpt;
