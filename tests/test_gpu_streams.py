@@ -138,11 +138,13 @@ def _cut(rng, data, sizes=(0, 1, 2, 3, 7, 100, 1000, 4096, 16384)):
     return reads
 
 
-def _run_cases(torch, eng, U, cases, rng, max_frames, use_reads=False):
+def _run_cases(torch, eng, U, cases, rng, max_frames, use_reads=False, gaps=(0, 0, 16, 48)):
     """One device call over every (product conn, oracle conn, reads) case, then the reference
     semantics: deliver_stream on the product side vs the oracle's process_data called once per
     read until a call fails (on_websocket_read, src/uvhttp_connection.c:1128-1164).  With
-    use_reads=False each case's reads are joined into ONE call (n_reads = 0)."""
+    use_reads=False each case's reads are joined into ONE call (n_reads = 0).  The gaps between
+    connections (rng.choice(gaps) bytes after 16-byte alignment) hold random bytes no kernel may
+    touch."""
     # batch wire: each connection's buffered bytes + new reads, 16-B aligned starts, gaps
     chunks, streams, read_end, pos = [], [], [], 0
     for prod, orc, reads in cases:
@@ -152,7 +154,7 @@ def _run_cases(torch, eng, U, cases, rng, max_frames, use_reads=False):
         buffered = C.string_at(st.recv_buffer, st.recv_buffer_pos) if st.recv_buffer_pos else b""
         data = buffered + b"".join(reads)
         pos = (pos + 15) & ~15
-        pos += rng.choice([0, 0, 16, 48])
+        pos += rng.choice(gaps)
         s = U.Stream()
         U.lib().uvhttp_ws_stream_init(prod.ptr, pos, len(data), C.byref(s))
         if use_reads:
@@ -164,11 +166,13 @@ def _run_cases(torch, eng, U, cases, rng, max_frames, use_reads=False):
         streams.append(s)
         chunks.append((pos, data))
         pos += len(data)
-    wire = np.zeros(pos + 64, np.uint8)
-    guard = np.frombuffer(bytes(rng.getrandbits(8) for _ in range(64)), np.uint8)
-    wire[pos:] = guard  # bytes past wire_len: never written
+    wire = np.random.default_rng(rng.getrandbits(32)).integers(0, 256, pos + 64, dtype=np.uint8)
+    guard = wire[pos:].copy()  # bytes past wire_len: never written
     for p, d in chunks:
         wire[p:p + len(d)] = np.frombuffer(d, np.uint8)
+    outside = np.ones(pos, bool)  # the gaps between connections
+    for p, d in chunks:
+        outside[p:p + len(d)] = False
     n = len(streams)
     sbytes = b"".join(bytes(s) for s in streams)
     dev_streams = torch.from_numpy(np.frombuffer(sbytes, np.uint8).copy()).to("cuda")
@@ -187,6 +191,7 @@ def _run_cases(torch, eng, U, cases, rng, max_frames, use_reads=False):
     host_desc = desc.cpu().numpy()
     # guard bytes: nothing past the wire, the desc array or the results array was written
     assert np.array_equal(host_wire[pos:], guard)
+    assert np.array_equal(host_wire[:pos][outside], wire[:pos][outside])
     assert (host_desc[max_frames * 32:] == 0xA5).all()
     assert (res.cpu().numpy()[n * U.STREAM_RESULT_BYTES:] == 0x5A).all()
     hw = (C.c_uint8 * host_wire.size).from_buffer(host_wire)
@@ -230,6 +235,17 @@ def test_streams_match_process_data(torch, eng, hooks, seed):
     bad = seed % 2 == 1
     cases = [c for c in (_conn_case(rng, U, bad) for _ in range(rng.choice([1, 5, 40, 200]))) if c]
     _run_cases(torch, eng, U, cases, rng, 4096)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_streams_tile_sized_gaps(torch, eng, hooks, seed):
+    """Gaps between connections of up to several 16 KiB map tiles (random bytes that must stay
+    as they are) and long undecoded tails: map tiles wholly between connections' frames stay
+    unclaimed (k_stream_desc's claim rule), every connection still decodes as process_data."""
+    import uvhttp_amd as U
+    rng = random.Random(9500 + seed)
+    cases = [c for c in (_conn_case(rng, U, seed == 1) for _ in range(rng.choice([20, 60]))) if c]
+    _run_cases(torch, eng, U, cases, rng, 4096, gaps=(0, 16, 16384, 20000, 49152, 70000))
 
 
 def test_streams_capacity_overflow(torch, eng):
