@@ -2890,6 +2890,7 @@ struct WalkArgs {
     uint32_t no_ticket;        // k_swalk_fused: blocks in blockIdx order (UVHTTP_WS_PLAN_TICKET=0)
     uint64_t* first_bad;       // Workspace::first_bad (k_swalk_fused: a look-back give-up)
     uint32_t nt_stores;        // UVHTTP_WS_STREAM_NT=1: frame records and descriptors as streaming stores
+    uint32_t desc_scan;        // k_stream_desc finds first frames itself (no k_swalk_scan)
 };
 
 // process_data's buffer growth: returns false on failure (*out = size then), else the size
@@ -3725,15 +3726,49 @@ __device__ inline void stream_desc_wave(const WalkArgs& w, uint32_t s, const uvh
 
 // k_stream_desc: one wave per connection (stream_desc_wave) after k_swalk_scan.  Capacity
 // overflow: every result says so, nothing else.
+// (desc_scan: at most kDescScanMax connections, so each workgroup's pass over the counts is
+// 16 loads per thread of a 16 KiB array every XCD's L2 holds)
+constexpr uint32_t kDescScanMax = 4096;
+
 __global__ __launch_bounds__(kBlock) void k_stream_desc(WalkArgs w) {
     StampScope stamp_(w.stamp, w.epoch, UVHTTP_WS_STAMP_STREAM_DESC, false);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint32_t s = stamp_.anchor_s(blockIdx.x * (kBlock / 64) + wave);
-    if (s >= w.n_streams) return;
+    uint32_t first, n_total;
+    if (w.desc_scan) {
+        // k_swalk_scan's work here: the walk left each connection's frame count in agg; every
+        // workgroup sums all of them (the total, capacity) and those before its first
+        // connection, then adds its own earlier waves' (one launch and its boundary fewer)
+        const uint32_t s0 = blockIdx.x * (kBlock / 64);
+        // (all 16 loads issued before any is used: as a loop they ran one round trip each,
+        // 15.7 us for this kernel instead of 11.5)
+        uint32_t v[kDescScanMax / kBlock];
+#pragma unroll
+        for (uint32_t k = 0; k < kDescScanMax / kBlock; ++k) {
+            const uint32_t j = threadIdx.x + k * kBlock;
+            v[k] = j < w.n_streams ? w.agg[j] : 0u;
+        }
+        uint64_t tot = 0, pre = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kDescScanMax / kBlock; ++k) {
+            tot += v[k];
+            pre += threadIdx.x + k * kBlock < s0 ? v[k] : 0u;
+        }
+        uint64_t all_pre, all_tot;
+        (void)block_exclusive_sum_u64(pre, &all_pre);
+        (void)block_exclusive_sum_u64(tot, &all_tot);
+        for (uint32_t k = s0; k < s && k < w.n_streams; ++k) all_pre += w.agg[k];
+        first = (uint32_t)all_pre;
+        n_total = all_tot <= w.max_frames ? (uint32_t)all_tot : 0u;
+        if (blockIdx.x == 0 && threadIdx.x == 0) *w.sc.n_total = n_total;
+        if (s >= w.n_streams) return;
+    } else {
+        if (s >= w.n_streams) return;
+        first = w.agg[s];  // (k_swalk_scan's prefix)
+        n_total = *w.sc.n_total;
+    }
     // every load of the setup issued together
     uvhttp_ws_stream_result_t r = w.results[s];
-    const uint32_t first = w.agg[s];  // (k_swalk_scan's prefix)
-    const uint32_t n_total = *w.sc.n_total;
     const uvhttp_ws_stream_t st = w.streams[s];
     r.first_frame = first;
     const bool fits = n_total != 0 || r.n_frames == 0;
@@ -4613,6 +4648,7 @@ struct uvhttp_ws_gpu_engine {
     int walk_single_off;       // UVHTTP_WS_WALK_SINGLE=0: always walk twice (tests, A/B)
     int walk_fuse;             // UVHTTP_WS_WALK_FUSE=1: k_swalk_fused for the single-pass wave walk
     int stream_nt;             // UVHTTP_WS_STREAM_NT=1: streaming stores in the walk and k_stream_desc (A/B)
+    int desc_scan_off;         // UVHTTP_WS_DESC_SCAN=0: k_swalk_scan before k_stream_desc always (A/B)
     int fused_block, fused_vpt;  // UVHTTP_WS_FUSED_TILE=BxV: the fused payload pass's tile (A/B)
     uint32_t fixup_blocks;     // k_fixup grid cap (UVHTTP_WS_FIXUP_BLOCKS, A/B)
     int fused_aux;             // fused payload stores' cache-policy bits (UVHTTP_WS_FUSED_AUX, A/B)
@@ -4726,6 +4762,7 @@ int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out) {
     e->wr_rec_on = 1;
     if (const char* wf = getenv("UVHTTP_WS_WALK_FUSE")) e->walk_fuse = atoi(wf) != 0;
     if (const char* sn = getenv("UVHTTP_WS_STREAM_NT")) e->stream_nt = atoi(sn) != 0;
+    if (const char* ds = getenv("UVHTTP_WS_DESC_SCAN")) e->desc_scan_off = atoi(ds) == 0;
     if (const char* wr = getenv("UVHTTP_WS_WALK_REC")) e->wr_rec_on = atoi(wr) != 0;
     if (const char* wm = getenv("UVHTTP_WS_WALK"))
         e->walk_mode = strcmp(wm, "lane") == 0 ? 1 : strcmp(wm, "wave") == 0 ? 2 : 0;
@@ -5652,6 +5689,7 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     w.max_polls = e->max_polls;
     w.no_ticket = e->plan_no_ticket;
     w.nt_stores = e->stream_nt ? 1u : 0u;
+    w.desc_scan = 0;
     w.first_bad = e->ws.first_bad;
     const uint32_t nsb = (n_streams + kBlock - 1) / kBlock;
     const uint32_t nwb = (n_streams + kBlock / 64 - 1) / (kBlock / 64);
@@ -5671,7 +5709,9 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
             if (w.single) hipLaunchKernelGGL(k_swalk_lane<2>, dim3(nsb), dim3(kBlock), 0, s, w);
             else hipLaunchKernelGGL(k_swalk_lane<0>, dim3(nsb), dim3(kBlock), 0, s, w);
         }
-        hipLaunchKernelGGL(k_swalk_scan, dim3(1), dim3(kBlock), 0, s, w, wave_walk ? 0u : 1u);
+        // (single-pass wave walk over at most kDescScanMax connections: k_stream_desc scans)
+        w.desc_scan = (wave_walk && w.single && n_streams <= kDescScanMax && !e->desc_scan_off) ? 1u : 0u;
+        if (!w.desc_scan) hipLaunchKernelGGL(k_swalk_scan, dim3(1), dim3(kBlock), 0, s, w, wave_walk ? 0u : 1u);
         if (!w.single) {
             if (wave_walk) hipLaunchKernelGGL(k_swalk_wave<1>, dim3(nwb), dim3(kBlock), 0, s, w);
             else hipLaunchKernelGGL(k_swalk_lane<1>, dim3(nsb), dim3(kBlock), 0, s, w);
