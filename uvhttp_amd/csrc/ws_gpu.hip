@@ -292,6 +292,9 @@ __device__ inline uint32_t tag_get(uint64_t v, uint32_t epoch, uint32_t none) {
     return (uint32_t)(v >> 32) == epoch ? ~(uint32_t)v : none;
 }
 
+// k_swalk_fused runs for the wave walk only (at most 16 384 connections, 4 per block)
+constexpr uint32_t kSwalkFusedMaxBlocks = 16384 / 4;
+
 // extra scratch of the stream decode (one allocation per engine, grown on demand)
 struct StreamScratch {
     uint64_t* frame_off;   // [max_frames] two-pass walk: frame starts
@@ -303,7 +306,7 @@ struct StreamScratch {
     uint32_t* agg;         // [n_streams / 256 + 1] lane walk block counts -> prefixes
     uint32_t* ctr;         // [4] k_swalk_fused: [0] block ticket, [1] connections done (both
                            // reset by their last taker), [2] epoch of a call over capacity
-    void* srec;            // [2 n_streams] k_swalk_fused look-back records (A, P per connection)
+    void* srec;            // [2 kSwalkFusedMaxBlocks] k_swalk_fused look-back records (A, P per block)
 };
 
 // parse_hdr's result for one frame, 16 bytes (stride batches: written by the payload pass,
@@ -4638,7 +4641,7 @@ struct uvhttp_ws_gpu_engine {
     uint32_t plan_no_ticket;   // UVHTTP_WS_PLAN_TICKET=0: blockIdx order instead of tickets
     int walk_mode;             // stream frame discovery: 0 automatic, 1 lane, 2 wave
     void* ss_mem;              // stream-decode scratch
-    uint32_t ss_frames, ss_reads, ss_streams;
+    uint32_t ss_frames, ss_reads;
     StreamScratch ss;
     void* wt_mem;              // single-pass walk scratch (frame starts per connection slice)
     uint64_t wt_cap;
@@ -5561,34 +5564,43 @@ int uvhttp_ws_gpu_decode_compact(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batc
 static int reserve_streams(uvhttp_ws_gpu_engine_t* e, uint32_t frames, uint32_t streams,
                            uint32_t reads) {
     if (reads == 0) reads = 1;
-    if (e->ss_mem && frames <= e->ss_frames && reads <= e->ss_reads && streams <= e->ss_streams)
-        return UVHTTP_WS_GPU_OK;
+    // (the look-back records are sized for the most blocks k_swalk_fused runs, 16 384 / 4, so
+    // the connection count of a call never reallocates: a caller such as the batcher issues a
+    // call while its previous one still runs on the stream)
+    (void)streams;
+    if (e->ss_mem && frames <= e->ss_frames && reads <= e->ss_reads) return UVHTTP_WS_GPU_OK;
     if (e->capturing)
         return set_err(e, UVHTTP_WS_GPU_EINVAL, "stream scratch too small for a captured call",
                        hipSuccess);
     const uint32_t fr = frames > e->ss_frames ? frames : e->ss_frames;
     const uint32_t rd = reads > e->ss_reads ? reads : e->ss_reads;
-    const uint32_t sn = streams > e->ss_streams ? streams : e->ss_streams;
     size_t o_off = 0;
     size_t o_tot = align_up(o_off + (size_t)fr * 8, 256);
     size_t o_rsize = align_up(o_tot + 16, 256);
     size_t o_agg = align_up(o_rsize + (size_t)rd * 8, 256);
     size_t o_ctr = align_up(o_agg + ((size_t)kMaxFrames / kBlock + 2) * 4, 256);
     size_t o_srec = align_up(o_ctr + 16, 256);
-    size_t bytes = align_up(o_srec + (size_t)sn * 32, 256);
+    size_t bytes = align_up(o_srec + (size_t)kSwalkFusedMaxBlocks * 32, 256);
     int prev = 0;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(e->device);
-    if (e->ss_mem) (void)hipFree(e->ss_mem);
+    // (a call of this engine may still run on the caller's stream: let it finish first)
+    if (e->ss_mem) {
+        (void)hipDeviceSynchronize();
+        (void)hipFree(e->ss_mem);
+    }
     e->ss_mem = nullptr;
     hipError_t h = hipMalloc(&e->ss_mem, bytes);
-    // (zero: the counters start at 0 and no record tag matches a live epoch)
+    // (zero: the counters start at 0 and no record tag matches a live epoch; finished before
+    // the call's kernels run on the caller's stream, which the null-stream memset does not
+    // order — as the workspace's reserve)
     if (h == hipSuccess) h = hipMemset(e->ss_mem, 0, bytes);
+    if (h == hipSuccess) h = hipDeviceSynchronize();
     (void)hipSetDevice(prev);
     if (h != hipSuccess) {
         if (e->ss_mem) (void)hipFree(e->ss_mem);
         e->ss_mem = nullptr;
-        e->ss_frames = e->ss_reads = e->ss_streams = 0;
+        e->ss_frames = e->ss_reads = 0;
         return set_err(e, UVHTTP_WS_GPU_ENOMEM, "hipMalloc stream scratch", h);
     }
     char* b = (char*)e->ss_mem;
@@ -5598,7 +5610,6 @@ static int reserve_streams(uvhttp_ws_gpu_engine_t* e, uint32_t frames, uint32_t 
     e->ss.agg = (uint32_t*)(b + o_agg);
     e->ss.ctr = (uint32_t*)(b + o_ctr);
     e->ss.srec = (void*)(b + o_srec);
-    e->ss_streams = sn;
     e->ss_frames = fr;
     e->ss_reads = rd;
     return UVHTTP_WS_GPU_OK;
@@ -5650,7 +5661,10 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     // slices: connection s's starts at walk_tmp[begin / 2 + s ...] (4-byte entries)
     const uint64_t want = wire_len / 2 + n_streams + 1;
     if (single_ok && !e->capturing && want * 4 <= (8ull << 30) && want > e->wt_cap) {
-        if (e->wt_mem) (void)hipFree(e->wt_mem);
+        if (e->wt_mem) {
+            (void)hipDeviceSynchronize();  // (an earlier call may still use the slices)
+            (void)hipFree(e->wt_mem);
+        }
         e->wt_mem = nullptr;
         e->wt_cap = 0;
         if (hipMalloc(&e->wt_mem, want * 4) == hipSuccess) e->wt_cap = want;
@@ -5659,7 +5673,10 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     // within 8 GiB together; larger calls gather every header again in k_stream_desc
     // (only the wave walk writes and reads them: none for the lane walk — 1 GB less for C2)
     if (single_ok && wave_walk && !e->capturing && want * 12 <= (8ull << 30) && want > e->wr_cap) {
-        if (e->wr_mem) (void)hipFree(e->wr_mem);
+        if (e->wr_mem) {
+            (void)hipDeviceSynchronize();
+            (void)hipFree(e->wr_mem);
+        }
         e->wr_mem = nullptr;
         e->wr_cap = 0;
         if (hipMalloc(&e->wr_mem, want * 8) == hipSuccess) e->wr_cap = want;
@@ -5698,7 +5715,8 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     // results are finished by the payload kernel's first workgroup, so not for an empty wire).
     // Not the default: it measured even with the three launches (C4 142.8 vs 142.6 us per
     // step, profiles/r05fy_*) and only without the block tickets (with them 155 us).
-    const bool fused = wave_walk && w.single && e->walk_fuse && wire_len > 0;
+    const bool fused = wave_walk && w.single && e->walk_fuse && wire_len > 0 &&
+                       n_streams <= kSwalkFusedMaxBlocks * (kBlock / 64);  // (its records)
     if (fused) {
         hipLaunchKernelGGL(k_swalk_fused, dim3(nwb), dim3(kBlock), 0, s, w);
     } else {
