@@ -248,6 +248,63 @@ def test_streams_tile_sized_gaps(torch, eng, hooks, seed):
     _run_cases(torch, eng, U, cases, rng, 4096, gaps=(0, 16, 16384, 20000, 49152, 70000))
 
 
+def _layout(U, cases, rng, gaps=(0, 16, 48)):
+    """the wire and stream table of a one-call decode of `cases` (their reads joined)"""
+    chunks, streams, pos = [], [], 0
+    for prod, _orc, reads in cases:
+        st = prod.struct
+        buffered = C.string_at(st.recv_buffer, st.recv_buffer_pos) if st.recv_buffer_pos else b""
+        data = buffered + b"".join(reads)
+        pos = ((pos + 15) & ~15) + rng.choice(gaps)
+        s = U.Stream()
+        U.lib().uvhttp_ws_stream_init(prod.ptr, pos, len(data), C.byref(s))
+        streams.append(s)
+        chunks.append((pos, data))
+        pos += len(data)
+    wire = np.zeros(pos + 64, np.uint8)
+    for p, d in chunks:
+        wire[p:p + len(d)] = np.frombuffer(d, np.uint8)
+    return wire, b"".join(bytes(s) for s in streams), len(streams), pos
+
+
+def test_streams_back_to_back_growth(torch, hooks):
+    """A call issued while the previous one still runs, with more connections and a longer wire
+    (the engine's stream scratch, slices and frame records grow under it — round 5's closing
+    run crashed on this in the batcher): both decode exactly as each does alone on a fresh
+    engine (wire, descriptors, results)."""
+    import uvhttp_amd as U
+    rng = random.Random(4242)
+    calls = []
+    for nconn in (3, 120, 400):
+        cases = [c for c in (_conn_case(rng, U, False) for _ in range(nconn)) if c]
+        calls.append(_layout(U, cases, rng))
+
+    def run(eng, k):
+        wire, sb, n, wl = calls[k]
+        dw = torch.from_numpy(wire.copy()).to("cuda")
+        ds = torch.from_numpy(np.frombuffer(sb, np.uint8).copy()).to("cuda")
+        desc, res = eng.decode_streams(dw, ds, n, 16384, wire_len=wl)
+        return dw, desc, res, ds
+
+    eng = U.GpuEngine(0)
+    outs = [run(eng, k) for k in range(len(calls))]  # no sync between the calls
+    torch.cuda.synchronize()
+    eng.sync()
+    for k, (dw, desc, res, _ds) in enumerate(outs):
+        alone = U.GpuEngine(0)
+        aw, adesc, ares, _ = run(alone, k)
+        torch.cuda.synchronize()
+        alone.sync()
+        n = calls[k][2]
+        ra, rb = eng.read_stream_results(res, n), alone.read_stream_results(ares, n)
+        assert [r.as_dict() for r in ra] == [r.as_dict() for r in rb], k
+        assert torch.equal(dw, aw), k
+        nf = max((r.first_frame + r.n_frames for r in ra), default=0)
+        assert torch.equal(desc[:nf * 32], adesc[:nf * 32]), k
+        alone.close()
+    eng.close()
+
+
 def test_streams_capacity_overflow(torch, eng):
     import uvhttp_amd as U
     frames = b"".join(_frame(2, 1, b"x", b"\x00\x00\x00\x01") for _ in range(50))
