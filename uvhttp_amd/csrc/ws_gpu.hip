@@ -562,11 +562,14 @@ __device__ inline uint32_t rotr32(uint32_t x, uint32_t s) {
 // come from the two ALIGNED 16-byte vectors around them and a byte funnel shift: an unaligned
 // 16-byte copy compiles to sixteen byte loads on gfx950 (k_plan spent most of its time there).
 // The last 32 bytes of the buffer go bytewise so nothing past `len` is read.
+template <bool NT = false>
 __device__ inline u32x4 load16_at(const uint8_t* base, uint64_t len, uint64_t o) {
     const uint64_t lo = o & ~(uint64_t)15;
     if (len >= 32 && lo <= len - 32) {  // (cannot wrap for o near 2^64)
-        const u32x4 v0 = *reinterpret_cast<const u32x4*>(base + lo);
-        const u32x4 v1 = *reinterpret_cast<const u32x4*>(base + lo + 16);
+        const u32x4 v0 = NT ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(base + lo))
+                            : *reinterpret_cast<const u32x4*>(base + lo);
+        const u32x4 v1 = NT ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(base + lo + 16))
+                            : *reinterpret_cast<const u32x4*>(base + lo + 16);
         uint64_t x0 = v0.x | ((uint64_t)v0.y << 32), x1 = v0.z | ((uint64_t)v0.w << 32);
         uint64_t x2 = v1.x | ((uint64_t)v1.y << 32);
         const uint64_t x3 = v1.z | ((uint64_t)v1.w << 32);
@@ -2894,6 +2897,7 @@ struct WalkArgs {
     uint64_t* first_bad;       // Workspace::first_bad (k_swalk_fused: a look-back give-up)
     uint32_t nt_stores;        // UVHTTP_WS_STREAM_NT=1: frame records and descriptors as streaming stores
     uint32_t desc_scan;        // k_stream_desc finds first frames itself (no k_swalk_scan)
+    uint32_t nt_loads;         // UVHTTP_WS_WALK_NT_LOAD=1: the wave walk's header loads non-temporal (A/B)
 };
 
 // process_data's buffer growth: returns false on failure (*out = size then), else the size
@@ -3347,7 +3351,10 @@ __device__ inline uvhttp_ws_stream_result_t walk_wave(const WalkArgs& w, uint32_
             // a header's 16 bytes (issued apart from the decode, so several are in flight), then
             // its fields and the frame's record for k_stream_desc: key and header bytes, kNoRec
             // for a 64-bit length
-            auto fetch = [&](uint64_t p) { return load16_at(w.wire, w.wire_len, st.begin + p); };
+            auto fetch = [&](uint64_t p) {
+                return w.nt_loads ? load16_at<true>(w.wire, w.wire_len, st.begin + p)
+                                  : load16_at(w.wire, w.wire_len, st.begin + p);
+            };
             auto decode16 = [&](const u32x4& v, uint32_t& b0, uint32_t& wl, uint64_t& plen, bool& bad,
                                 uint2& rec) {
                 const uint32_t x[4] = {v.x, v.y, v.z, v.w};
@@ -4652,6 +4659,7 @@ struct uvhttp_ws_gpu_engine {
     int walk_fuse;             // UVHTTP_WS_WALK_FUSE=1: k_swalk_fused for the single-pass wave walk
     int stream_nt;             // UVHTTP_WS_STREAM_NT=1: streaming stores in the walk and k_stream_desc (A/B)
     int desc_scan_off;         // UVHTTP_WS_DESC_SCAN=0: k_swalk_scan before k_stream_desc always (A/B)
+    int walk_nt_load;          // UVHTTP_WS_WALK_NT_LOAD=1: non-temporal header loads in the wave walk (A/B)
     int fused_block, fused_vpt;  // UVHTTP_WS_FUSED_TILE=BxV: the fused payload pass's tile (A/B)
     uint32_t fixup_blocks;     // k_fixup grid cap (UVHTTP_WS_FIXUP_BLOCKS, A/B)
     int fused_aux;             // fused payload stores' cache-policy bits (UVHTTP_WS_FUSED_AUX, A/B)
@@ -4766,6 +4774,7 @@ int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out) {
     if (const char* wf = getenv("UVHTTP_WS_WALK_FUSE")) e->walk_fuse = atoi(wf) != 0;
     if (const char* sn = getenv("UVHTTP_WS_STREAM_NT")) e->stream_nt = atoi(sn) != 0;
     if (const char* ds = getenv("UVHTTP_WS_DESC_SCAN")) e->desc_scan_off = atoi(ds) == 0;
+    if (const char* wn = getenv("UVHTTP_WS_WALK_NT_LOAD")) e->walk_nt_load = atoi(wn) != 0;
     if (const char* wr = getenv("UVHTTP_WS_WALK_REC")) e->wr_rec_on = atoi(wr) != 0;
     if (const char* wm = getenv("UVHTTP_WS_WALK"))
         e->walk_mode = strcmp(wm, "lane") == 0 ? 1 : strcmp(wm, "wave") == 0 ? 2 : 0;
@@ -5707,6 +5716,7 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     w.no_ticket = e->plan_no_ticket;
     w.nt_stores = e->stream_nt ? 1u : 0u;
     w.desc_scan = 0;
+    w.nt_loads = e->walk_nt_load ? 1u : 0u;
     w.first_bad = e->ws.first_bad;
     const uint32_t nsb = (n_streams + kBlock - 1) / kBlock;
     const uint32_t nwb = (n_streams + kBlock / 64 - 1) / (kBlock / 64);
