@@ -3635,15 +3635,37 @@ __device__ inline void stream_claim_tiles(const WalkArgs& w, uint64_t lo, uint64
         tag_claim(&w.tile_first[t], epoch, frame, w.cas_claims);
 }
 
+// (desc_scan, wave path: at most kDescScanMax connections, so each workgroup's pass over the counts is
+// 16 loads per thread of a 16 KiB array every XCD's L2 holds)
+constexpr uint32_t kDescScanMax = 4096;
+constexpr uint32_t kDescScanLaneMax = kBlock * kBlock;  // (k_stream_desc_lane: one block total per thread)
+
 // lane mode: one lane per connection (few frames each) writes its descriptors in order and
 // claims the tile map
 __global__ __launch_bounds__(kBlock) void k_stream_desc_lane(WalkArgs w) {
     StampScope stamp_(w.stamp, w.epoch, UVHTTP_WS_STAMP_STREAM_DESC, false);
     const uint32_t s = stamp_.anchor_v(blockIdx.x * kBlock + threadIdx.x);
-    const uint32_t first = lane_first(w, s);
+    uint32_t first, n_total;
+    if (w.desc_scan) {
+        // k_swalk_scan's work here (single pass, at most kDescScanLaneMax connections): the lane
+        // walk left each block's frame count in agg, at most one per thread of this block
+        const uint32_t nb = (w.n_streams + kBlock - 1) / kBlock;
+        const uint32_t v = threadIdx.x < nb ? w.agg[threadIdx.x] : 0u;
+        uint64_t pre_b, tot;
+        (void)block_exclusive_sum_u64(threadIdx.x < blockIdx.x ? v : 0u, &pre_b);
+        (void)block_exclusive_sum_u64(v, &tot);
+        const uint32_t c = s < w.n_streams ? w.results[s].n_frames : 0u;
+        uint32_t blk_total;
+        first = (uint32_t)pre_b + block_scan_u32(c, &blk_total);
+        n_total = tot <= w.max_frames ? (uint32_t)tot : 0u;
+        if (blockIdx.x == 0 && threadIdx.x == 0) *w.sc.n_total = n_total;
+    } else {
+        first = lane_first(w, s);
+        n_total = s < w.n_streams ? *w.sc.n_total : 0u;
+    }
     if (s >= w.n_streams) return;
     uvhttp_ws_stream_result_t r = w.results[s];
-    if (*w.sc.n_total == 0 && r.n_frames) {
+    if (n_total == 0 && r.n_frames) {
         capacity_result(r);
         w.results[s] = r;
         return;
@@ -3736,9 +3758,6 @@ __device__ inline void stream_desc_wave(const WalkArgs& w, uint32_t s, const uvh
 
 // k_stream_desc: one wave per connection (stream_desc_wave) after k_swalk_scan.  Capacity
 // overflow: every result says so, nothing else.
-// (desc_scan: at most kDescScanMax connections, so each workgroup's pass over the counts is
-// 16 loads per thread of a 16 KiB array every XCD's L2 holds)
-constexpr uint32_t kDescScanMax = 4096;
 
 __global__ __launch_bounds__(kBlock) void k_stream_desc(WalkArgs w) {
     StampScope stamp_(w.stamp, w.epoch, UVHTTP_WS_STAMP_STREAM_DESC, false);
@@ -5737,8 +5756,10 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
             if (w.single) hipLaunchKernelGGL(k_swalk_lane<2>, dim3(nsb), dim3(kBlock), 0, s, w);
             else hipLaunchKernelGGL(k_swalk_lane<0>, dim3(nsb), dim3(kBlock), 0, s, w);
         }
-        // (single-pass wave walk over at most kDescScanMax connections: k_stream_desc scans)
-        w.desc_scan = (wave_walk && w.single && n_streams <= kDescScanMax && !e->desc_scan_off) ? 1u : 0u;
+        // (single pass over at most kDescScanMax / kDescScanLaneMax connections: k_stream_desc /
+        // k_stream_desc_lane scan)
+        w.desc_scan = (w.single && n_streams <= (wave_walk ? kDescScanMax : kDescScanLaneMax) &&
+                       !e->desc_scan_off) ? 1u : 0u;
         if (!w.desc_scan) hipLaunchKernelGGL(k_swalk_scan, dim3(1), dim3(kBlock), 0, s, w, wave_walk ? 0u : 1u);
         if (!w.single) {
             if (wave_walk) hipLaunchKernelGGL(k_swalk_wave<1>, dim3(nwb), dim3(kBlock), 0, s, w);
