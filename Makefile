@@ -6,8 +6,11 @@ CC ?= gcc
 ARCH ?= gfx950
 BUILD := uvhttp_amd/build
 LIB := uvhttp_amd/lib/libuvhttp_ws_amd.so
-# the same library with the batcher's fault-injection hook compiled in (tests only)
+# the same library built with -DUVWS_TEST_HOOKS -DUVWS_EXPERIMENTS (tests and A/B tools only):
+# the batcher's fault-injection hook and the environment switches (UVHTTP_WS_*) the measurements
+# and the variant tests use.  The product library reads no environment.
 TESTLIB := uvhttp_amd/lib/libuvhttp_ws_amd_testhooks.so
+EXP := -DUVWS_EXPERIMENTS
 
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Iinclude -Wall -Werror \
             -mcode-object-version=5
@@ -29,7 +32,19 @@ $(BUILD)/ws_batcher.o: uvhttp_amd/csrc/ws_batcher.hip include/uvhttp_ws_amd.h
 
 $(BUILD)/ws_batcher_testhooks.o: uvhttp_amd/csrc/ws_batcher.hip include/uvhttp_ws_amd.h
 	@mkdir -p $(BUILD)
-	$(HIPCC) $(HIPFLAGS) -DUVWS_TEST_HOOKS -c -o $@ $<
+	$(HIPCC) $(HIPFLAGS) -DUVWS_TEST_HOOKS $(EXP) -c -o $@ $<
+
+$(BUILD)/ws_gpu_exp.o: uvhttp_amd/csrc/ws_gpu.hip include/uvhttp_ws_amd.h
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) $(EXP) -c -o $@ $<
+
+$(BUILD)/tls_gpu_exp.o: uvhttp_amd/csrc/tls_gpu.hip include/uvhttp_tls_amd.h
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) $(EXP) -c -o $@ $<
+
+$(BUILD)/ws_host_exp.o: uvhttp_amd/csrc/ws_host.c include/uvhttp_ws_amd.h
+	@mkdir -p $(BUILD)
+	$(CC) $(CFLAGS) $(EXP) -c -o $@ $<
 
 $(BUILD)/ws_host.o: uvhttp_amd/csrc/ws_host.c include/uvhttp_ws_amd.h
 	@mkdir -p $(BUILD)
@@ -45,7 +60,7 @@ $(LIB): $(BUILD)/ws_gpu.o $(BUILD)/tls_gpu.o $(BUILD)/ws_batcher.o $(BUILD)/ws_h
 	@mkdir -p $(dir $@)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
-$(TESTLIB): $(BUILD)/ws_gpu.o $(BUILD)/tls_gpu.o $(BUILD)/ws_batcher_testhooks.o $(BUILD)/ws_host.o \
+$(TESTLIB): $(BUILD)/ws_gpu_exp.o $(BUILD)/tls_gpu_exp.o $(BUILD)/ws_batcher_testhooks.o $(BUILD)/ws_host_exp.o \
             $(BUILD)/ws_batcher_group.o
 	@mkdir -p $(dir $@)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^

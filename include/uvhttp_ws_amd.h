@@ -366,9 +366,23 @@ typedef struct {
     uint64_t end_ns;    /* latest wave end */
 } uvhttp_ws_gpu_stamp_t;
 int uvhttp_ws_gpu_engine_set_stamps(uvhttp_ws_gpu_engine_t* eng, int enable);
-/* Waits for the device; *n_out = records written (at most cap). */
+/* Waits for the device; *n_out = records written (at most cap).  A pass launched as several
+ * dispatch pieces (over 2^24 workgroups, e.g. a C5 pass) reads as one record spanning all of
+ * them: begin = the first piece's start, end = the latest wave end of any piece. */
 int uvhttp_ws_gpu_engine_read_stamps(uvhttp_ws_gpu_engine_t* eng, uvhttp_ws_gpu_stamp_t* out,
                                      uint32_t cap, uint32_t* n_out);
+/* Host-only pieces of the stamp ring (no device needed; tests drive them):
+ * ring_words = the ring's size in 64-bit words; stamps_reduce = read_stamps's reduction of a
+ * ring copy (epoch = the engine's latest call, khz = wall-clock rate); stamp_simulate writes
+ * what one launch piece of `blocks` workgroups starting at pass index `base` stores, with the
+ * kernels' own slot mapping (workgroup i starts at t_begin + i (t_end - t_begin) / blocks and
+ * ends dur ticks later). */
+uint64_t uvhttp_ws_gpu_stamp_ring_words(void);
+int uvhttp_ws_gpu_stamps_reduce(const uint64_t* ring, uint32_t epoch, uint32_t khz,
+                                uvhttp_ws_gpu_stamp_t* out, uint32_t cap, uint32_t* n_out);
+int uvhttp_ws_gpu_stamp_simulate(uint64_t* ring, uint32_t epoch, uint32_t kind, uint64_t base,
+                                 uint32_t blocks, uint32_t waves, uint64_t t_begin, uint64_t t_end,
+                                 uint64_t dur);
 
 /* Streams and graphs.  An engine owns one workspace, so its calls must execute one after
  * another: when a call names a different stream than the previous call, the engine makes the
@@ -429,6 +443,13 @@ uint64_t uvhttp_ws_gen_frame_stride(uint64_t payload_len);
 int uvhttp_ws_gpu_gen_frames(uvhttp_ws_gpu_engine_t* eng, uint8_t* d_wire, uint32_t n_frames,
                              uint64_t payload_len, uint64_t seed, int opcode0, int fragmented,
                              int force_keys, void* stream);
+/* Frames [first, first + count) of that n_frames batch, written from d_wire on (the bench's
+ * ranks: rank r's shard is frames [first, ...) of the whole configuration, as
+ * oracle_gen_frames(first, count, n_frames) writes them). */
+int uvhttp_ws_gpu_gen_frames_range(uvhttp_ws_gpu_engine_t* eng, uint8_t* d_wire, uint32_t first,
+                                   uint32_t count, uint32_t n_frames, uint64_t payload_len,
+                                   uint64_t seed, int opcode0, int fragmented, int force_keys,
+                                   void* stream);
 
 /* ---- batched stateful stream decode (many connections per launch) --------------------- */
 /* One entry per connection: the bytes uvhttp_ws_process_data would hold after appending the

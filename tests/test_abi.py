@@ -70,3 +70,30 @@ def test_fault_injection_only_in_the_test_build():
     (libuvhttp_ws_amd_testhooks.so, -DUVWS_TEST_HOOKS); the product library has no such hook."""
     assert b"UVHTTP_WS_BATCHER_FAIL_EVERY" not in open(U.LIB_PATH, "rb").read()
     assert b"UVHTTP_WS_BATCHER_FAIL_EVERY" in open(U.TESTHOOKS_LIB_PATH, "rb").read()
+
+
+def test_product_library_reads_no_environment():
+    """the A/B switches — among them UVHTTP_WS_PLAN_TICKET=0 and
+    UVHTTP_WS_WALK_FUSE=1, whose workgroup orderings rely on in-order dispatch — are compiled
+    only into the experiment build (-DUVWS_EXPERIMENTS); the product library names none of them
+    and imports no getenv at all.  The Python mirror routes an engine created while a switch is
+    set to the experiment build."""
+    prod = open(U.LIB_PATH, "rb").read()
+    exp = open(U.TESTHOOKS_LIB_PATH, "rb").read()
+    for k in U.EXPERIMENT_KNOBS:
+        assert k.encode() not in prod, k
+    for k in ("UVHTTP_WS_PLAN_TICKET", "UVHTTP_WS_WALK_FUSE", "UVHTTP_WS_COMPACT", "UVHTTP_TLS_CRYPT_GRID"):
+        assert k.encode() in exp, k
+    import subprocess
+    syms = subprocess.run(["nm", "-D", "--undefined-only", U.LIB_PATH], capture_output=True,
+                          text=True).stdout
+    assert " getenv" not in syms and "secure_getenv" not in syms
+
+
+def test_knob_routes_to_experiment_build(monkeypatch):
+    monkeypatch.delenv("UVHTTP_WS_COMPACT", raising=False)
+    for k in U.EXPERIMENT_KNOBS:
+        monkeypatch.delenv(k, raising=False)
+    assert U.default_library() is U.lib()
+    monkeypatch.setenv("UVHTTP_WS_WALK", "lane")
+    assert U.default_library() is U.test_hooks_library()

@@ -333,3 +333,72 @@ def test_async_split_frames_stay_on_the_device(seed):
     for p in pairs:
         p.check(b, L)
     b.close()
+
+
+@pytest.mark.parametrize("between", ["submit", "forget_other", "alloc_other"])
+@pytest.mark.parametrize("device", DEVICES)
+def test_commit_refused_after_another_queueing_call(device, between):
+    """alloc_read(A), then another batcher call that queues (submit_read of B, a
+    forget, a second alloc_read), then commit_read(A) must be refused — B's bytes would
+    otherwise land in (device: share) the arena space A's socket read used — and both
+    connections' payloads arrive intact once A's bytes are submitted again."""
+    _need_device(device)
+    import uvhttp_amd as U
+    b = U.Batcher(device=device, min_device_bytes=0)
+    key = b"\x01\x02\x03\x04"
+    a = U.WsConnection(1, 16 << 20, 64 << 20, user_data=False)
+    bb = U.WsConnection(1, 16 << 20, 64 << 20, user_data=False)
+    other = U.WsConnection(1, 16 << 20, 64 << 20, user_data=False)
+    fa = _frame(2, 1, bytes(range(200)) * 3, key, True, 0)
+    fb = _frame(1, 1, b"B" * 333, key, True, 0)
+    assert b.submit(other, _frame(1, 1, b"o", key, True, 0)) == 0
+    rc, addr, n = b.alloc(a, len(fa))
+    assert rc == 0 and n >= len(fa)
+    C.memmove(addr, fa, len(fa))  # the socket read lands in the arena
+    if between == "submit":
+        assert b.submit(bb, fb) == 0
+    elif between == "forget_other":
+        b.forget(other)
+    else:
+        rc2, addr2, n2 = b.alloc(bb, len(fb))
+        assert rc2 == 0
+    assert b.commit(a, len(fa)) == -1  # UVHTTP_ERROR_INVALID_PARAM
+    assert b.submit(a, fa) == 0
+    if between != "submit":
+        assert b.submit(bb, fb) == 0
+    assert b.flush() == 0
+    got_a = [(t, p) for t, _, p in a.events if t == "message"]
+    got_b = [(t, p) for t, _, p in bb.events if t == "message"]
+    assert got_a == [("message", bytes(range(200)) * 3)]
+    assert got_b == [("message", b"B" * 333)]
+    b.close()
+    for c in (a, bb, other):
+        c.close()
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_alloc_read_hands_out_the_room_left(device):
+    """with some room left in the accumulating queue, alloc_read hands out that room
+    (shorter than libuv's 64 KiB suggestion) instead of handing the queue over and waiting; a
+    bogus suggestion is bounded on the direct path (no exception through the C ABI)"""
+    _need_device(device)
+    import uvhttp_amd as U
+    b = U.Batcher(device=device, min_device_bytes=0, max_bytes=48 * 1024)
+    key = b"\x01\x02\x03\x04"
+    c1 = U.WsConnection(1, 16 << 20, 64 << 20, user_data=False)
+    assert b.submit(c1, _frame(2, 1, b"x" * 30000, key, True, 0)) == 0
+    flushes = b.stats()["flushes"]
+    rc, addr, n = b.alloc(c1, 65536)
+    assert rc == 0 and 0 < n < 65536
+    assert b.stats()["flushes"] == flushes  # no hand-over for a read that still has room
+    assert b.commit(c1, 0) == 0
+    # a huge suggestion on a queue with no room: the direct buffer stays bounded
+    big = U.WsConnection(1, 16 << 20, 64 << 20, user_data=False)
+    rc, addr, n = b.alloc(big, 1 << 62)
+    assert rc == 0 and n <= 48 * 1024
+    assert b.commit(big, 0) == 0
+    assert b.flush() == 0
+    assert [(t, p) for t, _, p in c1.events if t == "message"] == [("message", b"x" * 30000)]
+    b.close()
+    c1.close()
+    big.close()

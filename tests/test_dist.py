@@ -132,3 +132,31 @@ def test_bench_torchrun_form_single_process():
     out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
     assert out["n_gpus"] == 1 and out["scaling"] == "weak"
     assert out["config"]["workload"].startswith("C3")
+
+
+def test_rank_shards_are_global_c5_frames():
+    """bench.py's rank r decodes frames [lo, ..) of THE C5 batch: its
+    generator arguments name global frame indices, so rank 1 of 2 holds frame 4 194 304 of the
+    8 388 608-frame batch, byte for byte the oracle's; c2-c4 ranks hold the config's batch."""
+    import sys
+    import numpy as np
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, repo)
+    import bench
+    import _oracle
+    n_c5, plen = bench.CONFIGS["c5"][0], bench.CONFIGS["c5"][1]
+    first, count, total = bench.gen_plan("c5", 1, 2)
+    assert (first, count, total) == (n_c5 // 2, 1048576, n_c5)
+    got, stride = _oracle.gen_frames(count, plen, bench.SEED, first=first, count=2, total=total)
+    exp, _ = _oracle.gen_frames(n_c5, plen, bench.SEED, first=n_c5 // 2, count=2, total=n_c5)
+    assert np.array_equal(got, exp)
+    # and it is not rank 0's frame (the shards hold different frames)
+    r0, _ = _oracle.gen_frames(count, plen, bench.SEED, first=0, count=1, total=total)
+    assert not np.array_equal(got[:stride], r0)
+    for w in (2, 4, 8):
+        for r in range(w):
+            f, c, t = bench.gen_plan("c5", r, w)
+            assert f == r * n_c5 // w and c == min(1048576, n_c5 // w) and t == n_c5
+    for cfg in ("c2", "c3", "c4"):
+        n = bench.CONFIGS[cfg][0]
+        assert bench.gen_plan(cfg, 1, 2) == (0, n, n)

@@ -314,6 +314,27 @@ def test_generator_matches_oracle(torch, eng, plen):
     assert np.array_equal(d[: stride * n].cpu().numpy(), wire)
 
 
+@pytest.mark.parametrize("plen", [0, 125, 256, 4096, 70000])
+def test_generator_range_matches_oracle(torch, eng, plen):
+    """frames [first, first + count) of a larger batch (bench.py's rank shards: rank r decodes
+    frames lo.. of the whole C5 batch, bench.gen_plan) equal the oracle's same range — and
+    the same frames of the whole batch generated at once"""
+    import uvhttp_amd as U
+    total, first, count = 101, 57, 44
+    frag = plen == 256
+    exp, stride = _oracle.gen_frames(total, plen, SEED, fragmented=frag, force_keys=True,
+                                     first=first, count=count, total=total)
+    whole, _ = _oracle.gen_frames(total, plen, SEED, fragmented=frag, force_keys=True)
+    assert np.array_equal(exp, whole[first * stride:(first + count) * stride])
+    d = torch.zeros(stride * count + 16, dtype=torch.uint8, device="cuda")
+    eng.gen_frames(d, count, plen, SEED, fragmented=frag, force_keys=True, first=first,
+                   count=count, total=total)
+    torch.cuda.synchronize()
+    assert np.array_equal(d[: stride * count].cpu().numpy(), exp)
+    with pytest.raises(U.GpuError):
+        eng.gen_frames(d, count, plen, SEED, first=first, count=count, total=first + count - 1)
+
+
 @pytest.mark.parametrize("off", [0, 1, 3, 15])
 def test_device_apply_mask(torch, eng, off):
     rng = np.random.default_rng(off)

@@ -267,11 +267,14 @@ def _layout(U, cases, rng, gaps=(0, 16, 48)):
     return wire, b"".join(bytes(s) for s in streams), len(streams), pos
 
 
-def test_streams_back_to_back_growth(torch, hooks):
+@pytest.mark.parametrize("side", [False, True], ids=["default_stream", "nonblocking_stream"])
+def test_streams_back_to_back_growth(torch, hooks, side):
     """A call issued while the previous one still runs, with more connections and a longer wire
     (the engine's stream scratch, slices and frame records grow under it — round 5's closing
     run crashed on this in the batcher): both decode exactly as each does alone on a fresh
-    engine (wire, descriptors, results)."""
+    engine (wire, descriptors, results).  nonblocking_stream: the crash's own conditions — the
+    calls on a torch side stream (non-blocking: the legacy null stream does not order it), issued
+    back to back with no host sync, the scratch grown on that stream (ws_gpu.hip scratch_grow)."""
     import uvhttp_amd as U
     rng = random.Random(4242)
     calls = []
@@ -279,20 +282,29 @@ def test_streams_back_to_back_growth(torch, hooks):
         cases = [c for c in (_conn_case(rng, U, False) for _ in range(nconn)) if c]
         calls.append(_layout(U, cases, rng))
 
-    def run(eng, k):
+    def inputs(k):
         wire, sb, n, wl = calls[k]
         dw = torch.from_numpy(wire.copy()).to("cuda")
         ds = torch.from_numpy(np.frombuffer(sb, np.uint8).copy()).to("cuda")
-        desc, res = eng.decode_streams(dw, ds, n, 16384, wire_len=wl)
+        return dw, ds
+
+    def run(eng, k, dw, ds, stream=None):
+        _, _, n, wl = calls[k]
+        desc, res = eng.decode_streams(dw, ds, n, 16384, wire_len=wl, stream=stream)
         return dw, desc, res, ds
 
     eng = U.GpuEngine(0)
-    outs = [run(eng, k) for k in range(len(calls))]  # no sync between the calls
+    ins = [inputs(k) for k in range(len(calls))]
     torch.cuda.synchronize()
-    eng.sync()
+    st = torch.cuda.Stream() if side else torch.cuda.current_stream()
+    with torch.cuda.stream(st):
+        outs = [run(eng, k, *ins[k], stream=st) for k in range(len(calls))]  # no sync between
+    st.synchronize()
+    torch.cuda.synchronize()
+    eng.sync(st)
     for k, (dw, desc, res, _ds) in enumerate(outs):
         alone = U.GpuEngine(0)
-        aw, adesc, ares, _ = run(alone, k)
+        aw, adesc, ares, _ = run(alone, k, *inputs(k))
         torch.cuda.synchronize()
         alone.sync()
         n = calls[k][2]

@@ -227,6 +227,32 @@ def test_hooks_library() -> C.CDLL:
     return _TESTHOOKS
 
 
+# Environment switches only the experiment build (libuvhttp_ws_amd_testhooks.so, -DUVWS_EXPERIMENTS)
+# reads; the product library reads no environment (ws_gpu.hip experiment_knobs).  Engines,
+# batchers and pipelines created while one of these is set load the experiment build, so A/B
+# tools and variant tests get the variant they name rather than a silently ignored switch.
+EXPERIMENT_KNOBS = (
+    "UVHTTP_WS_MAX_POLLS", "UVHTTP_WS_SCRATCH_POOL", "UVHTTP_WS_STORE_POLICY", "UVHTTP_WS_PLAN_FPT",
+    "UVHTTP_WS_PLAN_TICKET", "UVHTTP_WS_EPOCH_START", "UVHTTP_WS_BUILD_SMALL", "UVHTTP_WS_FUSED",
+    "UVHTTP_WS_FUSED_MAX", "UVHTTP_WS_PLAN_WIDE", "UVHTTP_WS_REC_SCAN", "UVHTTP_WS_BUILD_FRAMES",
+    "UVHTTP_WS_COMPACT", "UVHTTP_WS_WALK_SINGLE", "UVHTTP_WS_WALK_FUSE", "UVHTTP_WS_STREAM_NT",
+    "UVHTTP_WS_DESC_SCAN", "UVHTTP_WS_WALK_NT_LOAD", "UVHTTP_WS_WALK_REC", "UVHTTP_WS_WALK",
+    "UVHTTP_WS_TIME_CHAIN", "UVHTTP_WS_COMPACT_RECS", "UVHTTP_WS_SPEC", "UVHTTP_WS_SPEC_MAX",
+    "UVHTTP_WS_FUSED_AUX", "UVHTTP_WS_SUMMARY_FAST", "UVHTTP_WS_TILE", "UVHTTP_WS_FIXUP_BLOCKS",
+    "UVHTTP_WS_FUSED_TILE", "UVHTTP_WS_TIMING_FENCE", "UVHTTP_WS_PIPE_IN_FLIGHT",
+    "UVHTTP_TLS_CRYPT_GRID", "UVHTTP_WS_BATCHER_TRACE", "UVHTTP_WS_BATCHER_FAIL_EVERY",
+    "UVHTTP_WS_COPY_SSE2")
+
+
+def experiment_knobs_set():
+    return [k for k in EXPERIMENT_KNOBS if k in os.environ]
+
+
+def default_library() -> C.CDLL:
+    """the product library, or the experiment build while an experiment switch is set"""
+    return test_hooks_library() if experiment_knobs_set() else lib()
+
+
 def load_library(path: str) -> C.CDLL:
     """Load a build of libuvhttp_ws_amd.so from `path` and declare its entry points (lib()
     uses the in-tree build; tools/ab_lib.py loads a second build beside it for A/B runs)."""
@@ -261,6 +287,9 @@ def load_library(path: str) -> C.CDLL:
         "uvhttp_ws_gpu_engine_sync": (C.c_int, [vp, vp]),
         "uvhttp_ws_gpu_engine_set_stamps": (C.c_int, [vp, C.c_int]),
         "uvhttp_ws_gpu_engine_read_stamps": (C.c_int, [vp, vp, u32, C.POINTER(u32)]),
+        "uvhttp_ws_gpu_stamp_ring_words": (u64, []),
+        "uvhttp_ws_gpu_stamps_reduce": (C.c_int, [vp, u32, u32, vp, u32, C.POINTER(u32)]),
+        "uvhttp_ws_gpu_stamp_simulate": (C.c_int, [vp, u32, u32, u64, u32, u32, u64, u64, u64]),
         "uvhttp_ws_gpu_decode_inplace": (C.c_int, [vp, C.POINTER(Batch), vp, vp, vp]),
         "uvhttp_ws_gpu_decode_compact": (C.c_int, [vp, C.POINTER(Batch), vp, u64, vp, vp, vp,
                                                    vp]),
@@ -283,6 +312,8 @@ def load_library(path: str) -> C.CDLL:
                                                C.POINTER(Stream), C.POINTER(StreamResult)]),
         "uvhttp_ws_gpu_gen_frames": (C.c_int, [vp, vp, u32, u64, u64, C.c_int, C.c_int, C.c_int,
                                                vp]),
+        "uvhttp_ws_gpu_gen_frames_range": (C.c_int, [vp, vp, u32, u32, u32, u64, u64, C.c_int,
+                                                     C.c_int, C.c_int, vp]),
         # batcher (include/uvhttp_ws_amd.h)
         "uvhttp_ws_amd_batcher_config_init": (None, [C.POINTER(BatcherConfig)]),
         "uvhttp_ws_amd_batcher_create": (C.c_int, [C.POINTER(BatcherConfig), C.POINTER(vp)]),
@@ -453,7 +484,7 @@ class GpuEngine:
     def __init__(self, device: int = 0, library: C.CDLL = None):
         import torch
         self.torch = torch
-        L = library or lib()
+        L = library or default_library()
         self._L = L
         self.device = device
         h = C.c_void_p()
@@ -635,9 +666,18 @@ class GpuEngine:
             "apply_mask")
 
     def gen_frames(self, wire, n_frames, payload_len, seed, opcode0=2, fragmented=False,
-                   force_keys=False, stream=None):
-        self._check(self._L.uvhttp_ws_gpu_gen_frames(
-            self.h, C.c_void_p(wire.data_ptr()), n_frames, payload_len, seed, opcode0,
+                   force_keys=False, stream=None, first=0, count=None, total=None):
+        """frames [first, first + count) of a total-frame batch (default: all n_frames), as
+        _oracle.gen_frames(..., first=, count=, total=) writes them"""
+        if count is None and total is None and first == 0:
+            self._check(self._L.uvhttp_ws_gpu_gen_frames(
+                self.h, C.c_void_p(wire.data_ptr()), n_frames, payload_len, seed, opcode0,
+                1 if fragmented else 0, 1 if force_keys else 0, self._stream(stream)), "gen_frames")
+            return
+        count = n_frames if count is None else count
+        total = n_frames if total is None else total
+        self._check(self._L.uvhttp_ws_gpu_gen_frames_range(
+            self.h, C.c_void_p(wire.data_ptr()), first, count, total, payload_len, seed, opcode0,
             1 if fragmented else 0, 1 if force_keys else 0, self._stream(stream)), "gen_frames")
 
     # -- read-back helpers (host copies of device outputs) --
@@ -670,7 +710,7 @@ class GpuPipeline:
     def __init__(self, device=0, depth=3, slot_bytes=1 << 26, slot_frames=1 << 16):
         import numpy as np
         self.np = np
-        L = lib()
+        L = default_library()
         self._L = L
         h = C.c_void_p()
         rc = L.uvhttp_ws_gpu_pipeline_create(device, depth, slot_bytes, slot_frames, C.byref(h))
@@ -741,7 +781,7 @@ class TlsEngine:
     def __init__(self, device: int = 0, library: C.CDLL = None):
         import torch
         self.torch = torch
-        L = library or lib()
+        L = library or default_library()
         self._L = L
         self.device = device
         h = C.c_void_p()
@@ -820,7 +860,7 @@ class Batcher:
 
     def __init__(self, device=-1, min_device_bytes=0, max_bytes=32 << 20,
                  max_connections=16384, max_reads=1 << 18, library: C.CDLL = None):
-        L = library or lib()
+        L = library or default_library()
         self._L = L
         cfg = BatcherConfig()
         L.uvhttp_ws_amd_batcher_config_init(C.byref(cfg))
@@ -934,7 +974,7 @@ class BatcherGroup(Batcher):
 
     def __init__(self, devices, min_device_bytes=0, max_bytes=32 << 20, max_connections=16384,
                  max_reads=1 << 18):
-        L = lib()
+        L = default_library()
         self._L = L
         cfg = BatcherConfig()
         L.uvhttp_ws_amd_batcher_config_init(C.byref(cfg))

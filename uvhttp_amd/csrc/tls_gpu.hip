@@ -2324,8 +2324,12 @@ static int tls_timing_begin(uvhttp_tls_gpu_engine_t* e, hipStream_t s) {
         // timing-only events: no system-scope fence (a fenced marker between two kernels
         // idled the device ~5.8 us per event, profiles/r03p1 kernel trace); the caller's own
         // synchronisation still orders the results.  UVHTTP_WS_TIMING_FENCE=1: fenced (A/B)
+#ifdef UVWS_EXPERIMENTS
         static const unsigned flags = getenv("UVHTTP_WS_TIMING_FENCE") && atoi(getenv("UVHTTP_WS_TIMING_FENCE"))
                                           ? hipEventDefault : hipEventDisableSystemFence;
+#else
+        const unsigned flags = hipEventDisableSystemFence;
+#endif
         if (hipEventCreateWithFlags(&e->ev[e->ev_created], flags) != hipSuccess) return -1;
         e->ev_created++;
     }
@@ -2363,7 +2367,9 @@ int uvhttp_tls_gpu_engine_create(int device, uvhttp_tls_gpu_engine_t** out) {
     }
     // crypto grid: enough 4-wave workgroups for every CU several times over
     e->crypt_grid = prop.multiProcessorCount * 8;
+#ifdef UVWS_EXPERIMENTS  // (A/B builds only: the product library reads no environment)
     if (const char* g = getenv("UVHTTP_TLS_CRYPT_GRID")) e->crypt_grid = atoi(g) > 0 ? atoi(g) : e->crypt_grid;
+#endif
     (void)hipSetDevice(prev);
     if (h != hipSuccess) {
         if (e->te0) (void)hipFree(e->te0);

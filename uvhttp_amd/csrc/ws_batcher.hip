@@ -559,8 +559,12 @@ int launch_device(uvhttp_ws_amd_batcher_t* b, BatchQueue& q) {
     if (b->fail_every && ++b->launches % b->fail_every == 0) return UVHTTP_WS_GPU_ELAUNCH;
 #endif
     hipStream_t s = b->cs;
-    // UVHTTP_WS_BATCHER_TRACE=1: host time of each enqueue step on stderr (diagnostics)
+    // UVHTTP_WS_BATCHER_TRACE=1 (experiment builds): host time of each enqueue step on stderr
+#ifdef UVWS_EXPERIMENTS
     static const bool trace = getenv("UVHTTP_WS_BATCHER_TRACE") != nullptr;
+#else
+    constexpr bool trace = false;
+#endif
     auto tp = std::chrono::steady_clock::now();
     auto mark = [&](const char* what) {
         if (!trace) return;
@@ -1186,6 +1190,9 @@ void record_read(uvhttp_ws_amd_batcher_t* b, uvhttp_ws_connection_t* conn, uint6
 // queue one read (plain bytes, or a TLS connection's ciphertext)
 uvhttp_error_t queue_read(uvhttp_ws_amd_batcher_t* b, uvhttp_ws_connection_t* conn,
                           const uint8_t* data, size_t len, bool tls) {
+    // any other queueing call between alloc_read and commit_read voids the allocation: this read
+    // would take the arena bytes the socket read is landing in
+    b->pend.conn = nullptr;
     if (b->failed.count(conn)) return UVHTTP_ERROR_INVALID_PARAM;
     {
         const BatchQueue& q = b->q[b->cur];
@@ -1260,17 +1267,27 @@ uvhttp_error_t uvhttp_ws_amd_batcher_alloc_read(uvhttp_ws_amd_batcher_t* b,
         if (it != q.slot_of.end() && q.slots[it->second].tls != tls) return UVHTTP_ERROR_INVALID_PARAM;
     }
     uint64_t want = suggested ? suggested : 65536;
-    if (read_room(b, conn, tls) < want) {
-        // a full queue is handed over first; a read larger than a whole flush gets what one
-        // flush holds (the socket delivers the rest to the next read)
+    uint64_t room = read_room(b, conn, tls);
+    if (room == 0) {
+        // only a queue with no room left is handed over (libuv always suggests 64 KiB: a
+        // queue with some room hands out that room instead of waiting for the queue in flight,
+        // and the socket delivers the rest to the next read)
         if (make_room(b, conn, want, tls) < 0) return UVHTTP_ERROR_INVALID_PARAM;
-        const uint64_t room = read_room(b, conn, tls);
+        room = read_room(b, conn, tls);
         if (room == 0) {
             // not even one byte fits a flush beside the connection's recv-buffer prefix: the
             // read is decoded at commit, after the connection's earlier reads (submit_read's
-            // direct path; make_room delivered them if they were in flight)
+            // direct path; make_room delivered them if they were in flight).  The buffer is
+            // bounded whatever the caller suggests, and an allocation failure is an error code,
+            // not an exception through the C ABI.
             if (tls) return UVHTTP_ERROR_INVALID_PARAM;
-            b->direct.resize(want);
+            const uint64_t bound = b->cfg.max_bytes > 65536 ? b->cfg.max_bytes : 65536;
+            if (want > bound) want = bound;
+            try {
+                b->direct.resize(want);
+            } catch (...) {
+                return UVHTTP_ERROR_INVALID_PARAM;
+            }
             b->pend.conn = conn;
             b->pend.cap = want;
             b->pend.tls = false;
@@ -1279,8 +1296,8 @@ uvhttp_error_t uvhttp_ws_amd_batcher_alloc_read(uvhttp_ws_amd_batcher_t* b,
             *len = (size_t)want;
             return UVHTTP_OK;
         }
-        if (room < want) want = room;
     }
+    if (room < want) want = room;
     BatchQueue& q = b->q[b->cur];
     uint64_t off;
     uint8_t* base;
@@ -1337,6 +1354,7 @@ uvhttp_error_t uvhttp_ws_amd_batcher_commit_read(uvhttp_ws_amd_batcher_t* b,
 int uvhttp_ws_amd_batcher_set_tls(uvhttp_ws_amd_batcher_t* b, struct uvhttp_ws_connection* conn,
                                   const void* tls_key, uint64_t read_seq) {
     if (!b || !conn || !tls_key) return UVHTTP_WS_GPU_EINVAL;
+    b->pend.conn = nullptr;  // (an outstanding alloc_read is void: commit_read refuses it)
     if (!b->eng) return UVHTTP_WS_GPU_ENODEV;  // no host AEAD: TLS needs the device
     // plain reads of this connection still queued would be decoded after ciphertext that
     // follows them: flush them first
@@ -1377,7 +1395,7 @@ uvhttp_error_t uvhttp_ws_amd_batcher_submit_tls_read(uvhttp_ws_amd_batcher_t* b,
 
 void uvhttp_ws_amd_batcher_forget(uvhttp_ws_amd_batcher_t* b, struct uvhttp_ws_connection* conn) {
     if (!b || !conn) return;
-    if (b->pend.conn == conn) b->pend.conn = nullptr;  // its uncommitted allocation too
+    b->pend.conn = nullptr;  // an uncommitted allocation (of any connection) is void
     b->failed.erase(conn);
     b->tls.erase(conn);
     for (int i = 0; i < 2; ++i) {

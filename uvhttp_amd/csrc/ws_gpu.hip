@@ -432,6 +432,15 @@ __host__ __device__ inline uint32_t stamp_tag(uint32_t epoch) { return epoch % k
 __device__ inline uint64_t* stamp_slot(uint64_t* st, uint32_t epoch, uint32_t kind) {
     return st + ((uint64_t)(epoch % kStampRing) * kStampKinds + kind) * kStampPer;
 }
+// which workgroups (by index g in the whole pass) store an end word, and which end word wave w
+// of workgroup g stores (shared with the host-side simulation the stamp tests drive)
+__host__ __device__ inline bool stamp_sampled(uint64_t g) {
+    return g < 1024 || (g < 65536 ? (g & 63) == 63 : (g & 1023) == 1023);
+}
+__host__ __device__ inline uint32_t stamp_end_word(uint64_t g, uint32_t wave) {
+    const uint64_t blk = g < 1024 ? g : g < 65536 ? 1024 + (g >> 6) : 2048 + (g >> 10);
+    return (uint32_t)((blk * 4 + (wave & 3)) % kStampEnd);
+}
 // the constant-rate wall clock (100 MHz).  Inline asm without a memory clobber: the builtin
 // counts as a memory access, so a clock read at a kernel's start turned every later uniform
 // workspace load into a vector load (the compiler could no longer prove them unclobbered)
@@ -450,12 +459,21 @@ __device__ inline uint64_t stamp_clock() {
 // "begin" is the earliest END among their first 256 workgroups — late by one workgroup's
 // duration — unless the kernel reads it through anchor_s / anchor_v (the payload kernels, the
 // walks and k_stream_desc do).  The others (k_plan, scans, fix-ups) read the clock when they start.
+//
+// A pass too large for one dispatch packet is launched as pieces of <= 2^24 workgroups
+// (run_decode, build_frames); each piece passes its first workgroup's index in the whole pass
+// (`base`, the tile_base argument), and the words are placed by that global index, so only
+// the first piece stores begins and every piece's ends land in the same slot: the reader's
+// earliest begin / latest end then span the whole pass (blockIdx.x alone restarted in every
+// piece, and the slot kept the last piece: a C5 pass read as 6.7 us).
 struct StampScope {
     uint64_t* st;
     uint32_t epoch, kind;
     uint64_t t0;
-    __device__ StampScope(uint64_t* st_, uint32_t epoch_, uint32_t kind_, bool at_start = true)
-        : st(st_), epoch(epoch_), kind(kind_), t0(at_start && st_ ? stamp_clock() : 0) {}
+    uint64_t base;
+    __device__ StampScope(uint64_t* st_, uint32_t epoch_, uint32_t kind_, bool at_start = true,
+                          uint64_t base_ = 0)
+        : st(st_), epoch(epoch_), kind(kind_), t0(at_start && st_ ? stamp_clock() : 0), base(base_) {}
     // The start clock of a kernel whose uniform loads must stay scalar: read by an asm that is
     // not a memory access (so it clobbers nothing) and is pinned before the kernel's first
     // loads by passing the index they are computed from through it (v is returned unchanged).
@@ -481,19 +499,18 @@ struct StampScope {
         // Each end store costs: one in 64 of a C3 payload kernel's 4.2 M workgroups slowed it
         // by 6 %, one in 1024 by 0.2 % (profiles/r04_stamps_runtime_ab.txt).  Nothing from the
         // dispatch packet (grid or block size): a load of it in each wave cost as much.
-        const bool first = threadIdx.x == 0 && blockIdx.x < kStampBegin;
-        const uint32_t b = blockIdx.x;
-        const bool sample = b < 1024 || (b < 65536 ? (b & 63) == 63 : (b & 1023) == 1023);
+        const uint64_t g = base + blockIdx.x;  // the workgroup's index in the whole pass
+        const bool first = threadIdx.x == 0 && g < kStampBegin;
+        const bool sample = stamp_sampled(g);
         if (!first && !sample) return;
         uint64_t* sl = stamp_slot(st, epoch, kind);
         const uint64_t tag = (uint64_t)stamp_tag(epoch) << 40;
         const uint64_t now = stamp_clock();
-        if (first) sl[blockIdx.x] = tag | ((t0 ? t0 : now) & kStampLow);
+        if (first) sl[g] = tag | ((t0 ? t0 : now) & kStampLow);
         if (!sample) return;
         const uint64_t act = __ballot(1);
         if ((threadIdx.x & 63) != (uint32_t)__builtin_ctzll(act)) return;
-        const uint32_t blk = b < 1024 ? b : b < 65536 ? 1024 + (b >> 6) : 2048 + (b >> 10);
-        sl[kStampBegin + (blk * 4 + ((threadIdx.x >> 6) & 3)) % kStampEnd] = tag | (now & kStampLow);
+        sl[kStampBegin + stamp_end_word(g, threadIdx.x >> 6)] = tag | (now & kStampLow);
     }
 };
 
@@ -1612,7 +1629,7 @@ template <int BLOCK, int VPT, int STORE_AUX = 0>
 __global__ __launch_bounds__(BLOCK) void k_unmask_inplace(
     BatchArgs a, const uvhttp_ws_frame_desc_t* __restrict__ desc, Workspace ws,
     uint64_t tile_base) {
-    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_PAYLOAD, false);
+    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_PAYLOAD, false, tile_base);
     uint32_t n, nb;
     unmask_tile<BLOCK, VPT, STORE_AUX>(a, desc, ws, tile_base, n, nb, stamp_);  // resolves the epoch
     // batch in-place decode: the first ceil(n / BLOCK) workgroups then do k_finalize's work
@@ -1748,7 +1765,7 @@ __device__ inline void add_mask_rel(u32x4& m, int32_t r, int32_t ps, int32_t pe,
 
 template <int BLOCK, int VPT, int AUX = 18, bool SUM = false>
 __global__ __launch_bounds__(BLOCK) void k_unmask_stride(BatchArgs a, Workspace ws, uint64_t tile_base) {
-    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_PAYLOAD, false);
+    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_PAYLOAD, false, tile_base);
     constexpr uint64_t kT = (uint64_t)BLOCK * VPT * 16;
     constexpr int kMaxF = (int)(kT / kFusedMinStride) + 2;  // frames touching one tile
     __shared__ u32x4 s_tile[BLOCK * VPT + 1];               // the tile + the 16 bytes after
@@ -2815,7 +2832,7 @@ template <int BLOCK, int VPT>
 __global__ __launch_bounds__(BLOCK) void k_scatter_compact(
     BatchArgs a, const uvhttp_ws_frame_desc_t* __restrict__ desc, Workspace ws,
     uint64_t arena_bytes_cap, uint64_t tile_base) {
-    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_PAYLOAD, false);
+    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_PAYLOAD, false, tile_base);
     scatter_tile<BLOCK, VPT>(a, desc, ws, arena_bytes_cap, tile_base + stamp_.anchor_s(blockIdx.x));
     // k_finalize's work at the end of the first ceil(n / BLOCK) workgroups, as the in-place
     // kernel does (statuses after the first failure, control payloads unmasked in the wire —
@@ -4210,7 +4227,7 @@ __device__ inline void build_vector(const BuildArgs& b, uint64_t oa, uint64_t fs
 template <int BLOCK, int VPT>
 __global__ __launch_bounds__(BLOCK) void kb_emit(BuildArgs b, uint64_t tile_base) {
     resolve_epoch(b);
-    StampScope stamp_(b.stamp, b.epoch, UVHTTP_WS_STAMP_PAYLOAD, false);
+    StampScope stamp_(b.stamp, b.epoch, UVHTTP_WS_STAMP_PAYLOAD, false, tile_base);
     constexpr uint64_t kT = (uint64_t)BLOCK * VPT * 16;
     __shared__ uint64_t s_start[BLOCK];  // frame start in out
     __shared__ uint64_t s_pstart[BLOCK]; // payload start in out
@@ -4572,7 +4589,8 @@ __device__ __host__ inline uint64_t gen_header_size(uint64_t p) {
     return p < 126 ? 2 : p < 65536 ? 4 : 10;
 }
 
-__global__ __launch_bounds__(kBlock) void k_gen_frames(uint8_t* wire, uint32_t n, uint64_t plen,
+__global__ __launch_bounds__(kBlock) void k_gen_frames(uint8_t* wire, uint32_t first, uint32_t n,
+                                                       uint32_t n_total, uint64_t plen,
                                                        uint64_t seed, int opcode0, int fragmented,
                                                        int force_keys, uint64_t words_per_frame) {
     const uint64_t gid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -4580,14 +4598,15 @@ __global__ __launch_bounds__(kBlock) void k_gen_frames(uint8_t* wire, uint32_t n
     const uint64_t hs = gen_header_size(plen);
     const uint64_t stride = hs + 4 + plen;
     for (uint64_t g = gid; g < total; g += (uint64_t)gridDim.x * kBlock) {
-        const uint32_t i = (uint32_t)(g / words_per_frame);
-        const uint64_t wi = g - (uint64_t)i * words_per_frame;
-        uint8_t* w = wire + (uint64_t)i * stride;
+        const uint32_t li = (uint32_t)(g / words_per_frame);  // frame in this range
+        const uint32_t i = first + li;                        // frame in the whole batch
+        const uint64_t wi = g - (uint64_t)li * words_per_frame;
+        uint8_t* w = wire + (uint64_t)li * stride;
         uint32_t key = (uint32_t)splitmix64(seed ^ (uint64_t)i);
         if (force_keys && i == 0) key = 0u;
         if (force_keys && i == 1) key = 0xFFFFFFFFu;
         if (wi == 0) {
-            const int fin = !fragmented || i + 1 == n;
+            const int fin = !fragmented || i + 1 == n_total;
             const int op = (i == 0 || !fragmented) ? opcode0 : 0;
             w[0] = (uint8_t)((fin ? 0x80 : 0) | (op & 0x0F));
             if (hs == 2) {
@@ -4704,6 +4723,7 @@ struct uvhttp_ws_gpu_engine {
     int captured_ever;         // a call of this engine was captured (its replays leave later epochs)
     hipStream_t last_stream;   // stream of the previous call (calls are serialised on it)
     int have_last;
+    int pool_ok;               // the device has the stream-ordered allocator (scratch_grow)
     hipEvent_t order_ev;       // orders a call on a new stream after the previous stream's work
     hipEvent_t ev[2 * 1024];
     int ev_created;
@@ -4713,6 +4733,7 @@ struct uvhttp_ws_gpu_engine {
     char err[256];
 };
 
+static void scratch_free(uvhttp_ws_gpu_engine_t* e, void* p);
 static int set_err(uvhttp_ws_gpu_engine_t* e, int code, const char* what, hipError_t h) {
     if (e) snprintf(e->err, sizeof(e->err), "%s: %s", what, h == hipSuccess ? "" : hipGetErrorString(h));
     return code;
@@ -4737,6 +4758,62 @@ uint64_t uvhttp_ws_gen_frame_stride(uint64_t payload_len) {
     return gen_header_size(payload_len) + 4 + payload_len;
 }
 
+#ifdef UVWS_EXPERIMENTS
+// Experiment / test builds only (libuvhttp_ws_amd_testhooks.so, -DUVWS_EXPERIMENTS): the A/B
+// switches the measurements in DESIGN.md and profiles/ were taken with, and the test hooks
+// (look-back give-up, epoch wrap).  The product library reads no environment: two of these
+// (UVHTTP_WS_PLAN_TICKET=0, UVHTTP_WS_WALK_FUSE=1) order workgroups by blockIdx and rely on
+// in-order dispatch, which the product must not.  Every
+// variant reachable here gives the product's results (tests/ run them against the oracle).
+static void experiment_knobs(uvhttp_ws_gpu_engine_t* e) {
+    if (const char* mp = getenv("UVHTTP_WS_MAX_POLLS")) e->max_polls = (uint32_t)strtoul(mp, nullptr, 0);
+    if (const char* po = getenv("UVHTTP_WS_SCRATCH_POOL")) e->pool_ok &= atoi(po) != 0;
+    if (const char* sp = getenv("UVHTTP_WS_STORE_POLICY")) e->store_aux = atoi(sp) == 18 ? 18 : 0;
+    if (const char* fp = getenv("UVHTTP_WS_PLAN_FPT")) e->plan_fpt = atoi(fp);
+    if (const char* pt = getenv("UVHTTP_WS_PLAN_TICKET")) e->plan_no_ticket = atoi(pt) == 0;
+    // start near the end of the epoch space to exercise the wrap-around clear
+    if (const char* ep = getenv("UVHTTP_WS_EPOCH_START")) {
+        const unsigned long v = strtoul(ep, nullptr, 0);
+        e->epoch = v < kMaxHostEpoch ? (uint32_t)v : 0;
+    }
+    if (const char* bs = getenv("UVHTTP_WS_BUILD_SMALL")) e->build_small = atoi(bs);
+    if (const char* fu = getenv("UVHTTP_WS_FUSED")) e->fused_off = atoi(fu) == 0;
+    if (const char* fm = getenv("UVHTTP_WS_FUSED_MAX")) e->fused_max_avg = strtoull(fm, nullptr, 10);
+    if (const char* pw = getenv("UVHTTP_WS_PLAN_WIDE")) e->plan_wide = atoi(pw);
+    if (const char* rs = getenv("UVHTTP_WS_REC_SCAN")) e->rec_lookback = strcmp(rs, "3pass") != 0;
+    if (const char* bf = getenv("UVHTTP_WS_BUILD_FRAMES")) e->build_frames_max = strtoull(bf, nullptr, 10);
+    if (const char* cm = getenv("UVHTTP_WS_COMPACT"))
+        e->compact_mode = strcmp(cm, "gather") == 0 ? 1 : strcmp(cm, "scatter") == 0 ? 2 : 0;
+    if (const char* ws = getenv("UVHTTP_WS_WALK_SINGLE")) e->walk_single_off = atoi(ws) == 0;
+    if (const char* wf = getenv("UVHTTP_WS_WALK_FUSE")) e->walk_fuse = atoi(wf) != 0;
+    if (const char* sn = getenv("UVHTTP_WS_STREAM_NT")) e->stream_nt = atoi(sn) != 0;
+    if (const char* ds = getenv("UVHTTP_WS_DESC_SCAN")) e->desc_scan_off = atoi(ds) == 0;
+    if (const char* wn = getenv("UVHTTP_WS_WALK_NT_LOAD")) e->walk_nt_load = atoi(wn) != 0;
+    if (const char* wr = getenv("UVHTTP_WS_WALK_REC")) e->wr_rec_on = atoi(wr) != 0;
+    if (const char* wm = getenv("UVHTTP_WS_WALK"))
+        e->walk_mode = strcmp(wm, "lane") == 0 ? 1 : strcmp(wm, "wave") == 0 ? 2 : 0;
+    if (const char* tc = getenv("UVHTTP_WS_TIME_CHAIN")) e->time_chain = atoi(tc) != 0;
+    if (const char* cr = getenv("UVHTTP_WS_COMPACT_RECS")) e->compact_recs = atoi(cr) != 0;
+    if (const char* sp2 = getenv("UVHTTP_WS_SPEC")) e->spec_on = atoi(sp2) != 0;
+    if (const char* sm = getenv("UVHTTP_WS_SPEC_MAX")) e->spec_max_avg = strtoull(sm, nullptr, 10);
+    if (const char* fa = getenv("UVHTTP_WS_FUSED_AUX")) e->fused_aux = atoi(fa);
+    if (const char* sf = getenv("UVHTTP_WS_SUMMARY_FAST")) e->sum_fast = atoi(sf) != 0;
+    if (const char* tl = getenv("UVHTTP_WS_TILE")) {  // payload tile shape "BxV" (0x0 = auto)
+        int tb = 0, tv = 0;
+        if (sscanf(tl, "%dx%d", &tb, &tv) == 2) (void)uvhttp_ws_gpu_engine_set_tile(e, tb, tv);  // (validated)
+    }
+    if (const char* fx = getenv("UVHTTP_WS_FIXUP_BLOCKS")) e->fixup_blocks = (uint32_t)strtoul(fx, nullptr, 10);
+    if (e->fixup_blocks == 0) e->fixup_blocks = 1;
+    if (const char* ft = getenv("UVHTTP_WS_FUSED_TILE")) {
+        int fb = 0, fv = 0;
+        if (sscanf(ft, "%dx%d", &fb, &fv) == 2) {
+            e->fused_block = fb;
+            e->fused_vpt = fv;
+        }
+    }
+}
+#endif
+
 int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out) {
     if (!out) return UVHTTP_WS_GPU_EINVAL;
     *out = nullptr;
@@ -4749,9 +4826,22 @@ int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out) {
     uvhttp_ws_gpu_engine_t* e = (uvhttp_ws_gpu_engine_t*)calloc(1, sizeof(*e));
     if (!e) return UVHTTP_WS_GPU_ENOMEM;
     e->device = device;
+    // the product configuration (each choice measured: DESIGN.md §4-5)
     e->store_aux = 18;
     e->max_polls = kMaxPolls;
-    if (const char* mp = getenv("UVHTTP_WS_MAX_POLLS")) e->max_polls = (uint32_t)strtoul(mp, nullptr, 0);
+    e->fused_max_avg = kFusedMaxAvg;
+    // the fused path scans its records with k_plan's look-back (C4: 133-136 us per step against
+    // 144-145 for reduce-then-scan, profiles/r03p6_*)
+    e->rec_lookback = 1;
+    e->plan_wide = 0;  // 1024-thread blocks measured slower on C4 (1690 vs 1785 GiB/s, r03p7)
+    e->build_frames_max = 4096;
+    e->wr_rec_on = 1;
+    e->compact_recs = 0;
+    e->spec_on = 1;
+    e->spec_max_avg = kFusedMaxAvg;
+    e->fused_aux = 18;
+    e->fixup_blocks = 1024;
+    e->sum_fast = 1;
     {
         int prev = 0;
         (void)hipGetDevice(&prev);
@@ -4766,62 +4856,15 @@ int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out) {
             return UVHTTP_WS_GPU_ENOMEM;
         }
     }
-    if (const char* sp = getenv("UVHTTP_WS_STORE_POLICY")) e->store_aux = atoi(sp) == 18 ? 18 : 0;
-    if (const char* fp = getenv("UVHTTP_WS_PLAN_FPT")) e->plan_fpt = atoi(fp);
-    if (const char* pt = getenv("UVHTTP_WS_PLAN_TICKET")) e->plan_no_ticket = atoi(pt) == 0;
-    // test hook: start near the end of the epoch space to exercise the wrap-around clear
-    if (const char* ep = getenv("UVHTTP_WS_EPOCH_START")) {
-        const unsigned long v = strtoul(ep, nullptr, 0);
-        e->epoch = v < kMaxHostEpoch ? (uint32_t)v : 0;
+    {
+        int pools = 0;
+        if (hipDeviceGetAttribute(&pools, hipDeviceAttributeMemoryPoolsSupported, device) != hipSuccess)
+            pools = 0;
+        e->pool_ok = pools ? 1 : 0;
     }
-    if (const char* bs = getenv("UVHTTP_WS_BUILD_SMALL")) e->build_small = atoi(bs);
-    if (const char* fu = getenv("UVHTTP_WS_FUSED")) e->fused_off = atoi(fu) == 0;
-    e->fused_max_avg = kFusedMaxAvg;
-    if (const char* fm = getenv("UVHTTP_WS_FUSED_MAX")) e->fused_max_avg = strtoull(fm, nullptr, 10);
-    // the fused path scans its records with k_plan's look-back by default (C4: 133-136 us per
-    // step against 144-145 for reduce-then-scan, profiles/r03p6_*); UVHTTP_WS_REC_SCAN=3pass
-    e->rec_lookback = 1;
-    e->plan_wide = 0;  // 1024-thread blocks measured slower on C4 (1690 vs 1785 GiB/s, r03p7)
-    if (const char* pw = getenv("UVHTTP_WS_PLAN_WIDE")) e->plan_wide = atoi(pw);
-    if (const char* rs = getenv("UVHTTP_WS_REC_SCAN")) e->rec_lookback = strcmp(rs, "3pass") != 0;
-    e->build_frames_max = 4096;
-    if (const char* bf = getenv("UVHTTP_WS_BUILD_FRAMES")) e->build_frames_max = strtoull(bf, nullptr, 10);
-    if (const char* cm = getenv("UVHTTP_WS_COMPACT"))
-        e->compact_mode = strcmp(cm, "gather") == 0 ? 1 : strcmp(cm, "scatter") == 0 ? 2 : 0;
-    if (const char* ws = getenv("UVHTTP_WS_WALK_SINGLE")) e->walk_single_off = atoi(ws) == 0;
-    e->wr_rec_on = 1;
-    if (const char* wf = getenv("UVHTTP_WS_WALK_FUSE")) e->walk_fuse = atoi(wf) != 0;
-    if (const char* sn = getenv("UVHTTP_WS_STREAM_NT")) e->stream_nt = atoi(sn) != 0;
-    if (const char* ds = getenv("UVHTTP_WS_DESC_SCAN")) e->desc_scan_off = atoi(ds) == 0;
-    if (const char* wn = getenv("UVHTTP_WS_WALK_NT_LOAD")) e->walk_nt_load = atoi(wn) != 0;
-    if (const char* wr = getenv("UVHTTP_WS_WALK_REC")) e->wr_rec_on = atoi(wr) != 0;
-    if (const char* wm = getenv("UVHTTP_WS_WALK"))
-        e->walk_mode = strcmp(wm, "lane") == 0 ? 1 : strcmp(wm, "wave") == 0 ? 2 : 0;
-    if (const char* tc = getenv("UVHTTP_WS_TIME_CHAIN")) e->time_chain = atoi(tc) != 0;
-    e->compact_recs = 0;  // (UVHTTP_WS_COMPACT_RECS=1: under evaluation)
-    if (const char* cr = getenv("UVHTTP_WS_COMPACT_RECS")) e->compact_recs = atoi(cr) != 0;
-    e->spec_on = 1;
-    if (const char* sp2 = getenv("UVHTTP_WS_SPEC")) e->spec_on = atoi(sp2) != 0;
-    e->spec_max_avg = kFusedMaxAvg;
-    if (const char* sm = getenv("UVHTTP_WS_SPEC_MAX")) e->spec_max_avg = strtoull(sm, nullptr, 10);
-    e->fused_aux = 18;
-    if (const char* fa = getenv("UVHTTP_WS_FUSED_AUX")) e->fused_aux = atoi(fa);
-    e->fixup_blocks = 1024;
-    e->sum_fast = 1;
-    if (const char* sf = getenv("UVHTTP_WS_SUMMARY_FAST")) e->sum_fast = atoi(sf) != 0;
-    if (const char* tl = getenv("UVHTTP_WS_TILE")) {  // payload tile shape "BxV" (A/B; 0x0 = auto)
-        int tb = 0, tv = 0;
-        if (sscanf(tl, "%dx%d", &tb, &tv) == 2) (void)uvhttp_ws_gpu_engine_set_tile(e, tb, tv);  // (validated)
-    }
-    if (const char* fx = getenv("UVHTTP_WS_FIXUP_BLOCKS")) e->fixup_blocks = (uint32_t)strtoul(fx, nullptr, 10);
-    if (e->fixup_blocks == 0) e->fixup_blocks = 1;
-    if (const char* ft = getenv("UVHTTP_WS_FUSED_TILE")) {
-        int fb = 0, fv = 0;
-        if (sscanf(ft, "%dx%d", &fb, &fv) == 2) {
-            e->fused_block = fb;
-            e->fused_vpt = fv;
-        }
-    }
+#ifdef UVWS_EXPERIMENTS
+    experiment_knobs(e);
+#endif
     *out = e;
     return UVHTTP_WS_GPU_OK;
 }
@@ -4831,12 +4874,14 @@ void uvhttp_ws_gpu_engine_free(uvhttp_ws_gpu_engine_t* e) {
     int prev = 0;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(e->device);
-    if (e->ws_mem) (void)hipFree(e->ws_mem);
-    if (e->ss_mem) (void)hipFree(e->ss_mem);
-    if (e->bs_mem) (void)hipFree(e->bs_mem);
-    if (e->wt_mem) (void)hipFree(e->wt_mem);
-    if (e->wr_mem) (void)hipFree(e->wr_mem);
-    if (e->dscr) (void)hipFree(e->dscr);
+    (void)hipDeviceSynchronize();
+    scratch_free(e, e->ws_mem);
+    scratch_free(e, e->ss_mem);
+    scratch_free(e, e->bs_mem);
+    scratch_free(e, e->wt_mem);
+    scratch_free(e, e->wr_mem);
+    scratch_free(e, e->dscr);
+    if (e->pool_ok) (void)hipStreamSynchronize(nullptr);
     if (e->ctl) (void)hipFree(e->ctl);
     if (e->stamp_mem) (void)hipFree(e->stamp_mem);
     if (e->order_ev) (void)hipEventDestroy(e->order_ev);
@@ -4872,8 +4917,53 @@ int uvhttp_ws_gpu_engine_sync(uvhttp_ws_gpu_engine_t* e, void* stream) {
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-int uvhttp_ws_gpu_engine_reserve(uvhttp_ws_gpu_engine_t* e, uint32_t max_frames,
-                                 uint64_t max_wire_bytes, uint64_t max_arena_bytes) {
+// Scratch growth without a device-wide wait.  Inside a call (s = the call's
+// stream) the old block is released and the new one allocated and zeroed ON that stream with
+// the stream-ordered allocator: call_begin already ordered every earlier call of this engine
+// before s's next work, so those calls finish with the old block first, the call's own kernels
+// see the zeroed block, and no other stream of the process waits (hipDeviceSynchronize here made
+// a batcher's first large flush stall its upload stream and every other engine's work).  A later
+// call on another stream is ordered behind s by call_begin too.  From the host outside any call
+// (s = null: engine_reserve before a capture, a call's first use) the device is drained before the
+// old block goes and after the new one is zeroed, as the API promises a reserve that is complete
+// when it returns.  Devices without memory pools keep hipMalloc / hipFree and the device syncs.
+static hipError_t scratch_grow(uvhttp_ws_gpu_engine_t* e, void** p, size_t bytes, bool zero,
+                               hipStream_t s, bool in_call) {
+    hipError_t h = hipSuccess;
+    if (!in_call || !e->pool_ok) h = hipDeviceSynchronize();
+    if (*p) (void)(e->pool_ok ? hipFreeAsync(*p, in_call ? s : nullptr) : hipFree(*p));
+    *p = nullptr;
+    if (h != hipSuccess) return h;
+    if (e->pool_ok) {
+        const hipStream_t st = in_call ? s : nullptr;
+        h = hipMallocAsync(p, bytes, st);
+        if (h == hipSuccess && zero) h = hipMemsetAsync(*p, 0, bytes, st);
+        if (h == hipSuccess && !in_call) h = hipStreamSynchronize(nullptr);
+        if (h != hipSuccess && *p) {
+            (void)hipFreeAsync(*p, st);
+            *p = nullptr;
+        }
+        return h;
+    }
+    h = hipMalloc(p, bytes);
+    if (h == hipSuccess && zero) h = hipMemset(*p, 0, bytes);
+    if (h == hipSuccess) h = hipDeviceSynchronize();
+    if (h != hipSuccess && *p) {
+        (void)hipFree(*p);
+        *p = nullptr;
+    }
+    return h;
+}
+// an engine-owned scratch block at engine_free (the device is drained first)
+static void scratch_free(uvhttp_ws_gpu_engine_t* e, void* p) {
+    if (!p) return;
+    if (e->pool_ok) (void)hipFreeAsync(p, nullptr);
+    else (void)hipFree(p);
+}
+
+// the workspace for max_frames / wire / arena; in_call: grown on the call's stream s
+static int reserve_ws(uvhttp_ws_gpu_engine_t* e, uint32_t max_frames, uint64_t max_wire_bytes,
+                      uint64_t max_arena_bytes, hipStream_t s, bool in_call) {
     if (!e) return UVHTTP_WS_GPU_EINVAL;
     if (max_frames > kMaxFrames) return set_err(e, UVHTTP_WS_GPU_EINVAL, "too many frames", hipSuccess);
     const uint64_t tiles = (max_wire_bytes + kMapTile - 1) / kMapTile + 1;
@@ -4905,15 +4995,10 @@ int uvhttp_ws_gpu_engine_reserve(uvhttp_ws_gpu_engine_t* e, uint32_t max_frames,
     int prev = 0;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(e->device);
-    if (e->ws_mem) (void)hipFree(e->ws_mem);
-    e->ws_mem = nullptr;
-    hipError_t h = hipMalloc(&e->ws_mem, bytes);
     // zero: ticket counters start at 0 and no flag / tag matches a live epoch (epochs >= 1)
-    if (h == hipSuccess) h = hipMemset(e->ws_mem, 0, bytes);
-    if (h == hipSuccess) h = hipDeviceSynchronize();
+    hipError_t h = scratch_grow(e, &e->ws_mem, bytes, true, s, in_call);
     (void)hipSetDevice(prev);
     if (h != hipSuccess) {
-        if (e->ws_mem) (void)hipFree(e->ws_mem);
         e->ws_mem = nullptr;
         e->cap_frames = 0;
         e->cap_tiles = e->cap_arena_tiles = 0;
@@ -4939,6 +5024,11 @@ int uvhttp_ws_gpu_engine_reserve(uvhttp_ws_gpu_engine_t* e, uint32_t max_frames,
     e->cap_tiles = tl;
     e->cap_arena_tiles = at;
     return UVHTTP_WS_GPU_OK;
+}
+
+int uvhttp_ws_gpu_engine_reserve(uvhttp_ws_gpu_engine_t* e, uint32_t max_frames,
+                                 uint64_t max_wire_bytes, uint64_t max_arena_bytes) {
+    return reserve_ws(e, max_frames, max_wire_bytes, max_arena_bytes, nullptr, false);
 }
 
 int uvhttp_ws_gpu_engine_set_tile(uvhttp_ws_gpu_engine_t* e, int block, int vectors_per_lane) {
@@ -5031,9 +5121,23 @@ int uvhttp_ws_gpu_engine_read_stamps(uvhttp_ws_gpu_engine_t* e, uvhttp_ws_gpu_st
         return set_err(e, UVHTTP_WS_GPU_ELAUNCH, "read stamps", h);
     }
     if (khz <= 0) khz = 100000;  // gfx9 wall clock: 100 MHz
+    const int rc = uvhttp_ws_gpu_stamps_reduce(host, e->epoch, (uint32_t)khz, out, cap, n_out);
+    free(host);
+    return rc;
+}
+
+uint64_t uvhttp_ws_gpu_stamp_ring_words(void) { return kStampWords; }
+
+// the ring -> one record per (call, kernel): the newest call's words of each slot, earliest
+// begin and latest end (host only; read_stamps runs it on the copied ring, tests on a ring
+// written by uvhttp_ws_gpu_stamp_simulate)
+int uvhttp_ws_gpu_stamps_reduce(const uint64_t* host, uint32_t epoch, uint32_t khz,
+                                uvhttp_ws_gpu_stamp_t* out, uint32_t cap, uint32_t* n_out) {
+    if (!host || (!out && cap) || !n_out || !khz) return UVHTTP_WS_GPU_EINVAL;
+    *n_out = 0;
     // a call's age: how many calls ago it ran, from the latest call's tag (tags wrap after
     // 2^24 - 1 calls, so neither "largest tag" nor the tag order is the call order)
-    const uint32_t cur = stamp_tag(e->epoch);
+    const uint32_t cur = stamp_tag(epoch);
     auto age = [&](uint64_t t) -> uint32_t {
         return (uint32_t)((cur + (uint64_t)kStampTagPeriod - t) % kStampTagPeriod);
     };
@@ -5066,7 +5170,6 @@ int uvhttp_ws_gpu_engine_read_stamps(uvhttp_ws_gpu_engine_t* e, uvhttp_ws_gpu_st
             ++n;
         }
     }
-    free(host);
     if (n > cap) n = cap;
     // call order (oldest first), then start order within a call
     for (uint32_t i = 1; i < n; ++i) {
@@ -5082,6 +5185,27 @@ int uvhttp_ws_gpu_engine_read_stamps(uvhttp_ws_gpu_engine_t* e, uvhttp_ws_gpu_st
         ages[j] = xa;
     }
     *n_out = n;
+    return UVHTTP_WS_GPU_OK;
+}
+
+// What one launch piece of `blocks` workgroups (indices base .. base + blocks - 1 in the whole
+// pass, `waves` waves each) stores into the ring, as ~StampScope does: workgroup i of the piece
+// starts at t_begin + i * (t_end - t_begin) / blocks and its waves end `dur` ticks later.
+int uvhttp_ws_gpu_stamp_simulate(uint64_t* ring, uint32_t epoch, uint32_t kind, uint64_t base,
+                                 uint32_t blocks, uint32_t waves, uint64_t t_begin, uint64_t t_end,
+                                 uint64_t dur) {
+    if (!ring || kind >= kStampKinds || !blocks || !waves || t_end < t_begin) return UVHTTP_WS_GPU_EINVAL;
+    uint64_t* sl = ring + ((uint64_t)(epoch % kStampRing) * kStampKinds + kind) * kStampPer;
+    const uint64_t tag = (uint64_t)stamp_tag(epoch) << 40;
+    for (uint32_t i = 0; i < blocks; ++i) {
+        const uint64_t g = base + i;
+        const bool sample = stamp_sampled(g);
+        if (g >= kStampBegin && !sample) continue;
+        const uint64_t t0 = t_begin + (t_end - t_begin) * i / blocks;
+        if (g < kStampBegin) sl[g] = tag | (t0 & kStampLow);
+        if (!sample) continue;
+        for (uint32_t w = 0; w < waves; ++w) sl[kStampBegin + stamp_end_word(g, w)] = tag | ((t0 + dur) & kStampLow);
+    }
     return UVHTTP_WS_GPU_OK;
 }
 
@@ -5108,8 +5232,12 @@ static int timing_begin(uvhttp_ws_gpu_engine_t* e, hipStream_t s) {
         // timing-only events: no system-scope fence (a fenced marker between two kernels
         // idled the device ~5.8 us per event, profiles/r03p1 kernel trace); the caller's own
         // synchronisation still orders the results.  UVHTTP_WS_TIMING_FENCE=1: fenced (A/B)
+#ifdef UVWS_EXPERIMENTS
         static const unsigned flags = getenv("UVHTTP_WS_TIMING_FENCE") && atoi(getenv("UVHTTP_WS_TIMING_FENCE"))
                                           ? hipEventDefault : hipEventDisableSystemFence;
+#else
+        const unsigned flags = hipEventDisableSystemFence;
+#endif
         if (hipEventCreateWithFlags(&e->ev[e->ev_created], flags) != hipSuccess) return -1;
         e->ev_created++;
     }
@@ -5256,14 +5384,13 @@ static uint64_t max_payload_in(uint64_t slot, int32_t is_server) {
 
 // the engine's descriptor scratch for calls that pass d_desc == NULL on a path that needs
 // descriptors internally (grown on demand; a captured call must not grow it)
-static uvhttp_ws_frame_desc_t* desc_scratch(uvhttp_ws_gpu_engine_t* e, uint32_t n) {
+static uvhttp_ws_frame_desc_t* desc_scratch(uvhttp_ws_gpu_engine_t* e, uint32_t n, hipStream_t s) {
     const uint64_t want = n ? n : 1;
     if (e->dscr && e->dscr_cap >= want) return e->dscr;
     if (e->capturing) return nullptr;
-    if (e->dscr) (void)hipFree(e->dscr);
-    e->dscr = nullptr;
     e->dscr_cap = 0;
-    if (hipMalloc(&e->dscr, want * sizeof(uvhttp_ws_frame_desc_t)) != hipSuccess) {
+    if (scratch_grow(e, reinterpret_cast<void**>(&e->dscr), want * sizeof(uvhttp_ws_frame_desc_t),
+                     false, s, true) != hipSuccess) {
         e->dscr = nullptr;
         return nullptr;
     }
@@ -5309,7 +5436,7 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
     // arena tiles: bounded by both the capacity and the data payload that can exist
     uint64_t arena_need = arena ? (arena_cap < b->wire_len ? arena_cap : b->wire_len) : 0;
     const uint64_t n_atiles = arena ? (arena_need + kMapTile - 1) / kMapTile : 0;
-    rc = uvhttp_ws_gpu_engine_reserve(e, b->n_frames, b->wire_len, arena_need);
+    rc = reserve_ws(e, b->n_frames, b->wire_len, arena_need, (hipStream_t)stream, true);
     if (rc) return rc;
     int prev = 0;
     (void)hipGetDevice(&prev);
@@ -5386,7 +5513,7 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
             if (hs != hipSuccess) return set_err(e, UVHTTP_WS_GPU_ELAUNCH, "launch", hs);
             return UVHTTP_WS_GPU_OK;
         }
-        if (!d_desc && !(d_desc = desc_scratch(e, a.n))) {
+        if (!d_desc && !(d_desc = desc_scratch(e, a.n, s))) {
             if (prev != e->device) (void)hipSetDevice(prev);
             return set_err(e, UVHTTP_WS_GPU_ENOMEM, "descriptor scratch (reserve before capturing)", hipSuccess);
         }
@@ -5435,7 +5562,7 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
     // every other path keeps per-frame descriptors internally: a caller without them gets the
     // engine's scratch
     const bool no_desc = !d_desc;
-    if (!d_desc && !(d_desc = desc_scratch(e, a.n))) {
+    if (!d_desc && !(d_desc = desc_scratch(e, a.n, s))) {
         if (prev != e->device) (void)hipSetDevice(prev);
         return set_err(e, UVHTTP_WS_GPU_ENOMEM, "descriptor scratch (reserve before capturing)", hipSuccess);
     }
@@ -5590,7 +5717,7 @@ int uvhttp_ws_gpu_decode_compact(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batc
 }
 
 static int reserve_streams(uvhttp_ws_gpu_engine_t* e, uint32_t frames, uint32_t streams,
-                           uint32_t reads) {
+                           uint32_t reads, hipStream_t s) {
     if (reads == 0) reads = 1;
     // (the look-back records are sized for the most blocks k_swalk_fused runs, 16 384 / 4, so
     // the connection count of a call never reallocates: a caller such as the batcher issues a
@@ -5612,21 +5739,12 @@ static int reserve_streams(uvhttp_ws_gpu_engine_t* e, uint32_t frames, uint32_t 
     int prev = 0;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(e->device);
-    // (a call of this engine may still run on the caller's stream: let it finish first)
-    if (e->ss_mem) {
-        (void)hipDeviceSynchronize();
-        (void)hipFree(e->ss_mem);
-    }
-    e->ss_mem = nullptr;
-    hipError_t h = hipMalloc(&e->ss_mem, bytes);
-    // (zero: the counters start at 0 and no record tag matches a live epoch; finished before
-    // the call's kernels run on the caller's stream, which the null-stream memset does not
-    // order — as the workspace's reserve)
-    if (h == hipSuccess) h = hipMemset(e->ss_mem, 0, bytes);
-    if (h == hipSuccess) h = hipDeviceSynchronize();
+    // (zero: the counters start at 0 and no record tag matches a live epoch.  On the call's
+    // stream: a call of this engine may still run there with the old block — the batcher issues
+    // a call while its previous one runs — and releases it first; scratch_grow)
+    hipError_t h = scratch_grow(e, &e->ss_mem, bytes, true, s, true);
     (void)hipSetDevice(prev);
     if (h != hipSuccess) {
-        if (e->ss_mem) (void)hipFree(e->ss_mem);
         e->ss_mem = nullptr;
         e->ss_frames = e->ss_reads = 0;
         return set_err(e, UVHTTP_WS_GPU_ENOMEM, "hipMalloc stream scratch", h);
@@ -5671,8 +5789,8 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     CallScope scope{e};
     call_begin(e, (hipStream_t)stream);
     const uint32_t cap = max_frames ? max_frames : 1;
-    int rc = uvhttp_ws_gpu_engine_reserve(e, cap, wire_len, 0);
-    if (!rc) rc = reserve_streams(e, cap, n_streams, n_reads_total);
+    int rc = reserve_ws(e, cap, wire_len, 0, (hipStream_t)stream, true);
+    if (!rc) rc = reserve_streams(e, cap, n_streams, n_reads_total, (hipStream_t)stream);
     if (rc) return rc;
     int prev = 0;
     (void)hipGetDevice(&prev);
@@ -5689,25 +5807,16 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     // slices: connection s's starts at walk_tmp[begin / 2 + s ...] (4-byte entries)
     const uint64_t want = wire_len / 2 + n_streams + 1;
     if (single_ok && !e->capturing && want * 4 <= (8ull << 30) && want > e->wt_cap) {
-        if (e->wt_mem) {
-            (void)hipDeviceSynchronize();  // (an earlier call may still use the slices)
-            (void)hipFree(e->wt_mem);
-        }
-        e->wt_mem = nullptr;
+        // (an earlier call may still use the slices: released behind it on the stream)
         e->wt_cap = 0;
-        if (hipMalloc(&e->wt_mem, want * 4) == hipSuccess) e->wt_cap = want;
+        if (scratch_grow(e, &e->wt_mem, want * 4, false, s, true) == hipSuccess) e->wt_cap = want;
     }
     // the wave walk's frame records (8 bytes per slice entry) while slices and records stay
     // within 8 GiB together; larger calls gather every header again in k_stream_desc
     // (only the wave walk writes and reads them: none for the lane walk — 1 GB less for C2)
     if (single_ok && wave_walk && !e->capturing && want * 12 <= (8ull << 30) && want > e->wr_cap) {
-        if (e->wr_mem) {
-            (void)hipDeviceSynchronize();
-            (void)hipFree(e->wr_mem);
-        }
-        e->wr_mem = nullptr;
         e->wr_cap = 0;
-        if (hipMalloc(&e->wr_mem, want * 8) == hipSuccess) e->wr_cap = want;
+        if (scratch_grow(e, &e->wr_mem, want * 8, false, s, true) == hipSuccess) e->wr_cap = want;
     }
     WalkArgs w;
     w.wire = d_wire;
@@ -5835,7 +5944,7 @@ int uvhttp_ws_gpu_build_frames(uvhttp_ws_gpu_engine_t* e, const uint8_t* d_src, 
     CallScope scope{e};
     call_begin(e, (hipStream_t)stream);
     // scratch: reuse the engine workspace (block/group aggregates as u64, arena map)
-    int rc = uvhttp_ws_gpu_engine_reserve(e, n_frames ? n_frames : 1, 0, 0);
+    int rc = reserve_ws(e, n_frames ? n_frames : 1, 0, 0, (hipStream_t)stream, true);
     if (rc) return rc;
     int prev = 0;
     (void)hipGetDevice(&prev);
@@ -5875,16 +5984,11 @@ int uvhttp_ws_gpu_build_frames(uvhttp_ws_gpu_engine_t* e, const uint8_t* d_src, 
             return set_err(e, UVHTTP_WS_GPU_EINVAL, "build map too small for a captured call",
                            hipSuccess);
         }
-        if (e->bs_mem) (void)hipFree(e->bs_mem);
-        e->bs_mem = nullptr;
         e->bs_tiles = 0;
-        // + 1: kb_emit reads the record after its tile's; that spare entry is never tagged
-        hipError_t h = hipMalloc(&e->bs_mem, (b.n_map + 1) * sizeof(BuildRec));
+        // + 1: kb_emit reads the record after its tile's; that spare entry is never tagged.
         // zero: tag 0 never matches a live epoch (epochs >= 1)
-        if (h == hipSuccess) h = hipMemset(e->bs_mem, 0, (b.n_map + 1) * sizeof(BuildRec));
-        if (h == hipSuccess) h = hipDeviceSynchronize();
+        hipError_t h = scratch_grow(e, &e->bs_mem, (b.n_map + 1) * sizeof(BuildRec), true, s, true);
         if (h != hipSuccess) {
-            if (e->bs_mem) (void)hipFree(e->bs_mem);
             e->bs_mem = nullptr;
             if (prev != e->device) (void)hipSetDevice(prev);
             return set_err(e, UVHTTP_WS_GPU_ENOMEM, "hipMalloc build map", h);
@@ -5979,17 +6083,27 @@ int uvhttp_ws_gpu_apply_mask(uvhttp_ws_gpu_engine_t* e, uint8_t* d_data, uint64_
 int uvhttp_ws_gpu_gen_frames(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint32_t n_frames,
                              uint64_t payload_len, uint64_t seed, int opcode0, int fragmented,
                              int force_keys, void* stream) {
-    if (!e || (!d_wire && n_frames)) return UVHTTP_WS_GPU_EINVAL;
-    if (!n_frames) return UVHTTP_WS_GPU_OK;
+    return uvhttp_ws_gpu_gen_frames_range(e, d_wire, 0, n_frames, n_frames, payload_len, seed,
+                                          opcode0, fragmented, force_keys, stream);
+}
+
+int uvhttp_ws_gpu_gen_frames_range(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint32_t first,
+                                   uint32_t count, uint32_t n_frames, uint64_t payload_len,
+                                   uint64_t seed, int opcode0, int fragmented, int force_keys,
+                                   void* stream) {
+    if (!e || (!d_wire && count)) return UVHTTP_WS_GPU_EINVAL;
+    if ((uint64_t)first + count > n_frames) return set_err(e, UVHTTP_WS_GPU_EINVAL, "range past n_frames", hipSuccess);
+    if (!count) return UVHTTP_WS_GPU_OK;
     const uint64_t wpf = payload_len ? (payload_len + 7) / 8 : 1;
-    uint64_t total = (uint64_t)n_frames * wpf;
+    uint64_t total = (uint64_t)count * wpf;
     uint64_t grid = (total + kBlock - 1) / kBlock;
     if (grid > 65536) grid = 65536;
     int prev = 0;
     (void)hipGetDevice(&prev);
     if (prev != e->device) (void)hipSetDevice(e->device);
     hipLaunchKernelGGL(k_gen_frames, dim3((uint32_t)grid), dim3(kBlock), 0, (hipStream_t)stream,
-                       d_wire, n_frames, payload_len, seed, opcode0, fragmented, force_keys, wpf);
+                       d_wire, first, count, n_frames, payload_len, seed, opcode0, fragmented,
+                       force_keys, wpf);
     hipError_t h = hipGetLastError();
     if (prev != e->device) (void)hipSetDevice(prev);
     if (h != hipSuccess) return set_err(e, UVHTTP_WS_GPU_ELAUNCH, "launch", h);
@@ -6076,7 +6190,9 @@ int uvhttp_ws_gpu_pipeline_create(int device, int depth, uint64_t slot_bytes,
     p->slot_bytes = slot_bytes;
     p->slot_frames = slot_frames;
     p->in_flight = kPipeInFlight;
+#ifdef UVWS_EXPERIMENTS
     if (const char* pf = getenv("UVHTTP_WS_PIPE_IN_FLIGHT")) p->in_flight = atoi(pf);
+#endif
     p->slots = (PipeSlot*)calloc((size_t)depth, sizeof(PipeSlot));
     if (!p->slots) {
         free(p);

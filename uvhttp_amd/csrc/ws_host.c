@@ -507,9 +507,13 @@ __attribute__((visibility("hidden"))) void uvhttp_ws_amd_copy_stream(void* dst, 
         memcpy(dst, src, len);
         return;
     }
-    if (have_avx2 < 0) {  // (UVHTTP_WS_COPY_SSE2=1: the SSE2 path, for tests on AVX2 machines)
+    if (have_avx2 < 0) {
+#ifdef UVWS_EXPERIMENTS  /* UVHTTP_WS_COPY_SSE2=1: the SSE2 path, for tests on AVX2 machines */
         const char* f = getenv("UVHTTP_WS_COPY_SSE2");
         have_avx2 = (__builtin_cpu_supports("avx2") && !(f && f[0] == '1')) ? 1 : 0;
+#else
+        have_avx2 = __builtin_cpu_supports("avx2") ? 1 : 0;
+#endif
     }
     if (have_avx2)
         copy_stream_avx2((uint8_t*)dst, (const uint8_t*)src, len);
