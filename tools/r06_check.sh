@@ -1,0 +1,28 @@
+#!/bin/bash
+# Round-6 GPU check: full pytest -m gpu, smoke(), default bench, then the 2-rank C5 line on one GPU
+# (the N>1 roofline the round-5 verdict found broken).  Logs under gpurun_out/r06_$TAG*.
+# usage: TAG=a tools/r06_check.sh [tests|smoke|bench|c5x2|all ...]
+set -euo pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+TAG=${TAG:-a}
+O=gpurun_out/r06${TAG}
+STEPS=${*:-all}
+has() { [[ " $STEPS " == *" all "* || " $STEPS " == *" $1 "* ]]; }
+if has tests; then
+  PYARGS="-m gpu" tools/gpu_tests.sh r06${TAG}_pytest_gpu.log tests/
+fi
+if has smoke; then
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > ${O}_smoke.log 2>&1
+  tail -1 ${O}_smoke.log
+fi
+if has bench; then
+  timeout -k 10 600 python bench.py --steps 20 --warmup 5 > ${O}_bench.json 2> ${O}_bench.err
+  cat ${O}_bench.json
+fi
+if has c5x2; then
+  timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+    --master-port 29517 bench.py --gpus 2 --config c5 --steps 2 --warmup 1 --oversubscribe \
+    > ${O}_c5x2.json 2> ${O}_c5x2.err
+  cat ${O}_c5x2.json
+fi
