@@ -272,7 +272,10 @@ typedef struct {
 } uvhttp_ws_frame_desc_t;
 
 /* One complete data message (compact decode only, 32 bytes).  The payload handed to
- * on_message is arena[arena_off, arena_off + len); the opcode is the first frame's. */
+ * on_message is arena[arena_off, arena_off + len); the opcode is the first frame's.  When the
+ * summary reports pending_bytes != 0, entry [n_messages] describes the message still open
+ * after the last delivered frame (its bytes so far, last_frame = the latest fragment) and
+ * `reserved` holds its first fragment's payload length; otherwise reserved is 0. */
 typedef struct {
     uint64_t arena_off;
     uint64_t len;
@@ -596,6 +599,36 @@ int uvhttp_ws_gpu_pipeline_wait(uvhttp_ws_gpu_pipeline_t* p, int slot,
 uvhttp_error_t uvhttp_ws_deliver_batch(struct uvhttp_ws_connection* conn, const uint8_t* wire,
                                        const uvhttp_ws_frame_desc_t* desc,
                                        const uvhttp_ws_batch_summary_t* summary);
+
+/* Deliver a decoded COMPACT batch (uvhttp_ws_gpu_decode_compact, with or without descriptors)
+ * to a connection as uvhttp_ws_process_data would have (src/uvhttp_websocket.c:950-1084, the
+ * caller's dispatch src/uvhttp_connection.c:1234-1263): on_message(arena + msgs[m].arena_off,
+ * msgs[m].len, msgs[m].opcode) per complete message, CLOSE (on_close, echo, state = CLOSED) and
+ * PING (pong) through the same hooks as uvhttp_ws_deliver_batch, all in frame order; and a
+ * message still open after the last delivered frame (summary->pending_bytes != 0, described by
+ * msgs[summary->n_messages], which a compact decode writes then) is left in
+ * conn->fragmented_message with the reference's size, capacity and opcode, so the connection's
+ * next process_data call continues it.  Like uvhttp_ws_deliver_batch the batch's bytes never
+ * passed through recv_buffer, which is not touched; the connection must have no message open
+ * (the batch was decoded from a fresh connection's state), else UVHTTP_ERROR_INVALID_PARAM and
+ * nothing is delivered.
+ *   arena, msgs: host copies of arena[0, summary->arena_bytes) and msgs[0, n_messages + 1).
+ *   Control frames keep their (unmasked) payloads in the wire.  With descriptors (desc != NULL,
+ *   host copy of the n_delivered + 1 first entries) they are found there and read from `wire`
+ *   (host copy of the decoded wire; only control payloads are read).  Summary-only (desc ==
+ *   NULL) needs a fixed-stride batch with frame_stride >= 140 — a control frame (<= 131 wire
+ *   bytes) then cannot fill a slot, so only the LAST delivered frame can be one; when that
+ *   frame belongs to no message, `wire` must hold it at wire + (n_delivered - 1) *
+ *   frame_stride (a caller may copy back just those frame_stride bytes into a buffer it
+ *   offsets accordingly).  Reserved opcodes 3-7 / 11-15 are delivered without a callback, as
+ *   the reference ignores them.  Returns UVHTTP_OK, or UVHTTP_ERROR_INVALID_PARAM if the batch
+ *   failed (after delivering the frames before the failure, like process_data) or the
+ *   arguments cannot describe the batch. */
+uvhttp_error_t uvhttp_ws_deliver_messages(struct uvhttp_ws_connection* conn, const uint8_t* arena,
+                                          const uvhttp_ws_message_desc_t* msgs,
+                                          const uvhttp_ws_batch_summary_t* summary,
+                                          const uint8_t* wire, const uvhttp_ws_frame_desc_t* desc,
+                                          uint64_t frame_stride);
 
 /* ---- batcher: live libuv reads -> one device decode per flush -------------------------- */
 /* The caller side of the reference, on_websocket_read (src/uvhttp_connection.c:1098-1175),

@@ -195,6 +195,7 @@ size_t oracle_conn_recv_pos(const orc_conn_t* c) { return c->rbuf_pos; }
 size_t oracle_conn_recv_size(const orc_conn_t* c) { return c->rbuf_size; }
 size_t oracle_conn_frag_size(const orc_conn_t* c) { return c->frag ? c->frag_size : 0; }
 int oracle_conn_frag_pending(const orc_conn_t* c) { return c->frag != NULL; }
+size_t oracle_conn_frag_capacity(const orc_conn_t* c) { return c->frag ? c->frag_cap : 0; }
 int oracle_conn_frag_opcode(const orc_conn_t* c) { return c->frag_opcode; }
 /* harness: copy of recv_buffer[0, rbuf_pos) (tests compare the bytes left buffered) */
 size_t oracle_conn_recv_bytes(const orc_conn_t* c, uint8_t* out, size_t cap) {

@@ -60,6 +60,7 @@ def load():
         "oracle_conn_frag_size": (sz, [vp]),
         "oracle_conn_frag_opcode": (C.c_int, [vp]),
         "oracle_conn_frag_pending": (C.c_int, [vp]),
+        "oracle_conn_frag_capacity": (sz, [vp]),
         "oracle_conn_recv_bytes": (sz, [vp, vp, sz]),
         "oracle_conn_events": (sz, [vp, vp, sz]),
         "oracle_process_data": (C.c_int, [vp, vp, sz]),
@@ -152,6 +153,10 @@ class OracleConn:
     @property
     def frag_opcode(self):
         return self.L.oracle_conn_frag_opcode(self.c)
+
+    @property
+    def frag_capacity(self):
+        return self.L.oracle_conn_frag_capacity(self.c)
 
     @property
     def frag_pending(self):

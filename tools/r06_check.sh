@@ -26,3 +26,11 @@ if has c5x2; then
     > ${O}_c5x2.json 2> ${O}_c5x2.err
   cat ${O}_c5x2.json
 fi
+if has deliver; then
+  tools/gpu_tests.sh r06${TAG}_pytest_deliver.log tests/test_gpu_deliver_messages.py tests/test_gpu_summary_compact.py \
+    tests/test_gpu_spec_compact.py tests/test_gpu_parity.py
+fi
+if has abstamps; then
+  AB_STAMPS=1 timeout -k 10 300 python tools/ab_lib.py tree tree c3:inplace c2:inplace > ${O}_ab_stamps.txt 2>&1
+  cat ${O}_ab_stamps.txt
+fi

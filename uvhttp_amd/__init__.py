@@ -303,6 +303,8 @@ def load_library(path: str) -> C.CDLL:
                                                     i32]),
         "uvhttp_ws_gpu_pipeline_wait": (C.c_int, [vp, C.c_int, C.POINTER(vp), C.POINTER(vp)]),
         "uvhttp_ws_deliver_batch": (C.c_int, [C.POINTER(WsConnectionStruct), vp, vp, vp]),
+        "uvhttp_ws_deliver_messages": (C.c_int, [C.POINTER(WsConnectionStruct), vp, vp, vp, vp, vp,
+                                                 u64]),
         "uvhttp_ws_gpu_decode_streams": (C.c_int, [vp, vp, u64, vp, u32, u32, vp, vp, vp]),
         "uvhttp_ws_gpu_decode_reads": (C.c_int, [vp, vp, u64, vp, u32, vp, u32, u32, vp, vp, vp]),
         "uvhttp_ws_gpu_build_frames": (C.c_int, [vp, vp, u64, vp, u32, vp, u64, vp, vp]),
@@ -470,6 +472,31 @@ class WsConnection:
             self.close()
         except Exception:
             pass
+
+
+def _host_buf(x):
+    """a ctypes buffer holding a host copy of x (bytes, numpy array, torch tensor) or None"""
+    if x is None:
+        return None
+    if hasattr(x, "cpu"):
+        x = x.cpu().numpy()
+    raw = bytes(x.tobytes() if hasattr(x, "tobytes") else x)
+    return (C.c_uint8 * max(1, len(raw))).from_buffer_copy(raw or b"\0")
+
+
+def deliver_messages(conn, arena, msgs, summary, wire=None, desc=None, stride=0) -> int:
+    """uvhttp_ws_deliver_messages (include/uvhttp_ws_amd.h): a compact decode's arena,
+    message table (n_messages + 1 entries: the open message's too) and summary (a dict or its
+    raw bytes) delivered to a WsConnection; wire / desc only for control frames."""
+    if isinstance(summary, dict):
+        sb = BatchSummary(**summary)
+    else:
+        sb = BatchSummary.from_buffer_copy(bytes(summary.cpu().numpy().tobytes()
+                                                 if hasattr(summary, "cpu") else summary)[:C.sizeof(BatchSummary)])
+    bufs = [_host_buf(x) for x in (arena, msgs, wire, desc)]
+    ptrs = [C.cast(b, C.c_void_p) if b is not None else None for b in bufs]
+    return lib().uvhttp_ws_deliver_messages(conn.ptr, ptrs[0], ptrs[1], C.byref(sb), ptrs[2],
+                                            ptrs[3], stride)
 
 
 # ---- batched device surface -------------------------------------------------------------

@@ -403,6 +403,8 @@ struct BatchArgs {
     uint32_t gate;           // k_plan / k_spec_fix run only when ws.ctl[kCtlGate] holds this call's
                              // epoch (the summary-only compact decode's fallback)
     uint32_t cas_claims;     // the engine has captured calls: tag_claim displaces later epochs
+    uvhttp_ws_message_desc_t* msgs;  // compact decode: the message table (the summary writer
+                                     // adds the open message's entry at msgs[n_messages])
 };
 
 // ------------------------------------------------------------------------------------
@@ -1345,6 +1347,20 @@ __device__ void write_summary(const BatchArgs& a, const uvhttp_ws_frame_desc_t* 
     s.arena_bytes = a.arena ? e.data_pay : 0;
     s.pending_bytes = (e.last_data >= 0 && (e.bits & kLastOpen)) ? e.seg_pay : 0;
     *a.summary = s;
+    // compact: the message a fragmented start left open (the arena's last pending_bytes), so a
+    // caller can leave conn->fragmented_message as process_data does (uvhttp_ws_deliver_messages);
+    // reserved = its first fragment's length, from which the reference's capacity follows
+    // (src/uvhttp_websocket.c:794-816).  n_messages < n_frames here: the open start is no FIN.
+    if (a.msgs && s.pending_bytes && e.last_start >= 0) {
+        uvhttp_ws_message_desc_t m;
+        m.arena_off = e.data_pay - e.seg_pay;
+        m.len = e.seg_pay;
+        m.first_frame = (uint32_t)e.last_start;
+        m.last_frame = (uint32_t)e.last_data;
+        m.opcode = (int32_t)((e.bits & kOpMask) >> kOpShift);
+        m.reserved = (uint32_t)desc[e.last_start].payload_len;
+        a.msgs[s.n_messages] = m;
+    }
 }
 
 // k_finalize (batch mode, after the payload pass, one lane per frame): statuses after the
@@ -2445,6 +2461,16 @@ __global__ __launch_bounds__(kBlock) void k_sum_msgs(BatchArgs a, Workspace ws, 
     sm.arena_bytes = sm.payload_bytes;
     sm.pending_bytes = open ? (uint64_t)(nd - ls) * P : 0;
     *a.summary = sm;
+    if (open) {  // the open message (write_summary's entry; every fragment is P bytes)
+        uvhttp_ws_message_desc_t md;
+        md.arena_off = (uint64_t)ls * P;
+        md.len = sm.pending_bytes;
+        md.first_frame = ls;
+        md.last_frame = nd - 1;
+        md.opcode = bin ? 2 : 1;
+        md.reserved = (uint32_t)P;
+        msgs[nfin] = md;
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -5458,6 +5484,7 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
     a.arena_cap = arena_cap;
     a.n_arena_tiles = n_atiles;
     a.summary = d_summary;
+    a.msgs = arena ? d_msgs : nullptr;
     a.max_polls = e->max_polls;
     a.dev_epoch = e->capturing ? 1u : 0u;
     a.epoch = next_epoch(e, s);

@@ -344,6 +344,102 @@ uvhttp_error_t uvhttp_ws_deliver_batch(struct uvhttp_ws_connection* c, const uin
     return summary->status == 0 ? UVHTTP_OK : UVHTTP_ERROR_INVALID_PARAM;
 }
 
+/* A control frame of a compact decode (payload unmasked in place in the wire) through the
+ * same dispatch as process_data; data frames of reserved opcodes fall through to its default. */
+static void dispatch_control(uvhttp_ws_connection_t* c, int opcode, const uint8_t* payload,
+                             uint64_t len) {
+    uvhttp_ws_frame_header_t h;
+    memset(&h, 0, sizeof(h));
+    h.fin = 1;
+    h.opcode = (uint8_t)(opcode & 0x0F);
+    h.payload_length = len;
+    (void)dispatch_frame(c, &h, len ? payload : NULL);
+}
+
+/* The delivered frames of a compact decode are its messages (each fires at its last frame) and
+ * its non-data frames, merged in frame order (include/uvhttp_ws_amd.h). */
+uvhttp_error_t uvhttp_ws_deliver_messages(struct uvhttp_ws_connection* c, const uint8_t* arena,
+                                          const uvhttp_ws_message_desc_t* msgs,
+                                          const uvhttp_ws_batch_summary_t* summary,
+                                          const uint8_t* wire, const uvhttp_ws_frame_desc_t* desc,
+                                          uint64_t frame_stride) {
+    if (c == NULL || summary == NULL || c->fragmented_message != NULL)
+        return UVHTTP_ERROR_INVALID_PARAM;
+    const uint32_t nd = summary->n_delivered, nm = summary->n_messages;
+    const int open = summary->pending_bytes != 0;
+    if (nd > summary->n_frames || nm > nd || ((nm || open) && (msgs == NULL || arena == NULL)))
+        return UVHTTP_ERROR_INVALID_PARAM;
+    /* every message inside the arena, in frame order, ending at a delivered frame */
+    for (uint32_t m = 0; m < nm + (uint32_t)open; ++m) {
+        const uvhttp_ws_message_desc_t* d = &msgs[m];
+        if (d->arena_off > summary->arena_bytes || d->len > summary->arena_bytes - d->arena_off ||
+            d->first_frame > d->last_frame || d->last_frame >= nd ||
+            (m && d->first_frame <= msgs[m - 1].last_frame))
+            return UVHTTP_ERROR_INVALID_PARAM;
+    }
+    if (open && (msgs[nm].len != summary->pending_bytes || msgs[nm].reserved == 0))
+        return UVHTTP_ERROR_INVALID_PARAM;
+    /* summary-only: only the last delivered frame can be a non-data frame (frames of a
+     * >= 140-byte stride are too long to be control frames); find out whether it is one */
+    const uint8_t* last_ctl = NULL;
+    uvhttp_ws_frame_header_t lh;
+    size_t lhead = 0;
+    if (desc == NULL && nd > 0) {
+        if (frame_stride < 140) return UVHTTP_ERROR_INVALID_PARAM;
+        const uint32_t last = nd - 1;
+        const int covered = (nm && msgs[nm - 1].last_frame == last) || (open && msgs[nm].last_frame == last);
+        if (!covered) {
+            if (wire == NULL) return UVHTTP_ERROR_INVALID_PARAM;
+            last_ctl = wire + (size_t)last * frame_stride;
+            if (uvhttp_ws_parse_frame_header(last_ctl, (size_t)frame_stride, &lh, &lhead) != UVHTTP_OK)
+                return UVHTTP_ERROR_INVALID_PARAM;
+            if (lh.opcode < UVHTTP_WS_OPCODE_CLOSE) last_ctl = NULL; /* a data frame that completes
+                                                                      nothing: a zero-length start */
+        }
+    }
+    if (desc != NULL && nd > 0 && wire == NULL) {
+        for (uint32_t i = 0; i < nd; ++i)
+            if (desc[i].opcode >= UVHTTP_WS_OPCODE_CLOSE && desc[i].payload_len)
+                return UVHTTP_ERROR_INVALID_PARAM;
+    }
+
+    uint32_t m = 0;
+    if (desc != NULL) {
+        for (uint32_t i = 0; i < nd; ++i) {
+            const uvhttp_ws_frame_desc_t* d = &desc[i];
+            if (d->opcode < UVHTTP_WS_OPCODE_CLOSE) continue; /* data frames: their messages */
+            for (; m < nm && msgs[m].last_frame < i; ++m)
+                if (c->on_message)
+                    c->on_message(c, (const char*)arena + msgs[m].arena_off, (size_t)msgs[m].len,
+                                  msgs[m].opcode);
+            dispatch_control(c, d->opcode, wire ? wire + d->payload_off : NULL, d->payload_len);
+        }
+    }
+    for (; m < nm; ++m)
+        if (c->on_message)
+            c->on_message(c, (const char*)arena + msgs[m].arena_off, (size_t)msgs[m].len,
+                          msgs[m].opcode);
+    if (last_ctl != NULL)
+        dispatch_control(c, lh.opcode, last_ctl + lhead + (lh.mask ? 4u : 0u), lh.payload_length);
+    if (open) { /* the open message as append_fragment left it: capacity = first fragment
+                   doubled until it holds everything appended (src/uvhttp_websocket.c:794-816) */
+        const uvhttp_ws_message_desc_t* d = &msgs[nm];
+        size_t cap = (size_t)d->reserved;
+        while (cap < (size_t)d->len) {
+            if (cap > SIZE_MAX / 2) return UVHTTP_ERROR_INVALID_PARAM;
+            cap *= 2;
+        }
+        uint8_t* buf = (uint8_t*)malloc(cap);
+        if (buf == NULL) return UVHTTP_ERROR_INVALID_PARAM;
+        memcpy(buf, arena + d->arena_off, (size_t)d->len);
+        c->fragmented_message = buf;
+        c->fragmented_size = (size_t)d->len;
+        c->fragmented_capacity = cap;
+        c->fragmented_opcode = (uvhttp_ws_opcode_t)d->opcode;
+    }
+    return summary->status == 0 ? UVHTTP_OK : UVHTTP_ERROR_INVALID_PARAM;
+}
+
 /* ---- stream decode, host side (include/uvhttp_ws_amd.h) ---------------------------------- */
 
 void uvhttp_ws_stream_init(const struct uvhttp_ws_connection* c, uint64_t begin, uint64_t len,
