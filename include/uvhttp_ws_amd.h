@@ -588,6 +588,24 @@ int uvhttp_ws_gpu_pipeline_submit(uvhttp_ws_gpu_pipeline_t* p, int slot, uint64_
 int uvhttp_ws_gpu_pipeline_wait(uvhttp_ws_gpu_pipeline_t* p, int slot,
                                 const uvhttp_ws_frame_desc_t** desc,
                                 const uvhttp_ws_batch_summary_t** summary);
+/* Compact submissions: H2D -> uvhttp_ws_gpu_decode_compact -> D2H of the message arena, the
+ * message table and the summary, for uvhttp_ws_deliver_messages (messages reassembled on the
+ * device: on_message reads the arena, no fragment copying on the host).  A fixed-stride batch
+ * of >= 140-byte frames decodes summary-only (no descriptors) and only its last frame's slot
+ * comes back into the slot buffer; any other batch decodes into descriptors, which come back
+ * with the decoded wire.  wait_compact returns host pointers valid until the slot's next
+ * submission; *desc is NULL for a summary-only batch.  Deliver with
+ *   uvhttp_ws_deliver_messages(conn, arena, msgs, summary, slot_buffer(slot), desc, stride).
+ * A slot's arena and table are allocated at its first compact submission (slot_bytes + 64 and
+ * slot_frames entries). */
+int uvhttp_ws_gpu_pipeline_submit_compact(uvhttp_ws_gpu_pipeline_t* p, int slot, uint64_t wire_len,
+                                          int use_offsets, uint64_t stride, uint32_t n_frames,
+                                          int32_t max_frame_size, int32_t max_message_size,
+                                          int32_t is_server);
+int uvhttp_ws_gpu_pipeline_wait_compact(uvhttp_ws_gpu_pipeline_t* p, int slot, const uint8_t** arena,
+                                        const uvhttp_ws_message_desc_t** msgs,
+                                        const uvhttp_ws_frame_desc_t** desc,
+                                        const uvhttp_ws_batch_summary_t** summary);
 
 /* Deliver a decoded in-place batch to a connection exactly as uvhttp_ws_process_data would
  * have (src/uvhttp_websocket.c:950-1084): on_message per complete message (fragments

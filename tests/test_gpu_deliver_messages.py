@@ -167,3 +167,64 @@ def test_c4_full_size(torch, eng):
     arena, msgs, s, wire, _, fast = _device_compact(torch, eng, frames, stride=stride)
     assert fast and s["n_messages"] == 65536
     _deliver_and_check(frames, arena, msgs, s, wire, None, stride=stride)
+
+
+@pytest.mark.parametrize("depth", [2, 3, 5])
+def test_pipeline_compact(torch, depth):
+    """the host-memory pipeline's compact submissions (summary-only stride batches with a
+    control frame or an open message at the end; offset-table batches with descriptors),
+    interleaved with in-place submissions on the same slots, delivered with
+    uvhttp_ws_deliver_messages from the slots' host results"""
+    import uvhttp_amd as U
+    pipe = U.GpuPipeline(0, depth=depth, slot_bytes=4 << 20, slot_frames=8192)
+    rng = random.Random(77 + depth)
+    jobs = []
+    for b in range(9 + depth):
+        kind = b % 3
+        if kind == 0:  # summary-only stride batch
+            stride = rng.choice([140, 264, 1000])
+            frames = _uniform(rng, rng.randint(1, 3000), stride, rng.choice([0.0, 0.4, 1.0]))
+            if rng.random() < 0.5:
+                frames.append(rng.choice([D.Frame(8, 1, b"\x03\xe8x"), D.Frame(9, 1, b"p")]))
+            jobs.append(("sum", frames, stride))
+        elif kind == 1:  # descriptors
+            bad = rng.randrange(40) if b == 4 else None
+            jobs.append(("desc", D.mixed(rng, 40, bad_at=bad), 0))
+        else:  # in place, same slots
+            jobs.append(("inplace", D.mixed(rng, 30), 0))
+    inflight = {}
+
+    def finish(slot, job):
+        kind, frames, stride = job
+        if kind == "inplace":
+            dp, sp, s = pipe.wait(slot)
+            conn = U.WsConnection(1, MF, MM, user_data=True)
+            with D.control_sink() as sink:
+                rc = pipe.deliver(conn, slot, dp, sp)
+                D.check(conn, sink, D.expected(frames, s["n_delivered"], MF, MM), rc, s["status"])
+            return
+        ap, mp, dp, sp, s = pipe.wait_compact(slot)
+        assert (dp is None) == (kind == "sum")
+        conn = U.WsConnection(1, MF, MM, user_data=True)
+        with D.control_sink() as sink:
+            rc = pipe.deliver_messages(conn, slot, ap, mp, dp, sp, stride=stride)
+            D.check(conn, sink, D.expected(frames, s["n_delivered"], MF, MM), rc, s["status"])
+
+    for k, job in enumerate(jobs):
+        slot = k % depth
+        if slot in inflight:
+            finish(slot, inflight.pop(slot))
+        kind, frames, stride = job
+        wire = np.frombuffer(b"".join(f.bytes for f in frames), np.uint8)
+        pipe.buffer(slot)[: wire.size] = wire
+        if kind == "sum":
+            pipe.submit_compact(slot, wire.size, len(frames), stride=stride, max_message_size=MM)
+        else:
+            offs = np.cumsum([0] + [len(f.bytes) for f in frames[:-1]]).astype(np.uint64)
+            pipe.offsets(slot)[: offs.size] = offs
+            sub = pipe.submit if kind == "inplace" else pipe.submit_compact
+            sub(slot, wire.size, len(frames), use_offsets=True, max_message_size=MM)
+        inflight[slot] = job
+    for slot, job in inflight.items():
+        finish(slot, job)
+    pipe.close()

@@ -8,10 +8,13 @@ For each config: K calls back to back between two events (stamps on), then the s
 of those calls.  Reports the events' per-call time, the stamped chain (first kernel's begin to
 the last kernel's end) per call, and the ratio of the stamped span of all K calls (first begin
 to last end) to the events' span — a clock-rate error shows as that ratio != 1 on every config,
-a late / early stamp word as a per-call chain above the per-call event time."""
+a late / early stamp word as a per-call chain above the per-call event time.  The rows differ in
+what precedes the measured calls: nothing, an idle host pause, or the clearing read_stamps()
+(a 71 MB copy back) with and without warm-up calls after it — the device's clocks after an idle."""
 import os
 import statistics
 import sys
+import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
@@ -34,9 +37,14 @@ def main():
         for _ in range(3):
             e.decode_inplace(wire, n, stride=stride, wire_len=wl, desc=desc, summary=summ)
         torch.cuda.synchronize()
-        for stamps in (False, True):
+        # (stamps, idle before the measured calls, warm-up calls after the idle / the clear)
+        for stamps, idle, warm in ((False, 0, 0), (False, 0.05, 0), (True, 0, 0), (True, 0, 40),
+                                   (False, 0, 0)):
             e.set_stamps(stamps)
             e.read_stamps() if stamps else None
+            time.sleep(idle)
+            for _ in range(warm):
+                e.decode_inplace(wire, n, stride=stride, wire_len=wl, desc=desc, summary=summ)
             evs = [torch.cuda.Event(enable_timing=True) for _ in range(K + 1)]
             evs[0].record()
             for k in range(K):
@@ -45,7 +53,7 @@ def main():
             torch.cuda.synchronize()
             per = [evs[k].elapsed_time(evs[k + 1]) * 1000 for k in range(1, K)]  # (first: launch)
             span_ev = evs[1].elapsed_time(evs[K]) * 1000
-            line = f"{cfg} stamps={int(stamps)} event per call median {statistics.median(per):8.1f} us"
+            line = f"{cfg} stamps={int(stamps)} idle={idle} warm={warm:2d} event per call median {statistics.median(per):8.1f} us"
             if stamps:
                 recs = e.read_stamps()
                 calls = sorted({r[0] for r in recs})[-K:]

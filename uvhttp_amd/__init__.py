@@ -302,6 +302,10 @@ def load_library(path: str) -> C.CDLL:
         "uvhttp_ws_gpu_pipeline_submit": (C.c_int, [vp, C.c_int, u64, C.c_int, u64, u32, i32, i32,
                                                     i32]),
         "uvhttp_ws_gpu_pipeline_wait": (C.c_int, [vp, C.c_int, C.POINTER(vp), C.POINTER(vp)]),
+        "uvhttp_ws_gpu_pipeline_submit_compact": (C.c_int, [vp, C.c_int, u64, C.c_int, u64, u32, i32,
+                                                            i32, i32]),
+        "uvhttp_ws_gpu_pipeline_wait_compact": (C.c_int, [vp, C.c_int, C.POINTER(vp), C.POINTER(vp),
+                                                          C.POINTER(vp), C.POINTER(vp)]),
         "uvhttp_ws_deliver_batch": (C.c_int, [C.POINTER(WsConnectionStruct), vp, vp, vp]),
         "uvhttp_ws_deliver_messages": (C.c_int, [C.POINTER(WsConnectionStruct), vp, vp, vp, vp, vp,
                                                  u64]),
@@ -778,6 +782,29 @@ class GpuPipeline:
                             ("flags", "u1"), ("header_size", "u1"), ("status", "i1"),
                             ("wire_len", "<u4")])
         return self.np.frombuffer(raw, dtype=dt, count=n)
+
+    def submit_compact(self, slot, wire_len, n_frames, stride=0, use_offsets=False,
+                       max_frame_size=16 * 1024 * 1024, max_message_size=64 * 1024 * 1024,
+                       is_server=1):
+        rc = self._L.uvhttp_ws_gpu_pipeline_submit_compact(self.h, slot, wire_len,
+                                                           1 if use_offsets else 0, stride, n_frames,
+                                                           max_frame_size, max_message_size, is_server)
+        if rc != 0:
+            raise GpuError(f"pipeline submit_compact rc={rc}")
+
+    def wait_compact(self, slot):
+        """-> (arena ptr, msgs ptr, desc ptr (None: summary-only), summary ptr, summary dict)"""
+        ap, mp, dp, sp = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_void_p()
+        rc = self._L.uvhttp_ws_gpu_pipeline_wait_compact(self.h, slot, C.byref(ap), C.byref(mp),
+                                                         C.byref(dp), C.byref(sp))
+        if rc != 0:
+            raise GpuError(f"pipeline wait_compact rc={rc}")
+        return ap, mp, (dp if dp.value else None), sp, BatchSummary.from_address(sp.value).as_dict()
+
+    def deliver_messages(self, conn, slot, ap, mp, dp, sp, stride=0):
+        """uvhttp_ws_deliver_messages from this slot's compact results"""
+        ptr = self._L.uvhttp_ws_gpu_pipeline_slot_buffer(self.h, slot)
+        return self._L.uvhttp_ws_deliver_messages(conn.ptr, ap, mp, sp, C.c_void_p(ptr), dp, stride)
 
     def deliver(self, conn, slot, dp, sp):
         """uvhttp_ws_deliver_batch on a WsConnection from this slot's decoded bytes."""

@@ -6155,6 +6155,13 @@ struct PipeSlot {
     uvhttp_ws_batch_summary_t* d_sum;
     hipEvent_t up_ev, done_ev;
     int busy;
+    // compact submissions (allocated at a slot's first one): the message arena and table
+    uint8_t* h_arena;  // pinned
+    uvhttp_ws_message_desc_t* h_msgs;  // pinned
+    uint8_t* d_arena;
+    uvhttp_ws_message_desc_t* d_msgs;
+    int compact;       // the slot's last submission was compact
+    int with_desc;     //   ... and decoded into descriptors (not summary-only)
 };
 
 struct uvhttp_ws_gpu_pipeline {
@@ -6195,6 +6202,10 @@ void uvhttp_ws_gpu_pipeline_free(uvhttp_ws_gpu_pipeline_t* p) {
         if (s.d_off) (void)hipFree(s.d_off);
         if (s.d_desc) (void)hipFree(s.d_desc);
         if (s.d_sum) (void)hipFree(s.d_sum);
+        if (s.h_arena) (void)hipHostFree(s.h_arena);
+        if (s.h_msgs) (void)hipHostFree(s.h_msgs);
+        if (s.d_arena) (void)hipFree(s.d_arena);
+        if (s.d_msgs) (void)hipFree(s.d_msgs);
         if (s.up_ev) (void)hipEventDestroy(s.up_ev);
         if (s.done_ev) (void)hipEventDestroy(s.done_ev);
     }
@@ -6314,6 +6325,7 @@ int uvhttp_ws_gpu_pipeline_submit(uvhttp_ws_gpu_pipeline_t* p, int slot, uint64_
     if (!rc && h != hipSuccess) rc = UVHTTP_WS_GPU_ELAUNCH;
     if (!rc) {
         s.busy = 1;
+        s.compact = 0;
         p->recent[p->n_sub % 16] = slot;
         p->n_sub++;
     }
@@ -6321,12 +6333,116 @@ int uvhttp_ws_gpu_pipeline_submit(uvhttp_ws_gpu_pipeline_t* p, int slot, uint64_
     return rc;
 }
 
+// Compact submission (include/uvhttp_ws_amd.h): H2D -> decode_compact -> D2H of the arena, the
+// message table and the summary.  A stride batch of >= 140-byte frames decodes summary-only (the
+// fast path: no descriptors) and only its last frame's slot comes back into the slot buffer
+// (deliver_messages reads a control frame there); any other batch decodes into descriptors, and
+// they and the wire (control payloads, unmasked in place) come back too.
+int uvhttp_ws_gpu_pipeline_submit_compact(uvhttp_ws_gpu_pipeline_t* p, int slot, uint64_t wire_len,
+                                          int use_offsets, uint64_t stride, uint32_t n_frames,
+                                          int32_t max_frame_size, int32_t max_message_size,
+                                          int32_t is_server) {
+    if (!p || slot < 0 || slot >= p->depth) return UVHTTP_WS_GPU_EINVAL;
+    PipeSlot& s = p->slots[slot];
+    if (s.busy || wire_len > p->slot_bytes || n_frames > p->slot_frames) return UVHTTP_WS_GPU_EINVAL;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(p->device);
+    hipError_t h = hipSuccess;
+    const size_t arena_cap = (size_t)p->slot_bytes + 64;
+    const size_t msg_bytes = (size_t)p->slot_frames * sizeof(uvhttp_ws_message_desc_t);
+    if (!s.d_arena) {
+        if (hipHostMalloc((void**)&s.h_arena, arena_cap, hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc((void**)&s.h_msgs, msg_bytes, hipHostMallocDefault) != hipSuccess ||
+            hipMalloc((void**)&s.d_msgs, msg_bytes) != hipSuccess ||
+            hipMalloc((void**)&s.d_arena, arena_cap) != hipSuccess) {
+            if (s.h_arena) (void)hipHostFree(s.h_arena);
+            if (s.h_msgs) (void)hipHostFree(s.h_msgs);
+            if (s.d_msgs) (void)hipFree(s.d_msgs);
+            s.h_arena = nullptr;
+            s.h_msgs = nullptr;
+            s.d_msgs = nullptr;
+            s.d_arena = nullptr;
+            (void)hipSetDevice(prev);
+            return UVHTTP_WS_GPU_ENOMEM;
+        }
+    }
+    if (p->in_flight > 0 && p->in_flight < 16 && p->n_sub >= (uint64_t)p->in_flight)
+        h = hipEventSynchronize(p->slots[p->recent[(p->n_sub - p->in_flight) % 16]].done_ev);
+    if (h == hipSuccess && wire_len) h = hipMemcpyAsync(s.d_wire, s.h_wire, wire_len, hipMemcpyHostToDevice, p->up);
+    if (h == hipSuccess && use_offsets && n_frames)
+        h = hipMemcpyAsync(s.d_off, s.h_off, (size_t)n_frames * 8, hipMemcpyHostToDevice, p->up);
+    if (h == hipSuccess) h = hipEventRecord(s.up_ev, p->up);
+    if (h == hipSuccess) h = hipStreamWaitEvent(p->cs, s.up_ev, 0);
+    int rc = h == hipSuccess ? UVHTTP_WS_GPU_OK : UVHTTP_WS_GPU_ELAUNCH;
+    const bool sum_only = !use_offsets && stride >= 140;
+    if (!rc) {
+        uvhttp_ws_batch_t b;
+        b.wire = s.d_wire;
+        b.wire_len = wire_len;
+        b.frame_off = use_offsets ? s.d_off : nullptr;
+        b.frame_stride = stride;
+        b.n_frames = n_frames;
+        b.max_frame_size = max_frame_size;
+        b.max_message_size = max_message_size;
+        b.is_server = is_server;
+        rc = uvhttp_ws_gpu_decode_compact(p->eng, &b, s.d_arena, arena_cap, sum_only ? nullptr : s.d_desc,
+                                          s.d_msgs, s.d_sum, p->cs);
+    }
+    // the arena holds at most the wire's bytes; the table n_frames entries (the open one included)
+    if (!rc && wire_len) h = hipMemcpyAsync(s.h_arena, s.d_arena, wire_len, hipMemcpyDeviceToHost, p->cs);
+    if (!rc && h == hipSuccess && n_frames)
+        h = hipMemcpyAsync(s.h_msgs, s.d_msgs, (size_t)n_frames * sizeof(uvhttp_ws_message_desc_t),
+                           hipMemcpyDeviceToHost, p->cs);
+    if (!rc && h == hipSuccess && n_frames) {
+        if (sum_only) {  // the last frame's slot (a control frame there is read from it)
+            const uint64_t at = (uint64_t)(n_frames - 1) * stride;
+            if (at < wire_len)
+                h = hipMemcpyAsync(s.h_wire + at, s.d_wire + at, wire_len - at, hipMemcpyDeviceToHost, p->cs);
+        } else {
+            h = hipMemcpyAsync(s.h_desc, s.d_desc, (size_t)n_frames * sizeof(uvhttp_ws_frame_desc_t),
+                               hipMemcpyDeviceToHost, p->cs);
+            if (h == hipSuccess && wire_len)
+                h = hipMemcpyAsync(s.h_wire, s.d_wire, wire_len, hipMemcpyDeviceToHost, p->cs);
+        }
+    }
+    if (!rc && h == hipSuccess)
+        h = hipMemcpyAsync(s.h_sum, s.d_sum, sizeof(uvhttp_ws_batch_summary_t), hipMemcpyDeviceToHost, p->cs);
+    if (!rc && h == hipSuccess) h = hipEventRecord(s.done_ev, p->cs);
+    if (!rc && h != hipSuccess) rc = UVHTTP_WS_GPU_ELAUNCH;
+    if (!rc) {
+        s.busy = 1;
+        s.compact = 1;
+        s.with_desc = sum_only ? 0 : 1;
+        p->recent[p->n_sub % 16] = slot;
+        p->n_sub++;
+    }
+    (void)hipSetDevice(prev);
+    return rc;
+}
+
+int uvhttp_ws_gpu_pipeline_wait_compact(uvhttp_ws_gpu_pipeline_t* p, int slot, const uint8_t** arena,
+                                        const uvhttp_ws_message_desc_t** msgs,
+                                        const uvhttp_ws_frame_desc_t** desc,
+                                        const uvhttp_ws_batch_summary_t** summary) {
+    if (!p || slot < 0 || slot >= p->depth) return UVHTTP_WS_GPU_EINVAL;
+    PipeSlot& s = p->slots[slot];
+    if (!s.busy || !s.compact) return UVHTTP_WS_GPU_EINVAL;
+    const hipError_t h = hipEventSynchronize(s.done_ev);
+    s.busy = 0;
+    if (arena) *arena = s.h_arena;
+    if (msgs) *msgs = s.h_msgs;
+    if (desc) *desc = s.with_desc ? s.h_desc : nullptr;
+    if (summary) *summary = s.h_sum;
+    return h == hipSuccess ? UVHTTP_WS_GPU_OK : UVHTTP_WS_GPU_ELAUNCH;
+}
+
 int uvhttp_ws_gpu_pipeline_wait(uvhttp_ws_gpu_pipeline_t* p, int slot,
                                 const uvhttp_ws_frame_desc_t** desc,
                                 const uvhttp_ws_batch_summary_t** summary) {
     if (!p || slot < 0 || slot >= p->depth) return UVHTTP_WS_GPU_EINVAL;
     PipeSlot& s = p->slots[slot];
-    if (!s.busy) return UVHTTP_WS_GPU_EINVAL;
+    if (!s.busy || s.compact) return UVHTTP_WS_GPU_EINVAL;
     const hipError_t h = hipEventSynchronize(s.done_ev);
     s.busy = 0;
     if (desc) *desc = s.h_desc;
