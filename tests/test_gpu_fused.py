@@ -51,7 +51,8 @@ def engines(torch, request):
     1024- or 256-thread blocks) and the k_plan-first path; the fused path is forced for every
     frame size"""
     fused = _engine({"UVHTTP_WS_REC_SCAN": request.param[:8], "UVHTTP_WS_FUSED_MAX": str(1 << 40),
-                     "UVHTTP_WS_PLAN_WIDE": "0" if request.param.endswith("256") else "1"})
+                     "UVHTTP_WS_PLAN_WIDE": "0" if request.param.endswith("256") else "1",
+                     "UVHTTP_WS_DESC_EMIT": "0"})  # (k_desc_emit: test_gpu_desc_emit.py)
     plain = _engine({"UVHTTP_WS_FUSED": "0"})
     yield fused, plain
     fused.close()
@@ -172,7 +173,7 @@ def test_lookback_give_up_restores_everything(torch):
     n, plen = 300000, 250  # k_plan runs many blocks
     wire, _ = _batch(rng, n, plen)
     stride = wire.size // n
-    eng = _engine({"UVHTTP_WS_MAX_POLLS": "0", "UVHTTP_WS_REC_SCAN": "lookback"})
+    eng = _engine({"UVHTTP_WS_MAX_POLLS": "0", "UVHTTP_WS_REC_SCAN": "lookback", "UVHTTP_WS_DESC_EMIT": "0"})
     try:
         got = _decode(torch, eng, wire, n, stride, wire.size)
         s = got["summary"]

@@ -47,7 +47,7 @@ def test_stamps_batch_in_place(torch, calls):
     import uvhttp_amd as U
     eng = U.GpuEngine(0)
     try:
-        for plen, kern in ((65536, {"plan", "payload"}), (256, {"payload", "plan", "fixup"})):
+        for plen, kern in ((65536, {"plan", "payload"}), (256, {"payload", "sum_scan", "desc_emit"})):
             n = 4096 if plen == 65536 else 65536
             wire, stride = _wire(torch, U, eng, n, plen, frag=plen == 256)
             desc, summ = eng.alloc_outputs(n)

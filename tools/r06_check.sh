@@ -34,3 +34,21 @@ if has abstamps; then
   AB_STAMPS=1 timeout -k 10 300 python tools/ab_lib.py tree tree c3:inplace c2:inplace > ${O}_ab_stamps.txt 2>&1
   cat ${O}_ab_stamps.txt
 fi
+if has emit; then
+  tools/gpu_tests.sh r06${TAG}_pytest_emit.log tests/test_gpu_desc_emit.py tests/test_gpu_fused.py tests/test_gpu_stamps.py \
+    tests/test_gpu_engine.py tests/test_gpu_parity.py tests/test_gpu_summary_only.py
+fi
+if has c4; then
+  for m in inplace compact; do
+    timeout -k 10 300 python bench.py --steps 20 --warmup 5 --config c4 --mode $m --no-cpu-baseline \
+      > ${O}_bench_c4_$m.json 2>> ${O}_bench.err
+    python -c "import json,sys; d=json.load(open('${O}_bench_c4_$m.json')); t=d.get('device_timeline') or {}; print('$m', d['value'], d['ms_per_step'], t.get('kernels_us'), t.get('gaps_us'))"
+  done
+fi
+if has abemit; then
+  TH=uvhttp_amd/lib/libuvhttp_ws_amd_testhooks.so
+  for B in ${ABEMIT:-0}; do
+    AB_ENV_B=UVHTTP_WS_DESC_EMIT=$B timeout -k 10 300 python tools/ab_lib.py $TH $TH c4:inplace f2k:inplace > ${O}_ab_emit_$B.txt 2>&1
+    cat ${O}_ab_emit_$B.txt
+  done
+fi

@@ -244,7 +244,8 @@ struct Workspace {
     uint64_t* arena_first; // [n_arena_tiles]: tagged first data frame of the arena tile
     uint32_t* ctl;         // control words outside the clearable workspace (see kCtl*)
     void* recs;            // [n_frames] FrameRec: the fused stride path's parsed headers
-    void* parts;           // [n_frames / 4096 + 2] TilePart: summary-only decode, per k_sum_scan block
+    void* parts;           // [n_frames / 1024 + 2] TilePart: per k_sum_scan block (4 frames a thread)
+    uint8_t* info;         // [n_frames + 64]: info bytes beside the records (k_desc_emit's decode)
 };
 
 // ctl words (their own allocation, never cleared with the workspace)
@@ -1307,6 +1308,19 @@ __global__ __launch_bounds__(kBlock) void k_rec_resolve(BatchArgs a, uvhttp_ws_f
     plan_pass2<FPT>(a, desc, msgs, ws, i0, n, scan_combine(ws.block_excl[blockIdx.x], local), dv);
 }
 
+// A frame the call did not deliver (after the first failure, or every frame after a device
+// fault): SKIPPED, and no message id or MSG_END — the scan carries state past the first failure,
+// but nothing of it belongs to a delivered message, so every decode path leaves the same
+// descriptor (k_desc_emit never computes that state).  Word 5 = message, word 6 = opcode | flags
+// << 8 | header_size << 16 | status << 24.
+__device__ inline void skip_desc(uvhttp_ws_frame_desc_t* desc, uint64_t i) {
+    uint32_t* w = reinterpret_cast<uint32_t*>(desc + i);
+    const uint32_t w6 = w[6];
+    w[5] = 0u;
+    w[6] = (w6 & 0x00FFFFFFu & ~((uint32_t)UVHTTP_WS_FLAG_MSG_END << 8)) |
+           ((uint32_t)(uint8_t)UVHTTP_WS_FRAME_SKIPPED << 24);
+}
+
 // summary of a batch decode, after k_plan (one wave of k_finalize): E(nb) is
 // the exclusive scan value at the first failing frame (or the total)
 __device__ void write_summary(const BatchArgs& a, const uvhttp_ws_frame_desc_t* desc,
@@ -1374,7 +1388,7 @@ __device__ inline void finalize_frames(const BatchArgs& a, uvhttp_ws_frame_desc_
                                        uint32_t nb, bool controls = true) {
     const uint32_t i = blk * nthr + threadIdx.x;
     if (device_fault(a, ws)) {  // nothing was delivered (the payload pass saw first_bad = 0)
-        if (i < a.n) desc[i].status = UVHTTP_WS_FRAME_SKIPPED;
+        if (i < a.n) skip_desc(desc, i);
         if (blk == 0 && threadIdx.x == 0) {
             uvhttp_ws_batch_summary_t s;
             memset(&s, 0, sizeof(s));
@@ -1386,7 +1400,7 @@ __device__ inline void finalize_frames(const BatchArgs& a, uvhttp_ws_frame_desc_
         return;
     }
     if (i < a.n) {
-        if (i > nb) desc[i].status = UVHTTP_WS_FRAME_SKIPPED;
+        if (i > nb) skip_desc(desc, i);
         if (a.arena && i < nb && controls) {
             const uvhttp_ws_frame_desc_t d = desc[i];
             if (d.opcode > 2 && d.payload_len) {
@@ -1779,7 +1793,10 @@ __device__ inline void add_mask_rel(u32x4& m, int32_t r, int32_t ps, int32_t pe,
     m.w |= rk & lane_bytes(lo, hi, 3);
 }
 
-template <int BLOCK, int VPT, int AUX = 18, bool SUM = false>
+// what the payload pass leaves per frame: a 16-byte record (k_plan on records), an info byte
+// (the summary-only scan), or both (records for k_desc_emit, info bytes for its scan)
+constexpr int kLeaveRec = 0, kLeaveInfo = 1, kLeaveBoth = 2;
+template <int BLOCK, int VPT, int AUX = 18, int SUM = kLeaveRec>
 __global__ __launch_bounds__(BLOCK) void k_unmask_stride(BatchArgs a, Workspace ws, uint64_t tile_base) {
     StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_PAYLOAD, false, tile_base);
     constexpr uint64_t kT = (uint64_t)BLOCK * VPT * 16;
@@ -1842,8 +1859,12 @@ __global__ __launch_bounds__(BLOCK) void k_unmask_stride(BatchArgs a, Workspace 
         if (o >= t0) {  // (a frame that started earlier: its own tile's)
             // summary-only decode: one info byte per frame (k_sum_scan runs the state machine
             // on them); else the frame's 16-byte record for k_plan
-            if constexpr (SUM) reinterpret_cast<uint8_t*>(a.recs)[f] = info8_of(d);
-            else a.recs[f] = rec_of(d);
+            if constexpr (SUM == kLeaveInfo) {
+                reinterpret_cast<uint8_t*>(a.recs)[f] = info8_of(d);
+            } else {
+                a.recs[f] = rec_of(d);
+                if constexpr (SUM == kLeaveBoth) ws.info[f] = info8_of(d);
+            }
         }
         const bool ok = d.status == UVHTTP_WS_FRAME_OK;
         // speculative compact pass: the frame is uniform (a locally valid data frame with the
@@ -2041,7 +2062,7 @@ __global__ __launch_bounds__(kBlock) void k_fixup(BatchArgs a, uvhttp_ws_frame_d
     }
     if (nb >= n) return;  // every frame delivered: nothing to undo
     for (uint64_t i = tid; i < n; i += nthreads)
-        if (i > nb || fault) desc[i].status = UVHTTP_WS_FRAME_SKIPPED;
+        if (i > nb || fault) skip_desc(desc, i);
     const uint64_t wave = tid >> 6, nwaves = nthreads >> 6;
     for (uint64_t i = nb + wave; i < n; i += nwaves) {
         const FrameRec r = a.recs[i];
@@ -2115,20 +2136,40 @@ __device__ inline bool i8_uniform(uint32_t x, uint64_t D) {
     return (x & kI8Data) && kHm[x >> kI8HmShift] == D;
 }
 
-template <bool COMPACT>
+// the info byte of frame f from its 16-byte record (k_desc_emit's scan over the records)
+__device__ inline uint32_t info_of_rec(const FrameRec& r, uint64_t S, uint32_t f) {
+    uvhttp_ws_frame_desc_t d;
+    desc_of_rec(r, (uint64_t)f * S, d);
+    return info8_of(d);
+}
+
+template <bool COMPACT, uint32_t KIND = UVHTTP_WS_STAMP_PLAN, bool FROM_REC = false>
 __global__ __launch_bounds__(kBlock) void k_sum_scan(BatchArgs a, Workspace ws) {
     resolve_epoch(a, ws);
-    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_PLAN);
+    StampScope stamp_(a.stamp, a.epoch, KIND);
     const uint32_t n = a.n;
     const uint64_t S = a.frame_stride;
     const uint64_t D = S - a.spec_P;
     const uint8_t* info = reinterpret_cast<const uint8_t*>(a.recs);
     const uint32_t F0 = (blockIdx.x * kBlock + threadIdx.x) * kScanFpt;
-    // (info bytes past n are never used; the buffer holds at least n + 16)
-    const uint32_t w = F0 < n ? *reinterpret_cast<const uint32_t*>(info + F0) : 0u;
+    uint32_t w = 0u;
+    if constexpr (FROM_REC) {  // the info bytes rebuilt from the thread's 4 records (64 B)
+        FrameRec r[kScanFpt];
+#pragma unroll
+        for (uint32_t k = 0; k < kScanFpt; ++k) r[k] = a.recs[F0 + k < n ? F0 + k : n - 1];
+#pragma unroll
+        for (uint32_t k = 0; k < kScanFpt; ++k)
+            if (F0 + k < n) w |= info_of_rec(r[k], S, F0 + k) << (8 * k);
+    } else {
+        // (info bytes past n are never used; the buffer holds at least n + 16)
+        w = F0 < n ? *reinterpret_cast<const uint32_t*>(info + F0) : 0u;
+    }
     // the frame before this thread's first: the previous lane's last byte (lane 0: a load)
     const uint32_t up = __shfl_up(w, 1, 64);
-    uint32_t pb = (threadIdx.x & 63) ? up >> 24 : (F0 > 0 && F0 < n ? info[F0 - 1] : 0u);
+    uint32_t pb = (threadIdx.x & 63) ? up >> 24
+                                     : (F0 > 0 && F0 < n ? (FROM_REC ? info_of_rec(a.recs[F0 - 1], S, F0 - 1)
+                                                                     : (uint32_t)info[F0 - 1])
+                                                         : 0u);
     TilePart acc = part_identity();
     uint32_t sb = kNoFrame;  // compact: the thread's first delivered frame not at f * P
 #pragma unroll
@@ -2147,7 +2188,8 @@ __global__ __launch_bounds__(kBlock) void k_sum_scan(BatchArgs a, Workspace ws) 
                     break;
                 }
                 --g;
-                const uint32_t gi = g >= F0 ? (w >> (8 * (g - F0))) & 0xFF : info[g];
+                const uint32_t gi = g >= F0 ? (w >> (8 * (g - F0))) & 0xFF
+                                            : FROM_REC ? info_of_rec(a.recs[g], S, g) : (uint32_t)info[g];
                 if (!(gi & kI8Ok)) {  // a failure before f decides the batch anyway
                     p = 0u;
                     break;
@@ -2470,6 +2512,122 @@ __global__ __launch_bounds__(kBlock) void k_sum_msgs(BatchArgs a, Workspace ws, 
         md.opcode = bin ? 2 : 1;
         md.reserved = (uint32_t)P;
         msgs[nfin] = md;
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// Descriptor decode of a stride batch in place (d_desc != NULL, the summary-only bounds: stride
+// >= kSumMinStride, no message able to reach max_message_size), after k_unmask_stride<...,
+// kLeaveBoth> (16-byte record + info byte per frame, every locally valid frame unmasked) and
+// k_sum_scan (state machine on the info bytes, one part per 1024 frames, first_bad claimed):
+// k_desc_emit is fully parallel — no look-back, no block waits for another.  Block b takes the
+// 1024 frames of scan block b: message ids are the FIN data frames before a frame, i.e. the FIN
+// counts of parts [0, b) (a sum: each thread loads a few parts, as k_sum_msgs does) plus a block
+// scan; frames before first_bad are delivered (status OK, message id, MSG_END on a FIN data
+// frame), first_bad keeps its local status or fails the fragment check (src/uvhttp_websocket.c:
+// 964-996 — ERR_MESSAGE cannot fire under the bound), later frames are SKIPPED (skip_desc's
+// form).  Then k_fixup's work: block 0 the summary (parts in order, as k_sum_tail), and after a
+// failure each block re-masks its frames from first_bad on.  Replaces k_plan on the records + 
+// k_fixup for these batches (C4: 27 + 2 us and a look-back).
+// ------------------------------------------------------------------------------------
+// block-wide exclusive scan of a sum (uint64: four 16-bit counters packed, no carries between
+// them while each stays below 2^16) -> the thread's exclusive prefix and the block's total
+__device__ inline void block_exscan_u64(uint64_t v, uint64_t& ex, uint64_t& tot) {
+    __shared__ uint64_t s_w[kBlock / 64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint64_t inc = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t o = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += o;
+    }
+    if (lane == 63) s_w[wv] = inc;
+    __syncthreads();
+    uint64_t before = 0, all = 0;
+#pragma unroll
+    for (int k = 0; k < kBlock / 64; ++k) {
+        before += k < wv ? s_w[k] : 0u;
+        all += s_w[k];
+    }
+    ex = before + inc - v;
+    tot = all;
+}
+
+template <bool FROM_REC>
+__global__ __launch_bounds__(kBlock) void k_desc_emit(BatchArgs a, Workspace ws, uint32_t n_parts,
+                                                      uvhttp_ws_frame_desc_t* desc) {
+    resolve_epoch(a, ws);
+    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_DESC_EMIT);
+    const uint32_t n = a.n;
+    const uint64_t S = a.frame_stride;
+    const bool head = blockIdx.x == 0;
+    uvhttp_ws_frame_desc_t dl;
+    if (head && threadIdx.x == 0) (void)parse_one(a, n - 1, seg_info(a, n - 1, n), dl);
+    const uint32_t nb = first_bad_of(a, ws, n);
+    // the block's 1024 frames (scan block b's) in four rounds of 256: thread t takes frame
+    // B0 + 256 k + t, so every record load and descriptor store of a wave is contiguous (a
+    // thread per 4 consecutive frames stored 128-byte-strided descriptors: 15.6 us on C4)
+    const uint32_t B0 = blockIdx.x * kBlock * kScanFpt;
+    FrameRec r[kScanFpt];
+    uint32_t x[kScanFpt];
+    const uint32_t ilast = n - 1;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanFpt; ++k) {
+        const uint32_t f = B0 + k * kBlock + threadIdx.x;
+        r[k] = a.recs[f < n ? f : ilast];
+        if constexpr (!FROM_REC) x[k] = f < n ? ws.info[f] : 0u;
+    }
+    if constexpr (FROM_REC) {
+#pragma unroll
+        for (uint32_t k = 0; k < kScanFpt; ++k) x[k] = info_of_rec(r[k], S, B0 + k * kBlock + threadIdx.x);
+    }
+    uint32_t pre_fin = 0, pre_key = 0;
+    parts_fin_start(reinterpret_cast<const TilePart*>(ws.parts), blockIdx.x, pre_fin, pre_key);
+    // FIN data frames among the delivered ones, per round (16-bit fields)
+    uint64_t v = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanFpt; ++k) {
+        const uint32_t f = B0 + k * kBlock + threadIdx.x;
+        if (f < nb && f < n && (x[k] & kI8Data) && (x[k] & kI8Fin)) v += 1ull << (16 * k);
+    }
+    uint64_t ex, tot;
+    block_exscan_u64(v, ex, tot);
+    uint32_t round_base = pre_fin;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanFpt; ++k) {
+        const uint32_t f = B0 + k * kBlock + threadIdx.x;
+        if (f < n) {
+            uvhttp_ws_frame_desc_t d;
+            desc_of_rec(r[k], (uint64_t)f * S, d);
+            if (f < nb) {
+                if (is_data_op(d.opcode)) {
+                    d.message = round_base + (uint32_t)((ex >> (16 * k)) & 0xFFFFu);
+                    if (d.flags & UVHTTP_WS_FLAG_FIN) d.flags |= UVHTTP_WS_FLAG_MSG_END;
+                }
+            } else if (f == nb) {
+                if (d.status == UVHTTP_WS_FRAME_OK) d.status = UVHTTP_WS_FRAME_ERR_FRAGMENT;
+            } else {
+                d.status = UVHTTP_WS_FRAME_SKIPPED;
+            }
+            store_desc(desc, f, d);
+        }
+        round_base += (uint32_t)((tot >> (16 * k)) & 0xFFFFu);
+    }
+    if (head) {  // the summary (every block's part, in order), as k_sum_tail's block 0
+        const TilePart tp = parts_prefix(reinterpret_cast<const TilePart*>(ws.parts), n_parts);
+        if (threadIdx.x == 0) sum_summary(a, tp, dl, nb, false);
+    }
+    if (nb >= n) return;
+    // a failure: restore this block's frames the payload pass unmasked from first_bad on (a
+    // wave per frame, the records say which were locally valid)
+    const uint32_t b1 = B0 + kBlock * kScanFpt < n ? B0 + kBlock * kScanFpt : n;
+    const uint32_t wave = threadIdx.x >> 6;
+    for (uint32_t i = (nb > B0 ? nb : B0) + wave; i < b1; i += kBlock / 64) {
+        const FrameRec rr = a.recs[i];
+        if (rr.status != UVHTTP_WS_FRAME_OK || rr.payload_len == 0) continue;
+        uvhttp_ws_frame_desc_t d;
+        desc_of_rec(rr, (uint64_t)i * S, d);
+        remask_range(a.wire, d.payload_off, d.payload_off + d.payload_len, d.masking_key);
     }
 }
 
@@ -4750,6 +4908,7 @@ struct uvhttp_ws_gpu_engine {
     hipStream_t last_stream;   // stream of the previous call (calls are serialised on it)
     int have_last;
     int pool_ok;               // the device has the stream-ordered allocator (scratch_grow)
+    int desc_emit;             // stride batches with descriptors: k_desc_emit (not k_plan on records)
     hipEvent_t order_ev;       // orders a call on a new stream after the previous stream's work
     hipEvent_t ev[2 * 1024];
     int ev_created;
@@ -4824,6 +4983,7 @@ static void experiment_knobs(uvhttp_ws_gpu_engine_t* e) {
     if (const char* sm = getenv("UVHTTP_WS_SPEC_MAX")) e->spec_max_avg = strtoull(sm, nullptr, 10);
     if (const char* fa = getenv("UVHTTP_WS_FUSED_AUX")) e->fused_aux = atoi(fa);
     if (const char* sf = getenv("UVHTTP_WS_SUMMARY_FAST")) e->sum_fast = atoi(sf) != 0;
+    if (const char* de = getenv("UVHTTP_WS_DESC_EMIT")) e->desc_emit = atoi(de);
     if (const char* tl = getenv("UVHTTP_WS_TILE")) {  // payload tile shape "BxV" (0x0 = auto)
         int tb = 0, tv = 0;
         if (sscanf(tl, "%dx%d", &tb, &tv) == 2) (void)uvhttp_ws_gpu_engine_set_tile(e, tb, tv);  // (validated)
@@ -4868,6 +5028,7 @@ int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out) {
     e->fused_aux = 18;
     e->fixup_blocks = 1024;
     e->sum_fast = 1;
+    e->desc_emit = 1;
     {
         int prev = 0;
         (void)hipGetDevice(&prev);
@@ -5017,7 +5178,8 @@ static int reserve_ws(uvhttp_ws_gpu_engine_t* e, uint32_t max_frames, uint64_t m
     size_t off_arena = align_up(off_bad + 16, 256);
     size_t off_recs = align_up(off_arena + at * sizeof(uint64_t), 256);
     size_t off_parts = align_up(off_recs + (size_t)fr * 16, 256);
-    size_t bytes = align_up(off_parts + ((size_t)fr / (kBlock * kScanFpt) + 2) * sizeof(TilePart), 256);
+    size_t off_info = align_up(off_parts + ((size_t)fr / (kBlock * kScanFpt) + 2) * sizeof(TilePart), 256);
+    size_t bytes = align_up(off_info + (size_t)fr + 64, 256);
     int prev = 0;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(e->device);
@@ -5044,6 +5206,7 @@ static int reserve_ws(uvhttp_ws_gpu_engine_t* e, uint32_t max_frames, uint64_t m
     e->ws.arena_first = (uint64_t*)(b + off_arena);
     e->ws.recs = b + off_recs;
     e->ws.parts = b + off_parts;
+    e->ws.info = (uint8_t*)(b + off_info);
     e->ws.ctl = e->ctl;
     e->ws_bytes = bytes;
     e->cap_frames = fr;
@@ -5523,12 +5686,47 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
         // bound below) and leaves one TilePart per tile; k_sum_tail writes the summary and undoes
         // a failure.  No records, no k_plan, no descriptors.
         const bool sum_fast = !d_desc && fb == 256 && fv == 4 && e->fused_aux == 18 && sum_ok(e, b);
+        // descriptors under the same bounds: records + info bytes, the info-byte scan, then the
+        // parallel descriptor pass (k_desc_emit) instead of k_plan on the records + k_fixup
+        const bool desc_emit = d_desc && e->desc_emit && fb == 256 && fv == 4 && e->fused_aux == 18 &&
+                               sum_ok(e, b);
+        if (desc_emit) {
+            // (desc_emit 2: no info bytes — the scan and k_desc_emit rebuild them from the records)
+            const bool from_rec = e->desc_emit == 2;
+            const int stk = timing_begin(e, s);
+            for (uint64_t tb = 0; tb < f_tiles; tb += f_max) {
+                const uint32_t grid_p = (uint32_t)((f_tiles - tb) < f_max ? (f_tiles - tb) : f_max);
+                if (from_rec)
+                    hipLaunchKernelGGL((k_unmask_stride<256, 4, 18, kLeaveRec>), dim3(grid_p), dim3(256), 0, s, a,
+                                       e->ws, tb);
+                else
+                    hipLaunchKernelGGL((k_unmask_stride<256, 4, 18, kLeaveBoth>), dim3(grid_p), dim3(256), 0, s, a,
+                                       e->ws, tb);
+            }
+            timing_end(e, stk, s);
+            const uint32_t n_parts = (a.n + kBlock * kScanFpt - 1) / (kBlock * kScanFpt);
+            if (from_rec) {
+                hipLaunchKernelGGL((k_sum_scan<false, UVHTTP_WS_STAMP_SUM_SCAN, true>), dim3(n_parts), dim3(kBlock),
+                                   0, s, a, e->ws);
+                hipLaunchKernelGGL(k_desc_emit<true>, dim3(n_parts), dim3(kBlock), 0, s, a, e->ws, n_parts, d_desc);
+            } else {
+                BatchArgs ai = a;  // the scan reads the info bytes
+                ai.recs = reinterpret_cast<FrameRec*>(e->ws.info);
+                hipLaunchKernelGGL((k_sum_scan<false, UVHTTP_WS_STAMP_SUM_SCAN>), dim3(n_parts), dim3(kBlock), 0,
+                                   s, ai, e->ws);
+                hipLaunchKernelGGL(k_desc_emit<false>, dim3(n_parts), dim3(kBlock), 0, s, a, e->ws, n_parts, d_desc);
+            }
+            hipError_t hs = hipGetLastError();
+            if (prev != e->device) (void)hipSetDevice(prev);
+            if (hs != hipSuccess) return set_err(e, UVHTTP_WS_GPU_ELAUNCH, "launch", hs);
+            return UVHTTP_WS_GPU_OK;
+        }
         if (sum_fast) {
             a.recs = reinterpret_cast<FrameRec*>(e->ws.recs);  // (the info bytes: 1 per frame)
             const int stk = timing_begin(e, s);
             for (uint64_t tb = 0; tb < f_tiles; tb += f_max) {
                 const uint32_t grid_p = (uint32_t)((f_tiles - tb) < f_max ? (f_tiles - tb) : f_max);
-                hipLaunchKernelGGL((k_unmask_stride<256, 4, 18, true>), dim3(grid_p), dim3(256), 0, s, a,
+                hipLaunchKernelGGL((k_unmask_stride<256, 4, 18, kLeaveInfo>), dim3(grid_p), dim3(256), 0, s, a,
                                    e->ws, tb);
             }
             timing_end(e, stk, s);
@@ -5620,7 +5818,7 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
         for (uint64_t tb = 0; tb < s_tiles; tb += (1ull << 24)) {
             const uint32_t grid_s = (uint32_t)((s_tiles - tb) < (1ull << 24) ? (s_tiles - tb) : (1ull << 24));
             if (sum_c)
-                hipLaunchKernelGGL((k_unmask_stride<256, 4, kSpecCompact, true>), dim3(grid_s), dim3(256), 0, s, a,
+                hipLaunchKernelGGL((k_unmask_stride<256, 4, kSpecCompact, kLeaveInfo>), dim3(grid_s), dim3(256), 0, s, a,
                                    e->ws, tb);
             else
                 hipLaunchKernelGGL((k_unmask_stride<256, 4, kSpecCompact>), dim3(grid_s), dim3(256), 0, s, a, e->ws, tb);
