@@ -27,7 +27,7 @@ def torch():
     return t
 
 
-@pytest.fixture(scope="module", params=["1", "2"])
+@pytest.fixture(scope="module", params=["2", "1"])
 def engines(torch, request):
     """k_desc_emit with info bytes from the payload pass (1) or rebuilt from the records (2),
     k_plan on the records, the k_plan-first path"""
@@ -154,3 +154,79 @@ def test_c4_full_size(torch, engines):
         if bad is not None:
             w[bad * stride] |= 0x40  # RSV1
         _check(torch, engines[:2], w, n, stride, mm=256 << 20)
+
+
+@pytest.fixture(scope="module", params=["2", "1"])
+def compact_engines(torch, request):
+    """compact decodes with descriptors: k_sum_msgs writing them (info bytes rebuilt from the
+    records, 2, or left by the pass, 1), the speculative pass + k_plan on records + k_spec_fix
+    (UVHTTP_WS_DESC_EMIT=0), k_plan first + the scatter (UVHTTP_WS_SPEC=0)"""
+    e = [_engine({"UVHTTP_WS_DESC_EMIT": request.param}), _engine({"UVHTTP_WS_DESC_EMIT": "0"}),
+         _engine({"UVHTTP_WS_SPEC": "0"})]
+    e[0].set_stamps(True)
+    yield e
+    for x in e:
+        x.close()
+
+
+def _compact_all(torch, engines, wire, n, stride, mm=0, fast=None):
+    ref = _oracle.decode_batch(wire, n, stride=stride, max_frame_size=MF, max_message_size=mm,
+                               compact=True, arena_cap=wire.size + 64)
+    outs = []
+    engines[0].read_stamps()
+    for e in engines:
+        d = torch.from_numpy(np.concatenate([wire, np.zeros(64, np.uint8)])).to("cuda")
+        arena = torch.zeros(wire.size + 64, dtype=torch.uint8, device="cuda")
+        desc, msgs, summ = e.decode_compact(d, n, arena, stride=stride, wire_len=wire.size,
+                                            max_frame_size=MF, max_message_size=mm)
+        torch.cuda.synchronize()
+        s = e.read_summary(summ)
+        outs.append(dict(s=s, desc=e.read_desc(desc, n), msgs=e.read_msgs(msgs, s["n_messages"]),
+                         arena=arena[: s["arena_bytes"]].cpu().numpy(), wire=d[: wire.size].cpu().numpy()))
+    kinds = {r[1] for r in engines[0].read_stamps()}
+    if fast is not None:
+        assert (("fixup" not in kinds) and ("sum_scan" in kinds)) == fast, kinds
+    for k, o in enumerate(outs):
+        assert o["s"] == ref["summary"], (k, o["s"], ref["summary"])
+        assert np.array_equal(o["desc"]["status"], ref["status"]), k
+        assert np.array_equal(o["wire"], ref["wire"]), k
+        assert np.array_equal(o["arena"], ref["arena"][: o["s"]["arena_bytes"]]), k
+        assert np.array_equal(o["msgs"]["arena_off"], ref["msg_off"]), k
+        assert np.array_equal(o["msgs"]["len"], ref["msg_len"]), k
+    for k in (1, 2):
+        diff = np.nonzero(outs[0]["desc"] != outs[k]["desc"])[0]
+        assert diff.size == 0, (k, diff[:4], outs[0]["desc"][diff[:2]], outs[k]["desc"][diff[:2]])
+        assert np.array_equal(outs[0]["msgs"], outs[k]["msgs"]), k
+    return ref
+
+
+@pytest.mark.parametrize("plen", [132, 200, 256, 1000, 2000])
+def test_compact_with_descriptors(torch, compact_engines, plen):
+    """uniform batches (fast: the speculation holds), failures part-way (the frames after them
+    keep their wire payload offsets on every path), a control frame last (the fall-back)"""
+    rng = random.Random(plen + 1)
+    n = max(3, min(20000, (4 << 20) // (plen + 8)))
+    stride = (2 if plen < 126 else 4) + 4 + plen
+    for p_frag in (0.0, 0.5, 1.0):
+        _compact_all(torch, compact_engines, _frag_batch(rng, n, plen, p_frag), n, stride, fast=True)
+    for where in (0, 1023, n // 2, n - 1):
+        def tw(i, f, fin, open_msg, where=where):
+            if i != where:
+                return f, fin
+            b = bytearray(f)
+            b[0] |= 0x20  # RSV2
+            return bytes(b), fin
+        _compact_all(torch, compact_engines, _frag_batch(rng, n, plen, 0.4, tw), n, stride, fast=True)
+
+    def ctl_last(i, f, fin, open_msg):
+        return (_frame(9, 1, b"ping", rng.randbytes(4)), True) if i == n - 1 else (f, fin)
+    _compact_all(torch, compact_engines, _frag_batch(rng, n, plen, 0.4, ctl_last), n, stride, fast=False)
+
+
+def test_compact_c4_full_size(torch, compact_engines):
+    """C4 compact with descriptors: one 256 MiB message of 1 048 576 fragments"""
+    import uvhttp_amd as U
+    n, plen = 1048576, 256
+    stride = U.gen_frame_stride(plen)
+    ow, _ = _oracle.gen_frames(n, plen, 7, fragmented=True, opcode0=2)
+    _compact_all(torch, compact_engines[:2] + compact_engines[1:2], ow, n, stride, mm=256 << 20, fast=True)

@@ -35,7 +35,7 @@ if has abstamps; then
   cat ${O}_ab_stamps.txt
 fi
 if has emit; then
-  tools/gpu_tests.sh r06${TAG}_pytest_emit.log tests/test_gpu_desc_emit.py tests/test_gpu_fused.py tests/test_gpu_stamps.py \
+  tools/gpu_tests.sh r06${TAG}_pytest_emit.log tests/test_gpu_desc_emit.py tests/test_gpu_spec_compact.py tests/test_gpu_summary_compact.py tests/test_gpu_deliver_messages.py tests/test_gpu_fused.py tests/test_gpu_stamps.py \
     tests/test_gpu_engine.py tests/test_gpu_parity.py tests/test_gpu_summary_only.py
 fi
 if has c4; then
@@ -48,7 +48,13 @@ fi
 if has abemit; then
   TH=uvhttp_amd/lib/libuvhttp_ws_amd_testhooks.so
   for B in ${ABEMIT:-0}; do
-    AB_ENV_B=UVHTTP_WS_DESC_EMIT=$B timeout -k 10 300 python tools/ab_lib.py $TH $TH c4:inplace f2k:inplace > ${O}_ab_emit_$B.txt 2>&1
+    AB_ENV_B=UVHTTP_WS_DESC_EMIT=$B timeout -k 10 300 python tools/ab_lib.py $TH $TH ${ABCFG:-c4:inplace f2k:inplace} > ${O}_ab_emit_$B.txt 2>&1
     cat ${O}_ab_emit_$B.txt
   done
+fi
+if has abfused; then
+  TH=uvhttp_amd/lib/libuvhttp_ws_amd_testhooks.so
+  AB_ENV_B=UVHTTP_WS_FUSED_MAX=${FMAX:-8192} timeout -k 10 300 python tools/ab_lib.py $TH $TH c2:inplace c2:inplace_nd \
+    c2:compact c2:compact_nd > ${O}_ab_fused_max.txt 2>&1
+  cat ${O}_ab_fused_max.txt
 fi

@@ -1313,12 +1313,20 @@ __global__ __launch_bounds__(kBlock) void k_rec_resolve(BatchArgs a, uvhttp_ws_f
 // but nothing of it belongs to a delivered message, so every decode path leaves the same
 // descriptor (k_desc_emit never computes that state).  Word 5 = message, word 6 = opcode | flags
 // << 8 | header_size << 16 | status << 24.
-__device__ inline void skip_desc(uvhttp_ws_frame_desc_t* desc, uint64_t i) {
+// A compact decode's data frame keeps its payload in the wire then too (payload_off = the wire
+// offset parse_hdr gives; the scan past the failure may have assigned an arena offset).
+__device__ inline void skip_desc(const BatchArgs& a, uvhttp_ws_frame_desc_t* desc, uint64_t i) {
     uint32_t* w = reinterpret_cast<uint32_t*>(desc + i);
     const uint32_t w6 = w[6];
     w[5] = 0u;
     w[6] = (w6 & 0x00FFFFFFu & ~((uint32_t)UVHTTP_WS_FLAG_MSG_END << 8)) |
            ((uint32_t)(uint8_t)UVHTTP_WS_FRAME_SKIPPED << 24);
+    if (a.arena) {
+        const uint64_t o = frame_start(a, (uint32_t)i);
+        const uint64_t po = w[7] ? o + ((w6 >> 16) & 0xFFu) + (((w6 >> 8) & UVHTTP_WS_FLAG_MASK) ? 4u : 0u) : o;
+        w[0] = (uint32_t)po;
+        w[1] = (uint32_t)(po >> 32);
+    }
 }
 
 // summary of a batch decode, after k_plan (one wave of k_finalize): E(nb) is
@@ -1388,7 +1396,7 @@ __device__ inline void finalize_frames(const BatchArgs& a, uvhttp_ws_frame_desc_
                                        uint32_t nb, bool controls = true) {
     const uint32_t i = blk * nthr + threadIdx.x;
     if (device_fault(a, ws)) {  // nothing was delivered (the payload pass saw first_bad = 0)
-        if (i < a.n) skip_desc(desc, i);
+        if (i < a.n) skip_desc(a, desc, i);
         if (blk == 0 && threadIdx.x == 0) {
             uvhttp_ws_batch_summary_t s;
             memset(&s, 0, sizeof(s));
@@ -1400,7 +1408,7 @@ __device__ inline void finalize_frames(const BatchArgs& a, uvhttp_ws_frame_desc_
         return;
     }
     if (i < a.n) {
-        if (i > nb) skip_desc(desc, i);
+        if (i > nb) skip_desc(a, desc, i);
         if (a.arena && i < nb && controls) {
             const uvhttp_ws_frame_desc_t d = desc[i];
             if (d.opcode > 2 && d.payload_len) {
@@ -2062,7 +2070,7 @@ __global__ __launch_bounds__(kBlock) void k_fixup(BatchArgs a, uvhttp_ws_frame_d
     }
     if (nb >= n) return;  // every frame delivered: nothing to undo
     for (uint64_t i = tid; i < n; i += nthreads)
-        if (i > nb || fault) skip_desc(desc, i);
+        if (i > nb || fault) skip_desc(a, desc, i);
     const uint64_t wave = tid >> 6, nwaves = nthreads >> 6;
     for (uint64_t i = nb + wave; i < n; i += nwaves) {
         const FrameRec r = a.recs[i];
@@ -2350,6 +2358,29 @@ __device__ inline void block_exscan_sum_max(uint32_t c, uint32_t l, uint32_t& ec
     el = xl > bl ? xl : bl;
 }
 
+// block-wide exclusive scan of a sum (uint64: four 16-bit counters packed, no carries between
+// them while each stays below 2^16) -> the thread's exclusive prefix and the block's total
+__device__ inline void block_exscan_u64(uint64_t v, uint64_t& ex, uint64_t& tot) {
+    __shared__ uint64_t s_w[kBlock / 64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint64_t inc = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t o = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += o;
+    }
+    if (lane == 63) s_w[wv] = inc;
+    __syncthreads();
+    uint64_t before = 0, all = 0;
+#pragma unroll
+    for (int k = 0; k < kBlock / 64; ++k) {
+        before += k < wv ? s_w[k] : 0u;
+        all += s_w[k];
+    }
+    ex = before + inc - v;
+    tot = all;
+}
+
 // what a block of k_sum_msgs needs of the scan parts before it: FIN frames (sum) and the
 // latest start with its BINARY bit as ((ls + 1) << 1 | bin) (max; 0 = none) — commutative, so
 // each thread loads the parts t, t + kBlock, ... (one 16-byte load each: nfin, ls, last, bits)
@@ -2396,8 +2427,13 @@ __device__ inline void parts_fin_start(const TilePart* parts, uint32_t hi, uint3
 // count, the latest start and whether the last delivered frame left its message open.
 // (One launch after the scan; a single-block tail leaving ordered prefixes + this kernel took
 // 6.4 + 2.0 us and a boundary on C4, every block combining full parts in order 9.2 us.)
+// DESC (compact decode with descriptors, the payload pass leaving 16-byte records: FROM_REC):
+// every block also writes its 1024 frames' descriptors as k_desc_emit does, data frames at their
+// arena offset f * P; a call whose speculation failed has them rewritten by the fall-back.
+template <bool FROM_REC = false, bool DESC = false>
 __global__ __launch_bounds__(kBlock) void k_sum_msgs(BatchArgs a, Workspace ws, uint32_t n_parts,
-                                                     uvhttp_ws_message_desc_t* msgs) {
+                                                     uvhttp_ws_message_desc_t* msgs,
+                                                     uvhttp_ws_frame_desc_t* desc = nullptr) {
     resolve_epoch(a, ws);
     StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_FINALIZE);
     const uint32_t n = a.n;
@@ -2409,9 +2445,24 @@ __global__ __launch_bounds__(kBlock) void k_sum_msgs(BatchArgs a, Workspace ws, 
     const uint32_t nb = first_bad_of(a, ws, n);
     const uint32_t sb = tag_get(*ws.spec_bad, a.epoch, n);
     const uint32_t end = nb < n - 1 ? nb : n - 1;  // frames [0, end) here, the last one is block 0's
-    const uint8_t* info = reinterpret_cast<const uint8_t*>(a.recs);
+    // (DESC without FROM_REC: records in a.recs, the payload pass's info bytes in ws.info)
+    const uint8_t* info_b = (DESC && !FROM_REC) ? ws.info : reinterpret_cast<const uint8_t*>(a.recs);
+    auto info_at = [&](uint32_t f) -> uint32_t {
+        if constexpr (FROM_REC) return info_of_rec(a.recs[f], S, f);
+        else return info_b[f];
+    };
     const uint32_t F0 = (blockIdx.x * kBlock + threadIdx.x) * kScanFpt;
-    const uint32_t w = F0 < n ? *reinterpret_cast<const uint32_t*>(info + F0) : 0u;
+    uint32_t w = 0u;
+    if constexpr (FROM_REC) {
+        FrameRec r4[kScanFpt];
+#pragma unroll
+        for (uint32_t k = 0; k < kScanFpt; ++k) r4[k] = a.recs[F0 + k < n ? F0 + k : n - 1];
+#pragma unroll
+        for (uint32_t k = 0; k < kScanFpt; ++k)
+            if (F0 + k < n) w |= info_of_rec(r4[k], S, F0 + k) << (8 * k);
+    } else {
+        w = F0 < n ? *reinterpret_cast<const uint32_t*>(info_b + F0) : 0u;
+    }
     constexpr uint32_t kPartFrames = kBlock * kScanFpt;
     // block 0: the parts of every frame before `end` (a part stops at its first failure)
     const uint32_t hi = head ? (end / kPartFrames + 1 < n_parts ? end / kPartFrames + 1 : n_parts) : blockIdx.x;
@@ -2442,7 +2493,7 @@ __global__ __launch_bounds__(kBlock) void k_sum_msgs(BatchArgs a, Workspace ws, 
             if (x & kI8Fin) {
                 // the start's opcode: its info byte, or — before the block — the prefix's bit
                 const uint32_t xs = ls >= F0 ? (w >> (8 * (ls - F0))) & 0xFF
-                                    : ls == pre_ls ? ((pre_key & 1u) ? kI8Bin : 0u) : info[ls];
+                                    : ls == pre_ls ? ((pre_key & 1u) ? kI8Bin : 0u) : info_at(ls);
                 uvhttp_ws_message_desc_t md;
                 md.arena_off = (uint64_t)ls * P;
                 md.len = (uint64_t)(f - ls + 1) * P;
@@ -2452,6 +2503,51 @@ __global__ __launch_bounds__(kBlock) void k_sum_msgs(BatchArgs a, Workspace ws, 
                 md.reserved = 0;
                 msgs[m++] = md;
             }
+        }
+    }
+    if constexpr (DESC) {  // (strided rounds, as k_desc_emit: contiguous loads and stores)
+        const uint32_t B0 = blockIdx.x * kBlock * kScanFpt;
+        FrameRec r[kScanFpt];
+        uint32_t x[kScanFpt];
+#pragma unroll
+        for (uint32_t k = 0; k < kScanFpt; ++k) {
+            const uint32_t f = B0 + k * kBlock + threadIdx.x;
+            r[k] = a.recs[f < n ? f : n - 1];
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kScanFpt; ++k) {
+            const uint32_t f = B0 + k * kBlock + threadIdx.x;
+            x[k] = f < n ? (FROM_REC ? info_of_rec(r[k], S, f) : (uint32_t)info_b[f]) : 0u;
+        }
+        uint64_t v = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kScanFpt; ++k) {
+            const uint32_t f = B0 + k * kBlock + threadIdx.x;
+            if (f < nb && f < n && (x[k] & kI8Data) && (x[k] & kI8Fin)) v += 1ull << (16 * k);
+        }
+        uint64_t ex, tot;
+        block_exscan_u64(v, ex, tot);
+        uint32_t round_base = head ? 0u : tot_fin;  // (tot_fin: FIN frames of parts [0, b))
+#pragma unroll
+        for (uint32_t k = 0; k < kScanFpt; ++k) {
+            const uint32_t f = B0 + k * kBlock + threadIdx.x;
+            if (f < n) {
+                uvhttp_ws_frame_desc_t d;
+                desc_of_rec(r[k], (uint64_t)f * S, d);
+                if (f < nb) {
+                    if (is_data_op(d.opcode)) {
+                        d.message = round_base + (uint32_t)((ex >> (16 * k)) & 0xFFFFu);
+                        d.payload_off = (uint64_t)f * P;
+                        if (d.flags & UVHTTP_WS_FLAG_FIN) d.flags |= UVHTTP_WS_FLAG_MSG_END;
+                    }
+                } else if (f == nb) {
+                    if (d.status == UVHTTP_WS_FRAME_OK) d.status = UVHTTP_WS_FRAME_ERR_FRAGMENT;
+                } else {
+                    d.status = UVHTTP_WS_FRAME_SKIPPED;
+                }
+                store_desc(desc, f, d);
+            }
+            round_base += (uint32_t)((tot >> (16 * k)) & 0xFFFFu);
         }
     }
     if (!head || threadIdx.x != 0) return;
@@ -2475,7 +2571,7 @@ __global__ __launch_bounds__(kBlock) void k_sum_msgs(BatchArgs a, Workspace ws, 
         (void)parse_one(a, nb, seg_info(a, nb, n), d);
         sm.first_status = d.status != UVHTTP_WS_FRAME_OK ? d.status : UVHTTP_WS_FRAME_ERR_FRAGMENT;
         sm.consumed_bytes = (uint64_t)nb * S;
-        open = nb > 0 && !(info[nb - 1] & kI8Fin);
+        open = nb > 0 && !(info_at(nb - 1) & kI8Fin);
     } else {  // every frame, the last one (a uniform data frame) included
         nd = n;
         sm.first_status = 0;
@@ -2530,29 +2626,6 @@ __global__ __launch_bounds__(kBlock) void k_sum_msgs(BatchArgs a, Workspace ws, 
 // failure each block re-masks its frames from first_bad on.  Replaces k_plan on the records + 
 // k_fixup for these batches (C4: 27 + 2 us and a look-back).
 // ------------------------------------------------------------------------------------
-// block-wide exclusive scan of a sum (uint64: four 16-bit counters packed, no carries between
-// them while each stays below 2^16) -> the thread's exclusive prefix and the block's total
-__device__ inline void block_exscan_u64(uint64_t v, uint64_t& ex, uint64_t& tot) {
-    __shared__ uint64_t s_w[kBlock / 64];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint64_t inc = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint64_t o = __shfl_up(inc, d, 64);
-        if (lane >= d) inc += o;
-    }
-    if (lane == 63) s_w[wv] = inc;
-    __syncthreads();
-    uint64_t before = 0, all = 0;
-#pragma unroll
-    for (int k = 0; k < kBlock / 64; ++k) {
-        before += k < wv ? s_w[k] : 0u;
-        all += s_w[k];
-    }
-    ex = before + inc - v;
-    tot = all;
-}
-
 template <bool FROM_REC>
 __global__ __launch_bounds__(kBlock) void k_desc_emit(BatchArgs a, Workspace ws, uint32_t n_parts,
                                                       uvhttp_ws_frame_desc_t* desc) {
@@ -5028,7 +5101,10 @@ int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out) {
     e->fused_aux = 18;
     e->fixup_blocks = 1024;
     e->sum_fast = 1;
-    e->desc_emit = 1;
+    // 3: in place the scan and k_desc_emit rebuild the info bytes from the records (C4 step 114.0
+    // vs 115.9 us with them left by the payload pass, profiles/r06h_desc_emit_ab_*.txt); compact
+    // the speculative pass leaves them (123.9 vs 126.9 us, profiles/r06j_desc_emit_compact_ab.txt)
+    e->desc_emit = 3;
     {
         int prev = 0;
         (void)hipGetDevice(&prev);
@@ -5691,8 +5767,8 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
         const bool desc_emit = d_desc && e->desc_emit && fb == 256 && fv == 4 && e->fused_aux == 18 &&
                                sum_ok(e, b);
         if (desc_emit) {
-            // (desc_emit 2: no info bytes — the scan and k_desc_emit rebuild them from the records)
-            const bool from_rec = e->desc_emit == 2;
+            // (desc_emit >= 2: no info bytes — the scan and k_desc_emit rebuild them from the records)
+            const bool from_rec = e->desc_emit >= 2;
             const int stk = timing_begin(e, s);
             for (uint64_t tb = 0; tb < f_tiles; tb += f_max) {
                 const uint32_t grid_p = (uint32_t)((f_tiles - tb) < f_max ? (f_tiles - tb) : f_max);
@@ -5813,11 +5889,18 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
         // frame, another length, ...) is decoded again by k_plan + k_spec_fix, which otherwise
         // return at once (ctl[kCtlGate])
         const bool sum_c = no_desc && sum_ok(e, b) && arena_cap / spec_p >= a.n;
+        // with descriptors under the same bounds: the records pass, the scan and k_sum_msgs
+        // rebuilding the info bytes from the records, k_sum_msgs also writing the descriptors
+        const bool desc_c = !no_desc && e->desc_emit && sum_ok(e, b) && arena_cap / spec_p >= a.n;
         if (sum_c) a.recs = reinterpret_cast<FrameRec*>(e->ws.recs);  // (the info bytes)
         const int stk = timing_begin(e, s);
+        const bool both = desc_c && e->desc_emit != 2;  // (records + info bytes from the pass)
         for (uint64_t tb = 0; tb < s_tiles; tb += (1ull << 24)) {
             const uint32_t grid_s = (uint32_t)((s_tiles - tb) < (1ull << 24) ? (s_tiles - tb) : (1ull << 24));
-            if (sum_c)
+            if (both)
+                hipLaunchKernelGGL((k_unmask_stride<256, 4, kSpecCompact, kLeaveBoth>), dim3(grid_s), dim3(256), 0,
+                                   s, a, e->ws, tb);
+            else if (sum_c)
                 hipLaunchKernelGGL((k_unmask_stride<256, 4, kSpecCompact, kLeaveInfo>), dim3(grid_s), dim3(256), 0, s, a,
                                    e->ws, tb);
             else
@@ -5827,13 +5910,33 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
         if (sum_c) {
             const uint32_t n_parts = (a.n + kBlock * kScanFpt - 1) / (kBlock * kScanFpt);
             hipLaunchKernelGGL(k_sum_scan<true>, dim3(n_parts), dim3(kBlock), 0, s, a, e->ws);
-            hipLaunchKernelGGL(k_sum_msgs, dim3(n_parts), dim3(kBlock), 0, s, a, e->ws, n_parts, d_msgs);
+            hipLaunchKernelGGL(k_sum_msgs<>, dim3(n_parts), dim3(kBlock), 0, s, a, e->ws, n_parts, d_msgs,
+                               nullptr);
             a.recs = nullptr;  // the fallback's k_plan gathers the headers
             a.gate = 1;
+        } else if (desc_c) {
+            const uint32_t n_parts = (a.n + kBlock * kScanFpt - 1) / (kBlock * kScanFpt);
+            if (both) {
+                BatchArgs ai = a;  // the scan reads the info bytes
+                ai.recs = reinterpret_cast<FrameRec*>(e->ws.info);
+                hipLaunchKernelGGL((k_sum_scan<true, UVHTTP_WS_STAMP_SUM_SCAN>), dim3(n_parts), dim3(kBlock), 0, s,
+                                   ai, e->ws);
+                hipLaunchKernelGGL((k_sum_msgs<false, true>), dim3(n_parts), dim3(kBlock), 0, s, a, e->ws, n_parts,
+                                   d_msgs, d_desc);
+            } else {
+                hipLaunchKernelGGL((k_sum_scan<true, UVHTTP_WS_STAMP_SUM_SCAN, true>), dim3(n_parts), dim3(kBlock),
+                                   0, s, a, e->ws);
+                hipLaunchKernelGGL((k_sum_msgs<true, true>), dim3(n_parts), dim3(kBlock), 0, s, a, e->ws, n_parts,
+                                   d_msgs, d_desc);
+            }
+            a.gate = 1;  // (the fall-back's k_plan reads the same records)
         }
         launch_plan(e, a, a.n, d_desc, d_msgs, s);
+        // (gated — it returns at once unless the speculation failed — a smaller grid: the
+        // no-op launch costs less, the rare fall-back strides over more frames per block)
         const uint32_t nblk = (a.n + kBlock - 1) / kBlock;
-        hipLaunchKernelGGL(k_spec_fix, dim3(nblk < 1024 ? nblk : 1024), dim3(kBlock), 0, s, a, d_desc,
+        const uint32_t fix_max = a.gate ? 256u : 1024u;
+        hipLaunchKernelGGL(k_spec_fix, dim3(nblk < fix_max ? nblk : fix_max), dim3(kBlock), 0, s, a, d_desc,
                            e->ws, s_tiles);
         const hipError_t hs = hipGetLastError();
         if (prev != e->device) (void)hipSetDevice(prev);
