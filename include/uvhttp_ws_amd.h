@@ -364,6 +364,8 @@ int uvhttp_ws_gpu_engine_sync(uvhttp_ws_gpu_engine_t* eng, void* stream);
 #define UVHTTP_WS_STAMP_DESC_EMIT 13  /* k_desc_emit (stride batches with descriptors) */
 #define UVHTTP_WS_STAMP_SUM_SCAN 14   /* k_sum_scan ahead of k_desc_emit (the summary-only
                                          decodes' k_sum_scan stamps as PLAN) */
+#define UVHTTP_WS_STAMP_SPEC_PLAN 15  /* k_sspec_plan (speculative stream decode; its pass
+                                         stamps as PAYLOAD, k_sspec_emit as STREAM_DESC) */
 typedef struct {
     uint32_t call;      /* the call's tag: 1 .. 2^24 - 1, one more per decode call (after
                            2^24 - 1 wraps to 1); records come oldest call first */

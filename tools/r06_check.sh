@@ -58,3 +58,14 @@ if has abfused; then
     c2:compact c2:compact_nd > ${O}_ab_fused_max.txt 2>&1
   cat ${O}_ab_fused_max.txt
 fi
+if has sspec; then
+  tools/gpu_tests.sh r06${TAG}_pytest_sspec.log tests/test_gpu_stream_spec.py tests/test_gpu_streams_full.py \
+    tests/test_gpu_streams.py tests/test_gpu_batcher.py
+fi
+if has c4s; then
+  for c in c4 c2 c3; do
+    timeout -k 10 300 python bench.py --steps 20 --warmup 5 --config $c --mode streams --no-cpu-baseline \
+      > ${O}_bench_${c}_streams.json 2>> ${O}_bench.err
+    python -c "import json,sys; d=json.load(open('${O}_bench_${c}_streams.json')); t=d.get('device_timeline') or {}; print('$c streams', d['value'], d['ms_per_step'], t.get('kernels_us'), t.get('gaps_us'))"
+  done
+fi

@@ -116,7 +116,7 @@ class GpuStamp(C.Structure):
 STAMP_KERNELS = {0: "walk", 1: "walk_scan", 2: "walk2", 3: "stream_desc", 4: "claims",
                  5: "payload", 6: "plan", 7: "fixup", 8: "finalize", 9: "build_size",
                  10: "build_scan", 11: "build_scan2", 12: "build_offsets", 13: "desc_emit",
-                 14: "sum_scan"}
+                 14: "sum_scan", 15: "spec_plan"}
 
 
 class Batch(C.Structure):

@@ -255,7 +255,13 @@ constexpr int kCtlFaultEp = 2;   // epoch of the latest call whose look-back gav
 constexpr int kCtlFaults = 3;    // running count of such calls (engine_sync compares it)
 constexpr int kCtlGate = 4;      // epoch of the latest summary-only compact call whose speculation
                                  // failed (its k_plan + k_spec_fix then run, k_sum_msgs does not)
-constexpr int kCtlWords = 5;
+// speculative stream decode (k_sspec_*): epoch of the latest call whose connections k_sspec_plan
+// found ineligible (the walk decodes it), of the latest whose speculation a later kernel broke
+// (undone, then the walk), and k_sspec_plan's last-block counter
+constexpr int kCtlSpecOff = 5;
+constexpr int kCtlSpecBreak = 6;
+constexpr int kCtlSpecDone = 7;
+constexpr int kCtlWords = 8;
 // epochs: host-issued tags run 1 .. kMaxHostEpoch, device-issued ones (captured calls)
 // kMaxHostEpoch + 1 .. kMaxEpoch, so a replayed graph never meets a tag a host call left
 constexpr uint32_t kMaxHostEpoch = kMaxEpoch / 2;
@@ -3172,7 +3178,17 @@ struct WalkArgs {
     uint32_t nt_stores;        // UVHTTP_WS_STREAM_NT=1: frame records and descriptors as streaming stores
     uint32_t desc_scan;        // k_stream_desc finds first frames itself (no k_swalk_scan)
     uint32_t nt_loads;         // UVHTTP_WS_WALK_NT_LOAD=1: the wave walk's header loads non-temporal (A/B)
+    uint32_t spec;             // the speculative decode ran first: walk only if it gave way (spec_slow)
 };
+
+// Did the speculative stream decode give the call to the walk?  (Kernels of the walk path
+// launched behind k_sspec_* return at once otherwise.)
+__device__ inline bool spec_slow(const uint32_t* ctl, uint32_t epoch) {
+    return ctl[kCtlSpecOff] == epoch || ctl[kCtlSpecBreak] == epoch;
+}
+__device__ inline bool walk_skip(const WalkArgs& w) {
+    return w.spec && !spec_slow(w.ctl, w.dev_epoch ? w.ctl[kCtlEpoch] : w.epoch);
+}
 
 // process_data's buffer growth: returns false on failure (*out = size then), else the size
 // after the call
@@ -3463,6 +3479,7 @@ __device__ inline uint32_t walk_lane(const WalkArgs& w, uint32_t s, uint32_t lf)
 
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void k_swalk_lane(WalkArgs w) {
+    if (walk_skip(w)) return;
     StampScope stamp_(w.stamp, w.epoch, MODE == 1 ? UVHTTP_WS_STAMP_WALK2 : UVHTTP_WS_STAMP_WALK, false);
     const uint32_t s = stamp_.anchor_v(blockIdx.x * kBlock + threadIdx.x);
     const uint32_t lf = MODE == 1 ? lane_first(w, s) : 0;  // (before any thread leaves)
@@ -3793,6 +3810,7 @@ __device__ inline uvhttp_ws_stream_result_t walk_wave(const WalkArgs& w, uint32_
 
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void k_swalk_wave(WalkArgs w) {
+    if (walk_skip(w)) return;
     StampScope stamp_(w.stamp, w.epoch, MODE == 1 ? UVHTTP_WS_STAMP_WALK2 : UVHTTP_WS_STAMP_WALK, false);
     __shared__ __attribute__((aligned(16))) uint8_t ring[kBlock / 64][kRingBytes];
     // readfirstlane: the connection (and all walk state derived from it) is wave-uniform, so
@@ -3809,6 +3827,7 @@ __global__ __launch_bounds__(kBlock) void k_swalk_wave(WalkArgs w) {
 // 16384 connections) writes every connection's first frame itself.  Each thread takes a
 // contiguous chunk: sum it, scan the sums across the block, then write the chunk's prefixes.
 __global__ __launch_bounds__(kBlock) void k_swalk_scan(WalkArgs w, uint32_t lane_mode) {
+    if (walk_skip(w)) return;
     StampScope stamp_(w.stamp, w.epoch, UVHTTP_WS_STAMP_WALK_SCAN);
     const uint32_t m = lane_mode ? (w.n_streams + kBlock - 1) / kBlock : w.n_streams;
     const uint32_t per = (m + kBlock - 1) / kBlock;
@@ -3917,6 +3936,7 @@ constexpr uint32_t kDescScanLaneMax = kBlock * kBlock;  // (k_stream_desc_lane: 
 // lane mode: one lane per connection (few frames each) writes its descriptors in order and
 // claims the tile map
 __global__ __launch_bounds__(kBlock) void k_stream_desc_lane(WalkArgs w) {
+    if (walk_skip(w)) return;
     StampScope stamp_(w.stamp, w.epoch, UVHTTP_WS_STAMP_STREAM_DESC, false);
     const uint32_t s = stamp_.anchor_v(blockIdx.x * kBlock + threadIdx.x);
     uint32_t first, n_total;
@@ -4034,6 +4054,7 @@ __device__ inline void stream_desc_wave(const WalkArgs& w, uint32_t s, const uvh
 // overflow: every result says so, nothing else.
 
 __global__ __launch_bounds__(kBlock) void k_stream_desc(WalkArgs w) {
+    if (walk_skip(w)) return;
     StampScope stamp_(w.stamp, w.epoch, UVHTTP_WS_STAMP_STREAM_DESC, false);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint32_t s = stamp_.anchor_s(blockIdx.x * (kBlock / 64) + wave);
@@ -4085,6 +4106,642 @@ __global__ __launch_bounds__(kBlock) void k_stream_desc(WalkArgs w) {
     if (lane == 0) w.results[s].first_frame = r.first_frame;
     if (!r.n_frames) return;
     stream_desc_wave(w, s, st, r, claim_start(w, s, st), w.dev_epoch ? w.ctl[kCtlEpoch] : w.epoch);
+}
+
+// ---- speculative stream decode (k_sspec_*) ------------------------------------------------
+// The walk reads every frame's header on its own — a scattered 128-byte line per frame (C4
+// streams: 166 MB moved for 1 M headers, 31.5 us) — before the payload pass reads the same
+// lines again.  For a call of single-read connections whose frames all have the wire length of
+// their first frame (a client sending equal frames: the C4 stream shape) the payload pass can
+// find and check the headers itself:
+//   k_sspec_plan   a lane per connection: the growth check (src/uvhttp_websocket.c:832-857),
+//                  the first frame's header (its wire length L >= 64 is the speculation: N = len
+//                  / L complete frames, the rest an incomplete frame the call buffers), the
+//                  message-limit bound, frame counts and first frames (the last block to finish
+//                  scans the blocks' counts), and the 16 KiB tiles each connection's frames touch
+//                  claimed with its index (max of the tag: the smallest connection wins);
+//   k_sspec_pass   a workgroup per 16 KiB tile: the tile's connections (<= 64) from the claim
+//                  map, every frame of theirs touching the tile parsed from LDS with every check
+//                  before unmasking (:876-921) and its wire length checked against L, a 16-byte
+//                  record per frame, each frame that passes unmasked in place;
+//   k_sspec_emit   a wave per connection: the fragment state machine (:950-1015) in rounds of 64
+//                  frames, descriptors (as k_stream_desc writes them) and the result (as the walk
+//                  leaves it).
+// A connection the plan cannot speculate on (several reads, a layout or growth failure, a first
+// frame that fails, a complete frame of another length after the N-th, a message limit that could
+// bind, frames under 64 bytes) gives the whole call to the walk before anything is unmasked; a
+// frame the pass finds off the speculation, or a state-machine failure in the emit, gives it to
+// the walk after: k_sspec_pass<UNDO> masks again what the pass unmasked (the same per-frame
+// decision, XOR is its own inverse) and the walk path runs (its kernels, launched behind these,
+// return at once unless ctl says the call is theirs: walk_skip / spec_gate).
+// ------------------------------------------------------------------------------------------
+struct SpecConn {   // 64 bytes, written by k_sspec_plan
+    uint64_t b;       // begin in the wire
+    uint64_t len;
+    uint64_t size;    // recv_buffer_size after the call's growth
+    uint64_t pending; // pending_bytes in (the open message carried from earlier calls)
+    uint32_t L;       // speculated wire length of every frame (0: no complete frame)
+    uint32_t N;       // speculated complete frames
+    uint32_t local;   // frames of the block's earlier connections
+    int32_t mf;       // max_frame_size
+    uint32_t is_server;
+    uint32_t pad[3];
+};
+static_assert(sizeof(SpecConn) == 64, "one connection per 64 bytes");
+constexpr uint32_t kSpecMinL = 64;              // frames of >= 64 bytes: at most kT / 64 start in a tile
+constexpr uint32_t kSpecConnsPerTile = 32;      // (the general path's table)
+constexpr uint64_t kSpecT = kMapTile;           // k_sspec_pass tile = the claim map's tile
+// frames touching a tile: those starting in it (disjoint, >= 64 bytes) and the one covering its
+// start — whatever the connections.  (A table sized for 64 connections' edge frames took 24.6 KB
+// of LDS: 6 workgroups per CU, the pass 99 us on C4 streams.)
+constexpr uint32_t kSpecMaxF = (uint32_t)(kSpecT / kSpecMinL) + 2;
+constexpr uint32_t kSpecUndoGrid = 1024;        // k_sspec_fallback's grid (4 workgroups per CU)
+
+struct SpecArgs {
+    uint8_t* wire;
+    uint64_t wire_len;
+    const uvhttp_ws_stream_t* streams;
+    uint32_t n_streams;
+    uint32_t max_frames;
+    SpecConn* conns;
+    uint32_t* blk;            // [plan blocks]: frames per block, then their exclusive prefix
+    uint32_t n_blk;
+    uint64_t* conn_tile;      // [n_tiles]: tagged first connection whose frames touch the tile
+    struct SpecTile* tiles;   // [n_tiles]: what k_sspec_pass needs of the tile (k_sspec_plan)
+    uint64_t n_tiles;
+    FrameRec* recs;           // [max_frames]
+    uvhttp_ws_frame_desc_t* desc;
+    uvhttp_ws_stream_result_t* results;
+    uint32_t* ctl;
+    uint32_t epoch, dev_epoch, cas_claims;
+    uint64_t* stamp;
+};
+__device__ inline uint32_t spec_epoch(const SpecArgs& a) { return a.dev_epoch ? a.ctl[kCtlEpoch] : a.epoch; }
+
+// a stream frame's header from its 16-byte window: false if `avail` bytes do not hold the
+// header; else the fields and the status of the checks before unmasking (walk_calls' order)
+struct SpecHdr {
+    uint64_t plen, wl;
+    uint32_t hs, m, key, b0, b1;
+    int32_t st;
+};
+__device__ inline bool spec_parse(const u32x4& hv, uint64_t avail, int32_t mf, uint32_t is_server,
+                                  SpecHdr& h) {
+    const uint64_t hlo = hv.x | ((uint64_t)hv.y << 32), hhi = hv.z | ((uint64_t)hv.w << 32);
+    h.b0 = (uint32_t)(hlo & 0xFF);
+    h.b1 = (uint32_t)((hlo >> 8) & 0xFF);
+    const uint32_t code = h.b1 & 0x7F;
+    h.hs = code == 126 ? 4 : code == 127 ? 10 : 2;
+    if (avail < h.hs) return false;
+    if (h.hs == 2) {
+        h.plen = code;
+    } else if (h.hs == 4) {
+        h.plen = ((hlo >> 16) & 0xFF) << 8 | ((hlo >> 24) & 0xFF);
+    } else {
+        uint64_t v = 0;
+#pragma unroll
+        for (int q = 2; q < 10; ++q) v = (v << 8) | ((q < 8 ? hlo >> (8 * q) : hhi >> (8 * (q - 8))) & 0xFF);
+        h.plen = v;
+    }
+    h.m = (h.b1 & 0x80) ? 4u : 0u;
+    h.key = h.hs == 2 ? (uint32_t)(hlo >> 16) : h.hs == 4 ? (uint32_t)(hlo >> 32) : (uint32_t)(hhi >> 16);
+    if (!h.m) h.key = 0;
+    const uint32_t op = h.b0 & 0x0F;
+    const bool fin = h.b0 & 0x80;
+    int32_t st = UVHTTP_WS_FRAME_OK;
+    if (h.hs == 10 && (h.plen >> 63)) st = UVHTTP_WS_FRAME_ERR_PARSE;
+    else if (h.b0 & 0x70) st = UVHTTP_WS_FRAME_ERR_RSV;
+    else if (op >= 8 && (h.plen > 125 || !fin)) st = UVHTTP_WS_FRAME_ERR_CONTROL;
+    else if (is_server && !h.m) st = UVHTTP_WS_FRAME_ERR_UNMASKED;
+    else if (h.plen > (uint64_t)(int64_t)mf) st = UVHTTP_WS_FRAME_ERR_TOO_BIG;
+    h.st = st;
+    h.wl = st == UVHTTP_WS_FRAME_OK ? h.hs + h.m + h.plen : 0;
+    return true;
+}
+
+// What k_sspec_pass needs of a tile (one 64-byte record, loaded with the tile's bytes: no
+// dependent load before the parse), written by k_sspec_tiles: the tile's first connection (the
+// one whose frames cover the tile start, or the first beginning inside it) and the next one when
+// it begins inside the tile too, each as (begin, L, first frame touching the tile, how many, that
+// frame's index in the call), and the parsed header of the frame covering the tile start (it
+// began in an earlier tile).  A tile with a third connection takes the general path (the
+// connection table read from SpecConn through the claim map).  (The plan's connection threads
+// writing these records themselves, with frame records indexed by wire position so that no
+// first frame was needed: plan 17 us, pass 105, emit 15 on C4 — scattered records.)
+struct SpecTile {
+    uint32_t tag;        // the call's epoch (a stale record never matches)
+    uint32_t flags;      // kSt*
+    uint32_t cover_key;  // the covering frame's masking key
+    uint32_t pad;
+    struct {
+        uint64_t b;
+        uint32_t L, ka, cnt, first;
+    } c[2];
+};
+static_assert(sizeof(SpecTile) == 64, "one 64-byte record per tile");
+constexpr uint32_t kStConns = 3u, kStMore = 4u, kStCover = 8u, kStCoverGood = 16u, kStHmShift = 8,
+                   kStSrv0 = 1u << 12, kStSrv1 = 1u << 13;
+
+// the first-touching frame and count of a connection's frames in the tile at t0
+__device__ inline void spec_range(uint64_t b, uint32_t L, uint32_t N, uint64_t t0, uint32_t& ka, uint32_t& cnt) {
+    ka = 0;
+    cnt = 0;
+    if (!N) return;
+    const uint64_t reg = (uint64_t)N * L;  // (< 2^32: len < 2^32, the plan's check)
+    if (b + reg <= t0) return;
+    ka = t0 > b ? (uint32_t)(t0 - b) / L : 0u;
+    const uint64_t xl = t0 + kSpecT - 1 - b;
+    const uint32_t kb = xl < reg ? (uint32_t)xl / L : N - 1;
+    cnt = kb >= ka ? kb - ka + 1 : 0u;
+}
+
+__global__ __launch_bounds__(kBlock) void k_sspec_plan(SpecArgs a) {
+    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_SPEC_PLAN);
+    const uint32_t epoch = spec_epoch(a);
+    const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
+    bool ok = true;
+    uint32_t N = 0, L = 0;
+    if (s < a.n_streams) {
+        const uvhttp_ws_stream_t st = a.streams[s];
+        uint64_t size = st.recv_buffer_size;
+        // one process_data call, laid out in the wire after the previous connection (else the
+        // walk reports ERR_LAYOUT or walks the reads)
+        ok = st.n_reads == 0 && st.len <= a.wire_len && st.begin <= a.wire_len - st.len && !(st.len >> 32);
+        if (ok && s > 0) {
+            const uvhttp_ws_stream_t pv = a.streams[s - 1];
+            ok = st.begin >= pv.begin && st.begin - pv.begin >= pv.len;
+        }
+        ok = ok && grow_recv(st.len, st.recv_buffer_size, st.max_frame_size, &size);
+        // no message can reach max_message_size: what is open plus every byte of the call
+        const uint64_t lim = (uint64_t)(int64_t)st.max_message_size;
+        ok = ok && (lim == 0 || (st.pending_bytes <= lim && st.len <= lim - st.pending_bytes));
+        SpecHdr h;
+        if (ok && st.len >= 2 && spec_parse(load16_at(a.wire, a.wire_len, st.begin), st.len, st.max_frame_size,
+                                            (uint32_t)st.is_server, h)) {
+            if (h.st != UVHTTP_WS_FRAME_OK) {
+                ok = false;  // the call fails at its first frame: the walk reports it
+            } else if (h.wl <= st.len) {
+                L = (uint32_t)h.wl;
+                // (L - 2 <= max_frame_size: no frame of this length can fail TOO_BIG, so the
+                // pass checks the length alone)
+                ok = L >= kSpecMinL && (uint64_t)L - 2 <= (uint64_t)(int64_t)st.max_frame_size;
+                N = ok ? (uint32_t)(st.len / L) : 0u;
+                const uint64_t rem = st.len - (uint64_t)N * L;
+                SpecHdr h2;
+                // what follows the N-th frame must be a frame the call cannot complete
+                if (ok && rem >= 2 &&
+                    spec_parse(load16_at(a.wire, a.wire_len, st.begin + (uint64_t)N * L), rem, st.max_frame_size,
+                               (uint32_t)st.is_server, h2))
+                    ok = h2.st == UVHTTP_WS_FRAME_OK && h2.wl > rem;
+            }
+        }
+        if (!ok) N = L = 0;
+        SpecConn c;
+        c.b = st.begin;
+        c.len = st.len;
+        c.size = size;
+        c.pending = st.pending_bytes;
+        c.L = L;
+        c.N = N;
+        c.local = 0;
+        c.mf = st.max_frame_size;
+        c.is_server = (uint32_t)st.is_server;
+        c.pad[0] = c.pad[1] = c.pad[2] = 0;
+        a.conns[s] = c;
+        // the tiles this connection's frames touch (the tile of its begin and every tile
+        // starting inside its frames)
+        if (ok && N) {
+            const uint64_t fe = st.begin + (uint64_t)N * L;
+            tag_claim(&a.conn_tile[st.begin / kSpecT], epoch, s, a.cas_claims);
+            for (uint64_t t = st.begin / kSpecT + 1; t * kSpecT < fe; ++t) tag_claim(&a.conn_tile[t], epoch, s, a.cas_claims);
+        }
+    }
+    if (!ok) a.ctl[kCtlSpecOff] = epoch;
+    uint32_t total;
+    const uint32_t local = block_scan_u32(N, &total);
+    if (s < a.n_streams) a.conns[s].local = local;
+    // the last block to finish turns the blocks' counts into first frames
+    __shared__ uint32_t s_last;
+    if (threadIdx.x == 0) {
+        a.blk[blockIdx.x] = total;
+        __threadfence();
+        const uint32_t done = atomicAdd(&a.ctl[kCtlSpecDone], 1u);
+        s_last = done == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    uint64_t base = 0;
+    for (uint32_t b0 = 0; b0 < a.n_blk; b0 += kBlock) {
+        const uint32_t j = b0 + threadIdx.x;
+        const uint32_t v = j < a.n_blk ? __hip_atomic_load(&a.blk[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        uint64_t tot;
+        const uint64_t pre = block_exclusive_sum_u64(v, &tot);
+        if (j < a.n_blk) a.blk[j] = (uint32_t)(base + pre);
+        base += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        if (base > a.max_frames) a.ctl[kCtlSpecOff] = epoch;  // (ERR_CAPACITY: the walk reports it)
+        a.ctl[kCtlSpecDone] = 0;
+    }
+}
+
+// a thread per claimed tile (after k_sspec_plan: connections, first frames, claims)
+__global__ __launch_bounds__(kBlock) void k_sspec_tiles(SpecArgs a) {
+    const uint32_t epoch = spec_epoch(a);
+    if (a.ctl[kCtlSpecOff] == epoch) return;
+    const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= a.n_tiles) return;
+    const uint32_t c0 = tag_get(a.conn_tile[t], epoch, kNoFrame);
+    if (c0 == kNoFrame) return;
+    const uint64_t t0 = t * kSpecT;
+    const SpecConn s0 = a.conns[c0];
+    SpecConn s1;
+    const bool has1 = c0 + 1 < a.n_streams;
+    if (has1) s1 = a.conns[c0 + 1];
+    const bool in1 = has1 && s1.b < t0 + kSpecT;
+    const bool more = in1 && c0 + 2 < a.n_streams && a.conns[c0 + 2].b < t0 + kSpecT;
+    SpecTile r;
+    r.pad = 0;
+    r.cover_key = 0;
+    uint32_t flags = (in1 ? 2u : 1u) | (more ? kStMore : 0u) | (s0.is_server ? kStSrv0 : 0u);
+    spec_range(s0.b, s0.L, s0.N, t0, r.c[0].ka, r.c[0].cnt);
+    r.c[0].b = s0.b;
+    r.c[0].L = s0.L;
+    r.c[0].first = a.blk[c0 / kBlock] + s0.local + r.c[0].ka;
+    r.c[1].b = 0;
+    r.c[1].L = r.c[1].ka = r.c[1].cnt = r.c[1].first = 0;
+    if (in1) {
+        spec_range(s1.b, s1.L, s1.N, t0, r.c[1].ka, r.c[1].cnt);
+        r.c[1].b = s1.b;
+        r.c[1].L = s1.L;
+        r.c[1].first = a.blk[(c0 + 1) / kBlock] + s1.local + r.c[1].ka;
+        if (s1.is_server) flags |= kStSrv1;
+    }
+    if (r.c[0].cnt + r.c[1].cnt > kSpecMaxF) flags |= kStMore;
+    const uint64_t o = s0.b + (uint64_t)r.c[0].ka * s0.L;
+    if (r.c[0].cnt && o < t0) {  // the frame covering the tile start
+        SpecHdr h;
+        const bool good = spec_parse(load16_at(a.wire, a.wire_len, o), s0.L, INT32_MAX, s0.is_server, h) &&
+                          h.st == UVHTTP_WS_FRAME_OK && h.wl == s0.L;
+        flags |= kStCover | (good ? kStCoverGood : 0u) | ((h.hs + h.m) << kStHmShift);
+        r.cover_key = h.key;
+    }
+    r.flags = flags;
+    r.tag = epoch;
+    a.tiles[t] = r;
+}
+
+// One 16 KiB tile of the speculative pass (UNDO: mask again what the pass unmasked, nothing
+// else written).  Returns with every thread at the same point (the callers loop over tiles).
+template <bool UNDO>
+__device__ inline void sspec_tile(const SpecArgs& a, uint64_t tile, uint32_t epoch) {
+    constexpr int BLOCK = kBlock, VPT = 4;
+    constexpr uint64_t kT = kSpecT;
+    static_assert((uint64_t)BLOCK * VPT * 16 == kT, "tile = claim map tile");
+    __shared__ u32x4 s_tile[BLOCK * VPT + 1];
+    __shared__ int4 s_fr[kSpecMaxF];
+    __shared__ uint64_t s_cb[kSpecConnsPerTile];
+    __shared__ uint32_t s_cL[kSpecConnsPerTile], s_cka[kSpecConnsPerTile], s_cfirst[kSpecConnsPerTile];
+    __shared__ uint32_t s_cpre[kSpecConnsPerTile + 1];
+    __shared__ uint32_t s_csrv[kSpecConnsPerTile];
+    __shared__ uint32_t s_nc, s_bad, s_cov, s_covkey;  // s_cov: kStCover | kStCoverGood | hm
+    const uint64_t t0 = tile * kT;
+    const uint64_t vend = a.wire_len;
+    const uint64_t full_end = vend & ~(uint64_t)15;
+    const uint64_t clamp_va = full_end ? full_end - 16 : 0;
+    u32x4 data[VPT];
+    uint64_t va[VPT];
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {
+        va[v] = t0 + ((uint64_t)v * BLOCK + threadIdx.x) * 16u;
+        const uint64_t la = va[v] < full_end ? va[v] : clamp_va;
+        data[v] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.wire + la));
+    }
+    u32x4 extra = u32x4{0, 0, 0, 0};
+    if (threadIdx.x == 1) extra = load16_at(a.wire, vend, t0 + kT);
+    const SpecTile tr = a.tiles[tile];  // (uniform: scalar loads beside the tile's)
+    if (!UNDO && a.ctl[kCtlSpecOff] == epoch) return;  // the plan gave the call to the walk
+    const bool fast = tr.tag == epoch && !(tr.flags & kStMore);
+    if (fast) {
+        if (threadIdx.x == 0) {
+            const uint32_t nc = tr.flags & kStConns;
+            s_nc = nc;
+            s_bad = 0;
+            s_cpre[0] = 0;
+#pragma unroll
+            for (uint32_t l = 0; l < 2; ++l) {
+                s_cb[l] = tr.c[l].b;
+                s_cL[l] = tr.c[l].L;
+                s_cka[l] = tr.c[l].ka;
+                s_cfirst[l] = tr.c[l].first - tr.c[l].ka;  // (index of the connection's frame 0)
+                s_csrv[l] = (tr.flags & (l ? kStSrv1 : kStSrv0)) ? 1u : 0u;
+            }
+            s_cpre[1] = tr.c[0].cnt;
+            s_cpre[2] = tr.c[0].cnt + (nc > 1 ? tr.c[1].cnt : 0u);
+            s_cov = tr.flags & (kStCover | kStCoverGood | (0xFu << kStHmShift));
+            s_covkey = tr.cover_key;
+        }
+    } else {
+        // the general path: the tile's connections from the claim map and SpecConn
+        const uint32_t c0 = tag_get(a.conn_tile[tile], epoch, kNoFrame);
+        if (c0 == kNoFrame) return;  // (uniform) no connection's frames touch the tile
+        const uint32_t lane = threadIdx.x & 63;
+        if (threadIdx.x < 64) {
+            // c0 and the connections after it that begin before the tile's end
+            const uint32_t c = c0 + lane;
+            const bool valid = c < a.n_streams;
+            SpecConn sc;
+            if (valid) sc = a.conns[c];
+            const bool beyond = !valid || sc.b >= t0 + kT || lane >= kSpecConnsPerTile;
+            const uint64_t bm = __ballot(beyond);
+            const uint32_t nc = (uint32_t)__builtin_ctzll(bm);  // (lane kSpecConnsPerTile is beyond)
+            uint32_t cnt = 0, ka = 0;
+            if (lane < nc) spec_range(sc.b, sc.L, sc.N, t0, ka, cnt);
+            uint32_t inc = cnt;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t o = __shfl_up(inc, d, 64);
+                if (lane >= (uint32_t)d) inc += o;
+            }
+            if (lane < nc) {
+                s_cb[lane] = sc.b;
+                s_cL[lane] = sc.L;
+                s_cka[lane] = ka;
+                s_cfirst[lane] = sc.N ? a.blk[c / kBlock] + sc.local : 0u;
+                s_csrv[lane] = sc.is_server;
+                s_cpre[lane + 1] = inc;
+            }
+            const uint32_t F = __shfl(inc, 63, 64);
+            if (lane == 0) {
+                s_cpre[0] = 0;
+                s_nc = nc;
+                // more connections than one wave reads, or more frames than the table holds:
+                // the call goes to the walk (the undo pass decides the same: nothing unmasked)
+                s_bad = (nc == kSpecConnsPerTile && c0 + kSpecConnsPerTile < a.n_streams &&
+                         a.conns[c0 + kSpecConnsPerTile].b < t0 + kT) || F > kSpecMaxF;
+                // the frame covering the tile start (only the first connection's can begin before it)
+                s_cov = 0;
+                s_covkey = 0;
+                if (cnt && sc.b + (uint64_t)ka * sc.L < t0) {
+                    SpecHdr h;
+                    const bool good = spec_parse(load16_at(a.wire, vend, sc.b + (uint64_t)ka * sc.L), sc.L,
+                                                 INT32_MAX, sc.is_server, h) &&
+                                      h.st == UVHTTP_WS_FRAME_OK && h.wl == sc.L;
+                    s_cov = kStCover | (good ? kStCoverGood : 0u) | ((h.hs + h.m) << kStHmShift);
+                    s_covkey = h.key;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {
+        u32x4 x = data[v];
+        if (va[v] == full_end && full_end < vend) x = load16_at(a.wire, vend, full_end);
+        s_tile[v * BLOCK + threadIdx.x] = x;
+    }
+    if (threadIdx.x == 1) s_tile[BLOCK * VPT] = extra;
+    __syncthreads();
+    if (s_bad) {
+        if (!UNDO && threadIdx.x == 0) a.ctl[kCtlSpecBreak] = epoch;
+        return;
+    }
+    const uint32_t nc = s_nc, F = s_cpre[nc];
+    for (uint32_t j = threadIdx.x; j < F; j += BLOCK) {
+        uint32_t lo = 0, hi = nc - 1;  // the connection: last l with s_cpre[l] <= j
+        while (nc > 1 && lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (s_cpre[mid] <= j) lo = mid;
+            else hi = mid - 1;
+        }
+        const uint32_t l = lo;
+        const uint32_t k = s_cka[l] + (j - s_cpre[l]);
+        const uint32_t L = s_cL[l];
+        const uint64_t o = s_cb[l] + (uint64_t)k * L;
+        if (o < t0) {  // the covering frame (its header in an earlier tile: parsed before)
+            const uint32_t cov = s_cov, hm = (cov >> kStHmShift) & 0xFu;
+            const bool good = cov & kStCoverGood;
+            if (!UNDO && !good) a.ctl[kCtlSpecBreak] = epoch;
+            const uint64_t ps = o + hm;
+            s_fr[j] = int4{rel_clamp(ps, t0, kT, true), rel_clamp(good ? o + L : ps, t0, kT, false),
+                           (int32_t)s_covkey, 0};
+            continue;
+        }
+        SpecHdr h;
+        // (no TOO_BIG check: the plan required L - 2 <= max_frame_size, so no frame of wire
+        // length L can be too big, and one claiming a larger length fails wl == L)
+        const bool good = spec_parse(lds_window(s_tile, (uint32_t)(o - t0)), L, INT32_MAX, s_csrv[l], h) &&
+                          h.st == UVHTTP_WS_FRAME_OK && h.wl == L;
+        if (!UNDO) {
+            if (!good) a.ctl[kCtlSpecBreak] = epoch;
+            FrameRec r;
+            r.payload_len = h.plen;
+            r.masking_key = h.key;
+            r.opcode = (uint8_t)(h.b0 & 0x0F);
+            r.flags = (uint8_t)(((h.b0 >> 7) & 1) | ((h.b1 >> 7) << 1));
+            r.header_size = (uint8_t)h.hs;
+            r.status = (int8_t)(good ? UVHTTP_WS_FRAME_OK : UVHTTP_WS_FRAME_ERR_LAYOUT);
+            a.recs[s_cfirst[l] + k] = r;
+        }
+        const uint64_t ps = o + h.hs + h.m;
+        s_fr[j] = int4{rel_clamp(ps, t0, kT, true), rel_clamp(good ? ps + h.plen : ps, t0, kT, false),
+                       (int32_t)h.key, 0};
+    }
+    __syncthreads();
+    // each vector's mask.  Up to two connections in the tile (every tile of a call of large
+    // connections) by arithmetic, as k_unmask_stride: the frames of byte x of connection l are
+    // (x - start of its first frame in the tile) / L; more, by a binary search over the table
+    // (frames in wire order: payload ranges sorted and disjoint).  (A search per vector cost the
+    // pass 124 us on C4 streams.)
+    u32x4 m[VPT];
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) m[v] = u32x4{0, 0, 0, 0};
+    if (nc <= 2) {
+        for (uint32_t l = 0; l < nc; ++l) {
+            const uint32_t Ll = s_cL[l], cnt = s_cpre[l + 1] - s_cpre[l], base = s_cpre[l];
+            if (!cnt) continue;
+            const int64_t fs = (int64_t)(s_cb[l] + (uint64_t)s_cka[l] * Ll) - (int64_t)t0;  // first frame, tile-relative
+            const float inv_l = 1.0f / (float)Ll;
+#pragma unroll
+            for (int v = 0; v < VPT; ++v) {
+                if (va[v] >= vend) continue;
+                const int64_t rel = (int64_t)((v * BLOCK + threadIdx.x) * 16) - fs;
+                if (rel + 15 < 0) continue;
+                uint32_t lo, hi;
+                if (Ll < (1u << 20) && rel + 15 < (1 << 24)) {  // (div_small: offsets below 2^24)
+                    lo = rel < 0 ? 0u : div_small((uint32_t)rel, Ll, inv_l);
+                    hi = div_small((uint32_t)(rel + 15), Ll, inv_l);
+                } else {
+                    lo = rel < 0 ? 0u : (uint32_t)((uint64_t)rel / Ll);
+                    hi = (uint32_t)((uint64_t)(rel + 15) / Ll);
+                }
+                if (lo >= cnt) continue;
+                hi = hi < cnt - 1 ? hi : cnt - 1;
+                const int32_t r = (int32_t)((v * BLOCK + threadIdx.x) * 16);
+                for (uint32_t j = lo; j <= hi; ++j) {
+                    const int4 fr = s_fr[base + j];
+                    add_mask_rel(m[v], r, fr.x, fr.y, (uint32_t)fr.z);
+                }
+            }
+        }
+    } else {
+#pragma unroll
+        for (int v = 0; v < VPT; ++v) {
+            if (va[v] >= vend || F == 0) continue;
+            const int32_t r = (int32_t)((v * BLOCK + threadIdx.x) * 16);
+            uint32_t lo = 0, hi = F;  // first j with pe > r
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_fr[mid].y > r) hi = mid;
+                else lo = mid + 1;
+            }
+            for (uint32_t j = lo; j < F; ++j) {
+                const int4 fr = s_fr[j];
+                if (fr.x >= r + 16) break;
+                add_mask_rel(m[v], r, fr.x, fr.y, (uint32_t)fr.z);
+            }
+        }
+    }
+    const uint64_t room = vend > t0 ? vend - t0 : 0;
+    const uint32_t nrec = (uint32_t)(room < kT ? room : kT);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.wire + t0, 0, (int)nrec, 0x00020000);
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {
+        if (any_bits(m[v]) && va[v] + 16 <= vend) {
+            const u32x4 x = data[v] ^ m[v];
+            __builtin_amdgcn_raw_buffer_store_b128(
+                __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, x), rs,
+                (uint32_t)(va[v] - t0), 0, 18);
+        }
+    }
+    if (full_end != vend && full_end >= t0 && full_end < t0 + kT) {
+#pragma unroll
+        for (int v = 0; v < VPT; ++v) {
+            if (va[v] == full_end && any_bits(m[v])) {
+                const uint32_t mw[4] = {m[v].x, m[v].y, m[v].z, m[v].w};
+                for (uint64_t bq = 0; full_end + bq < vend; ++bq) {
+                    const uint8_t mb = (uint8_t)(mw[bq >> 2] >> (8 * (bq & 3)));
+                    if (mb) a.wire[full_end + bq] ^= mb;
+                }
+            }
+        }
+    }
+}
+
+// the pass: a workgroup per tile; UNDO (only when the speculation broke): a grid-stride loop
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) void k_sspec_pass(SpecArgs a, uint64_t tile_base) {
+    const uint32_t epoch = spec_epoch(a);
+    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_PAYLOAD, false, tile_base);
+    sspec_tile<false>(a, tile_base + stamp_.anchor_s(blockIdx.x), epoch);
+}
+
+
+// a wave per connection: the state machine over the pass's records, descriptors, the result
+__global__ __launch_bounds__(kBlock) void k_sspec_emit(SpecArgs a) {
+    const uint32_t epoch = spec_epoch(a);
+    if (a.ctl[kCtlSpecOff] == epoch || a.ctl[kCtlSpecBreak] == epoch) return;
+    StampScope stamp_(a.stamp, a.epoch, UVHTTP_WS_STAMP_STREAM_DESC, false);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const uint32_t s = stamp_.anchor_s(blockIdx.x * (kBlock / 64) + wave);
+    if (s >= a.n_streams) return;
+    const SpecConn sc = a.conns[s];
+    const uint32_t first = a.blk[s / kBlock] + sc.local;
+    bool open = sc.pending != 0;
+    uint64_t acc = sc.pending;
+    uint32_t msg = 0;
+    const uint64_t below = (1ull << lane) - 1;
+    for (uint32_t r0 = 0; r0 < sc.N; r0 += 64) {
+        const uint32_t k = r0 + lane;
+        const bool act = k < sc.N;
+        FrameRec rec;
+        rec.payload_len = 0;
+        rec.masking_key = 0;
+        rec.opcode = 8;
+        rec.flags = 0;
+        rec.header_size = 2;
+        rec.status = 0;
+        if (act) rec = a.recs[first + k];
+        const bool data = act && rec.opcode <= 2;
+        const bool fin = rec.flags & UVHTTP_WS_FLAG_FIN;
+        const bool cont = rec.opcode == 0;
+        // the message open after this frame (a data frame): CONT keeps it until FIN; a start
+        // opens one unless FIN or empty (an empty first fragment allocates nothing, :794-816)
+        const bool oa = cont ? !fin : (!fin && rec.payload_len != 0);
+        const uint64_t dm = __ballot(data), om = __ballot(data && oa);
+        const uint64_t prior = dm & below;
+        const bool open_before = prior ? ((om >> (63 - __builtin_clzll(prior))) & 1) : open;
+        const bool fail = data && (cont ? !open_before : open_before);
+        if (__ballot(fail)) {  // the reference stops here: the walk reports it
+            if (lane == 0) a.ctl[kCtlSpecBreak] = epoch;
+            return;
+        }
+        const bool fin_data = data && fin;
+        const uint64_t fm = __ballot(fin_data);
+        if (act) {
+            const uint64_t pos = (uint64_t)k * sc.L;
+            uvhttp_ws_frame_desc_t d;
+            d.payload_off = sc.b + pos + rec.header_size + ((rec.flags & UVHTTP_WS_FLAG_MASK) ? 4u : 0u);
+            d.payload_len = rec.payload_len;
+            d.masking_key = rec.masking_key;
+            d.message = data ? msg + (uint32_t)__builtin_popcountll(fm & below) : 0u;
+            d.opcode = rec.opcode;
+            d.flags = (uint8_t)(rec.flags | (fin_data ? UVHTTP_WS_FLAG_MSG_END : 0u));
+            d.header_size = rec.header_size;
+            d.status = UVHTTP_WS_FRAME_OK;
+            d.wire_len = sc.L;
+            a.desc[first + k] = d;
+        }
+        // what the round leaves open: the latest data frame decides; the bytes since the latest
+        // start (a start or a FIN resets them)
+        const uint64_t rm = __ballot(data && (!cont || fin));
+        const int jr = rm ? 63 - __builtin_clzll(rm) : -1;
+        uint64_t add = (data && (int)lane > jr) ? rec.payload_len : 0u;
+        if ((int)lane == jr && !cont && !fin) add = rec.payload_len;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) add += __shfl_xor(add, d, 64);
+        acc = jr >= 0 ? add : acc + add;
+        if (dm) open = (om >> (63 - __builtin_clzll(dm))) & 1;
+        msg += (uint32_t)__builtin_popcountll(fm);
+    }
+    if (lane == 0) {
+        uvhttp_ws_stream_result_t r;
+        r.first_frame = first;
+        r.n_frames = sc.N;
+        r.n_delivered = sc.N;
+        r.status = 0;
+        r.first_status = 0;
+        r.calls = 1;
+        r.consumed_bytes = (uint64_t)sc.N * sc.L;
+        r.recv_buffer_size = sc.size;
+        r.pending_bytes = open ? acc : 0u;
+        r.buffered_end = sc.len;
+        r.reserved = 0;
+        a.results[s] = r;
+    }
+}
+
+// The walk path behind a speculative attempt ends here, gated, in a grid-stride loop (a no-op
+// launch of one workgroup per tile costs more than the loop): when the pass ran and the
+// speculation broke, each tile first gets the pass's unmask undone (k_sspec_pass's decisions
+// again — the walk and k_stream_desc before this read only headers, which no pass changes),
+// then the in-place payload kernel's work from the walk's descriptors.
+__global__ __launch_bounds__(kBlock) void k_sspec_fallback(SpecArgs sa, BatchArgs a,
+                                                           const uvhttp_ws_frame_desc_t* __restrict__ desc,
+                                                           Workspace ws, uint64_t n_tiles) {
+    resolve_epoch(a, ws);
+    if (!spec_slow(ws.ctl, a.epoch)) return;
+    const bool undo = ws.ctl[kCtlSpecOff] != a.epoch;  // (the pass ran: its unmask is undone)
+    StampScope ss(nullptr, 0, 0, false);
+    for (uint64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+        __syncthreads();  // (the previous tile's LDS)
+        if (undo) {
+            sspec_tile<true>(sa, t, a.epoch);
+            __syncthreads();
+        }
+        uint32_t n, nb;
+        unmask_tile<kBlock, 4, 18>(a, desc, ws, t - blockIdx.x, n, nb, ss);
+    }
 }
 
 // ---- k_swalk_fused: walk, first frame and descriptors of a connection in one launch -------
@@ -4955,6 +5612,11 @@ struct uvhttp_ws_gpu_engine {
     int stream_nt;             // UVHTTP_WS_STREAM_NT=1: streaming stores in the walk and k_stream_desc (A/B)
     int desc_scan_off;         // UVHTTP_WS_DESC_SCAN=0: k_swalk_scan before k_stream_desc always (A/B)
     int walk_nt_load;          // UVHTTP_WS_WALK_NT_LOAD=1: non-temporal header loads in the wave walk (A/B)
+    int stream_spec;           // single-read stream calls try the speculative decode first (k_sspec_*;
+                               // UVHTTP_WS_STREAM_SPEC=0: the walk always)
+    void* sp_mem;              // its scratch: SpecConn per connection, block counts, tile claims
+    uint32_t sp_streams;
+    uint64_t sp_tiles;
     int fused_block, fused_vpt;  // UVHTTP_WS_FUSED_TILE=BxV: the fused payload pass's tile (A/B)
     uint32_t fixup_blocks;     // k_fixup grid cap (UVHTTP_WS_FIXUP_BLOCKS, A/B)
     int fused_aux;             // fused payload stores' cache-policy bits (UVHTTP_WS_FUSED_AUX, A/B)
@@ -5047,6 +5709,7 @@ static void experiment_knobs(uvhttp_ws_gpu_engine_t* e) {
     if (const char* sn = getenv("UVHTTP_WS_STREAM_NT")) e->stream_nt = atoi(sn) != 0;
     if (const char* ds = getenv("UVHTTP_WS_DESC_SCAN")) e->desc_scan_off = atoi(ds) == 0;
     if (const char* wn = getenv("UVHTTP_WS_WALK_NT_LOAD")) e->walk_nt_load = atoi(wn) != 0;
+    if (const char* sq = getenv("UVHTTP_WS_STREAM_SPEC")) e->stream_spec = atoi(sq) != 0;
     if (const char* wr = getenv("UVHTTP_WS_WALK_REC")) e->wr_rec_on = atoi(wr) != 0;
     if (const char* wm = getenv("UVHTTP_WS_WALK"))
         e->walk_mode = strcmp(wm, "lane") == 0 ? 1 : strcmp(wm, "wave") == 0 ? 2 : 0;
@@ -5105,6 +5768,7 @@ int uvhttp_ws_gpu_engine_create(int device, uvhttp_ws_gpu_engine_t** out) {
     // vs 115.9 us with them left by the payload pass, profiles/r06h_desc_emit_ab_*.txt); compact
     // the speculative pass leaves them (123.9 vs 126.9 us, profiles/r06j_desc_emit_compact_ab.txt)
     e->desc_emit = 3;
+    e->stream_spec = 1;
     {
         int prev = 0;
         (void)hipGetDevice(&prev);
@@ -5144,6 +5808,7 @@ void uvhttp_ws_gpu_engine_free(uvhttp_ws_gpu_engine_t* e) {
     scratch_free(e, e->wt_mem);
     scratch_free(e, e->wr_mem);
     scratch_free(e, e->dscr);
+    scratch_free(e, e->sp_mem);
     if (e->pool_ok) (void)hipStreamSynchronize(nullptr);
     if (e->ctl) (void)hipFree(e->ctl);
     if (e->stamp_mem) (void)hipFree(e->stamp_mem);
@@ -6089,6 +6754,33 @@ static int reserve_streams(uvhttp_ws_gpu_engine_t* e, uint32_t frames, uint32_t 
     return UVHTTP_WS_GPU_OK;
 }
 
+// the speculative stream decode's scratch (zeroed: no tile claim matches a live epoch)
+static int reserve_spec(uvhttp_ws_gpu_engine_t* e, uint32_t streams, uint64_t tiles, hipStream_t s) {
+    if (e->sp_mem && streams <= e->sp_streams && tiles <= e->sp_tiles) return UVHTTP_WS_GPU_OK;
+    if (e->capturing)
+        return set_err(e, UVHTTP_WS_GPU_EINVAL, "stream scratch too small for a captured call", hipSuccess);
+    const uint32_t ns = streams > e->sp_streams ? streams : e->sp_streams;
+    const uint64_t nt = tiles > e->sp_tiles ? tiles : e->sp_tiles;
+    const size_t o_blk = align_up((size_t)ns * sizeof(SpecConn), 256);
+    const size_t o_tile = align_up(o_blk + ((size_t)ns / kBlock + 2) * 4, 256);
+    const size_t o_trec = align_up(o_tile + (size_t)(nt + 1) * 8, 256);
+    const size_t bytes = align_up(o_trec + (size_t)(nt + 1) * sizeof(SpecTile), 256);
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(e->device);
+    const hipError_t h = scratch_grow(e, &e->sp_mem, bytes, true, s, true);
+    (void)hipSetDevice(prev);
+    if (h != hipSuccess) {
+        e->sp_mem = nullptr;
+        e->sp_streams = 0;
+        e->sp_tiles = 0;
+        return set_err(e, UVHTTP_WS_GPU_ENOMEM, "hipMalloc speculative stream scratch", h);
+    }
+    e->sp_streams = ns;
+    e->sp_tiles = nt;
+    return UVHTTP_WS_GPU_OK;
+}
+
 int uvhttp_ws_gpu_decode_streams(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint64_t wire_len,
                                  const uvhttp_ws_stream_t* d_streams, uint32_t n_streams,
                                  uint32_t max_frames, uvhttp_ws_frame_desc_t* d_desc,
@@ -6126,8 +6818,12 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     hipStream_t s = (hipStream_t)stream;
 
     // a wave per connection when the waves fill the chip in about one round, else a lane
-    // (UVHTTP_WS_WALK=lane|wave pins it)
-    const bool wave_walk = e->walk_mode ? e->walk_mode == 2 : n_streams <= 16384;
+    // (UVHTTP_WS_WALK=lane|wave pins it).  Behind a speculative attempt (below) the walk path is
+    // the fall-back, and its kernels are launched whether it runs or not: the lane walk and
+    // k_stream_desc_lane, whose grids are 64 times smaller, so the launches that return at once
+    // cost less (C4 streams: 1024 + 1024 workgroups against 16 + 16)
+    const bool spec_try = e->stream_spec && !d_read_end && wire_len > 0 && (uint64_t)max_frames >= 8ull * n_streams;
+    const bool wave_walk = e->walk_mode ? e->walk_mode == 2 : (n_streams <= 16384 && !spec_try);
     // single pass (starts written into per-connection slices) unless UVHTTP_WS_WALK_SINGLE=0.
     // (The idle between calls of some C2 stream runs, DESIGN.md §5, is not the slices: with
     // the lane walk in two passes and no slice scratch, 2 of 10 runs idled all the same, r03p51.)
@@ -6177,11 +6873,56 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     const uint32_t nsb = (n_streams + kBlock - 1) / kBlock;
     const uint32_t nwb = (n_streams + kBlock / 64 - 1) / (kBlock / 64);
     const int tk_chain = e->time_chain ? timing_begin(e, s) : -1;
+    // single-read calls whose connections carry several frames each (by the caller's frame
+    // capacity): the speculative decode first, the walk path behind it (gated)
+    const uint64_t sp_tiles = (wire_len + kSpecT - 1) / kSpecT;
+    const bool spec = spec_try && reserve_spec(e, n_streams, sp_tiles, s) == UVHTTP_WS_GPU_OK;
+    int tk_spec = -1;
+    SpecArgs sa_keep;
+    memset(&sa_keep, 0, sizeof(sa_keep));
+    if (spec) {
+        SpecArgs& sa = sa_keep;
+        sa.wire = d_wire;
+        sa.wire_len = wire_len;
+        sa.streams = d_streams;
+        sa.n_streams = n_streams;
+        sa.max_frames = max_frames;
+        char* sb = (char*)e->sp_mem;
+        sa.conns = (SpecConn*)sb;
+        sa.blk = (uint32_t*)(sb + align_up((size_t)e->sp_streams * sizeof(SpecConn), 256));
+        sa.n_blk = nsb;
+        sa.conn_tile = (uint64_t*)(sb + align_up(align_up((size_t)e->sp_streams * sizeof(SpecConn), 256) +
+                                                     ((size_t)e->sp_streams / kBlock + 2) * 4, 256));
+        sa.tiles = (SpecTile*)(sb + align_up(align_up(align_up((size_t)e->sp_streams * sizeof(SpecConn), 256) +
+                                                            ((size_t)e->sp_streams / kBlock + 2) * 4, 256) +
+                                                   (size_t)(e->sp_tiles + 1) * 8, 256));
+        sa.n_tiles = sp_tiles;
+        sa.recs = reinterpret_cast<FrameRec*>(e->ws.recs);
+        sa.desc = d_desc;
+        sa.results = d_results;
+        sa.ctl = e->ctl;
+        sa.epoch = w.epoch;
+        sa.dev_epoch = w.dev_epoch;
+        sa.cas_claims = w.cas_claims;
+        sa.stamp = w.stamp;
+        hipLaunchKernelGGL(k_sspec_plan, dim3(nsb), dim3(kBlock), 0, s, sa);
+        hipLaunchKernelGGL(k_sspec_tiles, dim3((uint32_t)((sp_tiles + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, sa);
+        tk_spec = timing_begin(e, s);
+        for (uint64_t tb = 0; tb < sp_tiles; tb += (1ull << 24)) {
+            const uint32_t g = (uint32_t)((sp_tiles - tb) < (1ull << 24) ? (sp_tiles - tb) : (1ull << 24));
+            hipLaunchKernelGGL(k_sspec_pass, dim3(g), dim3(kBlock), 0, s, sa, tb);
+        }
+        timing_end(e, tk_spec, s);
+        hipLaunchKernelGGL(k_sspec_emit, dim3(nwb), dim3(kBlock), 0, s, sa);
+        w.spec = 1;
+    } else {
+        w.spec = 0;
+    }
     // UVHTTP_WS_WALK_FUSE=1: walk, scan and descriptors in one launch (k_swalk_fused; its
     // results are finished by the payload kernel's first workgroup, so not for an empty wire).
     // Not the default: it measured even with the three launches (C4 142.8 vs 142.6 us per
     // step, profiles/r05fy_*) and only without the block tickets (with them 155 us).
-    const bool fused = wave_walk && w.single && e->walk_fuse && wire_len > 0 &&
+    const bool fused = !spec && wave_walk && w.single && e->walk_fuse && wire_len > 0 &&
                        n_streams <= kSwalkFusedMaxBlocks * (kBlock / 64);  // (its records)
     if (fused) {
         hipLaunchKernelGGL(k_swalk_fused, dim3(nwb), dim3(kBlock), 0, s, w);
@@ -6225,6 +6966,15 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     a.stamp = w.stamp;
     a.cas_claims = w.cas_claims;
     // (k_stream_desc / k_stream_desc_lane claimed the tile map)
+    if (spec) {  // the walk path's payload pass (after undoing the speculative one), gated
+        const uint32_t g = sp_tiles < kSpecUndoGrid ? (uint32_t)sp_tiles : kSpecUndoGrid;
+        hipLaunchKernelGGL(k_sspec_fallback, dim3(g), dim3(kBlock), 0, s, sa_keep, a, d_desc, e->ws, sp_tiles);
+        timing_end(e, tk_chain, s);
+        const hipError_t hs = hipGetLastError();
+        if (prev != e->device) (void)hipSetDevice(prev);
+        if (hs != hipSuccess) return set_err(e, UVHTTP_WS_GPU_ELAUNCH, "launch", hs);
+        return UVHTTP_WS_GPU_OK;
+    }
     // payload tile shape: the frame count is only known on the device, so the caller's frame
     // capacity stands in for it (wire bytes per frame slot; the same rule as the batch decode)
     int blk = e->tile_block, vpt = e->tile_vpt;
