@@ -149,10 +149,10 @@ def test_uniform_connections(torch, engines, plen):
 
 
 def test_many_connections_per_tile(torch, engines):
-    """connections of a few 64-byte frames: up to 64 of them share a 16 KiB tile; more than 64
+    """connections of a few 64-byte frames: up to 32 of them share a 16 KiB tile; more than 32
     send the call to the walk"""
     rng = random.Random(5)
-    for per, n_conns, ok in ((5, 200, True), (2, 300, False)):
+    for per, n_conns, ok in ((10, 200, True), (5, 200, False), (2, 300, False)):
         conns = [(_conn_frames(rng, per, 58, False, p_frag=0.0)[0], b"", 0, 0, 16 << 20, 0)
                  for _ in range(n_conns)]
         wire, st = _build(conns)
