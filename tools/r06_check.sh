@@ -69,3 +69,10 @@ if has c4s; then
     python -c "import json,sys; d=json.load(open('${O}_bench_${c}_streams.json')); t=d.get('device_timeline') or {}; print('$c streams', d['value'], d['ms_per_step'], t.get('kernels_us'), t.get('gaps_us'))"
   done
 fi
+if has build; then
+  tools/gpu_tests.sh r06${TAG}_pytest_build.log tests/test_gpu_build.py
+  for m in 0 1; do
+    AB_MASKED=$m timeout -k 10 300 python tools/ab_build.py c4 tree tools/bin/libws_zeroall.so > ${O}_ab_build_$m.txt 2>&1
+    cat ${O}_ab_build_$m.txt
+  done
+fi

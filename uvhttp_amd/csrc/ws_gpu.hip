@@ -2090,7 +2090,7 @@ __global__ __launch_bounds__(kBlock) void k_fixup(BatchArgs a, uvhttp_ws_frame_d
 // ------------------------------------------------------------------------------------
 // Summary-only decode, after k_unmask_stride<..., SUM = true> (which left one info byte per
 // frame and unmasked every locally valid frame):
-//   k_sum_scan  16 frames per thread: the fragment state machine — with every frame before a
+//   k_sum_scan  4 frames per thread (kScanFpt): the fragment state machine — with every frame before a
 //               delivered one delivered, no control frame filling a slot but the last (stride >=
 //               kSumMinStride) and no max_message_size check able to fire (run_decode's bound),
 //               the state before frame f is "the latest data frame before f left a message
@@ -5346,6 +5346,9 @@ void kb_emit_frames(BuildArgs b) {
     uint32_t* win32 = reinterpret_cast<uint32_t*>(s_win);
     for (uint64_t wlo = A & ~15ull; wlo < B; wlo += kEmitWin) {
         const uint64_t whi = wlo + kEmitWin;
+// (zeroing only the vectors that are OR-ed into — a frame's header and payload-edge vectors —
+        // measured even with zeroing the whole window: C4 build 97.8 vs 98.4 us, masked 103.0 vs
+        // 102.9, profiles/r06q_emit_zero_edges_ab_*.txt)
         for (uint32_t v = threadIdx.x; v < kEmitWin / 16; v += BLOCK) s_win[v] = u32x4{0, 0, 0, 0};
         if (one) {
             if (threadIdx.x == 0) s_q[0] = 0, s_q[1] = nitems;
