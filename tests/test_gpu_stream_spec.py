@@ -86,7 +86,7 @@ def _build(conns, gap=0, tail=None):
     return wire, st
 
 
-def _run(torch, engines, wire, st, max_frames=None, spec_expected=None):
+def _run(torch, engines, wire, st, max_frames=None, spec_expected=None, read_end=None):
     import uvhttp_amd as U
     n_st = st.size
     total_cap = max_frames or max(8 * n_st, _build.frames + n_st, 64)
@@ -97,7 +97,9 @@ def _run(torch, engines, wire, st, max_frames=None, spec_expected=None):
         desc_t = torch.full(((total_cap + 1) * 32,), 0xA5, dtype=torch.uint8, device="cuda")
         if k == 0:
             e.read_stamps()
-        desc, res = e.decode_streams(d, dev_st, n_st, total_cap, desc=desc_t, wire_len=wire.size)
+        re_dev = None if read_end is None else torch.from_numpy(read_end.view(np.int64).copy()).to("cuda")
+        desc, res = e.decode_streams(d, dev_st, n_st, total_cap, desc=desc_t, wire_len=wire.size,
+                                     read_end=re_dev, n_reads=0 if read_end is None else read_end.size)
         torch.cuda.synchronize()
         e.sync()
         kinds = {r[1] for r in e.read_stamps()} if k == 0 else set()
@@ -115,13 +117,14 @@ def _run(torch, engines, wire, st, max_frames=None, spec_expected=None):
     assert np.array_equal(a["wire"], b["wire"]), np.nonzero(a["wire"] != b["wire"])[0][:8]
     # and the oracle
     host = wire.copy()
-    out, frames, total = _oracle.decode_streams(host, st, None, max_frames=total_cap)
+    out, frames, total = _oracle.decode_streams(host, st, read_end, max_frames=total_cap)
     r, o = a["res"], out
     if (r["first_status"] == -10).all():  # capacity: nothing decoded
         assert np.array_equal(a["wire"], wire)
         return a
     assert np.array_equal(r["n_delivered"], o["n_frames"])
     assert np.array_equal(r["status"], o["rc"]) and np.array_equal(r["first_status"], o["reason"])
+    assert np.array_equal(r["calls"], o["calls"])
     assert np.array_equal(r["consumed_bytes"], o["consumed"])
     assert np.array_equal(r["recv_buffer_size"], o["recv_size"])
     assert np.array_equal(r["pending_bytes"], o["frag_size"])
@@ -226,3 +229,42 @@ def test_repeated_calls_alternate_paths(torch, engines):
     for conns, ok in ((good, True), (bad, False), (good, True), (bad, False)):
         wire, st = _build([tuple(c) for c in conns])
         _run(torch, engines, wire, st, spec_expected=ok)
+
+
+def _reads(rng, st, cuts, max_reads=None):
+    """a read table per connection: cut points at random sizes from `cuts` (the last = len)"""
+    re, first = [], 0
+    for i in range(st.size):
+        ln = int(st[i]["len"])
+        ends, pos = [], 0
+        while pos < ln:
+            pos = min(ln, pos + rng.choice(cuts))
+            ends.append(pos)
+        if not ends:
+            ends = [0]
+        if max_reads and len(ends) > max_reads:
+            ends = ends[:max_reads - 1] + [ln]
+        st[i]["first_read"] = first
+        st[i]["n_reads"] = len(ends)
+        re += ends
+        first += len(ends)
+    return np.array(re, dtype=np.uint64)
+
+
+@pytest.mark.parametrize("cuts", [[1 << 30], [16384], [1000, 7, 16384], [100, 65536]])
+def test_read_tables(torch, engines, cuts):
+    """connections fed several process_data calls (the batcher's live shape): the calls' growth
+    checks (a 4 KiB starting buffer growing by doubling, a max_frame_size the growth can hit) and
+    which call delivers a frame — the speculation holds unless a growth check fails"""
+    rng = random.Random(str(cuts))
+    conns = []
+    for i in range(24):
+        plen = rng.choice([250, 1000, 3000])
+        frames, _ = _conn_frames(rng, rng.choice([8, 40, 100]), plen, False, p_frag=0.3)
+        conns.append((frames, frames[0][:rng.randrange(0, 20)], 0, 0, rng.choice([16 << 20, 8192]), 0))
+    wire, st = _build(conns)
+    st["recv_buffer_size"] = 4096
+    re = _reads(rng, st, cuts)
+    # a growth check can fail only where max_frame_size (8 KiB) caps the buffer below what a
+    # call holds: then the call goes to the walk
+    _run(torch, engines, wire, st, read_end=re)

@@ -76,3 +76,10 @@ if has build; then
     cat ${O}_ab_build_$m.txt
   done
 fi
+if has walkcmp; then
+  for v in "" "UVHTTP_WS_STREAM_SPEC=0" "UVHTTP_WS_STREAM_SPEC=0 UVHTTP_WS_WALK=lane"; do
+    env $v timeout -k 10 300 python bench.py --steps 20 --warmup 5 --config c4 --mode streams --no-cpu-baseline \
+      > ${O}_walkcmp.json 2>> ${O}_bench.err
+    python -c "import json,sys; d=json.load(open('${O}_walkcmp.json')); t=d.get('device_timeline') or {}; print('[$v]', d['value'], d['ms_per_step'], t.get('kernels_us'))"
+  done
+fi

@@ -242,7 +242,7 @@ EXPERIMENT_KNOBS = (
     "UVHTTP_WS_FUSED_AUX", "UVHTTP_WS_SUMMARY_FAST", "UVHTTP_WS_TILE", "UVHTTP_WS_FIXUP_BLOCKS",
     "UVHTTP_WS_FUSED_TILE", "UVHTTP_WS_TIMING_FENCE", "UVHTTP_WS_PIPE_IN_FLIGHT",
     "UVHTTP_TLS_CRYPT_GRID", "UVHTTP_WS_BATCHER_TRACE", "UVHTTP_WS_BATCHER_FAIL_EVERY",
-    "UVHTTP_WS_COPY_SSE2")
+    "UVHTTP_WS_COPY_SSE2", "UVHTTP_WS_DESC_EMIT", "UVHTTP_WS_STREAM_SPEC")
 
 
 def experiment_knobs_set():

@@ -256,12 +256,11 @@ constexpr int kCtlFaults = 3;    // running count of such calls (engine_sync com
 constexpr int kCtlGate = 4;      // epoch of the latest summary-only compact call whose speculation
                                  // failed (its k_plan + k_spec_fix then run, k_sum_msgs does not)
 // speculative stream decode (k_sspec_*): epoch of the latest call whose connections k_sspec_plan
-// found ineligible (the walk decodes it), of the latest whose speculation a later kernel broke
-// (undone, then the walk), and k_sspec_plan's last-block counter
+// (or the capacity check in k_sspec_tiles) found ineligible — the walk decodes it — and of the
+// latest whose speculation a later kernel broke (undone, then the walk)
 constexpr int kCtlSpecOff = 5;
 constexpr int kCtlSpecBreak = 6;
-constexpr int kCtlSpecDone = 7;
-constexpr int kCtlWords = 8;
+constexpr int kCtlWords = 7;
 // epochs: host-issued tags run 1 .. kMaxHostEpoch, device-issued ones (captured calls)
 // kMaxHostEpoch + 1 .. kMaxEpoch, so a replayed graph never meets a tag a host call left
 constexpr uint32_t kMaxHostEpoch = kMaxEpoch / 2;
@@ -4111,9 +4110,9 @@ __global__ __launch_bounds__(kBlock) void k_stream_desc(WalkArgs w) {
 // ---- speculative stream decode (k_sspec_*) ------------------------------------------------
 // The walk reads every frame's header on its own — a scattered 128-byte line per frame (C4
 // streams: 166 MB moved for 1 M headers, 31.5 us) — before the payload pass reads the same
-// lines again.  For a call of single-read connections whose frames all have the wire length of
-// their first frame (a client sending equal frames: the C4 stream shape) the payload pass can
-// find and check the headers itself:
+// lines again.  For a call whose connections' frames all have the wire length of their first
+// frame (a client sending equal frames: the C4 stream shape) the payload pass can find and check
+// the headers itself:
 //   k_sspec_plan   a lane per connection: the growth check (src/uvhttp_websocket.c:832-857),
 //                  the first frame's header (its wire length L >= 64 is the speculation: N = len
 //                  / L complete frames, the rest an incomplete frame the call buffers), the
@@ -4127,7 +4126,9 @@ __global__ __launch_bounds__(kBlock) void k_stream_desc(WalkArgs w) {
 //   k_sspec_emit   a wave per connection: the fragment state machine (:950-1015) in rounds of 64
 //                  frames, descriptors (as k_stream_desc writes them) and the result (as the walk
 //                  leaves it).
-// A connection the plan cannot speculate on (several reads, a layout or growth failure, a first
+// The calls of a connection with a read table change nothing of this but the recv-buffer growth
+// (checked per call; which call delivers a frame shows in no output), so the plan follows it.
+// A connection the plan cannot speculate on (a layout or growth failure in any call, a first
 // frame that fails, a complete frame of another length after the N-th, a message limit that could
 // bind, frames under 64 bytes) gives the whole call to the walk before anything is unmasked; a
 // frame the pass finds off the speculation, or a state-machine failure in the emit, gives it to
@@ -4145,7 +4146,7 @@ struct SpecConn {   // 64 bytes, written by k_sspec_plan
     uint32_t local;   // frames of the block's earlier connections
     int32_t mf;       // max_frame_size
     uint32_t is_server;
-    uint32_t pad[3];
+    uint32_t pad[3];     // [0]: process_data calls (reads; 1 without a read table)
 };
 static_assert(sizeof(SpecConn) == 64, "one connection per 64 bytes");
 constexpr uint32_t kSpecMinL = 64;              // frames of >= 64 bytes: at most kT / 64 start in a tile
@@ -4163,8 +4164,11 @@ struct SpecArgs {
     const uvhttp_ws_stream_t* streams;
     uint32_t n_streams;
     uint32_t max_frames;
+    const uint64_t* read_end;  // [n_reads_total] or null (decode_streams)
+    uint32_t n_reads_total;
     SpecConn* conns;
-    uint32_t* blk;            // [plan blocks]: frames per block, then their exclusive prefix
+    uint32_t* blk;            // [plan blocks]: frames per block (k_sspec_plan)
+    uint32_t* blk_pre;        // [plan blocks]: their exclusive prefix (k_sspec_tiles)
     uint32_t n_blk;
     uint64_t* conn_tile;      // [n_tiles]: tagged first connection whose frames touch the tile
     struct SpecTile* tiles;   // [n_tiles]: what k_sspec_pass needs of the tile (k_sspec_plan)
@@ -4264,14 +4268,16 @@ __global__ __launch_bounds__(kBlock) void k_sspec_plan(SpecArgs a) {
     if (s < a.n_streams) {
         const uvhttp_ws_stream_t st = a.streams[s];
         uint64_t size = st.recv_buffer_size;
-        // one process_data call, laid out in the wire after the previous connection (else the
-        // walk reports ERR_LAYOUT or walks the reads)
-        ok = st.n_reads == 0 && st.len <= a.wire_len && st.begin <= a.wire_len - st.len && !(st.len >> 32);
+        // laid out in the wire after the previous connection, its read table (if any) in range
+        // and ending at len (else the walk reports ERR_LAYOUT)
+        const uint32_t K = st.n_reads;
+        ok = st.len <= a.wire_len && st.begin <= a.wire_len - st.len && !(st.len >> 32) &&
+             (K == 0 || (a.read_end && st.first_read <= a.n_reads_total && K <= a.n_reads_total - st.first_read &&
+                         a.read_end[st.first_read + K - 1] == st.len));
         if (ok && s > 0) {
             const uvhttp_ws_stream_t pv = a.streams[s - 1];
             ok = st.begin >= pv.begin && st.begin - pv.begin >= pv.len;
         }
-        ok = ok && grow_recv(st.len, st.recv_buffer_size, st.max_frame_size, &size);
         // no message can reach max_message_size: what is open plus every byte of the call
         const uint64_t lim = (uint64_t)(int64_t)st.max_message_size;
         ok = ok && (lim == 0 || (st.pending_bytes <= lim && st.len <= lim - st.pending_bytes));
@@ -4287,13 +4293,40 @@ __global__ __launch_bounds__(kBlock) void k_sspec_plan(SpecArgs a) {
                 ok = L >= kSpecMinL && (uint64_t)L - 2 <= (uint64_t)(int64_t)st.max_frame_size;
                 N = ok ? (uint32_t)(st.len / L) : 0u;
                 const uint64_t rem = st.len - (uint64_t)N * L;
+                // the middle and the last speculated frame must be frames of length L too: a
+                // connection of mixed frame sizes is left to the walk here, before the pass has
+                // unmasked anything (otherwise its break costs the call a pass, an undo and the walk)
+                const u32x4 hm = load16_at(a.wire, a.wire_len, st.begin + (uint64_t)(N / 2) * L);
+                const u32x4 hz = load16_at(a.wire, a.wire_len, st.begin + (uint64_t)(N ? N - 1 : 0) * L);
+                const u32x4 hr = load16_at(a.wire, a.wire_len, st.begin + (uint64_t)N * L);
+                SpecHdr h1;
+                ok = ok && spec_parse(hm, L, INT32_MAX, (uint32_t)st.is_server, h1) && h1.st == UVHTTP_WS_FRAME_OK &&
+                     h1.wl == L;
+                ok = ok && spec_parse(hz, L, INT32_MAX, (uint32_t)st.is_server, h1) && h1.st == UVHTTP_WS_FRAME_OK &&
+                     h1.wl == L;
                 SpecHdr h2;
                 // what follows the N-th frame must be a frame the call cannot complete
-                if (ok && rem >= 2 &&
-                    spec_parse(load16_at(a.wire, a.wire_len, st.begin + (uint64_t)N * L), rem, st.max_frame_size,
-                               (uint32_t)st.is_server, h2))
+                if (ok && rem >= 2 && spec_parse(hr, rem, st.max_frame_size, (uint32_t)st.is_server, h2))
                     ok = h2.st == UVHTTP_WS_FRAME_OK && h2.wl > rem;
             }
+        }
+        // the recv-buffer growth of every call (src/uvhttp_websocket.c:832-857): call k holds
+        // the bytes from the first frame the earlier calls did not complete to its read's end;
+        // a call whose growth fails gives the connection to the walk
+        uint32_t calls = 1;
+        if (ok && K <= 1) {
+            ok = grow_recv(st.len, st.recv_buffer_size, st.max_frame_size, &size);
+        } else if (ok) {
+            const uint64_t* re = a.read_end + st.first_read;
+            uint64_t prev = 0;
+            for (uint32_t k = 0; k < K && ok; ++k) {
+                const uint64_t end = re[k];
+                const uint64_t done = L ? prev / L : 0u;  // frames the earlier calls completed
+                const uint64_t pos = (done < N ? done : N) * (uint64_t)L;
+                ok = end >= prev && end <= st.len && grow_recv(end - pos, size, st.max_frame_size, &size);
+                prev = end;
+            }
+            calls = K;
         }
         if (!ok) N = L = 0;
         SpecConn c;
@@ -4306,7 +4339,8 @@ __global__ __launch_bounds__(kBlock) void k_sspec_plan(SpecArgs a) {
         c.local = 0;
         c.mf = st.max_frame_size;
         c.is_server = (uint32_t)st.is_server;
-        c.pad[0] = c.pad[1] = c.pad[2] = 0;
+        c.pad[0] = calls;
+        c.pad[1] = c.pad[2] = 0;
         a.conns[s] = c;
         // the tiles this connection's frames touch (the tile of its begin and every tile
         // starting inside its frames)
@@ -4320,37 +4354,41 @@ __global__ __launch_bounds__(kBlock) void k_sspec_plan(SpecArgs a) {
     uint32_t total;
     const uint32_t local = block_scan_u32(N, &total);
     if (s < a.n_streams) a.conns[s].local = local;
-    // the last block to finish turns the blocks' counts into first frames
-    __shared__ uint32_t s_last;
-    if (threadIdx.x == 0) {
-        a.blk[blockIdx.x] = total;
-        __threadfence();
-        const uint32_t done = atomicAdd(&a.ctl[kCtlSpecDone], 1u);
-        s_last = done == gridDim.x - 1;
-    }
-    __syncthreads();
-    if (!s_last) return;
-    __threadfence();
+    // (the blocks' counts become first frames in k_sspec_tiles, which every later kernel follows:
+    // a last-block scan here — a fence and an atomic per block — cost the plan about 3 us)
+    if (threadIdx.x == 0) a.blk[blockIdx.x] = total;
+}
+
+// exclusive prefixes of the plan blocks' frame counts in LDS (every thread), and their total
+__device__ inline uint64_t spec_blk_prefix(const SpecArgs& a, uint32_t* s_pre) {
     uint64_t base = 0;
     for (uint32_t b0 = 0; b0 < a.n_blk; b0 += kBlock) {
         const uint32_t j = b0 + threadIdx.x;
-        const uint32_t v = j < a.n_blk ? __hip_atomic_load(&a.blk[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        const uint32_t v = j < a.n_blk ? a.blk[j] : 0u;
         uint64_t tot;
         const uint64_t pre = block_exclusive_sum_u64(v, &tot);
-        if (j < a.n_blk) a.blk[j] = (uint32_t)(base + pre);
+        if (j < a.n_blk) s_pre[j] = (uint32_t)(base + pre);
         base += tot;
         __syncthreads();
     }
-    if (threadIdx.x == 0) {
-        if (base > a.max_frames) a.ctl[kCtlSpecOff] = epoch;  // (ERR_CAPACITY: the walk reports it)
-        a.ctl[kCtlSpecDone] = 0;
-    }
+    return base;
 }
+constexpr uint32_t kSpecMaxBlk = 4096;  // plan blocks (1 M connections) the LDS prefix holds
 
-// a thread per claimed tile (after k_sspec_plan: connections, first frames, claims)
+// a thread per claimed tile (after k_sspec_plan: connections and claims); every workgroup scans
+// the plan blocks' frame counts (the first frames; workgroup 0 leaves them in blk_pre for the
+// pass's general path and k_sspec_emit) and checks the capacity
 __global__ __launch_bounds__(kBlock) void k_sspec_tiles(SpecArgs a) {
     const uint32_t epoch = spec_epoch(a);
     if (a.ctl[kCtlSpecOff] == epoch) return;
+    __shared__ uint32_t s_pre[kSpecMaxBlk];
+    const uint64_t total = spec_blk_prefix(a, s_pre);
+    if (total > a.max_frames) {  // (ERR_CAPACITY: the walk reports it)
+        if (threadIdx.x == 0) a.ctl[kCtlSpecOff] = epoch;
+        return;
+    }
+    if (blockIdx.x == 0)
+        for (uint32_t j = threadIdx.x; j < a.n_blk; j += kBlock) a.blk_pre[j] = s_pre[j];
     const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (t >= a.n_tiles) return;
     const uint32_t c0 = tag_get(a.conn_tile[t], epoch, kNoFrame);
@@ -4369,14 +4407,14 @@ __global__ __launch_bounds__(kBlock) void k_sspec_tiles(SpecArgs a) {
     spec_range(s0.b, s0.L, s0.N, t0, r.c[0].ka, r.c[0].cnt);
     r.c[0].b = s0.b;
     r.c[0].L = s0.L;
-    r.c[0].first = a.blk[c0 / kBlock] + s0.local + r.c[0].ka;
+    r.c[0].first = s_pre[c0 / kBlock] + s0.local + r.c[0].ka;
     r.c[1].b = 0;
     r.c[1].L = r.c[1].ka = r.c[1].cnt = r.c[1].first = 0;
     if (in1) {
         spec_range(s1.b, s1.L, s1.N, t0, r.c[1].ka, r.c[1].cnt);
         r.c[1].b = s1.b;
         r.c[1].L = s1.L;
-        r.c[1].first = a.blk[(c0 + 1) / kBlock] + s1.local + r.c[1].ka;
+        r.c[1].first = s_pre[(c0 + 1) / kBlock] + s1.local + r.c[1].ka;
         if (s1.is_server) flags |= kStSrv1;
     }
     if (r.c[0].cnt + r.c[1].cnt > kSpecMaxF) flags |= kStMore;
@@ -4469,7 +4507,7 @@ __device__ inline void sspec_tile(const SpecArgs& a, uint64_t tile, uint32_t epo
                 s_cb[lane] = sc.b;
                 s_cL[lane] = sc.L;
                 s_cka[lane] = ka;
-                s_cfirst[lane] = sc.N ? a.blk[c / kBlock] + sc.local : 0u;
+                s_cfirst[lane] = sc.N ? a.blk_pre[c / kBlock] + sc.local : 0u;
                 s_csrv[lane] = sc.is_server;
                 s_cpre[lane + 1] = inc;
             }
@@ -4646,7 +4684,7 @@ __global__ __launch_bounds__(kBlock) void k_sspec_emit(SpecArgs a) {
     const uint32_t s = stamp_.anchor_s(blockIdx.x * (kBlock / 64) + wave);
     if (s >= a.n_streams) return;
     const SpecConn sc = a.conns[s];
-    const uint32_t first = a.blk[s / kBlock] + sc.local;
+    const uint32_t first = a.blk_pre[s / kBlock] + sc.local;
     bool open = sc.pending != 0;
     uint64_t acc = sc.pending;
     uint32_t msg = 0;
@@ -4711,7 +4749,7 @@ __global__ __launch_bounds__(kBlock) void k_sspec_emit(SpecArgs a) {
         r.n_delivered = sc.N;
         r.status = 0;
         r.first_status = 0;
-        r.calls = 1;
+        r.calls = sc.pad[0];
         r.consumed_bytes = (uint64_t)sc.N * sc.L;
         r.recv_buffer_size = sc.size;
         r.pending_bytes = open ? acc : 0u;
@@ -5615,7 +5653,7 @@ struct uvhttp_ws_gpu_engine {
     int stream_nt;             // UVHTTP_WS_STREAM_NT=1: streaming stores in the walk and k_stream_desc (A/B)
     int desc_scan_off;         // UVHTTP_WS_DESC_SCAN=0: k_swalk_scan before k_stream_desc always (A/B)
     int walk_nt_load;          // UVHTTP_WS_WALK_NT_LOAD=1: non-temporal header loads in the wave walk (A/B)
-    int stream_spec;           // single-read stream calls try the speculative decode first (k_sspec_*;
+    int stream_spec;           // stream calls try the speculative decode first (k_sspec_*;
                                // UVHTTP_WS_STREAM_SPEC=0: the walk always)
     void* sp_mem;              // its scratch: SpecConn per connection, block counts, tile claims
     uint32_t sp_streams;
@@ -6765,7 +6803,7 @@ static int reserve_spec(uvhttp_ws_gpu_engine_t* e, uint32_t streams, uint64_t ti
     const uint32_t ns = streams > e->sp_streams ? streams : e->sp_streams;
     const uint64_t nt = tiles > e->sp_tiles ? tiles : e->sp_tiles;
     const size_t o_blk = align_up((size_t)ns * sizeof(SpecConn), 256);
-    const size_t o_tile = align_up(o_blk + ((size_t)ns / kBlock + 2) * 4, 256);
+    const size_t o_tile = align_up(o_blk + ((size_t)ns / kBlock + 2) * 8, 256);  // (counts, prefixes)
     const size_t o_trec = align_up(o_tile + (size_t)(nt + 1) * 8, 256);
     const size_t bytes = align_up(o_trec + (size_t)(nt + 1) * sizeof(SpecTile), 256);
     int prev = 0;
@@ -6821,12 +6859,13 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     hipStream_t s = (hipStream_t)stream;
 
     // a wave per connection when the waves fill the chip in about one round, else a lane
-    // (UVHTTP_WS_WALK=lane|wave pins it).  Behind a speculative attempt (below) the walk path is
-    // the fall-back, and its kernels are launched whether it runs or not: the lane walk and
-    // k_stream_desc_lane, whose grids are 64 times smaller, so the launches that return at once
-    // cost less (C4 streams: 1024 + 1024 workgroups against 16 + 16)
-    const bool spec_try = e->stream_spec && !d_read_end && wire_len > 0 && (uint64_t)max_frames >= 8ull * n_streams;
-    const bool wave_walk = e->walk_mode ? e->walk_mode == 2 : (n_streams <= 16384 && !spec_try);
+    // (UVHTTP_WS_WALK=lane|wave pins it).  (Behind a speculative attempt, below, the walk path is
+    // the fall-back, launched whether it runs or not; the lane walk's 64 times smaller grids
+    // return at once a few us sooner, but as the fall-back of long connections it took C4 streams
+    // 848 us per step instead of 139: the same rule as without the attempt.)
+    const bool spec_try = e->stream_spec && wire_len > 0 && (uint64_t)max_frames >= 8ull * n_streams &&
+                          (n_streams + kBlock - 1) / kBlock <= kSpecMaxBlk;
+    const bool wave_walk = e->walk_mode ? e->walk_mode == 2 : n_streams <= 16384;
     // single pass (starts written into per-connection slices) unless UVHTTP_WS_WALK_SINGLE=0.
     // (The idle between calls of some C2 stream runs, DESIGN.md §5, is not the slices: with
     // the lane walk in two passes and no slice scratch, 2 of 10 runs idled all the same, r03p51.)
@@ -6876,7 +6915,7 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     const uint32_t nsb = (n_streams + kBlock - 1) / kBlock;
     const uint32_t nwb = (n_streams + kBlock / 64 - 1) / (kBlock / 64);
     const int tk_chain = e->time_chain ? timing_begin(e, s) : -1;
-    // single-read calls whose connections carry several frames each (by the caller's frame
+    // calls whose connections carry several frames each (by the caller's frame
     // capacity): the speculative decode first, the walk path behind it (gated)
     const uint64_t sp_tiles = (wire_len + kSpecT - 1) / kSpecT;
     const bool spec = spec_try && reserve_spec(e, n_streams, sp_tiles, s) == UVHTTP_WS_GPU_OK;
@@ -6890,14 +6929,17 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
         sa.streams = d_streams;
         sa.n_streams = n_streams;
         sa.max_frames = max_frames;
+        sa.read_end = d_read_end;
+        sa.n_reads_total = n_reads_total;
         char* sb = (char*)e->sp_mem;
         sa.conns = (SpecConn*)sb;
         sa.blk = (uint32_t*)(sb + align_up((size_t)e->sp_streams * sizeof(SpecConn), 256));
+        sa.blk_pre = sa.blk + ((size_t)e->sp_streams / kBlock + 2);
         sa.n_blk = nsb;
         sa.conn_tile = (uint64_t*)(sb + align_up(align_up((size_t)e->sp_streams * sizeof(SpecConn), 256) +
                                                      ((size_t)e->sp_streams / kBlock + 2) * 4, 256));
         sa.tiles = (SpecTile*)(sb + align_up(align_up(align_up((size_t)e->sp_streams * sizeof(SpecConn), 256) +
-                                                            ((size_t)e->sp_streams / kBlock + 2) * 4, 256) +
+                                                            ((size_t)e->sp_streams / kBlock + 2) * 8, 256) +
                                                    (size_t)(e->sp_tiles + 1) * 8, 256));
         sa.n_tiles = sp_tiles;
         sa.recs = reinterpret_cast<FrameRec*>(e->ws.recs);
