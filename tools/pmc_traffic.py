@@ -14,7 +14,7 @@ import statistics
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ("k_unmask_inplace", "k_gather_compact", "k_scatter_compact", "k_unmask_stride", "kb_emit")
+KERNELS = ("k_unmask_inplace", "k_gather_compact", "k_scatter_compact", "k_unmask_stride", "kb_emit", "k_sspec_pass")
 # written under gpurun_out/ (the only directory merged back from the GPU box); copy the
 # files into profiles/ to commit them
 EVID = os.path.join(REPO, "gpurun_out", "evidence")

@@ -83,3 +83,8 @@ if has walkcmp; then
     python -c "import json,sys; d=json.load(open('${O}_walkcmp.json')); t=d.get('device_timeline') or {}; print('[$v]', d['value'], d['ms_per_step'], t.get('kernels_us'))"
   done
 fi
+if has prof; then
+  for cm in ${PROFS:-c3:inplace c4:inplace c4:compact c4:streams}; do
+    TAG=r06${TAG} tools/profile.sh ${cm%%:*} ${cm##*:}
+  done
+fi
