@@ -87,7 +87,8 @@ def test_lookback_give_up_is_reported(torch):
         eng.sync()
     # the stream decode has no look-back (per-connection walk + one-block scan) unless the wave
     # walk runs fused (UVHTTP_WS_WALK_FUSE=1: k_swalk_fused finds first frames by a look-back
-    # over blocks of connections).  Fused, every block after the first gives up, so every
+    # over blocks of connections; the speculative decode, which has none and would take these
+    # connections first, is off).  Fused, every block after the first gives up, so every
     # stream reports ERR_DEVICE and nothing is unmasked ...
     st = np.zeros(64, U.STREAM_DT)
     per = w.size // 64
@@ -97,7 +98,7 @@ def test_lookback_give_up_is_reported(torch):
         st[k] = (cut[k], cut[k + 1] - cut[k], 1 << 30, 0, 0, 1 << 24, 1 << 26, 1, 0, 0, 0)
     sdev = torch.from_numpy(st.view(np.uint8).copy()).to("cuda")
     eng.close()
-    eng = _engine({"UVHTTP_WS_MAX_POLLS": "0", "UVHTTP_WS_WALK_FUSE": "1"})
+    eng = _engine({"UVHTTP_WS_MAX_POLLS": "0", "UVHTTP_WS_WALK_FUSE": "1", "UVHTTP_WS_STREAM_SPEC": "0"})
     d2 = before.clone()
     _, res = eng.decode_streams(d2, sdev, 64, 8192, wire_len=w.size)
     torch.cuda.synchronize()

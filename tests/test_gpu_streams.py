@@ -28,19 +28,22 @@ def torch():
 
 
 @pytest.fixture(scope="module", params=["lane", "lane-twopass", "wave", "wave-norec", "wave-twopass",
-                                        "wave-fuse", "wave-fuse-norec"])
+                                        "wave-fuse", "wave-fuse-norec", "wave-spec"])
 def eng(torch, request):
     """Every frame-discovery walk (a lane per connection, single pass or two walks; a wave per
     connection, single pass
     through the offset scratch — with the fast path's frame records or re-reading every header
     for the descriptors; in one launch (k_swalk_fused) or with the scan and k_stream_desc
-    apart — or the two-walk fallback) must decode alike."""
+    apart — or the two-walk fallback) must decode alike, and so must the default engine, whose
+    speculative decode takes the calls of connections with several equal frames first (the walk
+    variants run with it off, so that they see every call)."""
     import os
     import uvhttp_amd as U
     env = {"UVHTTP_WS_WALK": request.param.split("-")[0],
            "UVHTTP_WS_WALK_SINGLE": "0" if request.param.endswith("twopass") else "1",
            "UVHTTP_WS_WALK_REC": "0" if request.param.endswith("norec") else "1",
-           "UVHTTP_WS_WALK_FUSE": "1" if "-fuse" in request.param else "0"}
+           "UVHTTP_WS_WALK_FUSE": "1" if "-fuse" in request.param else "0",
+           "UVHTTP_WS_STREAM_SPEC": "1" if request.param.endswith("spec") else "0"}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:

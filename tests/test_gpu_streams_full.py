@@ -8,7 +8,8 @@ decode (uvhttp_ws_gpu_decode_streams / _decode_reads) at full size:
 * C2 / C3 as 65 536 connections of one 4 KiB / 64 KiB frame each (the lane walk, which the
   engine picks above 16 384 connections; C2 also forced onto the wave walk);
 * C4 as 4 096 connections x 256 frames, every connection continuing the one 256 MiB message
-  (pending_bytes carried: the wave walk; also forced onto the lane walk);
+  (pending_bytes carried: the speculative decode, k_sspec_*; also with it off on the lane walk
+  and, in 16 KiB reads, the wave walk);
 * each as ONE process_data call per connection and cut into 16 KiB libuv reads (C2 also into
   1000-byte reads, so headers straddle calls).
 
@@ -37,7 +38,7 @@ FULL = {  # frames, payload bytes, connections, fragmented (one message over all
 CASES = [
     ("c2", "auto", None), ("c2", "auto", 16384), ("c2", "auto", 1000), ("c2", "wave", None),
     ("c3", "auto", None), ("c3", "auto", 16384),
-    ("c4", "auto", None), ("c4", "auto", 16384), ("c4", "lane", None),
+    ("c4", "auto", None), ("c4", "auto", 16384), ("c4", "lane", None), ("c4", "wave", 16384),
 ]
 
 
@@ -50,17 +51,20 @@ def torch():
 
 
 def _engine(walk):
+    """auto: the default engine (C4's connections go to the speculative decode); a named walk
+    runs with the speculation off, so that the walk decodes every call"""
     import uvhttp_amd as U
-    old = os.environ.get("UVHTTP_WS_WALK")
-    if walk != "auto":
-        os.environ["UVHTTP_WS_WALK"] = walk
+    env = {} if walk == "auto" else {"UVHTTP_WS_WALK": walk, "UVHTTP_WS_STREAM_SPEC": "0"}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         return U.GpuEngine(0)
     finally:
-        if old is None:
-            os.environ.pop("UVHTTP_WS_WALK", None)
-        else:
-            os.environ["UVHTTP_WS_WALK"] = old
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
 
 
 def _layout(cfg, read):

@@ -243,7 +243,7 @@ struct Workspace {
                            // did not place (its arena offset or layout is not the uniform one)
     uint64_t* arena_first; // [n_arena_tiles]: tagged first data frame of the arena tile
     uint32_t* ctl;         // control words outside the clearable workspace (see kCtl*)
-    void* recs;            // [n_frames] FrameRec: the fused stride path's parsed headers
+    void* recs;            // [n_frames] FrameRec8: the payload passes' records, or info bytes
     void* parts;           // [n_frames / 1024 + 2] TilePart: per k_sum_scan block (4 frames a thread)
     uint8_t* info;         // [n_frames + 64]: info bytes beside the records (k_desc_emit's decode)
 };
@@ -315,8 +315,9 @@ struct StreamScratch {
     void* srec;            // [2 kSwalkFusedMaxBlocks] k_swalk_fused look-back records (A, P per block)
 };
 
-// parse_hdr's result for one frame, 16 bytes (stride batches: written by the payload pass,
-// read by k_plan and k_fixup instead of the headers).  flags bit 7 (kRecHasLen): the header
+// parse_hdr's result for one frame, 16 bytes: the in-register form of a frame record (the
+// payload passes store it packed, FrameRec8 below; k_plan, k_fixup, the scans and the
+// descriptor passes read those instead of the headers).  flags bit 7 (kRecHasLen): the header
 // parsed to a wire length (then payload_off / wire_len follow from header_size and the mask).
 struct alignas(16) FrameRec {
     uint64_t payload_len;
@@ -326,6 +327,53 @@ struct alignas(16) FrameRec {
 };
 static_assert(sizeof(FrameRec) == 16, "one 16-byte load per record");
 constexpr uint8_t kRecHasLen = 0x80;
+
+// What the payload passes actually write per frame: 8 bytes — the masking key and one packed
+// word — for a frame that parsed OK to a wire length with a payload under 2^23 bytes (every
+// delivered frame of a fused stride batch or of a speculated connection).  Any other frame is
+// written as kR8Esc and its reader parses the header from the wire again (rec_at: stride
+// batches leave headers untouched; the speculative stream decode never reads one — such a
+// frame breaks the speculation).  Packed word: payload_len [0, 23), opcode [23, 27), FIN [27],
+// MASK [28], header-size code [29, 31) (hs >> 2: 2 / 4 / 10 bytes), kR8Esc [31].  (16-byte
+// records cost C4 in place 50 MB of its 643 MB step traffic — written by the pass, read by the
+// scan and the descriptor pass; 8-byte ones: whole-step traffic 1.181 -> 1.135 x in place,
+// 1.150 -> 1.119 compact, 1.163 -> 1.132 streams, step times within 1 % either way,
+// profiles/r06x7_*, traffic_c4_*.json.  A 16-byte side record stored by the pass for escaped
+// frames — one conditional store in the parse loop — cost the speculative stream pass 11 us
+// on C4: profiles/r06x5_*, r06x_*.)
+struct alignas(8) FrameRec8 {
+    uint32_t key;
+    uint32_t w;
+};
+static_assert(sizeof(FrameRec8) == 8, "one 8-byte load per record");
+constexpr uint32_t kR8Esc = 1u << 31, kR8LenBits = 23;
+
+__device__ inline FrameRec8 rec8_pack(const FrameRec& r) {
+    const bool simple = r.status == UVHTTP_WS_FRAME_OK && (r.flags & kRecHasLen) &&
+                        !(r.flags & ~(kRecHasLen | UVHTTP_WS_FLAG_FIN | UVHTTP_WS_FLAG_MASK)) &&
+                        r.payload_len < (1ull << kR8LenBits) && r.opcode < 16 &&
+                        (r.header_size == 2 || r.header_size == 4 || r.header_size == 10);
+    FrameRec8 p;
+    p.key = r.masking_key;
+    p.w = simple ? ((uint32_t)r.payload_len | ((uint32_t)r.opcode << 23) | ((uint32_t)(r.flags & 3u) << 27) |
+                    ((uint32_t)(r.header_size >> 2) << 29))
+                 : kR8Esc;
+    return p;
+}
+
+// a simple record's fields (false: escaped, the caller re-parses the header)
+__device__ inline bool rec8_unpack(const FrameRec8& p, FrameRec& r) {
+    r.payload_len = p.w & ((1u << kR8LenBits) - 1);
+    r.masking_key = p.key;
+    r.opcode = (uint8_t)((p.w >> 23) & 0xF);
+    r.flags = (uint8_t)(kRecHasLen | ((p.w >> 27) & 3u));
+    const uint32_t hc = (p.w >> 29) & 3u;
+    r.header_size = (uint8_t)(hc == 0 ? 2 : hc == 1 ? 4 : 10);
+    r.status = UVHTTP_WS_FRAME_OK;
+    return !(p.w & kR8Esc);
+}
+
+__device__ inline void rec8_store(FrameRec8* r8, uint32_t i, const FrameRec& r) { r8[i] = rec8_pack(r); }
 
 // Summary-only decode (uvhttp_ws_gpu_decode_inplace with d_desc == NULL, stride batches): what
 // the batch summary needs from a run of consecutive frames, in frame order, up to the run's
@@ -380,7 +428,7 @@ struct BatchArgs {
     const uint64_t* frame_off;
     uint64_t frame_stride;
     double stride_inv;        // 1 / frame_stride (stride batches: frame index by multiply)
-    FrameRec* recs;           // stride batches decoded by the fused path (else null)
+    FrameRec8* recs;          // stride batches decoded by the fused path (else null); summary-only: info bytes
     uint32_t n;
     int32_t max_frame_size;
     int32_t max_message_size;
@@ -730,6 +778,29 @@ __device__ inline FrameRec rec_of(const uvhttp_ws_frame_desc_t& d) {
     return r;
 }
 
+// the 8-byte record straight from a parsed descriptor (rec8_pack(rec_of(d)), fewer steps in
+// the payload pass's parse loop)
+__device__ inline FrameRec8 rec8_of_desc(const uvhttp_ws_frame_desc_t& d) {
+    const uint32_t hs = d.header_size;
+    const bool simple = d.status == UVHTTP_WS_FRAME_OK && d.wire_len && !(d.flags & ~3u) &&
+                        d.payload_len < (1ull << kR8LenBits) && (hs == 2 || hs == 4 || hs == 10);
+    FrameRec8 p;
+    p.key = d.masking_key;
+    p.w = simple ? ((uint32_t)d.payload_len | ((uint32_t)d.opcode << 23) | ((uint32_t)d.flags << 27) | ((hs >> 2) << 29))
+                 : kR8Esc;
+    return p;
+}
+
+// frame i's record in a stride batch: the payload pass's, or — escaped — its header parsed again
+// from the wire (the pass's parse_hdr on the same bytes)
+__device__ inline FrameRec rec_at(const BatchArgs& a, const FrameRec8& p, uint32_t i) {
+    FrameRec r;
+    if (rec8_unpack(p, r)) return r;
+    uvhttp_ws_frame_desc_t d;
+    (void)parse_one(a, i, seg_info(a, i, a.n), d);
+    return rec_of(d);
+}
+
 // the descriptor parse_hdr wrote for the frame at o, rebuilt from its record
 __device__ inline void desc_of_rec(const FrameRec& r, uint64_t o, uvhttp_ws_frame_desc_t& d) {
     const bool has_len = r.flags & kRecHasLen;
@@ -1034,7 +1105,7 @@ template <int FPT>
 __device__ inline ScanElem rec_pass1(const BatchArgs& a, uint32_t i0, uint32_t n,
                                      uvhttp_ws_frame_desc_t (&dv)[FPT]) {
     ScanElem tagg = scan_identity();
-    FrameRec r[FPT];
+    FrameRec8 r[FPT];
     const uint32_t ilast = n ? n - 1 : 0;
 #pragma unroll
     for (int k = 0; k < FPT; ++k) r[k] = a.recs[i0 + k < n ? i0 + k : ilast];
@@ -1042,7 +1113,7 @@ __device__ inline ScanElem rec_pass1(const BatchArgs& a, uint32_t i0, uint32_t n
     for (int k = 0; k < FPT; ++k) {
         const uint32_t i = i0 + k;
         if (i < n) {
-            desc_of_rec(r[k], (uint64_t)i * a.frame_stride, dv[k]);
+            desc_of_rec(rec_at(a, r[k], i), (uint64_t)i * a.frame_stride, dv[k]);
             tagg = scan_combine(tagg, elem_of_parsed(dv[k], i, i == 0));
         }
     }
@@ -1131,50 +1202,21 @@ __global__ __launch_bounds__(NT) void k_plan(BatchArgs a, uvhttp_ws_frame_desc_t
     auto phase = [](int) {};
 #endif
     if constexpr (REC) {
-        // records path: the lane's 16-byte records stay in registers across the scan (64
-        // registers; the 32-byte descriptors built from them took 128 and spilled at 16 frames
-        // per lane) and pass 2 rebuilds each descriptor from its record
+        // records path: the lane's 8-byte records stay in registers across the scan (the
+        // 32-byte descriptors built from them took 128 registers and spilled at 16 frames per
+        // lane) and pass 2 rebuilds each descriptor from its record.  (Coalesced record loads
+        // handed to their owner lanes through LDS measured no faster: profiles/r03p49_*.)
         ScanElem tagg = scan_identity();
-        FrameRec r[FPT];
+        FrameRec8 r[FPT];
         const uint32_t ilast = n ? n - 1 : 0;
-#ifdef UVWS_REC_LDS
-        if constexpr (FPT == 16 && NT == kBlock) {
-            // experiment: coalesced record loads (load k of a wave reads 64 consecutive records),
-            // handed to their owner lanes through LDS (one pad vector per 16 records keeps the
-            // owner reads, 272 bytes apart, off a single bank)
-            __shared__ u32x4 s_rec[NT / 64][64 * FPT + 64];
-            const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-            const uint32_t wbase = (b * NT + wv * 64) * FPT;
-            const u32x4* rv = reinterpret_cast<const u32x4*>(a.recs);
-            u32x4 tmp[FPT];
 #pragma unroll
-            for (int k = 0; k < FPT; ++k) {
-                const uint32_t idx = wbase + k * 64 + lane;
-                tmp[k] = rv[idx < n ? idx : ilast];
-            }
-#pragma unroll
-            for (int k = 0; k < FPT; ++k) {
-                const uint32_t j = k * 64 + lane;
-                s_rec[wv][j + (j >> 4)] = tmp[k];
-            }
-            __syncthreads();
-#pragma unroll
-            for (int k = 0; k < FPT; ++k) {
-                const u32x4 v = s_rec[wv][lane * 17 + k];
-                __builtin_memcpy(&r[k], &v, sizeof v);
-            }
-        } else
-#endif
-        {
-#pragma unroll
-            for (int k = 0; k < FPT; ++k) r[k] = a.recs[i0 + k < n ? i0 + k : ilast];
-        }
+        for (int k = 0; k < FPT; ++k) r[k] = a.recs[i0 + k < n ? i0 + k : ilast];
 #pragma unroll
         for (int k = 0; k < FPT; ++k) {
             const uint32_t i = i0 + k;
             if (i < n) {
                 uvhttp_ws_frame_desc_t d;
-                desc_of_rec(r[k], (uint64_t)i * a.frame_stride, d);
+                desc_of_rec(rec_at(a, r[k], i), (uint64_t)i * a.frame_stride, d);
                 tagg = scan_combine(tagg, elem_of_parsed(d, i, i == 0));
             }
         }
@@ -1189,7 +1231,7 @@ __global__ __launch_bounds__(NT) void k_plan(BatchArgs a, uvhttp_ws_frame_desc_t
             const uint32_t i = i0 + k;
             if (i < n) {
                 uvhttp_ws_frame_desc_t d;
-                desc_of_rec(r[k], (uint64_t)i * a.frame_stride, d);
+                desc_of_rec(rec_at(a, r[k], i), (uint64_t)i * a.frame_stride, d);
                 const SegInfo g = seg_info(a, i, n);
                 const ScanElem e = elem_of_parsed(d, i, g.head);
                 resolve_one(a, msgs, ws, i, n, g, run, d);
@@ -1207,7 +1249,7 @@ __global__ __launch_bounds__(NT) void k_plan(BatchArgs a, uvhttp_ws_frame_desc_t
         if (i0 < n) {
             g = seg_info(a, i0, n);
             if (a.recs) {  // fused stride path: the payload pass parsed the header already
-                desc_of_rec(a.recs[i0], frame_start(a, i0), d);
+                desc_of_rec(rec_at(a, a.recs[i0], i0), frame_start(a, i0), d);
                 elem = elem_of_parsed(d, i0, g.head);
             } else {
                 elem = parse_one(a, i0, g, d);
@@ -1875,7 +1917,7 @@ __global__ __launch_bounds__(BLOCK) void k_unmask_stride(BatchArgs a, Workspace 
             if constexpr (SUM == kLeaveInfo) {
                 reinterpret_cast<uint8_t*>(a.recs)[f] = info8_of(d);
             } else {
-                a.recs[f] = rec_of(d);
+                a.recs[f] = rec8_of_desc(d);
                 if constexpr (SUM == kLeaveBoth) ws.info[f] = info8_of(d);
             }
         }
@@ -2078,7 +2120,7 @@ __global__ __launch_bounds__(kBlock) void k_fixup(BatchArgs a, uvhttp_ws_frame_d
         if (i > nb || fault) skip_desc(a, desc, i);
     const uint64_t wave = tid >> 6, nwaves = nthreads >> 6;
     for (uint64_t i = nb + wave; i < n; i += nwaves) {
-        const FrameRec r = a.recs[i];
+        const FrameRec r = rec_at(a, a.recs[i], (uint32_t)i);
         if (r.status != UVHTTP_WS_FRAME_OK || r.payload_len == 0) continue;  // not unmasked
         uvhttp_ws_frame_desc_t d;
         desc_of_rec(r, i * a.frame_stride, d);
@@ -2149,11 +2191,14 @@ __device__ inline bool i8_uniform(uint32_t x, uint64_t D) {
     return (x & kI8Data) && kHm[x >> kI8HmShift] == D;
 }
 
-// the info byte of frame f from its 16-byte record (k_desc_emit's scan over the records)
+// the info byte of frame f from its record (k_desc_emit's scan over the records)
 __device__ inline uint32_t info_of_rec(const FrameRec& r, uint64_t S, uint32_t f) {
     uvhttp_ws_frame_desc_t d;
     desc_of_rec(r, (uint64_t)f * S, d);
     return info8_of(d);
+}
+__device__ inline uint32_t info_of_rec(const BatchArgs& a, const FrameRec8& p, uint64_t S, uint32_t f) {
+    return info_of_rec(rec_at(a, p, f), S, f);
 }
 
 template <bool COMPACT, uint32_t KIND = UVHTTP_WS_STAMP_PLAN, bool FROM_REC = false>
@@ -2167,12 +2212,12 @@ __global__ __launch_bounds__(kBlock) void k_sum_scan(BatchArgs a, Workspace ws) 
     const uint32_t F0 = (blockIdx.x * kBlock + threadIdx.x) * kScanFpt;
     uint32_t w = 0u;
     if constexpr (FROM_REC) {  // the info bytes rebuilt from the thread's 4 records (64 B)
-        FrameRec r[kScanFpt];
+        FrameRec8 r[kScanFpt];
 #pragma unroll
         for (uint32_t k = 0; k < kScanFpt; ++k) r[k] = a.recs[F0 + k < n ? F0 + k : n - 1];
 #pragma unroll
         for (uint32_t k = 0; k < kScanFpt; ++k)
-            if (F0 + k < n) w |= info_of_rec(r[k], S, F0 + k) << (8 * k);
+            if (F0 + k < n) w |= info_of_rec(a, r[k], S, F0 + k) << (8 * k);
     } else {
         // (info bytes past n are never used; the buffer holds at least n + 16)
         w = F0 < n ? *reinterpret_cast<const uint32_t*>(info + F0) : 0u;
@@ -2180,7 +2225,7 @@ __global__ __launch_bounds__(kBlock) void k_sum_scan(BatchArgs a, Workspace ws) 
     // the frame before this thread's first: the previous lane's last byte (lane 0: a load)
     const uint32_t up = __shfl_up(w, 1, 64);
     uint32_t pb = (threadIdx.x & 63) ? up >> 24
-                                     : (F0 > 0 && F0 < n ? (FROM_REC ? info_of_rec(a.recs[F0 - 1], S, F0 - 1)
+                                     : (F0 > 0 && F0 < n ? (FROM_REC ? info_of_rec(a, a.recs[F0 - 1], S, F0 - 1)
                                                                      : (uint32_t)info[F0 - 1])
                                                          : 0u);
     TilePart acc = part_identity();
@@ -2202,7 +2247,7 @@ __global__ __launch_bounds__(kBlock) void k_sum_scan(BatchArgs a, Workspace ws) 
                 }
                 --g;
                 const uint32_t gi = g >= F0 ? (w >> (8 * (g - F0))) & 0xFF
-                                            : FROM_REC ? info_of_rec(a.recs[g], S, g) : (uint32_t)info[g];
+                                            : FROM_REC ? info_of_rec(a, a.recs[g], S, g) : (uint32_t)info[g];
                 if (!(gi & kI8Ok)) {  // a failure before f decides the batch anyway
                     p = 0u;
                     break;
@@ -2453,18 +2498,18 @@ __global__ __launch_bounds__(kBlock) void k_sum_msgs(BatchArgs a, Workspace ws, 
     // (DESC without FROM_REC: records in a.recs, the payload pass's info bytes in ws.info)
     const uint8_t* info_b = (DESC && !FROM_REC) ? ws.info : reinterpret_cast<const uint8_t*>(a.recs);
     auto info_at = [&](uint32_t f) -> uint32_t {
-        if constexpr (FROM_REC) return info_of_rec(a.recs[f], S, f);
+        if constexpr (FROM_REC) return info_of_rec(a, a.recs[f], S, f);
         else return info_b[f];
     };
     const uint32_t F0 = (blockIdx.x * kBlock + threadIdx.x) * kScanFpt;
     uint32_t w = 0u;
     if constexpr (FROM_REC) {
-        FrameRec r4[kScanFpt];
+        FrameRec8 r4[kScanFpt];
 #pragma unroll
         for (uint32_t k = 0; k < kScanFpt; ++k) r4[k] = a.recs[F0 + k < n ? F0 + k : n - 1];
 #pragma unroll
         for (uint32_t k = 0; k < kScanFpt; ++k)
-            if (F0 + k < n) w |= info_of_rec(r4[k], S, F0 + k) << (8 * k);
+            if (F0 + k < n) w |= info_of_rec(a, r4[k], S, F0 + k) << (8 * k);
     } else {
         w = F0 < n ? *reinterpret_cast<const uint32_t*>(info_b + F0) : 0u;
     }
@@ -2514,10 +2559,18 @@ __global__ __launch_bounds__(kBlock) void k_sum_msgs(BatchArgs a, Workspace ws, 
         const uint32_t B0 = blockIdx.x * kBlock * kScanFpt;
         FrameRec r[kScanFpt];
         uint32_t x[kScanFpt];
+        {
+            FrameRec8 p[kScanFpt];
 #pragma unroll
-        for (uint32_t k = 0; k < kScanFpt; ++k) {
-            const uint32_t f = B0 + k * kBlock + threadIdx.x;
-            r[k] = a.recs[f < n ? f : n - 1];
+            for (uint32_t k = 0; k < kScanFpt; ++k) {
+                const uint32_t f = B0 + k * kBlock + threadIdx.x;
+                p[k] = a.recs[f < n ? f : n - 1];
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < kScanFpt; ++k) {
+                const uint32_t f = B0 + k * kBlock + threadIdx.x;
+                r[k] = rec_at(a, p[k], f < n ? f : n - 1);
+            }
         }
 #pragma unroll
         for (uint32_t k = 0; k < kScanFpt; ++k) {
@@ -2649,11 +2702,19 @@ __global__ __launch_bounds__(kBlock) void k_desc_emit(BatchArgs a, Workspace ws,
     FrameRec r[kScanFpt];
     uint32_t x[kScanFpt];
     const uint32_t ilast = n - 1;
+    {
+        FrameRec8 p[kScanFpt];
 #pragma unroll
-    for (uint32_t k = 0; k < kScanFpt; ++k) {
-        const uint32_t f = B0 + k * kBlock + threadIdx.x;
-        r[k] = a.recs[f < n ? f : ilast];
-        if constexpr (!FROM_REC) x[k] = f < n ? ws.info[f] : 0u;
+        for (uint32_t k = 0; k < kScanFpt; ++k) {
+            const uint32_t f = B0 + k * kBlock + threadIdx.x;
+            p[k] = a.recs[f < n ? f : ilast];
+            if constexpr (!FROM_REC) x[k] = f < n ? ws.info[f] : 0u;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kScanFpt; ++k) {
+            const uint32_t f = B0 + k * kBlock + threadIdx.x;
+            r[k] = rec_at(a, p[k], f < n ? f : ilast);
+        }
     }
     if constexpr (FROM_REC) {
 #pragma unroll
@@ -2701,7 +2762,7 @@ __global__ __launch_bounds__(kBlock) void k_desc_emit(BatchArgs a, Workspace ws,
     const uint32_t b1 = B0 + kBlock * kScanFpt < n ? B0 + kBlock * kScanFpt : n;
     const uint32_t wave = threadIdx.x >> 6;
     for (uint32_t i = (nb > B0 ? nb : B0) + wave; i < b1; i += kBlock / 64) {
-        const FrameRec rr = a.recs[i];
+        const FrameRec rr = rec_at(a, a.recs[i], i);
         if (rr.status != UVHTTP_WS_FRAME_OK || rr.payload_len == 0) continue;
         uvhttp_ws_frame_desc_t d;
         desc_of_rec(rr, (uint64_t)i * S, d);
@@ -4173,7 +4234,7 @@ struct SpecArgs {
     uint64_t* conn_tile;      // [n_tiles]: tagged first connection whose frames touch the tile
     struct SpecTile* tiles;   // [n_tiles]: what k_sspec_pass needs of the tile (k_sspec_plan)
     uint64_t n_tiles;
-    FrameRec* recs;           // [max_frames]
+    FrameRec8* recs;          // [max_frames]
     uvhttp_ws_frame_desc_t* desc;
     uvhttp_ws_stream_result_t* results;
     uint32_t* ctl;
@@ -4290,7 +4351,8 @@ __global__ __launch_bounds__(kBlock) void k_sspec_plan(SpecArgs a) {
                 L = (uint32_t)h.wl;
                 // (L - 2 <= max_frame_size: no frame of this length can fail TOO_BIG, so the
                 // pass checks the length alone)
-                ok = L >= kSpecMinL && (uint64_t)L - 2 <= (uint64_t)(int64_t)st.max_frame_size;
+                ok = L >= kSpecMinL && (uint64_t)L - 2 <= (uint64_t)(int64_t)st.max_frame_size &&
+                     L <= (1u << kR8LenBits);  // (every payload fits its 8-byte record)
                 N = ok ? (uint32_t)(st.len / L) : 0u;
                 const uint64_t rem = st.len - (uint64_t)N * L;
                 // the middle and the last speculated frame must be frames of length L too: a
@@ -4577,10 +4639,10 @@ __device__ inline void sspec_tile(const SpecArgs& a, uint64_t tile, uint32_t epo
             r.payload_len = h.plen;
             r.masking_key = h.key;
             r.opcode = (uint8_t)(h.b0 & 0x0F);
-            r.flags = (uint8_t)(((h.b0 >> 7) & 1) | ((h.b1 >> 7) << 1));
+            r.flags = (uint8_t)(((h.b0 >> 7) & 1) | ((h.b1 >> 7) << 1) | kRecHasLen);
             r.header_size = (uint8_t)h.hs;
             r.status = (int8_t)(good ? UVHTTP_WS_FRAME_OK : UVHTTP_WS_FRAME_ERR_LAYOUT);
-            a.recs[s_cfirst[l] + k] = r;
+            rec8_store(a.recs, s_cfirst[l] + k, r);
         }
         const uint64_t ps = o + h.hs + h.m;
         s_fr[j] = int4{rel_clamp(ps, t0, kT, true), rel_clamp(good ? ps + h.plen : ps, t0, kT, false),
@@ -4699,7 +4761,9 @@ __global__ __launch_bounds__(kBlock) void k_sspec_emit(SpecArgs a) {
         rec.flags = 0;
         rec.header_size = 2;
         rec.status = 0;
-        if (act) rec = a.recs[first + k];
+        // (an escaped record — a payload of 2^23 bytes or more — gives the call to the walk;
+        // the plan keeps L <= 2^23, so a speculated frame never has one)
+        const bool esc = act && !rec8_unpack(a.recs[first + k], rec);
         const bool data = act && rec.opcode <= 2;
         const bool fin = rec.flags & UVHTTP_WS_FLAG_FIN;
         const bool cont = rec.opcode == 0;
@@ -4709,7 +4773,7 @@ __global__ __launch_bounds__(kBlock) void k_sspec_emit(SpecArgs a) {
         const uint64_t dm = __ballot(data), om = __ballot(data && oa);
         const uint64_t prior = dm & below;
         const bool open_before = prior ? ((om >> (63 - __builtin_clzll(prior))) & 1) : open;
-        const bool fail = data && (cont ? !open_before : open_before);
+        const bool fail = esc || (data && (cont ? !open_before : open_before));
         if (__ballot(fail)) {  // the reference stops here: the walk reports it
             if (lane == 0) a.ctl[kCtlSpecBreak] = epoch;
             return;
@@ -4724,7 +4788,7 @@ __global__ __launch_bounds__(kBlock) void k_sspec_emit(SpecArgs a) {
             d.masking_key = rec.masking_key;
             d.message = data ? msg + (uint32_t)__builtin_popcountll(fm & below) : 0u;
             d.opcode = rec.opcode;
-            d.flags = (uint8_t)(rec.flags | (fin_data ? UVHTTP_WS_FLAG_MSG_END : 0u));
+            d.flags = (uint8_t)((rec.flags & ~kRecHasLen) | (fin_data ? UVHTTP_WS_FLAG_MSG_END : 0u));
             d.header_size = rec.header_size;
             d.status = UVHTTP_WS_FRAME_OK;
             d.wire_len = sc.L;
@@ -5959,7 +6023,7 @@ static int reserve_ws(uvhttp_ws_gpu_engine_t* e, uint32_t max_frames, uint64_t m
     size_t off_bad = align_up(off_tiles + tl * sizeof(uint64_t), 256);
     size_t off_arena = align_up(off_bad + 16, 256);
     size_t off_recs = align_up(off_arena + at * sizeof(uint64_t), 256);
-    size_t off_parts = align_up(off_recs + (size_t)fr * 16, 256);
+    size_t off_parts = align_up(off_recs + (size_t)fr * sizeof(FrameRec8), 256);
     size_t off_info = align_up(off_parts + ((size_t)fr / (kBlock * kScanFpt) + 2) * sizeof(TilePart), 256);
     size_t bytes = align_up(off_info + (size_t)fr + 64, 256);
     int prev = 0;
@@ -6444,7 +6508,7 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
                        b->wire_len < (1ull << 52) &&
                        (uint64_t)(a.n - 1) <= (b->wire_len - 1) / b->frame_stride;
     if (fused) {
-        a.recs = reinterpret_cast<FrameRec*>(e->ws.recs);
+        a.recs = reinterpret_cast<FrameRec8*>(e->ws.recs);
         a.stride_inv = 1.0 / (double)b->frame_stride;
         // 16 KiB tiles at every fused frame size: the tile's LDS staging, parse and barriers
         // are paid per tile, so the fused pass wants larger tiles than the plain payload
@@ -6493,7 +6557,7 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
                 hipLaunchKernelGGL(k_desc_emit<true>, dim3(n_parts), dim3(kBlock), 0, s, a, e->ws, n_parts, d_desc);
             } else {
                 BatchArgs ai = a;  // the scan reads the info bytes
-                ai.recs = reinterpret_cast<FrameRec*>(e->ws.info);
+                ai.recs = reinterpret_cast<FrameRec8*>(e->ws.info);
                 hipLaunchKernelGGL((k_sum_scan<false, UVHTTP_WS_STAMP_SUM_SCAN>), dim3(n_parts), dim3(kBlock), 0,
                                    s, ai, e->ws);
                 hipLaunchKernelGGL(k_desc_emit<false>, dim3(n_parts), dim3(kBlock), 0, s, a, e->ws, n_parts, d_desc);
@@ -6504,7 +6568,7 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
             return UVHTTP_WS_GPU_OK;
         }
         if (sum_fast) {
-            a.recs = reinterpret_cast<FrameRec*>(e->ws.recs);  // (the info bytes: 1 per frame)
+            a.recs = reinterpret_cast<FrameRec8*>(e->ws.recs);  // (the info bytes: 1 per frame)
             const int stk = timing_begin(e, s);
             for (uint64_t tb = 0; tb < f_tiles; tb += f_max) {
                 const uint32_t grid_p = (uint32_t)((f_tiles - tb) < f_max ? (f_tiles - tb) : f_max);
@@ -6584,7 +6648,7 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
                       b->wire_len < (1ull << 52) && arena_cap < (1ull << 52) &&
                       (uint64_t)(a.n - 1) <= (b->wire_len - 1) / b->frame_stride;
     if (spec) {
-        a.recs = reinterpret_cast<FrameRec*>(e->ws.recs);
+        a.recs = reinterpret_cast<FrameRec8*>(e->ws.recs);
         a.stride_inv = 1.0 / (double)b->frame_stride;
         a.spec_P = spec_p;
         constexpr uint64_t kSt = 256ull * 4 * 16;
@@ -6598,7 +6662,7 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
         // with descriptors under the same bounds: the records pass, the scan and k_sum_msgs
         // rebuilding the info bytes from the records, k_sum_msgs also writing the descriptors
         const bool desc_c = !no_desc && e->desc_emit && sum_ok(e, b) && arena_cap / spec_p >= a.n;
-        if (sum_c) a.recs = reinterpret_cast<FrameRec*>(e->ws.recs);  // (the info bytes)
+        if (sum_c) a.recs = reinterpret_cast<FrameRec8*>(e->ws.recs);  // (the info bytes)
         const int stk = timing_begin(e, s);
         const bool both = desc_c && e->desc_emit != 2;  // (records + info bytes from the pass)
         for (uint64_t tb = 0; tb < s_tiles; tb += (1ull << 24)) {
@@ -6624,7 +6688,7 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
             const uint32_t n_parts = (a.n + kBlock * kScanFpt - 1) / (kBlock * kScanFpt);
             if (both) {
                 BatchArgs ai = a;  // the scan reads the info bytes
-                ai.recs = reinterpret_cast<FrameRec*>(e->ws.info);
+                ai.recs = reinterpret_cast<FrameRec8*>(e->ws.info);
                 hipLaunchKernelGGL((k_sum_scan<true, UVHTTP_WS_STAMP_SUM_SCAN>), dim3(n_parts), dim3(kBlock), 0, s,
                                    ai, e->ws);
                 hipLaunchKernelGGL((k_sum_msgs<false, true>), dim3(n_parts), dim3(kBlock), 0, s, a, e->ws, n_parts,
@@ -6659,7 +6723,7 @@ static int run_decode(uvhttp_ws_gpu_engine_t* e, const uvhttp_ws_batch_t* b, uin
                              b->wire_len < (1ull << 52) &&
                              (uint64_t)(a.n - 1) <= (b->wire_len - 1) / b->frame_stride;
     if (rec_compact) {
-        a.recs = reinterpret_cast<FrameRec*>(e->ws.recs);
+        a.recs = reinterpret_cast<FrameRec8*>(e->ws.recs);
         a.stride_inv = 1.0 / (double)b->frame_stride;
         constexpr uint64_t kRt = 256ull * 4 * 16;
         const uint64_t r_tiles = (b->wire_len + kRt - 1) / kRt;
@@ -6942,7 +7006,7 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
                                                             ((size_t)e->sp_streams / kBlock + 2) * 8, 256) +
                                                    (size_t)(e->sp_tiles + 1) * 8, 256));
         sa.n_tiles = sp_tiles;
-        sa.recs = reinterpret_cast<FrameRec*>(e->ws.recs);
+        sa.recs = reinterpret_cast<FrameRec8*>(e->ws.recs);
         sa.desc = d_desc;
         sa.results = d_results;
         sa.ctl = e->ctl;
