@@ -529,15 +529,6 @@ class GpuWorkload:
         avg = ms / 1e3 / k
         return 2 * self.wire_len / avg / 1e9, avg * 1e6
 
-    def stamp_timed(self):
-        """streams mode keeps the device stamps on during the timed steps (the idle between calls
-        some runs show happens there); timeline() then reads the last 128 timed calls (the
-        engine's stamp ring)"""
-        if self.streams_dev is not None:
-            self.eng.set_stamps(True)
-            self.eng.read_stamps()
-            self.stamped_timed = True
-
     def timeline(self, calls=16, step_ms=None):
         """Device-side kernel stamps (uvhttp_ws_gpu_engine_set_stamps) over `calls` more steps
         after the timed region, same process and buffers: when each kernel of a call ran on the
@@ -553,13 +544,6 @@ class GpuWorkload:
         if self.graph is not None:
             return None
         eng = self.eng
-        if getattr(self, "stamped_timed", False):
-            recs = eng.read_stamps()  # the last timed calls
-            eng.set_stamps(False)
-            out = summarize_stamps(recs)
-            if out:
-                out["calls_from"] = "the timed steps (stamps on while timed; up to the last 128)"
-            return out
         eng.set_stamps(True)
         eng.read_stamps()  # drop anything older
         keep = min(calls, 15)
@@ -656,8 +640,6 @@ def timed_run(wl, steps, warmup, world):
         wl.step()
     wl.check()
     wl.kernel_time()  # discard warmup events
-    if hasattr(wl, "stamp_timed") and not getattr(wl, "no_stamps", False):
-        wl.stamp_timed()
     wl.set_timing(True)
     if world > 1:
         dist.barrier()

@@ -3868,18 +3868,37 @@ __device__ inline uvhttp_ws_stream_result_t walk_wave(const WalkArgs& w, uint32_
     return r;
 }
 
+// the connections of (virtual) workgroup vb, a wave each
 template <int MODE>
-__global__ __launch_bounds__(kBlock) void k_swalk_wave(WalkArgs w) {
-    if (walk_skip(w)) return;
-    StampScope stamp_(w.stamp, w.epoch, MODE == 1 ? UVHTTP_WS_STAMP_WALK2 : UVHTTP_WS_STAMP_WALK, false);
+__device__ inline void swalk_wave_block(const WalkArgs& w, uint32_t vb, StampScope& stamp_) {
     __shared__ __attribute__((aligned(16))) uint8_t ring[kBlock / 64][kRingBytes];
     // readfirstlane: the connection (and all walk state derived from it) is wave-uniform, so
     // it lives in scalar registers and the walk's branches are scalar branches
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t s = stamp_.anchor_s(blockIdx.x * (kBlock / 64) + wave);
+    const uint32_t s = stamp_.anchor_s(vb * (kBlock / 64) + wave);
     if (s >= w.n_streams) return;
     if (MODE == 1 && !w.results[s].n_frames) return;
     (void)walk_wave<MODE>(w, s, ring[wave]);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_swalk_wave(WalkArgs w) {
+    if (walk_skip(w)) return;
+    StampScope stamp_(w.stamp, w.epoch, MODE == 1 ? UVHTTP_WS_STAMP_WALK2 : UVHTTP_WS_STAMP_WALK, false);
+    swalk_wave_block<MODE>(w, blockIdx.x, stamp_);
+}
+
+// Behind the speculative decode the walk path is a fall-back that almost never runs, and a
+// launch that returns at once costs about its workgroup count: 1024 workgroups per gated
+// kernel — three of them — put ~7 us between C4 stream calls (stamps, profiles/r06p_*), 256
+// about 1 (the gated compact fall-back's).  So the gated walk kernels stride over the blocks
+// with kGatedGrid workgroups.
+constexpr uint32_t kGatedGrid = 256;
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_swalk_wave_gated(WalkArgs w, uint32_t n_blocks) {
+    if (walk_skip(w)) return;
+    StampScope stamp_(w.stamp, w.epoch, MODE == 1 ? UVHTTP_WS_STAMP_WALK2 : UVHTTP_WS_STAMP_WALK, false);
+    for (uint32_t vb = blockIdx.x; vb < n_blocks; vb += gridDim.x) swalk_wave_block<MODE>(w, vb, stamp_);
 }
 
 // first frames, total, capacity (one workgroup).  Lane mode scans the walk's per-block
@@ -4113,17 +4132,15 @@ __device__ inline void stream_desc_wave(const WalkArgs& w, uint32_t s, const uvh
 // k_stream_desc: one wave per connection (stream_desc_wave) after k_swalk_scan.  Capacity
 // overflow: every result says so, nothing else.
 
-__global__ __launch_bounds__(kBlock) void k_stream_desc(WalkArgs w) {
-    if (walk_skip(w)) return;
-    StampScope stamp_(w.stamp, w.epoch, UVHTTP_WS_STAMP_STREAM_DESC, false);
+__device__ inline void stream_desc_block(const WalkArgs& w, uint32_t vb, StampScope& stamp_) {
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const uint32_t s = stamp_.anchor_s(blockIdx.x * (kBlock / 64) + wave);
+    const uint32_t s = stamp_.anchor_s(vb * (kBlock / 64) + wave);
     uint32_t first, n_total;
     if (w.desc_scan) {
         // k_swalk_scan's work here: the walk left each connection's frame count in agg; every
         // workgroup sums all of them (the total, capacity) and those before its first
         // connection, then adds its own earlier waves' (one launch and its boundary fewer)
-        const uint32_t s0 = blockIdx.x * (kBlock / 64);
+        const uint32_t s0 = vb * (kBlock / 64);
         // (all 16 loads issued before any is used: as a loop they ran one round trip each,
         // 15.7 us for this kernel instead of 11.5)
         uint32_t v[kDescScanMax / kBlock];
@@ -4144,7 +4161,7 @@ __global__ __launch_bounds__(kBlock) void k_stream_desc(WalkArgs w) {
         for (uint32_t k = s0; k < s && k < w.n_streams; ++k) all_pre += w.agg[k];
         first = (uint32_t)all_pre;
         n_total = all_tot <= w.max_frames ? (uint32_t)all_tot : 0u;
-        if (blockIdx.x == 0 && threadIdx.x == 0) *w.sc.n_total = n_total;
+        if (vb == 0 && threadIdx.x == 0) *w.sc.n_total = n_total;
         if (s >= w.n_streams) return;
     } else {
         if (s >= w.n_streams) return;
@@ -4166,6 +4183,22 @@ __global__ __launch_bounds__(kBlock) void k_stream_desc(WalkArgs w) {
     if (lane == 0) w.results[s].first_frame = r.first_frame;
     if (!r.n_frames) return;
     stream_desc_wave(w, s, st, r, claim_start(w, s, st), w.dev_epoch ? w.ctl[kCtlEpoch] : w.epoch);
+}
+
+__global__ __launch_bounds__(kBlock) void k_stream_desc(WalkArgs w) {
+    if (walk_skip(w)) return;
+    StampScope stamp_(w.stamp, w.epoch, UVHTTP_WS_STAMP_STREAM_DESC, false);
+    stream_desc_block(w, blockIdx.x, stamp_);
+}
+
+// (behind the speculative decode: k_swalk_wave_gated's grid)
+__global__ __launch_bounds__(kBlock) void k_stream_desc_gated(WalkArgs w, uint32_t n_blocks) {
+    if (walk_skip(w)) return;
+    StampScope stamp_(w.stamp, w.epoch, UVHTTP_WS_STAMP_STREAM_DESC, false);
+    for (uint32_t vb = blockIdx.x; vb < n_blocks; vb += gridDim.x) {
+        __syncthreads();  // (the previous block's LDS in the block sums)
+        stream_desc_block(w, vb, stamp_);
+    }
 }
 
 // ---- speculative stream decode (k_sspec_*) ------------------------------------------------
@@ -4217,7 +4250,7 @@ constexpr uint64_t kSpecT = kMapTile;           // k_sspec_pass tile = the claim
 // start — whatever the connections.  (A table sized for 64 connections' edge frames took 24.6 KB
 // of LDS: 6 workgroups per CU, the pass 99 us on C4 streams.)
 constexpr uint32_t kSpecMaxF = (uint32_t)(kSpecT / kSpecMinL) + 2;
-constexpr uint32_t kSpecUndoGrid = 1024;        // k_sspec_fallback's grid (4 workgroups per CU)
+constexpr uint32_t kSpecUndoGrid = 256;         // k_sspec_fallback's grid (kGatedGrid: a gated launch)
 
 struct SpecArgs {
     uint8_t* wire;
@@ -7036,7 +7069,13 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     if (fused) {
         hipLaunchKernelGGL(k_swalk_fused, dim3(nwb), dim3(kBlock), 0, s, w);
     } else {
-        if (wave_walk) {
+        // (behind the speculative decode, gated: the wave walk's kernels with kGatedGrid
+        // workgroups striding over the blocks)
+        const uint32_t ggrid = nwb < kGatedGrid ? nwb : kGatedGrid;
+        if (wave_walk && spec) {
+            if (w.single) hipLaunchKernelGGL(k_swalk_wave_gated<2>, dim3(ggrid), dim3(kBlock), 0, s, w, nwb);
+            else hipLaunchKernelGGL(k_swalk_wave_gated<0>, dim3(ggrid), dim3(kBlock), 0, s, w, nwb);
+        } else if (wave_walk) {
             if (w.single) hipLaunchKernelGGL(k_swalk_wave<2>, dim3(nwb), dim3(kBlock), 0, s, w);
             else hipLaunchKernelGGL(k_swalk_wave<0>, dim3(nwb), dim3(kBlock), 0, s, w);
         } else {
@@ -7049,10 +7088,12 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
                        !e->desc_scan_off) ? 1u : 0u;
         if (!w.desc_scan) hipLaunchKernelGGL(k_swalk_scan, dim3(1), dim3(kBlock), 0, s, w, wave_walk ? 0u : 1u);
         if (!w.single) {
-            if (wave_walk) hipLaunchKernelGGL(k_swalk_wave<1>, dim3(nwb), dim3(kBlock), 0, s, w);
+            if (wave_walk && spec) hipLaunchKernelGGL(k_swalk_wave_gated<1>, dim3(ggrid), dim3(kBlock), 0, s, w, nwb);
+            else if (wave_walk) hipLaunchKernelGGL(k_swalk_wave<1>, dim3(nwb), dim3(kBlock), 0, s, w);
             else hipLaunchKernelGGL(k_swalk_lane<1>, dim3(nsb), dim3(kBlock), 0, s, w);
         }
-        if (wave_walk) hipLaunchKernelGGL(k_stream_desc, dim3(nwb), dim3(kBlock), 0, s, w);
+        if (wave_walk && spec) hipLaunchKernelGGL(k_stream_desc_gated, dim3(ggrid), dim3(kBlock), 0, s, w, nwb);
+        else if (wave_walk) hipLaunchKernelGGL(k_stream_desc, dim3(nwb), dim3(kBlock), 0, s, w);
         else hipLaunchKernelGGL(k_stream_desc_lane, dim3(nsb), dim3(kBlock), 0, s, w);
     }
 
