@@ -2297,12 +2297,14 @@ constexpr uint32_t kSumTailGrid = 128;  // k_sum_tail blocks (all re-mask after 
 
 // the combination of parts [0, hi) in order, in every thread of the block (each thread a run
 // of consecutive parts, kU loads in flight)
+// (kU parts in flight per thread: 8 for k_sum_tail; k_desc_emit takes 2 — with 8 its block 0's
+// summary set the whole kernel's registers, 146 VGPRs and 3 waves per SIMD, against 62)
+template <uint32_t kU = 8>
 __device__ TilePart parts_prefix(const TilePart* parts, uint32_t hi) {
     __shared__ TilePart s_res;
     const uint32_t per = (hi + kBlock - 1) / kBlock;
     const uint32_t p0 = threadIdx.x * per;
     TilePart acc = part_identity();
-    constexpr uint32_t kU = 8;
     for (uint32_t pb = p0; pb < p0 + per && pb < hi; pb += kU) {
         TilePart r[kU];
 #pragma unroll
@@ -2692,8 +2694,6 @@ __global__ __launch_bounds__(kBlock) void k_desc_emit(BatchArgs a, Workspace ws,
     const uint32_t n = a.n;
     const uint64_t S = a.frame_stride;
     const bool head = blockIdx.x == 0;
-    uvhttp_ws_frame_desc_t dl;
-    if (head && threadIdx.x == 0) (void)parse_one(a, n - 1, seg_info(a, n - 1, n), dl);
     const uint32_t nb = first_bad_of(a, ws, n);
     // the block's 1024 frames (scan block b's) in four rounds of 256: thread t takes frame
     // B0 + 256 k + t, so every record load and descriptor store of a wave is contiguous (a
@@ -2753,8 +2753,12 @@ __global__ __launch_bounds__(kBlock) void k_desc_emit(BatchArgs a, Workspace ws,
         round_base += (uint32_t)((tot >> (16 * k)) & 0xFFFFu);
     }
     if (head) {  // the summary (every block's part, in order), as k_sum_tail's block 0
-        const TilePart tp = parts_prefix(reinterpret_cast<const TilePart*>(ws.parts), n_parts);
-        if (threadIdx.x == 0) sum_summary(a, tp, dl, nb, false);
+        const TilePart tp = parts_prefix<2>(reinterpret_cast<const TilePart*>(ws.parts), n_parts);
+        if (threadIdx.x == 0) {  // (the last frame parsed here: not live across the kernel)
+            uvhttp_ws_frame_desc_t dl;
+            (void)parse_one(a, n - 1, seg_info(a, n - 1, n), dl);
+            sum_summary(a, tp, dl, nb, false);
+        }
     }
     if (nb >= n) return;
     // a failure: restore this block's frames the payload pass unmasked from first_bad on (a
