@@ -15,7 +15,9 @@ import torch  # noqa: E402
 import uvhttp_amd as U  # noqa: E402
 
 CFG = {"c2": (65536, 4096), "c3": (65536, 65536), "c4": (1048576, 256),
-       "c1k": (262144, 1024), "c2k": (131072, 2048), "c64": (4194304, 64)}
+       "c1k": (262144, 1024), "c2k": (131072, 2048), "c64": (4194304, 64),
+       # mixed sizes (payloads 100-412 bytes, seeded): the frame-grouped kernel's LDS-window path
+       "mix": (1048576, 256)}
 
 
 def main():
@@ -27,6 +29,8 @@ def main():
                             ("fin", "u1"), ("mask", "u1"), ("r0", "u1"), ("r1", "<u8")])
     fr["po"] = np.arange(n, dtype=np.uint64) * plen
     fr["pl"] = plen
+    if sys.argv[1] == "mix":
+        fr["pl"] = np.random.default_rng(7).integers(100, 413, n, dtype=np.uint64)
     fr["key"] = np.arange(n, dtype=np.uint32) * 2654435761
     fr["op"], fr["fin"] = 2, 1
     fr["mask"] = int(os.environ.get("AB_MASKED", "0"))
