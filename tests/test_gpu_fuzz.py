@@ -11,6 +11,12 @@
   opcode including reserved ones, RSV bits, unmasked frames, oversize control frames, 16/64-bit
   length forms used for small payloads) cut into drawn read sizes; the host delivery must leave
   each connection exactly where the oracle's process_data per read leaves it.
+* The same for connections of EQUAL frames, the shape the speculative stream decode (k_sspec_*)
+  takes: a drawn frame length (64 bytes up, around the 16 / 64-bit length forms and the 16 KiB
+  tile), a drawn fragment pattern, an optional break (one frame of another length, a control
+  frame, RSV bits, an unmasked frame, a CONT without a start) at a drawn index, a drawn trailing
+  partial frame — so the speculation runs, is refused by the plan, or breaks in the pass or the
+  state machine and is undone.
 """
 import random
 
@@ -160,3 +166,82 @@ def test_hypothesis_streams_vs_oracle(torch, eng, hooks, conns, seed, per_read):
     if not cases:
         return
     _run_cases(torch, eng, U, cases, rng, 4096, use_reads=per_read)
+
+
+_SPEC_CONN = st.fixed_dictionaries({
+    "plen": st.sampled_from([58, 59, 60, 100, 121, 125, 126, 200, 250, 1000, 4090, 16378, 16390, 65530, 65536]),
+    "n": st.integers(1, 40),
+    "pattern": st.sampled_from(["whole", "frag", "mixed", "open_end"]),
+    "op": st.sampled_from([1, 2]),
+    "break_at": st.one_of(st.none(), st.integers(0, 39)),
+    "break_kind": st.sampled_from(["len", "ping", "close", "rsv", "unmasked", "cont", "start"]),
+    "tail": st.sampled_from([0, 0, 1, 3, 9, 100]),
+    "pending": st.booleans(),
+    "mm": st.sampled_from([0, 0, 64 * 1024 * 1024, 3000]),
+    "reads": st.lists(st.sampled_from([0, 100, 1000, 4096, 16384, 20000, 1 << 20]), min_size=1, max_size=4),
+})
+
+
+def _spec_case(U, rng, c):
+    plen, n, op = c["plen"], c["n"], c["op"]
+    if plen > 16000:
+        n = min(n, 6)  # (a few MB per connection at most: the oracle decodes it too)
+    prod = U.WsConnection(1, 16 * 1024 * 1024, c["mm"], user_data=True)
+    orc = _oracle.OracleConn(1, 16 * 1024 * 1024, c["mm"], record=1, wrapper=True)
+    prefix = _frame(op, 0, rng.randbytes(20), rng.randbytes(4)) if c["pending"] else b""
+    frames = []
+    for i in range(n):
+        if c["pattern"] == "whole":
+            fop, fin = (0 if c["pending"] and i == 0 else op), 1
+        elif c["pattern"] == "frag":  # one message over all frames
+            fop, fin = (op if i == 0 and not c["pending"] else 0), int(i == n - 1)
+        elif c["pattern"] == "mixed":  # messages of 3 frames
+            fop, fin = (op if i % 3 == 0 and not (c["pending"] and i == 0) else 0), int(i % 3 == 2)
+        else:  # every frame continues, the message stays open
+            fop, fin = (op if i == 0 and not c["pending"] else 0), 0
+        p, masked, rsv = plen, True, 0
+        if c["break_at"] == i:
+            k = c["break_kind"]
+            if k == "len":
+                p = plen + 1 if plen < 65536 else plen - 1
+            elif k in ("ping", "close"):
+                fop, fin, p = (9 if k == "ping" else 8), 1, min(plen, 125)
+            elif k == "rsv":
+                rsv = 4
+            elif k == "unmasked":
+                masked = False
+            elif k == "cont":
+                fop = 0
+            else:
+                fop = op
+        frames.append(_frame(fop, fin, rng.randbytes(p), rng.randbytes(4), masked, rsv))
+    new = b"".join(frames)
+    if c["tail"]:
+        t = _frame(0, 1, rng.randbytes(plen), rng.randbytes(4))
+        new += t[:min(c["tail"], len(t) - 1)]
+    r1, r2 = prod.process_data(prefix), orc.process_data(prefix)
+    assert r1 == r2
+    if r1 != 0:
+        return None
+    reads, pos, k = [], 0, 0
+    while pos < len(new):
+        sz = c["reads"][k % len(c["reads"])] or len(new)
+        reads.append(new[pos:pos + sz])
+        pos += sz
+        k += 1
+    return prod, orc, reads or [b""]
+
+
+@settings(max_examples=60, deadline=None, derandomize=True, database=None,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large,
+                                 HealthCheck.function_scoped_fixture])
+@given(conns=st.lists(_SPEC_CONN, min_size=1, max_size=12), seed=st.integers(0, 2**32 - 1),
+       per_read=st.booleans())
+def test_hypothesis_equal_frame_streams_vs_oracle(torch, eng, hooks, conns, seed, per_read):  # noqa: F811
+    import uvhttp_amd as U
+    rng = random.Random(seed)
+    cases = [c for c in (_spec_case(U, rng, c) for c in conns) if c]
+    if not cases:
+        return
+    # a frame capacity of at least 8 per connection: the speculative decode is tried
+    _run_cases(torch, eng, U, cases, rng, max(8 * len(cases), 64 * len(cases)), use_reads=per_read)
