@@ -19,7 +19,8 @@ import uvhttp_amd as U  # noqa: E402
 
 CFG = {"c2": (65536, 4096, False), "c3": (65536, 65536, False), "c4": (1048576, 256, True),
        # (extra frame sizes for shape rules: same 256 MiB of payload)
-       "f2k": (131072, 2048, False), "f8k": (32768, 8192, False), "f16k": (16384, 16384, False)}
+       "f2k": (131072, 2048, False), "f8k": (32768, 8192, False), "f16k": (16384, 16384, False),
+       "f24k": (10922, 24576, False), "f32k": (8192, 32768, False)}
 
 
 def main():

@@ -33,7 +33,11 @@ namespace {
 
 constexpr int kBlock = 256;                 // threads per workgroup (4 waves of 64)
 constexpr uint64_t kMapTile = 16384;        // granularity of the tile -> first-frame maps
-constexpr uint64_t kScatterAvg = 16384;     // compact decode: wire-driven below this frame size
+// compact decode: wire-driven (k_scatter_compact) below this average frame size, arena-driven
+// gather above.  (Same-process A/B, scatter vs gather: 16 KiB frames 97.0 vs 102.2 us per
+// 256 MiB step, 24 KiB 96.8 vs 102.8, 32 KiB 109.8 vs 101.2, 64 KiB 1775 vs 1338 per 4 GiB;
+// profiles/r06zd_*, r06ze_*.  16 KiB until round 6.)
+constexpr uint64_t kScatterAvg = 26624;
 constexpr uint32_t kMaxFrames = 1u << 26;   // k_scan handles <= 2^18 block aggregates
 constexpr uint32_t kNoFrame = 0xFFFFFFFFu;  // tile map entry no frame claimed this call
 constexpr uint32_t kMaxEpoch = (1u << 30) - 1;  // decode-call tags run 1 .. kMaxEpoch
