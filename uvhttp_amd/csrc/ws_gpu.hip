@@ -6976,8 +6976,10 @@ int uvhttp_ws_gpu_decode_reads(uvhttp_ws_gpu_engine_t* e, uint8_t* d_wire, uint6
     // the lane walk in two passes and no slice scratch, 2 of 10 runs idled all the same, r03p51.)
     const bool single_ok = e->walk_single_off == 0;
     // slices: connection s's starts at walk_tmp[begin / 2 + s ...] (4-byte entries)
+    // (up to 16 GiB of slices — twice the wire, on a 288 GB device: C3's 4.3 GB streams call
+    // walks in one pass; above 8 GiB it walked twice, the second walk + scan ~1 % of its step)
     const uint64_t want = wire_len / 2 + n_streams + 1;
-    if (single_ok && !e->capturing && want * 4 <= (8ull << 30) && want > e->wt_cap) {
+    if (single_ok && !e->capturing && want * 4 <= (16ull << 30) && want > e->wt_cap) {
         // (an earlier call may still use the slices: released behind it on the stream)
         e->wt_cap = 0;
         if (scratch_grow(e, &e->wt_mem, want * 4, false, s, true) == hipSuccess) e->wt_cap = want;
