@@ -31,12 +31,18 @@ def main():
     fr["pl"] = plen
     if sys.argv[1] == "mix":
         fr["pl"] = np.random.default_rng(7).integers(100, 413, n, dtype=np.uint64)
+    src_len = n * plen + 64
+    if os.environ.get("AB_ALIGN"):  # experiment: payload sources at the output's 16-byte phase
+        hm = (2 if plen < 126 else 4 if plen < 65536 else 10) + (4 if os.environ.get("AB_MASKED") == "1" else 0)
+        st = np.arange(n, dtype=np.uint64) * np.uint64(plen + hm)
+        fr["po"] = np.arange(n, dtype=np.uint64) * np.uint64(plen + 16) + (st + np.uint64(hm)) % np.uint64(16)
+        src_len = n * (plen + 16) + 64
     fr["key"] = np.arange(n, dtype=np.uint32) * 2654435761
     fr["op"], fr["fin"] = 2, 1
     fr["mask"] = int(os.environ.get("AB_MASKED", "0"))
     dev = "cuda"
     d = torch.from_numpy(fr.view(np.uint8).copy()).to(dev)
-    src = torch.randint(0, 256, (n * plen + 64,), dtype=torch.uint8, device=dev)
+    src = torch.randint(0, 256, (src_len,), dtype=torch.uint8, device=dev)
     outs = [torch.zeros(n * (plen + 14) + 64, dtype=torch.uint8, device=dev) for _ in engs]
     offs = [torch.zeros(n + 1, dtype=torch.int64, device=dev) for _ in engs]
     st = torch.cuda.current_stream()
