@@ -5535,16 +5535,26 @@ void kb_emit_frames(BuildArgs b) {
                 if (m.w) atomicOr(&win32[4 * wv + 3], m.w);
             }
         };
-        auto put_headers = [&]() {  // header bytes (one lane per frame)
+        auto put_headers = [&]() {  // header bytes (one lane per frame), a word per LDS atomic
             if (threadIdx.x >= nf) return;
             const uint32_t j = threadIdx.x;
             const uint64_t st = s_st[j], ps = s_ps[j];
             const u32x4 img = s_img[j];
             const uint32_t iw[4] = {img.x, img.y, img.z, img.w};
-            for (uint64_t k = st; k < ps; ++k) {
-                if (k < wlo || k >= whi) continue;
-                const uint32_t ib = (uint32_t)(k - st), wb = (uint32_t)(k - wlo);
-                atomicOr(&win32[wb >> 2], ((iw[ib >> 2] >> (8 * (ib & 3))) & 0xFFu) << (8 * (wb & 3)));
+            const uint64_t a0 = st > wlo ? st : wlo, a1 = ps < whi ? ps : whi;
+            // (an 8-byte masked header: 2-3 word atomics instead of 8 byte atomics; the window
+            // is 16-byte aligned, so output words are window words)
+            for (uint64_t d = a0 & ~3ull; d < a1; d += 4) {
+                uint32_t val = 0;
+#pragma unroll
+                for (uint32_t q = 0; q < 4; ++q) {
+                    const uint64_t k = d + q;
+                    if (k >= a0 && k < a1) {
+                        const uint32_t ib = (uint32_t)(k - st);
+                        val |= ((iw[ib >> 2] >> (8 * (ib & 3))) & 0xFFu) << (8 * q);
+                    }
+                }
+                atomicOr(&win32[(d - wlo) >> 2], val);
             }
         };
         if (one && b.src_len >= 16) {
